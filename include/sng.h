@@ -1,0 +1,173 @@
+/*
+ * sng.h -- C-ABI of libsng_hip.so, the MI355X-native SyNeRFgine render path.
+ *
+ * Plain pointers and sizes only (no torch / HIP C++ types in signatures).
+ * Device pointers are marked d_*; everything else is host memory.  Every call
+ * returns an int status (SNG_OK = 0) and records a message for
+ * sng_last_error() on failure -- the C equivalent of the reference's
+ * CUDA_CHECK_THROW -> std::runtime_error (main.cu:225-227).
+ *
+ * Each entry point names the reference interface it replaces (file:line,
+ * relative to the reference root).  INTEGRATION.md shows the binding a
+ * maintainer would add on the reference side.
+ */
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SNG_ABI_VERSION 1
+
+enum {
+    SNG_OK = 0,
+    SNG_ERR_INVALID = -1,   /* bad argument / shape mismatch */
+    SNG_ERR_HIP = -2,       /* HIP runtime error */
+    SNG_ERR_IO = -3,        /* file missing / parse error */
+    SNG_ERR_STATE = -4,     /* call order (e.g. render before a model is set) */
+    SNG_ERR_NOGPU = -5      /* no HIP device visible */
+};
+
+typedef struct sng_ctx sng_ctx;
+
+typedef struct {
+    int32_t device_id;       /* HIP device ordinal (one context per GPU / rank) */
+    int32_t reserved[7];
+} sng_ctx_desc;
+
+/* NerfNetwork configuration (configs/nerf/base.json:23-55; nerf_network.h:79-101).
+ * The fused kernel is specialised for the base.json shape: 64-neuron MLPs,
+ * density 1 hidden layer, rgb 2 hidden layers, SH degree 4, L*F = 32. */
+typedef struct {
+    uint32_t n_levels;              /* 8  */
+    uint32_t n_features_per_level;  /* 4  */
+    uint32_t log2_hashmap_size;     /* 19 */
+    uint32_t base_resolution;       /* 16 */
+    float per_level_scale;          /* from the snapshot (testbed.cu:3737-3741) */
+    uint32_t aabb_scale;            /* power of two; -> m_aabb, max_cascade, cone (testbed_nerf.cu:3069-3085) */
+    uint32_t reserved[6];
+} sng_nerf_config;
+
+typedef struct {
+    int32_t nerf_res[2];   /* NeRF render buffer resolution (Engine::resize, engine.cu:236-255) */
+    int32_t mesh_res[2];   /* virtual-object (raytracer) resolution */
+    int32_t syn_px_scale;  /* m_relative_vo_scale after resize */
+    int32_t reserved[3];
+} sng_resolution_info;
+
+typedef struct {
+    uint32_t spp;                /* render_buffer.spp: sample index for pixel jitter */
+    int32_t reset_accumulation;  /* 1: camera-moved semantics (fresh accumulation buffers) */
+    int32_t row_begin;           /* band of final-image rows to produce, [row_begin,row_end); 0,0 = all */
+    int32_t row_end;
+    int32_t collect_kernel_times;/* 1: hipEvent-time every network launch (bench roofline) */
+    uint32_t target_n_queries;   /* 0 = 2*1024*1024 (testbed_nerf.cu:2189) */
+    int32_t reserved[2];
+} sng_frame_params;
+
+typedef struct {
+    /* device buffers owned by the context, valid until the next render/resize */
+    float* d_final_rgba;      /* mesh_res, RGBA32F, overlay output (raytracer.cu:256) */
+    float* d_final_depth;     /* mesh_res */
+    float* d_nerf_rgba;       /* nerf_res, NeRF frame buffer after shadows */
+    float* d_nerf_depth;      /* nerf_res */
+    float* d_nerf_positions;  /* nerf_res x 3 */
+    float* d_nerf_normals;    /* nerf_res x 3 */
+    float* d_syn_rgba;        /* mesh_res, raytracer accumulation buffer (m_rays[0].rgba) */
+    float* d_syn_depth;       /* mesh_res */
+    /* statistics */
+    uint32_t n_iterations;    /* wavefront iterations of trace_alt */
+    uint32_t n_hit;           /* rays that reached the hit list */
+    uint64_t n_samples;       /* network samples evaluated (real, compacted) */
+    uint64_t n_reference_slots; /* slots the reference would evaluate (incl. stale + padding) */
+    float ms_frame;           /* device time of the whole frame (hipEvents) */
+    float ms_raytrace, ms_nerf, ms_shadow, ms_overlay;
+    float ms_network;         /* sum of fused network kernel durations (collect_kernel_times) */
+    uint32_t network_launches;
+    uint32_t alive_per_iter[64];
+    uint32_t steps_per_iter[64];
+    int32_t reserved[8];
+} sng_frame_result;
+
+typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;
+typedef struct { float ka[3], kd[3], ks[3]; float n, rg, spec_angle; int32_t type; /* 0 lambertian, 1 glossy */ } sng_material;
+typedef struct {
+    uint32_t n_nodes, n_tris;
+    float rot[9];      /* column-major mat3 */
+    float pos[3];
+    float scale;
+    int32_t mat_id;
+} sng_object_info;
+
+/* ---- context ------------------------------------------------------------- */
+const char* sng_last_error(void);
+int sng_abi_version(void);
+int sng_device_count(int* out);
+/* replaces Testbed::Testbed + Engine ctor (testbed.cu:3897, engine.cuh:22) */
+int sng_ctx_create(const sng_ctx_desc* desc, sng_ctx** out);
+int sng_ctx_destroy(sng_ctx* ctx);
+
+/* ---- model: Testbed::load_snapshot (testbed.cu:4878-5015, 4994) ---------- */
+int sng_load_snapshot(sng_ctx* ctx, const char* ingp_path);
+/* NerfNetwork params in tcnn order (nerf_network.h:356-371): density MLP, rgb MLP, grid; fp16 */
+int sng_set_nerf_model(sng_ctx* ctx, const sng_nerf_config* cfg, const uint16_t* params_f16, uint64_t n_params);
+uint64_t sng_nerf_param_count(const sng_nerf_config* cfg);
+/* density_grid_binary (fp16, 128^3 x (max_cascade+1)) -> bitfield
+ * (update_density_grid_mean_and_bitfield, testbed_nerf.cu:3212-3229) */
+int sng_set_density_grid(sng_ctx* ctx, const uint16_t* grid_f16, uint64_t n_cells);
+int sng_get_bitfield(sng_ctx* ctx, uint8_t* out, uint64_t n_bytes);
+int sng_get_density_mean(sng_ctx* ctx, float* out);
+
+/* ---- operator boundary: NerfNetwork::inference_mixed_precision (nerf_network.h:105-139)
+ * d_coords: NerfCoordinate AoS {pos(3), dt, dir(3)} with stride_floats >= 7;
+ * out_layout 0: tcnn GPUMatrix<half,RM> [16][n] (row c at c*n; row 3 = density);
+ * out_layout 1: AoS [n][4] = (r,g,b,density) raw network outputs. */
+int sng_nerf_inference(sng_ctx* ctx, const float* d_coords, uint32_t stride_floats, uint32_t n,
+                       uint16_t* d_out, int32_t out_layout, void* hip_stream);
+/* pos encoding only (tcnn GridEncoding forward), out [n][L*F] fp16 -- parity hook */
+int sng_hashgrid_encode(sng_ctx* ctx, const float* d_coords, uint32_t stride_floats, uint32_t n, uint16_t* d_out, void* hip_stream);
+
+/* ---- virtual scene: Engine::set_virtual_world + Engine::init keys (engine.cu:21-78, 129-234) */
+int sng_load_virtual_scene(sng_ctx* ctx, const char* json_path);
+int sng_clear_virtual_scene(sng_ctx* ctx);
+/* scalar engine/raytracer parameters by their scene-JSON key ("light_samples", "path_trace_depth",
+ * "syn_shadow_samples", "nerf_shadow_samples", "nerf_shadow_intensity", "exposure", "res_factor",
+ * "vo_scale", "shadow_on_nerf", "shadow_on_virtual_obj", "show_virtual_obj", "show_nerf", "lens_size",
+ * "depth_offset", "syn_shadow_intensity", "nerf_on_nerf_shadow_threshold", ...) and the CLI
+ * flags --sshadows/--nshadows (main.cu:93-126, engine.cuh:29-33) as "sshadows"/"nshadows". */
+int sng_set_param(sng_ctx* ctx, const char* key, double value);
+int sng_get_param(sng_ctx* ctx, const char* key, double* value);
+int sng_get_scene_counts(sng_ctx* ctx, uint32_t* n_objects, uint32_t* n_lights, uint32_t* n_materials);
+int sng_get_object(sng_ctx* ctx, uint32_t i, sng_object_info* out);
+int sng_get_object_bvh(sng_ctx* ctx, uint32_t i, float* nodes_out /* n_nodes x 8 */, float* tris_out /* n_tris x 9 */);
+int sng_get_light(sng_ctx* ctx, uint32_t i, sng_light* out);
+int sng_get_material(sng_ctx* ctx, uint32_t i, sng_material* out);
+
+/* ---- camera: Testbed::set_view_dir / set_look_at / set_scale (testbed.cu:405-425), set_fov (3562) */
+int sng_set_camera_view(sng_ctx* ctx, const float view_dir[3], const float look_at[3], float scale);
+int sng_set_camera_matrix(sng_ctx* ctx, const float m[12]);
+int sng_get_camera_matrix(sng_ctx* ctx, float m[12]);
+int sng_set_fov(sng_ctx* ctx, float degrees);                 /* fov_axis = 1 */
+int sng_get_focal_length(sng_ctx* ctx, int which /*0 nerf,1 mesh*/, float out[2]);
+
+/* ---- frame: Engine::resize + Engine::frame (engine.cu:236-255, 352-433) ---- */
+int sng_set_window(sng_ctx* ctx, int32_t width, int32_t height);
+int sng_get_resolution(sng_ctx* ctx, sng_resolution_info* out);
+int sng_render_frame(sng_ctx* ctx, const sng_frame_params* params, sng_frame_result* out);
+int sng_synchronize(sng_ctx* ctx);
+int sng_copy_to_host(sng_ctx* ctx, const void* d_src, void* h_dst, uint64_t n_bytes);
+/* device-to-device copy on the caller's stream (frame tiles -> collective buffers) */
+int sng_copy_device(sng_ctx* ctx, const void* d_src, void* d_dst, uint64_t n_bytes, void* hip_stream);
+/* curandState_t arrays (init_rand_state, synerfgine/common.cu:22-26) as 6 x u32 (v0..v4, d) per pixel */
+int sng_get_rng_states(sng_ctx* ctx, int which /*0 nerf,1 mesh*/, uint32_t* out, uint64_t n_states);
+int sng_set_rng_states(sng_ctx* ctx, int which, const uint32_t* in, uint64_t n_states);
+
+/* ---- host utilities (A13) -------------------------------------------------- */
+/* TriangleBvhWithBranchingFactor<2>::build (triangle_bvh.cu:615-692): tris reordered in place */
+int sng_bvh_build(float* tris /* n x 9 */, uint32_t n_tris, uint32_t prims_per_leaf, float* nodes_out /* cap x 8 */, uint32_t cap, uint32_t* n_nodes);
+
+#ifdef __cplusplus
+}
+#endif

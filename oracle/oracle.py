@@ -1,0 +1,264 @@
+"""ctypes binding of the CPU ORACLE (oracle/_build/libsng_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg -- never by the product package.  See
+oracle/sng_oracle.h for the parity status (partially pinned).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libsng_oracle.so")
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+class orc_model(ctypes.Structure):
+    _fields_ = [("n_levels", ctypes.c_uint32), ("n_features", ctypes.c_uint32), ("log2_hashmap_size", ctypes.c_uint32),
+                ("base_resolution", ctypes.c_uint32), ("per_level_scale", ctypes.c_float), ("params", ctypes.c_void_p)]
+
+
+class orc_volume(ctypes.Structure):
+    _fields_ = [("render_aabb_min", ctypes.c_float * 3), ("render_aabb_max", ctypes.c_float * 3),
+                ("train_aabb_min", ctypes.c_float * 3), ("train_aabb_max", ctypes.c_float * 3),
+                ("render_aabb_to_local", ctypes.c_float * 9), ("cone_angle_constant", ctypes.c_float),
+                ("max_mip", ctypes.c_uint32), ("min_transmittance", ctypes.c_float), ("bitfield", ctypes.c_void_p)]
+
+
+class orc_camera(ctypes.Structure):
+    _fields_ = [("camera", ctypes.c_float * 12), ("focal", ctypes.c_float * 2), ("screen_center", ctypes.c_float * 2),
+                ("res", ctypes.c_int32 * 2), ("spp", ctypes.c_uint32), ("snap_to_pixel_centers", ctypes.c_int32),
+                ("target_n_queries", ctypes.c_uint32)]
+
+
+class orc_object(ctypes.Structure):
+    _fields_ = [("nodes", ctypes.c_void_p), ("tris", ctypes.c_void_p), ("rot", ctypes.c_float * 9), ("pos", ctypes.c_float * 3),
+                ("scale", ctypes.c_float), ("mat_id", ctypes.c_int32)]
+
+
+class orc_light(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_float * 3), ("intensity", ctypes.c_float), ("size", ctypes.c_float), ("type", ctypes.c_int32)]
+
+
+class orc_material(ctypes.Structure):
+    _fields_ = [("ka", ctypes.c_float * 3), ("kd", ctypes.c_float * 3), ("ks", ctypes.c_float * 3), ("n", ctypes.c_float),
+                ("rg", ctypes.c_float), ("spec_angle", ctypes.c_float), ("type", ctypes.c_int32)]
+
+
+class orc_nerf_stats(ctypes.Structure):
+    _fields_ = [("n_iterations", ctypes.c_uint32), ("n_samples", ctypes.c_uint64), ("n_slots", ctypes.c_uint64),
+                ("n_hit", ctypes.c_uint32), ("alive_per_iter", ctypes.c_uint32 * 64), ("steps_per_iter", ctypes.c_uint32 * 64)]
+
+
+class orc_frame_params(ctypes.Structure):
+    _fields_ = [("nerf_res", ctypes.c_int32 * 2), ("mesh_res", ctypes.c_int32 * 2), ("syn_px_scale", ctypes.c_int32),
+                ("show_nerf", ctypes.c_int32), ("show_virtual_obj", ctypes.c_int32), ("shadow_on_nerf", ctypes.c_int32),
+                ("shadow_on_virtual_obj", ctypes.c_int32), ("nerf_shadow_intensity", ctypes.c_float),
+                ("nerf_on_nerf_shadow_threshold", ctypes.c_float), ("nerf_kernel_size", ctypes.c_int32),
+                ("light_samples", ctypes.c_uint32), ("path_trace_depth", ctypes.c_uint32), ("shadow_iters", ctypes.c_uint32),
+                ("shadow_steps", ctypes.c_uint32), ("lens_angle_constant", ctypes.c_float), ("syn_shadow_factor", ctypes.c_float),
+                ("rt_depth_offset", ctypes.c_float), ("exposure", ctypes.c_float), ("srgb_output", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = ctypes.CDLL(LIB)
+        vp = ctypes.c_void_p
+        u32, u64, f32, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float, ctypes.c_int32
+        sig = {
+            "orc_morton3D": (u32, [u32, u32, u32]), "orc_morton3D_invert": (u32, [u32]), "orc_sobol": (u32, [u32, u32]),
+            "orc_ld_random_val": (f32, [u32, u32, u32]), "orc_ld_random_pixel_offset": (None, [u32, vp]),
+            "orc_float_to_half": (ctypes.c_uint16, [f32]), "orc_half_to_float": (f32, [ctypes.c_uint16]),
+            "orc_xorwow_init": (None, [u64, u64, u64, vp]), "orc_xorwow_init_many": (None, [u64, u32, vp]),
+            "orc_xorwow_next": (u32, [vp]), "orc_curand_uniform": (f32, [vp]),
+            "orc_xorwow_jump_steps_naive": (None, [vp, u64]), "orc_xorwow_jump_matrix": (None, [vp, u32]),
+            "orc_grid_level_table": (u32, [vp, vp, vp]), "orc_n_params": (u32, [vp]),
+            "orc_hashgrid_encode": (None, [vp, vp, u32, u32, vp]), "orc_sh_encode": (None, [vp, u32, u32, u32, vp]),
+            "orc_nerf_inference": (None, [vp, vp, u32, u32, vp]),
+            "orc_density_grid_to_bitfield": (None, [vp, u32, vp, vp]),
+            "orc_render_nerf": (None, [vp, vp, vp, vp, vp, vp, vp, vp]),
+            "orc_shade_nerf_shadows": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, f32, f32, i32]),
+            "orc_bvh_build": (i32, [vp, u32, u32, vp, u32]),
+            "orc_depth_test_world": (None, [vp, u32, vp, vp, u32, vp, vp]),
+            "orc_mesh_init_rays": (None, [vp, vp, vp, vp, vp]),
+            "orc_raytrace": (None, [vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, u32, vp, vp, vp]),
+            "orc_overlay": (None, [vp, vp, vp, vp, vp, vp, vp]),
+            "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
+            "orc_num_threads": (i32, []),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(_lib, name)
+            fn.restype = res
+            fn.argtypes = args
+    return _lib
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+# ---- convenience wrappers -----------------------------------------------------------
+class Model:
+    def __init__(self, cfg, params):
+        self.params = np.ascontiguousarray(params, np.float16)
+        self.s = orc_model(cfg["n_levels"], cfg["n_features_per_level"], cfg["log2_hashmap_size"], cfg["base_resolution"],
+                           cfg["per_level_scale"], self.params.ctypes.data)
+
+    def ref(self):
+        return ctypes.byref(self.s)
+
+
+def level_table(cfg):
+    m = Model(cfg, np.zeros(1, np.float16))
+    offs = np.zeros(cfg["n_levels"] + 1, np.uint32)
+    res = np.zeros(cfg["n_levels"], np.uint32)
+    lib().orc_grid_level_table(m.ref(), ptr(offs), ptr(res))
+    return offs, res
+
+
+def encode(model, coords, stride):
+    n = coords.size // stride
+    out = np.zeros((n, 32), np.uint16)
+    lib().orc_hashgrid_encode(model.ref(), ptr(np.ascontiguousarray(coords, np.float32)), stride, n, ptr(out))
+    return out.view(np.float16)
+
+
+def inference(model, coords, stride=7):
+    c = np.ascontiguousarray(coords, np.float32)
+    n = c.size // stride
+    out = np.zeros((n, 16), np.uint16)
+    lib().orc_nerf_inference(model.ref(), ptr(c), stride, n, ptr(out))
+    return out.view(np.float16)
+
+
+def bitfield(grid_f16, max_cascade=0):
+    g = np.ascontiguousarray(grid_f16, np.float16)
+    bf = np.zeros(128 ** 3 // 8 * 8, np.uint8)
+    mean = ctypes.c_float()
+    lib().orc_density_grid_to_bitfield(ptr(g.view(np.uint16)), max_cascade, ptr(bf), ctypes.byref(mean))
+    return bf, mean.value
+
+
+def xorwow_states(n, seed=1999):
+    st = np.zeros((n, 6), np.uint32)
+    lib().orc_xorwow_init_many(seed, n, ptr(st))
+    return st
+
+
+def make_volume(bf, aabb_scale=1, min_transmittance=0.01):
+    h = 0.5 * min(128, aabb_scale)
+    lo, hi = [0.5 - h] * 3, [0.5 + h] * 3
+    mc = 0
+    while (1 << mc) < aabb_scale:
+        mc += 1
+    v = orc_volume()
+    v.render_aabb_min[:] = lo; v.render_aabb_max[:] = hi
+    v.train_aabb_min[:] = lo; v.train_aabb_max[:] = hi
+    v.render_aabb_to_local[:] = [1, 0, 0, 0, 1, 0, 0, 0, 1]
+    v.cone_angle_constant = 0.0 if aabb_scale <= 1 else 1.0 / 256.0
+    v.max_mip = mc
+    v.min_transmittance = min_transmittance
+    v._bf = bf
+    v.bitfield = bf.ctypes.data
+    return v
+
+
+def make_camera(matrix, focal, res, spp=0, screen_center=(0.5, 0.5), target=0):
+    c = orc_camera()
+    c.camera[:] = list(np.asarray(matrix, np.float32).ravel())
+    c.focal[:] = list(focal)
+    c.screen_center[:] = list(screen_center)
+    c.res[:] = list(res)
+    c.spp = spp
+    c.snap_to_pixel_centers = 0
+    c.target_n_queries = target
+    return c
+
+
+def make_objects(objs):
+    arr = (orc_object * max(1, len(objs)))()
+    keep = []
+    for i, o in enumerate(objs):
+        nodes = np.ascontiguousarray(o["nodes"], np.float32)
+        tris = np.ascontiguousarray(o["tris"], np.float32)
+        keep += [nodes, tris]
+        arr[i].nodes = nodes.ctypes.data
+        arr[i].tris = tris.ctypes.data
+        arr[i].rot[:] = list(np.asarray(o["rot"], np.float32))
+        arr[i].pos[:] = list(np.asarray(o["pos"], np.float32))
+        arr[i].scale = o["scale"]
+        arr[i].mat_id = o["mat_id"]
+    arr._keep = keep
+    return arr
+
+
+def make_lights(lights):
+    arr = (orc_light * max(1, len(lights)))()
+    for i, l in enumerate(lights):
+        arr[i].pos[:] = l["pos"]; arr[i].intensity = l["intensity"]; arr[i].size = l["size"]; arr[i].type = l["type"]
+    return arr
+
+
+def make_materials(mats):
+    arr = (orc_material * max(1, len(mats)))()
+    for i, m in enumerate(mats):
+        arr[i].ka[:] = m["ka"]; arr[i].kd[:] = m["kd"]; arr[i].ks[:] = m["ks"]
+        arr[i].n = m["n"]; arr[i].rg = m["rg"]; arr[i].spec_angle = m["spec_angle"]; arr[i].type = m["type"]
+    return arr
+
+
+def render_nerf(model, vol, cam):
+    W, H = cam.res[0], cam.res[1]
+    rgba = np.zeros((H, W, 4), np.float32)
+    depth = np.zeros((H, W), np.float32)
+    pos = np.zeros((H, W, 3), np.float32)
+    nrm = np.zeros((H, W, 3), np.float32)
+    st = orc_nerf_stats()
+    lib().orc_render_nerf(model.ref(), ctypes.byref(vol), ctypes.byref(cam), ptr(rgba), ptr(depth), ptr(pos), ptr(nrm), ctypes.byref(st))
+    return rgba, depth, pos, nrm, st
+
+
+def frame_params_from_engine(eng):
+    """orc_frame_params mirroring the Engine/RayTracer parameters of a product engine."""
+    r = eng.resolution()
+    p = orc_frame_params()
+    p.nerf_res[:] = list(r["nerf"]); p.mesh_res[:] = list(r["mesh"]); p.syn_px_scale = r["syn_px_scale"]
+    g = eng.get_param
+    p.show_nerf = int(g("show_nerf")); p.show_virtual_obj = int(g("show_virtual_obj"))
+    p.shadow_on_nerf = int(g("shadow_on_nerf")); p.shadow_on_virtual_obj = int(g("shadow_on_virtual_obj"))
+    p.nerf_shadow_intensity = g("nerf_shadow_intensity"); p.nerf_on_nerf_shadow_threshold = g("nerf_on_nerf_shadow_threshold")
+    p.nerf_kernel_size = int(g("nerf_shadow_samples")); p.light_samples = int(g("light_samples"))
+    p.path_trace_depth = int(g("path_trace_depth")); p.shadow_iters = int(g("syn_shadow_samples")); p.shadow_steps = int(g("n_steps"))
+    p.lens_angle_constant = g("lens_size"); p.syn_shadow_factor = g("syn_shadow_intensity"); p.rt_depth_offset = g("depth_offset")
+    p.exposure = g("exposure"); p.srgb_output = int(g("srgb"))
+    return p
+
+
+def render_frame(model, vol, tb, eng, nerf_rng, mesh_rng, spp=0, target=0):
+    """Whole Engine::frame on the CPU with the product's camera/scene/RNG inputs (rng arrays are advanced in place)."""
+    r = eng.resolution()
+    cam = tb.camera_matrix
+    ncam = make_camera(cam, tb.focal_length(0), r["nerf"], spp=spp, target=target)
+    mcam = make_camera(cam, tb.focal_length(1), r["mesh"], spp=spp, target=target)
+    p = frame_params_from_engine(eng)
+    objs, lights, mats = eng.scene()
+    oo, ll, mm = make_objects(objs), make_lights(lights), make_materials(mats)
+    (mw, mh), (nw, nh) = r["mesh"], r["nerf"]
+    final = np.zeros((mh, mw, 4), np.float32); final_d = np.zeros((mh, mw), np.float32)
+    nrgba = np.zeros((nh, nw, 4), np.float32); ndepth = np.zeros((nh, nw), np.float32)
+    st = orc_nerf_stats()
+    lib().orc_render_frame(model.ref(), ctypes.byref(vol), ctypes.byref(ncam), ctypes.byref(mcam), ctypes.byref(p), ctypes.addressof(oo),
+                           len(objs), ctypes.addressof(ll), len(lights), ctypes.addressof(mm), len(mats), ptr(nerf_rng), ptr(mesh_rng), ptr(final), ptr(final_d), ptr(nrgba), ptr(ndepth),
+                           ctypes.byref(st))
+    return dict(final=final, final_depth=final_d, nerf_rgba=nrgba, nerf_depth=ndepth, stats=st)

@@ -1,0 +1,1416 @@
+/*
+ * sng_oracle.cpp -- CPU ORACLE for the SyNeRFgine render hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library; the product
+ * (synerfgine_amd / libsng_hip.so) never links or calls it.
+ *
+ * A deliberately plain, scalar restatement of the reference algorithm,
+ * structured like the reference (wavefront trace_alt loop, per-pixel kernels
+ * as loops) so that it can be read side by side with the cited lines.  All
+ * citations are relative to the reference root (/root/reference).
+ *
+ * Float semantics: IEEE fp32 (built with -ffp-contract=off, no fast-math),
+ * except where the reference evaluates in double through implicit promotion
+ * (cited inline).  The reference itself builds with --use_fast_math
+ * (CMakeLists.txt:82), so results agree with it within the per-pixel
+ * tolerance stated in DESIGN.md, not bitwise.
+ *
+ * Parity: PARTIALLY PINNED -- see sng_oracle.h header and DESIGN.md.
+ */
+#include "sng_oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <stack>
+#include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace {
+
+/* ------------------------------------------------------------------------- */
+/* small vector math, mirroring tcnn's vec/mat semantics [tcnn, unvendored]    */
+/* ------------------------------------------------------------------------- */
+struct V2 { float x, y; };
+struct V3 { float x, y, z; float& operator[](int i) { return (&x)[i]; } float operator[](int i) const { return (&x)[i]; } };
+struct V4 { float x, y, z, w; };
+struct M3 { V3 c[3]; };   /* column-major */
+struct M43 { V3 c[4]; };  /* column-major, c[3] = translation */
+
+inline V3 v3(float x, float y, float z) { return {x, y, z}; }
+inline V3 v3s(float s) { return {s, s, s}; }
+inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+inline V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+inline V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+inline V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline V3 operator*(float s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+inline V3 operator/(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+inline V3 operator+(V3 a, float s) { return {a.x + s, a.y + s, a.z + s}; }
+inline V3 operator-(V3 a, float s) { return {a.x - s, a.y - s, a.z - s}; }
+inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline float length2(V3 a) { return dot(a, a); }
+inline float length(V3 a) { return std::sqrt(dot(a, a)); }
+/* tcnn normalize(): guards zero length by returning the first unit vector [tcnn, unvendored] */
+inline V3 normalize(V3 a) {
+    float l = length(a);
+    if (!(l > 0.0f)) return {1.0f, 0.0f, 0.0f};
+    return a / l;
+}
+inline float vmax(V3 a) { return std::max(std::max(a.x, a.y), a.z); }
+inline V3 vmin3(V3 a, V3 b) { return {std::fmin(a.x, b.x), std::fmin(a.y, b.y), std::fmin(a.z, b.z)}; }
+inline V3 vmax3(V3 a, V3 b) { return {std::fmax(a.x, b.x), std::fmax(a.y, b.y), std::fmax(a.z, b.z)}; }
+/* tmat * tvec: result = 0; result += m[i] * v[i] (column accumulation) [tcnn] */
+inline V3 mul(const M3& m, V3 v) {
+    V3 r = v3s(0.0f);
+    r = r + m.c[0] * v.x;
+    r = r + m.c[1] * v.y;
+    r = r + m.c[2] * v.z;
+    return r;
+}
+inline M3 mulm(const M3& a, const M3& b) { return {{mul(a, b.c[0]), mul(a, b.c[1]), mul(a, b.c[2])}}; }
+inline M3 m3_load(const float* p) { return {{v3(p[0], p[1], p[2]), v3(p[3], p[4], p[5]), v3(p[6], p[7], p[8])}}; }
+inline M43 m43_load(const float* p) { return {{v3(p[0], p[1], p[2]), v3(p[3], p[4], p[5]), v3(p[6], p[7], p[8]), v3(p[9], p[10], p[11])}}; }
+inline M3 m3_of(const M43& m) { return {{m.c[0], m.c[1], m.c[2]}}; }
+inline bool m3_is_identity(const M3& m) {
+    return m.c[0].x == 1 && m.c[0].y == 0 && m.c[0].z == 0 && m.c[1].x == 0 && m.c[1].y == 1 && m.c[1].z == 0 &&
+           m.c[2].x == 0 && m.c[2].y == 0 && m.c[2].z == 1;
+}
+/* glm-style adjugate inverse used by tcnn::inverse(tmat3) [tcnn, unvendored] */
+inline M3 inverse(const M3& m0) {
+    auto m = [&](int i, int j) { return m0.c[i][j]; };
+    float det = m(0, 0) * (m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) - m(1, 0) * (m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) +
+                m(2, 0) * (m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2));
+    M3 r;
+    r.c[0][0] = +(m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2));
+    r.c[1][0] = -(m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2));
+    r.c[2][0] = +(m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1));
+    r.c[0][1] = -(m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2));
+    r.c[1][1] = +(m(0, 0) * m(2, 2) - m(2, 0) * m(0, 2));
+    r.c[2][1] = -(m(0, 0) * m(2, 1) - m(2, 0) * m(0, 1));
+    r.c[0][2] = +(m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2));
+    r.c[1][2] = -(m(0, 0) * m(1, 2) - m(1, 0) * m(0, 2));
+    r.c[2][2] = +(m(0, 0) * m(1, 1) - m(1, 0) * m(0, 1));
+    for (int i = 0; i < 3; ++i) r.c[i] = r.c[i] / det;
+    return r;
+}
+
+inline float fractf(float x) { return x - std::floor(x); } /* random_val.cuh:82-84 */
+inline float logistic(float x) { return 1.0f / (1.0f + std::exp(-x)); } /* [tcnn] */
+inline float smoothstep(float x) { return x * x * (3.0f - 2.0f * x); } /* [tcnn] */
+inline float sgn(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+
+/* ---- constants: nerf_device.cuh:25-43, common_device.cuh:32-33 ----------- */
+constexpr uint32_t NERF_GRIDSIZE = 128;
+constexpr uint32_t NERF_GRID_N_CELLS = NERF_GRIDSIZE * NERF_GRIDSIZE * NERF_GRIDSIZE;
+constexpr uint32_t NERF_STEPS = 1024;
+constexpr uint32_t NERF_CASCADES = 8;
+constexpr float SQRT3 = 1.73205080757f;
+constexpr float STEPSIZE = SQRT3 / NERF_STEPS;
+constexpr float MIN_CONE_STEPSIZE = STEPSIZE;
+constexpr float MAX_CONE_STEPSIZE = STEPSIZE * (1 << (NERF_CASCADES - 1)) * NERF_STEPS / NERF_GRIDSIZE;
+constexpr float NERF_MIN_OPTICAL_THICKNESS = 0.01f;
+constexpr float MAX_DEPTH = 16384.0f;
+constexpr float MIN_DEPTH = 0.00001f;
+constexpr uint32_t MARCH_ITER = 10000;                 /* testbed_nerf.cu:47 */
+constexpr uint32_t MIN_STEPS_INBETWEEN_COMPACTION = 1; /* testbed_nerf.cu:49 */
+constexpr uint32_t MAX_STEPS_INBETWEEN_COMPACTION = 8; /* testbed_nerf.cu:50 */
+constexpr float PI_F = 3.14159265358979323846f;        /* tcnn::PI / random_val.cuh:27 */
+
+/* ------------------------------------------------------------------------- */
+/* fp16 conversion (round-to-nearest-even, subnormals preserved)              */
+/* ------------------------------------------------------------------------- */
+uint16_t half_round_ld(long double v) {
+    uint16_t sign = std::signbit((double)v) ? 0x8000u : 0u;
+    if (std::isnan((double)v)) return (uint16_t)(sign | 0x7e00u);
+    long double av = std::fabs(v);
+    if (av == 0.0L) return sign;
+    if (av >= 65520.0L) return (uint16_t)(sign | 0x7c00u);
+    int e;
+    std::frexp(av, &e); /* av = m*2^e, m in [0.5,1) */
+    int qexp = std::max(e - 1 - 10, -24);
+    long double scaled = std::ldexp(av, -qexp);
+    long double fl = std::floor(scaled);
+    long double rem = scaled - fl;
+    uint64_t h = (uint64_t)fl;
+    if (rem > 0.5L || (rem == 0.5L && (h & 1))) ++h;
+    if (qexp == -24 && h < 1024) return (uint16_t)(sign | h);
+    int E = qexp + 25;
+    if (h == 2048) { h = 1024; ++E; }
+    if (E >= 31) return (uint16_t)(sign | 0x7c00u);
+    return (uint16_t)(sign | (E << 10) | (h - 1024));
+}
+float h2f(uint16_t h) {
+    uint32_t sign = (h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1f;
+    uint32_t m = h & 0x3ff;
+    float r;
+    if (e == 0) r = std::ldexp((float)m, -24);
+    else if (e == 31) r = m ? std::numeric_limits<float>::quiet_NaN() : std::numeric_limits<float>::infinity();
+    else r = std::ldexp((float)(m | 0x400), (int)e - 25);
+    uint32_t bits;
+    std::memcpy(&bits, &r, 4);
+    bits |= sign;
+    std::memcpy(&r, &bits, 4);
+    return r;
+}
+inline uint16_t f2h(float f) { return half_round_ld((long double)f); }
+/* fused half fma: one rounding of the exact a*b+c, as __hfma / v_fma_f16 */
+inline uint16_t hfma(uint16_t a, uint16_t b, uint16_t c) {
+    long double r = (long double)h2f(a) * (long double)h2f(b) + (long double)h2f(c);
+    return half_round_ld(r);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Morton codes [tcnn common_device.h, unvendored; SURVEY Appendix C]         */
+/* ------------------------------------------------------------------------- */
+inline uint32_t expand_bits(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+inline uint32_t morton3D(uint32_t x, uint32_t y, uint32_t z) { return expand_bits(x) | (expand_bits(y) << 1) | (expand_bits(z) << 2); }
+inline uint32_t morton3D_invert(uint32_t x) {
+    x = x & 0x49249249u;
+    x = (x | (x >> 2)) & 0xc30c30c3u;
+    x = (x | (x >> 4)) & 0x0f00f00fu;
+    x = (x | (x >> 8)) & 0xff0000ffu;
+    x = (x | (x >> 16)) & 0x0000ffffu;
+    return x;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Scrambled Sobol: random_val.cuh:162-325                                    */
+/* ------------------------------------------------------------------------- */
+const uint32_t SOBOL_DIRECTIONS[5][32] = {
+    {0x80000000, 0x40000000, 0x20000000, 0x10000000, 0x08000000, 0x04000000, 0x02000000, 0x01000000,
+     0x00800000, 0x00400000, 0x00200000, 0x00100000, 0x00080000, 0x00040000, 0x00020000, 0x00010000,
+     0x00008000, 0x00004000, 0x00002000, 0x00001000, 0x00000800, 0x00000400, 0x00000200, 0x00000100,
+     0x00000080, 0x00000040, 0x00000020, 0x00000010, 0x00000008, 0x00000004, 0x00000002, 0x00000001},
+    {0x80000000, 0xc0000000, 0xa0000000, 0xf0000000, 0x88000000, 0xcc000000, 0xaa000000, 0xff000000,
+     0x80800000, 0xc0c00000, 0xa0a00000, 0xf0f00000, 0x88880000, 0xcccc0000, 0xaaaa0000, 0xffff0000,
+     0x80008000, 0xc000c000, 0xa000a000, 0xf000f000, 0x88008800, 0xcc00cc00, 0xaa00aa00, 0xff00ff00,
+     0x80808080, 0xc0c0c0c0, 0xa0a0a0a0, 0xf0f0f0f0, 0x88888888, 0xcccccccc, 0xaaaaaaaa, 0xffffffff},
+    {0x80000000, 0xc0000000, 0x60000000, 0x90000000, 0xe8000000, 0x5c000000, 0x8e000000, 0xc5000000,
+     0x68800000, 0x9cc00000, 0xee600000, 0x55900000, 0x80680000, 0xc09c0000, 0x60ee0000, 0x90550000,
+     0xe8808000, 0x5cc0c000, 0x8e606000, 0xc5909000, 0x6868e800, 0x9c9c5c00, 0xeeee8e00, 0x5555c500,
+     0x8000e880, 0xc0005cc0, 0x60008e60, 0x9000c590, 0xe8006868, 0x5c009c9c, 0x8e00eeee, 0xc5005555},
+    {0x80000000, 0xc0000000, 0x20000000, 0x50000000, 0xf8000000, 0x74000000, 0xa2000000, 0x93000000,
+     0xd8800000, 0x25400000, 0x59e00000, 0xe6d00000, 0x78080000, 0xb40c0000, 0x82020000, 0xc3050000,
+     0x208f8000, 0x51474000, 0xfbea2000, 0x75d93000, 0xa0858800, 0x914e5400, 0xdbe79e00, 0x25db6d00,
+     0x58800080, 0xe54000c0, 0x79e00020, 0xb6d00050, 0x800800f8, 0xc00c0074, 0x200200a2, 0x50050093},
+    {0x80000000, 0x40000000, 0x20000000, 0xb0000000, 0xf8000000, 0xdc000000, 0x7a000000, 0x9d000000,
+     0x5a800000, 0x2fc00000, 0xa1600000, 0xf0b00000, 0xda880000, 0x6fc40000, 0x81620000, 0x40bb0000,
+     0x22878000, 0xb3c9c000, 0xfb65a000, 0xddb2d000, 0x78022800, 0x9c0b3c00, 0x5a0fb600, 0x2d0ddb00,
+     0xa2878080, 0xf3c9c040, 0xdb65a020, 0x6db2d0b0, 0x800228f8, 0x400b3cdc, 0x200fb67a, 0xb00ddb9d},
+};
+inline uint32_t sobol(uint32_t index, uint32_t dim) {
+    uint32_t X = 0;
+    for (uint32_t bit = 0; bit < 32; bit++) X ^= ((index >> bit) & 1u) * SOBOL_DIRECTIONS[dim][bit];
+    return X;
+}
+inline uint32_t hash_combine(uint32_t seed, uint32_t v) { return seed ^ (v + (seed << 6) + (seed >> 2)); }
+inline uint32_t reverse_bits(uint32_t x) {
+    x = (((x & 0xaaaaaaaau) >> 1) | ((x & 0x55555555u) << 1));
+    x = (((x & 0xccccccccu) >> 2) | ((x & 0x33333333u) << 2));
+    x = (((x & 0xf0f0f0f0u) >> 4) | ((x & 0x0f0f0f0fu) << 4));
+    x = (((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8));
+    return ((x >> 16) | (x << 16));
+}
+inline uint32_t laine_karras_permutation(uint32_t x, uint32_t seed) {
+    x += seed;
+    x ^= x * 0x6c50b47cu;
+    x ^= x * 0xb82f1e52u;
+    x ^= x * 0xc7afe638u;
+    x ^= x * 0x8d22f6e6u;
+    return x;
+}
+inline uint32_t nested_uniform_scramble_base2(uint32_t x, uint32_t seed) {
+    x = reverse_bits(x);
+    x = laine_karras_permutation(x, seed);
+    return reverse_bits(x);
+}
+inline float ld_random_val(uint32_t index, uint32_t seed, uint32_t dim = 0) {
+    constexpr float S = float(1.0 / (1ull << 32));
+    index = nested_uniform_scramble_base2(index, seed);
+    return (float)nested_uniform_scramble_base2(sobol(index, dim), hash_combine(seed, dim)) * S;
+}
+inline V2 ld_random_val_2d(uint32_t index, uint32_t seed) {
+    constexpr float S = float(1.0 / (1ull << 32));
+    index = nested_uniform_scramble_base2(index, seed);
+    uint32_t x0 = nested_uniform_scramble_base2(sobol(index, 0), hash_combine(seed, 0));
+    uint32_t x1 = nested_uniform_scramble_base2(sobol(index, 1), hash_combine(seed, 1));
+    return {(float)x0 * S, (float)x1 * S};
+}
+inline V2 ld_random_pixel_offset(uint32_t spp) { /* random_val.cuh:320-325 */
+    V2 a = ld_random_val_2d(0, 0xdeadbeef), b = ld_random_val_2d(spp, 0xdeadbeef);
+    V2 o = {0.5f - a.x + b.x, 0.5f - a.y + b.y};
+    return {fractf(o.x), fractf(o.y)};
+}
+
+/* ------------------------------------------------------------------------- */
+/* cuRAND XORWOW [cuRAND, unvendored]: SURVEY Appendix C                       */
+/* ------------------------------------------------------------------------- */
+struct Gf2Mat { uint32_t col[160][5]; }; /* column j = image of basis vector e_j */
+void gf2_apply(const Gf2Mat& m, const uint32_t in[5], uint32_t out[5]) {
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int j = 0; j < 160; ++j)
+        if ((in[j >> 5] >> (j & 31)) & 1u)
+            for (int w = 0; w < 5; ++w) r[w] ^= m.col[j][w];
+    std::memcpy(out, r, sizeof(r));
+}
+void xorwow_step_v(uint32_t v[5]) {
+    uint32_t t = v[0] ^ (v[0] >> 2);
+    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+    v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+}
+Gf2Mat gf2_mul(const Gf2Mat& a, const Gf2Mat& b) {
+    Gf2Mat r;
+    for (int j = 0; j < 160; ++j) gf2_apply(a, b.col[j], r.col[j]);
+    return r;
+}
+struct XorwowTables {
+    Gf2Mat step_pow[64];   /* M^(2^i) */
+    Gf2Mat seq_pow[32];    /* M^(2^67 * 2^i) */
+    XorwowTables() {
+        Gf2Mat m;
+        for (int j = 0; j < 160; ++j) {
+            uint32_t v[5] = {0, 0, 0, 0, 0};
+            v[j >> 5] = 1u << (j & 31);
+            xorwow_step_v(v);
+            std::memcpy(m.col[j], v, sizeof(v));
+        }
+        step_pow[0] = m;
+        for (int i = 1; i < 64; ++i) step_pow[i] = gf2_mul(step_pow[i - 1], step_pow[i - 1]);
+        Gf2Mat a = step_pow[63];
+        for (int i = 63; i < 67; ++i) a = gf2_mul(a, a); /* M^(2^67) */
+        seq_pow[0] = a;
+        for (int i = 1; i < 32; ++i) seq_pow[i] = gf2_mul(seq_pow[i - 1], seq_pow[i - 1]);
+    }
+};
+const XorwowTables& xorwow_tables() {
+    static XorwowTables* t = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] { t = new XorwowTables(); });
+    return *t;
+}
+/* curand_init(seed, subsequence, offset): curand_kernel.h _curand_init_scratch */
+void xorwow_init(uint64_t seed, uint64_t subsequence, uint64_t offset, uint32_t st[6]) {
+    uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49u;
+    uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddu;
+    uint32_t t0 = 1099087573u * s0;
+    uint32_t t1 = 2591861531u * s1;
+    uint32_t v[5] = {123456789u + t0, 362436069u ^ t0, 521288629u + t1, 88675123u ^ t1, 5783321u + t0};
+    uint32_t d = 6615241u + t1 + t0;
+    const XorwowTables& T = xorwow_tables();
+    for (int i = 0; i < 32 && subsequence; ++i, subsequence >>= 1)
+        if (subsequence & 1) gf2_apply(T.seq_pow[i], v, v);
+    uint64_t off = offset;
+    for (int i = 0; i < 64 && off; ++i, off >>= 1)
+        if (off & 1) gf2_apply(T.step_pow[i], v, v);
+    d += (uint32_t)(offset * 362437ull);
+    std::memcpy(st, v, sizeof(v));
+    st[5] = d;
+}
+inline uint32_t xorwow_next(uint32_t* st) {
+    uint32_t t = st[0] ^ (st[0] >> 2);
+    st[0] = st[1]; st[1] = st[2]; st[2] = st[3]; st[3] = st[4];
+    st[4] = (st[4] ^ (st[4] << 4)) ^ (t ^ (t << 1));
+    st[5] += 362437u;
+    return st[4] + st[5];
+}
+/* curand_uniform: x * 2^-32 + 2^-33  (CURAND_2POW32_INV = 2.3283064e-10f) */
+inline float curand_uniform(uint32_t* st) {
+    const float INV = 2.3283064e-10f;
+    return (float)xorwow_next(st) * INV + (INV / 2.0f);
+}
+
+/* ------------------------------------------------------------------------- */
+/* AABB: bounding_box.cuh:163-222                                              */
+/* ------------------------------------------------------------------------- */
+struct BBox { V3 min, max; };
+inline V2 bb_ray_intersect(const BBox& b, V3 pos, V3 dir) {
+    float tmin = (b.min.x - pos.x) / dir.x;
+    float tmax = (b.max.x - pos.x) / dir.x;
+    if (tmin > tmax) std::swap(tmin, tmax);
+    float tymin = (b.min.y - pos.y) / dir.y;
+    float tymax = (b.max.y - pos.y) / dir.y;
+    if (tymin > tymax) std::swap(tymin, tymax);
+    const float FMAX = std::numeric_limits<float>::max();
+    if (tmin > tymax || tymin > tmax) return {FMAX, FMAX};
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = (b.min.z - pos.z) / dir.z;
+    float tzmax = (b.max.z - pos.z) / dir.z;
+    if (tzmin > tzmax) std::swap(tzmin, tzmax);
+    if (tmin > tzmax || tzmin > tmax) return {FMAX, FMAX};
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    return {tmin, tmax};
+}
+inline bool bb_contains(const BBox& b, V3 p) {
+    return p.x >= b.min.x && p.x <= b.max.x && p.y >= b.min.y && p.y <= b.max.y && p.z >= b.min.z && p.z <= b.max.z;
+}
+
+/* ------------------------------------------------------------------------- */
+/* occupancy stepping: nerf_device.cuh:266-495                                 */
+/* ------------------------------------------------------------------------- */
+inline V3 warp_position(V3 pos, const BBox& aabb) { return (pos - aabb.min) / (aabb.max - aabb.min); }
+inline V3 unwarp_position(V3 pos, const BBox& aabb) { return aabb.min + pos * (aabb.max - aabb.min); }
+inline V3 warp_direction(V3 dir) { return (dir + 1.0f) * 0.5f; }
+inline float warp_dt(float dt) {
+    float max_stepsize = MIN_CONE_STEPSIZE * (1 << (NERF_CASCADES - 1));
+    return (dt - MIN_CONE_STEPSIZE) / (max_stepsize - MIN_CONE_STEPSIZE);
+}
+inline float unwarp_dt(float dt) {
+    float max_stepsize = MIN_CONE_STEPSIZE * (1 << (NERF_CASCADES - 1));
+    return dt * (max_stepsize - MIN_CONE_STEPSIZE) + MIN_CONE_STEPSIZE;
+}
+inline uint32_t cascaded_grid_idx_at(V3 pos, uint32_t mip) {
+    float mip_scale = std::scalbn(1.0f, -(int)mip);
+    pos = pos - v3s(0.5f);
+    pos = pos * mip_scale;
+    pos = pos + v3s(0.5f);
+    V3 f = pos * (float)NERF_GRIDSIZE;
+    int ix = (int)f.x, iy = (int)f.y, iz = (int)f.z;
+    if (ix < 0 || ix >= (int)NERF_GRIDSIZE || iy < 0 || iy >= (int)NERF_GRIDSIZE || iz < 0 || iz >= (int)NERF_GRIDSIZE) return 0xFFFFFFFFu;
+    return morton3D(ix, iy, iz);
+}
+inline bool density_grid_occupied_at(V3 pos, const uint8_t* bf, uint32_t mip) {
+    uint32_t idx = cascaded_grid_idx_at(pos, mip);
+    if (idx == 0xFFFFFFFFu) return false;
+    return bf[idx / 8 + (NERF_GRID_N_CELLS * mip) / 8] & (1 << (idx % 8));
+}
+inline float distance_to_next_voxel(V3 pos, V3 dir, V3 idir, float res) {
+    V3 p = res * (pos - 0.5f);
+    float tx = (std::floor(p.x + 0.5f + 0.5f * sgn(dir.x)) - p.x) * idir.x;
+    float ty = (std::floor(p.y + 0.5f + 0.5f * sgn(dir.y)) - p.y) * idir.y;
+    float tz = (std::floor(p.z + 0.5f + 0.5f * sgn(dir.z)) - p.z) * idir.z;
+    float t = std::min(std::min(tx, ty), tz);
+    return std::fmax(t / res, 0.0f);
+}
+inline float to_stepping_space(float t, float cone_angle) {
+    if (cone_angle <= 1e-5f) return t / MIN_CONE_STEPSIZE;
+    float log1p_c = std::log(1.0f + cone_angle);
+    float a = (std::log(MIN_CONE_STEPSIZE) - std::log(log1p_c)) / log1p_c;
+    float b = (std::log(MAX_CONE_STEPSIZE) - std::log(log1p_c)) / log1p_c;
+    float at = std::exp(a * log1p_c);
+    float bt = std::exp(b * log1p_c);
+    if (t <= at) return (t - at) / MIN_CONE_STEPSIZE + a;
+    else if (t <= bt) return std::log(t) / log1p_c;
+    else return (t - bt) / MAX_CONE_STEPSIZE + b;
+}
+inline float from_stepping_space(float n, float cone_angle) {
+    if (cone_angle <= 1e-5f) return n * MIN_CONE_STEPSIZE;
+    float log1p_c = std::log(1.0f + cone_angle);
+    float a = (std::log(MIN_CONE_STEPSIZE) - std::log(log1p_c)) / log1p_c;
+    float b = (std::log(MAX_CONE_STEPSIZE) - std::log(log1p_c)) / log1p_c;
+    float at = std::exp(a * log1p_c);
+    float bt = std::exp(b * log1p_c);
+    if (n <= a) return (n - a) * MIN_CONE_STEPSIZE + at;
+    else if (n <= b) return std::exp(n * log1p_c);
+    else return (n - b) * MAX_CONE_STEPSIZE + bt;
+}
+inline float advance_n_steps(float t, float cone_angle, float n) { return from_stepping_space(to_stepping_space(t, cone_angle) + n, cone_angle); }
+inline float calc_dt(float t, float cone_angle) { return advance_n_steps(t, cone_angle, 1.0f) - t; }
+inline float advance_to_next_voxel(float t, float cone_angle, V3 pos, V3 dir, V3 idir, uint32_t mip) {
+    float res = std::scalbn((float)NERF_GRIDSIZE, -(int)mip);
+    float t_target = t + distance_to_next_voxel(pos, dir, idir, res);
+    t = to_stepping_space(t, cone_angle);
+    t_target = to_stepping_space(t_target, cone_angle);
+    return from_stepping_space(t + std::ceil(std::fmax(t_target - t, 0.5f)), cone_angle);
+}
+inline uint32_t mip_from_pos(V3 pos, uint32_t max_cascade) {
+    int exponent;
+    V3 d = pos - 0.5f;
+    float maxval = vmax(v3(std::fabs(d.x), std::fabs(d.y), std::fabs(d.z)));
+    std::frexp(maxval, &exponent);
+    return (uint32_t)std::min(std::max(exponent + 1, 0), (int)max_cascade);
+}
+struct Volume {
+    BBox render_aabb, train_aabb;
+    M3 to_local;
+    bool to_local_identity;
+    float cone;
+    uint32_t max_mip;
+    float min_transmittance;
+    const uint8_t* bitfield;
+};
+inline V3 to_local(const Volume& v, V3 p) { return v.to_local_identity ? p : mul(v.to_local, p); }
+float if_unoccupied_advance_to_next_occupied_voxel(float t, float cone_angle, V3 o, V3 d, V3 idir, const uint8_t* grid,
+                                                   uint32_t min_mip, uint32_t max_mip, const Volume& vol) {
+    while (true) {
+        V3 pos = o + d * t;
+        if (t >= MAX_DEPTH || !bb_contains(vol.render_aabb, to_local(vol, pos))) return MAX_DEPTH;
+        uint32_t mip = std::min(std::max(mip_from_pos(pos, NERF_CASCADES - 1), min_mip), max_mip);
+        if (!grid || density_grid_occupied_at(pos, grid, mip)) return t;
+        while (mip < max_mip && !density_grid_occupied_at(pos, grid, mip + 1)) ++mip;
+        t = advance_to_next_voxel(t, cone_angle, pos, d, idir, mip);
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* Network: NerfNetwork::inference_mixed_precision (nerf_network.h:105-139)   */
+/*   hash grid [tcnn GridEncoding, unvendored], SH deg 4 [tcnn], 2 MLPs       */
+/*   [tcnn FullyFusedMLP], extract_density (nerf_network.h:31-43)             */
+/* ------------------------------------------------------------------------- */
+struct Grid {
+    uint32_t L, F, log2T, Nmin;
+    float pls, log2_pls;
+    std::vector<uint32_t> offsets; /* L+1, in entries */
+    std::vector<uint32_t> res;
+    std::vector<float> scale;
+    const uint16_t* params;        /* grid params (entries x F) */
+};
+inline float grid_scale(uint32_t level, float log2_pls, uint32_t base_res) {
+    /* exp2f(level*log2(b)) * Nmin - 1, contracted to an fma as nvcc does */
+    return std::fma(std::exp2((float)level * log2_pls), (float)base_res, -1.0f);
+}
+inline uint32_t grid_resolution(float scale) { return (uint32_t)std::ceil(scale) + 1; }
+Grid make_grid(const orc_model* m) {
+    Grid g;
+    g.L = m->n_levels; g.F = m->n_features; g.log2T = m->log2_hashmap_size; g.Nmin = m->base_resolution;
+    g.pls = m->per_level_scale;
+    g.log2_pls = std::log2(m->per_level_scale);
+    uint32_t offset = 0;
+    for (uint32_t i = 0; i < g.L; ++i) {
+        float sc = grid_scale(i, g.log2_pls, g.Nmin);
+        uint32_t r = grid_resolution(sc);
+        uint32_t max_params = std::numeric_limits<uint32_t>::max() / 2;
+        uint32_t pil = std::pow((float)r, 3.0f) > (float)max_params ? max_params : r * r * r;
+        pil = (pil + 7u) / 8u * 8u;
+        pil = std::min(pil, 1u << g.log2T);
+        g.offsets.push_back(offset);
+        g.res.push_back(r);
+        g.scale.push_back(sc);
+        offset += pil;
+    }
+    g.offsets.push_back(offset);
+    g.params = m->params + 3072 + 7168;
+    return g;
+}
+inline uint32_t grid_index(uint32_t hashmap_size, uint32_t res, const uint32_t pg[3]) {
+    uint32_t stride = 1, index = 0;
+    for (uint32_t dim = 0; dim < 3 && stride <= hashmap_size; ++dim) {
+        index += pg[dim] * stride;
+        stride *= res;
+    }
+    if (hashmap_size < stride) index = (pg[0] * 1u) ^ (pg[1] * 2654435761u) ^ (pg[2] * 805459861u);
+    return index % hashmap_size;
+}
+void encode_one(const Grid& g, const float* x, uint16_t* out /* L*F */) {
+    for (uint32_t level = 0; level < g.L; ++level) {
+        const uint16_t* grid = g.params + (size_t)g.offsets[level] * g.F;
+        uint32_t hashmap_size = g.offsets[level + 1] - g.offsets[level];
+        float scale = g.scale[level];
+        uint32_t res = g.res[level];
+        float pos[3];
+        uint32_t pg[3];
+        for (int d = 0; d < 3; ++d) {
+            float p = std::fma(scale, x[d], 0.5f);
+            float tmp = std::floor(p);
+            pg[d] = (uint32_t)(int)tmp;
+            pos[d] = p - tmp;
+        }
+        uint16_t result[8] = {0};
+        for (uint32_t idx = 0; idx < 8; ++idx) {
+            float weight = 1.0f;
+            uint32_t pl[3];
+            for (uint32_t d = 0; d < 3; ++d) {
+                if ((idx & (1u << d)) == 0) { weight *= 1.0f - pos[d]; pl[d] = pg[d]; }
+                else { weight *= pos[d]; pl[d] = pg[d] + 1; }
+            }
+            uint32_t index = grid_index(hashmap_size, res, pl) * g.F;
+            uint16_t wh = f2h(weight);
+            for (uint32_t f = 0; f < g.F; ++f) result[f] = hfma(wh, grid[index + f], result[f]);
+        }
+        for (uint32_t f = 0; f < g.F; ++f) out[level * g.F + f] = result[f];
+    }
+}
+void sh_one(float dx, float dy, float dz, uint16_t* o) {
+    float x = dx * 2.f - 1.f, y = dy * 2.f - 1.f, z = dz * 2.f - 1.f;
+    float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+    o[0] = f2h(0.28209479177387814f);
+    o[1] = f2h(-0.48860251190291987f * y);
+    o[2] = f2h(0.48860251190291987f * z);
+    o[3] = f2h(-0.48860251190291987f * x);
+    o[4] = f2h(1.0925484305920792f * xy);
+    o[5] = f2h(-1.0925484305920792f * yz);
+    o[6] = f2h(0.94617469575755997f * z2 - 0.31539156525251999f);
+    o[7] = f2h(-1.0925484305920792f * xz);
+    o[8] = f2h(0.54627421529603959f * x2 - 0.54627421529603959f * y2);
+    o[9] = f2h(0.59004358992664352f * y * (-3.0f * x2 + y2));
+    o[10] = f2h(2.8906114426405538f * xy * z);
+    o[11] = f2h(0.45704579946446572f * y * (1.0f - 5.0f * z2));
+    o[12] = f2h(0.3731763325901154f * z * (5.0f * z2 - 3.0f));
+    o[13] = f2h(0.45704579946446572f * x * (1.0f - 5.0f * z2));
+    o[14] = f2h(1.4453057213202769f * z * (x2 - y2));
+    o[15] = f2h(0.59004358992664352f * x * (-x2 + 3.0f * y2));
+}
+/* dense layer y = W x (W row-major [n_out][n_in], fp16), fp32 accumulation,
+ * optional ReLU, result rounded to fp16 [tcnn FullyFusedMLP, unvendored] */
+void dense(const uint16_t* W, uint32_t n_out, uint32_t n_in, const uint16_t* x, uint16_t* y, bool relu) {
+    for (uint32_t o = 0; o < n_out; ++o) {
+        float acc = 0.0f;
+        for (uint32_t k = 0; k < n_in; ++k) acc += h2f(W[o * n_in + k]) * h2f(x[k]);
+        if (relu && acc < 0.0f) acc = 0.0f;
+        y[o] = f2h(acc);
+    }
+}
+/* one sample; coords = NerfCoordinate {pos(3), dt, dir(3)} (nerf_device.cuh:176-202);
+ * out16 = the 16 fp16 outputs of the rgb network with row 3 replaced by density (extract_density) */
+void network_one(const orc_model* m, const Grid& g, const float* coord, uint16_t* out16) {
+    const uint16_t* dW0 = m->params;           /* density W0 [64][32] */
+    const uint16_t* dW1 = dW0 + 64 * 32;       /* density W1 [16][64] */
+    const uint16_t* rW0 = m->params + 3072;    /* rgb W0 [64][32] */
+    const uint16_t* rW1 = rW0 + 64 * 32;       /* rgb W1 [64][64] */
+    const uint16_t* rW2 = rW1 + 64 * 64;       /* rgb W2 [16][64] */
+    uint16_t enc[32], h[64], h2[64], rgb_in[32], out[16];
+    encode_one(g, coord, enc);
+    dense(dW0, 64, 32, enc, h, true);
+    dense(dW1, 16, 64, h, rgb_in, false);       /* density_network_output = rgb_network_input rows 0..15 */
+    sh_one(coord[4], coord[5], coord[6], rgb_in + 16);
+    dense(rW0, 64, 32, rgb_in, h, true);
+    dense(rW1, 64, 64, h, h2, true);
+    dense(rW2, 16, 64, h2, out, false);
+    out[3] = rgb_in[0];                          /* extract_density: nerf_network.h:132-138 */
+    std::memcpy(out16, out, sizeof(out));
+}
+
+/* ------------------------------------------------------------------------- */
+/* BVH: triangle_bvh.cu:165-319 (traversal), 615-718 (build)                   */
+/* ------------------------------------------------------------------------- */
+struct Tri { V3 a, b, c; };
+struct Node { BBox bb; int left, right; };
+inline float tri_intersect(const Tri& tr, V3 ro, V3 rd) { /* triangle.cuh:45-59 */
+    V3 v1v0 = tr.b - tr.a, v2v0 = tr.c - tr.a, rov0 = ro - tr.a;
+    V3 n = cross(v1v0, v2v0);
+    V3 q = cross(rov0, rd);
+    float d = 1.0f / dot(rd, n);
+    float u = d * -dot(q, v2v0);
+    float v = d * dot(q, v1v0);
+    float t = d * -dot(n, rov0);
+    if (u < 0.0f || u > 1.0f || v < 0.0f || (u + v) > 1.0f || t < 0.0f) t = std::numeric_limits<float>::max();
+    return t;
+}
+inline V3 tri_normal(const Tri& t) { return normalize(cross(t.b - t.a, t.c - t.a)); }
+inline V3 tri_centroid(const Tri& t) { return (t.a + t.b + t.c) / 3.0f; }
+inline float tri_centroid_axis(const Tri& t, int axis) { return (t.a[axis] + t.b[axis] + t.c[axis]) / 3; }
+inline M3 tri_perturb(const Tri& t) { /* triangle.cuh:164-170 */
+    V3 N = tri_normal(t);
+    V3 T = normalize(tri_centroid(t) - t.a);
+    V3 B = cross(T, N);
+    return {{T, B, N}};
+}
+struct Object {
+    const float* nodes;
+    const Tri* tris;
+    M3 rot; V3 pos; float scale; int mat_id;
+    M3 world_to_obj; /* (I/scale) * inverse(rot) -- hoisted, same float ops (triangle_bvh.cu:313-319) */
+};
+inline Node load_node(const float* p, int idx) {
+    const float* n = p + 8 * idx;
+    Node r;
+    r.bb.min = v3(n[0], n[1], n[2]);
+    r.bb.max = v3(n[3], n[4], n[5]);
+    std::memcpy(&r.left, &n[6], 4);
+    std::memcpy(&r.right, &n[7], 4);
+    return r;
+}
+/* ray_intersect_nodes_f<2>: triangle_bvh.cu:263-307 */
+std::pair<int, float> ray_intersect_nodes(V3 ro, V3 rd, const float* nodes, const Tri* tris) {
+    int stack[32];
+    int count = 0;
+    stack[count++] = 0;
+    float mint = MAX_DEPTH;
+    int shortest = -1;
+    while (count > 0) {
+        int idx = stack[--count];
+        Node node = load_node(nodes, idx);
+        if (node.left < 0) {
+            int end = -node.right - 1;
+            for (int i = -node.left - 1; i < end; ++i) {
+                float t = tri_intersect(tris[i], ro, rd);
+                if (t < mint) { mint = t; shortest = i; }
+            }
+        } else {
+            struct DI { float dist; int idx; } ch[2];
+            for (int i = 0; i < 2; ++i) ch[i] = {bb_ray_intersect(load_node(nodes, node.left + i).bb, ro, rd).x, node.left + i};
+            if (ch[0].dist < ch[1].dist) std::swap(ch[0], ch[1]); /* sorting_network<2>: descending */
+            for (int i = 0; i < 2; ++i)
+                if (ch[i].dist < mint) {
+                    if (count >= 31) std::fprintf(stderr, "WARNING TOO BIG\n");
+                    stack[count++] = ch[i].idx;
+                }
+        }
+    }
+    return {shortest, mint};
+}
+std::pair<int, float> ray_intersect_object(V3 ro, V3 rd, const Object& o) {
+    V3 oro = mul(o.world_to_obj, ro - o.pos);
+    V3 ord = mul(o.world_to_obj, rd);
+    return ray_intersect_nodes(oro, ord, o.nodes, o.tris);
+}
+Object make_object(const orc_object& s) {
+    Object o;
+    o.nodes = s.nodes;
+    o.tris = (const Tri*)s.tris;
+    o.rot = m3_load(s.rot);
+    o.pos = v3(s.pos[0], s.pos[1], s.pos[2]);
+    o.scale = s.scale;
+    o.mat_id = s.mat_id;
+    M3 msc = {{v3(1.0f / s.scale, 0.0f / s.scale, 0.0f / s.scale), v3(0.0f / s.scale, 1.0f / s.scale, 0.0f / s.scale),
+               v3(0.0f / s.scale, 0.0f / s.scale, 1.0f / s.scale)}};
+    o.world_to_obj = mulm(msc, inverse(o.rot));
+    return o;
+}
+struct HitRecord {
+    V3 pos = v3s(0.0f), normal = v3s(0.0f);
+    M3 perturb = {{v3(1, 0, 0), v3(0, 1, 0), v3(0, 0, 1)}};
+    float t = MAX_DEPTH;
+    int material_idx = -1, object_idx = -1;
+    bool front_face = true;
+};
+/* sng::depth_test_world: synerfgine/common.cu:36-48 */
+float depth_test_world(V3 origin, V3 dir, const std::vector<Object>& objs, int& out_obj) {
+    float depth = MAX_DEPTH;
+    V3 off = origin + dir * MIN_DEPTH;
+    for (size_t c = 0; c < objs.size(); ++c) {
+        auto r = ray_intersect_object(off, dir, objs[c]);
+        if (r.second < depth && r.second > MIN_DEPTH) { out_obj = (int)c; depth = r.second; }
+    }
+    return depth;
+}
+/* sng::depth_test_world (+HitRecord): synerfgine/common.cu:50-67 */
+float depth_test_world_hit(V3 origin, V3 dir, const std::vector<Object>& objs, int& out_obj, HitRecord& h) {
+    V3 off = origin + dir * MIN_DEPTH;
+    for (size_t c = 0; c < objs.size(); ++c) {
+        const Object& obj = objs[c];
+        auto r = ray_intersect_object(off, dir, obj);
+        if (r.second < h.t && r.second > MIN_DEPTH) {
+            out_obj = (int)c;
+            h.t = r.second;
+            h.material_idx = obj.mat_id;
+            h.normal = mul(obj.rot, tri_normal(obj.tris[r.first]));
+            h.perturb = tri_perturb(obj.tris[r.first]);
+            h.object_idx = (int)c;
+        }
+    }
+    h.pos = origin + h.t * dir;
+    h.front_face = dot(dir, h.normal) < 0.0f;
+    return h.t;
+}
+/* sng::depth_test_nerf (full_d form): synerfgine/common.cu:69-83 */
+float depth_test_nerf_fd(float full_d, uint32_t n_steps, float cone, V3 src, V3 L, V3 invL, const Volume& vol, uint32_t min_mip, uint32_t max_mip) {
+    float s = 0.0f;
+    for (uint32_t j = 0; j < n_steps; ++j) {
+        s = if_unoccupied_advance_to_next_occupied_voxel(s, cone, src, L, invL, vol.bitfield, min_mip, max_mip, vol);
+        if (s >= full_d) { s = full_d; break; }
+        s += calc_dt(s, cone);
+    }
+    return s;
+}
+/* sng::depth_test_nerf (src,dst form): synerfgine/common.cu:85-102 */
+float depth_test_nerf_sd(uint32_t n_steps, float cone, V3 src, V3 dst, const Volume& vol, uint32_t min_mip, uint32_t max_mip) {
+    float full_d = length(dst - src);
+    V3 L = normalize(dst - src);
+    V3 invL = v3(1.0f / L.x, 1.0f / L.y, 1.0f / L.z);
+    return depth_test_nerf_fd(full_d, n_steps, cone, src, L, invL, vol, min_mip, max_mip);
+}
+
+/* sRGB: common_device.cuh:35-70 */
+inline float srgb_to_linear(float s) { return s <= 0.04045f ? s / 12.92f : std::pow((s + 0.055f) / 1.055f, 2.4f); }
+inline float linear_to_srgb(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * std::pow(l, 0.41666f) - 0.055f; }
+
+Volume make_volume(const orc_volume* v) {
+    Volume vol;
+    vol.render_aabb = {v3(v->render_aabb_min[0], v->render_aabb_min[1], v->render_aabb_min[2]), v3(v->render_aabb_max[0], v->render_aabb_max[1], v->render_aabb_max[2])};
+    vol.train_aabb = {v3(v->train_aabb_min[0], v->train_aabb_min[1], v->train_aabb_min[2]), v3(v->train_aabb_max[0], v->train_aabb_max[1], v->train_aabb_max[2])};
+    vol.to_local = m3_load(v->render_aabb_to_local);
+    vol.to_local_identity = m3_is_identity(vol.to_local);
+    vol.cone = v->cone_angle_constant;
+    vol.max_mip = v->max_mip;
+    vol.min_transmittance = v->min_transmittance;
+    vol.bitfield = v->bitfield;
+    return vol;
+}
+
+/* glm-style quat round trip used by get_xform_given_rolling_shutter
+ * (common_device.cuh:361-368) with start == end and pixel_t == 0 [tcnn quat, unvendored] */
+struct Quat { float x, y, z, w; };
+Quat quat_from_m3(const M3& m0) {
+    auto m = [&](int i, int j) { return m0.c[i][j]; };
+    float fx = m(0, 0) - m(1, 1) - m(2, 2), fy = m(1, 1) - m(0, 0) - m(2, 2), fz = m(2, 2) - m(0, 0) - m(1, 1), fw = m(0, 0) + m(1, 1) + m(2, 2);
+    int bi = 0;
+    float fb = fw;
+    if (fx > fb) { fb = fx; bi = 1; }
+    if (fy > fb) { fb = fy; bi = 2; }
+    if (fz > fb) { fb = fz; bi = 3; }
+    float bv = std::sqrt(fb + 1.0f) * 0.5f;
+    float mult = 0.25f / bv;
+    switch (bi) {
+        case 0: return {(m(1, 2) - m(2, 1)) * mult, (m(2, 0) - m(0, 2)) * mult, (m(0, 1) - m(1, 0)) * mult, bv};
+        case 1: return {bv, (m(0, 1) + m(1, 0)) * mult, (m(2, 0) + m(0, 2)) * mult, (m(1, 2) - m(2, 1)) * mult};
+        case 2: return {(m(0, 1) + m(1, 0)) * mult, bv, (m(1, 2) + m(2, 1)) * mult, (m(2, 0) - m(0, 2)) * mult};
+        default: return {(m(2, 0) + m(0, 2)) * mult, (m(1, 2) + m(2, 1)) * mult, bv, (m(0, 1) - m(1, 0)) * mult};
+    }
+}
+M3 rolling_shutter_rotation(const M3& rot) {
+    Quat q = quat_from_m3(rot);
+    /* slerp(q, q, 0) */
+    float cos_theta = q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+    Quat s;
+    if (cos_theta > 1.0f - std::numeric_limits<float>::epsilon()) {
+        s = {q.x * (1.0f - 0.0f) + q.x * 0.0f, q.y * (1.0f - 0.0f) + q.y * 0.0f, q.z * (1.0f - 0.0f) + q.z * 0.0f, q.w * (1.0f - 0.0f) + q.w * 0.0f};
+    } else {
+        float angle = std::acos(cos_theta);
+        float s0 = std::sin((1.0f - 0.0f) * angle), s1 = std::sin(0.0f * angle), sa = std::sin(angle);
+        s = {(s0 * q.x + s1 * q.x) / sa, (s0 * q.y + s1 * q.y) / sa, (s0 * q.z + s1 * q.z) / sa, (s0 * q.w + s1 * q.w) / sa};
+    }
+    float len = std::sqrt(s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w);
+    s = {s.x / len, s.y / len, s.z / len, s.w / len};
+    float qxx = s.x * s.x, qyy = s.y * s.y, qzz = s.z * s.z, qxz = s.x * s.z, qxy = s.x * s.y, qyz = s.y * s.z;
+    float qwx = s.w * s.x, qwy = s.w * s.y, qwz = s.w * s.z;
+    M3 r;
+    r.c[0][0] = 1.0f - 2.0f * (qyy + qzz); r.c[0][1] = 2.0f * (qxy + qwz); r.c[0][2] = 2.0f * (qxz - qwy);
+    r.c[1][0] = 2.0f * (qxy - qwz); r.c[1][1] = 1.0f - 2.0f * (qxx + qzz); r.c[1][2] = 2.0f * (qyz + qwx);
+    r.c[2][0] = 2.0f * (qxz + qwy); r.c[2][1] = 2.0f * (qyz - qwx); r.c[2][2] = 1.0f - 2.0f * (qxx + qyy);
+    return r;
+}
+
+struct Payload { V3 origin, dir; float t, max_weight; uint32_t idx; uint16_t n_steps; bool alive; };
+struct RayState { V4 rgba; float depth; Payload p; };
+
+}  // namespace
+
+/* =========================================================================== */
+/* C API                                                                        */
+/* =========================================================================== */
+extern "C" {
+
+uint32_t orc_morton3D(uint32_t x, uint32_t y, uint32_t z) { return morton3D(x, y, z); }
+uint32_t orc_morton3D_invert(uint32_t x) { return morton3D_invert(x); }
+uint32_t orc_sobol(uint32_t index, uint32_t dim) { return sobol(index, dim); }
+float orc_ld_random_val(uint32_t index, uint32_t seed, uint32_t dim) { return ld_random_val(index, seed, dim); }
+void orc_ld_random_pixel_offset(uint32_t spp, float out[2]) { V2 o = ld_random_pixel_offset(spp); out[0] = o.x; out[1] = o.y; }
+uint16_t orc_float_to_half(float f) { return f2h(f); }
+float orc_half_to_float(uint16_t h) { return h2f(h); }
+
+void orc_xorwow_init(uint64_t seed, uint64_t subsequence, uint64_t offset, uint32_t state[6]) { xorwow_init(seed, subsequence, offset, state); }
+void orc_xorwow_init_many(uint64_t seed, uint32_t n, uint32_t* states) {
+    /* init_rand_state: curand_init(PT_SEED, idx, 0) (synerfgine/common.cu:22-26) */
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) xorwow_init(seed, (uint64_t)i, 0, states + 6 * i);
+}
+uint32_t orc_xorwow_next(uint32_t state[6]) { return xorwow_next(state); }
+float orc_curand_uniform(uint32_t state[6]) { return curand_uniform(state); }
+void orc_xorwow_jump_steps_naive(uint32_t st[6], uint64_t steps) { for (uint64_t i = 0; i < steps; ++i) xorwow_next(st); }
+void orc_xorwow_jump_matrix(uint32_t st[6], uint32_t log2_steps) {
+    gf2_apply(xorwow_tables().step_pow[log2_steps], st, st);
+    st[5] += (uint32_t)((1ull << log2_steps) * 362437ull);
+}
+
+uint32_t orc_grid_level_table(const orc_model* m, uint32_t* offsets, uint32_t* resolutions) {
+    Grid g = make_grid(m);
+    for (uint32_t i = 0; i <= g.L; ++i) offsets[i] = g.offsets[i];
+    for (uint32_t i = 0; i < g.L; ++i) resolutions[i] = g.res[i];
+    return g.offsets[g.L];
+}
+uint32_t orc_n_params(const orc_model* m) { return 3072 + 7168 + make_grid(m).offsets[m->n_levels] * m->n_features; }
+
+void orc_hashgrid_encode(const orc_model* m, const float* coords, uint32_t stride, uint32_t n, uint16_t* out) {
+    Grid g = make_grid(m);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) encode_one(g, coords + (size_t)i * stride, out + (size_t)i * g.L * g.F);
+}
+void orc_sh_encode(const float* coords, uint32_t stride, uint32_t dir_offset, uint32_t n, uint16_t* out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* c = coords + (size_t)i * stride + dir_offset;
+        sh_one(c[0], c[1], c[2], out + 16 * (size_t)i);
+    }
+}
+void orc_nerf_inference(const orc_model* m, const float* coords, uint32_t stride, uint32_t n, uint16_t* out) {
+    Grid g = make_grid(m);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) network_one(m, g, coords + (size_t)i * stride, out + 16 * (size_t)i);
+}
+
+/* update_density_grid_mean_and_bitfield: testbed_nerf.cu:3212-3229,
+ * grid_to_bitfield 285-309, bitfield_max_pool 311-332 */
+void orc_density_grid_to_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, uint8_t* bf, float* mean_out) {
+    const uint32_t N = NERF_GRID_N_CELLS;
+    std::vector<float> grid((size_t)N * (max_cascade + 1));
+    for (size_t i = 0; i < grid.size(); ++i) grid[i] = h2f(grid_f16[i]);
+    double sum = 0.0;
+    for (uint32_t i = 0; i < N; ++i) sum += (double)(std::fmax(grid[i], 0.f) / N);
+    float mean = (float)sum;
+    if (mean_out) *mean_out = mean;
+    float thresh = std::min(NERF_MIN_OPTICAL_THICKNESS, mean);
+    uint32_t n_elements = N / 8 * NERF_CASCADES, n_nonzero = N / 8 * (max_cascade + 1);
+    for (uint32_t i = 0; i < n_elements; ++i) {
+        if (i >= n_nonzero) { bf[i] = 0; continue; }
+        uint8_t bits = 0;
+        for (uint8_t j = 0; j < 8; ++j) bits |= grid[i * 8 + j] > thresh ? ((uint8_t)1 << j) : 0;
+        bf[i] = bits;
+    }
+    for (uint32_t level = 1; level < NERF_CASCADES; ++level) {
+        const uint8_t* prev = bf + (size_t)N / 8 * (level - 1);
+        uint8_t* next = bf + (size_t)N / 8 * level;
+        for (uint32_t i = 0; i < N / 64; ++i) {
+            uint8_t bits = 0;
+            for (uint8_t j = 0; j < 8; ++j) bits |= prev[i * 8 + j] > 0 ? ((uint8_t)1 << j) : 0;
+            uint32_t x = morton3D_invert(i >> 0) + NERF_GRIDSIZE / 8;
+            uint32_t y = morton3D_invert(i >> 1) + NERF_GRIDSIZE / 8;
+            uint32_t z = morton3D_invert(i >> 2) + NERF_GRIDSIZE / 8;
+            next[morton3D(x, y, z)] |= bits;
+        }
+    }
+}
+
+/* Testbed::render_nerf_with_buffers (testbed_nerf.cu:2467-2613) with
+ * NerfTracer::init_rays_from_camera (2037-2120) and trace_alt (2128-2277). */
+void orc_render_nerf(const orc_model* m, const orc_volume* vdesc, const orc_camera* c,
+                     float* frame_rgba, float* frame_depth, float* positions, float* normals, orc_nerf_stats* stats) {
+    Volume vol = make_volume(vdesc);
+    Grid g = make_grid(m);
+    const int W = c->res[0], H = c->res[1];
+    const uint32_t n_px = (uint32_t)W * H;
+    M43 cam = m43_load(c->camera);
+    M3 rs_rot = rolling_shutter_rotation(m3_of(cam));
+    V2 focal = {c->focal[0], c->focal[1]};
+    V2 sc = {c->screen_center[0], c->screen_center[1]};
+    V3 cam_fwd = cam.c[2], cam_pos = cam.c[3];
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+
+    /* init_rays_with_payload_kernel_nerf: testbed_nerf.cu:1855-1970 */
+    std::vector<RayState> rays(n_px);
+    V2 pixel_offset = ld_random_pixel_offset(c->snap_to_pixel_centers ? 0 : c->spp);
+#pragma omp parallel for schedule(static)
+    for (int64_t idx = 0; idx < (int64_t)n_px; ++idx) {
+        int x = (int)(idx % W), y = (int)(idx / W);
+        RayState& r = rays[idx];
+        r.rgba = {0, 0, 0, 0};
+        r.depth = 0.0f; /* cudaMemsetAsync(m_rays[0].depth, 0) 2103 */
+        Payload& p = r.p;
+        p.max_weight = 0.0f;
+        frame_depth[idx] = MAX_DEPTH;
+        V2 uv = {((float)x + pixel_offset.x) / (float)W, ((float)y + pixel_offset.y) / (float)H};
+        /* uv_to_ray (common_device.cuh:403-470) with identity foveation, no lens, no parallax, aperture 0, near 0 */
+        V3 dir = v3((uv.x - sc.x) * (float)W / focal.x, (uv.y - sc.y) * (float)H / focal.y, 1.0f);
+        dir = mul(rs_rot, dir);
+        V3 origin = cam_pos;
+        frame_rgba[4 * idx + 0] = 0.0f; frame_rgba[4 * idx + 1] = 0.0f; frame_rgba[4 * idx + 2] = 0.0f; /* rgb only */
+        dir = normalize(dir);
+        float t = std::fmax(bb_ray_intersect(vol.render_aabb, to_local(vol, origin), to_local(vol, dir)).x, 0.0f) + 1e-6f;
+        p.origin = origin;
+        if (!bb_contains(vol.render_aabb, to_local(vol, origin + dir * t))) { p.alive = false; p.dir = dir; p.idx = (uint32_t)idx; continue; }
+        p.dir = dir; p.t = t; p.idx = (uint32_t)idx; p.n_steps = 0; p.alive = true;
+        /* advance_pos_nerf: testbed_nerf.cu:334-363 */
+        V3 idir = v3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+        float cone = vol.cone; /* calc_cone_angle returns the constant (nerf_device.cuh:370-377) */
+        float tt = advance_n_steps(p.t, cone, ld_random_val(c->spp, p.idx * 786433u));
+        tt = if_unoccupied_advance_to_next_occupied_voxel(tt, cone, origin, dir, idir, vol.bitfield, 0, vol.max_mip, vol);
+        if (tt >= MAX_DEPTH) p.alive = false;
+        else p.t = tt;
+    }
+    for (uint32_t i = 0; i < n_px; ++i) { positions[3 * i] = positions[3 * i + 1] = positions[3 * i + 2] = 0.0f; normals[3 * i] = normals[3 * i + 1] = normals[3 * i + 2] = 0.0f; }
+
+    /* trace_alt: double-buffered wavefront, testbed_nerf.cu:2155-2277 */
+    std::vector<RayState> current, hit;
+    std::vector<RayState>* src = &rays;
+    std::vector<float> coords;
+    std::vector<uint16_t> outs;
+    uint32_t i_step = 1, iter = 0;
+    uint32_t n_alive = n_px;
+    const uint32_t target = c->target_n_queries ? c->target_n_queries : 2u * 1024u * 1024u;
+    while (i_step < MARCH_ITER) {
+        /* compact_kernel_nerf 1830-1853 (order: stable, deterministic) */
+        current.clear();
+        for (uint32_t i = 0; i < n_alive; ++i) {
+            const RayState& r = (*src)[i];
+            if (r.p.alive) current.push_back(r);
+            else if (r.rgba.w > 0.001f) hit.push_back(r);
+        }
+        n_alive = (uint32_t)current.size();
+        if (n_alive == 0) break;
+        uint32_t n_steps = std::min(std::max(target / n_alive, MIN_STEPS_INBETWEEN_COMPACTION), MAX_STEPS_INBETWEEN_COMPACTION);
+        if (stats && iter < 64) { stats->alive_per_iter[iter] = n_alive; stats->steps_per_iter[iter] = n_steps; }
+        ++iter;
+        /* generate_next_nerf_network_inputs 790-837; slot i + j*n_alive */
+        coords.assign((size_t)n_alive * n_steps * 7, 0.0f);
+        uint64_t real = 0;
+#pragma omp parallel for schedule(static) reduction(+ : real)
+        for (int64_t i = 0; i < (int64_t)n_alive; ++i) {
+            Payload& p = current[i].p;
+            V3 o = p.origin, d = p.dir, idir = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+            float t = p.t;
+            uint32_t j = 0;
+            bool exhausted = false;
+            for (; j < n_steps; ++j) {
+                t = if_unoccupied_advance_to_next_occupied_voxel(t, vol.cone, o, d, idir, vol.bitfield, 0, vol.max_mip, vol);
+                if (t >= MAX_DEPTH) { p.n_steps = (uint16_t)j; exhausted = true; break; }
+                float dt = calc_dt(t, vol.cone);
+                V3 wp = warp_position(o + d * t, vol.train_aabb);
+                V3 wd = warp_direction(d);
+                float* cc = &coords[((size_t)i + (size_t)j * n_alive) * 7];
+                cc[0] = wp.x; cc[1] = wp.y; cc[2] = wp.z; cc[3] = warp_dt(dt); cc[4] = wd.x; cc[5] = wd.y; cc[6] = wd.z;
+                t += dt;
+            }
+            if (!exhausted) { p.t = t; p.n_steps = (uint16_t)n_steps; }
+            real += exhausted ? j : n_steps;
+        }
+        if (stats) { stats->n_samples += real; stats->n_slots += ((uint64_t)n_alive * n_steps + 255) / 256 * 256; }
+        /* inference_mixed_precision on the real slots (stale slots do not affect results) */
+        outs.assign((size_t)n_alive * n_steps * 4, 0);
+#pragma omp parallel for schedule(dynamic, 256)
+        for (int64_t s = 0; s < (int64_t)n_alive * n_steps; ++s) {
+            uint32_t i = (uint32_t)(s % n_alive), j = (uint32_t)(s / n_alive);
+            if (j >= current[i].p.n_steps) continue;
+            uint16_t o16[16];
+            network_one(m, g, &coords[(size_t)s * 7], o16);
+            std::memcpy(&outs[(size_t)s * 4], o16, 8);
+        }
+        /* composite_kernel_nerf_alt 476-575 */
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < (int64_t)n_alive; ++i) {
+            RayState& r = current[i];
+            Payload& p = r.p;
+            V4 lr = r.rgba;
+            float ld = r.depth;
+            uint32_t actual = p.n_steps, j = 0;
+            for (; j < actual; ++j) {
+                const uint16_t* o = &outs[((size_t)i + (size_t)j * n_alive) * 4];
+                const float* cc = &coords[((size_t)i + (size_t)j * n_alive) * 7];
+                V3 pos = unwarp_position(v3(cc[0], cc[1], cc[2]), vol.train_aabb);
+                float T = 1.f - lr.w;
+                float dt = unwarp_dt(cc[3]);
+                float alpha = 1.f - std::exp(-std::exp(h2f(o[3])) * dt);
+                float weight = alpha * T;
+                V3 rgb = v3(logistic(h2f(o[0])), logistic(h2f(o[1])), logistic(h2f(o[2])));
+                lr.x += rgb.x * weight; lr.y += rgb.y * weight; lr.z += rgb.z * weight; lr.w += weight;
+                ld = dot(cam_fwd, pos - cam_pos);
+                if (weight > p.max_weight) p.max_weight = weight;
+                if (lr.w > (1.0f - vol.min_transmittance)) {
+                    float a = lr.w;
+                    lr.x /= a; lr.y /= a; lr.z /= a; lr.w /= a;
+                    break;
+                }
+            }
+            if (j < n_steps) { p.alive = false; p.n_steps = (uint16_t)(j + i_step); }
+            r.rgba = lr;
+            r.depth = ld;
+            p.t = ld / dot(cam_fwd, p.dir);
+        }
+        src = &current;
+        std::vector<RayState> tmp = current; /* next compaction reads this buffer */
+        rays.swap(tmp);
+        src = &rays;
+        i_step += n_steps;
+    }
+    if (stats) { stats->n_iterations = iter; stats->n_hit = (uint32_t)hit.size(); }
+
+    /* extract_from_payload 1578-1612 (Shade mode) */
+    for (const RayState& r : hit) {
+        const Payload& p = r.p;
+        V3 orig_pos = cam_pos + p.dir * p.t;
+        float* fb = &frame_rgba[4 * (size_t)p.idx];
+        V4 tmp = {srgb_to_linear(r.rgba.x), srgb_to_linear(r.rgba.y), srgb_to_linear(r.rgba.z), r.rgba.w};
+        fb[0] = tmp.x + fb[0] * (1.0f - tmp.w);
+        fb[1] = tmp.y + fb[1] * (1.0f - tmp.w);
+        fb[2] = tmp.z + fb[2] * (1.0f - tmp.w);
+        fb[3] = tmp.w + fb[3] * (1.0f - tmp.w);
+        positions[3 * p.idx + 0] = orig_pos.x; positions[3 * p.idx + 1] = orig_pos.y; positions[3 * p.idx + 2] = orig_pos.z;
+        if (tmp.w > 0.2f) frame_depth[p.idx] = r.depth;
+    }
+
+    /* write_normals_to_buffer 1523-1576 */
+    static const int OFF[9][2] = {{1, 0}, {0, 1}, {-1, 0}, {0, -1}, {2, 0}, {0, 2}, {-2, 0}, {0, -2}, {1, 0}};
+#pragma omp parallel for schedule(static)
+    for (int64_t idx = 0; idx < (int64_t)n_px; ++idx) {
+        int x = (int)(idx % W), y = (int)(idx / W);
+        V3 pos = v3(positions[3 * idx], positions[3 * idx + 1], positions[3 * idx + 2]);
+        float factor = 0.0f;
+        V3 N = v3s(0.0f);
+        for (int t = 0; t < 8; ++t) {
+            int tx = x + OFF[t + 1][0], ty = y + OFF[t + 1][1], bx = x + OFF[t][0], by = y + OFF[t][1];
+            if (tx >= W || tx < 0 || ty >= H || ty < 0 || bx >= W || bx < 0 || by >= H || by < 0) continue;
+            const float* pt = &positions[3 * ((size_t)ty * W + tx)];
+            const float* pb = &positions[3 * ((size_t)by * W + bx)];
+            V3 T = v3(pt[0], pt[1], pt[2]) - pos;
+            V3 B = v3(pb[0], pb[1], pb[2]) - pos;
+            N = N + normalize(cross(normalize(T), B)); /* sng::get_normal, synerfgine/common.cuh:55-57 */
+            factor += 1.0f;
+        }
+        N = factor == 0.0f ? N : N / factor;
+        V3 n = normalize(N);
+        normals[3 * idx] = n.x; normals[3 * idx + 1] = n.y; normals[3 * idx + 2] = n.z;
+    }
+}
+
+/* shade_nerf_shadows (testbed_nerf.cu:2628-2677) -> shade_with_shadow (1702-1786)
+ * -> shadow_for_px (1614-1700).  The neighbourhood's light samples draw from the
+ * centre pixel's own RNG stream (the reference shares neighbour states racily,
+ * SURVEY Appendix A.5); identical to the reference for kernel_size/2 == 0. */
+void orc_shade_nerf_shadows(const orc_volume* vdesc, const int32_t res[2], float* frame_rgba, const float* positions, const float* normals,
+                            const orc_object* objd, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
+                            uint32_t* rng, float nerf_shadow_intensity, float thr, int32_t kernel_size) {
+    Volume vol = make_volume(vdesc);
+    std::vector<Object> objs;
+    for (uint32_t i = 0; i < n_objs; ++i) objs.push_back(make_object(objd[i]));
+    const int W = res[0], H = res[1];
+    const int r = kernel_size / 2;
+    const uint32_t n_steps = MAX_STEPS_INBETWEEN_COMPACTION;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t idx = 0; idx < (int64_t)W * H; ++idx) {
+        int x = (int)(idx % W), y = (int)(idx / W);
+        float sum = 0.0f;
+        int blend = 0;
+        uint32_t* st = rng + 6 * idx;
+        for (int i = -r; i <= r; ++i)
+            for (int j = -r; j <= r; ++j) {
+                int fx = x + i, fy = y + j;
+                if (fx < 0 || fy < 0 || fx >= W || fy >= H) continue;
+                size_t t = (size_t)fy * W + fx;
+                V3 pos = v3(positions[3 * t], positions[3 * t + 1], positions[3 * t + 2]);
+                V3 nrm = v3(normals[3 * t], normals[3 * t + 1], normals[3 * t + 2]);
+                float overall = 1.0f;
+                for (uint32_t li = 0; li < n_lights; ++li) {
+                    const orc_light& L = lights[li];
+                    V3 lp = v3(L.pos[0], L.pos[1], L.pos[2]);
+                    if (L.type == 0) {
+                        /* Light::sample (light.cuh:71-77) */
+                        float ox = fractf(curand_uniform(st)), oy = fractf(curand_uniform(st)), oz = fractf(curand_uniform(st));
+                        V3 lpos = lp + v3(ox, oy, oz) * L.size * 1.0f;
+                        V3 l = normalize(lpos - pos);
+                        float full_d = length(lpos - pos);
+                        int hit = -1;
+                        float syn_depth = depth_test_world(pos, l, objs, hit);
+                        float syn_mask = syn_depth / full_d;
+                        overall = std::min(overall, std::pow(syn_mask, nerf_shadow_intensity));
+                        V3 fract_offset = full_d * thr * lpos;
+                        float nerf_depth = std::min(full_d, depth_test_nerf_sd(n_steps, vol.cone, pos + fract_offset, lpos, vol, 0, vol.max_mip));
+                        /* (full_d * (1.0 - thr)) is a double expression (1664) */
+                        double mask = (double)(nerf_depth * (1.0f - std::min(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)thr));
+                        overall = (float)std::fmin((double)overall, mask);
+                    } else {
+                        V3 l = normalize(lp - pos);
+                        /* min(1.0, overall + min(0.0, dot(l, n)) * intensity): double (1677) */
+                        double v = (double)overall + std::fmin(0.0, (double)dot(l, nrm)) * (double)L.intensity;
+                        overall = (float)std::fmin(1.0, v);
+                    }
+                }
+                sum += overall;
+                ++blend;
+            }
+        sum /= (float)blend;
+        sum = std::pow(sum, nerf_shadow_intensity);
+        float* rgba = &frame_rgba[4 * idx];
+        rgba[0] = srgb_to_linear(rgba[0]) * sum;
+        rgba[1] = srgb_to_linear(rgba[1]) * sum;
+        rgba[2] = srgb_to_linear(rgba[2]) * sum;
+    }
+}
+
+/* TriangleBvhWithBranchingFactor<2>::build: triangle_bvh.cu:615-692 */
+int32_t orc_bvh_build(float* trisf, uint32_t n_tris, uint32_t ppl, float* nodes_out, uint32_t cap) {
+    std::vector<Tri> tris((Tri*)trisf, (Tri*)trisf + n_tris);
+    std::vector<Node> nodes;
+    auto bb_of = [&](std::vector<Tri>::iterator b, std::vector<Tri>::iterator e) {
+        BBox bb;
+        bb.min = bb.max = b->a;
+        for (auto it = b; it != e; ++it) {
+            bb.min = vmin3(bb.min, it->a); bb.max = vmax3(bb.max, it->a);
+            bb.min = vmin3(bb.min, it->b); bb.max = vmax3(bb.max, it->b);
+            bb.min = vmin3(bb.min, it->c); bb.max = vmax3(bb.max, it->c);
+        }
+        return bb;
+    };
+    nodes.push_back({});
+    nodes.front().bb = bb_of(tris.begin(), tris.end());
+    struct BuildNode { int node_idx; std::vector<Tri>::iterator begin, end; };
+    std::stack<BuildNode> st;
+    st.push({0, tris.begin(), tris.end()});
+    while (!st.empty()) {
+        BuildNode curr = st.top();
+        st.pop();
+        size_t node_idx = curr.node_idx;
+        BuildNode children[2];
+        children[0].begin = curr.begin;
+        children[0].end = curr.end;
+        int n_children = 1;
+        while (n_children < 2) {
+            for (int i = n_children - 1; i >= 0; --i) {
+                auto& child = children[i];
+                V3 mean = v3s(0.0f);
+                for (auto it = child.begin; it != child.end; ++it) mean = mean + tri_centroid(*it);
+                mean = mean / (float)std::distance(child.begin, child.end);
+                V3 var = v3s(0.0f);
+                for (auto it = child.begin; it != child.end; ++it) { V3 d = tri_centroid(*it) - mean; var = var + d * d; }
+                var = var / (float)std::distance(child.begin, child.end);
+                float mv = vmax(var);
+                int axis = var.x == mv ? 0 : (var.y == mv ? 1 : 2);
+                auto mid = child.begin + std::distance(child.begin, child.end) / 2;
+                std::nth_element(child.begin, mid, child.end, [&](const Tri& a, const Tri& b) { return tri_centroid_axis(a, axis) < tri_centroid_axis(b, axis); });
+                children[i * 2].begin = children[i].begin;
+                children[i * 2 + 1].end = children[i].end;
+                children[i * 2].end = children[i * 2 + 1].begin = mid;
+            }
+            n_children *= 2;
+        }
+        nodes[node_idx].left = (int)nodes.size();
+        for (int i = 0; i < 2; ++i) {
+            auto& child = children[i];
+            child.node_idx = (int)nodes.size();
+            nodes.push_back({});
+            nodes.back().bb = bb_of(child.begin, child.end);
+            if ((uint32_t)std::distance(child.begin, child.end) <= ppl) {
+                nodes.back().left = -(int)std::distance(tris.begin(), child.begin) - 1;
+                nodes.back().right = -(int)std::distance(tris.begin(), child.end) - 1;
+            } else {
+                st.push(child);
+            }
+        }
+        nodes[node_idx].right = (int)nodes.size();
+    }
+    if (nodes.size() > cap) return -1;
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        float* n = nodes_out + 8 * i;
+        n[0] = nodes[i].bb.min.x; n[1] = nodes[i].bb.min.y; n[2] = nodes[i].bb.min.z;
+        n[3] = nodes[i].bb.max.x; n[4] = nodes[i].bb.max.y; n[5] = nodes[i].bb.max.z;
+        std::memcpy(&n[6], &nodes[i].left, 4);
+        std::memcpy(&n[7], &nodes[i].right, 4);
+    }
+    std::memcpy(trisf, tris.data(), n_tris * sizeof(Tri));
+    return (int32_t)nodes.size();
+}
+
+void orc_depth_test_world(const orc_object* objd, uint32_t n_objs, const float* o, const float* d, uint32_t n, float* t_out, int32_t* obj_out) {
+    std::vector<Object> objs;
+    for (uint32_t i = 0; i < n_objs; ++i) objs.push_back(make_object(objd[i]));
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        int hit = -1;
+        t_out[i] = depth_test_world(v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]), objs, hit);
+        obj_out[i] = hit;
+    }
+}
+
+/* sng::init_rays_with_payload_kernel_nerf: synerfgine/raytracer.cu:59-99 */
+void orc_mesh_init_rays(const orc_camera* c, float* origins, float* dirs, float* acc_rgba, float* acc_depth) {
+    const int W = c->res[0], H = c->res[1];
+    M43 cam = m43_load(c->camera);
+    M3 rot = m3_of(cam);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            size_t idx = (size_t)y * W + x;
+            V2 uv = {(float)x / (float)W, (float)y / (float)H};
+            V3 dir = v3((uv.x - c->screen_center[0]) * (float)W / c->focal[0], (uv.y - c->screen_center[1]) * (float)H / c->focal[1], 1.0f);
+            dir = mul(rot, dir);
+            dir = normalize(dir);
+            origins[3 * idx] = cam.c[3].x; origins[3 * idx + 1] = cam.c[3].y; origins[3 * idx + 2] = cam.c[3].z;
+            dirs[3 * idx] = dir.x; dirs[3 * idx + 1] = dir.y; dirs[3 * idx + 2] = dir.z;
+            acc_rgba[4 * idx] = 0.0f; acc_rgba[4 * idx + 1] = 0.0f; acc_rgba[4 * idx + 2] = 0.0f; acc_rgba[4 * idx + 3] = 1.0f;
+            acc_depth[idx] = MAX_DEPTH;
+        }
+}
+
+}  // extern "C"
+
+namespace {
+/* sng::cone_random(orig, perturb_frame, longi, latid): synerfgine/common.cuh:33-36 */
+inline V3 cone_random_frame(V3 orig, const M3& frame, float longi, float latid) {
+    V3 off = v3(std::cos(longi) * std::sin(latid), std::sin(longi) * std::sin(latid), std::cos(longi));
+    return orig + mul(frame, off);
+}
+/* sng::cone_random(orig, up, longi, latid): synerfgine/common.cuh:37-48 */
+inline V3 cone_random_up(V3 orig, V3 up, float longi, float latid) {
+    V3 N = normalize(orig);
+    V3 B = normalize(cross(N, up));
+    V3 T = cross(B, N);
+    M3 frame = {{T, B, N}};
+    V3 off = v3(std::sin(longi) * std::cos(latid), std::sin(longi) * std::sin(latid), std::cos(longi));
+    return orig + mul(frame, off);
+}
+inline V3 reflect(V3 i, V3 n) { return 2.0f * dot(i, n) * n - i; }
+struct SampledRay { V3 pos = v3s(0.0f), dir = v3s(0.0f); float pdf = 0.0f, attenuation = 1.0f; };
+/* Material::local_color (material.cuh:96-98) */
+inline V3 local_color(const orc_material& m, V3 L, V3 N, V3 R, V3 V, const orc_light& light) {
+    float a = std::max(0.0f, dot(L, N));
+    V3 kd = v3(m.kd[0], m.kd[1], m.kd[2]), ks = v3(m.ks[0], m.ks[1], m.ks[2]);
+    return a * kd * light.intensity + std::pow(std::max(0.0f, dot(R, V)), m.n) * ks;
+}
+/* sng::shade_object: synerfgine/raytracer.cu:6-57 */
+V4 shade_object(V3 wi, SampledRay& ray, uint32_t shadow_count, HitRecord& hit, const orc_light* lights, uint32_t n_lights,
+                const std::vector<Object>& objs, const orc_material* mats, uint32_t n_steps, float cone, const Volume& vol,
+                uint32_t min_mip, uint32_t max_mip, uint32_t* st, float& out_nerf_shadow, bool no_shadow, float syn_shadow_factor) {
+    if (hit.material_idx < 0) return {0, 0, 0, 0};
+    const orc_material& mat = mats[hit.material_idx];
+    V3 color = v3s(0.0f);
+    for (uint32_t l = 0; l < n_lights; ++l) {
+        const orc_light& light = lights[l];
+        V3 lp = v3(light.pos[0], light.pos[1], light.pos[2]);
+        for (uint32_t s = 0; s < shadow_count; ++s) {
+            float ox = fractf(curand_uniform(st)), oy = fractf(curand_uniform(st)), oz = fractf(curand_uniform(st));
+            V3 lpos = lp + v3(ox, oy, oz) * light.size * 1.0f;
+            V3 L = lpos - hit.pos;
+            float full_dist = length(L);
+            L = normalize(L);
+            if (light.type == 0) {
+                V3 invL = v3(1.0f / L.x, 1.0f / L.y, 1.0f / L.z);
+                int obj_hit = -1;
+                float syn_shadow = no_shadow ? 1.0f : depth_test_world(hit.pos, L, objs, obj_hit);
+                /* full_d = syn_shadow + 1.0 is a double expression bound to const float& */
+                float nerf_shadow = no_shadow ? 1.0f : depth_test_nerf_fd((float)((double)syn_shadow + 1.0), n_steps, cone, hit.pos, L, invL, vol, min_mip, max_mip);
+                out_nerf_shadow = std::min(nerf_shadow / full_dist, out_nerf_shadow);
+                float shadow = std::min(std::min(nerf_shadow, syn_shadow), full_dist);
+                float mask = smoothstep(shadow / full_dist);
+                mask = std::pow(mask, syn_shadow_factor);
+                V3 R = reflect(L, hit.normal);
+                V3 V = normalize(-wi);
+                color = color + local_color(mat, L, hit.normal, R, V, light) * mask;
+            } else {
+                V3 R = reflect(L, hit.normal);
+                V3 V = normalize(-wi);
+                color = color + local_color(mat, L, hit.normal, R, V, light);
+            }
+        }
+    }
+    color = color / (float)shadow_count;
+    color = color + v3(mat.ka[0], mat.ka[1], mat.ka[2]);
+    /* Material::scatter(hit, wi, ray, rand) (material.cuh:112-123) */
+    ray.pos = hit.pos;
+    if (mat.type == 0 || mat.type == 1) {
+        float spec = mat.type == 0 ? PI_F / 2 : mat.spec_angle;
+        ray.dir = reflect(-wi, hit.normal);
+        float longi = curand_uniform(st) * spec;
+        float latid = (float)((double)curand_uniform(st) * 2.0 * (double)PI_F); /* double expression */
+        ray.dir = cone_random_frame(hit.normal, hit.perturb, longi, latid);
+        ray.pdf = 1.0f / std::max(1.0f, spec * 2.0f);
+        ray.attenuation *= mat.rg;
+    }
+    return {color.x, color.y, color.z, 1.0f};
+}
+}  // namespace
+
+extern "C" {
+
+/* sng::raytrace: synerfgine/raytracer.cu:101-218 (Final buffer) */
+void orc_raytrace(const orc_volume* vdesc, const float* camera, const orc_frame_params* P,
+                  const orc_object* objd, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
+                  const orc_material* mats, uint32_t n_mats, const float* origins, const float* dirs, uint32_t n,
+                  uint32_t* rng, float* acc_rgba, float* acc_depth) {
+    (void)n_mats;
+    Volume vol = make_volume(vdesc);
+    std::vector<Object> objs;
+    for (uint32_t i = 0; i < n_objs; ++i) objs.push_back(make_object(objd[i]));
+    M43 cam = m43_load(camera);
+    const V3 up_vec = cam.c[0];
+    const float lens = P->lens_angle_constant;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        uint32_t* st = rng + 6 * i;
+        V3 src_p = v3(origins[3 * i], origins[3 * i + 1], origins[3 * i + 2]);
+        V3 src_d = v3(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+        V3 shade = v3s(0.0f), normal = v3s(0.0f), view_pos = v3s(0.0f), next_pos = v3s(0.0f), view_dir = v3s(0.0f), next_dir = v3s(0.0f);
+        float nerf_shadow = 1.0f;
+        for (uint32_t spp = 0; spp < P->light_samples; ++spp) {
+            SampledRay ray;
+            float longi = curand_uniform(st) * lens;
+            /* lens ? 0.0 : curand_uniform * 2.0 * PI -- second draw only when lens == 0 */
+            float latid = lens != 0.0f ? 0.0f : (float)((double)curand_uniform(st) * 2.0 * (double)PI_F);
+            ray.pos = src_p;
+            ray.dir = cone_random_up(src_d, up_vec, longi, latid);
+            ray.pdf = 1.0f / (float)P->path_trace_depth;
+            ray.attenuation = 1.0f;
+            V3 shade_s = v3s(0.0f);
+            for (uint32_t bounce = 0; bounce < P->path_trace_depth; ++bounce) {
+                V3 sp = ray.pos, sd = ray.dir;
+                HitRecord hit;
+                int hit_obj = -1;
+                depth_test_world_hit(sp, sd, objs, hit_obj, hit);
+                if (!bounce) { normal = normal + hit.normal; view_pos = view_pos + sp; view_dir = view_dir + sd; next_pos = next_pos + hit.pos; }
+                if (hit_obj < 0) break;
+                SampledRay next;
+                V4 color = shade_object(sd, next, P->shadow_iters, hit, lights, n_lights, objs, mats, P->shadow_steps, vol.cone, vol, 0,
+                                        vol.max_mip, st, nerf_shadow, !P->shadow_on_virtual_obj, P->syn_shadow_factor);
+                shade_s = shade_s + v3(color.x, color.y, color.z) * ray.pdf * ray.attenuation;
+                if (!bounce) next_dir = next_dir + next.dir;
+                ray = next;
+            }
+            shade = shade + shade_s;
+        }
+        float weight = (float)P->light_samples;
+        view_pos = view_pos / weight; view_dir = view_dir / weight; next_pos = next_pos / weight;
+        next_dir = next_dir / weight; normal = normal / weight; shade = shade / weight;
+        float depth = dot(src_d, next_pos - src_p);
+        acc_depth[i] = depth;
+        V3 curr = v3(acc_rgba[4 * i], acc_rgba[4 * i + 1], acc_rgba[4 * i + 2]);
+        if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
+        acc_rgba[4 * i] = shade.x; acc_rgba[4 * i + 1] = shade.y; acc_rgba[4 * i + 2] = shade.z;
+    }
+}
+
+/* sng::overlay_nerf: synerfgine/raytracer.cu:220-258 (Identity tonemap) */
+void orc_overlay(const orc_frame_params* P, const float* syn_rgba, const float* syn_depth, const float* nerf_rgba, const float* nerf_depth,
+                 float* final_rgba, float* final_depth) {
+    const int W = P->mesh_res[0], H = P->mesh_res[1], s = P->syn_px_scale;
+    const int nW = W / s;
+    float e = std::pow(2.0f, P->exposure);
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            int sid = x + y * W;
+            int nid = std::min((x / s) + (y / s) * nW, P->nerf_res[0] * P->nerf_res[1] - 1);  /* clamp as the product does */
+            const float* sr = &syn_rgba[4 * (size_t)sid];
+            const float* nr = &nerf_rgba[4 * (size_t)nid];
+            float sdepth = syn_depth[sid], ndepth = nerf_depth[nid];
+            const float* use = (!P->show_nerf || sdepth - P->rt_depth_offset < ndepth) ? sr : nr;
+            float rgb[3] = {use[0] * e, use[1] * e, use[2] * e};
+            float* f = &final_rgba[4 * (size_t)sid];
+            for (int k = 0; k < 3; ++k) f[k] = P->srgb_output ? linear_to_srgb(rgb[k]) : rgb[k];
+            f[3] = use[3];
+            final_depth[sid] = sdepth;
+        }
+}
+
+/* Engine::frame (synerfgine/engine.cu:352-433): raytrace -> NeRF render (+ shadows) -> overlay.
+ * The mesh layer is re-initialised (camera reset semantics, raytracer.cu:327-336). */
+void orc_render_frame(const orc_model* m, const orc_volume* v, const orc_camera* nerf_cam, const orc_camera* mesh_cam,
+                      const orc_frame_params* P, const orc_object* objs, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
+                      const orc_material* mats, uint32_t n_mats, uint32_t* nerf_rng, uint32_t* mesh_rng,
+                      float* final_rgba, float* final_depth, float* nerf_rgba, float* nerf_depth, orc_nerf_stats* stats) {
+    size_t n_mesh = (size_t)mesh_cam->res[0] * mesh_cam->res[1];
+    size_t n_nerf = (size_t)nerf_cam->res[0] * nerf_cam->res[1];
+    std::vector<float> o(3 * n_mesh), d(3 * n_mesh), acc(4 * n_mesh), accd(n_mesh);
+    orc_mesh_init_rays(mesh_cam, o.data(), d.data(), acc.data(), accd.data());
+    if (P->show_virtual_obj)
+        orc_raytrace(v, mesh_cam->camera, P, objs, n_objs, lights, n_lights, mats, n_mats, o.data(), d.data(), (uint32_t)n_mesh, mesh_rng, acc.data(), accd.data());
+    if (P->show_nerf) {
+        std::vector<float> pos(3 * n_nerf), nrm(3 * n_nerf);
+        orc_render_nerf(m, v, nerf_cam, nerf_rgba, nerf_depth, pos.data(), nrm.data(), stats);
+        if (P->shadow_on_nerf)
+            orc_shade_nerf_shadows(v, nerf_cam->res, nerf_rgba, pos.data(), nrm.data(), objs, n_objs, lights, n_lights, nerf_rng,
+                                   P->nerf_shadow_intensity, P->nerf_on_nerf_shadow_threshold, P->nerf_kernel_size);
+    }
+    orc_overlay(P, acc.data(), accd.data(), nerf_rgba, nerf_depth, final_rgba, final_depth);
+}
+
+int32_t orc_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+}  // extern "C"

@@ -1,0 +1,164 @@
+/*
+ * sng_oracle.h -- CPU ORACLE (test infrastructure only).
+ *
+ * This is a plain scalar C++ restatement of SyNeRFgine's render hot path, used
+ * ONLY by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * parity checker.  The product (libsng_hip.so) never links or calls it.
+ *
+ * Parity status: PARTIALLY PINNED.  The reference (/root/reference) cannot be
+ * compiled here (CUDA headers absent, tiny-cuda-nn submodule unvendored) and
+ * ships no golden vectors.  Functions that restate reference code are cited
+ * (file:line, relative to the reference root); functions that restate
+ * tiny-cuda-nn / cuRAND semantics are marked [tcnn, unvendored] /
+ * [cuRAND, unvendored] and are pinned only by published constants
+ * (SURVEY.md Appendix B/C level tables, SH constants) -- "parity unpinned"
+ * for those parts.  See DESIGN.md "Oracle".
+ */
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- scene / model descriptors (oracle-private, plain C) ---------------- */
+typedef struct {
+    uint32_t n_levels;          /* L   (base.json:23-29) */
+    uint32_t n_features;        /* F   */
+    uint32_t log2_hashmap_size; /* log2 T */
+    uint32_t base_resolution;   /* Nmin */
+    float per_level_scale;      /* b (read from snapshot, testbed.cu:3737-3741) */
+    const uint16_t* params;     /* fp16 blob: density MLP (3072), rgb MLP (7168), grid */
+} orc_model;
+
+typedef struct {
+    float render_aabb_min[3], render_aabb_max[3];
+    float train_aabb_min[3], train_aabb_max[3];
+    float render_aabb_to_local[9]; /* column-major mat3 */
+    float cone_angle_constant;
+    uint32_t max_mip;              /* m_nerf.max_cascade */
+    float min_transmittance;       /* render_min_transmittance, testbed.h:867 */
+    const uint8_t* bitfield;       /* NERF_CASCADES * 128^3 / 8 bytes, Morton order */
+} orc_volume;
+
+typedef struct {
+    float camera[12];          /* mat4x3, column-major (right, down, fwd, pos) */
+    float focal[2];
+    float screen_center[2];
+    int32_t res[2];
+    uint32_t spp;              /* render_buffer.spp (sample index) */
+    int32_t snap_to_pixel_centers;
+    uint32_t target_n_queries; /* 2*1024*1024 in the reference (testbed_nerf.cu:2189) */
+} orc_camera;
+
+typedef struct {
+    const float* nodes;  /* n_nodes x 8 floats: bb.min xyz, bb.max xyz, left_idx (int bits), right_idx (int bits) */
+    const float* tris;   /* n_tris x 9 floats: a, b, c */
+    float rot[9];        /* column-major mat3 */
+    float pos[3];
+    float scale;
+    int32_t mat_id;
+} orc_object;
+
+typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } orc_light;
+typedef struct { float ka[3], kd[3], ks[3]; float n, rg, spec_angle; int32_t type; /* 0 lambertian, 1 glossy */ } orc_material;
+
+typedef struct {
+    uint32_t n_iterations;    /* wavefront iterations executed */
+    uint64_t n_samples;       /* real (non-stale) network samples */
+    uint64_t n_slots;         /* reference slots incl. stale + padding */
+    uint32_t n_hit;           /* rays in the hit list */
+    uint32_t alive_per_iter[64];
+    uint32_t steps_per_iter[64];
+} orc_nerf_stats;
+
+typedef struct {
+    int32_t nerf_res[2];
+    int32_t mesh_res[2];
+    int32_t syn_px_scale;           /* m_relative_vo_scale */
+    int32_t show_nerf;              /* m_show_nerf */
+    int32_t show_virtual_obj;       /* RayTracer::m_show_virtual_obj */
+    int32_t shadow_on_nerf;         /* m_view_syn_shadow */
+    int32_t shadow_on_virtual_obj;  /* RayTracer::m_view_nerf_shadow */
+    float nerf_shadow_intensity;    /* engine.cuh:117 */
+    float nerf_on_nerf_shadow_threshold; /* engine.cuh:119 */
+    int32_t nerf_kernel_size;       /* Testbed::sng_position_kernel_size (testbed.h:686) */
+    uint32_t light_samples;         /* RayTracer::m_samples */
+    uint32_t path_trace_depth;      /* RayTracer::m_ray_iters */
+    uint32_t shadow_iters;          /* RayTracer::m_shadow_iters */
+    uint32_t shadow_steps;          /* RayTracer::m_n_steps (8) */
+    float lens_angle_constant;      /* RayTracer::m_lens_angle_constant */
+    float syn_shadow_factor;        /* RayTracer::m_syn_shadow_factor */
+    float rt_depth_offset;          /* RayTracer::m_depth_offset (overlay z-test) */
+    float exposure;
+    int32_t srgb_output;            /* EColorSpace::SRGB (engine.cu:406) */
+} orc_frame_params;
+
+/* ---- primitives (KAT-level) --------------------------------------------- */
+uint32_t orc_morton3D(uint32_t x, uint32_t y, uint32_t z);
+uint32_t orc_morton3D_invert(uint32_t x);
+uint32_t orc_sobol(uint32_t index, uint32_t dim);
+float    orc_ld_random_val(uint32_t index, uint32_t seed, uint32_t dim);
+void     orc_ld_random_pixel_offset(uint32_t spp, float out[2]);
+uint16_t orc_float_to_half(float f);
+float    orc_half_to_float(uint16_t h);
+
+/* cuRAND XORWOW [cuRAND, unvendored] */
+void     orc_xorwow_init(uint64_t seed, uint64_t subsequence, uint64_t offset, uint32_t state[6]);
+void     orc_xorwow_init_many(uint64_t seed, uint32_t n, uint32_t* states /* n x 6 */);
+uint32_t orc_xorwow_next(uint32_t state[6]);
+float    orc_curand_uniform(uint32_t state[6]);
+void     orc_xorwow_jump_steps_naive(uint32_t state[6], uint64_t steps); /* stepping (test helper) */
+void     orc_xorwow_jump_matrix(uint32_t state[6], uint32_t log2_steps);  /* M^(2^k) (test helper) */
+
+/* ---- network (A6-A8) ----------------------------------------------------- */
+uint32_t orc_grid_level_table(const orc_model* m, uint32_t* offsets /* L+1 */, uint32_t* resolutions /* L */);
+uint32_t orc_n_params(const orc_model* m);
+void orc_hashgrid_encode(const orc_model* m, const float* coords, uint32_t stride_floats, uint32_t n, uint16_t* out /* n x L*F */);
+void orc_sh_encode(const float* coords, uint32_t stride_floats, uint32_t dir_offset, uint32_t n, uint16_t* out /* n x 16 */);
+void orc_nerf_inference(const orc_model* m, const float* coords, uint32_t stride_floats, uint32_t n, uint16_t* out /* n x 16 (tcnn rgbsigma row block) */);
+
+/* ---- occupancy (A17) ------------------------------------------------------ */
+void orc_density_grid_to_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, uint8_t* bitfield /* 8*128^3/8 */, float* mean_out);
+
+/* ---- NeRF render (A1-A5, A9-A10c) --------------------------------------- */
+void orc_render_nerf(const orc_model* m, const orc_volume* v, const orc_camera* c,
+                     float* frame_rgba /* W*H*4, in/out */, float* frame_depth /* W*H, in/out */,
+                     float* positions /* W*H*3 out */, float* normals /* W*H*3 out */,
+                     orc_nerf_stats* stats);
+
+/* ---- shadows on NeRF (A11) ---------------------------------------------- */
+void orc_shade_nerf_shadows(const orc_volume* v, const int32_t res[2],
+                            float* frame_rgba, const float* positions, const float* normals,
+                            const orc_object* objs, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
+                            uint32_t* rng_states /* W*H*6, in/out */,
+                            float nerf_shadow_intensity, float nerf_on_nerf_shadow_threshold, int32_t kernel_size);
+
+/* ---- BVH (A12, A13) ------------------------------------------------------ */
+int32_t orc_bvh_build(float* tris /* n x 9, reordered in place */, uint32_t n_tris, uint32_t prims_per_leaf, float* nodes_out /* cap x 8 */, uint32_t cap);
+void orc_depth_test_world(const orc_object* objs, uint32_t n_objs, const float* origins, const float* dirs, uint32_t n, float* t_out, int32_t* obj_out);
+
+/* ---- virtual objects (A14, A15, A19) ------------------------------------- */
+void orc_mesh_init_rays(const orc_camera* c, float* origins, float* dirs, float* acc_rgba, float* acc_depth);
+void orc_raytrace(const orc_volume* v, const float* camera /* mat4x3 */, const orc_frame_params* p,
+                  const orc_object* objs, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
+                  const orc_material* mats, uint32_t n_mats,
+                  const float* origins, const float* dirs, uint32_t n,
+                  uint32_t* rng_states, float* acc_rgba, float* acc_depth);
+void orc_overlay(const orc_frame_params* p, const float* syn_rgba, const float* syn_depth,
+                 const float* nerf_rgba, const float* nerf_depth, float* final_rgba, float* final_depth);
+
+/* ---- whole frame (A18-A20) ------------------------------------------------ */
+void orc_render_frame(const orc_model* m, const orc_volume* v, const orc_camera* nerf_cam, const orc_camera* mesh_cam,
+                      const orc_frame_params* p,
+                      const orc_object* objs, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
+                      const orc_material* mats, uint32_t n_mats,
+                      uint32_t* nerf_rng, uint32_t* mesh_rng,
+                      float* final_rgba, float* final_depth,
+                      float* nerf_rgba, float* nerf_depth, orc_nerf_stats* stats);
+
+int32_t orc_num_threads(void);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,224 @@
+"""synerfgine_amd -- MI355X-native SyNeRFgine render path.
+
+Host-side mirror of the reference's C++ objects on the hot path, thin over the
+C-ABI of libsng_hip.so (include/sng.h):
+
+    Testbed  ~ ngp::Testbed     (load_snapshot, NeRF model, density bitfield, camera,
+                                  NerfNetwork::inference_mixed_precision)
+    Engine   ~ sng::Engine      (set_virtual_world, init/resize, frame)
+
+All compute runs in the HIP kernels of libsng_hip.so; nothing here falls back
+to the CPU.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import SngError, check
+
+__all__ = ["Testbed", "Engine", "FrameResult", "SngError", "device_count"]
+
+
+def device_count():
+    lib = _lib.load()
+    n = ctypes.c_int(0)
+    check(lib.sng_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def _fptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+class Testbed:
+    """ngp::Testbed subset on the SyNeRFgine path (one context per GPU)."""
+
+    def __init__(self, device_id=0):
+        self._lib = _lib.load()
+        desc = _lib.sng_ctx_desc(device_id=device_id)
+        ctx = ctypes.c_void_p()
+        check(self._lib.sng_ctx_create(ctypes.byref(desc), ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.device_id = device_id
+
+    def close(self):
+        if self.ctx:
+            check(self._lib.sng_ctx_destroy(self.ctx))
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- model (Testbed::load_snapshot, testbed.cu:4994) -----------------------
+    def load_snapshot(self, path):
+        check(self._lib.sng_load_snapshot(self.ctx, str(path).encode()))
+
+    def set_nerf_model(self, cfg, params):
+        params = np.ascontiguousarray(params, dtype=np.float16)
+        c = _lib.sng_nerf_config(**cfg)
+        check(self._lib.sng_set_nerf_model(self.ctx, ctypes.byref(c), params.view(np.uint16).ctypes.data_as(_lib.U16P), params.size))
+
+    def set_density_grid(self, grid_f16):
+        g = np.ascontiguousarray(grid_f16, dtype=np.float16)
+        check(self._lib.sng_set_density_grid(self.ctx, g.view(np.uint16).ctypes.data_as(_lib.U16P), g.size))
+
+    def density_grid_bitfield(self):
+        out = np.zeros(128 ** 3 // 8 * 8, dtype=np.uint8)
+        check(self._lib.sng_get_bitfield(self.ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), out.size))
+        return out
+
+    def density_grid_mean(self):
+        v = ctypes.c_float()
+        check(self._lib.sng_get_density_mean(self.ctx, ctypes.byref(v)))
+        return v.value
+
+    # ---- NerfNetwork::inference_mixed_precision (nerf_network.h:105) -------------
+    def inference_mixed_precision(self, d_coords, stride_floats, n, d_out, layout=0, stream=0):
+        """Device pointers in, device pointer out (layout 0: tcnn [16][n]; 1: [n][4])."""
+        check(self._lib.sng_nerf_inference(self.ctx, ctypes.c_void_p(d_coords), stride_floats, n, ctypes.c_void_p(d_out), layout,
+                                           ctypes.c_void_p(stream)))
+
+    def encode(self, d_coords, stride_floats, n, d_out, stream=0):
+        check(self._lib.sng_hashgrid_encode(self.ctx, ctypes.c_void_p(d_coords), stride_floats, n, ctypes.c_void_p(d_out),
+                                            ctypes.c_void_p(stream)))
+
+    # ---- camera (testbed.cu:405-425) ---------------------------------------------
+    def set_camera_view(self, view_dir, look_at, scale):
+        v = np.asarray(view_dir, np.float32)
+        a = np.asarray(look_at, np.float32)
+        check(self._lib.sng_set_camera_view(self.ctx, _fptr(v), _fptr(a), float(scale)))
+
+    @property
+    def camera_matrix(self):
+        m = np.zeros(12, np.float32)
+        check(self._lib.sng_get_camera_matrix(self.ctx, _fptr(m)))
+        return m
+
+    @camera_matrix.setter
+    def camera_matrix(self, m):
+        m = np.ascontiguousarray(m, np.float32).ravel()
+        check(self._lib.sng_set_camera_matrix(self.ctx, _fptr(m)))
+
+    def set_fov(self, degrees):
+        check(self._lib.sng_set_fov(self.ctx, float(degrees)))
+
+    def focal_length(self, which=0):
+        f = np.zeros(2, np.float32)
+        check(self._lib.sng_get_focal_length(self.ctx, which, _fptr(f)))
+        return f
+
+
+class FrameResult:
+    def __init__(self, engine, r):
+        self._engine = engine
+        self.raw = r
+        for name in ("n_iterations", "n_hit", "n_samples", "n_reference_slots", "ms_frame", "ms_raytrace", "ms_nerf", "ms_shadow",
+                     "ms_overlay", "ms_network", "network_launches"):
+            setattr(self, name, getattr(r, name))
+        self.alive_per_iter = list(r.alive_per_iter)[: min(64, r.n_iterations)]
+        self.steps_per_iter = list(r.steps_per_iter)[: min(64, r.n_iterations)]
+
+    def download(self, name):
+        """Copy a device output buffer to host as float32 [H, W, C]."""
+        e = self._engine
+        res = e.resolution()
+        shapes = {
+            "final_rgba": (res["mesh"], 4), "final_depth": (res["mesh"], 1), "syn_rgba": (res["mesh"], 4), "syn_depth": (res["mesh"], 1),
+            "nerf_rgba": (res["nerf"], 4), "nerf_depth": (res["nerf"], 1), "nerf_positions": (res["nerf"], 3),
+            "nerf_normals": (res["nerf"], 3),
+        }
+        (w, h), c = shapes[name]
+        out = np.empty((h, w, c), np.float32)
+        ptr = getattr(self.raw, "d_" + name)
+        check(e._lib.sng_copy_to_host(e.ctx, ctypes.c_void_p(ptr), out.ctypes.data_as(ctypes.c_void_p), out.nbytes))
+        return out
+
+
+class Engine:
+    """sng::Engine (synerfgine/engine.cu): virtual world, resize and the frame loop."""
+
+    def __init__(self, testbed):
+        self.testbed = testbed
+        self._lib = testbed._lib
+        self.ctx = testbed.ctx
+
+    def set_virtual_world(self, json_path):
+        check(self._lib.sng_load_virtual_scene(self.ctx, str(json_path).encode()))
+
+    def init(self, width, height):
+        check(self._lib.sng_set_window(self.ctx, int(width), int(height)))
+
+    def set_syn_samples(self, spp):      # --sshadows (engine.cuh:29)
+        self.set_param("sshadows", spp)
+
+    def set_nerf_samples(self, k):       # --nshadows (engine.cuh:30-33)
+        self.set_param("nshadows", k)
+
+    def set_param(self, key, value):
+        check(self._lib.sng_set_param(self.ctx, key.encode(), float(value)))
+
+    def get_param(self, key):
+        v = ctypes.c_double()
+        check(self._lib.sng_get_param(self.ctx, key.encode(), ctypes.byref(v)))
+        return v.value
+
+    def resolution(self):
+        r = _lib.sng_resolution_info()
+        check(self._lib.sng_get_resolution(self.ctx, ctypes.byref(r)))
+        return {"nerf": tuple(r.nerf_res), "mesh": tuple(r.mesh_res), "syn_px_scale": r.syn_px_scale}
+
+    def frame(self, spp=0, reset=True, rows=None, collect_kernel_times=False, target_n_queries=0):
+        p = _lib.sng_frame_params(spp=spp, reset_accumulation=1 if reset else 0, collect_kernel_times=1 if collect_kernel_times else 0,
+                                  target_n_queries=target_n_queries)
+        if rows is not None:
+            p.row_begin, p.row_end = rows
+        r = _lib.sng_frame_result()
+        check(self._lib.sng_render_frame(self.ctx, ctypes.byref(p), ctypes.byref(r)))
+        return FrameResult(self, r)
+
+    # ---- scene inspection (tests) --------------------------------------------------
+    def scene(self):
+        no, nl, nm = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        check(self._lib.sng_get_scene_counts(self.ctx, ctypes.byref(no), ctypes.byref(nl), ctypes.byref(nm)))
+        objs = []
+        for i in range(no.value):
+            info = _lib.sng_object_info()
+            check(self._lib.sng_get_object(self.ctx, i, ctypes.byref(info)))
+            nodes = np.zeros((info.n_nodes, 8), np.float32)
+            tris = np.zeros((info.n_tris, 9), np.float32)
+            check(self._lib.sng_get_object_bvh(self.ctx, i, _fptr(nodes), _fptr(tris)))
+            objs.append(dict(nodes=nodes, tris=tris, rot=np.array(info.rot, np.float32), pos=np.array(info.pos, np.float32),
+                             scale=info.scale, mat_id=info.mat_id))
+        lights = []
+        for i in range(nl.value):
+            l = _lib.sng_light()
+            check(self._lib.sng_get_light(self.ctx, i, ctypes.byref(l)))
+            lights.append(dict(pos=list(l.pos), intensity=l.intensity, size=l.size, type=l.type))
+        mats = []
+        for i in range(nm.value):
+            m = _lib.sng_material()
+            check(self._lib.sng_get_material(self.ctx, i, ctypes.byref(m)))
+            mats.append(dict(ka=list(m.ka), kd=list(m.kd), ks=list(m.ks), n=m.n, rg=m.rg, spec_angle=m.spec_angle, type=m.type))
+        return objs, lights, mats
+
+    def rng_states(self, which):
+        res = self.resolution()
+        w, h = res["nerf"] if which == 0 else res["mesh"]
+        out = np.zeros((w * h, 6), np.uint32)
+        check(self._lib.sng_get_rng_states(self.ctx, which, out.ctypes.data_as(_lib.U32P), w * h))
+        return out
+
+
+def bvh_build(tris, prims_per_leaf=4):
+    """TriangleBvhWithBranchingFactor<2>::build on the host (A13). Returns (nodes [n,8], reordered tris)."""
+    lib = _lib.load()
+    t = np.ascontiguousarray(tris, np.float32).reshape(-1, 9).copy()
+    cap = 4 * t.shape[0] + 8
+    nodes = np.zeros((cap, 8), np.float32)
+    n = ctypes.c_uint32()
+    check(lib.sng_bvh_build(_fptr(t), t.shape[0], prims_per_leaf, _fptr(nodes), cap, ctypes.byref(n)))
+    return nodes[: n.value], t

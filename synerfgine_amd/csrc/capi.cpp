@@ -1,0 +1,1247 @@
+// capi.cpp -- host runtime (C++) behind the C-ABI in include/sng.h.
+//
+// Mirrors the reference's host objects on the hot path:
+//   Testbed   : model/snapshot, density bitfield, camera (testbed.cu:405-425, 3562, 4133-4140, 4878-5015)
+//   NerfTracer: the device-driven wavefront loop (testbed_nerf.cu:2128-2277)
+//   RayTracer : mesh rays, path tracing, overlay (synerfgine/raytracer.cu:260-392)
+//   Engine    : scene JSON, rendering.* keys, resize and frame (synerfgine/engine.cu:21-433)
+#include "../../include/sng.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <stack>
+#include <string>
+#include <vector>
+
+#include "json.h"
+#include "sng_internal.h"
+
+using namespace sng;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct SngError : std::runtime_error {
+    int code;
+    SngError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t e_ = (x);                                                                               \
+        if (e_ != hipSuccess) throw SngError(SNG_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return SNG_OK;
+    } catch (const SngError& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return SNG_ERR_INVALID;
+    }
+}
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t n) {
+        if (n <= bytes && p) return;
+        if (p) HIPCHK(hipFree(p));
+        p = nullptr;
+        bytes = 0;
+        if (n == 0) return;
+        HIPCHK(hipMalloc(&p, n));
+        bytes = n;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// ---- fp16 host conversion (RTE) ------------------------------------------------
+uint16_t f2h_host(float f) {
+    uint32_t x;
+    std::memcpy(&x, &f, 4);
+    uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+    if (ax > 0x7f800000u) return (uint16_t)(sign | 0x7e00u);
+    if (ax >= 0x47800000u) return (uint16_t)(sign | 0x7c00u);
+    if (ax >= 0x38800000u) {
+        uint32_t mant = ax & 0x7fffffu, e = (ax >> 23) - 127 + 15;
+        uint32_t h = (e << 10) | (mant >> 13), rem = mant & 0x1fffu;
+        if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+        return (uint16_t)(sign | h);
+    }
+    if (ax < 0x33000000u) return (uint16_t)sign;
+    uint32_t e = ax >> 23, mant = (ax & 0x7fffffu) | 0x800000u, shift = 126 - e;
+    uint32_t h = mant >> shift, rem = mant & ((1u << shift) - 1u), half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+}
+
+// ---- cuRAND XORWOW subsequence matrices M^(2^67 * 2^k), k < 32 -------------------
+struct Gf2 { uint32_t col[160][5]; };
+void gf2_apply(const Gf2& m, const uint32_t in[5], uint32_t out[5]) {
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int j = 0; j < 160; ++j)
+        if ((in[j >> 5] >> (j & 31)) & 1u)
+            for (int w = 0; w < 5; ++w) r[w] ^= m.col[j][w];
+    std::memcpy(out, r, sizeof(r));
+}
+void gf2_square(const Gf2& a, Gf2& out) {
+    Gf2 r;
+    for (int j = 0; j < 160; ++j) gf2_apply(a, a.col[j], r.col[j]);
+    out = r;
+}
+const std::vector<uint32_t>& xorwow_seq_tables() {
+    static std::vector<uint32_t> tab;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        Gf2 m;
+        for (int j = 0; j < 160; ++j) {
+            uint32_t v[5] = {0, 0, 0, 0, 0};
+            v[j >> 5] = 1u << (j & 31);
+            uint32_t t = v[0] ^ (v[0] >> 2);
+            v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+            v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+            std::memcpy(m.col[j], v, sizeof(v));
+        }
+        for (int i = 0; i < 67; ++i) gf2_square(m, m);
+        tab.resize((size_t)32 * 160 * 5);
+        for (int k = 0; k < 32; ++k) {
+            std::memcpy(&tab[(size_t)k * 800], m.col, 800 * 4);
+            gf2_square(m, m);
+        }
+    });
+    return tab;
+}
+
+// ---- OBJ (tinyobj::LoadObj subset: v + polygon faces, fan-triangulated) ----------
+std::vector<Tri> load_obj(const std::string& path) {
+    std::ifstream f(path);
+    if (!f) throw SngError(SNG_ERR_IO, "Error loading file: " + path);
+    std::vector<f3> verts;
+    std::vector<Tri> tris;
+    std::string line;
+    while (std::getline(f, line)) {
+        if (line.size() < 2) continue;
+        if (line[0] == 'v' && line[1] == ' ') {
+            std::istringstream ss(line.substr(2));
+            float x, y, z;
+            ss >> x >> y >> z;
+            verts.push_back({x, y, z});
+        } else if (line[0] == 'f' && line[1] == ' ') {
+            std::istringstream ss(line.substr(2));
+            std::string tok;
+            std::vector<int> idx;
+            while (ss >> tok) {
+                int vi = std::stoi(tok.substr(0, tok.find('/')));
+                idx.push_back(vi > 0 ? vi - 1 : (int)verts.size() + vi);
+            }
+            for (size_t k = 1; k + 1 < idx.size(); ++k) tris.push_back({verts.at(idx[0]), verts.at(idx[k]), verts.at(idx[k + 1])});
+        }
+    }
+    return tris;
+}
+
+// ---- TriangleBvhWithBranchingFactor<2>::build (triangle_bvh.cu:615-692) ----------
+std::vector<BvhNode> build_bvh(std::vector<Tri>& tris, uint32_t ppl) {
+    struct BB { f3 lo, hi; };
+    auto bb_of = [](std::vector<Tri>::iterator b, std::vector<Tri>::iterator e) {
+        BB bb{b->a, b->a};
+        auto grow = [&](f3 p) {
+            bb.lo = mk(fminf(bb.lo.x, p.x), fminf(bb.lo.y, p.y), fminf(bb.lo.z, p.z));
+            bb.hi = mk(fmaxf(bb.hi.x, p.x), fmaxf(bb.hi.y, p.y), fmaxf(bb.hi.z, p.z));
+        };
+        for (auto it = b; it != e; ++it) { grow(it->a); grow(it->b); grow(it->c); }
+        return bb;
+    };
+    auto centroid = [](const Tri& t) { return (t.a + t.b + t.c) / 3.0f; };
+    auto centroid_axis = [](const Tri& t, int ax) {
+        const float* a = &t.a.x; const float* b = &t.b.x; const float* c = &t.c.x;
+        return (a[ax] + b[ax] + c[ax]) / 3;
+    };
+    auto set_bb = [](BvhNode& n, const BB& bb) {
+        n.lo[0] = bb.lo.x; n.lo[1] = bb.lo.y; n.lo[2] = bb.lo.z;
+        n.hi[0] = bb.hi.x; n.hi[1] = bb.hi.y; n.hi[2] = bb.hi.z;
+    };
+    std::vector<BvhNode> nodes(1);
+    set_bb(nodes[0], bb_of(tris.begin(), tris.end()));
+    struct BuildNode { int node_idx; std::vector<Tri>::iterator begin, end; };
+    std::stack<BuildNode> st;
+    st.push({0, tris.begin(), tris.end()});
+    while (!st.empty()) {
+        BuildNode curr = st.top();
+        st.pop();
+        BuildNode ch[2];
+        ch[0].begin = curr.begin;
+        ch[0].end = curr.end;
+        {
+            auto& c = ch[0];
+            f3 mean = splat(0.0f);
+            for (auto it = c.begin; it != c.end; ++it) mean = mean + centroid(*it);
+            mean = mean / (float)std::distance(c.begin, c.end);
+            f3 var = splat(0.0f);
+            for (auto it = c.begin; it != c.end; ++it) { f3 d = centroid(*it) - mean; var = var + d * d; }
+            var = var / (float)std::distance(c.begin, c.end);
+            float mv = std::max(std::max(var.x, var.y), var.z);
+            int axis = var.x == mv ? 0 : (var.y == mv ? 1 : 2);
+            auto mid = c.begin + std::distance(c.begin, c.end) / 2;
+            std::nth_element(c.begin, mid, c.end, [&](const Tri& a, const Tri& b) { return centroid_axis(a, axis) < centroid_axis(b, axis); });
+            ch[1].end = c.end;
+            ch[0].end = ch[1].begin = mid;
+        }
+        nodes[curr.node_idx].left = (int)nodes.size();
+        for (int i = 0; i < 2; ++i) {
+            ch[i].node_idx = (int)nodes.size();
+            nodes.emplace_back();
+            set_bb(nodes.back(), bb_of(ch[i].begin, ch[i].end));
+            if ((uint32_t)std::distance(ch[i].begin, ch[i].end) <= ppl) {
+                nodes.back().left = -(int)std::distance(tris.begin(), ch[i].begin) - 1;
+                nodes.back().right = -(int)std::distance(tris.begin(), ch[i].end) - 1;
+            } else {
+                st.push(ch[i]);
+            }
+        }
+        nodes[curr.node_idx].right = (int)nodes.size();
+    }
+    return nodes;
+}
+
+// glm-style adjugate inverse (tcnn::inverse(mat3)) -- column-major m.c[i] = column i
+m3 inverse3(const m3& M) {
+    auto e = [&](int i, int j) { const f3& c = i == 0 ? M.c0 : (i == 1 ? M.c1 : M.c2); return j == 0 ? c.x : (j == 1 ? c.y : c.z); };
+    float det = e(0, 0) * (e(1, 1) * e(2, 2) - e(2, 1) * e(1, 2)) - e(1, 0) * (e(0, 1) * e(2, 2) - e(2, 1) * e(0, 2)) +
+                e(2, 0) * (e(0, 1) * e(1, 2) - e(1, 1) * e(0, 2));
+    float r[3][3];
+    r[0][0] = +(e(1, 1) * e(2, 2) - e(2, 1) * e(1, 2));
+    r[1][0] = -(e(1, 0) * e(2, 2) - e(2, 0) * e(1, 2));
+    r[2][0] = +(e(1, 0) * e(2, 1) - e(2, 0) * e(1, 1));
+    r[0][1] = -(e(0, 1) * e(2, 2) - e(2, 1) * e(0, 2));
+    r[1][1] = +(e(0, 0) * e(2, 2) - e(2, 0) * e(0, 2));
+    r[2][1] = -(e(0, 0) * e(2, 1) - e(2, 0) * e(0, 1));
+    r[0][2] = +(e(0, 1) * e(1, 2) - e(1, 1) * e(0, 2));
+    r[1][2] = -(e(0, 0) * e(1, 2) - e(1, 0) * e(0, 2));
+    r[2][2] = +(e(0, 0) * e(1, 1) - e(1, 0) * e(0, 1));
+    return {mk(r[0][0] / det, r[0][1] / det, r[0][2] / det), mk(r[1][0] / det, r[1][1] / det, r[1][2] / det),
+            mk(r[2][0] / det, r[2][1] / det, r[2][2] / det)};
+}
+
+// get_xform_given_rolling_shutter(start == end, t = 0) rotation: glm quat round trip
+// (common_device.cuh:361-368) [tcnn quat, unvendored]
+m3 rolling_shutter_rotation(const m3& M) {
+    auto e = [&](int i, int j) { const f3& c = i == 0 ? M.c0 : (i == 1 ? M.c1 : M.c2); return j == 0 ? c.x : (j == 1 ? c.y : c.z); };
+    float fx = e(0, 0) - e(1, 1) - e(2, 2), fy = e(1, 1) - e(0, 0) - e(2, 2), fz = e(2, 2) - e(0, 0) - e(1, 1), fw = e(0, 0) + e(1, 1) + e(2, 2);
+    int bi = 0;
+    float fb = fw;
+    if (fx > fb) { fb = fx; bi = 1; }
+    if (fy > fb) { fb = fy; bi = 2; }
+    if (fz > fb) { fb = fz; bi = 3; }
+    float bv = std::sqrt(fb + 1.0f) * 0.5f, mult = 0.25f / bv;
+    float q[4];  // x y z w
+    switch (bi) {
+        case 0: q[0] = (e(1, 2) - e(2, 1)) * mult; q[1] = (e(2, 0) - e(0, 2)) * mult; q[2] = (e(0, 1) - e(1, 0)) * mult; q[3] = bv; break;
+        case 1: q[0] = bv; q[1] = (e(0, 1) + e(1, 0)) * mult; q[2] = (e(2, 0) + e(0, 2)) * mult; q[3] = (e(1, 2) - e(2, 1)) * mult; break;
+        case 2: q[0] = (e(0, 1) + e(1, 0)) * mult; q[1] = bv; q[2] = (e(1, 2) + e(2, 1)) * mult; q[3] = (e(2, 0) - e(0, 2)) * mult; break;
+        default: q[0] = (e(2, 0) + e(0, 2)) * mult; q[1] = (e(1, 2) + e(2, 1)) * mult; q[2] = bv; q[3] = (e(0, 1) - e(1, 0)) * mult; break;
+    }
+    float cos_theta = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+    float s[4];
+    if (cos_theta > 1.0f - 1.1920929e-7f) {
+        for (int k = 0; k < 4; ++k) s[k] = q[k] * (1.0f - 0.0f) + q[k] * 0.0f;
+    } else {
+        float angle = std::acos(cos_theta);
+        float s0 = std::sin((1.0f - 0.0f) * angle), s1 = std::sin(0.0f * angle), sa = std::sin(angle);
+        for (int k = 0; k < 4; ++k) s[k] = (s0 * q[k] + s1 * q[k]) / sa;
+    }
+    float len = std::sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2] + s[3] * s[3]);
+    for (int k = 0; k < 4; ++k) s[k] = s[k] / len;
+    float qxx = s[0] * s[0], qyy = s[1] * s[1], qzz = s[2] * s[2], qxz = s[0] * s[2], qxy = s[0] * s[1], qyz = s[1] * s[2];
+    float qwx = s[3] * s[0], qwy = s[3] * s[1], qwz = s[3] * s[2];
+    return {mk(1.0f - 2.0f * (qyy + qzz), 2.0f * (qxy + qwz), 2.0f * (qxz - qwy)),
+            mk(2.0f * (qxy - qwz), 1.0f - 2.0f * (qxx + qzz), 2.0f * (qyz + qwx)),
+            mk(2.0f * (qxz + qwy), 2.0f * (qyz - qwx), 1.0f - 2.0f * (qxx + qyy))};
+}
+
+struct HostObject {
+    std::string file;
+    std::vector<Tri> tris;
+    std::vector<BvhNode> nodes;
+    m3 rot;
+    f3 pos;
+    float scale = 1.0f;
+    int mat = 0;
+    DevBuf d_nodes, d_tris;
+};
+
+const std::map<std::string, double>& default_params() {
+    static const std::map<std::string, double> d = {
+        {"res_factor", 64},                     // Testbed::m_fixed_res_factor (testbed.h:656)
+        {"vo_scale", 4},                        // Engine::m_relative_vo_scale (engine.cuh:113)
+        {"exposure", 0.0},                      // Testbed::m_exposure
+        {"path_trace_depth", 2},                // RayTracer::m_ray_iters (raytracer.cuh:160)
+        {"light_samples", 2},                   // RayTracer::m_samples
+        {"syn_shadow_samples", 4},              // RayTracer::m_shadow_iters
+        {"syn_shadow_intensity", 1.0},          // RayTracer::m_syn_shadow_factor
+        {"attenuation", 1.0},                   // RayTracer::m_attenuation_coeff (unused by raytrace)
+        {"lens_size", 0.009},                   // RayTracer::m_lens_angle_constant
+        {"depth_offset", 0.1},                  // RayTracer::m_depth_offset (overlay z-test)
+        {"n_steps", 8},                         // RayTracer::m_n_steps (NeRF shadow steps on meshes)
+        {"nerf_shadow_samples", 1},             // Testbed::sng_position_kernel_size (testbed.h:686)
+        {"nerf_shadow_intensity", 2.0},         // Engine::m_nerf_shadow_intensity (engine.cuh:117)
+        {"nerf_ao_intensity", 2.0},             // Engine::m_nerf_ao_intensity
+        {"nerf_on_nerf_shadow_threshold", 0.3}, // Engine::m_nerf_self_shadow_threshold
+        {"shadow_on_nerf", 1},                  // Engine::m_view_syn_shadow
+        {"shadow_on_virtual_obj", 1},           // RayTracer::m_view_nerf_shadow
+        {"show_virtual_obj", 1},                // RayTracer::m_show_virtual_obj
+        {"show_nerf", 1},                       // Engine::m_show_nerf
+        {"min_transmittance", 0.01},            // render_min_transmittance (testbed.h:867)
+        {"srgb", 1},                            // EColorSpace::SRGB passed to overlay (engine.cu:406)
+        {"smooth_threshold", 1.0},              // sng_position_kernel_threshold (unused by the path)
+        {"max_shadow_variance", 0.0},           // sng_shadow_depth_variance (unused by the path)
+    };
+    return d;
+}
+
+}  // namespace
+
+struct sng_ctx {
+    int device = 0;
+    int n_cus = 256;
+    hipStream_t s_nerf = nullptr, s_rt = nullptr;
+    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr;
+    std::vector<hipEvent_t> net_events;
+
+    // model
+    bool has_model = false;
+    sng_nerf_config cfg{};
+    NetworkDev net;
+    DevBuf d_wfrag, d_grid, d_levels;
+    std::vector<LevelInfo> levels;
+    uint64_t n_params = 0;
+    uint32_t max_cascade = 0;
+    float cone = 0.0f;
+    aabb box{};
+
+    // occupancy
+    bool has_bitfield = false;
+    DevBuf d_bitfield, d_grid_f16, d_grid_f32, d_partial, d_mean;
+
+    // camera (Testbed)
+    float cam[12] = {1, 0, 0, 0, -1, 0, 0, 0, -1, 0.5f, 0.5f, 2.0f};
+    float m_scale = 1.5f;
+    f3 up = {0.0f, 1.0f, 0.0f};
+    float rel_focal[2] = {0, 0};
+    int fov_axis = 1;
+    float zoom = 1.0f;
+    float screen_center[2] = {0.5f, 0.5f};
+
+    std::map<std::string, double> params = default_params();
+
+    // window / resolution
+    int win[2] = {0, 0};
+    int nerf_res[2] = {0, 0}, mesh_res[2] = {0, 0};
+    int vo_scale_eff = 1;
+    int last_res_factor = -1;
+
+    // buffers
+    DevBuf nerf_rgba, nerf_depth, nerf_pos, nerf_nrm;
+    DevBuf ray_ot[2], ray_di[2], ray_rgba[2], ray_depth[2];
+    DevBuf samp, coords, net_out, ctrl;
+    size_t ray_cap = 0, sample_cap = 0;
+    DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
+    DevBuf rng_nerf, rng_mesh;
+    uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
+    DevBuf d_seq;
+    MarchCtrl* h_ctrl = nullptr;
+    uint32_t* h_alive = nullptr;  // pinned readback [chunk][2]
+    bool mesh_reset = true;
+
+    // scene (Engine)
+    std::vector<HostObject> objs;
+    std::vector<sng_light> lights;
+    std::vector<sng_material> mats;
+    DevBuf d_objs, d_lights, d_mats;
+    bool scene_dirty = true;
+
+    double p(const char* k) const { return params.at(k); }
+};
+
+namespace {
+
+void upload(DevBuf& b, const void* src, size_t n) {
+    b.ensure(n);
+    if (n) HIPCHK(hipMemcpy(b.p, src, n, hipMemcpyHostToDevice));
+}
+
+void compute_levels(sng_ctx* c) {
+    const auto& g = c->cfg;
+    c->levels.clear();
+    float log2_pls = std::log2(g.per_level_scale);
+    uint32_t offset = 0;
+    for (uint32_t i = 0; i < g.n_levels; ++i) {
+        float scale = std::fma(std::exp2((float)i * log2_pls), (float)g.base_resolution, -1.0f);   // grid_scale [tcnn]
+        uint32_t res = (uint32_t)std::ceil(scale) + 1;                                             // grid_resolution [tcnn]
+        uint32_t max_params = 0xffffffffu / 2;
+        uint32_t pil = std::pow((float)res, 3.0f) > (float)max_params ? max_params : res * res * res;
+        pil = (pil + 7u) / 8u * 8u;
+        pil = std::min(pil, 1u << g.log2_hashmap_size);
+        // tcnn grid_index stride loop: dense index kept iff the loop ran all dims and stride <= size
+        uint64_t stride = 1;
+        uint32_t dims = 0;
+        for (; dims < 3 && stride <= pil; ++dims) stride *= res;
+        LevelInfo L{};
+        L.offset = offset;
+        L.size = pil;
+        L.pow2_mask = (pil & (pil - 1)) == 0 ? pil - 1 : 0;
+        L.dense = (dims == 3 && !(pil < stride)) ? 1u : 0u;
+        L.res = res;
+        L.res2 = res * res;
+        L.scale = scale;
+        c->levels.push_back(L);
+        offset += pil;
+    }
+    c->n_params = 3072 + 7168 + (uint64_t)offset * g.n_features_per_level;
+}
+
+// A-fragment image of one layer: frag(lane, j) = W[16mb + (lane&15)][k(kb, lane>>4, j)]
+void pack_layer(const uint16_t* W, int n_in, int mb, int kb, bool permuted, uint16_t* dst) {
+    for (int lane = 0; lane < 64; ++lane) {
+        int row = 16 * mb + (lane & 15), g = lane >> 4;
+        for (int j = 0; j < 8; ++j) {
+            int k = permuted ? 32 * kb + 16 * (j >= 4) + 4 * g + (j & 3) : 32 * kb + 8 * g + j;
+            dst[lane * 8 + j] = W[row * n_in + k];
+        }
+    }
+}
+
+void set_model(sng_ctx* c, const sng_nerf_config* cfg, const uint16_t* params, uint64_t n) {
+    if (!cfg) throw SngError(SNG_ERR_INVALID, "null config");
+    if (cfg->n_levels * cfg->n_features_per_level != 32 || (cfg->n_features_per_level != 4 && cfg->n_features_per_level != 2))
+        throw SngError(SNG_ERR_INVALID, "fused network supports L*F == 32 with F in {2,4} (base.json shape)");
+    if (cfg->aabb_scale == 0 || (cfg->aabb_scale & (cfg->aabb_scale - 1)) || cfg->aabb_scale > 128)
+        throw SngError(SNG_ERR_INVALID, "aabb_scale must be a power of two <= 128 (testbed_nerf.cu:3055-3067)");
+    c->cfg = *cfg;
+    compute_levels(c);
+    if (n != c->n_params) throw SngError(SNG_ERR_INVALID, "param count mismatch: got " + std::to_string(n) + ", expected " + std::to_string(c->n_params));
+    // weight fragments (network.hip header)
+    std::vector<uint16_t> frag(20 * 64 * 8);
+    const uint16_t* dW0 = params;
+    const uint16_t* dW1 = dW0 + 64 * 32;
+    const uint16_t* rW0 = params + 3072;
+    const uint16_t* rW1 = rW0 + 64 * 32;
+    const uint16_t* rW2 = rW1 + 64 * 64;
+    int f = 0;
+    for (int mb = 0; mb < 4; ++mb) pack_layer(dW0, 32, mb, 0, false, &frag[(f++) * 512]);
+    for (int kb = 0; kb < 2; ++kb) pack_layer(dW1, 64, 0, kb, true, &frag[(f++) * 512]);
+    for (int mb = 0; mb < 4; ++mb) pack_layer(rW0, 32, mb, 0, true, &frag[(f++) * 512]);
+    for (int mb = 0; mb < 4; ++mb)
+        for (int kb = 0; kb < 2; ++kb) pack_layer(rW1, 64, mb, kb, true, &frag[(f++) * 512]);
+    for (int kb = 0; kb < 2; ++kb) pack_layer(rW2, 64, 0, kb, true, &frag[(f++) * 512]);
+    upload(c->d_wfrag, frag.data(), frag.size() * 2);
+    upload(c->d_grid, params + 3072 + 7168, (n - 3072 - 7168) * 2);
+    upload(c->d_levels, c->levels.data(), c->levels.size() * sizeof(LevelInfo));
+    c->net.F = (int)cfg->n_features_per_level;
+    c->net.L = (int)cfg->n_levels;
+    c->net.n_cus = c->n_cus;
+    c->net.wfrag = c->d_wfrag.p;
+    c->net.grid = c->d_grid.p;
+    c->net.levels = c->d_levels.as<LevelInfo>();
+    // load_nerf_post (testbed_nerf.cu:3069-3085)
+    float half = 0.5f * (float)std::min(128u, cfg->aabb_scale);
+    c->box = {mk(0.5f - half, 0.5f - half, 0.5f - half), mk(0.5f + half, 0.5f + half, 0.5f + half)};
+    c->max_cascade = 0;
+    while ((1u << c->max_cascade) < cfg->aabb_scale) ++c->max_cascade;
+    c->cone = cfg->aabb_scale <= 1 ? 0.0f : 1.0f / 256.0f;
+    c->has_model = true;
+    c->has_bitfield = false;
+}
+
+void set_density_grid(sng_ctx* c, const uint16_t* grid, uint64_t n_cells) {
+    if (!c->has_model) throw SngError(SNG_ERR_STATE, "set the model before the density grid");
+    if (n_cells != (uint64_t)GRID_CELLS * (c->max_cascade + 1))
+        throw SngError(SNG_ERR_INVALID, "Incompatible number of grid cascades.");   // testbed.cu:4932
+    upload(c->d_grid_f16, grid, n_cells * 2);
+    c->d_grid_f32.ensure(n_cells * 4);
+    c->d_partial.ensure(1024 * sizeof(double));
+    c->d_mean.ensure(sizeof(float));
+    c->d_bitfield.ensure((size_t)GRID_CELLS / 8 * N_CASCADES);
+    launch_bitfield(c->d_grid_f16.as<uint16_t>(), c->max_cascade, c->d_grid_f32.as<float>(), c->d_partial.as<double>(), c->d_mean.as<float>(),
+                    c->d_bitfield.as<uint8_t>(), c->s_nerf);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->s_nerf));
+    c->has_bitfield = true;
+}
+
+Volume make_volume(const sng_ctx* c) {
+    Volume v{};
+    v.render_aabb = c->box;
+    v.train_aabb = c->box;
+    v.to_local = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)};
+    v.to_local_identity = 1;
+    v.cone = c->cone;
+    v.max_mip = c->max_cascade;
+    v.min_transmittance = (float)c->p("min_transmittance");
+    v.bitfield = c->d_bitfield.as<uint8_t>();
+    return v;
+}
+
+// ---- camera (testbed.cu:405-425) -------------------------------------------------
+f3 cam_col(const sng_ctx* c, int i) { return mk(c->cam[3 * i], c->cam[3 * i + 1], c->cam[3 * i + 2]); }
+void set_cam_col(sng_ctx* c, int i, f3 v) { c->cam[3 * i] = v.x; c->cam[3 * i + 1] = v.y; c->cam[3 * i + 2] = v.z; }
+f3 look_at(const sng_ctx* c) { return cam_col(c, 3) + cam_col(c, 2) * c->m_scale; }
+void set_look_at(sng_ctx* c, f3 pos) { set_cam_col(c, 3, cam_col(c, 3) + (pos - look_at(c))); }
+void set_scale(sng_ctx* c, float scale) {
+    f3 prev = look_at(c);
+    set_cam_col(c, 3, (cam_col(c, 3) - prev) * (scale / c->m_scale) + prev);
+    c->m_scale = scale;
+}
+void set_view_dir(sng_ctx* c, f3 dir) {
+    f3 old = look_at(c);
+    f3 c0 = normalize(cross(dir, c->up));
+    set_cam_col(c, 0, c0);
+    set_cam_col(c, 1, normalize(cross(dir, c0)));
+    set_cam_col(c, 2, normalize(dir));
+    set_look_at(c, old);
+}
+float fov_to_focal(float degrees) { return 0.5f * 1.0f / std::tan(0.5f * degrees * 3.14159265358979323846f / 180.0f); }
+
+// ---- scene JSON (Engine::set_virtual_world, engine.cu:21-78; Engine::init keys 148-228) ----
+std::string read_file(const std::string& p) {
+    std::ifstream f(p, std::ios::binary);
+    if (!f) throw SngError(SNG_ERR_IO, "JSON File not found: " + p);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    return ss.str();
+}
+bool file_exists(const std::string& p) { std::ifstream f(p); return (bool)f; }
+
+void upload_scene(sng_ctx* c) {
+    std::vector<ObjectGpu> og;
+    for (auto& o : c->objs) {
+        upload(o.d_nodes, o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
+        upload(o.d_tris, o.tris.data(), o.tris.size() * sizeof(Tri));
+        ObjectGpu g{};
+        g.nodes = o.d_nodes.as<BvhNode>();
+        g.tris = o.d_tris.as<Tri>();
+        g.rot = o.rot;
+        g.pos = o.pos;
+        g.scale = o.scale;
+        g.mat_id = o.mat;
+        m3 msc = {mk(1.0f / o.scale, 0.0f / o.scale, 0.0f / o.scale), mk(0.0f / o.scale, 1.0f / o.scale, 0.0f / o.scale),
+                  mk(0.0f / o.scale, 0.0f / o.scale, 1.0f / o.scale)};
+        g.world_to_obj = mulm(msc, inverse3(o.rot));   // m_scale * m_rotate (triangle_bvh.cu:313-319)
+        og.push_back(g);
+    }
+    upload(c->d_objs, og.data(), og.size() * sizeof(ObjectGpu));
+    std::vector<LightGpu> lg;
+    for (auto& l : c->lights) lg.push_back({mk(l.pos[0], l.pos[1], l.pos[2]), l.intensity, l.size, l.type});
+    upload(c->d_lights, lg.data(), lg.size() * sizeof(LightGpu));
+    std::vector<MaterialGpu> mg;
+    for (auto& m : c->mats)
+        mg.push_back({mk(m.ka[0], m.ka[1], m.ka[2]), mk(m.kd[0], m.kd[1], m.kd[2]), mk(m.ks[0], m.ks[1], m.ks[2]), m.n, m.rg, m.spec_angle, m.type});
+    upload(c->d_mats, mg.data(), mg.size() * sizeof(MaterialGpu));
+    c->scene_dirty = false;
+}
+
+void load_scene(sng_ctx* c, const std::string& path) {
+    JValue cfg = JsonParser(read_file(path)).parse();
+    std::string dir = path.find('/') == std::string::npos ? std::string(".") : path.substr(0, path.find_last_of('/'));
+    if (cfg.contains("camera")) {
+        const JValue& cc = cfg["camera"];
+        f3 view = splat(0.0f), at = splat(0.0f);
+        float zoom = 1.0f;
+        if (cc.contains("view")) view = mk(cc["view"][0].as_float(), cc["view"][1].as_float(), cc["view"][2].as_float());
+        if (cc.contains("at")) at = mk(cc["at"][0].as_float(), cc["at"][1].as_float(), cc["at"][2].as_float());
+        if (cc.contains("zoom")) zoom = cc["zoom"].as_float();
+        if (cc.contains("vo_scale")) c->params["vo_scale"] = cc["vo_scale"].as_num();
+        if (dot(view, view) != 0.0f) {   // Engine::init (engine.cu:148-152)
+            set_view_dir(c, view);
+            set_look_at(c, at);
+            set_scale(c, zoom);
+        }
+    }
+    if (cfg.contains("rendering")) {
+        const JValue& r = cfg["rendering"];
+        static const char* numeric[] = {"res_factor", "exposure", "smooth_threshold", "path_trace_depth", "light_samples", "nerf_shadow_samples",
+                                        "nerf_shadow_intensity", "syn_shadow_samples", "syn_shadow_intensity", "attenuation", "lens_size",
+                                        "nerf_on_nerf_shadow_threshold", "max_shadow_variance", "nerf_ao_intensity", "shadow_on_virtual_obj",
+                                        "shadow_on_nerf", "show_virtual_obj", "show_nerf", "depth_offset"};
+        for (const char* k : numeric)
+            if (r.contains(k)) c->params[k] = r[k].as_num();
+        if (r.contains("nerf_filter") && r["nerf_filter"].as_str() != "Shade")
+            throw SngError(SNG_ERR_INVALID, "nerf_filter '" + r["nerf_filter"].as_str() + "' is not on the accelerated path (Shade only)");
+        if (r.contains("syn_filter") && r["syn_filter"].as_str() != "Final")
+            throw SngError(SNG_ERR_INVALID, "syn_filter '" + r["syn_filter"].as_str() + "' is not on the accelerated path (Final only)");
+    }
+    std::vector<sng_material> mats;
+    for (size_t i = 0; i < cfg["materials"].size(); ++i) {   // Material(id, json) (material.cuh:26-48)
+        const JValue& m = cfg["materials"][i];
+        sng_material mm{};
+        mm.ks[0] = mm.ks[1] = mm.ks[2] = 1.0f;
+        const std::string& t = m["type"].as_str();
+        for (int k = 0; k < 3; ++k) mm.kd[k] = m["kd"][k].as_float();
+        if (m.contains("ka")) for (int k = 0; k < 3; ++k) mm.ka[k] = m["ka"][k].as_float();
+        if (m.contains("ks")) for (int k = 0; k < 3; ++k) mm.ks[k] = m["ks"][k].as_float();
+        mm.n = m["n"].as_float();
+        mm.rg = m.contains("rg") ? m["rg"].as_float() : 0.0f;
+        if (t == "lambertian") { mm.type = 0; mm.spec_angle = 0.0f; }
+        else if (t == "glossy") { mm.type = 1; mm.spec_angle = m.contains("spec_angle") ? m["spec_angle"].as_float() : 0.001f; }
+        else throw SngError(SNG_ERR_INVALID, "Material type " + t + " not supported");
+        mats.push_back(mm);
+    }
+    std::vector<HostObject> objs;
+    for (size_t i = 0; i < cfg["objfile"].size(); ++i) {   // VirtualObject(id, json) (virtual_object.cu:7-88)
+        const JValue& o = cfg["objfile"][i];
+        HostObject ho;
+        ho.file = o["file"].as_str();
+        std::string fp = ho.file;
+        if (!file_exists(fp)) fp = dir + "/" + ho.file;
+        ho.scale = o.contains("scale") ? o["scale"].as_float() : 1.0f;
+        uint32_t ppl = o.contains("primitives-per-leaf") ? (uint32_t)o["primitives-per-leaf"].as_num() : 4u;
+        ho.pos = o.contains("pos") ? mk(o["pos"][0].as_float(), o["pos"][1].as_float(), o["pos"][2].as_float()) : splat(0.0f);
+        ho.rot = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)};
+        if (o.contains("rot")) {
+            const JValue& a = o["rot"];
+            ho.rot = {mk(a[0].as_float(), a[1].as_float(), a[2].as_float()), mk(a[3].as_float(), a[4].as_float(), a[5].as_float()),
+                      mk(a[6].as_float(), a[7].as_float(), a[8].as_float())};
+        }
+        ho.mat = (int)o["material"].as_num();
+        ho.tris = load_obj(fp);
+        if (ho.tris.empty()) throw SngError(SNG_ERR_IO, "mesh has no triangles: " + fp);
+        ho.nodes = build_bvh(ho.tris, ppl);
+        objs.push_back(std::move(ho));
+    }
+    std::vector<sng_light> lights;
+    for (size_t i = 0; i < cfg["lights"].size(); ++i) {   // Light(id, json) (light.cuh:17-37)
+        const JValue& l = cfg["lights"][i];
+        sng_light ll{};
+        for (int k = 0; k < 3; ++k) ll.pos[k] = l["pos"][k].as_float();
+        ll.intensity = l["intensity"].as_float();
+        ll.size = l["size"].as_float();
+        ll.type = 0;
+        if (l.contains("type")) {
+            const std::string& t = l["type"].as_str();
+            if (t == "point") ll.type = 0;
+            else if (t == "directional") ll.type = 1;
+            else throw SngError(SNG_ERR_INVALID, t + " light not recognized");
+        }
+        lights.push_back(ll);
+    }
+    for (auto& o : objs)
+        if (o.mat < 0 || (size_t)o.mat >= mats.size()) throw SngError(SNG_ERR_INVALID, "object material index out of range");
+    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
+    c->objs = std::move(objs);
+    c->mats = mats;
+    c->lights = lights;
+    c->scene_dirty = true;
+    c->mesh_reset = true;
+}
+
+// ---- resize: Engine::resize (engine.cu:236-255) --------------------------------------
+void resize(sng_ctx* c) {
+    int res_factor = (int)c->p("res_factor");
+    float factor = std::min(1.0f, 8.0f / (float)res_factor);
+    auto clampi = [](int v, int lo, int hi) { return std::max(lo, std::min(hi, v)); };
+    int nw = clampi((int)((float)c->win[0] * factor), c->win[0] / 16, c->win[0]);
+    int nh = clampi((int)((float)c->win[1] * factor), c->win[1] / 16, c->win[1]);
+    float vs = (float)(int)c->p("vo_scale");
+    int rw = std::min(clampi((int)((float)nw * vs), nw / 16, nw * 16), c->win[0]);
+    int rh = std::min(clampi((int)((float)nh * vs), nh / 16, nh * 16), c->win[1]);
+    c->nerf_res[0] = nw; c->nerf_res[1] = nh;
+    c->mesh_res[0] = rw; c->mesh_res[1] = rh;
+    c->vo_scale_eff = std::max(1, rw / nw);
+    c->params["vo_scale"] = c->vo_scale_eff;   // m_relative_vo_scale = rt_res.r / new_res.r
+    c->last_res_factor = res_factor;
+    size_t nn = (size_t)nw * nh, nm = (size_t)rw * rh;
+    c->nerf_rgba.ensure(nn * 16);
+    c->nerf_depth.ensure(nn * 4);
+    c->nerf_pos.ensure(nn * 12);
+    c->nerf_nrm.ensure(nn * 12);
+    HIPCHK(hipMemset(c->nerf_rgba.p, 0, nn * 16));
+    for (int b = 0; b < 2; ++b) {
+        c->ray_ot[b].ensure(nn * 16);
+        c->ray_di[b].ensure(nn * 16);
+        c->ray_rgba[b].ensure(nn * 16);
+        c->ray_depth[b].ensure(nn * 4);
+    }
+    c->samp.ensure(nn * 8);
+    c->ray_cap = nn;
+    c->ctrl.ensure(sizeof(MarchCtrl));
+    c->mesh_o.ensure(nm * 16);
+    c->mesh_d.ensure(nm * 16);
+    c->acc_rgba.ensure(nm * 16);
+    c->acc_depth.ensure(nm * 4);
+    c->final_rgba.ensure(nm * 16);
+    c->final_depth.ensure(nm * 4);
+    // init_rand_state for NeRF px (engine.cu:246-247) and raytracer px (raytracer.cu:279)
+    const auto& tab = xorwow_seq_tables();
+    upload(c->d_seq, tab.data(), tab.size() * 4);
+    c->rng_nerf.ensure(nn * 24);
+    c->rng_mesh.ensure(nm * 24);
+    c->n_rng_nerf = (uint32_t)nn;
+    c->n_rng_mesh = (uint32_t)nm;
+    launch_xorwow_init((uint32_t)nn, PT_SEED, c->d_seq.as<uint32_t>(), c->rng_nerf.as<uint32_t>(), c->s_nerf);
+    launch_xorwow_init((uint32_t)nm, PT_SEED, c->d_seq.as<uint32_t>(), c->rng_mesh.as<uint32_t>(), c->s_nerf);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->s_nerf));
+    c->mesh_reset = true;
+}
+
+void ensure_samples(sng_ctx* c, uint32_t target) {
+    size_t cap = std::max<size_t>(target, c->ray_cap) + 64;
+    if (cap > c->sample_cap) {
+        c->coords.ensure(cap * 7 * 4);
+        c->net_out.ensure(cap * 8);
+        c->sample_cap = cap;
+    }
+}
+
+CamDev cam_dev(const sng_ctx* c) { return {cam_col(c, 0), cam_col(c, 1), cam_col(c, 2), cam_col(c, 3)}; }
+f2 focal_for(const sng_ctx* c, const int res[2]) {
+    float r = (float)res[c->fov_axis];
+    return {c->rel_focal[0] * r * c->zoom, c->rel_focal[1] * r * c->zoom};
+}
+f2 render_screen_center(const sng_ctx* c) {
+    return {(0.5f - c->screen_center[0]) * c->zoom + 0.5f, (0.5f - c->screen_center[1]) * c->zoom + 0.5f};
+}
+
+void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out) {
+    if (c->win[0] <= 0) throw SngError(SNG_ERR_STATE, "sng_set_window first");
+    if ((int)c->p("res_factor") != c->last_res_factor) resize(c);
+    const bool show_nerf = c->p("show_nerf") != 0.0;
+    if (show_nerf && !(c->has_model && c->has_bitfield)) throw SngError(SNG_ERR_STATE, "no NeRF model/density grid loaded");
+    if (c->scene_dirty) upload_scene(c);
+    sng_frame_params P{};
+    if (fp) P = *fp;
+    const uint32_t target = P.target_n_queries ? P.target_n_queries : 2u * 1024u * 1024u;
+    ensure_samples(c, target);
+    const int MW = c->mesh_res[0], MH = c->mesh_res[1], NW = c->nerf_res[0], NH = c->nerf_res[1], S = c->vo_scale_eff;
+    int y0 = P.row_begin, y1 = P.row_end;
+    if (y0 == 0 && y1 == 0) { y0 = 0; y1 = MH; }
+    if (y0 < 0 || y1 > MH || y0 >= y1) throw SngError(SNG_ERR_INVALID, "bad row band");
+    const int radius = (int)c->p("nerf_shadow_samples") / 2;
+    const bool shadows = c->p("shadow_on_nerf") != 0.0 && show_nerf;
+    // NeRF rows: overlay needs [ny0, ny1); shadows need normals +-r; normals need positions +-2
+    const int ny0 = std::min(NH, y0 / S), ny1 = std::min(NH, (y1 - 1) / S + 1);
+    const int halo_n = shadows ? radius : 0;
+    const int nr0 = std::max(0, ny0 - halo_n), nr1 = std::min(NH, ny1 + halo_n);
+    const int tr0 = std::max(0, nr0 - 2), tr1 = std::min(NH, nr1 + 2);
+    Volume vol = show_nerf ? make_volume(c) : Volume{};
+    if (!show_nerf) vol.bitfield = c->d_bitfield.as<uint8_t>();
+    if (!c->has_bitfield) { vol = Volume{}; vol.render_aabb = c->box; vol.train_aabb = c->box; vol.to_local_identity = 1; }
+    const CamDev cam = cam_dev(c);
+    const f2 sc = render_screen_center(c);
+
+    HIPCHK(hipEventRecord(c->ev_start, c->s_nerf));
+    HIPCHK(hipStreamWaitEvent(c->s_rt, c->ev_start, 0));
+    // ---- raytracer (RayTracer::render, raytracer.cu:312-370) on its own stream
+    HIPCHK(hipEventRecord(c->ev_rt0, c->s_rt));
+    if (c->mesh_reset || P.reset_accumulation) {
+        const int mres[2] = {MW, MH};
+        launch_mesh_rays(MW, MH, y0, y1, cam, focal_for(c, mres), sc, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->acc_rgba.as<float4>(),
+                         c->acc_depth.as<float>(), c->s_rt);
+        c->mesh_reset = false;
+    }
+    if (c->p("show_virtual_obj") != 0.0 && !c->objs.empty()) {
+        RaytraceArgs ra{};
+        ra.vol = vol;
+        ra.W = MW; ra.row0 = y0; ra.row1 = y1;
+        ra.up = cam.c0;
+        ra.objs = c->d_objs.as<ObjectGpu>(); ra.n_objs = (int)c->objs.size();
+        ra.lights = c->d_lights.as<LightGpu>(); ra.n_lights = (int)c->lights.size();
+        ra.mats = c->d_mats.as<MaterialGpu>();
+        ra.samples = (uint32_t)c->p("light_samples");
+        ra.bounces = (uint32_t)c->p("path_trace_depth");
+        ra.shadow_iters = (uint32_t)c->p("syn_shadow_samples");
+        ra.shadow_steps = (uint32_t)c->p("n_steps");
+        ra.lens = (float)c->p("lens_size");
+        ra.show_nerf_shadow = c->p("shadow_on_virtual_obj") != 0.0;
+        ra.syn_shadow_factor = (float)c->p("syn_shadow_intensity");
+        launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
+                        c->acc_depth.as<float>(), c->s_rt);
+    }
+    HIPCHK(hipEventRecord(c->ev_rt1, c->s_rt));
+
+    // ---- NeRF (Testbed::render SyNeRFgine overload, testbed.cu:4353-4404)
+    HIPCHK(hipEventRecord(c->ev_nerf0, c->s_nerf));
+    uint32_t net_launches = 0;
+    if (show_nerf) {
+        MarchCtrl* ctrl = c->ctrl.as<MarchCtrl>();
+        launch_ctrl_init(ctrl, c->s_nerf);
+        NerfFrameArgs a{};
+        a.vol = vol;
+        a.cam = cam;
+        m3 rot = {cam.c0, cam.c1, cam.c2};
+        a.ray_rot = rolling_shutter_rotation(rot);
+        const int nres[2] = {NW, NH};
+        a.focal = focal_for(c, nres);
+        a.screen_center = sc;
+        a.W = NW; a.H = NH; a.row0 = tr0; a.row1 = tr1;
+        a.spp = P.spp;
+        a.snap = 0;
+        a.reset = P.reset_accumulation ? 1 : 0;
+        a.target_n_queries = target;
+        RayBuf rb[2];
+        for (int b = 0; b < 2; ++b) rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>()};
+        launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
+        const uint32_t n_band = (uint32_t)(tr1 - tr0) * (uint32_t)NW;
+        const uint32_t blocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
+        const uint32_t max_tiles = (uint32_t)((c->sample_cap + 15) / 16);
+        const int CHUNK = 4;
+        int p = 0;
+        uint32_t iter = 0;
+        int chunk = 0;
+        bool done = false;
+        while (!done && iter < MARCH_ITER) {
+            for (int k = 0; k < CHUNK; ++k, ++iter) {
+                launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, c->s_nerf);
+                if (P.collect_kernel_times) {
+                    while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
+                    HIPCHK(hipEventRecord(c->net_events[2 * net_launches], c->s_nerf));
+                }
+                launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf);
+                if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->net_events[2 * net_launches + 1], c->s_nerf));
+                ++net_launches;
+                launch_composite(vol, cam, rb[p], rb[p ^ 1], ctrl, p, target, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
+                                 c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf);
+                p ^= 1;
+            }
+            // readback of the alive count after this chunk; check the previous chunk's (already landed)
+            HIPCHK(hipMemcpyAsync(&c->h_alive[2 * (chunk & 1)], &ctrl->n_alive[0], 8, hipMemcpyDeviceToHost, c->s_nerf));
+            HIPCHK(hipGetLastError());
+            if (chunk > 0) {
+                // wait for the previous chunk's readback (the current chunk stays queued behind it)
+                HIPCHK(hipEventSynchronize(c->ev_nerf1));
+                const uint32_t* h = &c->h_alive[2 * ((chunk - 1) & 1)];
+                if (h[0] == 0 && h[1] == 0) done = true;
+            }
+            HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
+            ++chunk;
+        }
+        launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
+    }
+    HIPCHK(hipEventRecord(c->ev_shadow1, c->s_nerf));   // end of the trace
+    if (shadows && !c->objs.empty()) {
+        ShadowArgs sa{};
+        sa.vol = vol;
+        sa.W = NW; sa.H = NH; sa.row0 = ny0; sa.row1 = ny1;
+        sa.radius = radius;
+        sa.intensity = (float)c->p("nerf_shadow_intensity");
+        sa.threshold = (float)c->p("nerf_on_nerf_shadow_threshold");
+        sa.objs = c->d_objs.as<ObjectGpu>(); sa.n_objs = (int)c->objs.size();
+        sa.lights = c->d_lights.as<LightGpu>(); sa.n_lights = (int)c->lights.size();
+        launch_shadows(sa, c->nerf_rgba.as<float4>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->rng_nerf.as<uint32_t>(), c->n_rng_nerf,
+                       c->s_nerf);
+    } else if (shadows) {
+        ShadowArgs sa{};
+        sa.vol = vol;
+        sa.W = NW; sa.H = NH; sa.row0 = ny0; sa.row1 = ny1;
+        sa.radius = radius;
+        sa.intensity = (float)c->p("nerf_shadow_intensity");
+        sa.threshold = (float)c->p("nerf_on_nerf_shadow_threshold");
+        sa.objs = c->d_objs.as<ObjectGpu>(); sa.n_objs = 0;
+        sa.lights = c->d_lights.as<LightGpu>(); sa.n_lights = (int)c->lights.size();
+        launch_shadows(sa, c->nerf_rgba.as<float4>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->rng_nerf.as<uint32_t>(), c->n_rng_nerf,
+                       c->s_nerf);
+    }
+    HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
+    // ---- overlay (RayTracer::overlay, raytracer.cu:372-392) after both streams
+    HIPCHK(hipStreamWaitEvent(c->s_nerf, c->ev_rt1, 0));
+    launch_overlay(MW, y0, y1, S, MW / S, NW * NH, show_nerf ? 1 : 0, (float)c->p("depth_offset"), std::pow(2.0f, (float)c->p("exposure")), (int)c->p("srgb"),
+                   c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->final_rgba.as<float4>(),
+                   c->final_depth.as<float>(), c->s_nerf);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_end, c->s_nerf));
+    if (show_nerf) HIPCHK(hipMemcpyAsync(c->h_ctrl, c->ctrl.p, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
+    HIPCHK(hipStreamSynchronize(c->s_nerf));
+
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        out->d_final_rgba = c->final_rgba.as<float>();
+        out->d_final_depth = c->final_depth.as<float>();
+        out->d_nerf_rgba = c->nerf_rgba.as<float>();
+        out->d_nerf_depth = c->nerf_depth.as<float>();
+        out->d_nerf_positions = c->nerf_pos.as<float>();
+        out->d_nerf_normals = c->nerf_nrm.as<float>();
+        out->d_syn_rgba = c->acc_rgba.as<float>();
+        out->d_syn_depth = c->acc_depth.as<float>();
+        if (show_nerf) {
+            out->n_iterations = c->h_ctrl->n_iter;
+            out->n_hit = c->h_ctrl->n_hit;
+            out->n_samples = c->h_ctrl->total_samples;
+            out->n_reference_slots = c->h_ctrl->ref_slots;
+            std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
+            std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
+        }
+        HIPCHK(hipEventElapsedTime(&out->ms_frame, c->ev_start, c->ev_end));
+        HIPCHK(hipEventElapsedTime(&out->ms_raytrace, c->ev_rt0, c->ev_rt1));
+        HIPCHK(hipEventElapsedTime(&out->ms_nerf, c->ev_nerf0, c->ev_shadow1));
+        HIPCHK(hipEventElapsedTime(&out->ms_shadow, c->ev_shadow1, c->ev_nerf1));
+        float ov = 0.0f;
+        HIPCHK(hipEventElapsedTime(&ov, c->ev_nerf1, c->ev_end));
+        out->ms_overlay = ov;
+        if (P.collect_kernel_times) {
+            float tot = 0.0f;
+            for (uint32_t k = 0; k < net_launches; ++k) {
+                float ms = 0.0f;
+                HIPCHK(hipEventElapsedTime(&ms, c->net_events[2 * k], c->net_events[2 * k + 1]));
+                tot += ms;
+            }
+            out->ms_network = tot;
+        }
+        out->network_launches = net_launches;
+    }
+}
+
+void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw SngError(SNG_ERR_NOGPU, "no HIP device visible");
+    int dev = desc ? desc->device_id : 0;
+    if (dev < 0 || dev >= n) throw SngError(SNG_ERR_INVALID, "device_id out of range");
+    HIPCHK(hipSetDevice(dev));
+    auto* c = new sng_ctx();
+    c->device = dev;
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev));
+    c->n_cus = prop.multiProcessorCount;
+    HIPCHK(hipStreamCreateWithFlags(&c->s_nerf, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->s_rt, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end}) HIPCHK(hipEventCreate(e));
+    HIPCHK(hipHostMalloc((void**)&c->h_ctrl, sizeof(MarchCtrl), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c->h_alive, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    float rf = fov_to_focal(50.625f);   // Testbed::reset_camera -> set_fov(50.625) (testbed.cu:480)
+    c->rel_focal[0] = c->rel_focal[1] = rf;
+    // reset_camera matrix: transpose(mat3x4{1,0,0,0.5; 0,-1,0,0.5; 0,0,-1,0.5}), then pos -= scale*dir
+    c->m_scale = 1.5f;
+    set_cam_col(c, 3, cam_col(c, 3) - cam_col(c, 2) * 0.0f);
+    c->cam[9] = 0.5f; c->cam[10] = 0.5f; c->cam[11] = 0.5f;
+    set_cam_col(c, 3, cam_col(c, 3) - c->m_scale * cam_col(c, 2));
+    *out = c;
+}
+
+void ctx_destroy(sng_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
+    for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
+                      &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats})
+        b->release();
+    for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); }
+    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end}) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
+    (void)hipHostFree(c->h_ctrl);
+    (void)hipHostFree(c->h_alive);
+    (void)hipStreamDestroy(c->s_nerf);
+    (void)hipStreamDestroy(c->s_rt);
+    delete c;
+}
+
+// ---- .ingp snapshot (Testbed::load_snapshot, testbed.cu:4878-5015; zlib(msgpack), 244-270) ----
+std::vector<uint8_t> inflate_all(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw SngError(SNG_ERR_IO, "Network snapshot '" + path + "' does not exist.");
+    std::vector<uint8_t> in((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    bool compressed = path.size() >= 5 && path.substr(path.size() - 5) == ".ingp";
+    if (!compressed) return in;
+    z_stream zs{};
+    if (inflateInit2(&zs, 15 + 32) != Z_OK) throw SngError(SNG_ERR_IO, "zlib init failed");
+    std::vector<uint8_t> out;
+    std::vector<uint8_t> buf(1 << 20);
+    zs.next_in = in.data();
+    zs.avail_in = (uInt)in.size();
+    int r;
+    do {
+        zs.next_out = buf.data();
+        zs.avail_out = (uInt)buf.size();
+        r = inflate(&zs, Z_NO_FLUSH);
+        if (r != Z_OK && r != Z_STREAM_END) { inflateEnd(&zs); throw SngError(SNG_ERR_IO, "zlib inflate failed"); }
+        out.insert(out.end(), buf.data(), buf.data() + (buf.size() - zs.avail_out));
+    } while (r != Z_STREAM_END);
+    inflateEnd(&zs);
+    return out;
+}
+float jnum(const JValue& v, float dflt) { return v.type == JValue::Null ? dflt : v.as_float(); }
+// tcnn vec/mat JSON: arrays; mat4x3 as 4 columns of 3 or 3 rows of 4 [tcnn vec_json.h, unvendored]
+void read_mat43(const JValue& m, float out[12]) {
+    if (m.size() == 4 && m[0].size() == 3) {
+        for (int i = 0; i < 4; ++i) for (int j = 0; j < 3; ++j) out[3 * i + j] = m[i][j].as_float();
+    } else if (m.size() == 3 && m[0].size() == 4) {
+        for (int i = 0; i < 4; ++i) for (int j = 0; j < 3; ++j) out[3 * i + j] = m[j][i].as_float();
+    } else throw SngError(SNG_ERR_IO, "unexpected camera matrix encoding");
+}
+void load_snapshot(sng_ctx* c, const std::string& path) {
+    std::vector<uint8_t> raw = inflate_all(path);
+    JValue root = MsgpackParser(raw.data(), raw.size()).parse();
+    if (!root.contains("snapshot")) throw SngError(SNG_ERR_IO, "not a snapshot");
+    const JValue& snap = root["snapshot"];
+    if (!snap.contains("version") || snap["version"].as_num() < 1) throw SngError(SNG_ERR_IO, "Snapshot uses an old format and can not be loaded.");
+    const JValue& enc = root["encoding"];
+    sng_nerf_config cfg{};
+    cfg.n_levels = (uint32_t)enc["n_levels"].as_num();
+    cfg.n_features_per_level = enc.contains("n_features_per_level") ? (uint32_t)enc["n_features_per_level"].as_num() : 2u;
+    cfg.log2_hashmap_size = enc.contains("log2_hashmap_size") ? (uint32_t)enc["log2_hashmap_size"].as_num() : 15u;
+    cfg.base_resolution = (uint32_t)enc["base_resolution"].as_num();
+    cfg.per_level_scale = enc["per_level_scale"].as_float();
+    cfg.aabb_scale = (uint32_t)snap["nerf"]["aabb_scale"].as_num();
+    const JValue& pb = snap["params_binary"];
+    std::string ptype = snap.contains("params_type") ? snap["params_type"].as_str() : std::string("__half");
+    std::vector<uint16_t> params;
+    if (ptype == "__half") {
+        params.resize(pb.str.size() / 2);
+        std::memcpy(params.data(), pb.str.data(), params.size() * 2);
+    } else if (ptype == "float") {
+        std::vector<float> fp(pb.str.size() / 4);
+        std::memcpy(fp.data(), pb.str.data(), fp.size() * 4);
+        for (float v : fp) params.push_back(f2h_host(v));
+    } else throw SngError(SNG_ERR_IO, "unsupported params_type " + ptype);
+    set_model(c, &cfg, params.data(), params.size());
+    const JValue& dg = snap["density_grid_binary"];
+    std::vector<uint16_t> grid(dg.str.size() / 2);
+    std::memcpy(grid.data(), dg.str.data(), grid.size() * 2);
+    if (!grid.empty()) set_density_grid(c, grid.data(), grid.size());
+    if (snap.contains("up_dir")) c->up = mk(snap["up_dir"][0].as_float(), snap["up_dir"][1].as_float(), snap["up_dir"][2].as_float());
+    if (snap.contains("camera")) {
+        const JValue& cam = snap["camera"];
+        if (cam.contains("matrix")) read_mat43(cam["matrix"], c->cam);
+        if (cam.contains("fov_axis")) c->fov_axis = (int)cam["fov_axis"].as_num();
+        if (cam.contains("relative_focal_length")) {
+            const JValue& r = cam["relative_focal_length"];
+            if (r.type == JValue::Array) { c->rel_focal[0] = r[0].as_float(); c->rel_focal[1] = r[1].as_float(); }
+            else c->rel_focal[0] = c->rel_focal[1] = r.as_float();
+        }
+        if (cam.contains("screen_center")) { c->screen_center[0] = cam["screen_center"][0].as_float(); c->screen_center[1] = cam["screen_center"][1].as_float(); }
+        if (cam.contains("zoom")) c->zoom = cam["zoom"].as_float();
+        if (cam.contains("scale")) c->m_scale = cam["scale"].as_float();
+    }
+    if (snap.contains("exposure")) c->params["exposure"] = snap["exposure"].as_num();
+}
+
+}  // namespace
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+extern "C" {
+
+const char* sng_last_error(void) { return g_err.c_str(); }
+int sng_abi_version(void) { return SNG_ABI_VERSION; }
+int sng_device_count(int* out) {
+    return guarded([&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        *out = n;
+    });
+}
+int sng_ctx_create(const sng_ctx_desc* desc, sng_ctx** out) { return guarded([&] { ctx_create(desc, out); }); }
+int sng_ctx_destroy(sng_ctx* ctx) { return guarded([&] { ctx_destroy(ctx); }); }
+
+int sng_load_snapshot(sng_ctx* c, const char* path) { return guarded([&] { HIPCHK(hipSetDevice(c->device)); load_snapshot(c, path); }); }
+uint64_t sng_nerf_param_count(const sng_nerf_config* cfg) {
+    sng_ctx tmp;
+    tmp.cfg = *cfg;
+    compute_levels(&tmp);
+    return tmp.n_params;
+}
+int sng_set_nerf_model(sng_ctx* c, const sng_nerf_config* cfg, const uint16_t* params, uint64_t n) {
+    return guarded([&] { HIPCHK(hipSetDevice(c->device)); set_model(c, cfg, params, n); });
+}
+int sng_set_density_grid(sng_ctx* c, const uint16_t* grid, uint64_t n) {
+    return guarded([&] { HIPCHK(hipSetDevice(c->device)); set_density_grid(c, grid, n); });
+}
+int sng_get_bitfield(sng_ctx* c, uint8_t* out, uint64_t n) {
+    return guarded([&] {
+        if (!c->has_bitfield) throw SngError(SNG_ERR_STATE, "no bitfield");
+        if (n != c->d_bitfield.bytes) throw SngError(SNG_ERR_INVALID, "bitfield size is " + std::to_string(c->d_bitfield.bytes));
+        HIPCHK(hipMemcpy(out, c->d_bitfield.p, n, hipMemcpyDeviceToHost));
+    });
+}
+int sng_get_density_mean(sng_ctx* c, float* out) {
+    return guarded([&] {
+        if (!c->has_bitfield) throw SngError(SNG_ERR_STATE, "no bitfield");
+        HIPCHK(hipMemcpy(out, c->d_mean.p, 4, hipMemcpyDeviceToHost));
+    });
+}
+int sng_nerf_inference(sng_ctx* c, const float* coords, uint32_t stride, uint32_t n, uint16_t* out, int32_t layout, void* stream) {
+    return guarded([&] {
+        if (!c->has_model) throw SngError(SNG_ERR_STATE, "no model");
+        if (stride < 7) throw SngError(SNG_ERR_INVALID, "NerfCoordinate stride must be >= 7 floats");
+        if (layout != 0 && layout != 1) throw SngError(SNG_ERR_INVALID, "out_layout must be 0 or 1");
+        if (n == 0) return;
+        launch_network(c->net, coords, stride, n, nullptr, out, layout, 0, (hipStream_t)stream);
+        HIPCHK(hipGetLastError());
+    });
+}
+int sng_hashgrid_encode(sng_ctx* c, const float* coords, uint32_t stride, uint32_t n, uint16_t* out, void* stream) {
+    return guarded([&] {
+        if (!c->has_model) throw SngError(SNG_ERR_STATE, "no model");
+        if (stride < 3) throw SngError(SNG_ERR_INVALID, "stride must be >= 3 floats");
+        launch_encode(c->net, coords, stride, n, out, (hipStream_t)stream);
+        HIPCHK(hipGetLastError());
+    });
+}
+
+int sng_load_virtual_scene(sng_ctx* c, const char* path) { return guarded([&] { load_scene(c, path); }); }
+int sng_clear_virtual_scene(sng_ctx* c) {
+    return guarded([&] {
+        for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
+        c->objs.clear(); c->lights.clear(); c->mats.clear();
+        c->scene_dirty = true;
+    });
+}
+int sng_set_param(sng_ctx* c, const char* key, double v) {
+    return guarded([&] {
+        std::string k = key;
+        if (k == "sshadows") k = "syn_shadow_samples";       // Engine::set_syn_samples (engine.cuh:29)
+        else if (k == "nshadows") k = "nerf_shadow_samples"; // Engine::set_nerf_samples (engine.cuh:30-33)
+        if (!default_params().count(k)) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
+        c->params[k] = v;
+        c->mesh_reset = true;
+    });
+}
+int sng_get_param(sng_ctx* c, const char* key, double* v) {
+    return guarded([&] {
+        std::string k = key;
+        if (k == "sshadows") k = "syn_shadow_samples";
+        else if (k == "nshadows") k = "nerf_shadow_samples";
+        auto it = c->params.find(k);
+        if (it == c->params.end()) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
+        *v = it->second;
+    });
+}
+int sng_get_scene_counts(sng_ctx* c, uint32_t* no, uint32_t* nl, uint32_t* nm) {
+    return guarded([&] {
+        *no = (uint32_t)c->objs.size();
+        *nl = (uint32_t)c->lights.size();
+        *nm = (uint32_t)c->mats.size();
+    });
+}
+int sng_get_object(sng_ctx* c, uint32_t i, sng_object_info* out) {
+    return guarded([&] {
+        if (i >= c->objs.size()) throw SngError(SNG_ERR_INVALID, "object index");
+        const auto& o = c->objs[i];
+        out->n_nodes = (uint32_t)o.nodes.size();
+        out->n_tris = (uint32_t)o.tris.size();
+        const f3 cols[3] = {o.rot.c0, o.rot.c1, o.rot.c2};
+        for (int k = 0; k < 3; ++k) { out->rot[3 * k] = cols[k].x; out->rot[3 * k + 1] = cols[k].y; out->rot[3 * k + 2] = cols[k].z; }
+        out->pos[0] = o.pos.x; out->pos[1] = o.pos.y; out->pos[2] = o.pos.z;
+        out->scale = o.scale;
+        out->mat_id = o.mat;
+    });
+}
+int sng_get_object_bvh(sng_ctx* c, uint32_t i, float* nodes_out, float* tris_out) {
+    return guarded([&] {
+        if (i >= c->objs.size()) throw SngError(SNG_ERR_INVALID, "object index");
+        const auto& o = c->objs[i];
+        if (nodes_out) std::memcpy(nodes_out, o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
+        if (tris_out) std::memcpy(tris_out, o.tris.data(), o.tris.size() * sizeof(Tri));
+    });
+}
+int sng_get_light(sng_ctx* c, uint32_t i, sng_light* out) {
+    return guarded([&] { if (i >= c->lights.size()) throw SngError(SNG_ERR_INVALID, "light index"); *out = c->lights[i]; });
+}
+int sng_get_material(sng_ctx* c, uint32_t i, sng_material* out) {
+    return guarded([&] { if (i >= c->mats.size()) throw SngError(SNG_ERR_INVALID, "material index"); *out = c->mats[i]; });
+}
+
+int sng_set_camera_view(sng_ctx* c, const float v[3], const float at[3], float scale) {
+    return guarded([&] {
+        set_view_dir(c, mk(v[0], v[1], v[2]));
+        set_look_at(c, mk(at[0], at[1], at[2]));
+        set_scale(c, scale);
+        c->mesh_reset = true;
+    });
+}
+int sng_set_camera_matrix(sng_ctx* c, const float m[12]) { return guarded([&] { std::memcpy(c->cam, m, 48); c->mesh_reset = true; }); }
+int sng_get_camera_matrix(sng_ctx* c, float m[12]) { return guarded([&] { std::memcpy(m, c->cam, 48); }); }
+int sng_set_fov(sng_ctx* c, float deg) { return guarded([&] { c->rel_focal[0] = c->rel_focal[1] = fov_to_focal(deg); c->mesh_reset = true; }); }
+int sng_get_focal_length(sng_ctx* c, int which, float out[2]) {
+    return guarded([&] {
+        const int* res = which == 0 ? c->nerf_res : c->mesh_res;
+        f2 f = focal_for(c, res);
+        out[0] = f.x; out[1] = f.y;
+    });
+}
+
+int sng_set_window(sng_ctx* c, int32_t w, int32_t h) {
+    return guarded([&] {
+        if (w <= 0 || h <= 0) throw SngError(SNG_ERR_INVALID, "bad window size");
+        HIPCHK(hipSetDevice(c->device));
+        c->win[0] = w; c->win[1] = h;
+        resize(c);
+    });
+}
+int sng_get_resolution(sng_ctx* c, sng_resolution_info* out) {
+    return guarded([&] {
+        std::memset(out, 0, sizeof(*out));
+        out->nerf_res[0] = c->nerf_res[0]; out->nerf_res[1] = c->nerf_res[1];
+        out->mesh_res[0] = c->mesh_res[0]; out->mesh_res[1] = c->mesh_res[1];
+        out->syn_px_scale = c->vo_scale_eff;
+    });
+}
+int sng_render_frame(sng_ctx* c, const sng_frame_params* p, sng_frame_result* out) {
+    return guarded([&] { HIPCHK(hipSetDevice(c->device)); render_frame(c, p, out); });
+}
+int sng_synchronize(sng_ctx* c) { return guarded([&] { HIPCHK(hipStreamSynchronize(c->s_nerf)); HIPCHK(hipStreamSynchronize(c->s_rt)); }); }
+int sng_copy_to_host(sng_ctx* c, const void* src, void* dst, uint64_t n) {
+    return guarded([&] { HIPCHK(hipSetDevice(c->device)); HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost)); });
+}
+int sng_copy_device(sng_ctx* c, const void* src, void* dst, uint64_t n, void* stream) {
+    return guarded([&] {
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    });
+}
+int sng_get_rng_states(sng_ctx* c, int which, uint32_t* out, uint64_t n) {
+    return guarded([&] {
+        DevBuf& b = which == 0 ? c->rng_nerf : c->rng_mesh;
+        uint32_t cnt = which == 0 ? c->n_rng_nerf : c->n_rng_mesh;
+        if (n != cnt) throw SngError(SNG_ERR_INVALID, "state count is " + std::to_string(cnt));
+        std::vector<uint32_t> soa((size_t)n * 6);
+        HIPCHK(hipMemcpy(soa.data(), b.p, soa.size() * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; ++i)
+            for (int k = 0; k < 6; ++k) out[6 * i + k] = soa[(size_t)k * n + i];
+    });
+}
+int sng_set_rng_states(sng_ctx* c, int which, const uint32_t* in, uint64_t n) {
+    return guarded([&] {
+        DevBuf& b = which == 0 ? c->rng_nerf : c->rng_mesh;
+        uint32_t cnt = which == 0 ? c->n_rng_nerf : c->n_rng_mesh;
+        if (n != cnt) throw SngError(SNG_ERR_INVALID, "state count is " + std::to_string(cnt));
+        std::vector<uint32_t> soa((size_t)n * 6);
+        for (size_t i = 0; i < n; ++i)
+            for (int k = 0; k < 6; ++k) soa[(size_t)k * n + i] = in[6 * i + k];
+        HIPCHK(hipMemcpy(b.p, soa.data(), soa.size() * 4, hipMemcpyHostToDevice));
+    });
+}
+int sng_bvh_build(float* tris, uint32_t n, uint32_t ppl, float* nodes_out, uint32_t cap, uint32_t* n_nodes) {
+    return guarded([&] {
+        if (n == 0) throw SngError(SNG_ERR_INVALID, "no triangles");
+        std::vector<Tri> t((Tri*)tris, (Tri*)tris + n);
+        auto nodes = build_bvh(t, ppl);
+        if (nodes.size() > cap) throw SngError(SNG_ERR_INVALID, "node capacity too small: need " + std::to_string(nodes.size()));
+        std::memcpy(nodes_out, nodes.data(), nodes.size() * sizeof(BvhNode));
+        std::memcpy(tris, t.data(), n * sizeof(Tri));
+        *n_nodes = (uint32_t)nodes.size();
+    });
+}
+
+}  // extern "C"

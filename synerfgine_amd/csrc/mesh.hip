@@ -1,0 +1,396 @@
+// mesh.hip -- virtual objects: BVH traversal, path tracer, NeRF shadow pass, overlay, RNG.
+//
+// Replaces ray_intersect_nodes (triangle_bvh.cu:263-319), sng::depth_test_world /
+// depth_test_nerf (synerfgine/common.cu:36-102), shade_with_shadow + shadow_for_px
+// (testbed_nerf.cu:1614-1786), sng::init_rays_with_payload_kernel_nerf, shade_object,
+// raytrace and overlay_nerf (synerfgine/raytracer.cu:6-258), and init_rand_state
+// (synerfgine/common.cu:22-26, cuRAND XORWOW seeding restated).
+//
+// BVH traversal keeps its 32-entry stack in LDS, interleaved by thread
+// ([depth][thread]) so a wave's pushes/pops at equal depth hit 64 distinct
+// banks.  Each pixel keeps its own XORWOW stream in SoA registers for the whole
+// kernel (one coalesced load/store of 24 B per pixel per frame).
+#include "sng_internal.h"
+#include "sng_math.h"
+
+namespace sng {
+
+constexpr int BVH_STACK = 32;
+constexpr int TPB = 128;   // threads per block for the traversal kernels
+
+struct Stack {
+    int* base;   // LDS
+    int n;
+    __device__ __forceinline__ void push(int v) { base[n * TPB] = v; ++n; }
+    __device__ __forceinline__ int pop() { --n; return base[n * TPB]; }
+};
+
+__device__ __forceinline__ float tri_intersect(const Tri& tr, f3 ro, f3 rd) {   // triangle.cuh:45-59
+    const f3 v1v0 = tr.b - tr.a, v2v0 = tr.c - tr.a, rov0 = ro - tr.a;
+    const f3 n = cross(v1v0, v2v0);
+    const f3 q = cross(rov0, rd);
+    const float d = 1.0f / dot(rd, n);
+    const float u = d * -dot(q, v2v0);
+    const float v = d * dot(q, v1v0);
+    float t = d * -dot(n, rov0);
+    if (u < 0.0f || u > 1.0f || v < 0.0f || (u + v) > 1.0f || t < 0.0f) t = 3.402823466e+38f;
+    return t;
+}
+
+// ray_intersect_nodes_f<2> (triangle_bvh.cu:263-307); returns t, writes triangle index
+__device__ float bvh_intersect(f3 ro, f3 rd, const BvhNode* __restrict__ nodes, const Tri* __restrict__ tris, int* stack_lds, int& tri_out) {
+    Stack st{stack_lds, 0};
+    st.push(0);
+    float mint = MAX_DEPTH;
+    int shortest = -1;
+    while (st.n > 0) {
+        const int idx = st.pop();
+        const BvhNode node = nodes[idx];
+        if (node.left < 0) {
+            const int end = -node.right - 1;
+            for (int i = -node.left - 1; i < end; ++i) {
+                const float t = tri_intersect(tris[i], ro, rd);
+                if (t < mint) { mint = t; shortest = i; }
+            }
+        } else {
+            const int c0 = node.left, c1 = node.left + 1;
+            const BvhNode n0 = nodes[c0], n1 = nodes[c1];
+            float d0 = aabb_entry({mk(n0.lo[0], n0.lo[1], n0.lo[2]), mk(n0.hi[0], n0.hi[1], n0.hi[2])}, ro, rd);
+            float d1 = aabb_entry({mk(n1.lo[0], n1.lo[1], n1.lo[2]), mk(n1.hi[0], n1.hi[1], n1.hi[2])}, ro, rd);
+            // sorting_network<2>: descending, so the nearer child is pushed last
+            int i0 = c0, i1 = c1;
+            if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = c1; i1 = c0; }
+            if (d0 < mint) { if (st.n >= BVH_STACK - 1) { /* FixedStack overflow: reference warns */ } else st.push(i0); }
+            if (d1 < mint) { if (st.n >= BVH_STACK - 1) { } else st.push(i1); }
+        }
+    }
+    tri_out = shortest;
+    return mint;
+}
+
+__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, int* stack, int& tri) {
+    const f3 oro = mul(o.world_to_obj, ro - o.pos);
+    const f3 ord = mul(o.world_to_obj, rd);
+    return bvh_intersect(oro, ord, o.nodes, o.tris, stack, tri);
+}
+
+// sng::depth_test_world (common.cu:36-48)
+__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, int* stack, int& out_obj) {
+    float depth = MAX_DEPTH;
+    const f3 off = origin + dir * MIN_DEPTH;
+    for (int c = 0; c < n_objs; ++c) {
+        int tri;
+        const float t = object_intersect(off, dir, objs[c], stack, tri);
+        if (t < depth && t > MIN_DEPTH) { out_obj = c; depth = t; }
+    }
+    return depth;
+}
+
+struct Hit {
+    f3 pos, normal;
+    m3 perturb;
+    float t;
+    int mat;
+};
+__device__ __forceinline__ f3 tri_normal(const Tri& t) { return normalize(cross(t.b - t.a, t.c - t.a)); }
+// sng::depth_test_world(+HitRecord) (common.cu:50-67)
+__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, int* stack, Hit& h) {
+    const f3 off = origin + dir * MIN_DEPTH;
+    int out_obj = -1;
+    h.t = MAX_DEPTH;
+    h.normal = splat(0.0f);
+    h.mat = -1;
+    h.perturb = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)};
+    for (int c = 0; c < n_objs; ++c) {
+        int tri;
+        const ObjectGpu& o = objs[c];
+        const float t = object_intersect(off, dir, o, stack, tri);
+        if (t < h.t && t > MIN_DEPTH) {
+            out_obj = c;
+            h.t = t;
+            h.mat = o.mat_id;
+            const Tri tr = o.tris[tri];
+            const f3 N = tri_normal(tr);
+            h.normal = mul(o.rot, N);
+            const f3 T = normalize((tr.a + tr.b + tr.c) / 3.0f - tr.a);   // Triangle::get_perturb_matrix (triangle.cuh:164-170)
+            h.perturb = {T, cross(T, N), N};
+        }
+    }
+    h.pos = origin + h.t * dir;
+    return out_obj;
+}
+
+// sng::depth_test_nerf (common.cu:69-83)
+__device__ float depth_test_nerf(float full_d, uint32_t n_steps, const Volume& vol, f3 src, f3 L, f3 invL, uint32_t min_mip, uint32_t max_mip) {
+    float s = 0.0f;
+    for (uint32_t j = 0; j < n_steps; ++j) {
+        s = advance_to_occupied(s, vol.cone, src, L, invL, min_mip, max_mip, vol);
+        if (s >= full_d) { s = full_d; break; }
+        s += calc_dt(s, vol.cone);
+    }
+    return s;
+}
+
+__device__ __forceinline__ Xorwow load_rng(const uint32_t* __restrict__ st, size_t n, size_t i) {
+    return {st[i], st[n + i], st[2 * n + i], st[3 * n + i], st[4 * n + i], st[5 * n + i]};
+}
+__device__ __forceinline__ void store_rng(uint32_t* __restrict__ st, size_t n, size_t i, const Xorwow& s) {
+    st[i] = s.v0; st[n + i] = s.v1; st[2 * n + i] = s.v2; st[3 * n + i] = s.v3; st[4 * n + i] = s.v4; st[5 * n + i] = s.d;
+}
+// Light::sample(rand_state) (light.cuh:71-77)
+__device__ __forceinline__ f3 light_sample(const LightGpu& l, Xorwow& r) {
+    const float x = fractf_(curand_uniform(r)), y = fractf_(curand_uniform(r)), z = fractf_(curand_uniform(r));
+    return l.pos + mk(x, y, z) * l.size * 1.0f;
+}
+
+// ---------------------------------------------------------------------------
+// shade_with_shadow (testbed_nerf.cu:1702-1786) / shadow_for_px (1614-1700)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TPB) void shade_shadow_kernel(ShadowArgs a, float4* __restrict__ rgba, const float* __restrict__ positions,
+                                                            const float* __restrict__ normals, uint32_t* __restrict__ rng, uint32_t n_rng) {
+    __shared__ int stack_lds[BVH_STACK * TPB];
+    int* stack = stack_lds + threadIdx.x;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (t >= n) return;
+    const int x = (int)(t % (uint32_t)a.W), y = a.row0 + (int)(t / (uint32_t)a.W);
+    const size_t idx = (size_t)x + (size_t)a.W * y;
+    Xorwow r = load_rng(rng, n_rng, idx);
+    float sum = 0.0f;
+    int blend = 0;
+    for (int i = -a.radius; i <= a.radius; ++i)
+        for (int j = -a.radius; j <= a.radius; ++j) {
+            const int fx = x + i, fy = y + j;
+            if (fx < 0 || fy < 0 || fx >= a.W || fy >= a.H) continue;
+            const size_t tid = (size_t)fy * a.W + fx;
+            const f3 pos = mk(positions[3 * tid], positions[3 * tid + 1], positions[3 * tid + 2]);
+            const f3 nrm = mk(normals[3 * tid], normals[3 * tid + 1], normals[3 * tid + 2]);
+            float overall = 1.0f;
+            for (int li = 0; li < a.n_lights; ++li) {
+                const LightGpu L = a.lights[li];
+                if (L.type == 0) {
+                    const f3 lpos = light_sample(L, r);
+                    const f3 l = normalize(lpos - pos);
+                    const float full_d = length(lpos - pos);
+                    int hit = -1;
+                    const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, stack, hit);
+                    overall = fminf(overall, powf(syn_depth / full_d, a.intensity));
+                    const f3 fract_offset = full_d * a.threshold * lpos;
+                    const f3 src = pos + fract_offset;
+                    const float fd = length(lpos - src);
+                    const f3 Ld = normalize(lpos - src);
+                    const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip));
+                    const double mask = (double)(nd * (1.0f - fminf(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)a.threshold));
+                    overall = (float)fmin((double)overall, mask);
+                } else {
+                    const f3 l = normalize(L.pos - pos);
+                    const double v = (double)overall + fmin(0.0, (double)dot(l, nrm)) * (double)L.intensity;
+                    overall = (float)fmin(1.0, v);
+                }
+            }
+            sum += overall;
+            ++blend;
+        }
+    sum /= (float)blend;
+    sum = powf(sum, a.intensity);
+    float4 c = rgba[idx];
+    c.x = srgb_to_linear(c.x) * sum;
+    c.y = srgb_to_linear(c.y) * sum;
+    c.z = srgb_to_linear(c.z) * sum;
+    rgba[idx] = c;
+    store_rng(rng, n_rng, idx, r);
+}
+
+// ---------------------------------------------------------------------------
+// mesh-layer camera rays (raytracer.cu:59-99) -- uv without the half-pixel offset
+// ---------------------------------------------------------------------------
+__global__ void mesh_rays_kernel(int W, int H, int row0, int row1, CamDev cam, f2 focal, f2 sc, float4* __restrict__ origin_out,
+                                 float4* __restrict__ dir_out, float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
+    if (t >= n) return;
+    const int x = (int)(t % (uint32_t)W), y = row0 + (int)(t / (uint32_t)W);
+    const size_t idx = (size_t)x + (size_t)W * y;
+    const f2 uv = {(float)x / (float)W, (float)y / (float)H};
+    f3 d = mk((uv.x - sc.x) * (float)W / focal.x, (uv.y - sc.y) * (float)H / focal.y, 1.0f);
+    d = mul(m3{cam.c0, cam.c1, cam.c2}, d);
+    d = normalize(d);
+    origin_out[idx] = make_float4(cam.c3.x, cam.c3.y, cam.c3.z, 0.0f);
+    dir_out[idx] = make_float4(d.x, d.y, d.z, 0.0f);
+    acc_rgba[idx] = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+    acc_depth[idx] = MAX_DEPTH;
+}
+
+// ---------------------------------------------------------------------------
+// sng::raytrace (raytracer.cu:101-218), Final buffer
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ f3 cone_random_up(f3 orig, f3 up, float longi, float latid) {   // common.cuh:37-48
+    const f3 N = normalize(orig);
+    const f3 B = normalize(cross(N, up));
+    const f3 T = cross(B, N);
+    const f3 off = mk(sinf(longi) * cosf(latid), sinf(longi) * sinf(latid), cosf(longi));
+    return orig + mul(m3{T, B, N}, off);
+}
+__device__ __forceinline__ f3 cone_random_frame(f3 orig, const m3& frame, float longi, float latid) {   // common.cuh:33-36
+    const f3 off = mk(cosf(longi) * sinf(latid), sinf(longi) * sinf(latid), cosf(longi));
+    return orig + mul(frame, off);
+}
+__global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, const float4* __restrict__ origins, const float4* __restrict__ dirs,
+                                                        uint32_t* __restrict__ rng, uint32_t n_rng, float4* __restrict__ acc_rgba,
+                                                        float* __restrict__ acc_depth) {
+    __shared__ int stack_lds[BVH_STACK * TPB];
+    int* stack = stack_lds + threadIdx.x;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (t >= n) return;
+    const size_t i = (size_t)a.row0 * a.W + t;
+    Xorwow r = load_rng(rng, n_rng, i);
+    const float4 o4 = origins[i], d4 = dirs[i];
+    const f3 src_p = mk(o4.x, o4.y, o4.z), src_d = mk(d4.x, d4.y, d4.z);
+    f3 shade = splat(0.0f), next_pos = splat(0.0f);
+    for (uint32_t spp = 0; spp < a.samples; ++spp) {
+        const float longi = curand_uniform(r) * a.lens;
+        const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+        f3 rp = src_p, rd = cone_random_up(src_d, a.up, longi, latid);
+        float pdf = 1.0f / (float)a.bounces, att = 1.0f;
+        f3 shade_s = splat(0.0f);
+        for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
+            Hit h;
+            const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, stack, h);
+            if (!bounce) next_pos = next_pos + h.pos;
+            if (hit_obj < 0) break;
+            // shade_object (raytracer.cu:6-57)
+            const MaterialGpu m = a.mats[h.mat];
+            f3 color = splat(0.0f);
+            for (int l = 0; l < a.n_lights; ++l) {
+                const LightGpu L = a.lights[l];
+                for (uint32_t s = 0; s < a.shadow_iters; ++s) {
+                    const f3 lpos = light_sample(L, r);
+                    f3 Lv = lpos - h.pos;
+                    const float full_dist = length(Lv);
+                    Lv = normalize(Lv);
+                    const f3 R = reflect(Lv, h.normal);
+                    const f3 V = normalize(-rd);
+                    const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                    if (L.type == 0) {
+                        float mask = 1.0f;
+                        const f3 invL = inv(Lv);
+                        int oh = -1;
+                        const float syn = a.show_nerf_shadow ? depth_test_world(h.pos, Lv, a.objs, a.n_objs, stack, oh) : 1.0f;
+                        const float nerf = a.show_nerf_shadow
+                                               ? depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, h.pos, Lv, invL, 0, a.vol.max_mip)
+                                               : 1.0f;
+                        const float sh = fminf(fminf(nerf, syn), full_dist);
+                        mask = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
+                        color = color + lc * mask;
+                    } else {
+                        color = color + lc;
+                    }
+                }
+            }
+            color = color / (float)a.shadow_iters;
+            color = color + m.ka;
+            // Material::scatter (material.cuh:112-123)
+            const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
+            const float lo = curand_uniform(r) * spec;
+            const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+            const f3 ndir = cone_random_frame(h.normal, h.perturb, lo, la);
+            shade_s = shade_s + color * pdf * att;
+            rp = h.pos;
+            rd = ndir;
+            pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
+            att = 1.0f * m.rg;
+        }
+        shade = shade + shade_s;
+    }
+    const float weight = (float)a.samples;
+    next_pos = next_pos / weight;
+    shade = shade / weight;
+    acc_depth[i] = dot(src_d, next_pos - src_p);
+    float4 cur = acc_rgba[i];
+    const f3 curr = mk(cur.x, cur.y, cur.z);
+    if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
+    acc_rgba[i] = make_float4(shade.x, shade.y, shade.z, cur.w);
+    store_rng(rng, n_rng, i, r);
+}
+
+// ---------------------------------------------------------------------------
+// overlay_nerf (raytracer.cu:220-258), Identity tonemap
+// ---------------------------------------------------------------------------
+__global__ void overlay_kernel(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
+                               const float4* __restrict__ syn_rgba, const float* __restrict__ syn_depth, const float4* __restrict__ nerf_rgba,
+                               const float* __restrict__ nerf_depth, float4* __restrict__ final_rgba, float* __restrict__ final_depth) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
+    if (t >= n) return;
+    const int x = (int)(t % (uint32_t)W), y = row0 + (int)(t / (uint32_t)W);
+    const int sid = x + y * W;
+    // nerf_res = syn_res / syn_px_scale as in the reference (raytracer.cu:242-246); clamped for memory safety
+    const int nid = min((x / scale) + (y / scale) * nerf_w, n_nerf - 1);
+    const float sdepth = syn_depth[sid];
+    const float4 use = (!show_nerf || sdepth - depth_offset < nerf_depth[nid]) ? syn_rgba[sid] : nerf_rgba[nid];
+    float r = use.x * exposure_mul, g = use.y * exposure_mul, b = use.z * exposure_mul;
+    if (srgb) { r = linear_to_srgb(r); g = linear_to_srgb(g); b = linear_to_srgb(b); }
+    final_rgba[sid] = make_float4(r, g, b, use.w);
+    final_depth[sid] = sdepth;
+}
+
+// ---------------------------------------------------------------------------
+// curand_init(PT_SEED, idx, 0): v <- (M^(2^67))^idx v via precomputed powers
+// ---------------------------------------------------------------------------
+__global__ void xorwow_init_kernel(uint32_t n, uint32_t seed_lo, uint32_t seed_hi, const uint32_t* __restrict__ seq_pow /* 32 x 160 x 5 */,
+                                   uint32_t* __restrict__ st) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s0 = seed_lo ^ 0xaad26b49u, s1 = seed_hi ^ 0xf7dcefddu;
+    const uint32_t t0 = 1099087573u * s0, t1 = 2591861531u * s1;
+    uint32_t v[5] = {123456789u + t0, 362436069u ^ t0, 521288629u + t1, 88675123u ^ t1, 5783321u + t0};
+    const uint32_t d = 6615241u + t1 + t0;
+    for (int k = 0; k < 32; ++k) {
+        if (!((i >> k) & 1u)) continue;
+        const uint32_t* m = seq_pow + (size_t)k * 160 * 5;
+        uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+        for (int j = 0; j < 160; ++j) {
+            const uint32_t w = (j < 32) ? v[0] : (j < 64) ? v[1] : (j < 96) ? v[2] : (j < 128) ? v[3] : v[4];
+            if ((w >> (j & 31)) & 1u) {
+                const uint32_t* c = m + j * 5;
+                r0 ^= c[0]; r1 ^= c[1]; r2 ^= c[2]; r3 ^= c[3]; r4 ^= c[4];
+            }
+        }
+        v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
+    }
+    st[i] = v[0]; st[n + i] = v[1]; st[2 * (size_t)n + i] = v[2]; st[3 * (size_t)n + i] = v[3]; st[4 * (size_t)n + i] = v[4];
+    st[5 * (size_t)n + i] = d;
+}
+
+// ---------------------------------------------------------------------------
+void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, hipStream_t s) {
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (!n) return;
+    hipLaunchKernelGGL(shade_shadow_kernel, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, a, rgba, pos, nrm, rng, n_rng);
+}
+void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
+                      hipStream_t s) {
+    const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
+    if (!n) return;
+    hipLaunchKernelGGL(mesh_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, H, row0, row1, cam, focal, sc, o, d, acc, accd);
+}
+void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
+                     hipStream_t s) {
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (!n) return;
+    hipLaunchKernelGGL(raytrace_kernel, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, a, o, d, rng, n_rng, acc, accd);
+}
+void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
+                    const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s) {
+    const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
+    if (!n) return;
+    hipLaunchKernelGGL(overlay_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, row0, row1, scale, nerf_w, n_nerf, show_nerf, depth_offset, exposure_mul,
+                       srgb, syn, synd, nerf, nerfd, fin, find);
+}
+void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(xorwow_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, (uint32_t)seed, (uint32_t)(seed >> 32), seq_pow, st);
+}
+
+}  // namespace sng

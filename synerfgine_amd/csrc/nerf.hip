@@ -1,0 +1,383 @@
+// nerf.hip -- occupancy-grid ray marcher, wavefront compactor and compositor.
+//
+// Replaces NerfTracer::init_rays_from_camera / trace_alt (testbed_nerf.cu:2037-2277)
+// and the kernels init_rays_with_payload_kernel_nerf (1855-1970), advance_pos_nerf
+// (334-384), compact_kernel_nerf (1830-1853), generate_next_nerf_network_inputs
+// (790-837), composite_kernel_nerf_alt (476-575), extract_from_payload (1578-1612),
+// write_normals_to_buffer (1523-1576) and the bitfield build (285-332, 3212-3229).
+//
+// MI355X design: the host never reads n_alive between iterations.  Each
+// iteration is three launches whose sizes come from a device control block:
+//   generate  : marches up to n_steps occupied samples per alive ray, reserves a
+//               contiguous sample range with one atomic per wave (wave scan), and
+//               writes only REAL samples (no stale slots, no 256-padding);
+//   network   : fused encode+MLP over exactly the reserved samples;
+//   composite : front-to-back compositing, then in the same kernel either the
+//               ray dies (extract_from_payload is applied directly to the frame
+//               buffer) or it is appended to the next alive buffer (compaction
+//               fused into the producer).
+// n_steps = clamp(2^21 / n_alive, 1, 8) and the payload.t reset to the last
+// sample (composite_kernel_nerf_alt:574) are reproduced exactly, so per-pixel
+// results follow the reference's schedule.
+#include "sng_internal.h"
+#include "sng_math.h"
+
+namespace sng {
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t o = __shfl_up(v, off, 64);
+        if (lane >= off) v += o;
+    }
+    return v;
+}
+
+// Append `pred` lanes to a buffer; returns each lane's slot (wave-aggregated atomic).
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred, int lane) {
+    unsigned long long mask = __ballot(pred);
+    uint32_t total = (uint32_t)__popcll(mask);
+    uint32_t base = 0;
+    int leader = mask ? (int)(__ffsll((long long)mask) - 1) : 0;
+    if (total && lane == leader) base = atomicAdd(counter, total);
+    base = __shfl(base, leader, 64);
+    uint32_t below = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    return base + below;
+}
+
+__device__ __forceinline__ uint32_t steps_for(uint32_t n_alive, uint32_t target) {
+    uint32_t s = target / n_alive;
+    return s < 1 ? 1 : (s > MAX_STEPS_BETWEEN_COMPACTION ? MAX_STEPS_BETWEEN_COMPACTION : s);
+}
+
+// ---------------------------------------------------------------------------
+// init_rays_with_payload_kernel_nerf + advance_pos_nerf + first compaction
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf out, MarchCtrl* ctrl, float4* __restrict__ frame_rgba,
+                                                        float* __restrict__ frame_depth, float* __restrict__ positions,
+                                                        float* __restrict__ normals) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t n_band = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    bool alive = false;
+    f3 origin = a.cam.c3, dir = splat(0.0f);
+    float tt = 0.0f;
+    uint32_t idx = 0;
+    if (t < n_band) {
+        const int x = (int)(t % (uint32_t)a.W), y = a.row0 + (int)(t / (uint32_t)a.W);
+        idx = (uint32_t)x + (uint32_t)a.W * (uint32_t)y;
+        f2 off = ld_random_pixel_offset(a.snap ? 0u : a.spp);
+        f2 uv = {((float)x + off.x) / (float)a.W, ((float)y + off.y) / (float)a.H};
+        // uv_to_ray (common_device.cuh:403-470): pinhole, no lens/foveation/parallax/aperture
+        f3 d = mk((uv.x - a.screen_center.x) * (float)a.W / a.focal.x, (uv.y - a.screen_center.y) * (float)a.H / a.focal.y, 1.0f);
+        d = mul(a.ray_rot, d);
+        float4 fb = frame_rgba[idx];
+        fb.x = 0.0f; fb.y = 0.0f; fb.z = 0.0f;
+        if (a.reset) fb.w = 0.0f;
+        frame_rgba[idx] = fb;
+        frame_depth[idx] = MAX_DEPTH;
+        positions[3 * idx + 0] = 0.0f; positions[3 * idx + 1] = 0.0f; positions[3 * idx + 2] = 0.0f;
+        normals[3 * idx + 0] = 0.0f; normals[3 * idx + 1] = 0.0f; normals[3 * idx + 2] = 0.0f;
+        dir = normalize(d);
+        const Volume& v = a.vol;
+        float t0 = fmaxf(aabb_entry(v.render_aabb, to_local(v, origin), to_local(v, dir)), 0.0f) + 1e-6f;
+        if (aabb_contains(v.render_aabb, to_local(v, origin + dir * t0))) {
+            // advance_pos_nerf (testbed_nerf.cu:334-363)
+            f3 idir = inv(dir);
+            float t1 = advance_n_steps(t0, v.cone, ld_random_val0(a.spp, idx * 786433u));
+            t1 = advance_to_occupied(t1, v.cone, origin, dir, idir, 0, v.max_mip, v);
+            if (t1 < MAX_DEPTH) { alive = true; tt = t1; }
+        }
+    }
+    uint32_t slot = wave_append(&ctrl->n_alive[0], alive, lane);
+    if (alive) {
+        out.o_t[slot] = make_float4(origin.x, origin.y, origin.z, tt);
+        out.d_idx[slot] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(idx));
+        out.rgba[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // memset(m_rays[0].rgba) 2102
+        out.depth[slot] = 0.0f;                                // memset(m_rays[0].depth) 2103
+    }
+}
+
+// ---------------------------------------------------------------------------
+// generate_next_nerf_network_inputs (790-837), real samples only
+// coords: NerfCoordinate AoS {warp(pos), warp_dt(dt), warp(dir)} (nerf_device.cuh:176-202)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
+                                                       float* __restrict__ coords, uint2* __restrict__ samp) {
+    const uint32_t n_alive = ctrl->n_alive[p];
+    const uint32_t i_step = ctrl->i_step[p];
+    const bool active = n_alive > 0 && i_step < MARCH_ITER;
+    const uint32_t n_steps = active ? steps_for(n_alive, target) : 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctrl->n_alive[p ^ 1] = 0;
+        ctrl->i_step[p ^ 1] = i_step + n_steps;
+        if (active) {
+            if (iter < 64) { ctrl->alive_hist[iter] = n_alive; ctrl->steps_hist[iter] = n_steps; }
+            ctrl->n_iter = iter + 1;
+            ctrl->ref_slots += ((unsigned long long)n_alive * n_steps + 255ull) / 256ull * 256ull;
+        }
+    }
+    if (!active) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+    const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
+    for (uint32_t base_i = gw * 64; base_i < n_alive; base_i += n_waves * 64) {
+        const uint32_t i = base_i + lane;
+        uint32_t cnt = 0;
+        float ts[MAX_STEPS_BETWEEN_COMPACTION];
+        f3 o = splat(0.0f), d = splat(1.0f);
+        if (i < n_alive) {
+            float4 ot = rays.o_t[i], di = rays.d_idx[i];
+            o = mk(ot.x, ot.y, ot.z);
+            d = mk(di.x, di.y, di.z);
+            const f3 idir = inv(d);
+            float t = ot.w;
+#pragma unroll
+            for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
+                if (j < n_steps && cnt == j) {
+                    t = advance_to_occupied(t, vol.cone, o, d, idir, 0, vol.max_mip, vol);
+                    if (t < MAX_DEPTH) {
+                        ts[j] = t;
+                        t += calc_dt(t, vol.cone);
+                        ++cnt;
+                    }
+                }
+            }
+        }
+        const uint32_t incl = wave_incl_scan(cnt, lane);
+        uint32_t base = 0;
+        if (lane == 63 && incl) base = atomicAdd(&ctrl->n_samples[p], incl);
+        base = __shfl(base, 63, 64) + incl - cnt;
+        if (i < n_alive) {
+            samp[i] = make_uint2(base, cnt);
+            const f3 wd = (d + 1.0f) * 0.5f;
+#pragma unroll
+            for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
+                if (j < cnt) {
+                    const float t = ts[j];
+                    const float dt = calc_dt(t, vol.cone);
+                    const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
+                    float* c = coords + (size_t)(base + j) * 7;
+                    c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// composite_kernel_nerf_alt (476-575) + compaction into the next buffer
+// (compact_kernel_nerf 1830-1853) + extract_from_payload (1578-1612)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p, uint32_t target,
+                                                        const float* __restrict__ coords, const uint2* __restrict__ samp,
+                                                        const uint2* __restrict__ net_out, float4* __restrict__ frame_rgba,
+                                                        float* __restrict__ frame_depth, float* __restrict__ positions) {
+    const uint32_t n_alive = ctrl->n_alive[p];
+    const uint32_t i_step = ctrl->i_step[p];
+    const bool active = n_alive > 0 && i_step < MARCH_ITER;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (active) ctrl->total_samples += ctrl->n_samples[p];
+        ctrl->n_samples[p ^ 1] = 0;
+    }
+    if (!active) return;
+    const uint32_t n_steps = steps_for(n_alive, target);
+    // the reference leaves the loop without another compaction once i >= MARCH_ITER
+    const bool last = i_step + n_steps >= MARCH_ITER;
+    const int lane = threadIdx.x & 63;
+    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+    const f3 diag = vol.train_aabb.hi - vol.train_aabb.lo;
+    for (uint32_t base_i = gw * 64; base_i < n_alive; base_i += n_waves * 64) {
+        const uint32_t i = base_i + lane;
+        bool survive = false, hit = false;
+        float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
+        float depth = 0.0f;
+        if (i < n_alive) {
+            rgba = in.rgba[i];
+            depth = in.depth[i];
+            ot = in.o_t[i];
+            di = in.d_idx[i];
+            const uint2 sc = samp[i];
+            uint32_t j = 0;
+            for (; j < sc.y; ++j) {
+                const uint2 raw = net_out[sc.x + j];
+                const float* c = coords + (size_t)(sc.x + j) * 7;
+                const f3 pos = vol.train_aabb.lo + mk(c[0], c[1], c[2]) * diag;
+                const float T = 1.f - rgba.w;
+                const float dt = unwarp_dt(c[3]);
+                const float r = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x & 0xffffu));
+                const float g = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x >> 16));
+                const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y & 0xffffu));
+                const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
+                const float alpha = 1.f - expf(-expf(s) * dt);
+                const float weight = alpha * T;
+                rgba.x += logistic(r) * weight;
+                rgba.y += logistic(g) * weight;
+                rgba.z += logistic(b) * weight;
+                rgba.w += weight;
+                depth = dot(cam.c2, pos - cam.c3);
+                if (rgba.w > (1.0f - vol.min_transmittance)) {
+                    const float aa = rgba.w;
+                    rgba.x /= aa; rgba.y /= aa; rgba.z /= aa; rgba.w /= aa;
+                    break;
+                }
+            }
+            const f3 dir = mk(di.x, di.y, di.z);
+            ot.w = depth / dot(cam.c2, dir);   // payload.t reset (576)
+            if (j < n_steps) hit = !last && rgba.w > 0.001f;
+            else survive = !last;
+        }
+        const uint32_t slot = wave_append(&ctrl->n_alive[p ^ 1], survive, lane);
+        if (survive) {
+            out.o_t[slot] = ot;
+            out.d_idx[slot] = di;
+            out.rgba[slot] = rgba;
+            out.depth[slot] = depth;
+        }
+        if (hit) {
+            const uint32_t idx = __float_as_uint(di.w);
+            const f3 dir = mk(di.x, di.y, di.z);
+            const f3 orig = cam.c3 + dir * ot.w;
+            float4 fb = frame_rgba[idx];
+            const float ta = rgba.w;
+            const float r = srgb_to_linear(rgba.x), g = srgb_to_linear(rgba.y), b = srgb_to_linear(rgba.z);
+            fb = make_float4(r + fb.x * (1.0f - ta), g + fb.y * (1.0f - ta), b + fb.z * (1.0f - ta), ta + fb.w * (1.0f - ta));
+            frame_rgba[idx] = fb;
+            positions[3 * idx + 0] = orig.x; positions[3 * idx + 1] = orig.y; positions[3 * idx + 2] = orig.z;
+            if (ta > 0.2f) frame_depth[idx] = depth;
+        }
+        const uint32_t nh = (uint32_t)__popcll(__ballot(hit));
+        if (lane == 0 && nh) atomicAdd(&ctrl->n_hit, nh);
+    }
+}
+
+// write_normals_to_buffer (1523-1576) for rows [row0,row1)
+__global__ __launch_bounds__(256) void normals_kernel(int W, int H, int row0, int row1, const float* __restrict__ positions,
+                                                      float* __restrict__ normals) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
+    if (t >= n) return;
+    const int x = (int)(t % (uint32_t)W), y = row0 + (int)(t / (uint32_t)W);
+    const size_t idx = (size_t)x + (size_t)W * y;
+    const f3 pos = mk(positions[3 * idx], positions[3 * idx + 1], positions[3 * idx + 2]);
+    const int OX[9] = {1, 0, -1, 0, 2, 0, -2, 0, 1};
+    const int OY[9] = {0, 1, 0, -1, 0, 2, 0, -2, 0};
+    float factor = 0.0f;
+    f3 N = splat(0.0f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int tx = x + OX[k + 1], ty = y + OY[k + 1], bx = x + OX[k], by = y + OY[k];
+        if (tx >= W || tx < 0 || ty >= H || ty < 0 || bx >= W || bx < 0 || by >= H || by < 0) continue;
+        const float* pt = positions + 3 * ((size_t)ty * W + tx);
+        const float* pb = positions + 3 * ((size_t)by * W + bx);
+        const f3 T = mk(pt[0], pt[1], pt[2]) - pos;
+        const f3 B = mk(pb[0], pb[1], pb[2]) - pos;
+        N = N + normalize(cross(normalize(T), B));
+        factor += 1.0f;
+    }
+    N = factor == 0.0f ? N : N / factor;
+    const f3 nn = normalize(N);
+    normals[3 * idx] = nn.x; normals[3 * idx + 1] = nn.y; normals[3 * idx + 2] = nn.z;
+}
+
+// ---------------------------------------------------------------------------
+// density grid -> bitfield (update_density_grid_mean_and_bitfield, 3212-3229)
+// ---------------------------------------------------------------------------
+__global__ void half_to_float_kernel(const uint16_t* __restrict__ in, float* __restrict__ out, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (float)__builtin_bit_cast(_Float16, in[i]);
+}
+// deterministic mean: per-block double partial sums of fmaxf(v,0)/N, then one block sums them
+__global__ __launch_bounds__(256) void mean_partial_kernel(const float* __restrict__ grid, uint32_t n, double* __restrict__ partial) {
+    __shared__ double sm[256];
+    double acc = 0.0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) acc += (double)(fmaxf(grid[i], 0.f) / (float)n);
+    sm[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) sm[threadIdx.x] += sm[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = sm[0];
+}
+__global__ void mean_final_kernel(const double* __restrict__ partial, int n_part, float* __restrict__ mean) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double s = 0.0;
+        for (int i = 0; i < n_part; ++i) s += partial[i];
+        *mean = (float)s;
+    }
+}
+__global__ void grid_to_bitfield_kernel(uint32_t n_elements, uint32_t n_nonzero, const float* __restrict__ grid, uint8_t* __restrict__ bf,
+                                        const float* __restrict__ mean) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_elements) return;
+    if (i >= n_nonzero) { bf[i] = 0; return; }
+    const float thresh = fminf(MIN_OPTICAL_THICKNESS, *mean);
+    uint8_t bits = 0;
+#pragma unroll
+    for (uint8_t j = 0; j < 8; ++j) bits |= grid[i * 8 + j] > thresh ? ((uint8_t)1 << j) : 0;
+    bf[i] = bits;
+}
+__global__ void bitfield_max_pool_kernel(uint32_t n_elements, const uint8_t* __restrict__ prev, uint8_t* __restrict__ next) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_elements) return;
+    uint8_t bits = 0;
+#pragma unroll
+    for (uint8_t j = 0; j < 8; ++j) bits |= prev[i * 8 + j] > 0 ? ((uint8_t)1 << j) : 0;
+    const uint32_t x = morton3D_invert(i >> 0) + GRID_SIZE / 8;
+    const uint32_t y = morton3D_invert(i >> 1) + GRID_SIZE / 8;
+    const uint32_t z = morton3D_invert(i >> 2) + GRID_SIZE / 8;
+    // each (x,y,z) is written by exactly one thread of this launch
+    next[morton3D(x, y, z)] |= bits;
+}
+
+__global__ void ctrl_init_kernel(MarchCtrl* c) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        c->n_alive[0] = 0; c->n_alive[1] = 0;
+        c->n_samples[0] = 0; c->n_samples[1] = 0;
+        c->i_step[0] = 1; c->i_step[1] = 1;   // trace_alt: uint32_t i = 1 (2163)
+        c->n_hit = 0; c->n_iter = 0;
+        c->total_samples = 0; c->ref_slots = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s) { hipLaunchKernelGGL(ctrl_init_kernel, dim3(1), dim3(64), 0, s, ctrl); }
+// ---------------------------------------------------------------------------
+void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm,
+                      hipStream_t s) {
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (!n) return;
+    hipLaunchKernelGGL(init_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, out, ctrl, fb, depth, pos, nrm);
+}
+void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
+                     uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL(generate_kernel, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp);
+}
+void launch_composite(const Volume& v, const CamDev& cam, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target,
+                      const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
+                      hipStream_t s) {
+    hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, s, v, cam, in, out, ctrl, p, target, coords, samp, net_out, fb, depth, pos);
+}
+void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {
+    const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
+    if (!n) return;
+    hipLaunchKernelGGL(normals_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, H, row0, row1, pos, nrm);
+}
+void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, hipStream_t s) {
+    const uint32_t N = GRID_CELLS;
+    const uint32_t n_cells = N * (max_cascade + 1);
+    hipLaunchKernelGGL(half_to_float_kernel, dim3((n_cells + 255) / 256), dim3(256), 0, s, grid_f16, grid_f32, n_cells);
+    hipLaunchKernelGGL(mean_partial_kernel, dim3(1024), dim3(256), 0, s, grid_f32, N, partial);
+    hipLaunchKernelGGL(mean_final_kernel, dim3(1), dim3(64), 0, s, partial, 1024, mean);
+    const uint32_t n_el = N / 8 * N_CASCADES;
+    hipLaunchKernelGGL(grid_to_bitfield_kernel, dim3((n_el + 255) / 256), dim3(256), 0, s, n_el, N / 8 * (max_cascade + 1), grid_f32, bf, mean);
+    for (uint32_t level = 1; level < N_CASCADES; ++level)
+        hipLaunchKernelGGL(bitfield_max_pool_kernel, dim3((N / 64 + 255) / 256), dim3(256), 0, s, N / 64, bf + (size_t)N / 8 * (level - 1),
+                           bf + (size_t)N / 8 * level);
+}
+
+}  // namespace sng

@@ -1,0 +1,116 @@
+// sng_internal.h -- device-side data layout shared by the host runtime and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sng_math.h"
+
+namespace sng {
+
+// Per-level hash-grid metadata (tcnn GridOffsetTable + grid_scale/grid_resolution).
+struct LevelInfo {
+    uint32_t offset;     // first entry of the level
+    uint32_t size;       // hashmap_size (entries)
+    uint32_t pow2_mask;  // size-1 if size is a power of two, else 0
+    uint32_t dense;      // 1 if the tcnn stride loop keeps the dense index
+    uint32_t res;        // grid_resolution(scale)
+    uint32_t res2;       // res*res (dense index)
+    float scale;         // grid_scale(level)
+    uint32_t pad;
+};
+
+struct NetworkDev {
+    int F = 4, L = 8;
+    int n_cus = 256;
+    void* wfrag = nullptr;      // 20 fragments x 64 lanes x 8 halves (MFMA A operands, permuted k)
+    void* grid = nullptr;       // fp16 grid params (entries x F)
+    LevelInfo* levels = nullptr;
+};
+
+// Wavefront control block (device), ping-pong by iteration parity.
+struct MarchCtrl {
+    uint32_t n_alive[2];
+    uint32_t n_samples[2];
+    uint32_t i_step[2];
+    uint32_t n_hit;
+    uint32_t n_iter;
+    unsigned long long total_samples;
+    unsigned long long ref_slots;
+    uint32_t alive_hist[64];
+    uint32_t steps_hist[64];
+};
+
+// Alive-ray SoA buffer (NerfPayload + rgba + depth, nerf_device.cuh:145-153; nerf.h:22-42)
+struct RayBuf {
+    float4* o_t;       // origin.xyz, t
+    float4* d_idx;     // dir.xyz, pixel index (bits)
+    float4* rgba;
+    float* depth;
+};
+
+struct CamDev {
+    f3 c0, c1, c2, c3;   // mat4x3 columns (right, down, fwd, position)
+};
+
+struct NerfFrameArgs {
+    Volume vol;
+    CamDev cam;          // camera0 (composite/extract)
+    m3 ray_rot;          // rotation after the rolling-shutter quat round trip (common_device.cuh:361-368)
+    f2 focal;
+    f2 screen_center;
+    int W, H;            // full NeRF resolution (pixel indices are global)
+    int row0, row1;      // rows traced for this band
+    uint32_t spp;
+    int snap;
+    int reset;           // clear alpha of the frame buffer (camera moved)
+    uint32_t target_n_queries;
+};
+
+int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
+                   uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream);
+int launch_encode(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n, uint16_t* out, hipStream_t stream);
+
+struct ShadowArgs {
+    Volume vol;
+    int W, H, row0, row1;
+    int radius;                 // kernel_size / 2
+    float intensity;            // nerf_shadow_intensity
+    float threshold;            // nerf_on_nerf_shadow_threshold
+    const ObjectGpu* objs; int n_objs;
+    const LightGpu* lights; int n_lights;
+};
+
+struct RaytraceArgs {
+    Volume vol;
+    int W, row0, row1;
+    f3 up;                      // camera[0]
+    const ObjectGpu* objs; int n_objs;
+    const LightGpu* lights; int n_lights;
+    const MaterialGpu* mats;
+    uint32_t samples, bounces, shadow_iters, shadow_steps;
+    float lens;
+    int show_nerf_shadow;
+    float syn_shadow_factor;
+};
+
+// nerf.hip
+void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, hipStream_t s);
+void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
+                     uint32_t blocks, hipStream_t s);
+void launch_composite(const Volume& v, const CamDev& cam, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target,
+                      const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
+                      hipStream_t s);
+void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s);
+void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, hipStream_t s);
+void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s);
+// mesh.hip
+void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, hipStream_t s);
+void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
+                      hipStream_t s);
+void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
+                     hipStream_t s);
+void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
+                    const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s);
+void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s);
+
+}  // namespace sng

@@ -1,0 +1,293 @@
+// sng_math.h -- host/device math for the MI355X SyNeRFgine render path.
+//
+// Float semantics follow the reference's device code (tcnn vec/mat, cited per
+// function) evaluated IEEE-exactly: the library is compiled with
+// -ffp-contract=off so that marching decisions match the CPU oracle bitwise.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SNG_HD __host__ __device__ __forceinline__
+
+namespace sng {
+
+// ---- constants: nerf_device.cuh:25-43, common_device.cuh:32-33, testbed_nerf.cu:47-50
+constexpr uint32_t GRID_SIZE = 128;
+constexpr uint32_t GRID_CELLS = GRID_SIZE * GRID_SIZE * GRID_SIZE;
+constexpr uint32_t N_CASCADES = 8;
+constexpr uint32_t NERF_STEPS = 1024;
+constexpr float SQRT3 = 1.73205080757f;
+constexpr float MIN_STEP = SQRT3 / NERF_STEPS;
+constexpr float MAX_STEP = MIN_STEP * (1 << (N_CASCADES - 1)) * NERF_STEPS / GRID_SIZE;
+constexpr float MAX_DEPTH = 16384.0f;
+constexpr float MIN_DEPTH = 0.00001f;
+constexpr uint32_t MARCH_ITER = 10000;
+constexpr uint32_t MAX_STEPS_BETWEEN_COMPACTION = 8;
+constexpr float MIN_OPTICAL_THICKNESS = 0.01f;
+constexpr float PI_F = 3.14159265358979323846f;
+constexpr uint32_t PT_SEED = 1999;  // synerfgine/common.cuh:20
+
+struct f3 { float x, y, z; };
+SNG_HD f3 mk(float x, float y, float z) { return {x, y, z}; }
+SNG_HD f3 splat(float s) { return {s, s, s}; }
+SNG_HD f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+SNG_HD f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+SNG_HD f3 operator-(f3 a) { return {-a.x, -a.y, -a.z}; }
+SNG_HD f3 operator*(f3 a, f3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+SNG_HD f3 operator/(f3 a, f3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+SNG_HD f3 operator*(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+SNG_HD f3 operator*(float s, f3 a) { return {s * a.x, s * a.y, s * a.z}; }
+SNG_HD f3 operator/(f3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+SNG_HD f3 operator+(f3 a, float s) { return {a.x + s, a.y + s, a.z + s}; }
+SNG_HD f3 operator-(f3 a, float s) { return {a.x - s, a.y - s, a.z - s}; }
+SNG_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+SNG_HD f3 cross(f3 a, f3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+SNG_HD float length(f3 a) { return sqrtf(dot(a, a)); }
+// tcnn normalize(): zero-length guard returns the first unit vector [tcnn vec.h]
+SNG_HD f3 normalize(f3 a) {
+    float l = length(a);
+    if (!(l > 0.0f)) return {1.0f, 0.0f, 0.0f};
+    return a / l;
+}
+SNG_HD f3 inv(f3 a) { return {1.0f / a.x, 1.0f / a.y, 1.0f / a.z}; }
+SNG_HD float fractf_(float x) { return x - floorf(x); }
+SNG_HD float sgnf(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+SNG_HD float logistic(float x) { return 1.0f / (1.0f + expf(-x)); }
+SNG_HD float smoothstep(float x) { return x * x * (3.0f - 2.0f * x); }
+SNG_HD f3 reflect(f3 i, f3 n) { return 2.0f * dot(i, n) * n - i; }
+
+// column-major 3x3; mat*vec accumulates columns as tcnn's tmat operator*
+struct m3 { f3 c0, c1, c2; };
+SNG_HD f3 mul(const m3& m, f3 v) {
+    f3 r = splat(0.0f);
+    r = r + m.c0 * v.x;
+    r = r + m.c1 * v.y;
+    r = r + m.c2 * v.z;
+    return r;
+}
+SNG_HD m3 mulm(const m3& a, const m3& b) { return {mul(a, b.c0), mul(a, b.c1), mul(a, b.c2)}; }
+
+// sRGB: common_device.cuh:35-70
+SNG_HD float srgb_to_linear(float s) { return s <= 0.04045f ? s / 12.92f : powf((s + 0.055f) / 1.055f, 2.4f); }
+SNG_HD float linear_to_srgb(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * powf(l, 0.41666f) - 0.055f; }
+
+// ---- Morton (tcnn common_device.h) --------------------------------------------
+SNG_HD uint32_t expand_bits(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+SNG_HD uint32_t morton3D(uint32_t x, uint32_t y, uint32_t z) { return expand_bits(x) | (expand_bits(y) << 1) | (expand_bits(z) << 2); }
+SNG_HD uint32_t morton3D_invert(uint32_t x) {
+    x = x & 0x49249249u;
+    x = (x | (x >> 2)) & 0xc30c30c3u;
+    x = (x | (x >> 4)) & 0x0f00f00fu;
+    x = (x | (x >> 8)) & 0xff0000ffu;
+    x = (x | (x >> 16)) & 0x0000ffffu;
+    return x;
+}
+
+// ---- AABB slab test: bounding_box.cuh:163-211 ---------------------------------
+struct aabb { f3 lo, hi; };
+struct f2 { float x, y; };
+SNG_HD void fswap(float& a, float& b) { float t = a; a = b; b = t; }
+SNG_HD float aabb_entry(const aabb& b, f3 pos, f3 dir) {
+    const float FMAX = 3.402823466e+38f;
+    float tmin = (b.lo.x - pos.x) / dir.x;
+    float tmax = (b.hi.x - pos.x) / dir.x;
+    if (tmin > tmax) fswap(tmin, tmax);
+    float tymin = (b.lo.y - pos.y) / dir.y;
+    float tymax = (b.hi.y - pos.y) / dir.y;
+    if (tymin > tymax) fswap(tymin, tymax);
+    if (tmin > tymax || tymin > tmax) return FMAX;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = (b.lo.z - pos.z) / dir.z;
+    float tzmax = (b.hi.z - pos.z) / dir.z;
+    if (tzmin > tzmax) fswap(tzmin, tzmax);
+    if (tmin > tzmax || tzmin > tmax) return FMAX;
+    if (tzmin > tmin) tmin = tzmin;
+    return tmin;
+}
+SNG_HD bool aabb_contains(const aabb& b, f3 p) {
+    return p.x >= b.lo.x && p.x <= b.hi.x && p.y >= b.lo.y && p.y <= b.hi.y && p.z >= b.lo.z && p.z <= b.hi.z;
+}
+
+// ---- stepping: nerf_device.cuh:266-441 ----------------------------------------
+SNG_HD float warp_dt(float dt) {
+    float max_stepsize = MIN_STEP * (1 << (N_CASCADES - 1));
+    return (dt - MIN_STEP) / (max_stepsize - MIN_STEP);
+}
+SNG_HD float unwarp_dt(float dt) {
+    float max_stepsize = MIN_STEP * (1 << (N_CASCADES - 1));
+    return dt * (max_stepsize - MIN_STEP) + MIN_STEP;
+}
+SNG_HD float to_stepping_space(float t, float cone) {
+    if (cone <= 1e-5f) return t / MIN_STEP;
+    float log1p_c = logf(1.0f + cone);
+    float a = (logf(MIN_STEP) - logf(log1p_c)) / log1p_c;
+    float b = (logf(MAX_STEP) - logf(log1p_c)) / log1p_c;
+    float at = expf(a * log1p_c);
+    float bt = expf(b * log1p_c);
+    if (t <= at) return (t - at) / MIN_STEP + a;
+    else if (t <= bt) return logf(t) / log1p_c;
+    else return (t - bt) / MAX_STEP + b;
+}
+SNG_HD float from_stepping_space(float n, float cone) {
+    if (cone <= 1e-5f) return n * MIN_STEP;
+    float log1p_c = logf(1.0f + cone);
+    float a = (logf(MIN_STEP) - logf(log1p_c)) / log1p_c;
+    float b = (logf(MAX_STEP) - logf(log1p_c)) / log1p_c;
+    float at = expf(a * log1p_c);
+    float bt = expf(b * log1p_c);
+    if (n <= a) return (n - a) * MIN_STEP + at;
+    else if (n <= b) return expf(n * log1p_c);
+    else return (n - b) * MAX_STEP + bt;
+}
+SNG_HD float advance_n_steps(float t, float cone, float n) { return from_stepping_space(to_stepping_space(t, cone) + n, cone); }
+SNG_HD float calc_dt(float t, float cone) { return advance_n_steps(t, cone, 1.0f) - t; }
+
+SNG_HD float distance_to_next_voxel(f3 pos, f3 dir, f3 idir, float res) {
+    f3 p = res * (pos - 0.5f);
+    float tx = (floorf(p.x + 0.5f + 0.5f * sgnf(dir.x)) - p.x) * idir.x;
+    float ty = (floorf(p.y + 0.5f + 0.5f * sgnf(dir.y)) - p.y) * idir.y;
+    float tz = (floorf(p.z + 0.5f + 0.5f * sgnf(dir.z)) - p.z) * idir.z;
+    float t = fminf(fminf(tx, ty), tz);
+    return fmaxf(t / res, 0.0f);
+}
+SNG_HD float advance_to_next_voxel(float t, float cone, f3 pos, f3 dir, f3 idir, uint32_t mip) {
+    float res = scalbnf((float)GRID_SIZE, -(int)mip);
+    float t_target = t + distance_to_next_voxel(pos, dir, idir, res);
+    t = to_stepping_space(t, cone);
+    t_target = to_stepping_space(t_target, cone);
+    return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), cone);
+}
+SNG_HD uint32_t mip_from_pos(f3 pos, uint32_t max_cascade) {
+    int exponent;
+    f3 d = pos - 0.5f;
+    float maxval = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    frexpf(maxval, &exponent);
+    int e = exponent + 1;
+    e = e < 0 ? 0 : e;
+    return (uint32_t)(e > (int)max_cascade ? (int)max_cascade : e);
+}
+SNG_HD uint32_t cascaded_grid_idx_at(f3 pos, uint32_t mip) {
+    float mip_scale = scalbnf(1.0f, -(int)mip);
+    pos = pos - splat(0.5f);
+    pos = pos * mip_scale;
+    pos = pos + splat(0.5f);
+    f3 f = pos * (float)GRID_SIZE;
+    int ix = (int)f.x, iy = (int)f.y, iz = (int)f.z;
+    if (ix < 0 || ix >= (int)GRID_SIZE || iy < 0 || iy >= (int)GRID_SIZE || iz < 0 || iz >= (int)GRID_SIZE) return 0xFFFFFFFFu;
+    return morton3D(ix, iy, iz);
+}
+SNG_HD bool occupied_at(f3 pos, const uint8_t* bf, uint32_t mip) {
+    uint32_t idx = cascaded_grid_idx_at(pos, mip);
+    if (idx == 0xFFFFFFFFu) return false;
+    return bf[idx / 8 + (GRID_CELLS * mip) / 8] & (1 << (idx % 8));
+}
+
+// Volume description shared by the marcher, shadow rays and the path tracer.
+struct Volume {
+    aabb render_aabb;    // m_render_aabb
+    aabb train_aabb;     // m_aabb (warp_position)
+    m3 to_local;         // m_render_aabb_to_local
+    int to_local_identity;
+    float cone;          // cone_angle_constant
+    uint32_t max_mip;    // max_cascade
+    float min_transmittance;
+    const uint8_t* bitfield;
+};
+SNG_HD f3 to_local(const Volume& v, f3 p) { return v.to_local_identity ? p : mul(v.to_local, p); }
+
+// if_unoccupied_advance_to_next_occupied_voxel<false>: nerf_device.cuh:462-495
+SNG_HD float advance_to_occupied(float t, float cone, f3 o, f3 d, f3 idir, uint32_t min_mip, uint32_t max_mip, const Volume& vol) {
+    while (true) {
+        f3 pos = o + d * t;
+        if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) return MAX_DEPTH;
+        uint32_t mip = mip_from_pos(pos, N_CASCADES - 1);
+        mip = mip < min_mip ? min_mip : mip;
+        mip = mip > max_mip ? max_mip : mip;
+        if (!vol.bitfield || occupied_at(pos, vol.bitfield, mip)) return t;
+        while (mip < max_mip && !occupied_at(pos, vol.bitfield, mip + 1)) ++mip;
+        t = advance_to_next_voxel(t, cone, pos, d, idir, mip);
+    }
+}
+
+// ---- scrambled Sobol: random_val.cuh:162-325 ---------------------------------
+SNG_HD uint32_t reverse_bits(uint32_t x) {
+    x = (((x & 0xaaaaaaaau) >> 1) | ((x & 0x55555555u) << 1));
+    x = (((x & 0xccccccccu) >> 2) | ((x & 0x33333333u) << 2));
+    x = (((x & 0xf0f0f0f0u) >> 4) | ((x & 0x0f0f0f0fu) << 4));
+    x = (((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8));
+    return ((x >> 16) | (x << 16));
+}
+SNG_HD uint32_t lk_permutation(uint32_t x, uint32_t seed) {
+    x += seed;
+    x ^= x * 0x6c50b47cu;
+    x ^= x * 0xb82f1e52u;
+    x ^= x * 0xc7afe638u;
+    x ^= x * 0x8d22f6e6u;
+    return x;
+}
+SNG_HD uint32_t nested_scramble(uint32_t x, uint32_t seed) { return reverse_bits(lk_permutation(reverse_bits(x), seed)); }
+SNG_HD uint32_t hash_combine(uint32_t seed, uint32_t v) { return seed ^ (v + (seed << 6) + (seed >> 2)); }
+// Sobol dimension 0 is the bit reversal (van der Corput); dimension 1 uses the
+// Pascal-matrix directions 0x80000000 ^ ... generated as (d_{k} = d_{k-1} ^ d_{k-1}>>1).
+SNG_HD uint32_t sobol_dim0(uint32_t index) { return reverse_bits(index); }
+SNG_HD uint32_t sobol_dim1(uint32_t index) {
+    uint32_t X = 0, d = 0x80000000u;
+    for (uint32_t bit = 0; bit < 32; ++bit) {
+        if ((index >> bit) & 1u) X ^= d;
+        d ^= d >> 1;
+    }
+    return X;
+}
+SNG_HD float ld_random_val0(uint32_t index, uint32_t seed) {
+    constexpr float S = float(1.0 / (1ull << 32));
+    index = nested_scramble(index, seed);
+    return (float)nested_scramble(sobol_dim0(index), hash_combine(seed, 0)) * S;
+}
+SNG_HD f2 ld_random_val_2d(uint32_t index, uint32_t seed) {
+    constexpr float S = float(1.0 / (1ull << 32));
+    index = nested_scramble(index, seed);
+    return {(float)nested_scramble(sobol_dim0(index), hash_combine(seed, 0)) * S,
+            (float)nested_scramble(sobol_dim1(index), hash_combine(seed, 1)) * S};
+}
+SNG_HD f2 ld_random_pixel_offset(uint32_t spp) {
+    f2 a = ld_random_val_2d(0, 0xdeadbeefu), b = ld_random_val_2d(spp, 0xdeadbeefu);
+    return {fractf_(0.5f - a.x + b.x), fractf_(0.5f - a.y + b.y)};
+}
+
+// ---- cuRAND XORWOW state (curand_kernel.h), SoA-friendly ----------------------
+struct Xorwow { uint32_t v0, v1, v2, v3, v4, d; };
+SNG_HD uint32_t xorwow_next(Xorwow& s) {
+    uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1; s.v1 = s.v2; s.v2 = s.v3; s.v3 = s.v4;
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.d += 362437u;
+    return s.v4 + s.d;
+}
+SNG_HD float curand_uniform(Xorwow& s) {
+    const float INV = 2.3283064e-10f;  // CURAND_2POW32_INV
+    return (float)xorwow_next(s) * INV + (INV / 2.0f);
+}
+
+// ---- scene records ------------------------------------------------------------
+struct BvhNode { float lo[3], hi[3]; int left, right; };   // TriangleBvhNode (32 B)
+struct Tri { f3 a, b, c; };                                 // Triangle (36 B)
+struct ObjectGpu {                                           // ObjectTransform + hoisted inverse
+    const BvhNode* nodes;
+    const Tri* tris;
+    m3 rot;
+    f3 pos;
+    float scale;
+    int mat_id;
+    m3 world_to_obj;   // (I/scale) * inverse(rot), triangle_bvh.cu:313-319
+};
+struct LightGpu { f3 pos; float intensity; float size; int type; };
+struct MaterialGpu { f3 ka, kd, ks; float n, rg, spec_angle; int type; };
+
+}  // namespace sng
