@@ -31,6 +31,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=["c2", "c3"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial-streams", action="store_true", help="run raytracer and NeRF back to back (profiling)")
     ap.add_argument("--cpu-baseline-scale", type=int, default=2, help="oracle renders the frame at 1/scale linear resolution")
     return ap.parse_args()
 
@@ -76,7 +77,7 @@ def main():
         dist.init_process_group("nccl")
     from synerfgine_amd import scene as S
 
-    tb, eng, eng_cfg = S.make_engine(args.config, device_id=local_rank)
+    tb, eng, eng_cfg = S.make_engine(args.config, device_id=local_rank, overrides={"concurrent_streams": 0} if args.serial_streams else None)
     res = eng.resolution()
     MW, MH = res["mesh"]
     band = MH // world

@@ -88,6 +88,7 @@ typedef struct {
     uint32_t network_launches;
     uint32_t alive_per_iter[64];
     uint32_t steps_per_iter[64];
+    uint32_t samples_per_iter[64];
     int32_t reserved[8];
 } sng_frame_result;
 

@@ -121,6 +121,7 @@ class FrameResult:
             setattr(self, name, getattr(r, name))
         self.alive_per_iter = list(r.alive_per_iter)[: min(64, r.n_iterations)]
         self.steps_per_iter = list(r.steps_per_iter)[: min(64, r.n_iterations)]
+        self.samples_per_iter = list(r.samples_per_iter)[: min(64, r.n_iterations)]
 
     def download(self, name):
         """Copy a device output buffer to host as float32 [H, W, C]."""

@@ -77,6 +77,7 @@ class sng_frame_result(ctypes.Structure):
         ("network_launches", ctypes.c_uint32),
         ("alive_per_iter", ctypes.c_uint32 * 64),
         ("steps_per_iter", ctypes.c_uint32 * 64),
+        ("samples_per_iter", ctypes.c_uint32 * 64),
         ("reserved", ctypes.c_int32 * 8),
     ]
 

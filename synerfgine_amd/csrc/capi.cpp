@@ -315,6 +315,8 @@ const std::map<std::string, double>& default_params() {
         {"srgb", 1},                            // EColorSpace::SRGB passed to overlay (engine.cu:406)
         {"smooth_threshold", 1.0},              // sng_position_kernel_threshold (unused by the path)
         {"max_shadow_variance", 0.0},           // sng_shadow_depth_variance (unused by the path)
+        {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
+        {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
     };
     return d;
 }
@@ -341,7 +343,7 @@ struct sng_ctx {
 
     // occupancy
     bool has_bitfield = false;
-    DevBuf d_bitfield, d_grid_f16, d_grid_f32, d_partial, d_mean;
+    DevBuf d_bitfield, d_occ_linear, d_grid_f16, d_grid_f32, d_partial, d_mean;
 
     // camera (Testbed)
     float cam[12] = {1, 0, 0, 0, -1, 0, 0, 0, -1, 0.5f, 0.5f, 2.0f};
@@ -482,8 +484,9 @@ void set_density_grid(sng_ctx* c, const uint16_t* grid, uint64_t n_cells) {
     c->d_partial.ensure(1024 * sizeof(double));
     c->d_mean.ensure(sizeof(float));
     c->d_bitfield.ensure((size_t)GRID_CELLS / 8 * N_CASCADES);
+    c->d_occ_linear.ensure((size_t)GRID_CELLS / 8);
     launch_bitfield(c->d_grid_f16.as<uint16_t>(), c->max_cascade, c->d_grid_f32.as<float>(), c->d_partial.as<double>(), c->d_mean.as<float>(),
-                    c->d_bitfield.as<uint8_t>(), c->s_nerf);
+                    c->d_bitfield.as<uint8_t>(), c->d_occ_linear.as<uint32_t>(), c->s_nerf);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->s_nerf));
     c->has_bitfield = true;
@@ -499,6 +502,8 @@ Volume make_volume(const sng_ctx* c) {
     v.max_mip = c->max_cascade;
     v.min_transmittance = (float)c->p("min_transmittance");
     v.bitfield = c->d_bitfield.as<uint8_t>();
+    v.occ_linear = c->d_occ_linear.as<uint32_t>();
+    v.linear = (c->max_cascade == 0 && c->cone <= 1e-5f && c->p("linear_marcher") != 0.0) ? 1 : 0;
     return v;
 }
 
@@ -778,6 +783,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                         c->acc_depth.as<float>(), c->s_rt);
     }
     HIPCHK(hipEventRecord(c->ev_rt1, c->s_rt));
+    if (c->p("concurrent_streams") == 0.0) HIPCHK(hipStreamWaitEvent(c->s_nerf, c->ev_rt1, 0));
 
     // ---- NeRF (Testbed::render SyNeRFgine overload, testbed.cu:4353-4404)
     HIPCHK(hipEventRecord(c->ev_nerf0, c->s_nerf));
@@ -819,7 +825,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf);
                 if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->net_events[2 * net_launches + 1], c->s_nerf));
                 ++net_launches;
-                launch_composite(vol, cam, rb[p], rb[p ^ 1], ctrl, p, target, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
+                launch_composite(vol, cam, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
                                  c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf);
                 p ^= 1;
             }
@@ -889,6 +895,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             out->n_reference_slots = c->h_ctrl->ref_slots;
             std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
             std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
+            std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
         }
         HIPCHK(hipEventElapsedTime(&out->ms_frame, c->ev_start, c->ev_end));
         HIPCHK(hipEventElapsedTime(&out->ms_raytrace, c->ev_rt0, c->ev_rt1));
@@ -941,7 +948,7 @@ void ctx_destroy(sng_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
-    for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
+    for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats})
         b->release();

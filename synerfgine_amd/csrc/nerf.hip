@@ -102,8 +102,16 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
 // generate_next_nerf_network_inputs (790-837), real samples only
 // coords: NerfCoordinate AoS {warp(pos), warp_dt(dt), warp(dir)} (nerf_device.cuh:176-202)
 // ---------------------------------------------------------------------------
+//
+// LIN (cone == 0, max_cascade == 0, the unit-cube scenes): the march is the exact linear
+// specialisation (advance_to_occupied_linear) and the loop is NOT unrolled -- the sample
+// distances of a ray go to LDS instead of 8 live registers, which keeps the kernel small
+// and at high occupancy (the DDA walk is latency bound: many waves in flight hide the
+// bitfield gathers).  The general path (cascades / cone stepping) keeps the unrolled form.
+template <bool LIN>
 __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                                                        float* __restrict__ coords, uint2* __restrict__ samp) {
+    __shared__ float ts_lds[LIN ? MAX_STEPS_BETWEEN_COMPACTION * 256 : 1];
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t i_step = ctrl->i_step[p];
     const bool active = n_alive > 0 && i_step < MARCH_ITER;
@@ -122,10 +130,11 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
     const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
+    const float cone = LIN ? 0.0f : vol.cone;
     for (uint32_t base_i = gw * 64; base_i < n_alive; base_i += n_waves * 64) {
         const uint32_t i = base_i + lane;
         uint32_t cnt = 0;
-        float ts[MAX_STEPS_BETWEEN_COMPACTION];
+        float ts[LIN ? 1 : MAX_STEPS_BETWEEN_COMPACTION];
         f3 o = splat(0.0f), d = splat(1.0f);
         if (i < n_alive) {
             float4 ot = rays.o_t[i], di = rays.d_idx[i];
@@ -133,14 +142,25 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
             d = mk(di.x, di.y, di.z);
             const f3 idir = inv(d);
             float t = ot.w;
+            if constexpr (LIN) {
+                const f3 hs = half_sign(d);
+#pragma unroll 1
+                for (; cnt < n_steps; ++cnt) {
+                    t = advance_to_occupied_linear(t, o, d, idir, hs, vol);
+                    if (t >= MAX_DEPTH) break;
+                    ts_lds[cnt * 256 + threadIdx.x] = t;
+                    t += calc_dt(t, 0.0f);
+                }
+            } else {
 #pragma unroll
-            for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
-                if (j < n_steps && cnt == j) {
-                    t = advance_to_occupied(t, vol.cone, o, d, idir, 0, vol.max_mip, vol);
-                    if (t < MAX_DEPTH) {
-                        ts[j] = t;
-                        t += calc_dt(t, vol.cone);
-                        ++cnt;
+                for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
+                    if (j < n_steps && cnt == j) {
+                        t = advance_to_occupied(t, cone, o, d, idir, 0, vol.max_mip, vol);
+                        if (t < MAX_DEPTH) {
+                            ts[j] = t;
+                            t += calc_dt(t, cone);
+                            ++cnt;
+                        }
                     }
                 }
             }
@@ -152,14 +172,25 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
         if (i < n_alive) {
             samp[i] = make_uint2(base, cnt);
             const f3 wd = (d + 1.0f) * 0.5f;
-#pragma unroll
-            for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
-                if (j < cnt) {
-                    const float t = ts[j];
-                    const float dt = calc_dt(t, vol.cone);
+            if constexpr (LIN) {
+#pragma unroll 1
+                for (uint32_t j = 0; j < cnt; ++j) {
+                    const float t = ts_lds[j * 256 + threadIdx.x];
+                    const float dt = calc_dt(t, 0.0f);
                     const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
                     float* c = coords + (size_t)(base + j) * 7;
                     c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+                }
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
+                    if (j < cnt) {
+                        const float t = ts[j];
+                        const float dt = calc_dt(t, cone);
+                        const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
+                        float* c = coords + (size_t)(base + j) * 7;
+                        c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+                    }
                 }
             }
         }
@@ -170,7 +201,7 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
 // composite_kernel_nerf_alt (476-575) + compaction into the next buffer
 // (compact_kernel_nerf 1830-1853) + extract_from_payload (1578-1612)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p, uint32_t target,
+__global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                                                         const float* __restrict__ coords, const uint2* __restrict__ samp,
                                                         const uint2* __restrict__ net_out, float4* __restrict__ frame_rgba,
                                                         float* __restrict__ frame_depth, float* __restrict__ positions) {
@@ -178,7 +209,10 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
     const uint32_t i_step = ctrl->i_step[p];
     const bool active = n_alive > 0 && i_step < MARCH_ITER;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (active) ctrl->total_samples += ctrl->n_samples[p];
+        if (active) {
+            ctrl->total_samples += ctrl->n_samples[p];
+            if (iter < 64) ctrl->samples_hist[iter] = ctrl->n_samples[p];
+        }
         ctrl->n_samples[p ^ 1] = 0;
     }
     if (!active) return;
@@ -333,6 +367,20 @@ __global__ void bitfield_max_pool_kernel(uint32_t n_elements, const uint8_t* __r
     next[morton3D(x, y, z)] |= bits;
 }
 
+// mip-0 occupancy as x-fastest bit rows: word (z*128 + y)*4 + x/32, bit x%32 == Morton bit (x,y,z).
+// Same bits, cheaper address math for the linear marcher.
+__global__ void bitfield_linear_kernel(const uint8_t* __restrict__ bf, uint32_t* __restrict__ occ) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= GRID_CELLS / 32) return;
+    const uint32_t z = w / (GRID_SIZE * GRID_SIZE / 32), y = (w / (GRID_SIZE / 32)) % GRID_SIZE, x0 = (w % (GRID_SIZE / 32)) * 32;
+    uint32_t bits = 0;
+    for (uint32_t b = 0; b < 32; ++b) {
+        const uint32_t m = morton3D(x0 + b, y, z);
+        bits |= (uint32_t)((bf[m >> 3] >> (m & 7)) & 1u) << b;
+    }
+    occ[w] = bits;
+}
+
 __global__ void ctrl_init_kernel(MarchCtrl* c) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         c->n_alive[0] = 0; c->n_alive[1] = 0;
@@ -355,19 +403,21 @@ void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl
 }
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
                      uint32_t blocks, hipStream_t s) {
-    hipLaunchKernelGGL(generate_kernel, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp);
+    if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp);
+    else hipLaunchKernelGGL(generate_kernel<false>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp);
 }
-void launch_composite(const Volume& v, const CamDev& cam, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target,
+void launch_composite(const Volume& v, const CamDev& cam, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                       const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
                       hipStream_t s) {
-    hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, s, v, cam, in, out, ctrl, p, target, coords, samp, net_out, fb, depth, pos);
+    hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, s, v, cam, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
 }
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
     if (!n) return;
     hipLaunchKernelGGL(normals_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, H, row0, row1, pos, nrm);
 }
-void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, hipStream_t s) {
+void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, uint32_t* occ_linear,
+                     hipStream_t s) {
     const uint32_t N = GRID_CELLS;
     const uint32_t n_cells = N * (max_cascade + 1);
     hipLaunchKernelGGL(half_to_float_kernel, dim3((n_cells + 255) / 256), dim3(256), 0, s, grid_f16, grid_f32, n_cells);
@@ -378,6 +428,7 @@ void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid
     for (uint32_t level = 1; level < N_CASCADES; ++level)
         hipLaunchKernelGGL(bitfield_max_pool_kernel, dim3((N / 64 + 255) / 256), dim3(256), 0, s, N / 64, bf + (size_t)N / 8 * (level - 1),
                            bf + (size_t)N / 8 * level);
+    hipLaunchKernelGGL(bitfield_linear_kernel, dim3(N / 32 / 256), dim3(256), 0, s, bf, occ_linear);
 }
 
 }  // namespace sng

@@ -69,6 +69,7 @@ __device__ __forceinline__ void encode_level(const LevelInfo& L, const _Float16*
             w *= (c & 1) ? f0 : 1.0f - f0;
             w *= (c & 2) ? f1 : 1.0f - f1;
             w *= (c & 4) ? f2 : 1.0f - f2;
+            asm volatile("" : "+v"(w));   // keep the f32 product rounded before the f16 cast (no v_fma_mix fusion): tcnn (T)weight
             _Float16 wh = (_Float16)w;
             h2 w2 = {wh, wh};
             h2 a = __builtin_bit_cast(h2, v[c].x), b = __builtin_bit_cast(h2, v[c].y);
@@ -87,6 +88,7 @@ __device__ __forceinline__ void encode_level(const LevelInfo& L, const _Float16*
             w *= (c & 1) ? f0 : 1.0f - f0;
             w *= (c & 2) ? f1 : 1.0f - f1;
             w *= (c & 4) ? f2 : 1.0f - f2;
+            asm volatile("" : "+v"(w));   // keep the f32 product rounded before the f16 cast (no v_fma_mix fusion): tcnn (T)weight
             _Float16 wh = (_Float16)w;
             h2 w2 = {wh, wh};
             r = __builtin_elementwise_fma(w2, __builtin_bit_cast(h2, v[c]), r);
@@ -212,8 +214,7 @@ __global__ __launch_bounds__(256) void hashgrid_encode_kernel(const float* __res
     if (s >= n) return;
     const float* c = coords + (size_t)s * stride;
     h8 e = encode_lane<F>(levels, grid, g, c[0], c[1], c[2]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) out[(size_t)s * 32 + g * 8 + j] = __builtin_bit_cast(uint16_t, e[j]);
+    *reinterpret_cast<h8*>(out + (size_t)s * 32 + g * 8) = e;   // 16-B store of the lane's 8 features
 }
 
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,

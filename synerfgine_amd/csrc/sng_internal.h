@@ -38,6 +38,7 @@ struct MarchCtrl {
     unsigned long long ref_slots;
     uint32_t alive_hist[64];
     uint32_t steps_hist[64];
+    uint32_t samples_hist[64];
 };
 
 // Alive-ray SoA buffer (NerfPayload + rgba + depth, nerf_device.cuh:145-153; nerf.h:22-42)
@@ -97,11 +98,12 @@ struct RaytraceArgs {
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, hipStream_t s);
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
                      uint32_t blocks, hipStream_t s);
-void launch_composite(const Volume& v, const CamDev& cam, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target,
+void launch_composite(const Volume& v, const CamDev& cam, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                       const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
                       hipStream_t s);
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s);
-void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, hipStream_t s);
+void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, uint32_t* occ_linear,
+                     hipStream_t s);
 void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s);
 // mesh.hip
 void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, hipStream_t s);

@@ -124,8 +124,18 @@ SNG_HD float unwarp_dt(float dt) {
     float max_stepsize = MIN_STEP * (1 << (N_CASCADES - 1));
     return dt * (max_stepsize - MIN_STEP) + MIN_STEP;
 }
+// x / d, correctly rounded, from y = RN(1/d): q0 = RN(x*y) plus one FMA remainder correction
+// (Markstein).  Verified bit-identical to IEEE division for every float t in [1e-9, 4e4] with
+// d = MIN_STEP and for 4e8 random (x, d) pairs (tools/divtest: 0 mismatches).
+SNG_HD float div_by(float x, float d, float y) {
+    const float q0 = x * y;
+    const float r = fmaf(-q0, d, x);
+    return fmaf(r, y, q0);
+}
+constexpr float INV_MIN_STEP = 1.0f / MIN_STEP;   // RN(1/MIN_STEP), folded at compile time
+
 SNG_HD float to_stepping_space(float t, float cone) {
-    if (cone <= 1e-5f) return t / MIN_STEP;
+    if (cone <= 1e-5f) return div_by(t, MIN_STEP, INV_MIN_STEP);   // == t / MIN_STEP
     float log1p_c = logf(1.0f + cone);
     float a = (logf(MIN_STEP) - logf(log1p_c)) / log1p_c;
     float b = (logf(MAX_STEP) - logf(log1p_c)) / log1p_c;
@@ -199,11 +209,43 @@ struct Volume {
     uint32_t max_mip;    // max_cascade
     float min_transmittance;
     const uint8_t* bitfield;
+    const uint32_t* occ_linear;  // mip-0 occupancy as x-fastest bit rows (same bits as the Morton bitfield)
+    int linear;                  // cone == 0 && max_mip == 0: the exact fast marcher applies
 };
 SNG_HD f3 to_local(const Volume& v, f3 p) { return v.to_local_identity ? p : mul(v.to_local, p); }
 
+// Exact specialisation of if_unoccupied_advance_to_next_occupied_voxel<false> for unit-cube
+// scenes (cone_angle_constant == 0, max_cascade == 0): every float operation of the general
+// path is kept (mip clamps to 0, scalbnf(.,0) is the identity, /128 is an exact *2^-7), only the
+// divisions by MIN_STEP use div_by and the Morton bitfield lookup uses an equivalent linear copy.
+SNG_HD bool occupied_linear(f3 pos, const uint32_t* occ) {
+    f3 q = ((pos - splat(0.5f)) + splat(0.5f)) * (float)GRID_SIZE;   // cascaded_grid_idx_at, mip 0
+    int ix = (int)q.x, iy = (int)q.y, iz = (int)q.z;
+    if (ix < 0 || ix >= (int)GRID_SIZE || iy < 0 || iy >= (int)GRID_SIZE || iz < 0 || iz >= (int)GRID_SIZE) return false;
+    return (occ[((uint32_t)iz * GRID_SIZE + (uint32_t)iy) * (GRID_SIZE / 32) + ((uint32_t)ix >> 5)] >> (ix & 31)) & 1u;
+}
+SNG_HD float advance_to_occupied_linear(float t, f3 o, f3 d, f3 idir, f3 hs /* 0.5*sign(d) */, const Volume& vol) {
+    while (true) {
+        const f3 pos = o + d * t;
+        if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) return MAX_DEPTH;
+        if (occupied_linear(pos, vol.occ_linear)) return t;
+        // advance_to_next_voxel(mip 0) with distance_to_next_voxel(res = 128)
+        const f3 p = (float)GRID_SIZE * (pos - 0.5f);
+        const float tx = (floorf(p.x + 0.5f + hs.x) - p.x) * idir.x;
+        const float ty = (floorf(p.y + 0.5f + hs.y) - p.y) * idir.y;
+        const float tz = (floorf(p.z + 0.5f + hs.z) - p.z) * idir.z;
+        const float dist = fmaxf(fminf(fminf(tx, ty), tz) * (1.0f / (float)GRID_SIZE), 0.0f);
+        const float t_target = t + dist;
+        const float ts = to_stepping_space(t, 0.0f);
+        const float tts = to_stepping_space(t_target, 0.0f);
+        t = (ts + ceilf(fmaxf(tts - ts, 0.5f))) * MIN_STEP;
+    }
+}
+SNG_HD f3 half_sign(f3 d) { return {0.5f * sgnf(d.x), 0.5f * sgnf(d.y), 0.5f * sgnf(d.z)}; }
+
 // if_unoccupied_advance_to_next_occupied_voxel<false>: nerf_device.cuh:462-495
 SNG_HD float advance_to_occupied(float t, float cone, f3 o, f3 d, f3 idir, uint32_t min_mip, uint32_t max_mip, const Volume& vol) {
+    if (vol.linear && vol.bitfield && min_mip == 0 && max_mip == 0 && cone <= 1e-5f) return advance_to_occupied_linear(t, o, d, idir, half_sign(d), vol);
     while (true) {
         f3 pos = o + d * t;
         if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) return MAX_DEPTH;

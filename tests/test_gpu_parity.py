@@ -77,7 +77,9 @@ def test_hashgrid_encode_bit_exact(tb, model, oracle_lib, n):
     tb.encode(dc.data_ptr(), 7, n, out.data_ptr())
     torch.cuda.synchronize()
     got = out.cpu().numpy()
-    assert np.array_equal(got.view(np.uint16), ref.view(np.uint16)), f"{np.sum(got != ref)} mismatching features"
+    bad = np.argwhere(got.view(np.uint16) != ref.view(np.uint16))
+    detail = [(int(i), int(f), c[i, :3].tolist(), float(got[i, f]), float(ref[i, f])) for i, f in bad[:6]]
+    assert len(bad) == 0, f"{len(bad)} mismatching features (sample, feature, pos, gpu, ref): {detail}"
 
 
 @pytest.mark.parametrize("n", [5, 16, 4096, 65539])
