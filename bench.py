@@ -76,23 +76,25 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
     from synerfgine_amd import scene as S
+    from synerfgine_amd import tiling as T
 
     tb, eng, eng_cfg = S.make_engine(args.config, device_id=local_rank, overrides={"concurrent_streams": 0} if args.serial_streams else None)
     res = eng.resolution()
     MW, MH = res["mesh"]
-    band = MH // world
-    rows = (rank * band, MH if rank == world - 1 else (rank + 1) * band)
+    rows = T.band_rows(MH, rank, world)
+    band = T.tile_height(MH, world)
     dev = torch.device("cuda", local_rank)
     stream = torch.cuda.current_stream(dev)
-    tile = torch.empty((band, MW, 4), dtype=torch.float32, device=dev)
+    tile = torch.zeros((band, MW, 4), dtype=torch.float32, device=dev)
     frame = torch.empty((world * band, MW, 4), dtype=torch.float32, device=dev) if world > 1 else None
 
     def step(collect):
         r = eng.frame(spp=0, reset=True, rows=rows if world > 1 else None, collect_kernel_times=collect)
         if world > 1:
-            off = rows[0] * MW * 16
-            tb._lib.sng_copy_device(tb.ctx, r.raw.d_final_rgba + off, tile.data_ptr(), band * MW * 16, stream.cuda_stream)
-            dist.all_gather_into_tensor(frame, tile)
+            n = (rows[1] - rows[0]) * MW * 16
+            if n:
+                tb._lib.sng_copy_device(tb.ctx, r.raw.d_final_rgba + rows[0] * MW * 16, tile.data_ptr(), n, stream.cuda_stream)
+            T.gather_bands(tile, frame)
         return r
 
     for _ in range(args.warmup):

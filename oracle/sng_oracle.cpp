@@ -817,8 +817,12 @@ uint32_t orc_xorwow_next(uint32_t state[6]) { return xorwow_next(state); }
 float orc_curand_uniform(uint32_t state[6]) { return curand_uniform(state); }
 void orc_xorwow_jump_steps_naive(uint32_t st[6], uint64_t steps) { for (uint64_t i = 0; i < steps; ++i) xorwow_next(st); }
 void orc_xorwow_jump_matrix(uint32_t st[6], uint32_t log2_steps) {
-    gf2_apply(xorwow_tables().step_pow[log2_steps], st, st);
-    st[5] += (uint32_t)((1ull << log2_steps) * 362437ull);
+    /* 0..63: M^(2^k) from step_pow; 67..98: the subsequence tables M^(2^67 * 2^(k-67)) */
+    const XorwowTables& T = xorwow_tables();
+    if (log2_steps < 64) gf2_apply(T.step_pow[log2_steps], st, st);
+    else if (log2_steps >= 67 && log2_steps < 99) gf2_apply(T.seq_pow[log2_steps - 67], st, st);
+    else return;
+    if (log2_steps < 32) st[5] += (uint32_t)((1ull << log2_steps) * 362437ull);   /* 2^k * 362437 == 0 mod 2^32 for k >= 32 */
 }
 
 uint32_t orc_grid_level_table(const orc_model* m, uint32_t* offsets, uint32_t* resolutions) {

@@ -109,7 +109,7 @@ void     orc_xorwow_init_many(uint64_t seed, uint32_t n, uint32_t* states /* n x
 uint32_t orc_xorwow_next(uint32_t state[6]);
 float    orc_curand_uniform(uint32_t state[6]);
 void     orc_xorwow_jump_steps_naive(uint32_t state[6], uint64_t steps); /* stepping (test helper) */
-void     orc_xorwow_jump_matrix(uint32_t state[6], uint32_t log2_steps);  /* M^(2^k) (test helper) */
+void     orc_xorwow_jump_matrix(uint32_t state[6], uint32_t log2_steps);  /* M^(2^k), k in 0..63 or 67..98 (test helper) */
 
 /* ---- network (A6-A8) ----------------------------------------------------- */
 uint32_t orc_grid_level_table(const orc_model* m, uint32_t* offsets /* L+1 */, uint32_t* resolutions /* L */);

@@ -316,7 +316,8 @@ const std::map<std::string, double>& default_params() {
         {"smooth_threshold", 1.0},              // sng_position_kernel_threshold (unused by the path)
         {"max_shadow_variance", 0.0},           // sng_shadow_depth_variance (unused by the path)
         {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
-        {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
+        {"linear_marcher", 1},
+        {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests                  // exact unit-cube fast path of the occupancy march
     };
     return d;
 }
@@ -552,6 +553,10 @@ void upload_scene(sng_ctx* c) {
         m3 msc = {mk(1.0f / o.scale, 0.0f / o.scale, 0.0f / o.scale), mk(0.0f / o.scale, 1.0f / o.scale, 0.0f / o.scale),
                   mk(0.0f / o.scale, 0.0f / o.scale, 1.0f / o.scale)};
         g.world_to_obj = mulm(msc, inverse3(o.rot));   // m_scale * m_rotate (triangle_bvh.cu:313-319)
+        float max_coord = 0.0f;
+        for (const BvhNode& n : o.nodes)
+            for (int k = 0; k < 3; ++k) max_coord = std::max(max_coord, std::max(std::fabs(n.lo[k]), std::fabs(n.hi[k])));
+        g.fast_slab = (c->p("fast_slab") != 0.0 && max_coord < SLAB_FAST_MAX_COORD) ? 1 : 0;
         og.push_back(g);
     }
     upload(c->d_objs, og.data(), og.size() * sizeof(ObjectGpu));
@@ -748,9 +753,11 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     const int halo_n = shadows ? radius : 0;
     const int nr0 = std::max(0, ny0 - halo_n), nr1 = std::min(NH, ny1 + halo_n);
     const int tr0 = std::max(0, nr0 - 2), tr1 = std::min(NH, nr1 + 2);
-    Volume vol = show_nerf ? make_volume(c) : Volume{};
-    if (!show_nerf) vol.bitfield = c->d_bitfield.as<uint8_t>();
-    if (!c->has_bitfield) { vol = Volume{}; vol.render_aabb = c->box; vol.train_aabb = c->box; vol.to_local_identity = 1; }
+    // the raytracer's NeRF shadow test uses the density bitfield whether or not the NeRF is shown
+    // (engine.cu:386-397 passes m_nerf.density_grid_bitfield unconditionally)
+    Volume vol{};
+    if (c->has_model && c->has_bitfield) vol = make_volume(c);
+    else { vol.render_aabb = c->box; vol.train_aabb = c->box; vol.to_local = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)}; vol.to_local_identity = 1; }
     const CamDev cam = cam_dev(c);
     const f2 sc = render_screen_center(c);
 
@@ -1122,6 +1129,7 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
         if (!default_params().count(k)) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
         c->params[k] = v;
         c->mesh_reset = true;
+        if (k == "fast_slab" && !c->objs.empty()) upload_scene(c);
     });
 }
 int sng_get_param(sng_ctx* c, const char* key, double* v) {

@@ -91,6 +91,16 @@ SNG_HD uint32_t morton3D_invert(uint32_t x) {
 
 // ---- AABB slab test: bounding_box.cuh:163-211 ---------------------------------
 struct aabb { f3 lo, hi; };
+// x / d, correctly rounded, from y = RN(1/d): q0 = RN(x*y) plus one FMA remainder correction
+// (Markstein).  Verified bit-identical to IEEE division for every float t in [1e-9, 4e4] with
+// d = MIN_STEP and for 4e8 random (x, d) pairs (tools/divtest: 0 mismatches).
+SNG_HD float div_by(float x, float d, float y) {
+    const float q0 = x * y;
+    const float r = fmaf(-q0, d, x);
+    return fmaf(r, y, q0);
+}
+constexpr float INV_MIN_STEP = 1.0f / MIN_STEP;   // RN(1/MIN_STEP), folded at compile time
+
 struct f2 { float x, y; };
 SNG_HD void fswap(float& a, float& b) { float t = a; a = b; b = t; }
 SNG_HD float aabb_entry(const aabb& b, f3 pos, f3 dir) {
@@ -111,6 +121,34 @@ SNG_HD float aabb_entry(const aabb& b, f3 pos, f3 dir) {
     if (tzmin > tmin) tmin = tzmin;
     return tmin;
 }
+// aabb_entry with each division x / dir_i evaluated as div_by(x, dir_i, 1/dir_i) -- bit-identical
+// to aabb_entry (Markstein correction, see div_by) provided no intermediate over/underflows, which
+// slab_fast_ok() guarantees for the ray and the host guarantees for the boxes (|coord| < 2^40).
+SNG_HD float aabb_entry_fast(const aabb& b, f3 pos, f3 dir, f3 y) {
+    const float FMAX = 3.402823466e+38f;
+    float tmin = div_by(b.lo.x - pos.x, dir.x, y.x);
+    float tmax = div_by(b.hi.x - pos.x, dir.x, y.x);
+    if (tmin > tmax) fswap(tmin, tmax);
+    float tymin = div_by(b.lo.y - pos.y, dir.y, y.y);
+    float tymax = div_by(b.hi.y - pos.y, dir.y, y.y);
+    if (tymin > tymax) fswap(tymin, tymax);
+    if (tmin > tymax || tymin > tmax) return FMAX;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = div_by(b.lo.z - pos.z, dir.z, y.z);
+    float tzmax = div_by(b.hi.z - pos.z, dir.z, y.z);
+    if (tzmin > tzmax) fswap(tzmin, tzmax);
+    if (tmin > tzmax || tzmin > tmax) return FMAX;
+    if (tzmin > tmin) tmin = tzmin;
+    return tmin;
+}
+constexpr float SLAB_FAST_MAX_COORD = 1099511627776.0f;   // 2^40
+SNG_HD bool slab_fast_ok(f3 pos, f3 dir) {
+    const float lo = 8.673617379884035e-19f /* 2^-60 */, hi = 1.152921504606846976e18f /* 2^60 */;
+    const float ax = fabsf(dir.x), ay = fabsf(dir.y), az = fabsf(dir.z);
+    return ax >= lo && ax <= hi && ay >= lo && ay <= hi && az >= lo && az <= hi && fabsf(pos.x) < SLAB_FAST_MAX_COORD &&
+           fabsf(pos.y) < SLAB_FAST_MAX_COORD && fabsf(pos.z) < SLAB_FAST_MAX_COORD;
+}
 SNG_HD bool aabb_contains(const aabb& b, f3 p) {
     return p.x >= b.lo.x && p.x <= b.hi.x && p.y >= b.lo.y && p.y <= b.hi.y && p.z >= b.lo.z && p.z <= b.hi.z;
 }
@@ -124,16 +162,6 @@ SNG_HD float unwarp_dt(float dt) {
     float max_stepsize = MIN_STEP * (1 << (N_CASCADES - 1));
     return dt * (max_stepsize - MIN_STEP) + MIN_STEP;
 }
-// x / d, correctly rounded, from y = RN(1/d): q0 = RN(x*y) plus one FMA remainder correction
-// (Markstein).  Verified bit-identical to IEEE division for every float t in [1e-9, 4e4] with
-// d = MIN_STEP and for 4e8 random (x, d) pairs (tools/divtest: 0 mismatches).
-SNG_HD float div_by(float x, float d, float y) {
-    const float q0 = x * y;
-    const float r = fmaf(-q0, d, x);
-    return fmaf(r, y, q0);
-}
-constexpr float INV_MIN_STEP = 1.0f / MIN_STEP;   // RN(1/MIN_STEP), folded at compile time
-
 SNG_HD float to_stepping_space(float t, float cone) {
     if (cone <= 1e-5f) return div_by(t, MIN_STEP, INV_MIN_STEP);   // == t / MIN_STEP
     float log1p_c = logf(1.0f + cone);
@@ -328,6 +356,7 @@ struct ObjectGpu {                                           // ObjectTransform 
     float scale;
     int mat_id;
     m3 world_to_obj;   // (I/scale) * inverse(rot), triangle_bvh.cu:313-319
+    int fast_slab;     // every BVH box coordinate < 2^40 in magnitude: aabb_entry_fast is exact
 };
 struct LightGpu { f3 pos; float intensity; float size; int type; };
 struct MaterialGpu { f3 ka, kd, ks; float n, rg, spec_angle; int type; };

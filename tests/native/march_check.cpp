@@ -1,0 +1,92 @@
+// Host-side checks of the product's exact fast paths (synerfgine_amd/csrc/sng_math.h), compiled
+// by tests/test_host_fastpaths.py with hipcc as plain host code (no GPU needed):
+//   1. div_by(x, d, RN(1/d)) == x / d bit for bit (random pairs + a sweep of t / MIN_STEP);
+//   2. advance_to_occupied_linear == the general advance_to_occupied (nerf_device.cuh:462-495) on
+//      cone == 0, max_mip == 0 volumes for random rays through a random occupancy grid;
+//   3. aabb_entry_fast == aabb_entry for random boxes and rays.
+#include "sng_math.h"
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+using namespace sng;
+static uint32_t bits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+static bool same(float a, float b) { return bits(a) == bits(b) || (a != a && b != b); }
+
+int main() {
+    std::mt19937 g(7);
+    long bad_div = 0, n_div = 0;
+    {
+        std::uniform_real_distribution<float> E(-30.f, 30.f), S(0.f, 1.f);
+        for (int i = 0; i < 4000000; ++i) {
+            float x = std::ldexp(S(g) + 0.5f, (int)E(g)) * (g() & 1 ? 1.f : -1.f);
+            float d = std::ldexp(S(g) + 0.5f, (int)E(g)) * (g() & 1 ? 1.f : -1.f);
+            volatile float y = 1.0f / d;
+            ++n_div;
+            if (!same(div_by(x, d, y), x / d)) ++bad_div;
+        }
+        float t = 1e-6f;
+        for (int i = 0; i < 4000000; ++i, t = std::nextafter(t, 1e9f) * 1.0000037f) {
+            ++n_div;
+            if (!same(div_by(t, MIN_STEP, INV_MIN_STEP), t / MIN_STEP)) ++bad_div;
+        }
+    }
+    // occupancy grid (Morton bitfield + its linear copy)
+    std::vector<uint8_t> bf(GRID_CELLS / 8 * N_CASCADES, 0);
+    for (uint32_t z = 0; z < 128; ++z)
+        for (uint32_t y = 0; y < 128; ++y)
+            for (uint32_t x = 0; x < 128; ++x) {
+                float dx = x - 64.f, dy = y - 60.f, dz = z - 70.f;
+                bool occ = (dx * dx + dy * dy + dz * dz < 1600.f && ((x / 4 + y / 4 + z / 4) % 3 == 0)) || (g() % 1000 == 0);
+                if (occ) { uint32_t m = morton3D(x, y, z); bf[m >> 3] |= 1u << (m & 7); }
+            }
+    std::vector<uint32_t> occ(GRID_CELLS / 32, 0);
+    for (uint32_t w = 0; w < GRID_CELLS / 32; ++w) {
+        uint32_t z = w / (128 * 4), y = (w / 4) % 128, x0 = (w % 4) * 32, b = 0;
+        for (uint32_t k = 0; k < 32; ++k) { uint32_t m = morton3D(x0 + k, y, z); b |= (uint32_t)((bf[m >> 3] >> (m & 7)) & 1) << k; }
+        occ[w] = b;
+    }
+    Volume v{};
+    v.render_aabb = {splat(0.f), splat(1.f)};
+    v.train_aabb = v.render_aabb;
+    v.to_local = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)};
+    v.to_local_identity = 1;
+    v.bitfield = bf.data();
+    v.occ_linear = occ.data();
+    std::uniform_real_distribution<float> U(-1, 1), U01(0, 1);
+    long bad_march = 0, n_march = 0, n_samples = 0;
+    for (int it = 0; it < 200000; ++it) {
+        f3 o = (it % 3 == 0) ? mk(U01(g), U01(g), U01(g)) : mk(U(g) * 2.f + 0.5f, U(g) * 2.f + 0.5f, U(g) * 2.f + 0.5f);
+        f3 d = normalize(mk(U(g), U(g), U(g)));
+        if (it % 17 == 0) d.x = 0.f;
+        if (it % 19 == 0) d = normalize(mk(0.f, 0.f, U(g)));
+        const f3 idir = inv(d);
+        float t0 = fmaxf(aabb_entry(v.render_aabb, o, d), 0.0f) + 1e-6f;
+        float ta = t0, tb = t0;
+        for (int s = 0; s < 12; ++s) {
+            v.linear = 0;
+            ta = advance_to_occupied(ta, 0.f, o, d, idir, 0, 0, v);
+            tb = advance_to_occupied_linear(tb, o, d, idir, half_sign(d), v);
+            ++n_march;
+            if (!same(ta, tb)) { ++bad_march; break; }
+            if (ta >= MAX_DEPTH) break;
+            ++n_samples;
+            const float dt = calc_dt(ta, 0.f);
+            ta += dt; tb += dt;
+        }
+    }
+    long bad_slab = 0, n_slab = 0;
+    for (int it = 0; it < 2000000; ++it) {
+        f3 a = mk(U(g), U(g), U(g)), b = mk(U(g), U(g), U(g));
+        aabb box = {mk(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z)), mk(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z))};
+        f3 o = mk(U(g) * 3.f, U(g) * 3.f, U(g) * 3.f);
+        f3 d = normalize(mk(U(g), U(g), U(g)));
+        if (it % 7 == 0) d = d * 37.5f;
+        if (!slab_fast_ok(o, d)) continue;
+        ++n_slab;
+        if (!same(aabb_entry_fast(box, o, d, inv(d)), aabb_entry(box, o, d))) ++bad_slab;
+    }
+    std::printf("{\"div\": [%ld, %ld], \"march\": [%ld, %ld, %ld], \"slab\": [%ld, %ld]}\n", n_div, bad_div, n_march, n_samples, bad_march,
+                n_slab, bad_slab);
+    return (bad_div || bad_march || bad_slab) ? 1 : 0;
+}

@@ -1,0 +1,67 @@
+"""Multi-process band tiling (the N>1 path of bench.py) on CPU with the gloo backend, world_size 2 and 3."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("height,world", [(1080, 1), (1080, 2), (1080, 8), (1080, 7), (64, 3), (5, 8), (1, 2)])
+def test_bands_cover_rows_once(height, world):
+    from synerfgine_amd.tiling import band_rows, tile_height
+    seen = np.zeros(height, np.int32)
+    th = tile_height(height, world)
+    for r in range(world):
+        r0, r1 = band_rows(height, r, world)
+        assert 0 <= r0 <= r1 <= height and r1 - r0 <= th
+        seen[r0:r1] += 1
+    assert (seen == 1).all()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from synerfgine_amd.tiling import band_rows, gather_bands, tile_height
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = np.load(os.path.join(HERE, "golden", "frame_nerf_64.npz"))["rgba"]   # oracle-rendered 64x64 frame
+        H, W, C = full.shape
+        r0, r1 = band_rows(H, rank, world)
+        th = tile_height(H, world)
+        tile = torch.zeros((th, W, C), dtype=torch.float32)
+        tile[: r1 - r0] = torch.from_numpy(full[r0:r1])        # this rank's band, as sng_render_frame(rows) leaves it
+        frame = torch.empty((world * th, W, C), dtype=torch.float32)
+        gather_bands(tile, frame)
+        ok = bool(np.array_equal(frame[:H].numpy(), full))
+        t = torch.tensor([1.0 if ok else 0.0])
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)                # same reduction bench.py uses for timing
+        q.put((rank, ok, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_band_gather_reassembles_frame(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok and agree == 1.0 for _, ok, agree in res)

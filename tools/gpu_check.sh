@@ -12,5 +12,5 @@ run() {  # name timeout cmd...
   return 0
 }
 run smoke 400 python __graft_entry__.py smoke
-run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS}
+run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ${PYTEST_K:+-k "$PYTEST_K"}
 run bench 400 python bench.py --steps 10 --warmup 2 ${BENCH_ARGS}
