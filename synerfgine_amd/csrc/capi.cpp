@@ -317,7 +317,9 @@ const std::map<std::string, double>& default_params() {
         {"max_shadow_variance", 0.0},           // sng_shadow_depth_variance (unused by the path)
         {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
         {"linear_marcher", 1},
-        {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests                  // exact unit-cube fast path of the occupancy march
+        {"fast_slab", 1},
+        {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
+        {"rt_queue_gb", 48},                    // device-memory budget for those queues                       // exact reciprocal-multiply BVH box tests                  // exact unit-cube fast path of the occupancy march
     };
     return d;
 }
@@ -369,6 +371,7 @@ struct sng_ctx {
     DevBuf samp, coords, net_out, ctrl;
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
+    DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count;   // deferred-shadow raytracer queues
     DevBuf rng_nerf, rng_mesh;
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
     DevBuf d_seq;
@@ -786,8 +789,33 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         ra.lens = (float)c->p("lens_size");
         ra.show_nerf_shadow = c->p("shadow_on_virtual_obj") != 0.0;
         ra.syn_shadow_factor = (float)c->p("syn_shadow_intensity");
-        launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
-                        c->acc_depth.as<float>(), c->s_rt);
+        // deferred shadow rays (wavefront) whenever the path has point-light shadow tests and the
+        // worst-case queues (every pixel hits on every sample and bounce) fit the budget
+        uint32_t n_point = 0;
+        for (auto& l : c->lights) n_point += l.type == 0 ? 1u : 0u;
+        const uint64_t n_px = (uint64_t)(y1 - y0) * (uint64_t)MW;
+        const uint64_t cap = n_px * ra.samples * ra.bounces;
+        RtQueue q{};
+        q.nls = (uint32_t)c->lights.size() * ra.shadow_iters;
+        q.nps = n_point * ra.shadow_iters;
+        q.rec_stride = 2 + (3 * q.nls + 3) / 4;
+        const uint64_t bytes = cap * (16ull * q.rec_stride + 32ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
+        const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
+                               bytes <= (uint64_t)(c->p("rt_queue_gb") * 1073741824.0);
+        if (wavefront) {
+            c->rt_rec.ensure(cap * 16ull * q.rec_stride);
+            c->rt_srec.ensure(cap * 32ull * q.nps);
+            c->rt_mask.ensure(cap * 4ull * q.nps);
+            c->rt_head.ensure((uint64_t)MW * MH * 4);
+            c->rt_count.ensure(16);
+            q.rec = c->rt_rec.as<float4>(); q.srec = c->rt_srec.as<float4>(); q.mask = c->rt_mask.as<float>();
+            q.head = c->rt_head.as<int>(); q.count = c->rt_count.as<uint32_t>(); q.cap = (uint32_t)cap;
+            launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
+                                      c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), (uint32_t)c->n_cus * 16, c->s_rt);
+        } else {
+            launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
+                            c->acc_depth.as<float>(), c->s_rt);
+        }
     }
     HIPCHK(hipEventRecord(c->ev_rt1, c->s_rt));
     if (c->p("concurrent_streams") == 0.0) HIPCHK(hipStreamWaitEvent(c->s_nerf, c->ev_rt1, 0));
@@ -957,7 +985,7 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats})
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end}) (void)hipEventDestroy(e);

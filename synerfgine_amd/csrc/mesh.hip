@@ -25,6 +25,16 @@ struct Stack {
     __device__ __forceinline__ int pop() { --n; return base[n * TPB]; }
 };
 
+// one slot per active lane from a device counter, one atomic per wave
+__device__ __forceinline__ uint32_t wave_alloc(uint32_t* counter, int lane) {
+    const unsigned long long mask = __ballot(1);
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader, 64);
+    return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
 __device__ __forceinline__ float tri_intersect(const Tri& tr, f3 ro, f3 rd) {   // triangle.cuh:45-59
     const f3 v1v0 = tr.b - tr.a, v2v0 = tr.c - tr.a, rov0 = ro - tr.a;
     const f3 n = cross(v1v0, v2v0);
@@ -42,10 +52,10 @@ __device__ __forceinline__ float tri_intersect(const Tri& tr, f3 ro, f3 rd) {   
 // object allow it, which removes 12 IEEE divisions per interior node without changing a bit.
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __restrict__ nodes, const Tri* __restrict__ tris, int* stack_lds,
-                                          int& tri_out) {
+                                          int& tri_out, float t_max) {
     Stack st{stack_lds, 0};
     st.push(0);
-    float mint = MAX_DEPTH;
+    float mint = t_max;
     int shortest = -1;
     while (st.n > 0) {
         const int idx = st.pop();
@@ -73,25 +83,28 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
     tri_out = shortest;
     return mint;
 }
+// t_max < MAX_DEPTH culls everything at or beyond t_max (the result is then min(closest, t_max));
+// only the shadow kernel uses it, where any value >= full_dist yields the same mask.
 __device__ float bvh_intersect(f3 ro, f3 rd, const BvhNode* __restrict__ nodes, const Tri* __restrict__ tris, int* stack_lds, int& tri_out,
-                               bool fast_obj) {
-    if (fast_obj && slab_fast_ok(ro, rd)) return bvh_walk<true>(ro, rd, inv(rd), nodes, tris, stack_lds, tri_out);
-    return bvh_walk<false>(ro, rd, rd, nodes, tris, stack_lds, tri_out);
+                               bool fast_obj, float t_max = MAX_DEPTH) {
+    if (fast_obj && slab_fast_ok(ro, rd)) return bvh_walk<true>(ro, rd, inv(rd), nodes, tris, stack_lds, tri_out, t_max);
+    return bvh_walk<false>(ro, rd, rd, nodes, tris, stack_lds, tri_out, t_max);
 }
 
-__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, int* stack, int& tri) {
+__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, int* stack, int& tri, float t_max = MAX_DEPTH) {
     const f3 oro = mul(o.world_to_obj, ro - o.pos);
     const f3 ord = mul(o.world_to_obj, rd);
-    return bvh_intersect(oro, ord, o.nodes, o.tris, stack, tri, o.fast_slab != 0);
+    return bvh_intersect(oro, ord, o.nodes, o.tris, stack, tri, o.fast_slab != 0, t_max);
 }
 
 // sng::depth_test_world (common.cu:36-48)
-__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, int* stack, int& out_obj) {
+__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, int* stack, int& out_obj,
+                                  float t_max = MAX_DEPTH) {
     float depth = MAX_DEPTH;
     const f3 off = origin + dir * MIN_DEPTH;
     for (int c = 0; c < n_objs; ++c) {
         int tri;
-        const float t = object_intersect(off, dir, objs[c], stack, tri);
+        const float t = object_intersect(off, dir, objs[c], stack, tri, t_max);
         if (t < depth && t > MIN_DEPTH) { out_obj = c; depth = t; }
     }
     return depth;
@@ -246,19 +259,29 @@ __device__ __forceinline__ f3 cone_random_frame(f3 orig, const m3& frame, float 
     const f3 off = mk(cosf(longi) * sinf(latid), sinf(longi) * sinf(latid), cosf(longi));
     return orig + mul(frame, off);
 }
-__global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, const float4* __restrict__ origins, const float4* __restrict__ dirs,
-                                                        uint32_t* __restrict__ rng, uint32_t n_rng, float4* __restrict__ acc_rgba,
-                                                        float* __restrict__ acc_depth) {
+//
+// DEFER = false: the whole path per pixel in one kernel (reference structure).
+// DEFER = true : the same path and RNG sequence, but every point-light shadow test is written to
+//                a shadow-ray queue and the light colours to a hit record; shadow_rays_kernel
+//                traces the queue with every lane busy, and rt_accumulate_kernel replays the
+//                colour sums in the original order.  Bit-identical to DEFER = false.
+template <bool DEFER>
+__global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, RtQueue q, const float4* __restrict__ origins,
+                                                        const float4* __restrict__ dirs, uint32_t* __restrict__ rng, uint32_t n_rng,
+                                                        float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
     __shared__ int stack_lds[BVH_STACK * TPB];
     int* stack = stack_lds + threadIdx.x;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (t >= n) return;
     const size_t i = (size_t)a.row0 * a.W + t;
+    const int lane = threadIdx.x & 63;
     Xorwow r = load_rng(rng, n_rng, i);
     const float4 o4 = origins[i], d4 = dirs[i];
     const f3 src_p = mk(o4.x, o4.y, o4.z), src_d = mk(d4.x, d4.y, d4.z);
     f3 shade = splat(0.0f), next_pos = splat(0.0f);
+    int prev_rec = -1;
+    if (DEFER) q.head[i] = -1;
     for (uint32_t spp = 0; spp < a.samples; ++spp) {
         const float longi = curand_uniform(r) * a.lens;
         const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
@@ -273,9 +296,22 @@ __global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, const flo
             // shade_object (raytracer.cu:6-57)
             const MaterialGpu m = a.mats[h.mat];
             f3 color = splat(0.0f);
+            uint32_t k = 0;
+            float* lc_out = nullptr;
+            if (DEFER) {
+                k = wave_alloc(q.count, lane);
+                float4* rk = q.rec + (size_t)k * q.rec_stride;
+                rk[0] = make_float4(__int_as_float(-1), __uint_as_float(spp), __int_as_float(h.mat), 0.0f);
+                rk[1] = make_float4(pdf, att, 0.0f, 0.0f);
+                lc_out = reinterpret_cast<float*>(rk + 2);
+                if (prev_rec < 0) q.head[i] = (int)k;
+                else reinterpret_cast<int*>(q.rec + (size_t)prev_rec * q.rec_stride)[0] = (int)k;
+                prev_rec = (int)k;
+            }
+            uint32_t jl = 0, jp = 0;
             for (int l = 0; l < a.n_lights; ++l) {
                 const LightGpu L = a.lights[l];
-                for (uint32_t s = 0; s < a.shadow_iters; ++s) {
+                for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
                     const f3 lpos = light_sample(L, r);
                     f3 Lv = lpos - h.pos;
                     const float full_dist = length(Lv);
@@ -283,7 +319,15 @@ __global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, const flo
                     const f3 R = reflect(Lv, h.normal);
                     const f3 V = normalize(-rd);
                     const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
-                    if (L.type == 0) {
+                    if (DEFER) {
+                        lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
+                        if (L.type == 0) {
+                            float4* sr = q.srec + 2 * ((size_t)k * q.nps + jp);
+                            sr[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, full_dist);
+                            sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
+                            ++jp;
+                        }
+                    } else if (L.type == 0) {
                         float mask = 1.0f;
                         const f3 invL = inv(Lv);
                         int oh = -1;
@@ -299,30 +343,94 @@ __global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, const flo
                     }
                 }
             }
-            color = color / (float)a.shadow_iters;
-            color = color + m.ka;
+            if (!DEFER) {
+                color = color / (float)a.shadow_iters;
+                color = color + m.ka;
+            }
             // Material::scatter (material.cuh:112-123)
             const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
             const float lo = curand_uniform(r) * spec;
             const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
             const f3 ndir = cone_random_frame(h.normal, h.perturb, lo, la);
-            shade_s = shade_s + color * pdf * att;
+            if (!DEFER) shade_s = shade_s + color * pdf * att;
             rp = h.pos;
             rd = ndir;
             pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
             att = 1.0f * m.rg;
         }
-        shade = shade + shade_s;
+        if (!DEFER) shade = shade + shade_s;
     }
     const float weight = (float)a.samples;
     next_pos = next_pos / weight;
-    shade = shade / weight;
     acc_depth[i] = dot(src_d, next_pos - src_p);
+    if (!DEFER) {
+        shade = shade / weight;
+        float4 cur = acc_rgba[i];
+        const f3 curr = mk(cur.x, cur.y, cur.z);
+        if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
+        acc_rgba[i] = make_float4(shade.x, shade.y, shade.z, cur.w);
+    }
+    store_rng(rng, n_rng, i, r);
+}
+
+// Shadow rays of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
+// mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
+// the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
+// depend on its cap syn + 1 >= full_dist), so the result is bit-identical.
+__global__ __launch_bounds__(TPB) void shadow_rays_kernel(RaytraceArgs a, RtQueue q) {
+    __shared__ int stack_lds[BVH_STACK * TPB];
+    int* stack = stack_lds + threadIdx.x;
+    const uint32_t total = *q.count * q.nps;
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
+        const float4 s0 = q.srec[2 * (size_t)j], s1 = q.srec[2 * (size_t)j + 1];
+        const f3 pos = mk(s0.x, s0.y, s0.z), Lv = mk(s1.x, s1.y, s1.z);
+        const float full_dist = s0.w;
+        int oh = -1;
+        const float syn = depth_test_world(pos, Lv, a.objs, a.n_objs, stack, oh, full_dist);
+        const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip);
+        const float sh = fminf(fminf(nerf, syn), full_dist);
+        q.mask[j] = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
+    }
+}
+
+// Colour replay of the deferred raytracer, in raytrace_kernel's exact float order.
+__global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQueue q, float4* __restrict__ acc_rgba) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (t >= n) return;
+    const size_t i = (size_t)a.row0 * a.W + t;
+    int k = q.head[i];
+    f3 shade = splat(0.0f);
+    for (uint32_t spp = 0; spp < a.samples; ++spp) {
+        f3 shade_s = splat(0.0f);
+        while (k >= 0) {
+            const float4* rk = q.rec + (size_t)k * q.rec_stride;
+            const float4 h0 = rk[0], h1 = rk[1];
+            if (__float_as_uint(h0.y) != spp) break;
+            const float* lc = reinterpret_cast<const float*>(rk + 2);
+            const float* mk_ = q.mask + (size_t)k * q.nps;
+            f3 color = splat(0.0f);
+            uint32_t jl = 0, jp = 0;
+            for (int l = 0; l < a.n_lights; ++l) {
+                const bool point = a.lights[l].type == 0;
+                for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
+                    const f3 c = mk(lc[3 * jl], lc[3 * jl + 1], lc[3 * jl + 2]);
+                    if (point) color = color + c * mk_[jp++];
+                    else color = color + c;
+                }
+            }
+            color = color / (float)a.shadow_iters;
+            color = color + a.mats[__float_as_int(h0.z)].ka;
+            shade_s = shade_s + color * h1.x * h1.y;
+            k = __float_as_int(h0.x);
+        }
+        shade = shade + shade_s;
+    }
+    shade = shade / (float)a.samples;
     float4 cur = acc_rgba[i];
     const f3 curr = mk(cur.x, cur.y, cur.z);
     if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
     acc_rgba[i] = make_float4(shade.x, shade.y, shade.z, cur.w);
-    store_rng(rng, n_rng, i, r);
 }
 
 // ---------------------------------------------------------------------------
@@ -390,7 +498,16 @@ void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, ui
                      hipStream_t s) {
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
-    hipLaunchKernelGGL(raytrace_kernel, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, a, o, d, rng, n_rng, acc, accd);
+    hipLaunchKernelGGL(raytrace_kernel<false>, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, a, RtQueue{}, o, d, rng, n_rng, acc, accd);
+}
+void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
+                               float* accd, uint32_t shadow_blocks, hipStream_t s) {
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (!n) return;
+    (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);   // errors surface through hipGetLastError in the caller
+    hipLaunchKernelGGL(raytrace_kernel<true>, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, a, q, o, d, rng, n_rng, acc, accd);
+    hipLaunchKernelGGL(shadow_rays_kernel, dim3(shadow_blocks), dim3(TPB), 0, s, a, q);
+    hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc);
 }
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
                     const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s) {

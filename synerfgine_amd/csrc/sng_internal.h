@@ -94,6 +94,22 @@ struct RaytraceArgs {
     float syn_shadow_factor;
 };
 
+// Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
+// sample, bounce) that hit an object: header {next, spp, mat, -} {pdf, att, -, -} + the light
+// colour lc of every (light, shadow iteration) in loop order.  One "shadow ray" per point-light
+// sample: {pos, full_dist} {L, -}; its mask is written by the shadow kernel.
+struct RtQueue {
+    float4* rec;          // cap x rec_stride float4
+    float4* srec;         // cap x nps x 2 float4
+    float* mask;          // cap x nps
+    int* head;            // per mesh pixel: first hit record or -1
+    uint32_t* count;      // hit records allocated (device counter)
+    uint32_t rec_stride;  // float4 per hit record = 2 + ceil(3 * nls / 4)
+    uint32_t nls;         // n_lights * shadow_iters
+    uint32_t nps;         // n_point_lights * shadow_iters
+    uint32_t cap;
+};
+
 // nerf.hip
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, hipStream_t s);
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
@@ -109,6 +125,8 @@ void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s);
 void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, hipStream_t s);
 void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
                       hipStream_t s);
+void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
+                               float* accd, uint32_t shadow_blocks, hipStream_t s);
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
                      hipStream_t s);
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,

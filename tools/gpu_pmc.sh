@@ -1,0 +1,11 @@
+#!/bin/bash
+# HBM traffic of the hot kernels: two separate PMC passes (FETCH_SIZE, WRITE_SIZE), kernel trace only,
+# then tools/pmc_summary.py -> profiles/pmc_network_r01.json.  Run from the repo root on the GPU box.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/pmc
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 400 rocprofv3 --pmc $c -d gpurun_out/pmc/$c -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --serial-streams > gpurun_out/pmc/$c.log 2>&1
+  rc=$?; echo "$c rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/pmc/$c.log; exit $rc; }
+done
+python3 tools/pmc_summary.py gpurun_out/pmc profiles/pmc_network_r01.json

@@ -1,0 +1,57 @@
+"""Per-launch HBM bytes of the hot kernels from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB.  MI355X_MICROARCH.md (HBM [CDNA4]):
+on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads -> x2; WRITE_SIZE is exact for
+16-B-per-lane stores.  half_to_float_kernel (reads 2 B, writes 4 B per density-grid cell, 128^3
+cells, runs once per model load) is reported beside as a calibration point.
+usage: python tools/pmc_summary.py <pmc dir> <out.json>
+"""
+import csv
+import glob
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def short(n):
+    return re.sub(r"\(.*", "", n).replace("void ", "").replace("sng::", "")
+
+
+def load(d, counter):
+    f = glob.glob(f"{d}/{counter}/**/*counter_collection.csv", recursive=True)
+    if not f:
+        raise SystemExit(f"no counter_collection.csv for {counter}")
+    per = defaultdict(list)
+    for r in csv.DictReader(open(f[0])):
+        if r.get("Counter_Name", counter) != counter:
+            continue
+        per[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    d, out = sys.argv[1], sys.argv[2]
+    fetch, write = load(d, "FETCH_SIZE"), load(d, "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k, []), write.get(k, [])
+        fa = sum(f) / len(f) if f else 0.0
+        wa = sum(w) / len(w) if w else 0.0
+        kernels[k] = {"launches": len(f), "fetch_kib_raw_avg": fa, "write_kib_avg": wa,
+                      "hbm_bytes_per_launch": 2.0 * fa * 1024 + wa * 1024}
+    net = [k for k in kernels if "nerf_network_kernel" in k]
+    res = {"note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes; averages over all launches of bench.py --steps 3 --warmup 1 --serial-streams",
+           "kernel": net[0] if net else None,
+           "hbm_bytes_per_launch": kernels[net[0]]["hbm_bytes_per_launch"] if net else None,
+           "calibration_half_to_float": dict(kernels.get("half_to_float_kernel", {}), expected_read_bytes=2 * 128 ** 3,
+                                             expected_write_bytes=4 * 128 ** 3),
+           "kernels": kernels}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+    for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * max(1, kv[1]["launches"]))[:12]:
+        print(f"{k[:60]:60s} n={v['launches']:4d} fetch={v['fetch_kib_raw_avg']:12.1f}KiB write={v['write_kib_avg']:12.1f}KiB")
+
+
+if __name__ == "__main__":
+    main()
