@@ -147,6 +147,24 @@ __device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restri
 // sng::depth_test_nerf (common.cu:69-83)
 __device__ float depth_test_nerf(float full_d, uint32_t n_steps, const Volume& vol, f3 src, f3 L, f3 invL, uint32_t min_mip, uint32_t max_mip) {
     float s = 0.0f;
+    if (vol.linear && vol.bitfield && min_mip == 0 && max_mip == 0 && vol.cone <= 1e-5f) {
+        // the same march flattened into one loop (one DDA step or one sample per trip), see generate_kernel
+        const f3 hs = half_sign(L);
+        uint32_t j = 0;
+        while (j < n_steps) {
+            const f3 pos = src + L * s;
+            const bool out = s >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos));
+            if (out || occupied_linear(pos, vol.occ_linear)) {
+                if (out) s = MAX_DEPTH;
+                if (s >= full_d) { s = full_d; break; }
+                s += calc_dt(s, 0.0f);
+                ++j;
+            } else {
+                s = dda_step_linear(s, pos, invL, hs);
+            }
+        }
+        return s;
+    }
     for (uint32_t j = 0; j < n_steps; ++j) {
         s = advance_to_occupied(s, vol.cone, src, L, invL, min_mip, max_mip, vol);
         if (s >= full_d) { s = full_d; break; }

@@ -143,13 +143,21 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
             const f3 idir = inv(d);
             float t = ot.w;
             if constexpr (LIN) {
+                // advance_to_occupied_linear + sample, flattened into ONE loop: each trip either
+                // records a sample (occupied voxel) or takes one DDA step, so a lane's cost is its
+                // own total step count instead of the wave's worst walk summed over all 8 samples.
                 const f3 hs = half_sign(d);
 #pragma unroll 1
-                for (; cnt < n_steps; ++cnt) {
-                    t = advance_to_occupied_linear(t, o, d, idir, hs, vol);
-                    if (t >= MAX_DEPTH) break;
-                    ts_lds[cnt * 256 + threadIdx.x] = t;
-                    t += calc_dt(t, 0.0f);
+                while (cnt < n_steps) {
+                    const f3 pos = o + d * t;
+                    if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
+                    if (occupied_linear(pos, vol.occ_linear)) {
+                        ts_lds[cnt * 256 + threadIdx.x] = t;
+                        t += calc_dt(t, 0.0f);
+                        ++cnt;
+                    } else {
+                        t = dda_step_linear(t, pos, idir, hs);
+                    }
                 }
             } else {
 #pragma unroll

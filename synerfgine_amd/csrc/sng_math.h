@@ -252,21 +252,24 @@ SNG_HD bool occupied_linear(f3 pos, const uint32_t* occ) {
     if (ix < 0 || ix >= (int)GRID_SIZE || iy < 0 || iy >= (int)GRID_SIZE || iz < 0 || iz >= (int)GRID_SIZE) return false;
     return (occ[((uint32_t)iz * GRID_SIZE + (uint32_t)iy) * (GRID_SIZE / 32) + ((uint32_t)ix >> 5)] >> (ix & 31)) & 1u;
 }
+// advance_to_next_voxel(mip 0) with distance_to_next_voxel(res = 128), cone == 0
+SNG_HD float dda_step_linear(float t, f3 pos, f3 idir, f3 hs /* 0.5*sign(d) */) {
+    const f3 p = (float)GRID_SIZE * (pos - 0.5f);
+    const float tx = (floorf(p.x + 0.5f + hs.x) - p.x) * idir.x;
+    const float ty = (floorf(p.y + 0.5f + hs.y) - p.y) * idir.y;
+    const float tz = (floorf(p.z + 0.5f + hs.z) - p.z) * idir.z;
+    const float dist = fmaxf(fminf(fminf(tx, ty), tz) * (1.0f / (float)GRID_SIZE), 0.0f);
+    const float t_target = t + dist;
+    const float ts = to_stepping_space(t, 0.0f);
+    const float tts = to_stepping_space(t_target, 0.0f);
+    return (ts + ceilf(fmaxf(tts - ts, 0.5f))) * MIN_STEP;
+}
 SNG_HD float advance_to_occupied_linear(float t, f3 o, f3 d, f3 idir, f3 hs /* 0.5*sign(d) */, const Volume& vol) {
     while (true) {
         const f3 pos = o + d * t;
         if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) return MAX_DEPTH;
         if (occupied_linear(pos, vol.occ_linear)) return t;
-        // advance_to_next_voxel(mip 0) with distance_to_next_voxel(res = 128)
-        const f3 p = (float)GRID_SIZE * (pos - 0.5f);
-        const float tx = (floorf(p.x + 0.5f + hs.x) - p.x) * idir.x;
-        const float ty = (floorf(p.y + 0.5f + hs.y) - p.y) * idir.y;
-        const float tz = (floorf(p.z + 0.5f + hs.z) - p.z) * idir.z;
-        const float dist = fmaxf(fminf(fminf(tx, ty), tz) * (1.0f / (float)GRID_SIZE), 0.0f);
-        const float t_target = t + dist;
-        const float ts = to_stepping_space(t, 0.0f);
-        const float tts = to_stepping_space(t_target, 0.0f);
-        t = (ts + ceilf(fmaxf(tts - ts, 0.5f))) * MIN_STEP;
+        t = dda_step_linear(t, pos, idir, hs);
     }
 }
 SNG_HD f3 half_sign(f3 d) { return {0.5f * sgnf(d.x), 0.5f * sgnf(d.y), 0.5f * sgnf(d.z)}; }
