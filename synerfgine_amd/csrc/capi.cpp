@@ -318,7 +318,8 @@ const std::map<std::string, double>& default_params() {
         {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
         {"linear_marcher", 1},
         {"fast_slab", 1},
-        {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
+        {"rt_wavefront", 1},
+        {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit                    // deferred shadow-ray queues for the path tracer
         {"rt_queue_gb", 48},                    // device-memory budget for those queues                       // exact reciprocal-multiply BVH box tests                  // exact unit-cube fast path of the occupancy march
     };
     return d;
@@ -371,7 +372,7 @@ struct sng_ctx {
     DevBuf samp, coords, net_out, ctrl;
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
-    DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count;   // deferred-shadow raytracer queues
+    DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rng_nerf, rng_mesh;
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
     DevBuf d_seq;
@@ -384,6 +385,8 @@ struct sng_ctx {
     std::vector<sng_light> lights;
     std::vector<sng_material> mats;
     DevBuf d_objs, d_lights, d_mats;
+    DevBuf d_scene_blob;          // every object's nodes + triangles (traversal kernels copy it to LDS)
+    uint32_t scene_f4 = 0, bvh_depth = 0;
     bool scene_dirty = true;
 
     double p(const char* k) const { return params.at(k); }
@@ -541,8 +544,29 @@ std::string read_file(const std::string& p) {
 }
 bool file_exists(const std::string& p) { std::ifstream f(p); return (bool)f; }
 
+// depth of a BVH built by build_bvh (root depth 0)
+uint32_t bvh_depth(const std::vector<BvhNode>& nodes) {
+    std::vector<uint32_t> d(nodes.size(), 0);
+    uint32_t m = 0;
+    for (size_t i = 0; i < nodes.size(); ++i)
+        if (nodes[i].left >= 0) {
+            d[nodes[i].left] = d[nodes[i].left + 1] = d[i] + 1;
+            m = std::max(m, d[i] + 1);
+        }
+    return m;
+}
+
 void upload_scene(sng_ctx* c) {
     std::vector<ObjectGpu> og;
+    // scene blob: per object [nodes][triangles], each array 16-B aligned
+    std::vector<uint8_t> blob;
+    auto append = [&](const void* p, size_t bytes) {
+        const size_t off = blob.size();
+        blob.resize((off + bytes + 15) / 16 * 16, 0);
+        std::memcpy(blob.data() + off, p, bytes);
+        return (uint32_t)off;
+    };
+    c->bvh_depth = 0;
     for (auto& o : c->objs) {
         upload(o.d_nodes, o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
         upload(o.d_tris, o.tris.data(), o.tris.size() * sizeof(Tri));
@@ -560,9 +584,15 @@ void upload_scene(sng_ctx* c) {
         for (const BvhNode& n : o.nodes)
             for (int k = 0; k < 3; ++k) max_coord = std::max(max_coord, std::max(std::fabs(n.lo[k]), std::fabs(n.hi[k])));
         g.fast_slab = (c->p("fast_slab") != 0.0 && max_coord < SLAB_FAST_MAX_COORD) ? 1 : 0;
+        g.lds_nodes = append(o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
+        g.lds_tris = append(o.tris.data(), o.tris.size() * sizeof(Tri));
+        c->bvh_depth = std::max(c->bvh_depth, bvh_depth(o.nodes));
         og.push_back(g);
     }
     upload(c->d_objs, og.data(), og.size() * sizeof(ObjectGpu));
+    if (blob.empty()) blob.resize(16, 0);
+    upload(c->d_scene_blob, blob.data(), blob.size());
+    c->scene_f4 = (uint32_t)(blob.size() / 16);
     std::vector<LightGpu> lg;
     for (auto& l : c->lights) lg.push_back({mk(l.pos[0], l.pos[1], l.pos[2]), l.intensity, l.size, l.type});
     upload(c->d_lights, lg.data(), lg.size() * sizeof(LightGpu));
@@ -789,6 +819,14 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         ra.lens = (float)c->p("lens_size");
         ra.show_nerf_shadow = c->p("shadow_on_virtual_obj") != 0.0;
         ra.syn_shadow_factor = (float)c->p("syn_shadow_intensity");
+        ra.scene_blob = c->d_scene_blob.as<float4>();
+        ra.scene_f4 = c->scene_f4;
+        // max stack use of the reference traversal is depth + 1; FixedStack<32> drops pushes at 31
+        ra.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
+        ra.scene_in_lds = (c->p("scene_lds") != 0.0 && (uint64_t)c->scene_f4 * 16 + (uint64_t)ra.stack_depth * 512 * 4 <= 80u * 1024u) ? 1 : 0;
+        ra.persistent_blocks = (uint32_t)c->n_cus;
+        c->rt_work.ensure(16);
+        ra.work = c->rt_work.as<uint32_t>();
         // deferred shadow rays (wavefront) whenever the path has point-light shadow tests and the
         // worst-case queues (every pixel hits on every sample and bounce) fit the budget
         uint32_t n_point = 0;
@@ -963,8 +1001,12 @@ void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, dev));
     c->n_cus = prop.multiProcessorCount;
-    HIPCHK(hipStreamCreateWithFlags(&c->s_nerf, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->s_rt, hipStreamNonBlocking));
+    // the NeRF wavefront (short, dependent launches) gets the higher queue priority so its
+    // workgroups are dispatched ahead of the long raytracer grids it overlaps with
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&c->s_nerf, hipStreamNonBlocking, prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&c->s_rt, hipStreamNonBlocking, prio_lo));
     for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end}) HIPCHK(hipEventCreate(e));
     HIPCHK(hipHostMalloc((void**)&c->h_ctrl, sizeof(MarchCtrl), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&c->h_alive, 4 * sizeof(uint32_t), hipHostMallocDefault));
@@ -985,7 +1027,7 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats})
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end}) (void)hipEventDestroy(e);
@@ -1157,7 +1199,7 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
         if (!default_params().count(k)) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
         c->params[k] = v;
         c->mesh_reset = true;
-        if (k == "fast_slab" && !c->objs.empty()) upload_scene(c);
+        if ((k == "fast_slab" || k == "scene_lds") && !c->objs.empty()) upload_scene(c);
     });
 }
 int sng_get_param(sng_ctx* c, const char* key, double* v) {

@@ -10,6 +10,7 @@
 // ([depth][thread]) so a wave's pushes/pops at equal depth hit 64 distinct
 // banks.  Each pixel keeps its own XORWOW stream in SoA registers for the whole
 // kernel (one coalesced load/store of 24 B per pixel per frame).
+#include <algorithm>
 #include "sng_internal.h"
 #include "sng_math.h"
 
@@ -19,10 +20,30 @@ constexpr int BVH_STACK = 32;
 constexpr int TPB = 128;   // threads per block for the traversal kernels
 
 struct Stack {
-    int* base;   // LDS
+    int* base;   // LDS, [depth][thread]
+    int stride;  // threads per block
     int n;
-    __device__ __forceinline__ void push(int v) { base[n * TPB] = v; ++n; }
-    __device__ __forceinline__ int pop() { --n; return base[n * TPB]; }
+    __device__ __forceinline__ void push(int v) { base[n * stride] = v; ++n; }
+    __device__ __forceinline__ int pop() { --n; return base[n * stride]; }
+};
+
+// Where a traversal finds its stack and the BVH arrays.  LDS = true: every object's nodes and
+// triangles were copied once per workgroup into LDS (scene blob, capi.cpp upload_scene) and the
+// stack is only as deep as the deepest BVH needs (max depth + 2 <= 32, so the reference's
+// FixedStack<32> overflow rule can never trigger differently).
+template <bool LDS>
+struct TraceCtx {
+    int* stack;            // this thread's first stack slot
+    int stride;
+    const char* scene;     // LDS scene blob (LDS = true)
+    __device__ __forceinline__ const BvhNode* nodes(const ObjectGpu& o) const {
+        if constexpr (LDS) return reinterpret_cast<const BvhNode*>(scene + o.lds_nodes);
+        else return o.nodes;
+    }
+    __device__ __forceinline__ const Tri* tris(const ObjectGpu& o) const {
+        if constexpr (LDS) return reinterpret_cast<const Tri*>(scene + o.lds_tris);
+        else return o.tris;
+    }
 };
 
 // one slot per active lane from a device counter, one atomic per wave
@@ -35,16 +56,22 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* counter, int lane) {
     return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
 }
 
-__device__ __forceinline__ float tri_intersect(const Tri& tr, f3 ro, f3 rd) {   // triangle.cuh:45-59
+// Triangle::ray_intersect (triangle.cuh:45-59) fused with the caller's `t < mint` test: t is
+// formed first and u, v only when t can win.  The accept set is unchanged: the reference replaces
+// a rejected t by FLT_MAX, which never passes `t < mint` (mint <= MAX_DEPTH), and a NaN t fails
+// both forms; u, v are evaluated with the reference's expressions and comparisons.
+__device__ __forceinline__ bool tri_hit(const Tri& tr, f3 ro, f3 rd, float mint, float& t_out) {
     const f3 v1v0 = tr.b - tr.a, v2v0 = tr.c - tr.a, rov0 = ro - tr.a;
     const f3 n = cross(v1v0, v2v0);
-    const f3 q = cross(rov0, rd);
     const float d = 1.0f / dot(rd, n);
+    const float t = d * -dot(n, rov0);
+    if (!(t >= 0.0f && t < mint)) return false;
+    const f3 q = cross(rov0, rd);
     const float u = d * -dot(q, v2v0);
     const float v = d * dot(q, v1v0);
-    float t = d * -dot(n, rov0);
-    if (u < 0.0f || u > 1.0f || v < 0.0f || (u + v) > 1.0f || t < 0.0f) t = 3.402823466e+38f;
-    return t;
+    if (u < 0.0f || u > 1.0f || v < 0.0f || (u + v) > 1.0f) return false;
+    t_out = t;
+    return true;
 }
 
 // ray_intersect_nodes_f<2> (triangle_bvh.cu:263-307); returns t, writes triangle index.
@@ -52,8 +79,8 @@ __device__ __forceinline__ float tri_intersect(const Tri& tr, f3 ro, f3 rd) {   
 // object allow it, which removes 12 IEEE divisions per interior node without changing a bit.
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __restrict__ nodes, const Tri* __restrict__ tris, int* stack_lds,
-                                          int& tri_out, float t_max) {
-    Stack st{stack_lds, 0};
+                                          int stride, int& tri_out, float t_max) {
+    Stack st{stack_lds, stride, 0};
     st.push(0);
     float mint = t_max;
     int shortest = -1;
@@ -63,8 +90,8 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
         if (node.left < 0) {
             const int end = -node.right - 1;
             for (int i = -node.left - 1; i < end; ++i) {
-                const float t = tri_intersect(tris[i], ro, rd);
-                if (t < mint) { mint = t; shortest = i; }
+                float t;
+                if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
             }
         } else {
             const int c0 = node.left, c1 = node.left + 1;
@@ -85,26 +112,23 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
 }
 // t_max < MAX_DEPTH culls everything at or beyond t_max (the result is then min(closest, t_max));
 // only the shadow kernel uses it, where any value >= full_dist yields the same mask.
-__device__ float bvh_intersect(f3 ro, f3 rd, const BvhNode* __restrict__ nodes, const Tri* __restrict__ tris, int* stack_lds, int& tri_out,
-                               bool fast_obj, float t_max = MAX_DEPTH) {
-    if (fast_obj && slab_fast_ok(ro, rd)) return bvh_walk<true>(ro, rd, inv(rd), nodes, tris, stack_lds, tri_out, t_max);
-    return bvh_walk<false>(ro, rd, rd, nodes, tris, stack_lds, tri_out, t_max);
-}
-
-__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, int* stack, int& tri, float t_max = MAX_DEPTH) {
+template <bool LDS>
+__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, const TraceCtx<LDS>& cx, int& tri, float t_max = MAX_DEPTH) {
     const f3 oro = mul(o.world_to_obj, ro - o.pos);
     const f3 ord = mul(o.world_to_obj, rd);
-    return bvh_intersect(oro, ord, o.nodes, o.tris, stack, tri, o.fast_slab != 0, t_max);
+    if (o.fast_slab && slab_fast_ok(oro, ord)) return bvh_walk<true>(oro, ord, inv(ord), cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max);
+    return bvh_walk<false>(oro, ord, ord, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max);
 }
 
 // sng::depth_test_world (common.cu:36-48)
-__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, int* stack, int& out_obj,
+template <bool LDS>
+__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS>& cx, int& out_obj,
                                   float t_max = MAX_DEPTH) {
     float depth = MAX_DEPTH;
     const f3 off = origin + dir * MIN_DEPTH;
     for (int c = 0; c < n_objs; ++c) {
         int tri;
-        const float t = object_intersect(off, dir, objs[c], stack, tri, t_max);
+        const float t = object_intersect(off, dir, objs[c], cx, tri, t_max);
         if (t < depth && t > MIN_DEPTH) { out_obj = c; depth = t; }
     }
     return depth;
@@ -118,7 +142,8 @@ struct Hit {
 };
 __device__ __forceinline__ f3 tri_normal(const Tri& t) { return normalize(cross(t.b - t.a, t.c - t.a)); }
 // sng::depth_test_world(+HitRecord) (common.cu:50-67)
-__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, int* stack, Hit& h) {
+template <bool LDS>
+__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS>& cx, Hit& h) {
     const f3 off = origin + dir * MIN_DEPTH;
     int out_obj = -1;
     h.t = MAX_DEPTH;
@@ -128,12 +153,12 @@ __device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restri
     for (int c = 0; c < n_objs; ++c) {
         int tri;
         const ObjectGpu& o = objs[c];
-        const float t = object_intersect(off, dir, o, stack, tri);
+        const float t = object_intersect(off, dir, o, cx, tri);
         if (t < h.t && t > MIN_DEPTH) {
             out_obj = c;
             h.t = t;
             h.mat = o.mat_id;
-            const Tri tr = o.tris[tri];
+            const Tri tr = cx.tris(o)[tri];
             const f3 N = tri_normal(tr);
             h.normal = mul(o.rot, N);
             const f3 T = normalize((tr.a + tr.b + tr.c) / 3.0f - tr.a);   // Triangle::get_perturb_matrix (triangle.cuh:164-170)
@@ -191,7 +216,7 @@ __device__ __forceinline__ f3 light_sample(const LightGpu& l, Xorwow& r) {
 __global__ __launch_bounds__(TPB) void shade_shadow_kernel(ShadowArgs a, float4* __restrict__ rgba, const float* __restrict__ positions,
                                                             const float* __restrict__ normals, uint32_t* __restrict__ rng, uint32_t n_rng) {
     __shared__ int stack_lds[BVH_STACK * TPB];
-    int* stack = stack_lds + threadIdx.x;
+    const TraceCtx<false> cx{stack_lds + threadIdx.x, TPB, nullptr};
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (t >= n) return;
@@ -215,7 +240,7 @@ __global__ __launch_bounds__(TPB) void shade_shadow_kernel(ShadowArgs a, float4*
                     const f3 l = normalize(lpos - pos);
                     const float full_d = length(lpos - pos);
                     int hit = -1;
-                    const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, stack, hit);
+                    const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, cx, hit);
                     overall = fminf(overall, powf(syn_depth / full_d, a.intensity));
                     const f3 fract_offset = full_d * a.threshold * lpos;
                     const f3 src = pos + fract_offset;
@@ -283,15 +308,23 @@ __device__ __forceinline__ f3 cone_random_frame(f3 orig, const m3& frame, float 
 //                a shadow-ray queue and the light colours to a hit record; shadow_rays_kernel
 //                traces the queue with every lane busy, and rt_accumulate_kernel replays the
 //                colour sums in the original order.  Bit-identical to DEFER = false.
-template <bool DEFER>
-__global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, RtQueue q, const float4* __restrict__ origins,
-                                                        const float4* __restrict__ dirs, uint32_t* __restrict__ rng, uint32_t n_rng,
-                                                        float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
-    __shared__ int stack_lds[BVH_STACK * TPB];
-    int* stack = stack_lds + threadIdx.x;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
-    if (t >= n) return;
+// Dynamic LDS of the traversal kernels: [scene blob (LDS = true)][stack: stack_depth x blockDim ints].
+// Workgroups are persistent (grid-stride), so each copies the scene blob once.
+template <bool LDS>
+__device__ __forceinline__ TraceCtx<LDS> trace_ctx_setup(const RaytraceArgs& a) {
+    extern __shared__ float4 smem4[];
+    if constexpr (LDS) {
+        for (uint32_t k = threadIdx.x; k < a.scene_f4; k += blockDim.x) smem4[k] = a.scene_blob[k];
+        __syncthreads();
+    }
+    int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
+    return TraceCtx<LDS>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4)};
+}
+
+template <bool DEFER, bool LDS>
+__device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS>& cx, uint32_t t,
+                                               const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
+                                               uint32_t n_rng, float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
     const size_t i = (size_t)a.row0 * a.W + t;
     const int lane = threadIdx.x & 63;
     Xorwow r = load_rng(rng, n_rng, i);
@@ -308,7 +341,7 @@ __global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, RtQueue q
         f3 shade_s = splat(0.0f);
         for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
             Hit h;
-            const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, stack, h);
+            const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h);
             if (!bounce) next_pos = next_pos + h.pos;
             if (hit_obj < 0) break;
             // shade_object (raytracer.cu:6-57)
@@ -349,7 +382,7 @@ __global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, RtQueue q
                         float mask = 1.0f;
                         const f3 invL = inv(Lv);
                         int oh = -1;
-                        const float syn = a.show_nerf_shadow ? depth_test_world(h.pos, Lv, a.objs, a.n_objs, stack, oh) : 1.0f;
+                        const float syn = a.show_nerf_shadow ? depth_test_world(h.pos, Lv, a.objs, a.n_objs, cx, oh) : 1.0f;
                         const float nerf = a.show_nerf_shadow
                                                ? depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, h.pos, Lv, invL, 0, a.vol.max_mip)
                                                : 1.0f;
@@ -391,20 +424,48 @@ __global__ __launch_bounds__(TPB) void raytrace_kernel(RaytraceArgs a, RtQueue q
     store_rng(rng, n_rng, i, r);
 }
 
+// Persistent workgroups; each wave takes 8x8 pixel tiles from a device counter (dynamic balance:
+// only ~15 % of the pixels hit an object and those cost ~100x the others).  Square tiles keep a
+// wave's primary rays coherent (fewer hit/miss-divergent waves than 64-pixel row segments).
+template <bool DEFER, bool LDS>
+__global__ __launch_bounds__(512) void raytrace_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins,
+                                                        const float4* __restrict__ dirs, uint32_t* __restrict__ rng, uint32_t n_rng,
+                                                        float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
+    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    const int lane = threadIdx.x & 63;
+    const uint32_t rows = (uint32_t)(a.row1 - a.row0);
+    const uint32_t tiles_x = ((uint32_t)a.W + 7) / 8, n_tiles = tiles_x * ((rows + 7) / 8);
+    while (true) {
+        uint32_t tile = 0;
+        if (lane == 0) tile = atomicAdd(work, 1u);
+        tile = __shfl(tile, 0, 64);
+        if (tile >= n_tiles) break;
+        const uint32_t x = (tile % tiles_x) * 8 + (lane & 7), y = (tile / tiles_x) * 8 + (lane >> 3);
+        if (x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth);
+    }
+}
+
 // Shadow rays of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
 // depend on its cap syn + 1 >= full_dist), so the result is bit-identical.
-__global__ __launch_bounds__(TPB) void shadow_rays_kernel(RaytraceArgs a, RtQueue q) {
-    __shared__ int stack_lds[BVH_STACK * TPB];
-    int* stack = stack_lds + threadIdx.x;
+template <bool LDS>
+__global__ __launch_bounds__(512) void shadow_rays_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work) {
+    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
     const uint32_t total = *q.count * q.nps;
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < total; j += gridDim.x * blockDim.x) {
+    const int lane = threadIdx.x & 63;
+    while (true) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(work, 64u);
+        base = __shfl(base, 0, 64);
+        if (base >= total) break;
+        const uint32_t j = base + (uint32_t)lane;
+        if (j >= total) continue;
         const float4 s0 = q.srec[2 * (size_t)j], s1 = q.srec[2 * (size_t)j + 1];
         const f3 pos = mk(s0.x, s0.y, s0.z), Lv = mk(s1.x, s1.y, s1.z);
         const float full_dist = s0.w;
         int oh = -1;
-        const float syn = depth_test_world(pos, Lv, a.objs, a.n_objs, stack, oh, full_dist);
+        const float syn = depth_test_world(pos, Lv, a.objs, a.n_objs, cx, oh, full_dist);
         const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip);
         const float sh = fminf(fminf(nerf, syn), full_dist);
         q.mask[j] = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
@@ -512,19 +573,47 @@ void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 fo
     if (!n) return;
     hipLaunchKernelGGL(mesh_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, H, row0, row1, cam, focal, sc, o, d, acc, accd);
 }
+static size_t trace_lds_bytes(const RaytraceArgs& a, bool lds, uint32_t tpb) {
+    return (lds ? (size_t)a.scene_f4 * 16 : 0) + (size_t)a.stack_depth * tpb * 4;
+}
+template <typename K>
+static void allow_lds(K kernel, size_t bytes) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
                      hipStream_t s) {
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
-    hipLaunchKernelGGL(raytrace_kernel<false>, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, a, RtQueue{}, o, d, rng, n_rng, acc, accd);
+    const uint32_t tpb = 256, blocks = std::min((n + tpb - 1) / tpb, a.persistent_blocks * 3);
+    const size_t lds = trace_lds_bytes(a, false, tpb);
+    (void)hipMemsetAsync(a.work, 0, 2 * sizeof(uint32_t), s);
+    allow_lds(raytrace_kernel<false, false>, lds);
+    hipLaunchKernelGGL((raytrace_kernel<false, false>), dim3(blocks), dim3(tpb), lds, s, a, RtQueue{}, a.work, o, d, rng, n_rng, acc, accd);
 }
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
                                float* accd, uint32_t shadow_blocks, hipStream_t s) {
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
     (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);   // errors surface through hipGetLastError in the caller
-    hipLaunchKernelGGL(raytrace_kernel<true>, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, a, q, o, d, rng, n_rng, acc, accd);
-    hipLaunchKernelGGL(shadow_rays_kernel, dim3(shadow_blocks), dim3(TPB), 0, s, a, q);
+    (void)hipMemsetAsync(a.work, 0, 2 * sizeof(uint32_t), s);
+    // path kernel: ~160 VGPRs -> 3 waves/SIMD = 768 threads/CU: 2 x 384-thread workgroups
+    // shadow kernel: ~100 VGPRs -> 5 waves/SIMD; LDS-bound at 2 x 512-thread workgroups
+    const uint32_t tp = 384, ts = 512;
+    const bool lds = a.scene_in_lds != 0;
+    const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
+    const uint32_t bp = std::min((n + tp - 1) / tp, a.persistent_blocks * 2);
+    (void)shadow_blocks;
+    if (lds) {
+        allow_lds(raytrace_kernel<true, true>, lp);
+        allow_lds(shadow_rays_kernel<true>, ls);
+        hipLaunchKernelGGL((raytrace_kernel<true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
+        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
+    } else {
+        allow_lds(raytrace_kernel<true, false>, lp);
+        allow_lds(shadow_rays_kernel<false>, ls);
+        hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
+        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
+    }
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc);
 }
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,

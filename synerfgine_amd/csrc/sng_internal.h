@@ -92,6 +92,13 @@ struct RaytraceArgs {
     float lens;
     int show_nerf_shadow;
     float syn_shadow_factor;
+    // traversal resources (capi.cpp upload_scene / render_frame)
+    const float4* scene_blob;   // all objects' BVH nodes + triangles, 16-B aligned (ObjectGpu::lds_nodes/lds_tris)
+    uint32_t scene_f4;          // blob size in float4
+    int scene_in_lds;           // copy the blob into LDS per workgroup
+    uint32_t stack_depth;       // traversal stack entries per thread (max BVH depth + 2, <= 32)
+    uint32_t persistent_blocks; // workgroups per launch unit (number of CUs)
+    uint32_t* work;             // 2 device work counters (pixel tiles, shadow-ray chunks)
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,

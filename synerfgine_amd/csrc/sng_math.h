@@ -360,6 +360,7 @@ struct ObjectGpu {                                           // ObjectTransform 
     int mat_id;
     m3 world_to_obj;   // (I/scale) * inverse(rot), triangle_bvh.cu:313-319
     int fast_slab;     // every BVH box coordinate < 2^40 in magnitude: aabb_entry_fast is exact
+    uint32_t lds_nodes, lds_tris;   // byte offsets of this object's arrays in the scene blob
 };
 struct LightGpu { f3 pos; float intensity; float size; int type; };
 struct MaterialGpu { f3 ka, kd, ks; float n, rg, spec_angle; int type; };

@@ -235,7 +235,7 @@ def test_errors_are_loud(tb):
         tb.inference_mixed_precision(0, 3, 16, 0)
 
 
-@pytest.mark.parametrize("overrides", [{}, {"path_trace_depth": 3, "light_samples": 3}, {"fast_slab": 0}])
+@pytest.mark.parametrize("overrides", [{}, {"path_trace_depth": 3, "light_samples": 3}, {"fast_slab": 0}, {"scene_lds": 0}])
 def test_wavefront_raytracer_equals_megakernel(overrides):
     """Deferred shadow-ray queues (rt_wavefront=1) reproduce the one-kernel path tracer bit for bit."""
     import ctypes
