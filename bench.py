@@ -154,12 +154,16 @@ def main():
                        "width": MW, "height": MH, "nerf_res": list(res["nerf"]), "tiles": f"{world} horizontal bands + RCCL all_gather",
                        "samples_per_frame": int(s0.n_samples), "reference_slots_per_frame": int(s0.n_reference_slots),
                        "wavefront_iterations": int(s0.n_iterations), "hit_rays": int(s0.n_hit)},
+            "streams": "serialized (raytracer then NeRF)" if args.serial_streams else "concurrent (raytracer || NeRF, NeRF stream high priority)",
             "stages_ms_last_frame": {"frame": round(s0.ms_frame, 3), "raytrace": round(s0.ms_raytrace, 3), "nerf": round(s0.ms_nerf, 3),
                                      "shadow": round(s0.ms_shadow, 3), "overlay": round(s0.ms_overlay, 3)},
             "roofline": {"kernel": "nerf_network_kernel<4,1> (fused hash grid + SH + density/rgb MLP)", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
                          "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
+                         "timing": "hipEvents around every launch on the NeRF stream over the timed region" +
+                                   ("" if args.serial_streams else "; the kernel shares the GPU with the raytracer stream, so this is the "
+                                    "contended duration (uncontended: --serial-streams)"),
                          "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / MFMA_F16_PEAK_TFLOPS, 4)},
         }
     tb.close()
