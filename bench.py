@@ -24,12 +24,20 @@ HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md: HBM3E 8.0 TB
 MFMA_F16_PEAK_TFLOPS = 2500.0                # dense fp16/bf16 MFMA
 
 
+WORKLOADS = {
+    "c2": "lego-like NeRF only (show_virtual_obj=0, shadows off)",
+    "c3": "lego-like NeRF + armadillo.json (light_samples 8, path_trace_depth 2, shadow_on_nerf + shadow_on_virtual_obj)",
+    "c4": "kitchen-like NeRF (aabb_scale 16, 5 cascades, cone stepping) + kitchen-rocks.json (bunny/rock/box, light_samples 4, "
+          "nerf_shadow_samples 4)",
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=["c2", "c3"])
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-streams", action="store_true", help="run raytracer and NeRF back to back (profiling)")
     ap.add_argument("--cpu-baseline-scale", type=int, default=2, help="oracle renders the frame at 1/scale linear resolution")
@@ -48,8 +56,7 @@ def cpu_baseline(eng_cfg, config, scale):
     w, h = full["width"] // scale, full["height"] // scale
     tb, eng, _ = S.make_engine(config, width=w, height=h)
     model = O.Model(ncfg, params)
-    bf, _ = O.bitfield(grid)
-    vol = O.make_volume(bf)
+    vol = O.volume_for(ncfg, grid)
     r = eng.resolution()
     nrng = O.xorwow_states(r["nerf"][0] * r["nerf"][1])
     mrng = O.xorwow_states(r["mesh"][0] * r["mesh"][1])
@@ -147,10 +154,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp16 (hash grid + MLP, MFMA f16->f32), fp32 (marching, compositing, shading)",
-            "data": "synthetic: random-init base.json NeRF (L=8,F=4,T=2^19) with analytic lego-like density; armadillo.obj scene",
-            "config": {"workload": f"{args.config}: " + ("lego-like NeRF + armadillo.json (light_samples 8, path_trace_depth 2, "
-                                                         "shadow_on_nerf + shadow_on_virtual_obj)" if args.config == "c3" else
-                                                         "lego-like NeRF only"),
+            "data": "synthetic: random-init base.json NeRF (L=8,F=4,T=2^19) with an analytic density (synthetic.py); scene JSON + OBJ meshes "
+                    "from scenes/ and data/obj/",
+            "config": {"workload": f"{args.config}: " + WORKLOADS[args.config],
                        "width": MW, "height": MH, "nerf_res": list(res["nerf"]), "tiles": f"{world} horizontal bands + RCCL all_gather",
                        "samples_per_frame": int(s0.n_samples), "reference_slots_per_frame": int(s0.n_reference_slots),
                        "wavefront_iterations": int(s0.n_iterations), "hit_rays": int(s0.n_hit)},

@@ -156,6 +156,16 @@ def xorwow_states(n, seed=1999):
     return st
 
 
+def volume_for(cfg, grid_f16, min_transmittance=0.01):
+    """Bitfield + volume of a model config (aabb_scale -> max_cascade, cone) from its density grid."""
+    a = int(cfg.get("aabb_scale", 1))
+    mc = 0
+    while (1 << mc) < a:
+        mc += 1
+    bf, _ = bitfield(grid_f16, max_cascade=mc)
+    return make_volume(bf, aabb_scale=a, min_transmittance=min_transmittance)
+
+
 def make_volume(bf, aabb_scale=1, min_transmittance=0.01):
     h = 0.5 * min(128, aabb_scale)
     lo, hi = [0.5 - h] * 3, [0.5 + h] * 3

@@ -105,7 +105,42 @@ inline M3 inverse(const M3& m0) {
 }
 
 inline float fractf(float x) { return x - std::floor(x); } /* random_val.cuh:82-84 */
-inline float logistic(float x) { return 1.0f / (1.0f + std::exp(-x)); } /* [tcnn] */
+/* exp / log as the device computes them (synerfgine_amd/csrc/sng_math.h sng_expf/sng_logf):
+ * the reference's --use_fast_math __expf/__logf are approximations, so CPU and GPU share one
+ * deterministic <= ~1 ulp formulation wherever a marching/termination decision depends on it. */
+inline float det_expf(float x) {
+    if (x != x) return x;
+    if (x > 88.72283935f) return HUGE_VALF;
+    if (x < -103.972084f) return 0.0f;
+    const float n = std::rint(x * 1.44269502f);
+    float r = std::fma(n, -0.693145752f, x);
+    r = std::fma(n, -1.42860677e-06f, r);
+    float p = 1.98412698e-04f;
+    p = std::fma(p, r, 1.38888889e-03f);
+    p = std::fma(p, r, 8.33333377e-03f);
+    p = std::fma(p, r, 4.16666679e-02f);
+    p = std::fma(p, r, 1.66666672e-01f);
+    p = std::fma(p, r, 0.5f);
+    p = std::fma(p, r, 1.0f);
+    p = std::fma(p, r, 1.0f);
+    return std::scalbn(p, (int)n);
+}
+inline float det_logf(float x) {
+    if (x != x || x < 0.0f) return x != x ? x : NAN;
+    if (x == 0.0f) return -HUGE_VALF;
+    if (x == HUGE_VALF) return x;
+    int e;
+    float m = std::frexp(x, &e);
+    if (m < 0.707106769f) { m = m * 2.0f; e -= 1; }
+    const float f = m - 1.0f;
+    const float s = f / (2.0f + f);
+    const float z = s * s;
+    const float R = z * std::fma(z, std::fma(z, std::fma(z, 0.222222224f, 0.285714298f), 0.400000006f), 0.666666687f);
+    const float hf = 0.5f * f * f;
+    const float dk = (float)e;
+    return std::fma(dk, 0.693145752f, (f - (hf - std::fma(s, hf + R, dk * 1.42860677e-06f))));
+}
+inline float logistic(float x) { return 1.0f / (1.0f + det_expf(-x)); } /* [tcnn] */
 inline float smoothstep(float x) { return x * x * (3.0f - 2.0f * x); } /* [tcnn] */
 inline float sgn(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
 
@@ -402,24 +437,24 @@ inline float distance_to_next_voxel(V3 pos, V3 dir, V3 idir, float res) {
 }
 inline float to_stepping_space(float t, float cone_angle) {
     if (cone_angle <= 1e-5f) return t / MIN_CONE_STEPSIZE;
-    float log1p_c = std::log(1.0f + cone_angle);
-    float a = (std::log(MIN_CONE_STEPSIZE) - std::log(log1p_c)) / log1p_c;
-    float b = (std::log(MAX_CONE_STEPSIZE) - std::log(log1p_c)) / log1p_c;
-    float at = std::exp(a * log1p_c);
-    float bt = std::exp(b * log1p_c);
+    float log1p_c = det_logf(1.0f + cone_angle);
+    float a = (det_logf(MIN_CONE_STEPSIZE) - det_logf(log1p_c)) / log1p_c;
+    float b = (det_logf(MAX_CONE_STEPSIZE) - det_logf(log1p_c)) / log1p_c;
+    float at = det_expf(a * log1p_c);
+    float bt = det_expf(b * log1p_c);
     if (t <= at) return (t - at) / MIN_CONE_STEPSIZE + a;
-    else if (t <= bt) return std::log(t) / log1p_c;
+    else if (t <= bt) return det_logf(t) / log1p_c;
     else return (t - bt) / MAX_CONE_STEPSIZE + b;
 }
 inline float from_stepping_space(float n, float cone_angle) {
     if (cone_angle <= 1e-5f) return n * MIN_CONE_STEPSIZE;
-    float log1p_c = std::log(1.0f + cone_angle);
-    float a = (std::log(MIN_CONE_STEPSIZE) - std::log(log1p_c)) / log1p_c;
-    float b = (std::log(MAX_CONE_STEPSIZE) - std::log(log1p_c)) / log1p_c;
-    float at = std::exp(a * log1p_c);
-    float bt = std::exp(b * log1p_c);
+    float log1p_c = det_logf(1.0f + cone_angle);
+    float a = (det_logf(MIN_CONE_STEPSIZE) - det_logf(log1p_c)) / log1p_c;
+    float b = (det_logf(MAX_CONE_STEPSIZE) - det_logf(log1p_c)) / log1p_c;
+    float at = det_expf(a * log1p_c);
+    float bt = det_expf(b * log1p_c);
     if (n <= a) return (n - a) * MIN_CONE_STEPSIZE + at;
-    else if (n <= b) return std::exp(n * log1p_c);
+    else if (n <= b) return det_expf(n * log1p_c);
     else return (n - b) * MAX_CONE_STEPSIZE + bt;
 }
 inline float advance_n_steps(float t, float cone_angle, float n) { return from_stepping_space(to_stepping_space(t, cone_angle) + n, cone_angle); }
@@ -999,7 +1034,7 @@ void orc_render_nerf(const orc_model* m, const orc_volume* vdesc, const orc_came
                 V3 pos = unwarp_position(v3(cc[0], cc[1], cc[2]), vol.train_aabb);
                 float T = 1.f - lr.w;
                 float dt = unwarp_dt(cc[3]);
-                float alpha = 1.f - std::exp(-std::exp(h2f(o[3])) * dt);
+                float alpha = 1.f - det_expf(-det_expf(h2f(o[3])) * dt);
                 float weight = alpha * T;
                 V3 rgb = v3(logistic(h2f(o[0])), logistic(h2f(o[1])), logistic(h2f(o[2])));
                 lr.x += rgb.x * weight; lr.y += rgb.y * weight; lr.z += rgb.z * weight; lr.w += weight;

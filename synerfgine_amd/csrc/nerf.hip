@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
                 const float g = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x >> 16));
                 const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y & 0xffffu));
                 const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
-                const float alpha = 1.f - expf(-expf(s) * dt);
+                const float alpha = 1.f - sng_expf(-sng_expf(s) * dt);
                 const float weight = alpha * T;
                 rgba.x += logistic(r) * weight;
                 rgba.y += logistic(g) * weight;

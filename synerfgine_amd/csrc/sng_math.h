@@ -52,7 +52,44 @@ SNG_HD f3 normalize(f3 a) {
 SNG_HD f3 inv(f3 a) { return {1.0f / a.x, 1.0f / a.y, 1.0f / a.z}; }
 SNG_HD float fractf_(float x) { return x - floorf(x); }
 SNG_HD float sgnf(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
-SNG_HD float logistic(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Deterministic exp / log.  The reference builds with --use_fast_math (CMakeLists.txt:82), so its
+// expf/logf are approximations; no bit pattern is "the" reference.  These two are written with
+// IEEE basic operations and fmaf only (<= ~1 ulp), so the CPU oracle (its own copy in
+// oracle/sng_oracle.cpp) and the GPU produce identical bits wherever a marching or termination
+// DECISION depends on them (cone stepping, compositing alpha).
+SNG_HD float sng_expf(float x) {
+    if (x != x) return x;
+    if (x > 88.72283935f) return __builtin_huge_valf();
+    if (x < -103.972084f) return 0.0f;
+    const float n = rintf(x * 1.44269502f);
+    float r = fmaf(n, -0.693145752f, x);          // ln2 split: hi has 12 trailing zero bits
+    r = fmaf(n, -1.42860677e-06f, r);
+    float p = 1.98412698e-04f;                    // Taylor to r^7 on |r| <= 0.35
+    p = fmaf(p, r, 1.38888889e-03f);
+    p = fmaf(p, r, 8.33333377e-03f);
+    p = fmaf(p, r, 4.16666679e-02f);
+    p = fmaf(p, r, 1.66666672e-01f);
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    return scalbnf(p, (int)n);
+}
+SNG_HD float sng_logf(float x) {
+    if (x != x || x < 0.0f) return x != x ? x : __builtin_nanf("");
+    if (x == 0.0f) return -__builtin_huge_valf();
+    if (x == __builtin_huge_valf()) return x;
+    int e;
+    float m = frexpf(x, &e);                      // [0.5, 1)
+    if (m < 0.707106769f) { m = m * 2.0f; e -= 1; }
+    const float f = m - 1.0f;                     // exact (Sterbenz)
+    const float s = f / (2.0f + f);
+    const float z = s * s;
+    const float R = z * fmaf(z, fmaf(z, fmaf(z, 0.222222224f, 0.285714298f), 0.400000006f), 0.666666687f);
+    const float hf = 0.5f * f * f;
+    const float dk = (float)e;
+    return fmaf(dk, 0.693145752f, (f - (hf - fmaf(s, hf + R, dk * 1.42860677e-06f))));
+}
+SNG_HD float logistic(float x) { return 1.0f / (1.0f + sng_expf(-x)); }
 SNG_HD float smoothstep(float x) { return x * x * (3.0f - 2.0f * x); }
 SNG_HD f3 reflect(f3 i, f3 n) { return 2.0f * dot(i, n) * n - i; }
 
@@ -164,24 +201,24 @@ SNG_HD float unwarp_dt(float dt) {
 }
 SNG_HD float to_stepping_space(float t, float cone) {
     if (cone <= 1e-5f) return div_by(t, MIN_STEP, INV_MIN_STEP);   // == t / MIN_STEP
-    float log1p_c = logf(1.0f + cone);
-    float a = (logf(MIN_STEP) - logf(log1p_c)) / log1p_c;
-    float b = (logf(MAX_STEP) - logf(log1p_c)) / log1p_c;
-    float at = expf(a * log1p_c);
-    float bt = expf(b * log1p_c);
+    float log1p_c = sng_logf(1.0f + cone);
+    float a = (sng_logf(MIN_STEP) - sng_logf(log1p_c)) / log1p_c;
+    float b = (sng_logf(MAX_STEP) - sng_logf(log1p_c)) / log1p_c;
+    float at = sng_expf(a * log1p_c);
+    float bt = sng_expf(b * log1p_c);
     if (t <= at) return (t - at) / MIN_STEP + a;
-    else if (t <= bt) return logf(t) / log1p_c;
+    else if (t <= bt) return sng_logf(t) / log1p_c;
     else return (t - bt) / MAX_STEP + b;
 }
 SNG_HD float from_stepping_space(float n, float cone) {
     if (cone <= 1e-5f) return n * MIN_STEP;
-    float log1p_c = logf(1.0f + cone);
-    float a = (logf(MIN_STEP) - logf(log1p_c)) / log1p_c;
-    float b = (logf(MAX_STEP) - logf(log1p_c)) / log1p_c;
-    float at = expf(a * log1p_c);
-    float bt = expf(b * log1p_c);
+    float log1p_c = sng_logf(1.0f + cone);
+    float a = (sng_logf(MIN_STEP) - sng_logf(log1p_c)) / log1p_c;
+    float b = (sng_logf(MAX_STEP) - sng_logf(log1p_c)) / log1p_c;
+    float at = sng_expf(a * log1p_c);
+    float bt = sng_expf(b * log1p_c);
     if (n <= a) return (n - a) * MIN_STEP + at;
-    else if (n <= b) return expf(n * log1p_c);
+    else if (n <= b) return sng_expf(n * log1p_c);
     else return (n - b) * MAX_STEP + bt;
 }
 SNG_HD float advance_n_steps(float t, float cone, float n) { return from_stepping_space(to_stepping_space(t, cone) + n, cone); }

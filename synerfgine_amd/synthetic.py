@@ -131,3 +131,96 @@ def _expand_bits(v):
 
 def _morton3d(x, y, z):
     return (_expand_bits(x) | (_expand_bits(y) << 1) | (_expand_bits(z) << 2)).astype(np.int64)
+
+
+# ---------------------------------------------------------------------------------------------
+# 'kitchen-like' snapshot for config C4: aabb_scale 16 -> m_aabb = [-7.5, 8.5]^3, max_cascade 4,
+# cone_angle_constant 1/256 (testbed_nerf.cu:3069-3085).  Exercises the cascaded, exponential-step
+# marcher (the general advance_to_occupied path).  b = float(exp(log(2048*16/16)/7)) = 0x403E350F.
+# ---------------------------------------------------------------------------------------------
+KITCHEN_AABB_SCALE = 16
+KITCHEN_PER_LEVEL_SCALE = float(np.array([0x403E350F], np.uint32).view(np.float32)[0])
+KITCHEN_CASCADES = 5
+
+
+def kitchen_level_table():
+    """Offsets / resolutions with the reference's float expressions (only res matters for offsets)."""
+    log2b = np.float32(np.log2(np.float32(KITCHEN_PER_LEVEL_SCALE)))
+    offsets, res = [0], []
+    for l in range(L):
+        scale = np.float32(np.float64(np.exp2(np.float32(l) * log2b)) * NMIN - 1.0)
+        r = int(np.ceil(scale)) + 1
+        offsets.append(offsets[-1] + min(((r ** 3 + 7) // 8) * 8, 1 << LOG2T))
+        res.append(r)
+    return offsets, res
+
+
+def kitchen_sdf(p):
+    """A room (floor, walls, ceiling) with a table, a cabinet and a bowl, in NeRF coordinates (y up)."""
+    p = np.asarray(p, dtype=np.float64)
+
+    def box(c, h):
+        q = np.abs(p - np.asarray(c)) - np.asarray(h)
+        return np.linalg.norm(np.maximum(q, 0.0), axis=-1) + np.minimum(q.max(axis=-1), 0.0)
+
+    def sphere(c, r):
+        return np.linalg.norm(p - np.asarray(c), axis=-1) - r
+
+    d = box((0.5, 0.30, 0.8), (0.9, 0.15, 0.6))                # table top at y = 0.45
+    d = np.minimum(d, box((-0.7, 0.2, 1.6), (0.35, 0.9, 0.35)))   # cabinet
+    d = np.minimum(d, sphere((0.75, 0.62, 1.0), 0.2))            # bowl
+    d = np.minimum(d, box((0.5, -1.2, 0.5), (6.5, 0.2, 6.5)))     # floor
+    d = np.minimum(d, box((0.5, 3.4, 0.5), (6.5, 0.2, 6.5)))      # ceiling
+    d = np.minimum(d, box((0.5, 1.0, 3.6), (6.5, 2.5, 0.2)))      # back wall
+    d = np.minimum(d, box((0.5, 1.0, -3.2), (6.5, 2.5, 0.2)))     # wall behind the camera
+    d = np.minimum(d, box((-3.4, 1.0, 0.5), (0.2, 2.5, 6.5)))     # side walls
+    d = np.minimum(d, box((4.6, 1.0, 0.5), (0.2, 2.5, 6.5)))
+    return d
+
+
+def kitchen_like(seed=1337, ramp=0.2, a=2.6, b=2.3):
+    """Returns (config dict, params fp16, density grid fp16 [5 * 128^3]) for aabb_scale 16."""
+    rng = np.random.default_rng(seed)
+    lo, size = 0.5 - 0.5 * KITCHEN_AABB_SCALE, float(KITCHEN_AABB_SCALE)
+    offsets, res = kitchen_level_table()
+    # density from level 1 (dense, 48^3 over the 16-unit box), feature 0 = clamped inside-ness
+    dW0 = _xavier(rng, 64, 32, 0.8)
+    dW0[0:2, :] = 0.0
+    dW0[0, 4] = a
+    dW0[1, 4] = -a
+    dW1 = _xavier(rng, 16, 64)
+    dW1[0, :] = 0.0
+    dW1[0, 0], dW1[0, 1] = b, -b
+    rW0 = _xavier(rng, 64, 32)
+    rW1 = _xavier(rng, 64, 64)
+    rW2 = _xavier(rng, 16, 64, 2.0)
+    mlp = np.concatenate([dW0.ravel(), dW1.ravel(), rW0.ravel(), rW1.ravel(), rW2.ravel()])
+    grid = rng.uniform(-0.08, 0.08, size=(offsets[-1], F))
+    grid[offsets[0]:offsets[1]] = rng.uniform(-0.6, 0.6, size=(offsets[1] - offsets[0], F))
+    r1 = res[1]
+    scale1 = np.float64(np.float32(np.float64(np.exp2(np.float32(1) * np.float32(np.log2(np.float32(KITCHEN_PER_LEVEL_SCALE))))) * NMIN - 1.0))
+    v = (np.arange(r1) - 0.5) / scale1              # warped coordinate of dense vertex v
+    X, Y, Z = np.meshgrid(v, v, v, indexing="ij")
+    pts = np.stack([X, Y, Z], axis=-1) * size + lo
+    s = np.clip(-kitchen_sdf(pts) / ramp, -1.0, 1.0)
+    lvl1 = grid[offsets[1]:offsets[2]]
+    lvl1[:, 0] = np.transpose(s, (2, 1, 0)).ravel()
+    lvl1[:, 1:] = rng.uniform(-0.5, 0.5, size=(lvl1.shape[0], F - 1))
+    params = np.concatenate([mlp, grid.ravel()]).astype(np.float16)
+    # density grid, one 128^3 Morton block per cascade m covering 0.5 +- 2^(m-1)
+    xi, yi, zi = np.meshgrid(np.arange(GRID), np.arange(GRID), np.arange(GRID), indexing="ij")
+    morton = _morton3d(xi.ravel(), yi.ravel(), zi.ravel())
+    dg = np.zeros(KITCHEN_CASCADES * GRID ** 3, dtype=np.float32)
+    c = (np.arange(GRID) + 0.5) / GRID
+    for m in range(KITCHEN_CASCADES):
+        w = 2.0 ** m
+        cc = 0.5 + (c - 0.5) * w
+        CX, CY, CZ = np.meshgrid(cc, cc, cc, indexing="ij")
+        d = kitchen_sdf(np.stack([CX, CY, CZ], axis=-1)) - np.sqrt(3.0) * w / GRID / 2.0
+        sig = np.exp(a * b * np.clip(-d / ramp, -1.0, 1.0)) * MIN_STEP
+        blk = np.zeros(GRID ** 3, dtype=np.float32)
+        blk[morton] = sig.ravel()
+        dg[m * GRID ** 3:(m + 1) * GRID ** 3] = blk
+    cfg = dict(n_levels=L, n_features_per_level=F, log2_hashmap_size=LOG2T, base_resolution=NMIN,
+               per_level_scale=KITCHEN_PER_LEVEL_SCALE, aabb_scale=KITCHEN_AABB_SCALE)
+    return cfg, params, dg.astype(np.float16)

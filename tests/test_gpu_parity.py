@@ -142,15 +142,15 @@ def test_rng_states_match_curand_restatement(oracle_lib):
         tb.close()
 
 
-def _frame_vs_oracle(w, h, overrides=None, target=0):
+def _frame_vs_oracle(w, h, overrides=None, target=0, config="c3"):
     import oracle as O
-    tb, eng, (cfg, params, grid) = _engine(w, h, overrides)
+    tb, eng, (cfg, params, grid) = _engine(w, h, overrides, config)
     try:
         nrng, mrng = eng.rng_states(0).copy(), eng.rng_states(1).copy()
         r = eng.frame(spp=0, reset=True, target_n_queries=target)
         got = {k: r.download(k) for k in ("final_rgba", "nerf_rgba", "nerf_depth", "syn_rgba", "syn_depth", "nerf_positions")}
         model = O.Model(cfg, params)
-        vol = O.make_volume(O.bitfield(grid)[0])
+        vol = O.volume_for(cfg, grid)
         ref = O.render_frame(model, vol, tb, eng, nrng, mrng, target=target)
         st = ref["stats"]
         return r, got, ref, st
@@ -256,3 +256,24 @@ def test_wavefront_raytracer_equals_megakernel(overrides):
         assert (out[1][1] < 100).mean() > 0.05    # the object is in view
     finally:
         tb.close()
+
+
+def test_kitchen_cascaded_nerf_matches_oracle():
+    """C4 class: aabb_scale 16, 5 cascades, cone stepping -- the general marcher path."""
+    r, got, ref, st = _frame_vs_oracle(128, 72, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, config="c4")
+    assert r.n_iterations == st.n_iterations
+    assert list(r.alive_per_iter) == list(st.alive_per_iter)[: st.n_iterations]
+    assert r.n_samples == st.n_samples
+    assert r.n_hit > 0.5 * 128 * 72
+    err = np.abs(got["nerf_rgba"] - ref["nerf_rgba"])
+    assert (err.max(axis=-1) <= 2e-3).mean() >= 0.995, f"max err {err.max()}"
+
+
+def test_kitchen_full_frame_matches_oracle():
+    """C4 with the bunny/rock/box scene, NeRF shadows r = 2 (25 samples) and the path tracer."""
+    r, got, ref, st = _frame_vs_oracle(96, 54, {}, config="c4")
+    fin, exp = got["final_rgba"], ref["final"]
+    assert np.isfinite(fin).all()
+    p = _psnr(fin[..., :3], exp[..., :3])
+    close = (np.abs(np.clip(fin, 0, 1) - np.clip(exp, 0, 1))[..., :3].max(axis=-1) <= 2 / 255).mean()
+    assert p >= 40.0 and close >= 0.995, f"PSNR {p:.2f} dB, {close:.4f} of pixels within 2/255"
