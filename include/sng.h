@@ -112,6 +112,10 @@ int sng_ctx_destroy(sng_ctx* ctx);
 
 /* ---- model: Testbed::load_snapshot (testbed.cu:4878-5015, 4994) ---------- */
 int sng_load_snapshot(sng_ctx* ctx, const char* ingp_path);
+/* host-only parse of the same file (no device): config, sizes, and optionally the fp16 params and
+ * density grid copied out (buffers may be NULL) -- the load_snapshot parse step (testbed.cu:4880-4931) */
+int sng_snapshot_probe(const char* ingp_path, sng_nerf_config* cfg, uint64_t* n_params, uint64_t* n_grid_cells,
+                       uint16_t* params_out, uint64_t params_cap, uint16_t* grid_out, uint64_t grid_cap);
 /* NerfNetwork params in tcnn order (nerf_network.h:356-371): density MLP, rgb MLP, grid; fp16 */
 int sng_set_nerf_model(sng_ctx* ctx, const sng_nerf_config* cfg, const uint16_t* params_f16, uint64_t n_params);
 uint64_t sng_nerf_param_count(const sng_nerf_config* cfg);

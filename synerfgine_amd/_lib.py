@@ -126,6 +126,8 @@ SIGNATURES = {
     "sng_ctx_create": (ctypes.c_int, [ctypes.POINTER(sng_ctx_desc), ctypes.POINTER(P)]),
     "sng_ctx_destroy": (ctypes.c_int, [P]),
     "sng_load_snapshot": (ctypes.c_int, [P, ctypes.c_char_p]),
+    "sng_snapshot_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(sng_nerf_config), ctypes.POINTER(U64), ctypes.POINTER(U64), U16P, U64,
+                                          U16P, U64]),
     "sng_set_nerf_model": (ctypes.c_int, [P, ctypes.POINTER(sng_nerf_config), U16P, U64]),
     "sng_nerf_param_count": (U64, [ctypes.POINTER(sng_nerf_config)]),
     "sng_set_density_grid": (ctypes.c_int, [P, U16P, U64]),

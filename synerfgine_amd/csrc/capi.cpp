@@ -1072,14 +1072,24 @@ void read_mat43(const JValue& m, float out[12]) {
         for (int i = 0; i < 4; ++i) for (int j = 0; j < 3; ++j) out[3 * i + j] = m[j][i].as_float();
     } else throw SngError(SNG_ERR_IO, "unexpected camera matrix encoding");
 }
-void load_snapshot(sng_ctx* c, const std::string& path) {
+// Testbed::load_snapshot (testbed.cu:4878-5015): zlib(msgpack) -> model config, fp16 params,
+// fp16 density grid and camera.  Host-only parse, shared by sng_load_snapshot and sng_snapshot_probe.
+struct ParsedSnapshot {
+    sng_nerf_config cfg{};
+    std::vector<uint16_t> params, grid;
+    JValue root;
+};
+ParsedSnapshot parse_snapshot(const std::string& path) {
+    ParsedSnapshot ps;
     std::vector<uint8_t> raw = inflate_all(path);
-    JValue root = MsgpackParser(raw.data(), raw.size()).parse();
+    ps.root = MsgpackParser(raw.data(), raw.size()).parse();
+    const JValue& root = ps.root;
     if (!root.contains("snapshot")) throw SngError(SNG_ERR_IO, "not a snapshot");
     const JValue& snap = root["snapshot"];
     if (!snap.contains("version") || snap["version"].as_num() < 1) throw SngError(SNG_ERR_IO, "Snapshot uses an old format and can not be loaded.");
+    if (!root.contains("encoding")) throw SngError(SNG_ERR_IO, "snapshot has no encoding config");
     const JValue& enc = root["encoding"];
-    sng_nerf_config cfg{};
+    sng_nerf_config& cfg = ps.cfg;
     cfg.n_levels = (uint32_t)enc["n_levels"].as_num();
     cfg.n_features_per_level = enc.contains("n_features_per_level") ? (uint32_t)enc["n_features_per_level"].as_num() : 2u;
     cfg.log2_hashmap_size = enc.contains("log2_hashmap_size") ? (uint32_t)enc["log2_hashmap_size"].as_num() : 15u;
@@ -1088,20 +1098,27 @@ void load_snapshot(sng_ctx* c, const std::string& path) {
     cfg.aabb_scale = (uint32_t)snap["nerf"]["aabb_scale"].as_num();
     const JValue& pb = snap["params_binary"];
     std::string ptype = snap.contains("params_type") ? snap["params_type"].as_str() : std::string("__half");
-    std::vector<uint16_t> params;
     if (ptype == "__half") {
-        params.resize(pb.str.size() / 2);
-        std::memcpy(params.data(), pb.str.data(), params.size() * 2);
+        ps.params.resize(pb.str.size() / 2);
+        std::memcpy(ps.params.data(), pb.str.data(), ps.params.size() * 2);
     } else if (ptype == "float") {
         std::vector<float> fp(pb.str.size() / 4);
         std::memcpy(fp.data(), pb.str.data(), fp.size() * 4);
-        for (float v : fp) params.push_back(f2h_host(v));
+        for (float v : fp) ps.params.push_back(f2h_host(v));
     } else throw SngError(SNG_ERR_IO, "unsupported params_type " + ptype);
-    set_model(c, &cfg, params.data(), params.size());
-    const JValue& dg = snap["density_grid_binary"];
-    std::vector<uint16_t> grid(dg.str.size() / 2);
-    std::memcpy(grid.data(), dg.str.data(), grid.size() * 2);
-    if (!grid.empty()) set_density_grid(c, grid.data(), grid.size());
+    if (snap.contains("density_grid_binary")) {
+        const JValue& dg = snap["density_grid_binary"];
+        ps.grid.resize(dg.str.size() / 2);
+        std::memcpy(ps.grid.data(), dg.str.data(), ps.grid.size() * 2);
+    }
+    return ps;
+}
+
+void load_snapshot(sng_ctx* c, const std::string& path) {
+    ParsedSnapshot ps = parse_snapshot(path);
+    const JValue& snap = ps.root["snapshot"];
+    set_model(c, &ps.cfg, ps.params.data(), ps.params.size());
+    if (!ps.grid.empty()) set_density_grid(c, ps.grid.data(), ps.grid.size());
     if (snap.contains("up_dir")) c->up = mk(snap["up_dir"][0].as_float(), snap["up_dir"][1].as_float(), snap["up_dir"][2].as_float());
     if (snap.contains("camera")) {
         const JValue& cam = snap["camera"];
@@ -1139,6 +1156,23 @@ int sng_ctx_create(const sng_ctx_desc* desc, sng_ctx** out) { return guarded([&]
 int sng_ctx_destroy(sng_ctx* ctx) { return guarded([&] { ctx_destroy(ctx); }); }
 
 int sng_load_snapshot(sng_ctx* c, const char* path) { return guarded([&] { HIPCHK(hipSetDevice(c->device)); load_snapshot(c, path); }); }
+int sng_snapshot_probe(const char* path, sng_nerf_config* cfg, uint64_t* n_params, uint64_t* n_grid_cells, uint16_t* params_out,
+                       uint64_t params_cap, uint16_t* grid_out, uint64_t grid_cap) {
+    return guarded([&] {
+        ParsedSnapshot ps = parse_snapshot(path);
+        if (cfg) *cfg = ps.cfg;
+        if (n_params) *n_params = ps.params.size();
+        if (n_grid_cells) *n_grid_cells = ps.grid.size();
+        if (params_out) {
+            if (params_cap < ps.params.size()) throw SngError(SNG_ERR_INVALID, "params buffer too small");
+            std::memcpy(params_out, ps.params.data(), ps.params.size() * 2);
+        }
+        if (grid_out) {
+            if (grid_cap < ps.grid.size()) throw SngError(SNG_ERR_INVALID, "grid buffer too small");
+            std::memcpy(grid_out, ps.grid.data(), ps.grid.size() * 2);
+        }
+    });
+}
 uint64_t sng_nerf_param_count(const sng_nerf_config* cfg) {
     sng_ctx tmp;
     tmp.cfg = *cfg;

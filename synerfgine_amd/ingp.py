@@ -1,0 +1,42 @@
+"""`.ingp` snapshot writer: zlib(msgpack) with the keys Testbed::load_snapshot reads
+(testbed.cu:4812-4876 save, 4878-5015 load).
+
+Host tooling: turns the synthetic snapshot content (synthetic.py) into a real file so the
+product's loader (sng_load_snapshot / sng_snapshot_probe) is exercised end to end.  Written
+tcnn fields: params_binary (+ params_type "__half", n_params), density_grid_binary (fp16,
+128^3 x (max_cascade+1)), density_grid_size, nerf.aabb_scale, camera {matrix, fov_axis,
+relative_focal_length, screen_center, zoom, scale}, version 1, and the encoding config.
+"""
+import zlib
+
+import numpy as np
+
+
+def write_ingp(path, cfg, params_f16, grid_f16, camera=None, aabb_scale=None):
+    import msgpack
+    params = np.ascontiguousarray(params_f16, np.float16)
+    grid = np.ascontiguousarray(grid_f16, np.float16)
+    a = int(aabb_scale if aabb_scale is not None else cfg.get("aabb_scale", 1))
+    snap = {
+        "version": 1,
+        "mode": "nerf",
+        "params_type": "__half",
+        "n_params": int(params.size),
+        "params_binary": params.tobytes(),
+        "density_grid_size": 128,
+        "density_grid_binary": grid.tobytes(),
+        "nerf": {"aabb_scale": a, "dataset": {"aabb_scale": a}},
+    }
+    if camera is not None:
+        snap["camera"] = camera
+    root = {
+        "snapshot": snap,
+        "encoding": {"otype": "HashGrid", "n_levels": int(cfg["n_levels"]), "n_features_per_level": int(cfg["n_features_per_level"]),
+                     "log2_hashmap_size": int(cfg["log2_hashmap_size"]), "base_resolution": int(cfg["base_resolution"]),
+                     "per_level_scale": float(cfg["per_level_scale"])},
+        "network": {"otype": "FullyFusedMLP", "activation": "ReLU", "output_activation": "None", "n_neurons": 64, "n_hidden_layers": 1},
+        "dir_encoding": {"otype": "SphericalHarmonics", "degree": 4},
+        "rgb_network": {"otype": "FullyFusedMLP", "activation": "ReLU", "output_activation": "None", "n_neurons": 64, "n_hidden_layers": 2},
+    }
+    with open(path, "wb") as f:
+        f.write(zlib.compress(msgpack.packb(root, use_bin_type=True), 6))

@@ -112,3 +112,37 @@ def test_bvh_build_rejects_bad_input(lib):
     from synerfgine_amd import SngError, bvh_build
     with pytest.raises(SngError):
         bvh_build(np.zeros((0, 9), np.float32))
+
+
+@pytest.mark.parametrize("which", ["lego", "kitchen"])
+def test_ingp_snapshot_probe_round_trip(lib, tmp_path, which):
+    """write_ingp -> sng_snapshot_probe (host parse of Testbed::load_snapshot): config, params and grid bit for bit."""
+    pytest.importorskip("msgpack")
+    from synerfgine_amd import _lib, ingp
+    from synerfgine_amd.scene import model_for
+    cfg, params, grid = model_for("c4" if which == "kitchen" else "c3")
+    path = tmp_path / "snap.ingp"
+    ingp.write_ingp(path, cfg, params, grid)
+    c = _lib.sng_nerf_config()
+    n_p, n_g = ctypes.c_uint64(), ctypes.c_uint64()
+    _lib.check(lib.sng_snapshot_probe(str(path).encode(), ctypes.byref(c), ctypes.byref(n_p), ctypes.byref(n_g), None, 0, None, 0))
+    assert (c.n_levels, c.n_features_per_level, c.log2_hashmap_size, c.base_resolution, c.aabb_scale) == \
+        (cfg["n_levels"], cfg["n_features_per_level"], cfg["log2_hashmap_size"], cfg["base_resolution"], cfg["aabb_scale"])
+    assert c.per_level_scale == np.float32(cfg["per_level_scale"])
+    assert n_p.value == params.size and n_g.value == grid.size
+    pp = np.zeros(params.size, np.uint16)
+    gg = np.zeros(grid.size, np.uint16)
+    _lib.check(lib.sng_snapshot_probe(str(path).encode(), None, None, None, pp.ctypes.data_as(_lib.U16P), pp.size,
+                                      gg.ctypes.data_as(_lib.U16P), gg.size))
+    assert np.array_equal(pp, params.view(np.uint16)) and np.array_equal(gg, grid.view(np.uint16))
+
+
+def test_ingp_probe_errors_are_loud(lib, tmp_path):
+    from synerfgine_amd import _lib
+    bad = tmp_path / "bad.ingp"
+    bad.write_bytes(b"not a snapshot")
+    rc = lib.sng_snapshot_probe(str(bad).encode(), None, None, None, None, 0, None, 0)
+    assert rc == _lib.SNG_ERR_IO if hasattr(_lib, "SNG_ERR_IO") else rc == -3
+    assert lib.sng_last_error()
+    rc = lib.sng_snapshot_probe(str(tmp_path / "missing.ingp").encode(), None, None, None, None, 0, None, 0)
+    assert rc != 0

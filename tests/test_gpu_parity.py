@@ -277,3 +277,30 @@ def test_kitchen_full_frame_matches_oracle():
     p = _psnr(fin[..., :3], exp[..., :3])
     close = (np.abs(np.clip(fin, 0, 1) - np.clip(exp, 0, 1))[..., :3].max(axis=-1) <= 2 / 255).mean()
     assert p >= 40.0 and close >= 0.995, f"PSNR {p:.2f} dB, {close:.4f} of pixels within 2/255"
+
+
+def test_load_snapshot_equals_direct_model(tmp_path):
+    """sng_load_snapshot(.ingp) reproduces set_nerf_model + set_density_grid: same bitfield, same frame bits."""
+    pytest.importorskip("msgpack")
+    import os
+    from synerfgine_amd import Engine, Testbed, ingp
+    from synerfgine_amd import scene as S
+    tb, eng, (cfg, params, grid) = _engine(128, 72)
+    try:
+        path = tmp_path / "lego_like.ingp"
+        ingp.write_ingp(path, cfg, params, grid, camera={"matrix": tb.camera_matrix.reshape(4, 3).tolist(), "fov_axis": 1})
+        a = eng.frame().download("final_rgba")
+        tb2 = Testbed(0)
+        try:
+            tb2.load_snapshot(path)
+            assert np.array_equal(tb2.density_grid_bitfield(), tb.density_grid_bitfield())
+            eng2 = Engine(tb2)
+            eng2.set_virtual_world(os.path.join(S.SCENES, "armadillo.json"))
+            eng2.set_param("res_factor", 8)
+            eng2.init(128, 72)
+            b = eng2.frame().download("final_rgba")
+            assert np.array_equal(a, b)
+        finally:
+            tb2.close()
+    finally:
+        tb.close()
