@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-streams", action="store_true", help="run raytracer and NeRF back to back (profiling)")
     ap.add_argument("--cpu-baseline-scale", type=int, default=2, help="oracle renders the frame at 1/scale linear resolution")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help="gloo: CPU-side gather (rehearsal on one GPU)")
+    ap.add_argument("--even-bands", action="store_true", help="equal-height bands instead of cost-balanced ones")
+    ap.add_argument("--balance-iters", type=int, default=8, help="untimed calibration frames for the band split")
     return ap.parse_args()
 
 
@@ -79,28 +82,45 @@ def main():
     import torch
     import torch.distributed as dist
 
+    n_dev = torch.cuda.device_count()
+    dev_id = local_rank % max(1, n_dev)   # ranks > GPUs only in the gloo rehearsal mode (--dist-backend gloo)
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(dev_id)
+        dist.init_process_group(args.dist_backend)
     from synerfgine_amd import scene as S
     from synerfgine_amd import tiling as T
 
-    tb, eng, eng_cfg = S.make_engine(args.config, device_id=local_rank, overrides={"concurrent_streams": 0} if args.serial_streams else None)
+    tb, eng, eng_cfg = S.make_engine(args.config, device_id=dev_id, overrides={"concurrent_streams": 0} if args.serial_streams else None)
     res = eng.resolution()
     MW, MH = res["mesh"]
-    rows = T.band_rows(MH, rank, world)
-    band = T.tile_height(MH, world)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", dev_id)
     stream = torch.cuda.current_stream(dev)
-    tile = torch.zeros((band, MW, 4), dtype=torch.float32, device=dev)
-    frame = torch.empty((world * band, MW, 4), dtype=torch.float32, device=dev) if world > 1 else None
+    bounds = T.even_bounds(MH, world)
+
+    if world > 1 and not args.even_bands:
+        # untimed calibration: re-split the rows until every band costs the same device time
+        # (sky rows are ~free, object rows ~100x dearer), then keep the split fixed
+        for _ in range(args.balance_iters):
+            r = eng.frame(spp=0, reset=True, rows=(bounds[rank], bounds[rank + 1]))
+            t = torch.tensor([r.ms_frame], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+            ts = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(ts, t)
+            bounds = T.balance_bounds(MH, bounds, [float(x.item()) for x in ts])
+    rows = (bounds[rank], bounds[rank + 1])
+    band = max(bounds[k + 1] - bounds[k] for k in range(world))
+    on_dev = args.dist_backend == "nccl"
+    tile = torch.zeros((band, MW, 4), dtype=torch.float32, device=dev if on_dev else "cpu")
+    frame = torch.empty((world * band, MW, 4), dtype=torch.float32, device=dev if on_dev else "cpu") if world > 1 else None
+    tile_dev = tile if on_dev else torch.zeros((band, MW, 4), dtype=torch.float32, device=dev)
 
     def step(collect):
         r = eng.frame(spp=0, reset=True, rows=rows if world > 1 else None, collect_kernel_times=collect)
         if world > 1:
             n = (rows[1] - rows[0]) * MW * 16
             if n:
-                tb._lib.sng_copy_device(tb.ctx, r.raw.d_final_rgba + rows[0] * MW * 16, tile.data_ptr(), n, stream.cuda_stream)
+                tb._lib.sng_copy_device(tb.ctx, r.raw.d_final_rgba + rows[0] * MW * 16, tile_dev.data_ptr(), n, stream.cuda_stream)
+            if not on_dev:
+                tile.copy_(tile_dev)
             T.gather_bands(tile, frame)
         return r
 
@@ -118,7 +138,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if on_dev else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -157,7 +177,7 @@ def main():
             "data": "synthetic: random-init base.json NeRF (L=8,F=4,T=2^19) with an analytic density (synthetic.py); scene JSON + OBJ meshes "
                     "from scenes/ and data/obj/",
             "config": {"workload": f"{args.config}: " + WORKLOADS[args.config],
-                       "width": MW, "height": MH, "nerf_res": list(res["nerf"]), "tiles": f"{world} horizontal bands + RCCL all_gather",
+                       "width": MW, "height": MH, "nerf_res": list(res["nerf"]), "tiles": f"{world} horizontal bands (rows {bounds}) + " + ("RCCL all_gather" if args.dist_backend == "nccl" else "gloo all_gather"),
                        "samples_per_frame": int(s0.n_samples), "reference_slots_per_frame": int(s0.n_reference_slots),
                        "wavefront_iterations": int(s0.n_iterations), "hit_rays": int(s0.n_hit)},
             "streams": "serialized (raytracer then NeRF)" if args.serial_streams else "concurrent (raytracer || NeRF, NeRF stream high priority)",

@@ -319,7 +319,8 @@ const std::map<std::string, double>& default_params() {
         {"linear_marcher", 1},
         {"fast_slab", 1},
         {"rt_wavefront", 1},
-        {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit                    // deferred shadow-ray queues for the path tracer
+        {"scene_lds", 1},
+        {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost                       // BVH nodes + triangles staged in LDS per workgroup when they fit                    // deferred shadow-ray queues for the path tracer
         {"rt_queue_gb", 48},                    // device-memory budget for those queues                       // exact reciprocal-multiply BVH box tests                  // exact unit-cube fast path of the occupancy march
     };
     return d;
@@ -373,6 +374,8 @@ struct sng_ctx {
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
     DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
+    DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
+    uint64_t rt_tile_key = 0;             // band geometry the costs belong to
     DevBuf rng_nerf, rng_mesh;
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
     DevBuf d_seq;
@@ -827,6 +830,18 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         ra.persistent_blocks = (uint32_t)c->n_cus;
         c->rt_work.ensure(16);
         ra.work = c->rt_work.as<uint32_t>();
+        if (c->p("rt_tile_order") != 0.0) {
+            const uint32_t n_tiles = (uint32_t)((MW + 7) / 8) * (uint32_t)((y1 - y0 + 7) / 8);
+            const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1;
+            c->rt_tile_cost.ensure((size_t)n_tiles * 4);
+            c->rt_tile_order.ensure((size_t)n_tiles * 4);
+            if (key == c->rt_tile_key) {
+                launch_tile_sort(c->rt_tile_cost.as<uint32_t>(), n_tiles, c->rt_tile_order.as<uint32_t>(), c->s_rt);
+                ra.tile_order = c->rt_tile_order.as<uint32_t>();
+            }
+            ra.tile_cost = c->rt_tile_cost.as<uint32_t>();
+            c->rt_tile_key = key;
+        }
         // deferred shadow rays (wavefront) whenever the path has point-light shadow tests and the
         // worst-case queues (every pixel hits on every sample and bounce) fit the budget
         uint32_t n_point = 0;
@@ -1027,7 +1042,7 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end}) (void)hipEventDestroy(e);

@@ -436,12 +436,17 @@ __global__ __launch_bounds__(512) void raytrace_kernel(RaytraceArgs a, RtQueue q
     const uint32_t rows = (uint32_t)(a.row1 - a.row0);
     const uint32_t tiles_x = ((uint32_t)a.W + 7) / 8, n_tiles = tiles_x * ((rows + 7) / 8);
     while (true) {
-        uint32_t tile = 0;
-        if (lane == 0) tile = atomicAdd(work, 1u);
-        tile = __shfl(tile, 0, 64);
-        if (tile >= n_tiles) break;
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(work, 1u);
+        k = __shfl(k, 0, 64);
+        if (k >= n_tiles) break;
+        // tiles in descending cost of the previous frame (tile_sort_kernel), so the few expensive
+        // object tiles start first instead of being the latency tail of the launch
+        const uint32_t tile = a.tile_order ? a.tile_order[k] : k;
+        const uint64_t t0 = wall_clock64();
         const uint32_t x = (tile % tiles_x) * 8 + (lane & 7), y = (tile / tiles_x) * 8 + (lane >> 3);
         if (x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth);
+        if (a.tile_cost && lane == 0) a.tile_cost[tile] = (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull);
     }
 }
 
@@ -573,6 +578,24 @@ void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 fo
     if (!n) return;
     hipLaunchKernelGGL(mesh_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, H, row0, row1, cam, focal, sc, o, d, acc, accd);
 }
+// Order tiles by descending previous-frame cost: 32 log2 buckets, one workgroup (n_tiles <= 2^20).
+__global__ __launch_bounds__(1024) void tile_sort_kernel(const uint32_t* __restrict__ cost, uint32_t n, uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[32], base[32];
+    if (threadIdx.x < 32) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[31 - min(31, 31 - __clz(cost[i] | 1u))], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int b = 0; b < 32; ++b) { base[b] = acc; acc += hist[b]; }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&base[31 - min(31, 31 - __clz(cost[i] | 1u))], 1u)] = i;
+}
+void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, hipStream_t s) {
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(1), dim3(1024), 0, s, cost, n, order);
+}
+
 static size_t trace_lds_bytes(const RaytraceArgs& a, bool lds, uint32_t tpb) {
     return (lds ? (size_t)a.scene_f4 * 16 : 0) + (size_t)a.stack_depth * tpb * 4;
 }

@@ -99,6 +99,8 @@ struct RaytraceArgs {
     uint32_t stack_depth;       // traversal stack entries per thread (max BVH depth + 2, <= 32)
     uint32_t persistent_blocks; // workgroups per launch unit (number of CUs)
     uint32_t* work;             // 2 device work counters (pixel tiles, shadow-ray chunks)
+    const uint32_t* tile_order; // 8x8 tile visiting order (nullptr: row-major)
+    uint32_t* tile_cost;        // per-tile cycles of this frame (nullptr: not recorded)
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
@@ -134,6 +136,7 @@ void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 fo
                       hipStream_t s);
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
                                float* accd, uint32_t shadow_blocks, hipStream_t s);
+void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, hipStream_t s);
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
                      hipStream_t s);
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,

@@ -33,3 +33,47 @@ def gather_bands(tile, frame, group=None):
         return frame
     dist.all_gather_into_tensor(frame, tile, group=group)
     return frame
+
+
+def even_bounds(height, world):
+    """Row boundaries [b0=0, b1, ..., b_world=height] of the equal-height bands."""
+    return [band_rows(height, r, world)[0] for r in range(world)] + [height]
+
+
+def balance_bounds(height, bounds, times, min_rows=8, damping=0.75):
+    """Re-split rows so every band costs the same, from the previous split's per-band times.
+
+    SURVEY.md §8e: sky rows are nearly free while rows through the NeRF object and the mesh cost
+    ~100x more, so equal-height bands scale poorly.  The cost is modelled as piecewise constant per
+    band (time / rows) and the cumulative cost is cut into equal parts; `damping` blends the new
+    boundaries with the old ones so the iteration converges without oscillating.  Deterministic:
+    every rank computes the same bounds from the same gathered times.
+    """
+    world = len(times)
+    if world == 1:
+        return [0, height]
+    dens = []
+    for r in range(world):
+        rows = max(1, bounds[r + 1] - bounds[r])
+        dens.append(max(float(times[r]), 1e-6) / rows)
+    cum = [0.0]
+    for r in range(world):
+        cum.append(cum[-1] + dens[r] * (bounds[r + 1] - bounds[r]))
+    total = cum[-1]
+    new = [0]
+    for k in range(1, world):
+        target = total * k / world
+        r = 0
+        while r < world - 1 and cum[r + 1] < target:
+            r += 1
+        row = bounds[r] + (target - cum[r]) / dens[r]
+        row = damping * row + (1.0 - damping) * bounds[k]
+        new.append(int(round(row)))
+    new.append(height)
+    # monotone with at least min_rows per band (when the frame allows it)
+    m = min(min_rows, height // world)
+    for k in range(1, world):
+        new[k] = max(new[k], new[k - 1] + m)
+    for k in range(world - 1, 0, -1):
+        new[k] = min(new[k], new[k + 1] - m)
+    return new

@@ -65,3 +65,20 @@ def test_gloo_band_gather_reassembles_frame(world):
     res = sorted(q.get(timeout=5) for _ in range(world))
     assert all(p.exitcode == 0 for p in procs)
     assert all(ok and agree == 1.0 for _, ok, agree in res)
+
+
+def test_balance_bounds_equalises_cost():
+    from synerfgine_amd.tiling import balance_bounds, even_bounds
+    H, N = 1080, 8
+    cost = np.ones(H)
+    cost[300:700] = 60.0          # an object in the middle rows
+    b = even_bounds(H, N)
+    for _ in range(12):
+        t = [cost[b[r]:b[r + 1]].sum() for r in range(N)]
+        b = balance_bounds(H, b, t)
+    t = [cost[b[r]:b[r + 1]].sum() for r in range(N)]
+    assert b[0] == 0 and b[-1] == H and all(b[k] < b[k + 1] for k in range(N))
+    assert max(t) / (sum(t) / N) < 1.15
+    # equal cost stays (nearly) equal-height
+    b2 = balance_bounds(H, even_bounds(H, N), [1.0] * N)
+    assert max(abs(x - y) for x, y in zip(b2, even_bounds(H, N))) <= 1
