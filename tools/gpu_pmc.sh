@@ -8,4 +8,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c -d gpurun_out/pmc/$c -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --serial-streams > gpurun_out/pmc/$c.log 2>&1
   rc=$?; echo "$c rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/pmc/$c.log; exit $rc; }
 done
-python3 tools/pmc_summary.py gpurun_out/pmc profiles/pmc_network_r01.json
+python3 tools/pmc_summary.py gpurun_out/pmc profiles/pmc_network_r01.json && mkdir -p gpurun_out/profiles && cp profiles/pmc_network_r01.json gpurun_out/profiles/
