@@ -40,10 +40,11 @@ def parse():
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-streams", action="store_true", help="run raytracer and NeRF back to back (profiling)")
-    ap.add_argument("--cpu-baseline-scale", type=int, default=2, help="oracle renders the frame at 1/scale linear resolution")
+    ap.add_argument("--cpu-baseline-scale", type=float, default=1.5, help="oracle renders the frame at 1/scale linear resolution")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help="gloo: CPU-side gather (rehearsal on one GPU)")
     ap.add_argument("--even-bands", action="store_true", help="equal-height bands instead of cost-balanced ones")
     ap.add_argument("--balance-iters", type=int, default=8, help="untimed calibration frames for the band split")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="engine parameter override (sng_set_param)")
     return ap.parse_args()
 
 
@@ -56,7 +57,7 @@ def cpu_baseline(eng_cfg, config, scale):
 
     ncfg, params, grid = eng_cfg
     full = S.CONFIGS[config]
-    w, h = full["width"] // scale, full["height"] // scale
+    w, h = int(round(full["width"] / scale)), int(round(full["height"] / scale))
     tb, eng, _ = S.make_engine(config, width=w, height=h)
     model = O.Model(ncfg, params)
     vol = O.volume_for(ncfg, grid)
@@ -67,10 +68,11 @@ def cpu_baseline(eng_cfg, config, scale):
     O.render_frame(model, vol, tb, eng, nrng, mrng)
     dt = time.perf_counter() - t0
     tb.close()
-    fps_full = 1.0 / (dt * scale * scale)   # pixel-count scaling to the full-resolution frame
+    frac = (w * h) / float(full["width"] * full["height"])
+    fps_full = frac / dt   # pixel-count scaling to the full-resolution frame
     return {"value": round(fps_full, 5), "unit": "frames/s", "cores": O.lib().orc_num_threads(), "kind": "port",
-            "sample": f"oracle (C++ OpenMP) Engine::frame of {config} at {w}x{h} ({1.0/(scale*scale):.3g} of the pixels) took "
-                      f"{dt:.2f}s; extrapolated x{scale*scale} to {full['width']}x{full['height']}"}
+            "sample": f"oracle (C++ OpenMP) Engine::frame of {config} at {w}x{h} ({frac:.3g} of the pixels) took "
+                      f"{dt:.2f}s; extrapolated by pixel count to {full['width']}x{full['height']}"}
 
 
 def main():
@@ -90,7 +92,11 @@ def main():
     from synerfgine_amd import scene as S
     from synerfgine_amd import tiling as T
 
-    tb, eng, eng_cfg = S.make_engine(args.config, device_id=dev_id, overrides={"concurrent_streams": 0} if args.serial_streams else None)
+    overrides = {"concurrent_streams": 0} if args.serial_streams else {}
+    for kv in args.set:
+        k, v = kv.split("=", 1)
+        overrides[k] = float(v)
+    tb, eng, eng_cfg = S.make_engine(args.config, device_id=dev_id, overrides=overrides)
     res = eng.resolution()
     MW, MH = res["mesh"]
     dev = torch.device("cuda", dev_id)
@@ -180,7 +186,9 @@ def main():
                        "width": MW, "height": MH, "nerf_res": list(res["nerf"]), "tiles": f"{world} horizontal bands (rows {bounds}) + " + ("RCCL all_gather" if args.dist_backend == "nccl" else "gloo all_gather"),
                        "samples_per_frame": int(s0.n_samples), "reference_slots_per_frame": int(s0.n_reference_slots),
                        "wavefront_iterations": int(s0.n_iterations), "hit_rays": int(s0.n_hit)},
-            "streams": "serialized (raytracer then NeRF)" if args.serial_streams else "concurrent (raytracer || NeRF, NeRF stream high priority)",
+            "streams": "serialized (raytracer then NeRF)" if args.serial_streams else
+                       "concurrent (NeRF head alone, then raytracer || NeRF tail; NeRF stream high priority)",
+            "overrides": overrides,
             "stages_ms_last_frame": {"frame": round(s0.ms_frame, 3), "raytrace": round(s0.ms_raytrace, 3), "nerf": round(s0.ms_nerf, 3),
                                      "shadow": round(s0.ms_shadow, 3), "overlay": round(s0.ms_overlay, 3)},
             "roofline": {"kernel": "nerf_network_kernel<4,1> (fused hash grid + SH + density/rgb MLP)", "bound": "hbm",

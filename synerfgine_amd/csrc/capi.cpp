@@ -315,7 +315,8 @@ const std::map<std::string, double>& default_params() {
         {"srgb", 1},                            // EColorSpace::SRGB passed to overlay (engine.cu:406)
         {"smooth_threshold", 1.0},              // sng_position_kernel_threshold (unused by the path)
         {"max_shadow_variance", 0.0},           // sng_shadow_depth_variance (unused by the path)
-        {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
+        {"concurrent_streams", 1},
+        {"rt_start_chunk", 1},                  // concurrent mode: raytracer starts after this many 4-iteration NeRF chunks              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
         {"linear_marcher", 1},
         {"fast_slab", 1},
         {"rt_wavefront", 1},
@@ -332,7 +333,7 @@ struct sng_ctx {
     int device = 0;
     int n_cus = 256;
     hipStream_t s_nerf = nullptr, s_rt = nullptr;
-    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr;
+    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr;
     std::vector<hipEvent_t> net_events;
 
     // model
@@ -798,80 +799,94 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     const f2 sc = render_screen_center(c);
 
     HIPCHK(hipEventRecord(c->ev_start, c->s_nerf));
-    HIPCHK(hipStreamWaitEvent(c->s_rt, c->ev_start, 0));
-    // ---- raytracer (RayTracer::render, raytracer.cu:312-370) on its own stream
-    HIPCHK(hipEventRecord(c->ev_rt0, c->s_rt));
-    if (c->mesh_reset || P.reset_accumulation) {
-        const int mres[2] = {MW, MH};
-        launch_mesh_rays(MW, MH, y0, y1, cam, focal_for(c, mres), sc, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->acc_rgba.as<float4>(),
-                         c->acc_depth.as<float>(), c->s_rt);
-        c->mesh_reset = false;
-    }
-    if (c->p("show_virtual_obj") != 0.0 && !c->objs.empty()) {
-        RaytraceArgs ra{};
-        ra.vol = vol;
-        ra.W = MW; ra.row0 = y0; ra.row1 = y1;
-        ra.up = cam.c0;
-        ra.objs = c->d_objs.as<ObjectGpu>(); ra.n_objs = (int)c->objs.size();
-        ra.lights = c->d_lights.as<LightGpu>(); ra.n_lights = (int)c->lights.size();
-        ra.mats = c->d_mats.as<MaterialGpu>();
-        ra.samples = (uint32_t)c->p("light_samples");
-        ra.bounces = (uint32_t)c->p("path_trace_depth");
-        ra.shadow_iters = (uint32_t)c->p("syn_shadow_samples");
-        ra.shadow_steps = (uint32_t)c->p("n_steps");
-        ra.lens = (float)c->p("lens_size");
-        ra.show_nerf_shadow = c->p("shadow_on_virtual_obj") != 0.0;
-        ra.syn_shadow_factor = (float)c->p("syn_shadow_intensity");
-        ra.scene_blob = c->d_scene_blob.as<float4>();
-        ra.scene_f4 = c->scene_f4;
-        // max stack use of the reference traversal is depth + 1; FixedStack<32> drops pushes at 31
-        ra.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
-        ra.scene_in_lds = (c->p("scene_lds") != 0.0 && (uint64_t)c->scene_f4 * 16 + (uint64_t)ra.stack_depth * 512 * 4 <= 80u * 1024u) ? 1 : 0;
-        ra.persistent_blocks = (uint32_t)c->n_cus;
-        c->rt_work.ensure(16);
-        ra.work = c->rt_work.as<uint32_t>();
-        if (c->p("rt_tile_order") != 0.0) {
-            const uint32_t n_tiles = (uint32_t)((MW + 7) / 8) * (uint32_t)((y1 - y0 + 7) / 8);
-            const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1;
-            c->rt_tile_cost.ensure((size_t)n_tiles * 4);
-            c->rt_tile_order.ensure((size_t)n_tiles * 4);
-            if (key == c->rt_tile_key) {
-                launch_tile_sort(c->rt_tile_cost.as<uint32_t>(), n_tiles, c->rt_tile_order.as<uint32_t>(), c->s_rt);
-                ra.tile_order = c->rt_tile_order.as<uint32_t>();
+    // The raytracer (s_rt) and the NeRF wavefront (s_nerf) are independent until the overlay.
+    // concurrent_streams = 1: the raytracer starts after the first `rt_start_chunk` chunks of
+    // wavefront iterations, i.e. once the NeRF's throughput-heavy head (nearly all rays alive)
+    // has run on the whole GPU; it then overlaps the latency-bound tail iterations.
+    const bool concurrent = c->p("concurrent_streams") != 0.0;
+    const int rt_start_chunk = (concurrent && show_nerf) ? (int)c->p("rt_start_chunk") : 0;
+    bool rt_enqueued = false;
+    auto enqueue_raytracer = [&](hipEvent_t after) {
+        HIPCHK(hipStreamWaitEvent(c->s_rt, after, 0));
+        // ---- raytracer (RayTracer::render, raytracer.cu:312-370) on its own stream
+        // ---- raytracer (RayTracer::render, raytracer.cu:312-370) on its own stream
+        HIPCHK(hipEventRecord(c->ev_rt0, c->s_rt));
+        if (c->mesh_reset || P.reset_accumulation) {
+            const int mres[2] = {MW, MH};
+            launch_mesh_rays(MW, MH, y0, y1, cam, focal_for(c, mres), sc, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->acc_rgba.as<float4>(),
+                             c->acc_depth.as<float>(), c->s_rt);
+            c->mesh_reset = false;
+        }
+        if (c->p("show_virtual_obj") != 0.0 && !c->objs.empty()) {
+            RaytraceArgs ra{};
+            ra.vol = vol;
+            ra.W = MW; ra.row0 = y0; ra.row1 = y1;
+            ra.up = cam.c0;
+            ra.objs = c->d_objs.as<ObjectGpu>(); ra.n_objs = (int)c->objs.size();
+            ra.lights = c->d_lights.as<LightGpu>(); ra.n_lights = (int)c->lights.size();
+            ra.mats = c->d_mats.as<MaterialGpu>();
+            ra.samples = (uint32_t)c->p("light_samples");
+            ra.bounces = (uint32_t)c->p("path_trace_depth");
+            ra.shadow_iters = (uint32_t)c->p("syn_shadow_samples");
+            ra.shadow_steps = (uint32_t)c->p("n_steps");
+            ra.lens = (float)c->p("lens_size");
+            ra.show_nerf_shadow = c->p("shadow_on_virtual_obj") != 0.0;
+            ra.syn_shadow_factor = (float)c->p("syn_shadow_intensity");
+            ra.scene_blob = c->d_scene_blob.as<float4>();
+            ra.scene_f4 = c->scene_f4;
+            // max stack use of the reference traversal is depth + 1; FixedStack<32> drops pushes at 31
+            ra.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
+            ra.scene_in_lds = (c->p("scene_lds") != 0.0 && (uint64_t)c->scene_f4 * 16 + (uint64_t)ra.stack_depth * 512 * 4 <= 80u * 1024u) ? 1 : 0;
+            ra.persistent_blocks = (uint32_t)c->n_cus;
+            c->rt_work.ensure(16);
+            ra.work = c->rt_work.as<uint32_t>();
+            if (c->p("rt_tile_order") != 0.0) {
+                const uint32_t n_tiles = (uint32_t)((MW + 7) / 8) * (uint32_t)((y1 - y0 + 7) / 8);
+                const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1;
+                c->rt_tile_cost.ensure((size_t)n_tiles * 4);
+                c->rt_tile_order.ensure((size_t)n_tiles * 4);
+                if (key == c->rt_tile_key) {
+                    launch_tile_sort(c->rt_tile_cost.as<uint32_t>(), n_tiles, c->rt_tile_order.as<uint32_t>(), c->s_rt);
+                    ra.tile_order = c->rt_tile_order.as<uint32_t>();
+                }
+                ra.tile_cost = c->rt_tile_cost.as<uint32_t>();
+                c->rt_tile_key = key;
             }
-            ra.tile_cost = c->rt_tile_cost.as<uint32_t>();
-            c->rt_tile_key = key;
+            // deferred shadow rays (wavefront) whenever the path has point-light shadow tests and the
+            // worst-case queues (every pixel hits on every sample and bounce) fit the budget
+            uint32_t n_point = 0;
+            for (auto& l : c->lights) n_point += l.type == 0 ? 1u : 0u;
+            const uint64_t n_px = (uint64_t)(y1 - y0) * (uint64_t)MW;
+            const uint64_t cap = n_px * ra.samples * ra.bounces;
+            RtQueue q{};
+            q.nls = (uint32_t)c->lights.size() * ra.shadow_iters;
+            q.nps = n_point * ra.shadow_iters;
+            q.rec_stride = 2 + (3 * q.nls + 3) / 4;
+            const uint64_t bytes = cap * (16ull * q.rec_stride + 32ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
+            const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
+                                   bytes <= (uint64_t)(c->p("rt_queue_gb") * 1073741824.0);
+            if (wavefront) {
+                c->rt_rec.ensure(cap * 16ull * q.rec_stride);
+                c->rt_srec.ensure(cap * 32ull * q.nps);
+                c->rt_mask.ensure(cap * 4ull * q.nps);
+                c->rt_head.ensure((uint64_t)MW * MH * 4);
+                c->rt_count.ensure(16);
+                q.rec = c->rt_rec.as<float4>(); q.srec = c->rt_srec.as<float4>(); q.mask = c->rt_mask.as<float>();
+                q.head = c->rt_head.as<int>(); q.count = c->rt_count.as<uint32_t>(); q.cap = (uint32_t)cap;
+                launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
+                                          c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), (uint32_t)c->n_cus * 16, c->s_rt);
+            } else {
+                launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
+                                c->acc_depth.as<float>(), c->s_rt);
+            }
         }
-        // deferred shadow rays (wavefront) whenever the path has point-light shadow tests and the
-        // worst-case queues (every pixel hits on every sample and bounce) fit the budget
-        uint32_t n_point = 0;
-        for (auto& l : c->lights) n_point += l.type == 0 ? 1u : 0u;
-        const uint64_t n_px = (uint64_t)(y1 - y0) * (uint64_t)MW;
-        const uint64_t cap = n_px * ra.samples * ra.bounces;
-        RtQueue q{};
-        q.nls = (uint32_t)c->lights.size() * ra.shadow_iters;
-        q.nps = n_point * ra.shadow_iters;
-        q.rec_stride = 2 + (3 * q.nls + 3) / 4;
-        const uint64_t bytes = cap * (16ull * q.rec_stride + 32ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
-        const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
-                               bytes <= (uint64_t)(c->p("rt_queue_gb") * 1073741824.0);
-        if (wavefront) {
-            c->rt_rec.ensure(cap * 16ull * q.rec_stride);
-            c->rt_srec.ensure(cap * 32ull * q.nps);
-            c->rt_mask.ensure(cap * 4ull * q.nps);
-            c->rt_head.ensure((uint64_t)MW * MH * 4);
-            c->rt_count.ensure(16);
-            q.rec = c->rt_rec.as<float4>(); q.srec = c->rt_srec.as<float4>(); q.mask = c->rt_mask.as<float>();
-            q.head = c->rt_head.as<int>(); q.count = c->rt_count.as<uint32_t>(); q.cap = (uint32_t)cap;
-            launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
-                                      c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), (uint32_t)c->n_cus * 16, c->s_rt);
-        } else {
-            launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
-                            c->acc_depth.as<float>(), c->s_rt);
-        }
-    }
-    HIPCHK(hipEventRecord(c->ev_rt1, c->s_rt));
-    if (c->p("concurrent_streams") == 0.0) HIPCHK(hipStreamWaitEvent(c->s_nerf, c->ev_rt1, 0));
+        HIPCHK(hipEventRecord(c->ev_rt1, c->s_rt));
+
+
+        rt_enqueued = true;
+    };
+    if (rt_start_chunk <= 0) enqueue_raytracer(c->ev_start);
+    if (!concurrent) HIPCHK(hipStreamWaitEvent(c->s_nerf, c->ev_rt1, 0));
 
     // ---- NeRF (Testbed::render SyNeRFgine overload, testbed.cu:4353-4404)
     HIPCHK(hipEventRecord(c->ev_nerf0, c->s_nerf));
@@ -928,8 +943,13 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             }
             HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
             ++chunk;
+            if (!rt_enqueued && chunk == rt_start_chunk) enqueue_raytracer(c->ev_nerf1);
         }
         launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
+    }
+    if (!rt_enqueued) {
+        HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));
+        enqueue_raytracer(c->ev_rt_go);
     }
     HIPCHK(hipEventRecord(c->ev_shadow1, c->s_nerf));   // end of the trace
     if (shadows && !c->objs.empty()) {
@@ -1022,7 +1042,7 @@ void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_nerf, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_rt, hipStreamNonBlocking, prio_lo));
-    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end}) HIPCHK(hipEventCreate(e));
+    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go}) HIPCHK(hipEventCreate(e));
     HIPCHK(hipHostMalloc((void**)&c->h_ctrl, sizeof(MarchCtrl), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&c->h_alive, 4 * sizeof(uint32_t), hipHostMallocDefault));
     float rf = fov_to_focal(50.625f);   // Testbed::reset_camera -> set_fov(50.625) (testbed.cu:480)
@@ -1045,7 +1065,7 @@ void ctx_destroy(sng_ctx* c) {
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); }
-    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end}) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);
