@@ -161,6 +161,10 @@ int sng_get_focal_length(sng_ctx* ctx, int which /*0 nerf,1 mesh*/, float out[2]
 int sng_set_window(sng_ctx* ctx, int32_t width, int32_t height);
 int sng_get_resolution(sng_ctx* ctx, sng_resolution_info* out);
 int sng_render_frame(sng_ctx* ctx, const sng_frame_params* params, sng_frame_result* out);
+/* Testbed::render_nerf (testbed_nerf.cu:2679-2837): the instant-NGP tracer (NerfTracer::trace 2279-2401,
+ * composite_kernel_nerf 577-788, shade_kernel_nerf 1788-1828) into d_nerf_rgba / d_nerf_depth at NeRF
+ * resolution; parameters "render_mode" (ERenderMode) and "depth_scale".  row_begin/row_end are NeRF rows. */
+int sng_render_nerf_ngp(sng_ctx* ctx, const sng_frame_params* params, sng_frame_result* out);
 int sng_synchronize(sng_ctx* ctx);
 int sng_copy_to_host(sng_ctx* ctx, const void* d_src, void* h_dst, uint64_t n_bytes);
 /* device-to-device copy on the caller's stream (frame tiles -> collective buffers) */

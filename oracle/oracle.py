@@ -88,6 +88,7 @@ def lib():
             "orc_nerf_inference": (None, [vp, vp, u32, u32, vp]),
             "orc_density_grid_to_bitfield": (None, [vp, u32, vp, vp]),
             "orc_render_nerf": (None, [vp, vp, vp, vp, vp, vp, vp, vp]),
+            "orc_render_nerf_ngp": (None, [vp, vp, vp, i32, f32, vp, vp, vp]),
             "orc_shade_nerf_shadows": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, f32, f32, i32]),
             "orc_bvh_build": (i32, [vp, u32, u32, vp, u32]),
             "orc_depth_test_world": (None, [vp, u32, vp, vp, u32, vp, vp]),
@@ -237,6 +238,16 @@ def render_nerf(model, vol, cam):
     st = orc_nerf_stats()
     lib().orc_render_nerf(model.ref(), ctypes.byref(vol), ctypes.byref(cam), ptr(rgba), ptr(depth), ptr(pos), ptr(nrm), ctypes.byref(st))
     return rgba, depth, pos, nrm, st
+
+
+def render_nerf_ngp(model, vol, cam, render_mode=1, depth_scale=1.0):
+    """instant-NGP render path (A22): returns rgba [H,W,4], depth [H,W], stats."""
+    W, H = cam.res[0], cam.res[1]
+    rgba = np.zeros((H, W, 4), np.float32)
+    depth = np.zeros((H, W), np.float32)
+    st = orc_nerf_stats()
+    lib().orc_render_nerf_ngp(model.ref(), ctypes.byref(vol), ctypes.byref(cam), render_mode, depth_scale, ptr(rgba), ptr(depth), ctypes.byref(st))
+    return rgba, depth, st
 
 
 def frame_params_from_engine(eng):

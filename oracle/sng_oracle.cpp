@@ -919,8 +919,12 @@ void orc_density_grid_to_bitfield(const uint16_t* grid_f16, uint32_t max_cascade
 
 /* Testbed::render_nerf_with_buffers (testbed_nerf.cu:2467-2613) with
  * NerfTracer::init_rays_from_camera (2037-2120) and trace_alt (2128-2277). */
-void orc_render_nerf(const orc_model* m, const orc_volume* vdesc, const orc_camera* c,
-                     float* frame_rgba, float* frame_depth, float* positions, float* normals, orc_nerf_stats* stats) {
+/* ngp = 0: SyNeRFgine's trace_alt + composite_kernel_nerf_alt + extract_from_payload + normals.
+ * ngp = 1: instant-NGP's NerfTracer::trace (2279-2401) + composite_kernel_nerf (577-788) +
+ *          shade_kernel_nerf (1788-1828): depth at the max-weight sample, no payload.t reset,
+ *          render modes AO / Shade / Positions / Depth / Cost / EncodingVis. */
+static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const orc_camera* c, int ngp, int render_mode, float depth_scale,
+                             float* frame_rgba, float* frame_depth, float* positions, float* normals, orc_nerf_stats* stats) {
     Volume vol = make_volume(vdesc);
     Grid g = make_grid(m);
     const int W = c->res[0], H = c->res[1];
@@ -1037,9 +1041,19 @@ void orc_render_nerf(const orc_model* m, const orc_volume* vdesc, const orc_came
                 float alpha = 1.f - det_expf(-det_expf(h2f(o[3])) * dt);
                 float weight = alpha * T;
                 V3 rgb = v3(logistic(h2f(o[0])), logistic(h2f(o[1])), logistic(h2f(o[2])));
+                if (ngp) {
+                    if (render_mode == 3) rgb = (pos - 0.5f) / 2.0f + 0.5f;                                /* Positions */
+                    else if (render_mode == 10) rgb = v3(cc[0], cc[1], cc[2]);                             /* EncodingVis */
+                    else if (render_mode == 4) rgb = v3s(dot(cam_fwd, pos - p.origin) * depth_scale);      /* Depth */
+                    else if (render_mode == 0) rgb = v3s(alpha);                                           /* AO */
+                }
                 lr.x += rgb.x * weight; lr.y += rgb.y * weight; lr.z += rgb.z * weight; lr.w += weight;
-                ld = dot(cam_fwd, pos - cam_pos);
-                if (weight > p.max_weight) p.max_weight = weight;
+                if (ngp) {
+                    if (weight > p.max_weight) { p.max_weight = weight; ld = dot(cam_fwd, pos - cam_pos); }
+                } else {
+                    ld = dot(cam_fwd, pos - cam_pos);
+                    if (weight > p.max_weight) p.max_weight = weight;
+                }
                 if (lr.w > (1.0f - vol.min_transmittance)) {
                     float a = lr.w;
                     lr.x /= a; lr.y /= a; lr.z /= a; lr.w /= a;
@@ -1049,7 +1063,7 @@ void orc_render_nerf(const orc_model* m, const orc_volume* vdesc, const orc_came
             if (j < n_steps) { p.alive = false; p.n_steps = (uint16_t)(j + i_step); }
             r.rgba = lr;
             r.depth = ld;
-            p.t = ld / dot(cam_fwd, p.dir);
+            if (!ngp) p.t = ld / dot(cam_fwd, p.dir);   /* composite_kernel_nerf_alt:574; trace keeps generate's t */
         }
         src = &current;
         std::vector<RayState> tmp = current; /* next compaction reads this buffer */
@@ -1059,6 +1073,22 @@ void orc_render_nerf(const orc_model* m, const orc_volume* vdesc, const orc_came
     }
     if (stats) { stats->n_iterations = iter; stats->n_hit = (uint32_t)hit.size(); }
 
+    if (ngp) {
+        /* shade_kernel_nerf 1788-1828 (gbuffer_hard_edges = false, train_in_linear_colors = false) */
+        for (const RayState& r : hit) {
+            const Payload& p = r.p;
+            V4 tmp = r.rgba;
+            if (render_mode == 6) { float col = (float)p.n_steps / 128; tmp = {col, col, col, 1.0f}; }   /* Cost */
+            if (render_mode == 1) { tmp.x = srgb_to_linear(tmp.x); tmp.y = srgb_to_linear(tmp.y); tmp.z = srgb_to_linear(tmp.z); }
+            float* fb = &frame_rgba[4 * (size_t)p.idx];
+            fb[0] = tmp.x + fb[0] * (1.0f - tmp.w);
+            fb[1] = tmp.y + fb[1] * (1.0f - tmp.w);
+            fb[2] = tmp.z + fb[2] * (1.0f - tmp.w);
+            fb[3] = tmp.w + fb[3] * (1.0f - tmp.w);
+            if (tmp.w > 0.2f) frame_depth[p.idx] = r.depth;
+        }
+        return;
+    }
     /* extract_from_payload 1578-1612 (Shade mode) */
     for (const RayState& r : hit) {
         const Payload& p = r.p;
@@ -1453,3 +1483,14 @@ int32_t orc_num_threads(void) {
 }
 
 }  // extern "C"
+
+void orc_render_nerf(const orc_model* m, const orc_volume* v, const orc_camera* c, float* frame_rgba, float* frame_depth, float* positions,
+                     float* normals, orc_nerf_stats* stats) {
+    render_nerf_impl(m, v, c, 0, 1, 1.0f, frame_rgba, frame_depth, positions, normals, stats);
+}
+void orc_render_nerf_ngp(const orc_model* m, const orc_volume* v, const orc_camera* c, int32_t render_mode, float depth_scale, float* frame_rgba,
+                         float* frame_depth, orc_nerf_stats* stats) {
+    const int W = c->res[0], H = c->res[1];
+    std::vector<float> pos((size_t)W * H * 3), nrm((size_t)W * H * 3);
+    render_nerf_impl(m, v, c, 1, render_mode, depth_scale, frame_rgba, frame_depth, pos.data(), nrm.data(), stats);
+}

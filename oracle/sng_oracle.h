@@ -128,6 +128,11 @@ void orc_render_nerf(const orc_model* m, const orc_volume* v, const orc_camera* 
                      orc_nerf_stats* stats);
 
 /* ---- shadows on NeRF (A11) ---------------------------------------------- */
+/* instant-NGP render path (A22): NerfTracer::trace + composite_kernel_nerf + shade_kernel_nerf
+ * (testbed_nerf.cu:2279-2401, 577-788, 1788-1828).  render_mode: ERenderMode (0 AO, 1 Shade,
+ * 3 Positions, 4 Depth, 6 Cost, 10 EncodingVis); depth_scale = 1 / dataset.scale. */
+void orc_render_nerf_ngp(const orc_model* m, const orc_volume* v, const orc_camera* c, int32_t render_mode, float depth_scale,
+                         float* frame_rgba /* W*H*4 */, float* frame_depth /* W*H */, orc_nerf_stats* stats);
 void orc_shade_nerf_shadows(const orc_volume* v, const int32_t res[2],
                             float* frame_rgba, const float* positions, const float* normals,
                             const orc_object* objs, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,

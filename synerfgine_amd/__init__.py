@@ -181,6 +181,18 @@ class Engine:
         check(self._lib.sng_render_frame(self.ctx, ctypes.byref(p), ctypes.byref(r)))
         return FrameResult(self, r)
 
+    def render_nerf(self, spp=0, reset=True, rows=None, render_mode=None, collect_kernel_times=False, target_n_queries=0):
+        """Testbed::render_nerf: the instant-NGP tracer (composite_kernel_nerf + shade_kernel_nerf), NeRF only."""
+        if render_mode is not None:
+            self.set_param("render_mode", render_mode)
+        p = _lib.sng_frame_params(spp=spp, reset_accumulation=1 if reset else 0, collect_kernel_times=1 if collect_kernel_times else 0,
+                                  target_n_queries=target_n_queries)
+        if rows is not None:
+            p.row_begin, p.row_end = rows
+        r = _lib.sng_frame_result()
+        check(self._lib.sng_render_nerf_ngp(self.ctx, ctypes.byref(p), ctypes.byref(r)))
+        return FrameResult(self, r)
+
     # ---- scene inspection (tests) --------------------------------------------------
     def scene(self):
         no, nl, nm = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()

@@ -152,6 +152,7 @@ SIGNATURES = {
     "sng_set_window": (ctypes.c_int, [P, I32, I32]),
     "sng_get_resolution": (ctypes.c_int, [P, ctypes.POINTER(sng_resolution_info)]),
     "sng_render_frame": (ctypes.c_int, [P, ctypes.POINTER(sng_frame_params), ctypes.POINTER(sng_frame_result)]),
+    "sng_render_nerf_ngp": (ctypes.c_int, [P, ctypes.POINTER(sng_frame_params), ctypes.POINTER(sng_frame_result)]),
     "sng_synchronize": (ctypes.c_int, [P]),
     "sng_copy_to_host": (ctypes.c_int, [P, P, P, U64]),
     "sng_copy_device": (ctypes.c_int, [P, P, P, U64, P]),

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -321,7 +322,9 @@ const std::map<std::string, double>& default_params() {
         {"fast_slab", 1},
         {"rt_wavefront", 1},
         {"scene_lds", 1},
-        {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost                       // BVH nodes + triangles staged in LDS per workgroup when they fit                    // deferred shadow-ray queues for the path tracer
+        {"rt_tile_order", 1},
+        {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
+        {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)                   // visit raytracer tiles in descending previous-frame cost                       // BVH nodes + triangles staged in LDS per workgroup when they fit                    // deferred shadow-ray queues for the path tracer
         {"rt_queue_gb", 48},                    // device-memory budget for those queues                       // exact reciprocal-multiply BVH box tests                  // exact unit-cube fast path of the occupancy march
     };
     return d;
@@ -370,7 +373,7 @@ struct sng_ctx {
 
     // buffers
     DevBuf nerf_rgba, nerf_depth, nerf_pos, nerf_nrm;
-    DevBuf ray_ot[2], ray_di[2], ray_rgba[2], ray_depth[2];
+    DevBuf ray_ot[2], ray_di[2], ray_rgba[2], ray_depth[2], ray_mw[2];
     DevBuf samp, coords, net_out, ctrl;
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
@@ -727,6 +730,7 @@ void resize(sng_ctx* c) {
         c->ray_di[b].ensure(nn * 16);
         c->ray_rgba[b].ensure(nn * 16);
         c->ray_depth[b].ensure(nn * 4);
+        c->ray_mw[b].ensure(nn * 4);
     }
     c->samp.ensure(nn * 8);
     c->ray_cap = nn;
@@ -767,6 +771,72 @@ f2 focal_for(const sng_ctx* c, const int res[2]) {
 }
 f2 render_screen_center(const sng_ctx* c) {
     return {(0.5f - c->screen_center[0]) * c->zoom + 0.5f, (0.5f - c->screen_center[1]) * c->zoom + 0.5f};
+}
+
+// NerfTracer::init_rays_from_camera + trace_alt / trace (testbed_nerf.cu:2037-2401) for NeRF rows
+// [tr0, tr1): device-driven wavefront, host readback of the alive count once per CHUNK iterations.
+// on_chunk(k) runs after the k-th chunk is enqueued (render_frame starts the raytracer there).
+// Returns the number of network launches.
+uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, const CamDev& cam, f2 sc, int tr0, int tr1, TraceMode mode,
+                    uint32_t target, const std::function<void(int)>& on_chunk) {
+    const int NW = c->nerf_res[0], NH = c->nerf_res[1];
+    uint32_t net_launches = 0;
+    MarchCtrl* ctrl = c->ctrl.as<MarchCtrl>();
+    launch_ctrl_init(ctrl, c->s_nerf);
+    NerfFrameArgs a{};
+    a.vol = vol;
+    a.cam = cam;
+    m3 rot = {cam.c0, cam.c1, cam.c2};
+    a.ray_rot = rolling_shutter_rotation(rot);
+    const int nres[2] = {NW, NH};
+    a.focal = focal_for(c, nres);
+    a.screen_center = sc;
+    a.W = NW; a.H = NH; a.row0 = tr0; a.row1 = tr1;
+    a.spp = P.spp;
+    a.snap = 0;
+    a.reset = P.reset_accumulation ? 1 : 0;
+    a.target_n_queries = target;
+    a.mode = mode;
+    RayBuf rb[2];
+    for (int b = 0; b < 2; ++b)
+        rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>()};
+    launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
+    const uint32_t n_band = (uint32_t)(tr1 - tr0) * (uint32_t)NW;
+    const uint32_t blocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
+    const uint32_t max_tiles = (uint32_t)((c->sample_cap + 15) / 16);
+    const int CHUNK = 4;
+    int p = 0;
+    uint32_t iter = 0;
+    int chunk = 0;
+    bool done = false;
+    while (!done && iter < MARCH_ITER) {
+        for (int k = 0; k < CHUNK; ++k, ++iter) {
+            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, mode.ngp, c->s_nerf);
+            if (P.collect_kernel_times) {
+                while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
+                HIPCHK(hipEventRecord(c->net_events[2 * net_launches], c->s_nerf));
+            }
+            launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf);
+            if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->net_events[2 * net_launches + 1], c->s_nerf));
+            ++net_launches;
+            launch_composite(vol, cam, mode, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
+                             c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf);
+            p ^= 1;
+        }
+        // readback of the alive count after this chunk; check the previous chunk's (already landed)
+        HIPCHK(hipMemcpyAsync(&c->h_alive[2 * (chunk & 1)], &ctrl->n_alive[0], 8, hipMemcpyDeviceToHost, c->s_nerf));
+        HIPCHK(hipGetLastError());
+        if (chunk > 0) {
+            // wait for the previous chunk's readback (the current chunk stays queued behind it)
+            HIPCHK(hipEventSynchronize(c->ev_nerf1));
+            const uint32_t* h = &c->h_alive[2 * ((chunk - 1) & 1)];
+            if (h[0] == 0 && h[1] == 0) done = true;
+        }
+        HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
+        ++chunk;
+        on_chunk(chunk);
+    }
+    return net_launches;
 }
 
 void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out) {
@@ -892,59 +962,10 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     HIPCHK(hipEventRecord(c->ev_nerf0, c->s_nerf));
     uint32_t net_launches = 0;
     if (show_nerf) {
-        MarchCtrl* ctrl = c->ctrl.as<MarchCtrl>();
-        launch_ctrl_init(ctrl, c->s_nerf);
-        NerfFrameArgs a{};
-        a.vol = vol;
-        a.cam = cam;
-        m3 rot = {cam.c0, cam.c1, cam.c2};
-        a.ray_rot = rolling_shutter_rotation(rot);
-        const int nres[2] = {NW, NH};
-        a.focal = focal_for(c, nres);
-        a.screen_center = sc;
-        a.W = NW; a.H = NH; a.row0 = tr0; a.row1 = tr1;
-        a.spp = P.spp;
-        a.snap = 0;
-        a.reset = P.reset_accumulation ? 1 : 0;
-        a.target_n_queries = target;
-        RayBuf rb[2];
-        for (int b = 0; b < 2; ++b) rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>()};
-        launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
-        const uint32_t n_band = (uint32_t)(tr1 - tr0) * (uint32_t)NW;
-        const uint32_t blocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
-        const uint32_t max_tiles = (uint32_t)((c->sample_cap + 15) / 16);
-        const int CHUNK = 4;
-        int p = 0;
-        uint32_t iter = 0;
-        int chunk = 0;
-        bool done = false;
-        while (!done && iter < MARCH_ITER) {
-            for (int k = 0; k < CHUNK; ++k, ++iter) {
-                launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, c->s_nerf);
-                if (P.collect_kernel_times) {
-                    while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
-                    HIPCHK(hipEventRecord(c->net_events[2 * net_launches], c->s_nerf));
-                }
-                launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf);
-                if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->net_events[2 * net_launches + 1], c->s_nerf));
-                ++net_launches;
-                launch_composite(vol, cam, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
-                                 c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf);
-                p ^= 1;
-            }
-            // readback of the alive count after this chunk; check the previous chunk's (already landed)
-            HIPCHK(hipMemcpyAsync(&c->h_alive[2 * (chunk & 1)], &ctrl->n_alive[0], 8, hipMemcpyDeviceToHost, c->s_nerf));
-            HIPCHK(hipGetLastError());
-            if (chunk > 0) {
-                // wait for the previous chunk's readback (the current chunk stays queued behind it)
-                HIPCHK(hipEventSynchronize(c->ev_nerf1));
-                const uint32_t* h = &c->h_alive[2 * ((chunk - 1) & 1)];
-                if (h[0] == 0 && h[1] == 0) done = true;
-            }
-            HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
-            ++chunk;
+        TraceMode mode{0, 1, 1.0f};
+        net_launches = trace_nerf(c, P, vol, cam, sc, tr0, tr1, mode, target, [&](int chunk) {
             if (!rt_enqueued && chunk == rt_start_chunk) enqueue_raytracer(c->ev_nerf1);
-        }
+        });
         launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
     }
     if (!rt_enqueued) {
@@ -1025,6 +1046,62 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     }
 }
 
+// Testbed::render_nerf (testbed_nerf.cu:2679-2837): the instant-NGP render path --
+// NerfTracer::trace + composite_kernel_nerf + shade_kernel_nerf into the NeRF frame buffer, with
+// ERenderMode "render_mode" (0 AO, 1 Shade, 3 Positions, 4 Depth, 6 Cost, 10 EncodingVis) and
+// "depth_scale" (1 / dataset.scale).  NeRF only: no mesh, shadows or overlay.
+void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out) {
+    if (c->win[0] <= 0) throw SngError(SNG_ERR_STATE, "sng_set_window first");
+    if ((int)c->p("res_factor") != c->last_res_factor) resize(c);
+    if (!(c->has_model && c->has_bitfield)) throw SngError(SNG_ERR_STATE, "no NeRF model/density grid loaded");
+    const int rm = (int)c->p("render_mode");
+    if (!(rm == 0 || rm == 1 || rm == 3 || rm == 4 || rm == 6 || rm == 10))
+        throw SngError(SNG_ERR_INVALID, "render_mode " + std::to_string(rm) + " is not supported by the instant-NGP path (AO, Shade, Positions, Depth, Cost, EncodingVis)");
+    sng_frame_params P{};
+    if (fp) P = *fp;
+    const uint32_t target = P.target_n_queries ? P.target_n_queries : 2u * 1024u * 1024u;
+    ensure_samples(c, target);
+    const int NH = c->nerf_res[1];
+    int r0 = P.row_begin, r1 = P.row_end;
+    if (r0 == 0 && r1 == 0) { r0 = 0; r1 = NH; }
+    if (r0 < 0 || r1 > NH || r0 >= r1) throw SngError(SNG_ERR_INVALID, "bad row band");
+    const Volume vol = make_volume(c);
+    const CamDev cam = cam_dev(c);
+    const f2 sc = render_screen_center(c);
+    const TraceMode mode{1, rm, (float)c->p("depth_scale")};
+    HIPCHK(hipEventRecord(c->ev_start, c->s_nerf));
+    HIPCHK(hipEventRecord(c->ev_nerf0, c->s_nerf));
+    const uint32_t net_launches = trace_nerf(c, P, vol, cam, sc, r0, r1, mode, target, [](int) {});
+    HIPCHK(hipEventRecord(c->ev_end, c->s_nerf));
+    HIPCHK(hipMemcpyAsync(c->h_ctrl, c->ctrl.p, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->s_nerf));
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        out->d_nerf_rgba = c->nerf_rgba.as<float>();
+        out->d_nerf_depth = c->nerf_depth.as<float>();
+        out->n_iterations = c->h_ctrl->n_iter;
+        out->n_hit = c->h_ctrl->n_hit;
+        out->n_samples = c->h_ctrl->total_samples;
+        out->n_reference_slots = c->h_ctrl->ref_slots;
+        std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
+        std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
+        std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
+        HIPCHK(hipEventElapsedTime(&out->ms_frame, c->ev_start, c->ev_end));
+        out->ms_nerf = out->ms_frame;
+        if (P.collect_kernel_times) {
+            float tot = 0.0f;
+            for (uint32_t k = 0; k < net_launches; ++k) {
+                float ms = 0.0f;
+                HIPCHK(hipEventElapsedTime(&ms, c->net_events[2 * k], c->net_events[2 * k + 1]));
+                tot += ms;
+            }
+            out->ms_network = tot;
+        }
+        out->network_launches = net_launches;
+    }
+}
+
 void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw SngError(SNG_ERR_NOGPU, "no HIP device visible");
@@ -1064,7 +1141,7 @@ void ctx_destroy(sng_ctx* c) {
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
-    for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); }
+    for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);
@@ -1350,6 +1427,9 @@ int sng_get_resolution(sng_ctx* c, sng_resolution_info* out) {
         out->mesh_res[0] = c->mesh_res[0]; out->mesh_res[1] = c->mesh_res[1];
         out->syn_px_scale = c->vo_scale_eff;
     });
+}
+int sng_render_nerf_ngp(sng_ctx* c, const sng_frame_params* p, sng_frame_result* out) {
+    return guarded([&] { HIPCHK(hipSetDevice(c->device)); render_nerf_ngp(c, p, out); });
 }
 int sng_render_frame(sng_ctx* c, const sng_frame_params* p, sng_frame_result* out) {
     return guarded([&] { HIPCHK(hipSetDevice(c->device)); render_frame(c, p, out); });

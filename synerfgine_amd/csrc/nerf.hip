@@ -95,6 +95,7 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
         out.d_idx[slot] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(idx));
         out.rgba[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // memset(m_rays[0].rgba) 2102
         out.depth[slot] = 0.0f;                                // memset(m_rays[0].depth) 2103
+        if (a.mode.ngp) out.mw[slot] = 0.0f;                   // payload.max_weight = 0 (1964)
     }
 }
 
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
 // bitfield gathers).  The general path (cascades / cone stepping) keeps the unrolled form.
 template <bool LIN>
 __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
-                                                       float* __restrict__ coords, uint2* __restrict__ samp) {
+                                                       float* __restrict__ coords, uint2* __restrict__ samp, int store_t) {
     __shared__ float ts_lds[LIN ? MAX_STEPS_BETWEEN_COMPACTION * 256 : 1];
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t i_step = ctrl->i_step[p];
@@ -172,6 +173,9 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
                     }
                 }
             }
+            // NerfTracer::trace keeps generate's t (payload.t = t after n_steps samples, 836);
+            // trace_alt overwrites it in the compositor
+            if (store_t && cnt == n_steps) reinterpret_cast<float*>(rays.o_t + i)[3] = t;
         }
         const uint32_t incl = wave_incl_scan(cnt, lane);
         uint32_t base = 0;
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
 // composite_kernel_nerf_alt (476-575) + compaction into the next buffer
 // (compact_kernel_nerf 1830-1853) + extract_from_payload (1578-1612)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
+__global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, TraceMode mode, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                                                         const float* __restrict__ coords, const uint2* __restrict__ samp,
                                                         const uint2* __restrict__ net_out, float4* __restrict__ frame_rgba,
                                                         float* __restrict__ frame_depth, float* __restrict__ positions) {
@@ -235,12 +239,14 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
         const uint32_t i = base_i + lane;
         bool survive = false, hit = false;
         float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
-        float depth = 0.0f;
+        float depth = 0.0f, mw = 0.0f;
+        uint32_t death_step = 0;
         if (i < n_alive) {
             rgba = in.rgba[i];
             depth = in.depth[i];
             ot = in.o_t[i];
             di = in.d_idx[i];
+            if (mode.ngp) mw = in.mw[i];
             const uint2 sc = samp[i];
             uint32_t j = 0;
             for (; j < sc.y; ++j) {
@@ -255,11 +261,22 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
                 const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
                 const float alpha = 1.f - sng_expf(-sng_expf(s) * dt);
                 const float weight = alpha * T;
-                rgba.x += logistic(r) * weight;
-                rgba.y += logistic(g) * weight;
-                rgba.z += logistic(b) * weight;
+                f3 rgb = mk(logistic(r), logistic(g), logistic(b));
+                if (mode.ngp) {   // composite_kernel_nerf render modes (testbed_nerf.cu:709-723)
+                    if (mode.render_mode == 3) rgb = (pos - 0.5f) / 2.0f + 0.5f;
+                    else if (mode.render_mode == 10) rgb = mk(c[0], c[1], c[2]);
+                    else if (mode.render_mode == 4) rgb = splat(dot(cam.c2, pos - mk(ot.x, ot.y, ot.z)) * mode.depth_scale);
+                    else if (mode.render_mode == 0) rgb = splat(alpha);
+                }
+                rgba.x += rgb.x * weight;
+                rgba.y += rgb.y * weight;
+                rgba.z += rgb.z * weight;
                 rgba.w += weight;
-                depth = dot(cam.c2, pos - cam.c3);
+                if (mode.ngp) {   // depth of the max-weight sample (738-742)
+                    if (weight > mw) { mw = weight; depth = dot(cam.c2, pos - cam.c3); }
+                } else {
+                    depth = dot(cam.c2, pos - cam.c3);
+                }
                 if (rgba.w > (1.0f - vol.min_transmittance)) {
                     const float aa = rgba.w;
                     rgba.x /= aa; rgba.y /= aa; rgba.z /= aa; rgba.w /= aa;
@@ -267,8 +284,8 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
                 }
             }
             const f3 dir = mk(di.x, di.y, di.z);
-            ot.w = depth / dot(cam.c2, dir);   // payload.t reset (576)
-            if (j < n_steps) hit = !last && rgba.w > 0.001f;
+            if (!mode.ngp) ot.w = depth / dot(cam.c2, dir);   // payload.t reset (576); trace keeps generate's t
+            if (j < n_steps) { hit = !last && rgba.w > 0.001f; death_step = j + i_step; }
             else survive = !last;
         }
         const uint32_t slot = wave_append(&ctrl->n_alive[p ^ 1], survive, lane);
@@ -277,8 +294,19 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
             out.d_idx[slot] = di;
             out.rgba[slot] = rgba;
             out.depth[slot] = depth;
+            if (mode.ngp) out.mw[slot] = mw;
         }
-        if (hit) {
+        if (hit && mode.ngp) {
+            // shade_kernel_nerf (1788-1828), gbuffer_hard_edges = false, train_in_linear_colors = false
+            const uint32_t idx = __float_as_uint(di.w);
+            float4 tmp = rgba;
+            if (mode.render_mode == 6) { const float col = (float)death_step / 128; tmp = make_float4(col, col, col, 1.0f); }
+            if (mode.render_mode == 1) { tmp.x = srgb_to_linear(tmp.x); tmp.y = srgb_to_linear(tmp.y); tmp.z = srgb_to_linear(tmp.z); }
+            float4 fb = frame_rgba[idx];
+            fb = make_float4(tmp.x + fb.x * (1.0f - tmp.w), tmp.y + fb.y * (1.0f - tmp.w), tmp.z + fb.z * (1.0f - tmp.w), tmp.w + fb.w * (1.0f - tmp.w));
+            frame_rgba[idx] = fb;
+            if (tmp.w > 0.2f) frame_depth[idx] = depth;
+        } else if (hit) {
             const uint32_t idx = __float_as_uint(di.w);
             const f3 dir = mk(di.x, di.y, di.z);
             const f3 orig = cam.c3 + dir * ot.w;
@@ -410,14 +438,14 @@ void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl
     hipLaunchKernelGGL(init_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, out, ctrl, fb, depth, pos, nrm);
 }
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
-                     uint32_t blocks, hipStream_t s) {
-    if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp);
-    else hipLaunchKernelGGL(generate_kernel<false>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp);
+                     uint32_t blocks, int store_t, hipStream_t s) {
+    if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t);
+    else hipLaunchKernelGGL(generate_kernel<false>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t);
 }
-void launch_composite(const Volume& v, const CamDev& cam, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
+void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                       const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
                       hipStream_t s) {
-    hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, s, v, cam, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
+    hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, s, v, cam, mode, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
 }
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;

@@ -47,6 +47,16 @@ struct RayBuf {
     float4* d_idx;     // dir.xyz, pixel index (bits)
     float4* rgba;
     float* depth;
+    float* mw;         // payload.max_weight (instant-NGP trace path only)
+};
+
+// Which NeRF tracer runs: SyNeRFgine's trace_alt (ngp = 0: depth of the last sample,
+// payload.t reset to it, extract_from_payload) or instant-NGP's trace (ngp = 1: depth of the
+// max-weight sample, no t reset, shade_kernel_nerf with ERenderMode render_mode).
+struct TraceMode {
+    int ngp;
+    int render_mode;     // ERenderMode: 0 AO, 1 Shade, 3 Positions, 4 Depth, 6 Cost, 10 EncodingVis
+    float depth_scale;   // 1 / dataset.scale
 };
 
 struct CamDev {
@@ -65,6 +75,7 @@ struct NerfFrameArgs {
     int snap;
     int reset;           // clear alpha of the frame buffer (camera moved)
     uint32_t target_n_queries;
+    TraceMode mode;
 };
 
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
@@ -122,8 +133,8 @@ struct RtQueue {
 // nerf.hip
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, hipStream_t s);
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
-                     uint32_t blocks, hipStream_t s);
-void launch_composite(const Volume& v, const CamDev& cam, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
+                     uint32_t blocks, int store_t, hipStream_t s);
+void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                       const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
                       hipStream_t s);
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s);

@@ -304,3 +304,37 @@ def test_load_snapshot_equals_direct_model(tmp_path):
             tb2.close()
     finally:
         tb.close()
+
+
+@pytest.mark.parametrize("render_mode", [1, 0, 3, 4, 6, 10])
+def test_instant_ngp_render_path_matches_oracle(render_mode):
+    """SURVEY A22: Testbed::render_nerf (NerfTracer::trace + composite_kernel_nerf + shade_kernel_nerf) per ERenderMode."""
+    import oracle as O
+    tb, eng, (cfg, params, grid) = _engine(128, 72, {"show_virtual_obj": 0, "shadow_on_nerf": 0})
+    try:
+        eng.set_param("depth_scale", 3.0)
+        r = eng.render_nerf(render_mode=render_mode)
+        got = r.download("nerf_rgba")
+        gd = r.download("nerf_depth")[..., 0]
+        res = eng.resolution()["nerf"]
+        cam = O.make_camera(tb.camera_matrix, tb.focal_length(0), res)
+        ref, rd, st = O.render_nerf_ngp(O.Model(cfg, params), O.volume_for(cfg, grid), cam, render_mode, 3.0)
+        assert r.n_iterations == st.n_iterations
+        assert list(r.alive_per_iter) == list(st.alive_per_iter)[: st.n_iterations]
+        assert r.n_samples == st.n_samples and r.n_hit == st.n_hit
+        err = np.abs(got - ref).max(axis=-1)
+        assert (err <= 2e-3).mean() >= 0.995, f"max err {err.max()}"
+        dmask = (rd < 1e4) & (gd < 1e4)
+        assert (np.abs(gd - rd)[dmask] <= 1e-3 * np.maximum(1.0, rd[dmask])).mean() >= 0.995
+    finally:
+        tb.close()
+
+
+def test_instant_ngp_rejects_unsupported_modes():
+    from synerfgine_amd import SngError
+    tb, eng, _ = _engine(32, 18, {"show_virtual_obj": 0})
+    try:
+        with pytest.raises(SngError):
+            eng.render_nerf(render_mode=2)   # Normals needs network input gradients
+    finally:
+        tb.close()
