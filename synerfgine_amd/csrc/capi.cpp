@@ -316,16 +316,17 @@ const std::map<std::string, double>& default_params() {
         {"srgb", 1},                            // EColorSpace::SRGB passed to overlay (engine.cu:406)
         {"smooth_threshold", 1.0},              // sng_position_kernel_threshold (unused by the path)
         {"max_shadow_variance", 0.0},           // sng_shadow_depth_variance (unused by the path)
-        {"concurrent_streams", 1},
-        {"rt_start_chunk", 1},                  // concurrent mode: raytracer starts after this many 4-iteration NeRF chunks              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
-        {"linear_marcher", 1},
-        {"fast_slab", 1},
-        {"rt_wavefront", 1},
-        {"scene_lds", 1},
-        {"rt_tile_order", 1},
+        {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
+        {"rt_start_chunk", 1},                  // concurrent mode: raytracer starts after this many 4-iteration NeRF chunks
+        {"rt_reserved_cus", 16},                // concurrent mode: CUs (2 per XCD) the persistent raytracer grids leave to the NeRF stream
+        {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
+        {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
+        {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
+        {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
+        {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
-        {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)                   // visit raytracer tiles in descending previous-frame cost                       // BVH nodes + triangles staged in LDS per workgroup when they fit                    // deferred shadow-ray queues for the path tracer
-        {"rt_queue_gb", 48},                    // device-memory budget for those queues                       // exact reciprocal-multiply BVH box tests                  // exact unit-cube fast path of the occupancy march
+        {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)
+        {"rt_queue_gb", 48},                    // device-memory budget for the deferred-shadow queues
     };
     return d;
 }
@@ -907,7 +908,10 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             // max stack use of the reference traversal is depth + 1; FixedStack<32> drops pushes at 31
             ra.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
             ra.scene_in_lds = (c->p("scene_lds") != 0.0 && (uint64_t)c->scene_f4 * 16 + (uint64_t)ra.stack_depth * 512 * 4 <= 80u * 1024u) ? 1 : 0;
-            ra.persistent_blocks = (uint32_t)c->n_cus;
+            // persistent raytracer grids leave `rt_reserved_cus` CUs' worth of room for the NeRF
+            // wavefront running beside them on the other stream (concurrent mode only)
+            const int reserve = concurrent && show_nerf ? (int)c->p("rt_reserved_cus") : 0;
+            ra.persistent_blocks = (uint32_t)std::max(1, c->n_cus - std::max(0, reserve));
             c->rt_work.ensure(16);
             ra.work = c->rt_work.as<uint32_t>();
             if (c->p("rt_tile_order") != 0.0) {

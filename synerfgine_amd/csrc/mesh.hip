@@ -428,7 +428,7 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
 // only ~15 % of the pixels hit an object and those cost ~100x the others).  Square tiles keep a
 // wave's primary rays coherent (fewer hit/miss-divergent waves than 64-pixel row segments).
 template <bool DEFER, bool LDS>
-__global__ __launch_bounds__(512) void raytrace_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void raytrace_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins,
                                                         const float4* __restrict__ dirs, uint32_t* __restrict__ rng, uint32_t n_rng,
                                                         float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
     const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
@@ -619,9 +619,10 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     if (!n) return;
     (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);   // errors surface through hipGetLastError in the caller
     (void)hipMemsetAsync(a.work, 0, 2 * sizeof(uint32_t), s);
-    // path kernel: ~160 VGPRs -> 3 waves/SIMD = 768 threads/CU: 2 x 384-thread workgroups
+    // path kernel: capped at 128 VGPRs (amdgpu_waves_per_eu(4), a few spills) -> 4 waves/SIMD = 2 x 512-thread workgroups;
+    // measured faster than 3 waves/SIMD without spills
     // shadow kernel: ~100 VGPRs -> 5 waves/SIMD; LDS-bound at 2 x 512-thread workgroups
-    const uint32_t tp = 384, ts = 512;
+    const uint32_t tp = 512, ts = 512;
     const bool lds = a.scene_in_lds != 0;
     const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
     const uint32_t bp = std::min((n + tp - 1) / tp, a.persistent_blocks * 2);
