@@ -151,7 +151,10 @@ def main():
     # dominant kernel: fused hash-grid + MLP, timed with hipEvents on its own stream over the timed region
     ms_net = sum(s.ms_network for s in stats)
     launches = sum(s.network_launches for s in stats)
-    samples = sum(s.n_samples for s in stats)
+    # samples evaluated by the network kernel: one launch per wavefront iteration; the ray-local
+    # tail (fused.hip) evaluates the remaining iterations' samples inside its own kernel
+    samples = sum(sum(s.samples_per_iter[: s.network_launches]) for s in stats)
+    tail_samples = sum(s.n_samples for s in stats) - samples
     avg_launch_ms = ms_net / max(1, launches)
     bytes_per_launch = samples * BYTES_PER_SAMPLE / max(1, launches)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
@@ -195,6 +198,7 @@ def main():
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
                          "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
+                         "samples_in_launches": int(samples), "samples_in_fused_tail": int(tail_samples),
                          "timing": "hipEvents around every launch on the NeRF stream over the timed region" +
                                    ("" if args.serial_streams else "; the kernel shares the GPU with the raytracer stream, so this is the "
                                     "contended duration (uncontended: --serial-streams)"),

@@ -327,6 +327,9 @@ const std::map<std::string, double>& default_params() {
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)
         {"rt_queue_gb", 48},                    // device-memory budget for the deferred-shadow queues
+        {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
+        {"nerf_fused_after", 4},                // ... after this many whole-GPU wavefront iterations
+        {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
     };
     return d;
 }
@@ -380,6 +383,9 @@ struct sng_ctx {
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
     DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
+    DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
+    bool fused_last = false;               // the last trace finished in the fused kernel
+    uint32_t fused_k0 = 0;                 // ... from this iteration on
     uint64_t rt_tile_key = 0;             // band geometry the costs belong to
     DevBuf rng_nerf, rng_mesh;
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
@@ -774,6 +780,15 @@ f2 render_screen_center(const sng_ctx* c) {
     return {(0.5f - c->screen_center[0]) * c->zoom + 0.5f, (0.5f - c->screen_center[1]) * c->zoom + 0.5f};
 }
 
+// slots the reference would evaluate: sum over iterations of n_alive * n_steps padded to 256
+// (testbed_nerf.cu:2210); the fused kernel only records the per-iteration alive counts
+uint64_t ref_slots_of(const sng_ctx* c) {
+    uint64_t s = c->h_ctrl->ref_slots;   // accumulated by generate_kernel for the wavefront iterations
+    if (!c->fused_last) return s;
+    for (uint32_t k = c->fused_k0; k < std::min<uint32_t>(64u, c->h_ctrl->n_iter); ++k) s += ((uint64_t)c->h_ctrl->alive_hist[k] * 8 + 255) / 256 * 256;
+    return s;
+}
+
 // NerfTracer::init_rays_from_camera + trace_alt / trace (testbed_nerf.cu:2037-2401) for NeRF rows
 // [tr0, tr1): device-driven wavefront, host readback of the alive count once per CHUNK iterations.
 // on_chunk(k) runs after the k-th chunk is enqueued (render_frame starts the raytracer there).
@@ -803,6 +818,20 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>()};
     launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
     const uint32_t n_band = (uint32_t)(tr1 - tr0) * (uint32_t)NW;
+    c->fused_last = false;
+    c->fused_k0 = 0;
+    // Hybrid schedule (fused.hip): the first `nerf_fused_after` iterations run as whole-GPU
+    // wavefront launches (nearly every ray alive: throughput bound), the rest -- the latency-bound
+    // tail -- in the ray-local fused kernel.  Valid when every iteration takes 8 steps, i.e. the
+    // initial alive count satisfies n_alive * 8 <= target (it only shrinks).
+    bool fuse = false;
+    uint32_t fuse_after = 0;
+    if (c->p("nerf_fused") != 0.0) {
+        HIPCHK(hipMemcpyAsync(c->h_alive, &ctrl->n_alive[0], 4, hipMemcpyDeviceToHost, c->s_nerf));
+        HIPCHK(hipStreamSynchronize(c->s_nerf));
+        fuse = (uint64_t)c->h_alive[0] * MAX_STEPS_BETWEEN_COMPACTION <= target;
+        fuse_after = (uint32_t)std::max(0.0, c->p("nerf_fused_after"));
+    }
     const uint32_t blocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
     const uint32_t max_tiles = (uint32_t)((c->sample_cap + 15) / 16);
     const int CHUNK = 4;
@@ -811,7 +840,25 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     int chunk = 0;
     bool done = false;
     while (!done && iter < MARCH_ITER) {
-        for (int k = 0; k < CHUNK; ++k, ++iter) {
+        if (fuse && iter >= fuse_after) {
+            c->fused_work.ensure(16);
+            FusedArgs fa{};
+            fa.vol = vol; fa.cam = cam; fa.mode = mode; fa.rays = rb[p]; fa.ctrl = ctrl; fa.p = p;
+            fa.wfrag = c->net.wfrag; fa.grid_params = c->net.grid; fa.levels = c->net.levels;
+            fa.frame_rgba = c->nerf_rgba.as<float4>(); fa.frame_depth = c->nerf_depth.as<float>(); fa.positions = c->nerf_pos.as<float>();
+            fa.work = c->fused_work.as<uint32_t>();
+            // concurrent frames: the tail runs beside the raytracer on the CUs its grids leave free
+            double fb = c->p("nerf_fused_blocks");
+            if (fb < 0) fb = (c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0) ? 2.0 * std::max(1.0, c->p("rt_reserved_cus")) : 0.0;
+            launch_nerf_fused(fa, c->net, iter == 0 ? c->h_alive[0] : n_band, (uint32_t)fb, c->s_nerf);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
+            c->fused_last = true;
+            c->fused_k0 = iter;
+            on_chunk(chunk + 1);
+            break;
+        }
+        for (int k = 0; k < CHUNK && !(fuse && iter >= fuse_after); ++k, ++iter) {
             launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, mode.ngp, c->s_nerf);
             if (P.collect_kernel_times) {
                 while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
@@ -1025,7 +1072,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             out->n_iterations = c->h_ctrl->n_iter;
             out->n_hit = c->h_ctrl->n_hit;
             out->n_samples = c->h_ctrl->total_samples;
-            out->n_reference_slots = c->h_ctrl->ref_slots;
+            out->n_reference_slots = ref_slots_of(c);
             std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
             std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
             std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
@@ -1087,7 +1134,7 @@ void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* o
         out->n_iterations = c->h_ctrl->n_iter;
         out->n_hit = c->h_ctrl->n_hit;
         out->n_samples = c->h_ctrl->total_samples;
-        out->n_reference_slots = c->h_ctrl->ref_slots;
+        out->n_reference_slots = ref_slots_of(c);
         std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
         std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
         std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
@@ -1143,7 +1190,7 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go}) (void)hipEventDestroy(e);

@@ -418,6 +418,9 @@ __global__ void bitfield_linear_kernel(const uint8_t* __restrict__ bf, uint32_t*
 }
 
 __global__ void ctrl_init_kernel(MarchCtrl* c) {
+    if (threadIdx.x < 64) {   // the fused tail kernel accumulates into the histograms
+        c->alive_hist[threadIdx.x] = 0; c->steps_hist[threadIdx.x] = 0; c->samples_hist[threadIdx.x] = 0;
+    }
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         c->n_alive[0] = 0; c->n_alive[1] = 0;
         c->n_samples[0] = 0; c->n_samples[1] = 0;

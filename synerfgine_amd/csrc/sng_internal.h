@@ -78,6 +78,24 @@ struct NerfFrameArgs {
     TraceMode mode;
 };
 
+// fused.hip: ray-local NeRF wavefront (generate + field + composite in one persistent kernel)
+struct FusedArgs {
+    Volume vol;
+    CamDev cam;
+    TraceMode mode;
+    RayBuf rays;                  // initial alive rays (init_rays_kernel output), count = ctrl->n_alive[0]
+    MarchCtrl* ctrl;
+    const void* wfrag;            // MFMA weight fragments (NetworkDev::wfrag)
+    const void* grid_params;      // fp16 hash grid
+    const LevelInfo* levels;
+    float4* frame_rgba;
+    float* frame_depth;
+    float* positions;
+    uint32_t* work;               // ray-queue cursor (zeroed by the launcher)
+    int p;                        // ping-pong buffer holding the alive rays (MarchCtrl::n_alive[p], i_step[p])
+};
+void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s);
+
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
                    uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream);
 int launch_encode(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n, uint16_t* out, hipStream_t stream);

@@ -338,3 +338,22 @@ def test_instant_ngp_rejects_unsupported_modes():
             eng.render_nerf(render_mode=2)   # Normals needs network input gradients
     finally:
         tb.close()
+
+
+@pytest.mark.parametrize("config,ngp_mode", [("c3", None), ("c3", 1), ("c3", 4), ("c3", 6), ("c4", None)])
+def test_fused_nerf_kernel_equals_wavefront(config, ngp_mode):
+    """fused.hip (ray-local generate + field + composite) reproduces the per-iteration wavefront bit for bit."""
+    tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, config)
+    try:
+        out = {}
+        for fused in (0, 1):
+            eng.set_param("nerf_fused", fused)
+            r = eng.frame() if ngp_mode is None else eng.render_nerf(render_mode=ngp_mode)
+            bufs = ["nerf_rgba", "nerf_depth"] + (["nerf_positions"] if ngp_mode is None else [])
+            out[fused] = ([r.download(b) for b in bufs], (r.n_samples, r.n_hit, r.n_iterations, r.n_reference_slots), list(r.alive_per_iter),
+                          list(r.samples_per_iter))
+        for a, b in zip(out[0][0], out[1][0]):
+            assert np.array_equal(a, b)
+        assert out[0][1:] == out[1][1:]
+    finally:
+        tb.close()

@@ -10,7 +10,8 @@ from synerfgine_amd import scene as S
 from synerfgine_amd.tiling import balance_bounds, band_rows, even_bounds
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
-tb, eng, _ = S.make_engine(cfg)
+ov = dict((kv.split("=")[0], float(kv.split("=")[1])) for kv in sys.argv[2:])
+tb, eng, _ = S.make_engine(cfg, overrides=ov)
 H = eng.resolution()["mesh"][1]
 
 
@@ -25,7 +26,7 @@ def t_frame(rows, reps=5):
 
 
 full = t_frame(None)
-out = {"config": cfg, "full_ms": round(full, 3)}
+out = {"config": cfg, "overrides": ov, "full_ms": round(full, 3)}
 for n in (2, 4, 8):
     ts = [round(t_frame(band_rows(H, r, n)), 3) for r in range(n)]
     out[f"n{n}"] = {"band_ms": ts, "max": max(ts), "pred_eff": round(full / (n * max(ts)), 3)}
