@@ -322,6 +322,7 @@ const std::map<std::string, double>& default_params() {
         {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
+        {"rt_staged", 0},                       // ... plus primary / shade / bounce stages over compacted queues
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
@@ -384,6 +385,7 @@ struct sng_ctx {
     DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
+    DevBuf rt_hits, rt_rays, rt_next_pos, rt_tail, rt_counters;   // staged path tracer
     bool fused_last = false;               // the last trace finished in the fused kernel
     uint32_t fused_k0 = 0;                 // ... from this iteration on
     uint64_t rt_tile_key = 0;             // band geometry the costs belong to
@@ -994,8 +996,19 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 c->rt_count.ensure(16);
                 q.rec = c->rt_rec.as<float4>(); q.srec = c->rt_srec.as<float4>(); q.mask = c->rt_mask.as<float>();
                 q.head = c->rt_head.as<int>(); q.count = c->rt_count.as<uint32_t>(); q.cap = (uint32_t)cap;
-                launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
-                                          c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), (uint32_t)c->n_cus * 16, c->s_rt);
+                if (c->p("rt_staged") != 0.0) {
+                    c->rt_hits.ensure(n_px * 48);
+                    c->rt_rays.ensure(n_px * 48);
+                    c->rt_next_pos.ensure((uint64_t)MW * MH * 16);
+                    c->rt_tail.ensure((uint64_t)MW * MH * 4);
+                    c->rt_counters.ensure((4 + (uint64_t)ra.samples * ra.bounces * 4) * 4);
+                    RtStage st{c->rt_hits.as<float4>(), c->rt_rays.as<float4>(), nullptr, c->rt_next_pos.as<float4>(), q.head, c->rt_tail.as<int>()};
+                    launch_raytrace_staged(ra, q, st, c->rt_counters.as<uint32_t>(), c->mesh_o.as<float4>(), c->mesh_d.as<float4>(),
+                                           c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), c->s_rt);
+                } else {
+                    launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
+                                              c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), (uint32_t)c->n_cus * 16, c->s_rt);
+                }
             } else {
                 launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
                                 c->acc_depth.as<float>(), c->s_rt);
@@ -1190,7 +1203,7 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go}) (void)hipEventDestroy(e);

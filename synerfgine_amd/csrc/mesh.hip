@@ -46,6 +46,17 @@ struct TraceCtx {
     }
 };
 
+// slot per lane with pred set, one atomic per wave
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred, int lane) {
+    const unsigned long long mask = __ballot(pred);
+    const uint32_t total = (uint32_t)__popcll(mask);
+    uint32_t base = 0;
+    const int leader = mask ? (int)(__ffsll((long long)mask) - 1) : 0;
+    if (total && lane == leader) base = atomicAdd(counter, total);
+    base = __shfl(base, leader, 64);
+    return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+}
+
 // one slot per active lane from a device counter, one atomic per wave
 __device__ __forceinline__ uint32_t wave_alloc(uint32_t* counter, int lane) {
     const unsigned long long mask = __ballot(1);
@@ -450,6 +461,201 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     }
 }
 
+// ===========================================================================================
+// Staged path tracer (rt_mode 2): the same per-pixel path and RNG sequence as raytrace_pixel,
+// split into dense stages per sample -- primary traversal over all pixels, then for every
+// bounce: shade (light samples -> hit records + shadow queue, scatter) over the compacted hits
+// and traversal over the compacted bounce rays.  A pixel's stages run in its original order
+// (spp-major, bounce-minor), so its XORWOW draws, hit records and next_pos sums are identical;
+// every traversal/shading lane does useful work instead of idling beside other lanes' paths.
+// ===========================================================================================
+// hit entry: [pos, pixel] [rd, spp] [pdf, att, obj, tri] ; ray entry: [origin, pixel] [dir, spp] [pdf, att, -, -]
+
+// depth_test_world(+HitRecord) (common.cu:50-67) without the normal/perturb (the shade stage
+// derives them from (obj, tri) with the same expressions)
+template <bool LDS>
+__device__ __forceinline__ int nearest_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS>& cx, float& t_out,
+                                           int& tri_out) {
+    const f3 off = origin + dir * MIN_DEPTH;
+    int out_obj = -1, out_tri = -1;
+    float best = MAX_DEPTH;
+    for (int c = 0; c < n_objs; ++c) {
+        int tri;
+        const float t = object_intersect(off, dir, objs[c], cx, tri);
+        if (t < best && t > MIN_DEPTH) { out_obj = c; best = t; out_tri = tri; }
+    }
+    t_out = best;
+    tri_out = out_tri;
+    return out_obj;
+}
+
+__device__ __forceinline__ uint32_t wave_claim(uint32_t* counter, uint32_t n, int lane) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(counter, n);
+    return __shfl(base, 0, 64);
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(512) void rt_primary_kernel(RaytraceArgs a, RtStage st, uint32_t spp, uint32_t* __restrict__ work,
+                                                          const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
+                                                          uint32_t n_rng) {
+    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    const int lane = threadIdx.x & 63;
+    const uint32_t rows = (uint32_t)(a.row1 - a.row0);
+    const uint32_t tiles_x = ((uint32_t)a.W + 7) / 8, n_tiles = tiles_x * ((rows + 7) / 8);
+    // static round-robin over the (cost-ordered) tiles: the expensive tiles spread over all waves
+    // without a contended work counter (one launch per sample makes per-tile atomics add up)
+    const uint32_t wave_id = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t kk = wave_id; kk < n_tiles; kk += n_waves) {
+        const uint32_t tile = a.tile_order ? a.tile_order[kk] : kk;
+        const uint64_t t0 = wall_clock64();
+        const uint32_t x = (tile % tiles_x) * 8 + (lane & 7), y = (tile / tiles_x) * 8 + (lane >> 3);
+        bool hit = false;
+        f3 hpos = splat(0.0f), rd = splat(0.0f);
+        int obj = -1, tri = -1;
+        uint32_t pix = 0;
+        if (x < (uint32_t)a.W && y < rows) {
+            pix = (uint32_t)a.row0 * (uint32_t)a.W + y * (uint32_t)a.W + x;
+            if (spp == 0) { st.head[pix] = -1; st.tail[pix] = -1; }
+            Xorwow r = load_rng(rng, n_rng, pix);
+            const float4 o4 = origins[pix], d4 = dirs[pix];
+            const f3 src_p = mk(o4.x, o4.y, o4.z), src_d = mk(d4.x, d4.y, d4.z);
+            const float longi = curand_uniform(r) * a.lens;
+            const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+            rd = cone_random_up(src_d, a.up, longi, latid);
+            float t;
+            obj = nearest_hit(src_p, rd, a.objs, a.n_objs, cx, t, tri);
+            hpos = src_p + t * rd;
+            const float4 np = spp ? st.next_pos[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const f3 n3 = mk(np.x, np.y, np.z) + hpos;
+            st.next_pos[pix] = make_float4(n3.x, n3.y, n3.z, 0.0f);
+            store_rng(rng, n_rng, pix, r);
+            hit = obj >= 0;
+        }
+        const uint32_t slot = wave_append(st.hit_count, hit, lane);
+        if (hit) {
+            float4* e = st.hits + 3 * (size_t)slot;
+            e[0] = make_float4(hpos.x, hpos.y, hpos.z, __uint_as_float(pix));
+            e[1] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(spp));
+            e[2] = make_float4(1.0f / (float)a.bounces, 1.0f, __int_as_float(obj), __int_as_float(tri));
+        }
+        if (a.tile_cost && lane == 0) a.tile_cost[tile] = (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull);
+    }
+}
+
+// shade_object (raytracer.cu:6-57) for the compacted hits of one bounce; writes the hit record
+// (light colours), the point-light shadow rays, and the scattered ray of the next bounce.
+__global__ __launch_bounds__(256) void rt_shade_kernel(RaytraceArgs a, RtQueue q, RtStage st, uint32_t bounce, const uint32_t* __restrict__ n_hits_dev,
+                                                       float4* __restrict__ rays_out, uint32_t* __restrict__ ray_count, uint32_t* __restrict__ rng, uint32_t n_rng) {
+    const uint32_t n_hits = *n_hits_dev;
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n_hits; base += gridDim.x * blockDim.x) {
+        const uint32_t e_i = base + (uint32_t)lane;
+        const bool valid = e_i < n_hits;
+        const uint32_t k = wave_append(q.count, valid, lane);   // hit record of this entry
+        bool next = false;
+        f3 hpos = splat(0.0f), ndir = splat(0.0f);
+        uint32_t pix = 0, spp = 0;
+        float pdf_n = 0.0f, att_n = 0.0f;
+        if (valid) {
+            const float4* e = st.hits + 3 * (size_t)e_i;
+            const float4 e0 = e[0], e1 = e[1], e2 = e[2];
+            hpos = mk(e0.x, e0.y, e0.z);
+            pix = __float_as_uint(e0.w);
+            const f3 rd = mk(e1.x, e1.y, e1.z);
+            spp = __float_as_uint(e1.w);
+            const float pdf = e2.x, att = e2.y;
+            const ObjectGpu& o = a.objs[__float_as_int(e2.z)];
+            const Tri tr = o.tris[__float_as_int(e2.w)];
+            const f3 N = tri_normal(tr);
+            const f3 normal = mul(o.rot, N);
+            const f3 T = normalize((tr.a + tr.b + tr.c) / 3.0f - tr.a);   // Triangle::get_perturb_matrix (triangle.cuh:164-170)
+            const m3 perturb = {T, cross(T, N), N};
+            const MaterialGpu m = a.mats[o.mat_id];
+            Xorwow r = load_rng(rng, n_rng, pix);
+            // hit record, appended to the pixel's list (stages run in the pixel's path order)
+            float4* rk = q.rec + (size_t)k * q.rec_stride;
+            rk[0] = make_float4(__int_as_float(-1), __uint_as_float(spp), __int_as_float(o.mat_id), 0.0f);
+            rk[1] = make_float4(pdf, att, 0.0f, 0.0f);
+            float* lc_out = reinterpret_cast<float*>(rk + 2);
+            const int prev = st.tail[pix];
+            if (prev < 0) q.head[pix] = (int)k;
+            else reinterpret_cast<int*>(q.rec + (size_t)prev * q.rec_stride)[0] = (int)k;
+            st.tail[pix] = (int)k;
+            uint32_t jl = 0, jp = 0;
+            for (int l = 0; l < a.n_lights; ++l) {
+                const LightGpu L = a.lights[l];
+                for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
+                    const f3 lpos = light_sample(L, r);
+                    f3 Lv = lpos - hpos;
+                    const float full_dist = length(Lv);
+                    Lv = normalize(Lv);
+                    const f3 R = reflect(Lv, normal);
+                    const f3 V = normalize(-rd);
+                    const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                    lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
+                    if (L.type == 0) {
+                        float4* sr = q.srec + 2 * ((size_t)k * q.nps + jp);
+                        sr[0] = make_float4(hpos.x, hpos.y, hpos.z, full_dist);
+                        sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
+                        ++jp;
+                    }
+                }
+            }
+            // Material::scatter (material.cuh:112-123)
+            const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
+            const float lo = curand_uniform(r) * spec;
+            const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+            ndir = cone_random_frame(normal, perturb, lo, la);
+            pdf_n = 1.0f / fmaxf(1.0f, spec * 2.0f);
+            att_n = 1.0f * m.rg;
+            store_rng(rng, n_rng, pix, r);
+            next = bounce + 1 < a.bounces;
+        }
+        const uint32_t slot = wave_append(ray_count, next, lane);
+        if (next) {
+            float4* e = rays_out + 3 * (size_t)slot;
+            e[0] = make_float4(hpos.x, hpos.y, hpos.z, __uint_as_float(pix));
+            e[1] = make_float4(ndir.x, ndir.y, ndir.z, __uint_as_float(spp));
+            e[2] = make_float4(pdf_n, att_n, 0.0f, 0.0f);
+        }
+    }
+}
+
+// traversal of the compacted bounce rays; hits go to the next shade stage
+template <bool LDS>
+__global__ __launch_bounds__(512) void rt_bounce_kernel(RaytraceArgs a, RtStage st, const float4* __restrict__ rays_in, const uint32_t* __restrict__ n_rays_dev,
+                                                         uint32_t* __restrict__ work) {
+    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    const int lane = threadIdx.x & 63;
+    const uint32_t n_rays = *n_rays_dev;
+    while (true) {
+        const uint32_t base = wave_claim(work, 64u, lane);
+        if (base >= n_rays) break;
+        const uint32_t j = base + (uint32_t)lane;
+        bool hit = false;
+        float4 e0, e1, e2;
+        f3 hpos = splat(0.0f);
+        int obj = -1, tri = -1;
+        if (j < n_rays) {
+            const float4* e = rays_in + 3 * (size_t)j;
+            e0 = e[0]; e1 = e[1]; e2 = e[2];
+            const f3 rp = mk(e0.x, e0.y, e0.z), rd = mk(e1.x, e1.y, e1.z);
+            float t;
+            obj = nearest_hit(rp, rd, a.objs, a.n_objs, cx, t, tri);
+            hpos = rp + t * rd;
+            hit = obj >= 0;
+        }
+        const uint32_t slot = wave_append(st.hit_count, hit, lane);
+        if (hit) {
+            float4* e = st.hits + 3 * (size_t)slot;
+            e[0] = make_float4(hpos.x, hpos.y, hpos.z, e0.w);
+            e[1] = e1;
+            e[2] = make_float4(e2.x, e2.y, __int_as_float(obj), __int_as_float(tri));
+        }
+    }
+}
+
 // Shadow rays of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
@@ -478,7 +684,8 @@ __global__ __launch_bounds__(512) void shadow_rays_kernel(RaytraceArgs a, RtQueu
 }
 
 // Colour replay of the deferred raytracer, in raytrace_kernel's exact float order.
-__global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQueue q, float4* __restrict__ acc_rgba) {
+__global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQueue q, float4* __restrict__ acc_rgba, const float4* __restrict__ next_pos,
+                                                            const float4* __restrict__ origins, const float4* __restrict__ dirs, float* __restrict__ acc_depth) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (t >= n) return;
@@ -511,6 +718,11 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
         shade = shade + shade_s;
     }
     shade = shade / (float)a.samples;
+    if (next_pos) {   // staged mode: raytrace_pixel's depth from the summed first hits
+        const float4 np = next_pos[i], o4 = origins[i], d4 = dirs[i];
+        const f3 npv = mk(np.x, np.y, np.z) / (float)a.samples;
+        acc_depth[i] = dot(mk(d4.x, d4.y, d4.z), npv - mk(o4.x, o4.y, o4.z));
+    }
     float4 cur = acc_rgba[i];
     const f3 curr = mk(cur.x, cur.y, cur.z);
     if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
@@ -638,7 +850,47 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
         hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
         hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
     }
-    hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc);
+    hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
+}
+
+// staged mode: per sample, primary traversal over all pixels then shade / bounce-traversal stages
+// over compacted queues; counters: [0] hit records, then per (spp, bounce) {hits, rays, work}.
+void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st, uint32_t* counters, const float4* o, const float4* d, uint32_t* rng,
+                            uint32_t n_rng, float4* acc, float* accd, hipStream_t s) {
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (!n) return;
+    const uint32_t n_counters = 4 + a.samples * a.bounces * 4;
+    (void)hipMemsetAsync(counters, 0, n_counters * sizeof(uint32_t), s);
+    RtQueue qq = q;
+    qq.count = counters;
+    const uint32_t tp = 512, ts = 512;
+    const bool lds = a.scene_in_lds != 0;
+    const size_t lp = trace_lds_bytes(a, lds, tp);
+    const uint32_t bp = std::min((n + tp - 1) / tp, a.persistent_blocks * 2);
+    if (lds) { allow_lds(rt_primary_kernel<true>, lp); allow_lds(rt_bounce_kernel<true>, lp); allow_lds(shadow_rays_kernel<true>, trace_lds_bytes(a, lds, ts)); }
+    else { allow_lds(rt_primary_kernel<false>, lp); allow_lds(rt_bounce_kernel<false>, lp); allow_lds(shadow_rays_kernel<false>, trace_lds_bytes(a, lds, ts)); }
+    const uint32_t shade_blocks = std::max(1u, std::min((n + 255) / 256, a.persistent_blocks * 8));
+    for (uint32_t sp = 0; sp < a.samples; ++sp) {
+        uint32_t* c = counters + 4 + sp * a.bounces * 4;
+        st.hit_count = c;
+        if (lds) hipLaunchKernelGGL(rt_primary_kernel<true>, dim3(bp), dim3(tp), lp, s, a, st, sp, c + 3, o, d, rng, n_rng);
+        else hipLaunchKernelGGL(rt_primary_kernel<false>, dim3(bp), dim3(tp), lp, s, a, st, sp, c + 3, o, d, rng, n_rng);
+        for (uint32_t b = 0; b < a.bounces; ++b) {
+            uint32_t* cb = c + b * 4;   // {hits of bounce b, rays of bounce b+1, -, work}
+            hipLaunchKernelGGL(rt_shade_kernel, dim3(shade_blocks), dim3(256), 0, s, a, qq, st, b, cb, st.rays, cb + 1, rng, n_rng);
+            if (b + 1 < a.bounces) {
+                uint32_t* cn = c + (b + 1) * 4;
+                RtStage sb = st;
+                sb.hit_count = cn;
+                if (lds) hipLaunchKernelGGL(rt_bounce_kernel<true>, dim3(bp), dim3(tp), lp, s, a, sb, st.rays, cb + 1, cn + 3);
+                else hipLaunchKernelGGL(rt_bounce_kernel<false>, dim3(bp), dim3(tp), lp, s, a, sb, st.rays, cb + 1, cn + 3);
+            }
+        }
+    }
+    (void)hipMemsetAsync(a.work + 1, 0, sizeof(uint32_t), s);
+    if (lds) hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + 1);
+    else hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + 1);
+    hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, qq, acc, st.next_pos, o, d, accd);
 }
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
                     const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s) {

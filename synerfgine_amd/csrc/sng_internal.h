@@ -165,6 +165,18 @@ void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 fo
                       hipStream_t s);
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
                                float* accd, uint32_t shadow_blocks, hipStream_t s);
+// staged path tracer buffers (mesh.hip, rt_staged): hit / ray queues of one stage (3 float4 per entry,
+// capacity = band pixels) and per-pixel state carried across stages
+struct RtStage {
+    float4* hits;            // [pos, pixel] [rd, spp] [pdf, att, obj, tri]
+    float4* rays;            // [origin, pixel] [dir, spp] [pdf, att, -, -]
+    uint32_t* hit_count;     // set per launch
+    float4* next_pos;        // per pixel: sum of the primary hits over the samples
+    int* head;               // per pixel: first hit record (RtQueue::head)
+    int* tail;               // per pixel: last hit record
+};
+void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st, uint32_t* counters, const float4* o, const float4* d, uint32_t* rng,
+                            uint32_t n_rng, float4* acc, float* accd, hipStream_t s);
 void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, hipStream_t s);
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
                      hipStream_t s);

@@ -235,9 +235,11 @@ def test_errors_are_loud(tb):
         tb.inference_mixed_precision(0, 3, 16, 0)
 
 
-@pytest.mark.parametrize("overrides", [{}, {"path_trace_depth": 3, "light_samples": 3}, {"fast_slab": 0}, {"scene_lds": 0}])
+@pytest.mark.parametrize("overrides", [{}, {"path_trace_depth": 3, "light_samples": 3}, {"fast_slab": 0}, {"scene_lds": 0}, {"rt_staged": 1},
+                                       {"rt_staged": 1, "path_trace_depth": 3, "light_samples": 3}, {"rt_staged": 1, "scene_lds": 0}])
 def test_wavefront_raytracer_equals_megakernel(overrides):
-    """Deferred shadow-ray queues (rt_wavefront=1) reproduce the one-kernel path tracer bit for bit."""
+    """Deferred shadow-ray queues (rt_wavefront=1) and the staged tracer (rt_staged=1) reproduce the one-kernel
+    path tracer bit for bit."""
     import ctypes
     tb, eng, _ = _engine(192, 108, overrides)
     try:
@@ -245,10 +247,12 @@ def test_wavefront_raytracer_equals_megakernel(overrides):
         m0 = eng.rng_states(1).copy()
         n0 = eng.rng_states(0).copy()
         out = {}
+        staged = overrides.get("rt_staged", 0)
         for mode in (0, 1):
             tb._lib.sng_set_rng_states(tb.ctx, 0, n0.ctypes.data_as(P), n0.shape[0])
             tb._lib.sng_set_rng_states(tb.ctx, 1, m0.ctypes.data_as(P), m0.shape[0])
             eng.set_param("rt_wavefront", mode)
+            eng.set_param("rt_staged", staged if mode else 0)
             r = eng.frame()
             out[mode] = (r.download("syn_rgba"), r.download("syn_depth"), eng.rng_states(1).copy())
         for a, b in zip(out[0], out[1]):
