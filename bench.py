@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-baseline-scale", type=float, default=1.5, help="oracle renders the frame at 1/scale linear resolution")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help="gloo: CPU-side gather (rehearsal on one GPU)")
     ap.add_argument("--even-bands", action="store_true", help="equal-height bands instead of cost-balanced ones")
+    ap.add_argument("--local-schedule", action="store_true",
+                    help="N>1: step each band from its own alive count (no per-iteration count all-reduce; not bit-identical to N=1)")
     ap.add_argument("--balance-iters", type=int, default=8, help="untimed calibration frames for the band split")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="engine parameter override (sng_set_param)")
     return ap.parse_args()
@@ -102,6 +104,17 @@ def main():
     dev = torch.device("cuda", dev_id)
     stream = torch.cuda.current_stream(dev)
     bounds = T.even_bounds(MH, world)
+    if world > 1 and not args.local_schedule:
+        # frame-wide step schedule: one uint32 all-reduce per wavefront iteration
+        # keeps every band bit-identical to the single-GPU frame
+        if args.dist_backend == "nccl":
+            eng.attach_comm()
+        else:
+            def _reduce(vals):
+                t = torch.tensor(vals, dtype=torch.int64)
+                dist.all_reduce(t)
+                return t.tolist()
+            eng.attach_host_reducer(_reduce)
 
     if world > 1 and not args.even_bands:
         # untimed calibration: re-split the rows until every band costs the same device time
@@ -187,6 +200,7 @@ def main():
                     "from scenes/ and data/obj/",
             "config": {"workload": f"{args.config}: " + WORKLOADS[args.config],
                        "width": MW, "height": MH, "nerf_res": list(res["nerf"]), "tiles": f"{world} horizontal bands (rows {bounds}) + " + ("RCCL all_gather" if args.dist_backend == "nccl" else "gloo all_gather"),
+                       "step_schedule": "band-local" if (world > 1 and args.local_schedule) else ("frame-wide (per-iteration alive-count all-reduce)" if world > 1 else "frame-wide"),
                        "samples_per_frame": int(s0.n_samples), "reference_slots_per_frame": int(s0.n_reference_slots),
                        "wavefront_iterations": int(s0.n_iterations), "hit_rays": int(s0.n_hit)},
             "streams": "serialized (raytracer then NeRF)" if args.serial_streams else

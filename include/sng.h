@@ -165,6 +165,23 @@ int sng_render_frame(sng_ctx* ctx, const sng_frame_params* params, sng_frame_res
  * composite_kernel_nerf 577-788, shade_kernel_nerf 1788-1828) into d_nerf_rgba / d_nerf_depth at NeRF
  * resolution; parameters "render_mode" (ERenderMode) and "depth_scale".  row_begin/row_end are NeRF rows. */
 int sng_render_nerf_ngp(sng_ctx* ctx, const sng_frame_params* params, sng_frame_result* out);
+/* ---- multi-GPU step schedule --------------------------------------------------
+ * trace_alt sizes each wavefront iteration from the FRAME-wide alive count
+ * (n_steps = clamp(2^21 / n_alive, 1, 8), testbed_nerf.cu:2180-2190).  A rank that renders one row
+ * band (sng_frame_params.row_begin/row_end) reproduces the single-GPU frame bit for bit only if it
+ * uses that frame-wide count, so with a communicator or reducer attached each iteration sums the
+ * alive rays of every band's own rows across ranks (one uint32 all-reduce) before stepping.
+ * The bands of all ranks must tile [0, height) without overlap, and every rank renders every frame. */
+#define SNG_COMM_ID_BYTES 128
+/* ncclGetUniqueId: rank 0 calls it and broadcasts the bytes to the other ranks */
+int sng_comm_unique_id(uint8_t out_id[SNG_COMM_ID_BYTES]);
+/* ncclCommInitRank on the context's device (RCCL over xGMI); unique_id NULL detaches */
+int sng_set_comm(sng_ctx* ctx, const uint8_t* unique_id, int rank, int world);
+/* host-side alternative (tests, gloo): fn sums values[0..n) over all ranks in place, returns 0 on
+ * success; called once per wavefront iteration after a stream sync.  fn NULL detaches. */
+typedef int (*sng_sched_reduce_fn)(uint32_t* values, uint32_t n, void* user);
+int sng_set_sched_reducer(sng_ctx* ctx, sng_sched_reduce_fn fn, void* user);
+
 int sng_synchronize(sng_ctx* ctx);
 int sng_copy_to_host(sng_ctx* ctx, const void* d_src, void* h_dst, uint64_t n_bytes);
 /* device-to-device copy on the caller's stream (frame tiles -> collective buffers) */

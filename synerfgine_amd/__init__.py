@@ -193,6 +193,41 @@ class Engine:
         check(self._lib.sng_render_nerf_ngp(self.ctx, ctypes.byref(p), ctypes.byref(r)))
         return FrameResult(self, r)
 
+    # ---- multi-GPU step schedule (include/sng.h) ------------------------
+    def attach_comm(self, group=None):
+        """RCCL communicator over the ranks of `group` (torch.distributed) for the frame-wide step
+        schedule: rank 0 makes the ncclUniqueId, the other ranks receive it by broadcast."""
+        import torch
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = (ctypes.c_uint8 * _lib.SNG_COMM_ID_BYTES)()
+        if rank == 0:
+            check(self._lib.sng_comm_unique_id(uid))
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = (ctypes.c_uint8 * _lib.SNG_COMM_ID_BYTES)(*t.cpu().tolist())
+        check(self._lib.sng_set_comm(self.ctx, uid, rank, world))
+
+    def attach_host_reducer(self, reduce_fn):
+        """Host-side schedule exchange: reduce_fn(list_of_ints) -> list of the sums over ranks
+        (e.g. a gloo all_reduce); called once per wavefront iteration."""
+        def cb(values, n, user):
+            try:
+                out = reduce_fn([values[i] for i in range(n)])
+                for i in range(n):
+                    values[i] = int(out[i])
+                return 0
+            except Exception:   # reported through sng_last_error as "schedule reducer failed"
+                return 1
+        self._reduce_cb = _lib.SCHED_REDUCE_FN(cb)   # keep alive while attached
+        check(self._lib.sng_set_sched_reducer(self.ctx, ctypes.cast(self._reduce_cb, ctypes.c_void_p), None))
+
+    def detach_comm(self):
+        check(self._lib.sng_set_comm(self.ctx, None, 0, 0))
+        check(self._lib.sng_set_sched_reducer(self.ctx, None, None))
+        self._reduce_cb = None
+
     # ---- scene inspection (tests) --------------------------------------------------
     def scene(self):
         no, nl, nm = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
@@ -224,6 +259,10 @@ class Engine:
         out = np.zeros((w * h, 6), np.uint32)
         check(self._lib.sng_get_rng_states(self.ctx, which, out.ctypes.data_as(_lib.U32P), w * h))
         return out
+
+    def set_rng_states(self, which, states):
+        states = np.ascontiguousarray(states, np.uint32)
+        check(self._lib.sng_set_rng_states(self.ctx, which, states.ctypes.data_as(_lib.U32P), states.shape[0]))
 
 
 def bvh_build(tris, prims_per_leaf=4):

@@ -118,6 +118,10 @@ FP = ctypes.POINTER(ctypes.c_float)
 U16P = ctypes.POINTER(ctypes.c_uint16)
 U32P = ctypes.POINTER(ctypes.c_uint32)
 
+SNG_COMM_ID_BYTES = 128
+# int (*sng_sched_reduce_fn)(uint32_t* values, uint32_t n, void* user)
+SCHED_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_void_p)
+
 # name -> (restype, argtypes); every symbol declared in include/sng.h
 SIGNATURES = {
     "sng_last_error": (ctypes.c_char_p, []),
@@ -153,6 +157,9 @@ SIGNATURES = {
     "sng_get_resolution": (ctypes.c_int, [P, ctypes.POINTER(sng_resolution_info)]),
     "sng_render_frame": (ctypes.c_int, [P, ctypes.POINTER(sng_frame_params), ctypes.POINTER(sng_frame_result)]),
     "sng_render_nerf_ngp": (ctypes.c_int, [P, ctypes.POINTER(sng_frame_params), ctypes.POINTER(sng_frame_result)]),
+    "sng_comm_unique_id": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint8)]),
+    "sng_set_comm": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int]),
+    "sng_set_sched_reducer": (ctypes.c_int, [P, P, P]),
     "sng_synchronize": (ctypes.c_int, [P]),
     "sng_copy_to_host": (ctypes.c_int, [P, P, P, U64]),
     "sng_copy_device": (ctypes.c_int, [P, P, P, U64, P]),

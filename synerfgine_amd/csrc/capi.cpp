@@ -31,10 +31,6 @@ namespace {
 
 thread_local std::string g_err;
 
-struct SngError : std::runtime_error {
-    int code;
-    SngError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
 #define HIPCHK(x)                                                                                          \
     do {                                                                                                   \
         hipError_t e_ = (x);                                                                               \
@@ -393,7 +389,8 @@ struct sng_ctx {
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
     DevBuf d_seq;
     MarchCtrl* h_ctrl = nullptr;
-    uint32_t* h_alive = nullptr;  // pinned readback [chunk][2]
+    uint32_t* h_alive = nullptr;  // pinned readback [chunk][2], [4..5] host-reducer exchange
+    SchedComm sched_comm;         // frame-wide step schedule across ranks (comm.cpp)
     bool mesh_reset = true;
 
     // scene (Engine)
@@ -795,8 +792,10 @@ uint64_t ref_slots_of(const sng_ctx* c) {
 // [tr0, tr1): device-driven wavefront, host readback of the alive count once per CHUNK iterations.
 // on_chunk(k) runs after the k-th chunk is enqueued (render_frame starts the raytracer there).
 // Returns the number of network launches.
-uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, const CamDev& cam, f2 sc, int tr0, int tr1, TraceMode mode,
-                    uint32_t target, const std::function<void(int)>& on_chunk) {
+// own0/own1: the NeRF rows this band owns (the bands of all ranks partition the frame's rows);
+// only used when a schedule communicator is attached (Sched).
+uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, const CamDev& cam, f2 sc, int tr0, int tr1, int own0, int own1,
+                    TraceMode mode, uint32_t target, const std::function<void(int)>& on_chunk) {
     const int NW = c->nerf_res[0], NH = c->nerf_res[1];
     uint32_t net_launches = 0;
     MarchCtrl* ctrl = c->ctrl.as<MarchCtrl>();
@@ -815,10 +814,28 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     a.reset = P.reset_accumulation ? 1 : 0;
     a.target_n_queries = target;
     a.mode = mode;
+    const bool gsched = c->sched_comm.active();
+    a.sched = {gsched ? 1 : 0, (uint32_t)own0 * (uint32_t)NW, (uint32_t)own1 * (uint32_t)NW};
+    // sched_alive[q] <- sum over ranks of n_owned[q] (the frame-wide alive count of the next iteration)
+    auto reduce_sched = [&](int q) {
+        if (!gsched) return;
+        if (c->sched_comm.comm) {
+            HIPCHK(hipMemcpyAsync(&ctrl->sched_alive[q], &ctrl->n_owned[q], 4, hipMemcpyDeviceToDevice, c->s_nerf));
+            comm_allreduce_u32(c->sched_comm, &ctrl->sched_alive[q], 1, c->s_nerf);
+        } else {
+            uint32_t* h = &c->h_alive[4];
+            HIPCHK(hipMemcpyAsync(h, &ctrl->n_owned[q], 4, hipMemcpyDeviceToHost, c->s_nerf));
+            HIPCHK(hipStreamSynchronize(c->s_nerf));
+            if (c->sched_comm.host_fn(h, 1, c->sched_comm.host_user) != 0) throw SngError(SNG_ERR_STATE, "schedule reducer failed");
+            HIPCHK(hipMemcpyAsync(&ctrl->sched_alive[q], h, 4, hipMemcpyHostToDevice, c->s_nerf));
+        }
+    };
+    uint32_t* const sched_src = gsched ? &ctrl->sched_alive[0] : &ctrl->n_alive[0];   // counts the host loop reads
     RayBuf rb[2];
     for (int b = 0; b < 2; ++b)
         rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>()};
     launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
+    reduce_sched(0);
     const uint32_t n_band = (uint32_t)(tr1 - tr0) * (uint32_t)NW;
     c->fused_last = false;
     c->fused_k0 = 0;
@@ -829,7 +846,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     bool fuse = false;
     uint32_t fuse_after = 0;
     if (c->p("nerf_fused") != 0.0) {
-        HIPCHK(hipMemcpyAsync(c->h_alive, &ctrl->n_alive[0], 4, hipMemcpyDeviceToHost, c->s_nerf));
+        HIPCHK(hipMemcpyAsync(c->h_alive, sched_src, 4, hipMemcpyDeviceToHost, c->s_nerf));
         HIPCHK(hipStreamSynchronize(c->s_nerf));
         fuse = (uint64_t)c->h_alive[0] * MAX_STEPS_BETWEEN_COMPACTION <= target;
         fuse_after = (uint32_t)std::max(0.0, c->p("nerf_fused_after"));
@@ -852,7 +869,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // concurrent frames: the tail runs beside the raytracer on the CUs its grids leave free
             double fb = c->p("nerf_fused_blocks");
             if (fb < 0) fb = (c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0) ? 2.0 * std::max(1.0, c->p("rt_reserved_cus")) : 0.0;
-            launch_nerf_fused(fa, c->net, iter == 0 ? c->h_alive[0] : n_band, (uint32_t)fb, c->s_nerf);
+            launch_nerf_fused(fa, c->net, iter == 0 ? std::min(c->h_alive[0], n_band) : n_band, (uint32_t)fb, c->s_nerf);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
             c->fused_last = true;
@@ -861,7 +878,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             break;
         }
         for (int k = 0; k < CHUNK && !(fuse && iter >= fuse_after); ++k, ++iter) {
-            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, mode.ngp, c->s_nerf);
+            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, mode.ngp, a.sched.global, c->s_nerf);
             if (P.collect_kernel_times) {
                 while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
                 HIPCHK(hipEventRecord(c->net_events[2 * net_launches], c->s_nerf));
@@ -869,12 +886,13 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf);
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->net_events[2 * net_launches + 1], c->s_nerf));
             ++net_launches;
-            launch_composite(vol, cam, mode, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
+            launch_composite(vol, cam, mode, a.sched, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
                              c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf);
+            reduce_sched(p ^ 1);
             p ^= 1;
         }
         // readback of the alive count after this chunk; check the previous chunk's (already landed)
-        HIPCHK(hipMemcpyAsync(&c->h_alive[2 * (chunk & 1)], &ctrl->n_alive[0], 8, hipMemcpyDeviceToHost, c->s_nerf));
+        HIPCHK(hipMemcpyAsync(&c->h_alive[2 * (chunk & 1)], sched_src, 8, hipMemcpyDeviceToHost, c->s_nerf));
         HIPCHK(hipGetLastError());
         if (chunk > 0) {
             // wait for the previous chunk's readback (the current chunk stays queued behind it)
@@ -910,6 +928,8 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     const int halo_n = shadows ? radius : 0;
     const int nr0 = std::max(0, ny0 - halo_n), nr1 = std::min(NH, ny1 + halo_n);
     const int tr0 = std::max(0, nr0 - 2), tr1 = std::min(NH, nr1 + 2);
+    // owned NeRF rows: [ceil(y0 / S), ceil(y1 / S)) -- consecutive mesh bands partition the NeRF rows
+    const int own0 = std::min(ny1, (y0 + S - 1) / S), own1 = ny1;
     // the raytracer's NeRF shadow test uses the density bitfield whether or not the NeRF is shown
     // (engine.cu:386-397 passes m_nerf.density_grid_bitfield unconditionally)
     Volume vol{};
@@ -1027,7 +1047,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     uint32_t net_launches = 0;
     if (show_nerf) {
         TraceMode mode{0, 1, 1.0f};
-        net_launches = trace_nerf(c, P, vol, cam, sc, tr0, tr1, mode, target, [&](int chunk) {
+        net_launches = trace_nerf(c, P, vol, cam, sc, tr0, tr1, own0, own1, mode, target, [&](int chunk) {
             if (!rt_enqueued && chunk == rt_start_chunk) enqueue_raytracer(c->ev_nerf1);
         });
         launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
@@ -1135,7 +1155,7 @@ void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* o
     const TraceMode mode{1, rm, (float)c->p("depth_scale")};
     HIPCHK(hipEventRecord(c->ev_start, c->s_nerf));
     HIPCHK(hipEventRecord(c->ev_nerf0, c->s_nerf));
-    const uint32_t net_launches = trace_nerf(c, P, vol, cam, sc, r0, r1, mode, target, [](int) {});
+    const uint32_t net_launches = trace_nerf(c, P, vol, cam, sc, r0, r1, r0, r1, mode, target, [](int) {});
     HIPCHK(hipEventRecord(c->ev_end, c->s_nerf));
     HIPCHK(hipMemcpyAsync(c->h_ctrl, c->ctrl.p, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
     HIPCHK(hipGetLastError());
@@ -1185,7 +1205,7 @@ void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
     HIPCHK(hipStreamCreateWithPriority(&c->s_rt, hipStreamNonBlocking, prio_lo));
     for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go}) HIPCHK(hipEventCreate(e));
     HIPCHK(hipHostMalloc((void**)&c->h_ctrl, sizeof(MarchCtrl), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc((void**)&c->h_alive, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c->h_alive, 8 * sizeof(uint32_t), hipHostMallocDefault));
     float rf = fov_to_focal(50.625f);   // Testbed::reset_camera -> set_fov(50.625) (testbed.cu:480)
     c->rel_focal[0] = c->rel_focal[1] = rf;
     // reset_camera matrix: transpose(mat3x4{1,0,0,0.5; 0,-1,0,0.5; 0,0,-1,0.5}), then pos -= scale*dir
@@ -1200,6 +1220,7 @@ void ctx_destroy(sng_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
+    comm_destroy(c->sched_comm);
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
@@ -1497,6 +1518,31 @@ int sng_render_nerf_ngp(sng_ctx* c, const sng_frame_params* p, sng_frame_result*
 }
 int sng_render_frame(sng_ctx* c, const sng_frame_params* p, sng_frame_result* out) {
     return guarded([&] { HIPCHK(hipSetDevice(c->device)); render_frame(c, p, out); });
+}
+int sng_comm_unique_id(uint8_t* out) {
+    return guarded([&] {
+        if (!out) throw SngError(SNG_ERR_INVALID, "null id buffer");
+        comm_unique_id(out);
+    });
+}
+int sng_set_comm(sng_ctx* c, const uint8_t* id, int rank, int world) {
+    return guarded([&] {
+        if (!c) throw SngError(SNG_ERR_INVALID, "null context");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipStreamSynchronize(c->s_nerf));
+        if (!id) { comm_destroy(c->sched_comm); return; }
+        if (world < 1 || rank < 0 || rank >= world) throw SngError(SNG_ERR_INVALID, "bad rank/world");
+        if (c->sched_comm.host_fn) throw SngError(SNG_ERR_STATE, "a host schedule reducer is attached");
+        comm_init(c->sched_comm, id, rank, world);
+    });
+}
+int sng_set_sched_reducer(sng_ctx* c, sng_sched_reduce_fn fn, void* user) {
+    return guarded([&] {
+        if (!c) throw SngError(SNG_ERR_INVALID, "null context");
+        if (fn && c->sched_comm.comm) throw SngError(SNG_ERR_STATE, "an RCCL communicator is attached");
+        c->sched_comm.host_fn = fn;
+        c->sched_comm.host_user = fn ? user : nullptr;
+    });
 }
 int sng_synchronize(sng_ctx* c) { return guarded([&] { HIPCHK(hipStreamSynchronize(c->s_nerf)); HIPCHK(hipStreamSynchronize(c->s_rt)); }); }
 int sng_copy_to_host(sng_ctx* c, const void* src, void* dst, uint64_t n) {

@@ -90,6 +90,7 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
         }
     }
     uint32_t slot = wave_append(&ctrl->n_alive[0], alive, lane);
+    if (a.sched.global) (void)wave_append(&ctrl->n_owned[0], alive && idx >= a.sched.own_lo && idx < a.sched.own_hi, lane);
     if (alive) {
         out.o_t[slot] = make_float4(origin.x, origin.y, origin.z, tt);
         out.d_idx[slot] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(idx));
@@ -111,14 +112,16 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
 // bitfield gathers).  The general path (cascades / cone stepping) keeps the unrolled form.
 template <bool LIN>
 __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
-                                                       float* __restrict__ coords, uint2* __restrict__ samp, int store_t) {
+                                                       float* __restrict__ coords, uint2* __restrict__ samp, int store_t, int global_sched) {
     __shared__ float ts_lds[LIN ? MAX_STEPS_BETWEEN_COMPACTION * 256 : 1];
     const uint32_t n_alive = ctrl->n_alive[p];
+    const uint32_t n_sched = global_sched ? ctrl->sched_alive[p] : n_alive;   // Sched
     const uint32_t i_step = ctrl->i_step[p];
-    const bool active = n_alive > 0 && i_step < MARCH_ITER;
-    const uint32_t n_steps = active ? steps_for(n_alive, target) : 0;
+    const bool active = n_sched > 0 && i_step < MARCH_ITER;
+    const uint32_t n_steps = active ? steps_for(n_sched, target) : 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctrl->n_alive[p ^ 1] = 0;
+        ctrl->n_owned[p ^ 1] = 0;
         ctrl->i_step[p ^ 1] = i_step + n_steps;
         if (active) {
             if (iter < 64) { ctrl->alive_hist[iter] = n_alive; ctrl->steps_hist[iter] = n_steps; }
@@ -213,13 +216,14 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
 // composite_kernel_nerf_alt (476-575) + compaction into the next buffer
 // (compact_kernel_nerf 1830-1853) + extract_from_payload (1578-1612)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, TraceMode mode, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
-                                                        const float* __restrict__ coords, const uint2* __restrict__ samp,
+__global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, TraceMode mode, Sched sched, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p,
+                                                        uint32_t target, uint32_t iter, const float* __restrict__ coords, const uint2* __restrict__ samp,
                                                         const uint2* __restrict__ net_out, float4* __restrict__ frame_rgba,
                                                         float* __restrict__ frame_depth, float* __restrict__ positions) {
     const uint32_t n_alive = ctrl->n_alive[p];
+    const uint32_t n_sched = sched.global ? ctrl->sched_alive[p] : n_alive;
     const uint32_t i_step = ctrl->i_step[p];
-    const bool active = n_alive > 0 && i_step < MARCH_ITER;
+    const bool active = n_sched > 0 && i_step < MARCH_ITER;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (active) {
             ctrl->total_samples += ctrl->n_samples[p];
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
         ctrl->n_samples[p ^ 1] = 0;
     }
     if (!active) return;
-    const uint32_t n_steps = steps_for(n_alive, target);
+    const uint32_t n_steps = steps_for(n_sched, target);
     // the reference leaves the loop without another compaction once i >= MARCH_ITER
     const bool last = i_step + n_steps >= MARCH_ITER;
     const int lane = threadIdx.x & 63;
@@ -289,6 +293,10 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
             else survive = !last;
         }
         const uint32_t slot = wave_append(&ctrl->n_alive[p ^ 1], survive, lane);
+        if (sched.global) {
+            const uint32_t idx = __float_as_uint(di.w);
+            (void)wave_append(&ctrl->n_owned[p ^ 1], survive && idx >= sched.own_lo && idx < sched.own_hi, lane);
+        }
         if (survive) {
             out.o_t[slot] = ot;
             out.d_idx[slot] = di;
@@ -423,6 +431,8 @@ __global__ void ctrl_init_kernel(MarchCtrl* c) {
     }
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         c->n_alive[0] = 0; c->n_alive[1] = 0;
+        c->n_owned[0] = 0; c->n_owned[1] = 0;
+        c->sched_alive[0] = 0; c->sched_alive[1] = 0;
         c->n_samples[0] = 0; c->n_samples[1] = 0;
         c->i_step[0] = 1; c->i_step[1] = 1;   // trace_alt: uint32_t i = 1 (2163)
         c->n_hit = 0; c->n_iter = 0;
@@ -441,14 +451,14 @@ void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl
     hipLaunchKernelGGL(init_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, out, ctrl, fb, depth, pos, nrm);
 }
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
-                     uint32_t blocks, int store_t, hipStream_t s) {
-    if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t);
-    else hipLaunchKernelGGL(generate_kernel<false>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t);
+                     uint32_t blocks, int store_t, int global_sched, hipStream_t s) {
+    if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
+    else hipLaunchKernelGGL(generate_kernel<false>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
 }
-void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
-                      const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
-                      hipStream_t s) {
-    hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, s, v, cam, mode, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
+void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const Sched& sched, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p,
+                      uint32_t target, uint32_t iter, const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos,
+                      uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
 }
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;

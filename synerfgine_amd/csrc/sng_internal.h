@@ -3,6 +3,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdexcept>
+#include <string>
+
+#include "../../include/sng.h"
+
 #include "sng_math.h"
 
 namespace sng {
@@ -30,6 +35,8 @@ struct NetworkDev {
 // Wavefront control block (device), ping-pong by iteration parity.
 struct MarchCtrl {
     uint32_t n_alive[2];
+    uint32_t n_owned[2];      // alive rays of the band's own rows (Sched::own_lo/hi), counted when Sched::global
+    uint32_t sched_alive[2];  // frame-wide alive count (sum of n_owned over ranks) the step schedule uses
     uint32_t n_samples[2];
     uint32_t i_step[2];
     uint32_t n_hit;
@@ -63,6 +70,15 @@ struct CamDev {
     f3 c0, c1, c2, c3;   // mat4x3 columns (right, down, fwd, position)
 };
 
+// Step schedule of a band: n_steps = clamp(target / n_alive, 1, 8) uses the
+// FRAME-wide alive count (testbed_nerf.cu:2189-2190).  global = 1: the kernels read
+// MarchCtrl::sched_alive (the sum over ranks of the rays alive in each band's own rows, pixel
+// indices [own_lo, own_hi)), so every band marches with the single-GPU schedule.
+struct Sched {
+    int global;
+    uint32_t own_lo, own_hi;
+};
+
 struct NerfFrameArgs {
     Volume vol;
     CamDev cam;          // camera0 (composite/extract)
@@ -76,6 +92,7 @@ struct NerfFrameArgs {
     int reset;           // clear alpha of the frame buffer (camera moved)
     uint32_t target_n_queries;
     TraceMode mode;
+    Sched sched;
 };
 
 // fused.hip: ray-local NeRF wavefront (generate + field + composite in one persistent kernel)
@@ -151,9 +168,9 @@ struct RtQueue {
 // nerf.hip
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, hipStream_t s);
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
-                     uint32_t blocks, int store_t, hipStream_t s);
-void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
-                      const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
+                     uint32_t blocks, int store_t, int global_sched, hipStream_t s);
+void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const Sched& sched, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p,
+                      uint32_t target, uint32_t iter, const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
                       hipStream_t s);
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s);
 void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, uint32_t* occ_linear,
@@ -183,5 +200,25 @@ void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, ui
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
                     const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s);
 void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s);
+
+// error carrying an sng_status code (capi.cpp turns it into the return value + sng_last_error)
+struct SngError : std::runtime_error {
+    int code;
+    SngError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// comm.cpp: the frame-wide step schedule exchange (Sched).  Either an RCCL communicator (device
+// all-reduce on the NeRF stream) or a host callback (sng_set_sched_reducer) sums the counts.
+struct SchedComm {
+    void* comm = nullptr;              // ncclComm_t
+    int rank = 0, world = 0;
+    sng_sched_reduce_fn host_fn = nullptr;
+    void* host_user = nullptr;
+    bool active() const { return comm != nullptr || host_fn != nullptr; }
+};
+void comm_unique_id(uint8_t out[SNG_COMM_ID_BYTES]);
+void comm_init(SchedComm& c, const uint8_t* id, int rank, int world);
+void comm_destroy(SchedComm& c);
+void comm_allreduce_u32(SchedComm& c, uint32_t* dev, size_t n, hipStream_t s);
 
 }  // namespace sng

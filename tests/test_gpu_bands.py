@@ -1,0 +1,146 @@
+"""Multi-GPU band path: row bands rendered by separate ranks, with the frame-wide
+step schedule exchanged every wavefront iteration, reproduce the single-GPU frame bit for bit.
+
+The ranks here are processes sharing the one GPU of the test box; the schedule exchange runs
+through the host reducer (gloo all_reduce), the transport-independent half of sng_set_comm.
+The RCCL transport itself is checked at world size 1 (a second rank cannot share the GPU).
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+# a smaller wavefront budget than the default 2^21 so that clamp(target / n_alive, 1, 8) varies
+# over the iterations (at 2^21 every C3 iteration takes 8 steps and the schedule is moot)
+TARGET = 1 << 17
+
+
+def _prefix_equal(a, b):
+    n = min(len(a), len(b))   # the fused tail may end a band's iterations early
+    return n > 0 and np.array_equal(a[:n], b[:n])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _band_worker(rank, world, port, bounds, overrides, out_dir):
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from synerfgine_amd import scene as S
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tb, eng, _ = S.make_engine("c3", overrides=overrides)
+
+        def reduce_fn(vals):
+            t = torch.tensor(vals, dtype=torch.int64)
+            dist.all_reduce(t)
+            return t.tolist()
+
+        r0, r1 = bounds[rank], bounds[rank + 1]
+        rng = [eng.rng_states(0), eng.rng_states(1)]
+
+        def fresh():   # every frame below starts from the same per-pixel RNG streams
+            eng.set_rng_states(0, rng[0])
+            eng.set_rng_states(1, rng[1])
+
+        res = {}
+        # independent bands (local schedule) first, then the frame-wide schedule
+        fresh()
+        r = eng.frame(rows=(r0, r1), target_n_queries=TARGET)
+        res["local_steps"] = np.array(r.steps_per_iter, np.int64)
+        eng.attach_host_reducer(reduce_fn)
+        fresh()
+        r = eng.frame(rows=(r0, r1), target_n_queries=TARGET)
+        res["global_steps"] = np.array(r.steps_per_iter, np.int64)
+        res["band"] = r.download("final_rgba")[r0:r1]
+        eng.detach_comm()
+        if rank == 0:   # the single-GPU frame
+            fresh()
+            r = eng.frame(target_n_queries=TARGET)
+            res["full_steps"] = np.array(r.steps_per_iter, np.int64)
+            res["full"] = r.download("final_rgba")
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
+        tb.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bounds,overrides", [
+    ([0, 540, 1080], {}),
+    ([0, 301, 777, 1080], {}),
+    ([0, 301, 1080], {"res_factor": 16}),   # NeRF at half resolution: bands split NeRF rows by ceil(y / 2)
+], ids=["even2", "uneven3", "halfres2"])
+def test_bands_with_global_schedule_equal_single_gpu(bounds, overrides):
+    import torch.multiprocessing as mp
+    world = len(bounds) - 1
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        procs = [ctx.Process(target=_band_worker, args=(r, world, port, bounds, overrides, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=400)
+        codes = [p.exitcode for p in procs]
+        for p in procs:
+            if p.exitcode is None:
+                p.kill()
+        assert codes == [0] * world, codes
+        res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
+    full = res[0]["full"]
+    for r in range(world):
+        r0, r1 = bounds[r], bounds[r + 1]
+        # the frame-wide schedule is the single-GPU one ...
+        assert _prefix_equal(res[r]["global_steps"], res[0]["full_steps"])
+        # ... and the band equals the single-GPU frame's rows bit for bit
+        assert np.array_equal(res[r]["band"].view(np.uint32), full[r0:r1].view(np.uint32)), f"rank {r}"
+    # without the exchange the bands step differently (the check above is not vacuous)
+    assert any(not _prefix_equal(res[r]["local_steps"], res[0]["full_steps"]) for r in range(world))
+
+
+def test_rccl_schedule_world1_matches_local():
+    """sng_set_comm at world size 1: RCCL all-reduce of the count on the NeRF stream."""
+    import ctypes
+    from synerfgine_amd import _lib
+    from synerfgine_amd import scene as S
+    tb, eng, _ = S.make_engine("c3")
+    try:
+        rng = [eng.rng_states(0), eng.rng_states(1)]
+
+        def fresh():
+            eng.set_rng_states(0, rng[0])
+            eng.set_rng_states(1, rng[1])
+
+        fresh()
+        a = eng.frame(target_n_queries=TARGET)
+        ref = a.download("final_rgba")
+        lib = eng._lib
+        uid = (ctypes.c_uint8 * _lib.SNG_COMM_ID_BYTES)()
+        _lib.check(lib.sng_comm_unique_id(uid))
+        _lib.check(lib.sng_set_comm(eng.ctx, uid, 0, 1))
+        fresh()
+        b = eng.frame(target_n_queries=TARGET)
+        got = b.download("final_rgba")
+        assert list(b.steps_per_iter) == list(a.steps_per_iter)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+        # a host reducer cannot be attached on top of a communicator
+        with pytest.raises(_lib.SngError):
+            eng.attach_host_reducer(lambda v: v)
+        eng.detach_comm()
+        fresh()
+        c = eng.frame(target_n_queries=TARGET)
+        assert np.array_equal(c.download("final_rgba").view(np.uint32), ref.view(np.uint32))
+    finally:
+        tb.close()
