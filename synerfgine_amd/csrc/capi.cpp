@@ -280,12 +280,45 @@ struct HostObject {
     std::string file;
     std::vector<Tri> tris;
     std::vector<BvhNode> nodes;
+    std::vector<BvhWide> wide;    // traversal layout of `nodes` (wide_bvh), empty if not representable
+    int root_ref = 0;
     m3 rot;
     f3 pos;
     float scale = 1.0f;
     int mat = 0;
-    DevBuf d_nodes, d_tris;
+    DevBuf d_nodes, d_tris, d_wide;
 };
+
+// BvhWide records of the inner nodes of a TriangleBvhNode array (children at left, left + 1).
+// Returns false when a leaf range does not fit the reference encoding (the walk then uses nodes).
+bool wide_bvh(const std::vector<BvhNode>& nodes, std::vector<BvhWide>& wide, int& root_ref) {
+    std::vector<int> id(nodes.size(), -1);
+    int n_inner = 0;
+    for (size_t i = 0; i < nodes.size(); ++i)
+        if (nodes[i].left >= 0) id[i] = n_inner++;
+    bool ok = true;
+    auto ref_of = [&](int i) -> int {
+        const BvhNode& n = nodes[i];
+        if (n.left >= 0) return id[i];
+        const int b = -n.left - 1, e = -n.right - 1;
+        if (b < 0 || e < b || (uint32_t)b >= WIDE_MAX_BEGIN || (uint32_t)(e - b) > WIDE_MAX_COUNT) { ok = false; return 0; }
+        return (int)~((uint32_t)b | ((uint32_t)(e - b) << 24));
+    };
+    wide.assign(n_inner, BvhWide{});
+    for (size_t i = 0; i < nodes.size(); ++i) {
+        const BvhNode& n = nodes[i];
+        if (n.left < 0) continue;
+        if ((size_t)n.left + 1 >= nodes.size()) return false;
+        BvhWide& w = wide[id[i]];
+        const BvhNode &c0 = nodes[n.left], &c1 = nodes[n.left + 1];
+        for (int k = 0; k < 3; ++k) { w.lo0[k] = c0.lo[k]; w.hi0[k] = c0.hi[k]; w.lo1[k] = c1.lo[k]; w.hi1[k] = c1.hi[k]; }
+        w.ref0 = ref_of(n.left);
+        w.ref1 = ref_of(n.left + 1);
+    }
+    root_ref = nodes.empty() ? 0 : ref_of(0);
+    if (!ok) wide.clear();
+    return ok;
+}
 
 const std::map<std::string, double>& default_params() {
     static const std::map<std::string, double> d = {
@@ -313,12 +346,14 @@ const std::map<std::string, double>& default_params() {
         {"smooth_threshold", 1.0},              // sng_position_kernel_threshold (unused by the path)
         {"max_shadow_variance", 0.0},           // sng_shadow_depth_variance (unused by the path)
         {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
-        {"rt_start_chunk", 1},                  // concurrent mode: raytracer starts after this many 4-iteration NeRF chunks
+        {"rt_start_chunk", -1},                 // concurrent mode: raytracer starts after this many 4-iteration NeRF chunks (-1: 1 for
+                                                //   bands of >= 60 % of the rows, else 0 -- thin bands are latency bound)
         {"rt_reserved_cus", 16},                // concurrent mode: CUs (2 per XCD) the persistent raytracer grids leave to the NeRF stream
         {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"rt_staged", 0},                       // ... plus primary / shade / bounce stages over compacted queues
+        {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
@@ -597,7 +632,16 @@ void upload_scene(sng_ctx* c) {
         for (const BvhNode& n : o.nodes)
             for (int k = 0; k < 3; ++k) max_coord = std::max(max_coord, std::max(std::fabs(n.lo[k]), std::fabs(n.hi[k])));
         g.fast_slab = (c->p("fast_slab") != 0.0 && max_coord < SLAB_FAST_MAX_COORD) ? 1 : 0;
-        g.lds_nodes = append(o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
+        const bool wide = c->p("bvh_wide") != 0.0 && wide_bvh(o.nodes, o.wide, o.root_ref);
+        if (wide) {
+            upload(o.d_wide, o.wide.data(), std::max<size_t>(1, o.wide.size()) * sizeof(BvhWide));
+            g.wide = o.d_wide.as<BvhWide>();
+            g.lds_wide = append(o.wide.data(), o.wide.size() * sizeof(BvhWide));
+            g.root_ref = o.root_ref;
+            g.lds_nodes = 0;   // the node array is not needed by the traversal
+        } else {
+            g.lds_nodes = append(o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
+        }
         g.lds_tris = append(o.tris.data(), o.tris.size() * sizeof(Tri));
         c->bvh_depth = std::max(c->bvh_depth, bvh_depth(o.nodes));
         og.push_back(g);
@@ -702,7 +746,7 @@ void load_scene(sng_ctx* c, const std::string& path) {
     }
     for (auto& o : objs)
         if (o.mat < 0 || (size_t)o.mat >= mats.size()) throw SngError(SNG_ERR_INVALID, "object material index out of range");
-    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
+    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_wide.release(); }
     c->objs = std::move(objs);
     c->mats = mats;
     c->lights = lights;
@@ -944,7 +988,8 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     // wavefront iterations, i.e. once the NeRF's throughput-heavy head (nearly all rays alive)
     // has run on the whole GPU; it then overlaps the latency-bound tail iterations.
     const bool concurrent = c->p("concurrent_streams") != 0.0;
-    const int rt_start_chunk = (concurrent && show_nerf) ? (int)c->p("rt_start_chunk") : 0;
+    int rt_start_chunk = (concurrent && show_nerf) ? (int)c->p("rt_start_chunk") : 0;
+    if (rt_start_chunk < 0) rt_start_chunk = (y1 - y0) * 10 >= MH * 6 ? 1 : 0;
     bool rt_enqueued = false;
     auto enqueue_raytracer = [&](hipEvent_t after) {
         HIPCHK(hipStreamWaitEvent(c->s_rt, after, 0));
@@ -1221,7 +1266,7 @@ void ctx_destroy(sng_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     comm_destroy(c->sched_comm);
-    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
+    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_wide.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
@@ -1417,7 +1462,7 @@ int sng_hashgrid_encode(sng_ctx* c, const float* coords, uint32_t stride, uint32
 int sng_load_virtual_scene(sng_ctx* c, const char* path) { return guarded([&] { load_scene(c, path); }); }
 int sng_clear_virtual_scene(sng_ctx* c) {
     return guarded([&] {
-        for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); }
+        for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_wide.release(); }
         c->objs.clear(); c->lights.clear(); c->mats.clear();
         c->scene_dirty = true;
     });
@@ -1430,7 +1475,7 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
         if (!default_params().count(k)) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
         c->params[k] = v;
         c->mesh_reset = true;
-        if ((k == "fast_slab" || k == "scene_lds") && !c->objs.empty()) upload_scene(c);
+        if ((k == "fast_slab" || k == "scene_lds" || k == "bvh_wide") && !c->objs.empty()) upload_scene(c);
     });
 }
 int sng_get_param(sng_ctx* c, const char* key, double* v) {

@@ -40,6 +40,10 @@ struct TraceCtx {
         if constexpr (LDS) return reinterpret_cast<const BvhNode*>(scene + o.lds_nodes);
         else return o.nodes;
     }
+    __device__ __forceinline__ const BvhWide* wide(const ObjectGpu& o) const {
+        if constexpr (LDS) return reinterpret_cast<const BvhWide*>(scene + o.lds_wide);
+        else return o.wide;
+    }
     __device__ __forceinline__ const Tri* tris(const ObjectGpu& o) const {
         if constexpr (LDS) return reinterpret_cast<const Tri*>(scene + o.lds_tris);
         else return o.tris;
@@ -121,13 +125,51 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
     tri_out = shortest;
     return mint;
 }
+// The same traversal over the BvhWide layout: identical box tests, push order, overflow rule and
+// triangle order, so identical results; one record load per inner node, none per leaf.
+template <bool FAST>
+__device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const Tri* __restrict__ tris, int root_ref,
+                                               int* stack_lds, int stride, int& tri_out, float t_max) {
+    Stack st{stack_lds, stride, 0};
+    st.push(root_ref);
+    float mint = t_max;
+    int shortest = -1;
+    while (st.n > 0) {
+        const int ref = st.pop();
+        if (ref < 0) {
+            const uint32_t e = ~(uint32_t)ref;
+            const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
+            for (int i = b; i < end; ++i) {
+                float t;
+                if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
+            }
+        } else {
+            const BvhWide w = wide[ref];
+            const aabb b0 = {mk(w.lo0[0], w.lo0[1], w.lo0[2]), mk(w.hi0[0], w.hi0[1], w.hi0[2])};
+            const aabb b1 = {mk(w.lo1[0], w.lo1[1], w.lo1[2]), mk(w.hi1[0], w.hi1[1], w.hi1[2])};
+            float d0 = FAST ? aabb_entry_fast(b0, ro, rd, y) : aabb_entry(b0, ro, rd);
+            float d1 = FAST ? aabb_entry_fast(b1, ro, rd, y) : aabb_entry(b1, ro, rd);
+            int i0 = w.ref0, i1 = w.ref1;
+            if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = w.ref1; i1 = w.ref0; }
+            if (d0 < mint) { if (st.n >= BVH_STACK - 1) { } else st.push(i0); }
+            if (d1 < mint) { if (st.n >= BVH_STACK - 1) { } else st.push(i1); }
+        }
+    }
+    tri_out = shortest;
+    return mint;
+}
 // t_max < MAX_DEPTH culls everything at or beyond t_max (the result is then min(closest, t_max));
 // only the shadow kernel uses it, where any value >= full_dist yields the same mask.
 template <bool LDS>
 __device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, const TraceCtx<LDS>& cx, int& tri, float t_max = MAX_DEPTH) {
     const f3 oro = mul(o.world_to_obj, ro - o.pos);
     const f3 ord = mul(o.world_to_obj, rd);
-    if (o.fast_slab && slab_fast_ok(oro, ord)) return bvh_walk<true>(oro, ord, inv(ord), cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max);
+    const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
+    if (o.wide) {
+        if (fast) return bvh_walk_wide<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
+        return bvh_walk_wide<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
+    }
+    if (fast) return bvh_walk<true>(oro, ord, inv(ord), cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max);
     return bvh_walk<false>(oro, ord, ord, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max);
 }
 

@@ -388,6 +388,12 @@ SNG_HD float curand_uniform(Xorwow& s) {
 // ---- scene records ------------------------------------------------------------
 struct BvhNode { float lo[3], hi[3]; int left, right; };   // TriangleBvhNode (32 B)
 struct Tri { f3 a, b, c; };                                 // Triangle (36 B)
+// Traversal layout of the same BVH (capi.cpp wide_bvh): one 64-B record per INNER node holding
+// both children's boxes and references, so visiting a node is one load and a leaf needs none
+// (its triangle range travels in the stack entry).  ref >= 0: inner record index;
+// ref < 0: leaf, ~ref = first_triangle | triangle_count << 24.
+struct BvhWide { float lo0[3], hi0[3], lo1[3], hi1[3]; int ref0, ref1, pad0, pad1; };
+constexpr uint32_t WIDE_MAX_BEGIN = 1u << 24, WIDE_MAX_COUNT = 127u;
 struct ObjectGpu {                                           // ObjectTransform + hoisted inverse
     const BvhNode* nodes;
     const Tri* tris;
@@ -398,6 +404,9 @@ struct ObjectGpu {                                           // ObjectTransform 
     m3 world_to_obj;   // (I/scale) * inverse(rot), triangle_bvh.cu:313-319
     int fast_slab;     // every BVH box coordinate < 2^40 in magnitude: aabb_entry_fast is exact
     uint32_t lds_nodes, lds_tris;   // byte offsets of this object's arrays in the scene blob
+    const BvhWide* wide;            // traversal layout (nullptr: walk the TriangleBvhNode array)
+    uint32_t lds_wide;              // its byte offset in the scene blob
+    int root_ref;                   // stack entry of the root
 };
 struct LightGpu { f3 pos; float intensity; float size; int type; };
 struct MaterialGpu { f3 ka, kd, ks; float n, rg, spec_angle; int type; };

@@ -262,6 +262,26 @@ def test_wavefront_raytracer_equals_megakernel(overrides):
         tb.close()
 
 
+@pytest.mark.parametrize("config,overrides", [("c3", {}), ("c3", {"scene_lds": 0}), ("c3", {"rt_wavefront": 0}), ("c4", {})])
+def test_wide_bvh_layout_equals_node_walk(config, overrides):
+    """The BvhWide traversal layout (bvh_wide=1) reproduces the TriangleBvhNode walk bit for bit."""
+    tb, eng, _ = _engine(192, 108, overrides, config=config)
+    try:
+        m0, n0 = eng.rng_states(1).copy(), eng.rng_states(0).copy()
+        out = {}
+        for wide in (0, 1):
+            eng.set_rng_states(0, n0)
+            eng.set_rng_states(1, m0)
+            eng.set_param("bvh_wide", wide)
+            r = eng.frame()
+            out[wide] = (r.download("syn_rgba"), r.download("syn_depth"), r.download("final_rgba"), eng.rng_states(1).copy())
+        for a, b in zip(out[0], out[1]):
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert (out[1][1] < 100).mean() > 0.02    # objects are in view
+    finally:
+        tb.close()
+
+
 def test_kitchen_cascaded_nerf_matches_oracle():
     """C4 class: aabb_scale 16, 5 cascades, cone stepping -- the general marcher path."""
     r, got, ref, st = _frame_vs_oracle(128, 72, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, config="c4")
