@@ -165,6 +165,37 @@ int sng_render_frame(sng_ctx* ctx, const sng_frame_params* params, sng_frame_res
  * composite_kernel_nerf 577-788, shade_kernel_nerf 1788-1828) into d_nerf_rgba / d_nerf_depth at NeRF
  * resolution; parameters "render_mode" (ERenderMode) and "depth_scale".  row_begin/row_end are NeRF rows. */
 int sng_render_nerf_ngp(sng_ctx* ctx, const sng_frame_params* params, sng_frame_result* out);
+/* ---- online training (BASELINE config 5; Testbed::train_nerf, testbed_nerf.cu:3298-3780) ----------
+ * Training images: n RGBA8 sRGB images of w x h (0x00FF00FF = masked pixel), one camera per image
+ * as a column-major mat4x3 in NGP space (c0 c1 c2 c3, i.e. nerf_matrix_to_ngp already applied,
+ * nerf_loader.h:101-120), focal lengths in pixels, principal points in uv.  The model (config,
+ * aabb, cascades) is the one set by sng_set_nerf_model / sng_load_snapshot. */
+typedef struct {
+    uint32_t step;                              /* training steps done */
+    float loss;                                 /* loss of the last step (NerfCounters::update_after_training) */
+    uint32_t rays_per_batch;                    /* adapted to reach the target batch */
+    uint32_t measured_batch;                    /* compacted samples of the last step */
+    uint32_t measured_batch_before_compaction;
+    float ms;                                   /* device time of the call */
+    uint32_t reserved[10];
+} sng_train_stats;
+/* 8-bit PNG -> RGBA8 (host): the dataset loader's image decode (nerf_loader.cu, stb_image); out may be NULL to query the size */
+int sng_image_load_png(const char* path, uint8_t* out_rgba8, uint64_t capacity, int32_t* width, int32_t* height);
+int sng_train_set_dataset(sng_ctx* ctx, uint32_t n_images, uint32_t width, uint32_t height, const uint8_t* rgba8, const float* xforms_4x3,
+                          const float* focal_px, const float* principal_uv);
+/* Testbed::reset_network's training state: fp32 master weights from the current model, zero
+ * moments, m_rng = pcg32(seed), density_grid_rng = pcg32(m_rng.next_uint()) (testbed.cu:3654-3667) */
+int sng_train_reset(sng_ctx* ctx, uint64_t seed);
+/* n_steps x (training_prep_nerf schedule + train_nerf_step + optimizer step); afterwards the EMA
+ * weights and the trained density grid are the render path's model */
+int sng_train(sng_ctx* ctx, uint32_t n_steps, sng_train_stats* stats);
+/* snapshot fields of the trained model: params fp16 (tcnn order) and density_grid fp16 */
+int sng_train_export(sng_ctx* ctx, uint16_t* params_out, uint64_t n_params, uint16_t* density_grid_out, uint64_t n_cells);
+/* parity hook: run train_nerf_step up to `stage` (1 samples, 2 network outputs, 3 loss, 4 gradients)
+ * without an optimizer step, then copy the named buffer ("ctrl", "ray_indices", "rays", "numsteps",
+ * "coords", "mlp_out", "coords_c", "dloss", "loss", "grads", "acts", "grid", "master") to host */
+int sng_train_debug(sng_ctx* ctx, int stage, const char* buffer, void* out, uint64_t capacity_bytes, uint64_t* size_bytes);
+
 /* ---- multi-GPU step schedule --------------------------------------------------
  * trace_alt sizes each wavefront iteration from the FRAME-wide alive count
  * (n_steps = clamp(2^21 / n_alive, 1, 8), testbed_nerf.cu:2180-2190).  A rank that renders one row

@@ -76,6 +76,40 @@ class Testbed:
         check(self._lib.sng_get_density_mean(self.ctx, ctypes.byref(v)))
         return v.value
 
+    # ---- online training (Testbed::train_nerf, testbed_nerf.cu:3298-3780) ---------
+    def set_training_dataset(self, images_rgba8, xforms, focal, principal=None):
+        """images [n, h, w, 4] uint8 sRGB; xforms [n, 3, 4] NGP-space camera (columns c0..c3);
+        focal [n, 2] in pixels; principal [n, 2] in uv (default 0.5)."""
+        im = np.ascontiguousarray(images_rgba8, np.uint8)
+        n, h, w, _ = im.shape
+        xf = np.ascontiguousarray(np.asarray(xforms, np.float32).reshape(n, 3, 4).transpose(0, 2, 1).reshape(n, 12))   # column-major
+        fo = np.ascontiguousarray(np.asarray(focal, np.float32).reshape(n, 2))
+        pp = np.ascontiguousarray(np.full((n, 2), 0.5, np.float32) if principal is None else np.asarray(principal, np.float32).reshape(n, 2))
+        check(self._lib.sng_train_set_dataset(self.ctx, n, w, h, im.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _fptr(xf), _fptr(fo), _fptr(pp)))
+
+    def train_reset(self, seed=1337):
+        check(self._lib.sng_train_reset(self.ctx, int(seed)))
+
+    def train(self, n_steps):
+        st = _lib.sng_train_stats()
+        check(self._lib.sng_train(self.ctx, int(n_steps), ctypes.byref(st)))
+        return {k: getattr(st, k) for k in ("step", "loss", "rays_per_batch", "measured_batch", "measured_batch_before_compaction", "ms")}
+
+    def training_snapshot(self, n_params, n_cells):
+        """(params fp16, density grid fp16) of the trained model -- the .ingp snapshot fields"""
+        p = np.zeros(n_params, np.uint16)
+        g = np.zeros(n_cells, np.uint16)
+        check(self._lib.sng_train_export(self.ctx, p.ctypes.data_as(_lib.U16P), n_params, g.ctypes.data_as(_lib.U16P), n_cells))
+        return p.view(np.float16), g.view(np.float16)
+
+    def train_debug(self, stage, name, dtype=np.uint8):
+        """parity hook: run the training step up to `stage`, return the named device buffer"""
+        n = ctypes.c_uint64()
+        check(self._lib.sng_train_debug(self.ctx, int(stage), name.encode(), None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, np.uint8)
+        check(self._lib.sng_train_debug(self.ctx, 0, name.encode(), out.ctypes.data_as(ctypes.c_void_p), out.nbytes, None))
+        return out.view(dtype)
+
     # ---- NerfNetwork::inference_mixed_precision (nerf_network.h:105) -------------
     def inference_mixed_precision(self, d_coords, stride_floats, n, d_out, layout=0, stream=0):
         """Device pointers in, device pointer out (layout 0: tcnn [16][n]; 1: [n][4])."""

@@ -118,6 +118,18 @@ FP = ctypes.POINTER(ctypes.c_float)
 U16P = ctypes.POINTER(ctypes.c_uint16)
 U32P = ctypes.POINTER(ctypes.c_uint32)
 
+class sng_train_stats(ctypes.Structure):
+    _fields_ = [
+        ("step", ctypes.c_uint32),
+        ("loss", ctypes.c_float),
+        ("rays_per_batch", ctypes.c_uint32),
+        ("measured_batch", ctypes.c_uint32),
+        ("measured_batch_before_compaction", ctypes.c_uint32),
+        ("ms", ctypes.c_float),
+        ("reserved", ctypes.c_uint32 * 10),
+    ]
+
+
 SNG_COMM_ID_BYTES = 128
 # int (*sng_sched_reduce_fn)(uint32_t* values, uint32_t n, void* user)
 SCHED_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_void_p)
@@ -157,6 +169,12 @@ SIGNATURES = {
     "sng_get_resolution": (ctypes.c_int, [P, ctypes.POINTER(sng_resolution_info)]),
     "sng_render_frame": (ctypes.c_int, [P, ctypes.POINTER(sng_frame_params), ctypes.POINTER(sng_frame_result)]),
     "sng_render_nerf_ngp": (ctypes.c_int, [P, ctypes.POINTER(sng_frame_params), ctypes.POINTER(sng_frame_result)]),
+    "sng_image_load_png": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), U64, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
+    "sng_train_set_dataset": (ctypes.c_int, [P, U32, U32, U32, ctypes.POINTER(ctypes.c_uint8), FP, FP, FP]),
+    "sng_train_reset": (ctypes.c_int, [P, U64]),
+    "sng_train": (ctypes.c_int, [P, U32, ctypes.POINTER(sng_train_stats)]),
+    "sng_train_export": (ctypes.c_int, [P, U16P, U64, U16P, U64]),
+    "sng_train_debug": (ctypes.c_int, [P, ctypes.c_int, ctypes.c_char_p, P, U64, ctypes.POINTER(U64)]),
     "sng_comm_unique_id": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint8)]),
     "sng_set_comm": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int]),
     "sng_set_sched_reducer": (ctypes.c_int, [P, P, P]),

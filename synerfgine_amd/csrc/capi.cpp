@@ -24,6 +24,7 @@
 
 #include "json.h"
 #include "sng_internal.h"
+#include "train.h"
 
 using namespace sng;
 
@@ -358,7 +359,10 @@ const std::map<std::string, double>& default_params() {
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)
-        {"rt_queue_gb", 48},                    // device-memory budget for the deferred-shadow queues
+        {"rt_queue_gb", 48},
+        {"train_batch", 262144},                // m_training_batch_size (testbed.h:1103)
+        {"train_random_bg", 1},
+        {"train_debug", 0},                     // parity hook: generate writes per-ray step counts (sng_train_debug)                 // m_nerf.training.random_bg_color (testbed.h:790)                    // device-memory budget for the deferred-shadow queues
         {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
         {"nerf_fused_after", 4},                // ... after this many whole-GPU wavefront iterations
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
@@ -426,6 +430,23 @@ struct sng_ctx {
     MarchCtrl* h_ctrl = nullptr;
     uint32_t* h_alive = nullptr;  // pinned readback [chunk][2], [4..5] host-reducer exchange
     SchedComm sched_comm;         // frame-wide step schedule across ranks (comm.cpp)
+    DevBuf d_params;              // the model's fp16 parameter blob (tcnn order), training source
+
+    // ---- online training (train.hip; Testbed::train_nerf, testbed_nerf.cu:3298-3780)
+    struct Train {
+        bool ready = false;
+        uint32_t step = 0, grid_ema_step = 0;
+        uint32_t rays_per_batch = 1u << 12;            // testbed.h:509
+        uint32_t measured = 0, measured_before = 0;
+        Pcg32 rng{}, grid_rng{};
+        int w = 0, h = 0, n_images = 0;
+        DevBuf pixels, xforms, focal, pp;
+        DevBuf master, grads, m1, m2, steps, ema, p_train, p_infer, wfrag_train, wfrag_t;
+        DevBuf grid, grid_tmp, grid_coords, grid_idx, grid_out;
+        DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts;
+        uint32_t target = 1u << 18;                    // m_training_batch_size (testbed.h:1103)
+        float last_loss = 0.0f;
+    } tr;
     bool mesh_reset = true;
 
     // scene (Engine)
@@ -513,6 +534,8 @@ void set_model(sng_ctx* c, const sng_nerf_config* cfg, const uint16_t* params, u
     for (int kb = 0; kb < 2; ++kb) pack_layer(rW2, 64, 0, kb, true, &frag[(f++) * 512]);
     upload(c->d_wfrag, frag.data(), frag.size() * 2);
     upload(c->d_grid, params + 3072 + 7168, (n - 3072 - 7168) * 2);
+    upload(c->d_params, params, n * 2);
+    c->tr.ready = false;
     upload(c->d_levels, c->levels.data(), c->levels.size() * sizeof(LevelInfo));
     c->net.F = (int)cfg->n_features_per_level;
     c->net.L = (int)cfg->n_levels;
@@ -1179,6 +1202,197 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
 // NerfTracer::trace + composite_kernel_nerf + shade_kernel_nerf into the NeRF frame buffer, with
 // ERenderMode "render_mode" (0 AO, 1 Shade, 3 Positions, 4 Depth, 6 Cost, 10 EncodingVis) and
 // "depth_scale" (1 / dataset.scale).  NeRF only: no mesh, shadows or overlay.
+// ================================================================================================
+// Online training (BASELINE config 5): Testbed::train_nerf + training_prep_nerf on train.hip
+// ================================================================================================
+TrainImages train_images(sng_ctx* c) {
+    auto& t = c->tr;
+    return {t.pixels.as<uint32_t>(), t.xforms.as<float>(), t.focal.as<float>(), t.pp.as<float>(), t.w, t.h, t.n_images};
+}
+
+// Testbed::reset_network's training state: fp32 master weights from the current model, zeroed
+// optimizer moments, m_rng = pcg32(seed), density_grid_rng = pcg32(m_rng.next_uint()) (testbed.cu:3654-3667)
+void train_reset(sng_ctx* c, uint64_t seed) {
+    if (!c->has_model) throw SngError(SNG_ERR_STATE, "set or load a model before training");
+    auto& t = c->tr;
+    const uint64_t n = c->n_params;
+    t.master.ensure(n * 4); t.grads.ensure(n * 4); t.m1.ensure(n * 4); t.m2.ensure(n * 4); t.steps.ensure(n * 4); t.ema.ensure(n * 4);
+    t.p_train.ensure(n * 2); t.p_infer.ensure(n * 2);
+    t.wfrag_train.ensure(20 * 512 * 2); t.wfrag_t.ensure(36 * 256 * 2);
+    std::vector<uint16_t> h(n);
+    HIPCHK(hipMemcpy(h.data(), c->d_params.p, n * 2, hipMemcpyDeviceToHost));
+    std::vector<float> f(n);
+    for (uint64_t i = 0; i < n; ++i) f[i] = h2f(h[i]);
+    HIPCHK(hipMemcpy(t.master.p, f.data(), n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.ema.p, f.data(), n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.p_train.p, h.data(), n * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.p_infer.p, h.data(), n * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(t.m1.p, 0, n * 4)); HIPCHK(hipMemset(t.m2.p, 0, n * 4)); HIPCHK(hipMemset(t.steps.p, 0, n * 4));
+    const uint32_t n_cells = GRID_CELLS * (c->max_cascade + 1);
+    t.grid.ensure((size_t)n_cells * 4); t.grid_tmp.ensure((size_t)n_cells * 4);
+    HIPCHK(hipMemset(t.grid.p, 0, (size_t)n_cells * 4));
+    t.rng = Pcg32::seeded(seed);
+    t.grid_rng = Pcg32::seeded(t.rng.next_uint());
+    t.step = 0; t.grid_ema_step = 0; t.rays_per_batch = 1u << 12; t.measured = 0; t.measured_before = 0;
+    t.target = (uint32_t)c->p("train_batch");
+    const uint32_t target = t.target, max_samples = target * 16;
+    t.ctrl.ensure(sizeof(TrainCtrl));
+    const size_t max_rays = 1u << 18;   // rays_per_batch is capped at 2^18 (update_after_training)
+    t.ray_indices.ensure(max_rays * 4); t.rays.ensure(max_rays * 32); t.numsteps.ensure(max_rays * 8);
+    t.coords.ensure((size_t)max_samples * 28); t.mlp_out.ensure((size_t)max_samples * 8);
+    t.coords_c.ensure((size_t)target * 28); t.dloss.ensure((size_t)target * 8); t.loss.ensure(max_rays * 4);
+    t.acts.ensure((size_t)((target + 15) / 16) * TRAIN_FEATS * 16 * 2);
+    // the bitfield the training marcher reads (density grid -> bitfield after every update)
+    c->d_grid_f32.ensure((size_t)n_cells * 4);
+    c->d_partial.ensure(1024 * sizeof(double));
+    c->d_mean.ensure(sizeof(float));
+    c->d_bitfield.ensure((size_t)GRID_CELLS / 8 * N_CASCADES);
+    c->d_occ_linear.ensure((size_t)GRID_CELLS / 8);
+    t.ready = true;
+}
+
+NetworkDev train_net(sng_ctx* c, const DevBuf& params, const DevBuf& wfrag) {
+    NetworkDev n = c->net;
+    n.wfrag = wfrag.p;
+    n.grid = static_cast<uint16_t*>(params.p) + 3072 + 7168;
+    return n;
+}
+
+// update_density_grid_nerf (testbed_nerf.cu:3121-3210) + update_density_grid_mean_and_bitfield
+void train_density_update(sng_ctx* c, hipStream_t s) {
+    auto& t = c->tr;
+    const uint32_t n_casc = c->max_cascade + 1, n_cells = GRID_CELLS * n_casc;
+    if (t.step == 0) {
+        t.grid_ema_step = 0;
+        launch_train_mark_untrained(n_cells, t.grid.as<float>(), train_images(c), 1, s);
+    }
+    const uint32_t n_uni = t.step < 256 ? n_cells : n_cells / 4, n_non = t.step < 256 ? 0 : n_cells / 4;
+    const uint32_t n_tot = n_uni + n_non;
+    t.grid_coords.ensure((size_t)n_tot * 28); t.grid_idx.ensure((size_t)n_tot * 4); t.grid_out.ensure((size_t)n_tot * 8);
+    HIPCHK(hipMemsetAsync(t.grid_tmp.p, 0, (size_t)n_cells * 4, s));
+    launch_train_grid_samples(n_uni, t.grid_rng, t.grid_ema_step, c->box, t.grid.as<float>(), t.grid_coords.as<float>(), t.grid_idx.as<uint32_t>(), n_casc, -0.01f, s);
+    t.grid_rng.advance();
+    launch_train_grid_samples(n_non, t.grid_rng, t.grid_ema_step, c->box, t.grid.as<float>(), t.grid_coords.as<float>() + (size_t)n_uni * 7,
+                              t.grid_idx.as<uint32_t>() + n_uni, n_casc, NERF_MIN_OPTICAL_THICKNESS, s);
+    t.grid_rng.advance();
+    // density of the training parameters (m_nerf_network->density, use_inference_params = false)
+    launch_train_pack(t.p_train.as<uint16_t>(), t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
+    launch_network(train_net(c, t.p_train, t.wfrag_train), t.grid_coords.as<float>(), 7, n_tot, nullptr, t.grid_out.as<uint16_t>(), 1, 0, s);
+    launch_train_grid_splat_ema(n_tot, t.grid_idx.as<uint32_t>(), t.grid_out.as<uint16_t>(), t.grid_tmp.as<float>(), n_cells, 0.95f, t.grid.as<float>(), s);
+    ++t.grid_ema_step;
+    HIPCHK(hipMemcpyAsync(c->d_grid_f32.p, t.grid.p, (size_t)n_cells * 4, hipMemcpyDeviceToDevice, s));
+    launch_bitfield(nullptr, c->max_cascade, c->d_grid_f32.as<float>(), c->d_partial.as<double>(), c->d_mean.as<float>(), c->d_bitfield.as<uint8_t>(),
+                    c->d_occ_linear.as<uint32_t>(), s);
+    c->has_bitfield = true;
+}
+
+TrainStepArgs train_args(sng_ctx* c) {
+    auto& t = c->tr;
+    TrainStepArgs a{};
+    a.vol = make_volume(c);
+    a.n_rays = t.rays_per_batch;
+    a.target_batch = t.target;
+    const uint32_t max_samples = t.target * 16;
+    a.max_samples = t.measured_before == 0 ? max_samples : (std::min(t.measured_before, max_samples) + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY;
+    a.random_bg = c->p("train_random_bg") != 0.0 ? 1 : 0;
+    a.background = mk(0.0f, 0.0f, 0.0f);
+    a.loss_scale = 128.0f;   // default_loss_scale<__half>
+    a.near_distance = 0.1f;
+    a.debug = c->p("train_debug") != 0.0 ? 1 : 0;
+    return a;
+}
+
+TrainBatch train_batch(sng_ctx* c) {
+    auto& t = c->tr;
+    return {t.ctrl.as<TrainCtrl>(), t.ray_indices.as<uint32_t>(), t.rays.as<float4>(), t.numsteps.as<uint2>(), t.coords.as<float>(), t.mlp_out.as<uint16_t>(),
+            t.coords_c.as<float>(), t.dloss.as<uint16_t>(), t.loss.as<float>(), t.acts.as<uint16_t>()};
+}
+
+// train_nerf_step (3532-3780) up to the gradients; stage > 0 stops early (parity hooks):
+// 1 = samples generated, 2 = network outputs, 3 = loss / compaction, 4 = gradients
+void train_forward_backward(sng_ctx* c, int stage, hipStream_t s) {
+    auto& t = c->tr;
+    const TrainStepArgs a = train_args(c);
+    const TrainBatch b = train_batch(c);
+    const TrainImages im = train_images(c);
+    HIPCHK(hipMemsetAsync(t.ctrl.p, 0, sizeof(TrainCtrl), s));
+    HIPCHK(hipMemsetAsync(t.loss.p, 0, (size_t)a.n_rays * 4, s));
+    launch_train_generate(a, im, b, t.rng, s);
+    if (stage == 1) return;
+    // inference forward of every sample with the training params
+    launch_train_pack(t.p_train.as<uint16_t>(), t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
+    const NetworkDev net = train_net(c, t.p_train, t.wfrag_train);
+    // count = min(numsteps_counter, max_samples): the generator drops rays beyond max_samples
+    launch_train_clamp_count(&b.ctrl->numsteps_counter, a.max_samples, t.ctrl.as<uint32_t>() + 3, s);
+    launch_network(net, b.coords, 7, 0, t.ctrl.as<uint32_t>() + 3, b.mlp_out, 1, (a.max_samples + 15) / 16, s);
+    if (stage == 2) return;
+    launch_train_loss(a, im, b, t.rng, c->d_mean.as<float>(), s);
+    if (stage == 3) return;
+    HIPCHK(hipMemsetAsync(t.grads.p, 0, c->n_params * 4, s));
+    float* g = t.grads.as<float>();
+    launch_train_field(a, b, net, t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), static_cast<uint16_t*>(net.grid), g + 3072 + 7168, s);
+    launch_train_dw(a, b.acts, g, (uint32_t)c->n_cus, s);
+}
+
+void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
+    if (!c->tr.ready) train_reset(c, 1337);
+    auto& t = c->tr;
+    if (t.n_images == 0) throw SngError(SNG_ERR_STATE, "no training images (sng_train_set_dataset)");
+    hipStream_t s = c->s_nerf;
+    HIPCHK(hipEventRecord(c->ev_start, s));
+    double loss_acc = 0.0;
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        // Testbed::train: training_prep_nerf every clamp(step / 16, 1, 16) steps (testbed.cu:4081-4091)
+        const uint32_t skip = std::min(16u, std::max(1u, t.step / 16u));
+        if (t.step % skip == 0) train_density_update(c, s);
+        train_forward_backward(c, 0, s);
+        // optimizer_step: Ema(ExponentialDecay(Adam)) (base.json)
+        AdamArgs o{};
+        const uint32_t decays = t.step >= 20000 ? (t.step - 20000) / 10000 + 1 : 0;
+        o.lr = 1e-2f * std::pow(0.33f, (float)decays);
+        o.beta1 = 0.9f; o.beta2 = 0.99f; o.epsilon = 1e-15f; o.l2_reg = 1e-6f; o.loss_scale = 128.0f; o.ema_decay = 0.95f; o.ema_step = t.step;
+        launch_train_adam(o, c->n_params, 3072 + 7168, t.master.as<float>(), t.grads.as<float>(), t.m1.as<float>(), t.m2.as<float>(), t.steps.as<uint32_t>(),
+                          t.ema.as<float>(), t.p_train.as<uint16_t>(), t.p_infer.as<uint16_t>(), s);
+        t.rng.advance();
+        ++t.step;
+        // NerfCounters::update_after_training (3272-3296): host readback of the two sample counts
+        TrainCtrl h{};
+        HIPCHK(hipMemcpyAsync(&h, t.ctrl.p, sizeof(TrainCtrl), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (h.numsteps_counter == 0 || h.numsteps_compacted == 0) {
+            t.measured = t.measured_before = 0;
+        } else {
+            t.measured_before = h.numsteps_counter;
+            t.measured = h.numsteps_compacted;
+            uint32_t r = (uint32_t)((float)t.rays_per_batch * (float)t.target / (float)t.measured);
+            t.rays_per_batch = std::min((r + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY, 1u << 18);
+        }
+        if (out && k + 1 == n_steps) {
+            std::vector<float> l(std::max<uint32_t>(1, h.ray_counter));
+            const uint32_t nr = std::min<uint32_t>(h.ray_counter, (uint32_t)(t.loss.bytes / 4));
+            if (nr) HIPCHK(hipMemcpy(l.data(), t.loss.p, nr * 4, hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < nr; ++i) loss_acc += l[i];
+            t.last_loss = (float)(loss_acc * (double)t.measured / (double)t.target);
+        }
+    }
+    HIPCHK(hipEventRecord(c->ev_end, s));
+    // inference params (EMA) -> the render path's weights and grid
+    launch_train_pack(t.p_infer.as<uint16_t>(), c->d_wfrag.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
+    HIPCHK(hipMemcpyAsync(c->d_grid.p, static_cast<uint16_t*>(t.p_infer.p) + 3072 + 7168, (c->n_params - 3072 - 7168) * 2, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->d_params.p, t.p_infer.p, c->n_params * 2, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    if (out) {
+        std::memset(out, 0, sizeof(*out));
+        out->step = t.step;
+        out->loss = t.last_loss;
+        out->rays_per_batch = t.rays_per_batch;
+        out->measured_batch = t.measured;
+        out->measured_batch_before_compaction = t.measured_before;
+        HIPCHK(hipEventElapsedTime(&out->ms, c->ev_start, c->ev_end));
+    }
+}
+
 void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out) {
     if (c->win[0] <= 0) throw SngError(SNG_ERR_STATE, "sng_set_window first");
     if ((int)c->p("res_factor") != c->last_res_factor) resize(c);
@@ -1536,6 +1750,9 @@ int sng_get_camera_matrix(sng_ctx* c, float m[12]) { return guarded([&] { std::m
 int sng_set_fov(sng_ctx* c, float deg) { return guarded([&] { c->rel_focal[0] = c->rel_focal[1] = fov_to_focal(deg); c->mesh_reset = true; }); }
 int sng_get_focal_length(sng_ctx* c, int which, float out[2]) {
     return guarded([&] {
+        // a pending res_factor change resizes first (the next frame would), so the focal length
+        // reported is the one that frame uses
+        if (c->win[0] > 0 && (int)c->p("res_factor") != c->last_res_factor) { HIPCHK(hipSetDevice(c->device)); resize(c); }
         const int* res = which == 0 ? c->nerf_res : c->mesh_res;
         f2 f = focal_for(c, res);
         out[0] = f.x; out[1] = f.y;
@@ -1552,6 +1769,7 @@ int sng_set_window(sng_ctx* c, int32_t w, int32_t h) {
 }
 int sng_get_resolution(sng_ctx* c, sng_resolution_info* out) {
     return guarded([&] {
+        if (c->win[0] > 0 && (int)c->p("res_factor") != c->last_res_factor) { HIPCHK(hipSetDevice(c->device)); resize(c); }
         std::memset(out, 0, sizeof(*out));
         out->nerf_res[0] = c->nerf_res[0]; out->nerf_res[1] = c->nerf_res[1];
         out->mesh_res[0] = c->mesh_res[0]; out->mesh_res[1] = c->mesh_res[1];
@@ -1563,6 +1781,128 @@ int sng_render_nerf_ngp(sng_ctx* c, const sng_frame_params* p, sng_frame_result*
 }
 int sng_render_frame(sng_ctx* c, const sng_frame_params* p, sng_frame_result* out) {
     return guarded([&] { HIPCHK(hipSetDevice(c->device)); render_frame(c, p, out); });
+}
+// 8-bit RGB / RGBA / grey(+alpha) non-interlaced PNG -> RGBA8 (the nerf_synthetic training images;
+// the reference loads them through stb_image, nerf_loader.cu).  Host-only utility.
+int sng_image_load_png(const char* path, uint8_t* out, uint64_t capacity, int32_t* width, int32_t* height) {
+    return guarded([&] {
+        std::ifstream f(path, std::ios::binary);
+        if (!f) throw SngError(SNG_ERR_IO, std::string("cannot open ") + path);
+        std::vector<uint8_t> d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+        if (d.size() < 8 || std::memcmp(d.data(), sig, 8) != 0) throw SngError(SNG_ERR_IO, "not a PNG");
+        auto be32 = [&](size_t o) { return (uint32_t)d[o] << 24 | (uint32_t)d[o + 1] << 16 | (uint32_t)d[o + 2] << 8 | d[o + 3]; };
+        uint32_t w = 0, h = 0;
+        int depth = 0, ctype = 0, interlace = 0;
+        std::vector<uint8_t> idat;
+        for (size_t o = 8; o + 8 <= d.size();) {
+            const uint32_t len = be32(o);
+            const std::string type(reinterpret_cast<const char*>(&d[o + 4]), 4);
+            if (o + 12 + len > d.size()) throw SngError(SNG_ERR_IO, "truncated PNG");
+            const uint8_t* p = &d[o + 8];
+            if (type == "IHDR") {
+                w = be32(o + 8); h = be32(o + 12); depth = p[8]; ctype = p[9]; interlace = p[12];
+            } else if (type == "IDAT") {
+                idat.insert(idat.end(), p, p + len);
+            } else if (type == "IEND") {
+                break;
+            }
+            o += 12 + len;
+        }
+        const int ch = ctype == 6 ? 4 : ctype == 2 ? 3 : ctype == 4 ? 2 : ctype == 0 ? 1 : 0;
+        if (depth != 8 || ch == 0 || interlace != 0 || !w || !h) throw SngError(SNG_ERR_IO, "unsupported PNG (8-bit non-interlaced grey/RGB/RGBA only)");
+        if (width) *width = (int32_t)w;
+        if (height) *height = (int32_t)h;
+        if (!out) return;
+        if (capacity < (uint64_t)w * h * 4) throw SngError(SNG_ERR_INVALID, "output buffer too small");
+        const size_t stride = (size_t)w * ch;
+        std::vector<uint8_t> raw((stride + 1) * h);
+        uLongf rl = (uLongf)raw.size();
+        if (uncompress(raw.data(), &rl, idat.data(), (uLong)idat.size()) != Z_OK || rl != raw.size()) throw SngError(SNG_ERR_IO, "bad PNG data");
+        std::vector<uint8_t> prev(stride, 0), cur(stride);
+        for (uint32_t y = 0; y < h; ++y) {
+            const uint8_t ft = raw[y * (stride + 1)];
+            const uint8_t* src = &raw[y * (stride + 1) + 1];
+            for (size_t i = 0; i < stride; ++i) {
+                const int a = i >= (size_t)ch ? cur[i - ch] : 0, b = prev[i], cc = i >= (size_t)ch ? prev[i - ch] : 0;
+                int v = src[i];
+                if (ft == 1) v += a;
+                else if (ft == 2) v += b;
+                else if (ft == 3) v += (a + b) / 2;
+                else if (ft == 4) {
+                    const int pp = a + b - cc, pa = std::abs(pp - a), pb = std::abs(pp - b), pc = std::abs(pp - cc);
+                    v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : cc);
+                }
+                cur[i] = (uint8_t)v;
+            }
+            uint8_t* o = out + (size_t)y * w * 4;
+            for (uint32_t x = 0; x < w; ++x) {
+                const uint8_t* px = &cur[(size_t)x * ch];
+                if (ch >= 3) { o[4 * x] = px[0]; o[4 * x + 1] = px[1]; o[4 * x + 2] = px[2]; o[4 * x + 3] = ch == 4 ? px[3] : 255; }
+                else { o[4 * x] = o[4 * x + 1] = o[4 * x + 2] = px[0]; o[4 * x + 3] = ch == 2 ? px[1] : 255; }
+            }
+            std::swap(prev, cur);
+        }
+    });
+}
+int sng_train_set_dataset(sng_ctx* c, uint32_t n, uint32_t w, uint32_t h, const uint8_t* rgba, const float* xf, const float* focal, const float* pp) {
+    return guarded([&] {
+        if (!c || !rgba || !xf || !focal || !pp || !n || !w || !h) throw SngError(SNG_ERR_INVALID, "bad training dataset");
+        HIPCHK(hipSetDevice(c->device));
+        auto& t = c->tr;
+        upload(t.pixels, rgba, (size_t)n * w * h * 4);
+        upload(t.xforms, xf, (size_t)n * 12 * 4);
+        upload(t.focal, focal, (size_t)n * 2 * 4);
+        upload(t.pp, pp, (size_t)n * 2 * 4);
+        t.w = (int)w; t.h = (int)h; t.n_images = (int)n;
+    });
+}
+int sng_train_reset(sng_ctx* c, uint64_t seed) {
+    return guarded([&] { HIPCHK(hipSetDevice(c->device)); train_reset(c, seed); });
+}
+int sng_train(sng_ctx* c, uint32_t n_steps, sng_train_stats* st) {
+    return guarded([&] { HIPCHK(hipSetDevice(c->device)); train_steps(c, n_steps, st); });
+}
+int sng_train_export(sng_ctx* c, uint16_t* params, uint64_t n_params, uint16_t* grid, uint64_t n_cells) {
+    return guarded([&] {
+        HIPCHK(hipSetDevice(c->device));
+        if (!c->tr.ready) throw SngError(SNG_ERR_STATE, "no training state");
+        if (params) {
+            if (n_params != c->n_params) throw SngError(SNG_ERR_INVALID, "param count mismatch");
+            HIPCHK(hipMemcpy(params, c->tr.p_infer.p, n_params * 2, hipMemcpyDeviceToHost));
+        }
+        if (grid) {
+            const uint64_t nc = (uint64_t)GRID_CELLS * (c->max_cascade + 1);
+            if (n_cells != nc) throw SngError(SNG_ERR_INVALID, "grid cell count mismatch");
+            std::vector<float> f(nc);
+            HIPCHK(hipMemcpy(f.data(), c->tr.grid.p, nc * 4, hipMemcpyDeviceToHost));
+            for (uint64_t i = 0; i < nc; ++i) grid[i] = f2h(f[i]);
+        }
+    });
+}
+int sng_train_debug(sng_ctx* c, int stage, const char* name, void* out, uint64_t cap, uint64_t* size) {
+    return guarded([&] {
+        HIPCHK(hipSetDevice(c->device));
+        if (!c->tr.ready) train_reset(c, 1337);
+        auto& t = c->tr;
+        if (t.n_images == 0) throw SngError(SNG_ERR_STATE, "no training images");
+        if (stage > 0) {
+            if (t.step == 0 && !c->has_bitfield) train_density_update(c, c->s_nerf);
+            train_forward_backward(c, stage, c->s_nerf);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(c->s_nerf));
+        if (!name) return;
+        const std::string k = name;
+        const std::map<std::string, DevBuf*> bufs = {{"ctrl", &t.ctrl}, {"ray_indices", &t.ray_indices}, {"rays", &t.rays}, {"numsteps", &t.numsteps},
+                                                     {"coords", &t.coords}, {"mlp_out", &t.mlp_out}, {"coords_c", &t.coords_c}, {"dloss", &t.dloss},
+                                                     {"loss", &t.loss}, {"grads", &t.grads}, {"acts", &t.acts}, {"grid", &t.grid}, {"master", &t.master}};
+        auto it = bufs.find(k);
+        if (it == bufs.end()) throw SngError(SNG_ERR_INVALID, "unknown training buffer " + k);
+        const uint64_t n = it->second->bytes;
+        if (size) *size = n;
+        if (out) HIPCHK(hipMemcpy(out, it->second->p, std::min(n, cap), hipMemcpyDeviceToHost));
+    });
 }
 int sng_comm_unique_id(uint8_t* out) {
     return guarded([&] {

@@ -469,7 +469,7 @@ void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid
                      hipStream_t s) {
     const uint32_t N = GRID_CELLS;
     const uint32_t n_cells = N * (max_cascade + 1);
-    hipLaunchKernelGGL(half_to_float_kernel, dim3((n_cells + 255) / 256), dim3(256), 0, s, grid_f16, grid_f32, n_cells);
+    if (grid_f16) hipLaunchKernelGGL(half_to_float_kernel, dim3((n_cells + 255) / 256), dim3(256), 0, s, grid_f16, grid_f32, n_cells);   // else grid_f32 is given
     hipLaunchKernelGGL(mean_partial_kernel, dim3(1024), dim3(256), 0, s, grid_f32, N, partial);
     hipLaunchKernelGGL(mean_final_kernel, dim3(1), dim3(64), 0, s, partial, 1024, mean);
     const uint32_t n_el = N / 8 * N_CASCADES;

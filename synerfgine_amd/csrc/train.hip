@@ -1,0 +1,618 @@
+// train.hip -- online NeRF training (BASELINE config 5): one training step
+// of Testbed::train_nerf (testbed_nerf.cu:3298-3530, train_nerf_step 3532-3780) on gfx950.
+//
+//   train_generate_kernel  generate_training_samples_nerf (838-998): random pixels, occupancy march
+//   (network)              inference forward of every sample (nerf_network_kernel, layout [n][4])
+//   train_loss_kernel      compute_loss_kernel_train_nerf (1000-1313): composite, Huber loss,
+//                          dL/d(rgb, sigma) per sample, compaction of the samples that contribute
+//   train_rollover_kernel  tcnn fill_rollover(_and_rescale): pad the compacted batch to its target size
+//   train_field_kernel     NerfNetwork forward + backward (nerf_network.h:144-268) per 16-sample
+//                          tile on MFMA: activations and pre-activation gradients go to a tiled HBM
+//                          buffer, hash-grid gradients are scattered with f32 atomics
+//   train_dw_kernel        the five weight gradients dW = delta x activation^T, K = samples, MFMA
+//   train_adam_kernel      tcnn Ema(ExponentialDecay(Adam)) (base.json:5-22), fp32 master weights
+//   density grid           update_density_grid_nerf (3121-3210): mark_untrained_density_grid,
+//                          generate_grid_samples_nerf_nonuniform, splat max, ema_grid_samples_nerf
+//
+// tiny-cuda-nn (GridEncoding / FullyFusedMLP backward, Adam, EMA, pcg32) is unvendored; its
+// published algorithms are restated.  MFMA operand layout of v_mfma_f32_16x16x16f16:
+// A lane l = (row l%16, k 4(l/16)..+3), B lane l = (k 4(l/16)..+3, col l%16), D lane l = (rows
+// 4(l/16)..+3, col l%16) -- so a layer's D fragment IS the next backward layer's B fragment.
+#include <algorithm>
+
+#include "nerf_field.h"
+#include "train.h"
+
+namespace sng {
+
+typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4v mfma16k16(h4v a, h4v b, f4v c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
+
+// ---------------------------------------------------------------------------------------------
+// generate_training_samples_nerf (testbed_nerf.cu:838-998), no error-map CDFs, no distortion,
+// no envmap, max_level_rand_training off, pinhole lens
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void train_generate_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n_rays) return;
+    const uint32_t img = ((i * im.n) / a.n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
+    rng.advance((uint64_t)i * N_MAX_RANDOM_SAMPLES_PER_RAY);
+    const f2 uv = train_image_pos(rng, im);
+    if (read_rgba(im, img, uv).x < 0.0f) return;              // masked pixel
+    (void)rng.next_float();                                    // motionblur_time
+    const TrainRay ray = train_ray(im, img, uv);
+    const f3 dn = normalize(ray.d);
+    const aabb box = a.vol.train_aabb;
+    float tmin = fmaxf(aabb_entry(box, ray.o, dn), 0.0f);      // aabb.ray_intersect(...).x, clamped at 0
+    const float cone = a.vol.cone;
+    const float startt = advance_n_steps(tmin, cone, rng.next_float());
+    const f3 idir = inv(dn);
+    uint32_t j = 0;
+    float t = startt;
+    f3 pos;
+    while (aabb_contains(box, pos = ray.o + t * dn) && j < NERF_STEPS) {
+        const float dt = calc_dt(t, cone);
+        const uint32_t mip = mip_from_dt(dt, pos, a.vol.max_mip);
+        if (occupied_at(pos, a.vol.bitfield, mip)) { ++j; t += dt; }
+        else t = advance_to_next_voxel(t, cone, pos, dn, idir, mip);
+    }
+    if (a.debug) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
+    if (j == 0) return;
+    const uint32_t numsteps = j;
+    const uint32_t base = atomicAdd(&b.ctrl->numsteps_counter, numsteps);
+    if (base + numsteps > a.max_samples) return;
+    const uint32_t ray_idx = atomicAdd(&b.ctrl->ray_counter, 1u);
+    b.ray_indices[ray_idx] = i;
+    b.rays[2 * ray_idx] = make_float4(ray.o.x, ray.o.y, ray.o.z, 0.0f);
+    b.rays[2 * ray_idx + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
+    b.numsteps[ray_idx] = make_uint2(numsteps, base);
+    const f3 wd = (dn + 1.0f) * 0.5f;   // warp_direction
+    const f3 diag = box.hi - box.lo;
+    t = startt;
+    j = 0;
+    float* co = b.coords + (size_t)base * 7;
+    while (aabb_contains(box, pos = ray.o + t * dn) && j < numsteps) {
+        const float dt = calc_dt(t, cone);
+        const uint32_t mip = mip_from_dt(dt, pos, a.vol.max_mip);
+        if (occupied_at(pos, a.vol.bitfield, mip)) {
+            const f3 wp = (pos - box.lo) / diag;   // warp_position = aabb.relative_pos
+            float* c = co + (size_t)j * 7;
+            c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+            ++j;
+            t += dt;
+        } else {
+            t = advance_to_next_voxel(t, cone, pos, dn, idir, mip);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// compute_loss_kernel_train_nerf (testbed_nerf.cu:1000-1313): Logistic rgb / Exponential density,
+// SRGB colour space (train_in_linear_colors = false), random background colour, no envmap,
+// error map, sharpness, exposure or depth supervision
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, const float* __restrict__ mean_density) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.ctrl->ray_counter) return;
+    const uint2 ns = b.numsteps[i];
+    const uint32_t numsteps = ns.x, base = ns.y;
+    const float* cin = b.coords + (size_t)base * 7;
+    const uint16_t* nout = b.mlp_out + (size_t)base * 4;
+    const aabb box = a.vol.train_aabb;
+    const f3 diag = box.hi - box.lo;
+    const float4 ro4 = b.rays[2 * i];
+    const f3 ray_o = mk(ro4.x, ro4.y, ro4.z);
+    float T = 1.0f;
+    const float EPSILON = 1e-4f;
+    f3 rgb_ray = splat(0.0f);
+    uint32_t cn = 0;
+    for (; cn < numsteps; ++cn) {
+        if (T < EPSILON) break;
+        const float* c = cin + (size_t)cn * 7;
+        const uint16_t* o = nout + (size_t)cn * 4;
+        const f3 rgb = mk(logistic(h2f(o[0])), logistic(h2f(o[1])), logistic(h2f(o[2])));
+        const float dt = unwarp_dt(c[3]);
+        const float density = sng_expf(h2f(o[3]));
+        const float alpha = 1.0f - sng_expf(-density * dt);
+        const float weight = alpha * T;
+        rgb_ray = rgb_ray + weight * rgb;
+        T *= (1.0f - alpha);
+    }
+    // same RNG draws as train_generate_kernel for this ray: uv, (max_level off), motionblur, then bg
+    const uint32_t ray_idx = b.ray_indices[i];
+    rng.advance((uint64_t)ray_idx * N_MAX_RANDOM_SAMPLES_PER_RAY);
+    const uint32_t img = ((ray_idx * im.n) / a.n_rays) % im.n;
+    const f2 uv = train_image_pos(rng, im);
+    rng.advance(1);   // motionblur_time
+    f3 bg = a.background;
+    if (a.random_bg) { const float x = rng.next_float(), y = rng.next_float(), z = rng.next_float(); bg = mk(x, y, z); }
+    bg = mk(srgb_to_linear(bg.x), srgb_to_linear(bg.y), srgb_to_linear(bg.z));
+    const float4 tex = read_rgba(im, img, uv);
+    bg = mk(linear_to_srgb(bg.x), linear_to_srgb(bg.y), linear_to_srgb(bg.z));
+    f3 target;
+    if (tex.w > 0.0f) {
+        const f3 lin = mk(tex.x / tex.w, tex.y / tex.w, tex.z / tex.w);   // exposure_scale = exp(0) = 1
+        target = mk(linear_to_srgb(lin.x), linear_to_srgb(lin.y), linear_to_srgb(lin.z)) * tex.w + (1.0f - tex.w) * bg;
+    } else {
+        target = bg;
+    }
+    if (cn == numsteps) rgb_ray = rgb_ray + T * bg;
+
+    const uint32_t cbase = atomicAdd(&b.ctrl->numsteps_compacted, cn);
+    const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
+    if (ccount == 0) return;
+    // Huber loss (alpha = 0.1) / 5, loss_and_gradient (nerf_device.cuh:100-117, 601-616)
+    f3 grad;
+    float loss_sum = 0.0f;
+    {
+        const float alpha_h = 0.1f;
+        const float dv[3] = {rgb_ray.x - target.x, rgb_ray.y - target.y, rgb_ray.z - target.z};
+        float gv[3];
+        for (int k = 0; k < 3; ++k) {
+            const float ad = fabsf(dv[k]);
+            const float sq = 0.5f / alpha_h * dv[k] * dv[k];
+            const float l = ad > alpha_h ? (ad - 0.5f * alpha_h) : sq;
+            gv[k] = (ad > alpha_h ? (dv[k] > 0 ? 1.0f : -1.0f) : (dv[k] / alpha_h)) / 5.0f;
+            loss_sum += l / 5.0f;
+        }
+        grad = mk(gv[0], gv[1], gv[2]);
+    }
+    b.loss[i] = (loss_sum / 3.0f) / (float)a.n_rays;
+    const float loss_scale = a.loss_scale / (float)a.n_rays;
+    const float l1_reg_density = *mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
+    f3 rgb_ray2 = splat(0.0f);
+    T = 1.0f;
+    float* cout = b.coords_c + (size_t)cbase * 7;
+    uint16_t* dout = b.dloss + (size_t)cbase * 4;
+    for (uint32_t j = 0; j < ccount; ++j) {
+        const float* c = cin + (size_t)j * 7;
+        for (int k = 0; k < 7; ++k) cout[(size_t)j * 7 + k] = c[k];
+        const f3 pos = box.lo + mk(c[0], c[1], c[2]) * diag;   // unwarp_position
+        const float depth = length(pos - ray_o);
+        const float dt = unwarp_dt(c[3]);
+        const uint16_t* o = nout + (size_t)j * 4;
+        const float o0 = h2f(o[0]), o1 = h2f(o[1]), o2 = h2f(o[2]), o3 = h2f(o[3]);
+        const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
+        const float density = sng_expf(o3);
+        const float alpha = 1.0f - sng_expf(-density * dt);
+        const float weight = alpha * T;
+        rgb_ray2 = rgb_ray2 + weight * rgb;
+        T *= (1.0f - alpha);
+        const f3 suffix = rgb_ray - rgb_ray2;
+        const f3 dl_drgb = weight * grad;
+        const float d0 = loss_scale * (dl_drgb.x * (rgb.x * (1.0f - rgb.x)));
+        const float d1 = loss_scale * (dl_drgb.y * (rgb.y * (1.0f - rgb.y)));
+        const float d2 = loss_scale * (dl_drgb.z * (rgb.z * (1.0f - rgb.z)));
+        const float dens_deriv = sng_expf(fminf(fmaxf(o3, -15.0f), 15.0f));
+        const float dl_dmlp = dens_deriv * (dt * dot(grad, T * rgb - suffix));
+        const float d3 = loss_scale * dl_dmlp + (o3 < 0.0f ? -l1_reg_density : 0.0f) + (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f);
+        dout[(size_t)j * 4 + 0] = f2h(d0);
+        dout[(size_t)j * 4 + 1] = f2h(d1);
+        dout[(size_t)j * 4 + 2] = f2h(d2);
+        dout[(size_t)j * 4 + 3] = f2h(d3);
+    }
+}
+
+// tcnn fill_rollover / fill_rollover_and_rescale: entries [n_in, target) repeat entry (i mod n_in);
+// rolled-over gradients are scaled by n_in / target
+__global__ void train_rollover_kernel(TrainStepArgs a, TrainBatch b) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.target_batch) return;
+    const uint32_t n_in = min(b.ctrl->numsteps_compacted, a.target_batch);
+    if (n_in == 0 || i < n_in) return;
+    const uint32_t src = i % n_in;
+    for (int k = 0; k < 7; ++k) b.coords_c[(size_t)i * 7 + k] = b.coords_c[(size_t)src * 7 + k];
+    const float s = (float)n_in / (float)a.target_batch;
+    for (int k = 0; k < 4; ++k) b.dloss[(size_t)i * 4 + k] = f2h(h2f(b.dloss[(size_t)src * 4 + k]) * s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// MLP weight fragments from an fp16 parameter blob (tcnn order, nerf_network.h:356-371):
+// forward A fragments (20 x 64 lanes x 8, the same image capi.cpp set_model packs on the host)
+// and backward A fragments of W^T (36 x 64 lanes x 4) for v_mfma_f32_16x16x16f16
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint16_t fwd_frag_elem(const uint16_t* W, int n_in, int mb, int kb, bool permuted, int lane, int j) {
+    const int row = 16 * mb + (lane & 15), g = lane >> 4;
+    const int k = permuted ? 32 * kb + 16 * (j >= 4) + 4 * g + (j & 3) : 32 * kb + 8 * g + j;
+    return W[row * n_in + k];
+}
+__global__ void train_pack_kernel(const uint16_t* __restrict__ p, uint16_t* __restrict__ wfrag, uint16_t* __restrict__ wfrag_t) {
+    const int lane = threadIdx.x & 63, f = blockIdx.x;   // grid: 20 forward + 36 backward fragments
+    const uint16_t *dW0 = p, *dW1 = p + 64 * 32, *rW0 = p + 3072, *rW1 = rW0 + 64 * 32, *rW2 = rW1 + 64 * 64;
+    if (f < 20) {
+        for (int j = 0; j < 8; ++j) {
+            uint16_t v;
+            if (f < 4) v = fwd_frag_elem(dW0, 32, f, 0, false, lane, j);
+            else if (f < 6) v = fwd_frag_elem(dW1, 64, 0, f - 4, true, lane, j);
+            else if (f < 10) v = fwd_frag_elem(rW0, 32, f - 6, 0, true, lane, j);
+            else if (f < 18) v = fwd_frag_elem(rW1, 64, (f - 10) / 2, (f - 10) % 2, true, lane, j);
+            else v = fwd_frag_elem(rW2, 64, 0, f - 18, true, lane, j);
+            wfrag[(f * 64 + lane) * 8 + j] = v;
+        }
+        return;
+    }
+    // W^T fragment (i, q): lane l, j -> W[16q + 4(l/16) + j][16i + l%16]
+    const int b = f - 20;
+    const uint16_t* W;
+    int n_in, i, q;
+    if (b < 4) { W = rW2; n_in = 64; i = b; q = 0; }                       // dh2 <- do      (T_RGB2)
+    else if (b < 20) { W = rW1; n_in = 64; i = (b - 4) / 4; q = (b - 4) % 4; }   // dh1 <- dh2 (T_RGB1)
+    else if (b < 24) { W = rW0; n_in = 32; i = 0; q = b - 20; }            // drin[0:16] <- dh1 (T_RGB0)
+    else if (b < 28) { W = dW1; n_in = 64; i = b - 24; q = 0; }            // dh0 <- ddens   (T_DEN1)
+    else { W = dW0; n_in = 32; i = (b - 28) / 4; q = (b - 28) % 4; }       // denc <- dh0    (T_DEN0)
+    for (int j = 0; j < 4; ++j) wfrag_t[(b * 64 + lane) * 4 + j] = W[(16 * q + 4 * (lane >> 4) + j) * n_in + 16 * i + (lane & 15)];
+}
+constexpr int T_RGB2 = 0, T_RGB1 = 4, T_RGB0 = 20, T_DEN1 = 24, T_DEN0 = 28;
+
+__device__ __forceinline__ h4v to_h4(f4v v) { return {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]}; }
+__device__ __forceinline__ f4v relu_mask(f4v d, f4v pre) {
+    // ReLU backward on the post-activation value (tcnn: grad *= (y > 0)); y = relu(pre) > 0 <=> pre > 0
+    // with y rounded to fp16 exactly as the forward stores it
+    f4v r;
+    for (int k = 0; k < 4; ++k) r[k] = ((_Float16)fmaxf(pre[k], 0.0f) > (_Float16)0.0f) ? d[k] : 0.0f;
+    return r;
+}
+// tiled activation/gradient store: [tile][feature][16 samples] fp16
+__device__ __forceinline__ void store_rows(uint16_t* tile_base, int feat0, int g, int col, f4v v) {
+    for (int k = 0; k < 4; ++k) tile_base[(feat0 + 4 * g + k) * 16 + col] = __builtin_bit_cast(uint16_t, (_Float16)v[k]);
+}
+__device__ __forceinline__ void store_rows_relu(uint16_t* tile_base, int feat0, int g, int col, f4v v) {
+    for (int k = 0; k < 4; ++k) tile_base[(feat0 + 4 * g + k) * 16 + col] = __builtin_bit_cast(uint16_t, (_Float16)fmaxf(v[k], 0.0f));
+}
+
+// hash-grid backward for one level and F features of one sample: d(param) += w_corner * d(feature)
+// (tcnn kernel_grid_backward: float weights, atomic adds)
+template <int F>
+__device__ __forceinline__ void grid_backward_level(const LevelInfo& L, float* __restrict__ ggrad, float x0, float x1, float x2, const float* dfeat) {
+    const float p0 = fmaf(L.scale, x0, 0.5f), p1 = fmaf(L.scale, x1, 0.5f), p2 = fmaf(L.scale, x2, 0.5f);
+    const float q0 = floorf(p0), q1 = floorf(p1), q2 = floorf(p2);
+    const uint32_t g0 = (uint32_t)(int)q0, g1 = (uint32_t)(int)q1, g2 = (uint32_t)(int)q2;
+    const float f0 = p0 - q0, f1 = p1 - q1, f2 = p2 - q2;
+    float* tbl = ggrad + (size_t)L.offset * F;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float w = 1.0f;
+        w *= (c & 1) ? f0 : 1.0f - f0;
+        w *= (c & 2) ? f1 : 1.0f - f1;
+        w *= (c & 4) ? f2 : 1.0f - f2;
+        const uint32_t idx = grid_index(L, g0 + (c & 1), g1 + ((c >> 1) & 1), g2 + ((c >> 2) & 1)) * F;
+#pragma unroll
+        for (int f = 0; f < F; ++f)
+            if (dfeat[f] != 0.0f) atomicAdd(tbl + idx + f, w * dfeat[f]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// NerfNetwork forward + backward per 16-sample tile (nerf_network.h:144-268).  Activations
+// (post-ReLU, fp16) and pre-activation gradients (fp16) go to acts[tile][TRAIN_FEATS][16] for
+// train_dw_kernel; the encoding gradient is scattered into the f32 grid gradient.
+// ---------------------------------------------------------------------------------------------
+template <int F>
+__global__ __launch_bounds__(256) void train_field_kernel(TrainStepArgs a, TrainBatch b, const h8* __restrict__ wfrag, const h4v* __restrict__ wfrag_t,
+                                                          const _Float16* __restrict__ grid, const LevelInfo* __restrict__ levels,
+                                                          float* __restrict__ ggrad) {
+    const uint32_t n = a.target_batch;
+    const uint32_t n_tiles = (n + 15) >> 4;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    const f4v zero = {0.0f, 0.0f, 0.0f, 0.0f};
+    h8 W[20];
+#pragma unroll
+    for (int f = 0; f < 20; ++f) W[f] = wfrag[f * 64 + lane];
+    for (uint32_t tile = wave; tile < n_tiles; tile += n_waves) {
+        const uint32_t s = tile * 16 + col;
+        const bool valid = s < n;
+        const float* c = b.coords_c + (size_t)(valid ? s : n - 1) * 7;
+        const float x0 = c[0], x1 = c[1], x2 = c[2], d0 = c[4], d1 = c[5], d2 = c[6];
+        uint16_t* tb = b.acts + (size_t)tile * TRAIN_FEATS * 16;
+        // ---- forward (field_tile, keeping the activations)
+        const h8 enc = encode_lane<F>(levels, grid, g, x0, x1, x2);
+        f4v a0 = mfma16(W[0], enc, zero), a1 = mfma16(W[1], enc, zero), a2 = mfma16(W[2], enc, zero), a3 = mfma16(W[3], enc, zero);
+        f4v dens = mfma16(W[4], pack_relu(a0, a1), zero);
+        dens = mfma16(W[5], pack_relu(a2, a3), dens);
+        float sh[4];
+        sh_lane(g, d0, d1, d2, sh);
+        h8 rin;
+        rin[0] = (_Float16)dens[0]; rin[1] = (_Float16)dens[1]; rin[2] = (_Float16)dens[2]; rin[3] = (_Float16)dens[3];
+        rin[4] = (_Float16)sh[0]; rin[5] = (_Float16)sh[1]; rin[6] = (_Float16)sh[2]; rin[7] = (_Float16)sh[3];
+        f4v b0 = mfma16(W[6], rin, zero), b1 = mfma16(W[7], rin, zero), b2 = mfma16(W[8], rin, zero), b3 = mfma16(W[9], rin, zero);
+        const h8 k0 = pack_relu(b0, b1), k1 = pack_relu(b2, b3);
+        f4v c0 = mfma16(W[10], k0, zero); c0 = mfma16(W[11], k1, c0);
+        f4v c1 = mfma16(W[12], k0, zero); c1 = mfma16(W[13], k1, c1);
+        f4v c2 = mfma16(W[14], k0, zero); c2 = mfma16(W[15], k1, c2);
+        f4v c3 = mfma16(W[16], k0, zero); c3 = mfma16(W[17], k1, c3);
+        // activations for the weight gradients
+        for (int k = 0; k < 8; ++k) tb[(A_ENC + 8 * g + k) * 16 + col] = __builtin_bit_cast(uint16_t, enc[k]);
+        store_rows_relu(tb, A_H0 + 0, g, col, a0); store_rows_relu(tb, A_H0 + 16, g, col, a1);
+        store_rows_relu(tb, A_H0 + 32, g, col, a2); store_rows_relu(tb, A_H0 + 48, g, col, a3);
+        for (int k = 0; k < 4; ++k) {
+            tb[(A_RIN + 4 * g + k) * 16 + col] = __builtin_bit_cast(uint16_t, rin[k]);
+            tb[(A_RIN + 16 + 4 * g + k) * 16 + col] = __builtin_bit_cast(uint16_t, rin[4 + k]);
+        }
+        store_rows_relu(tb, A_H1 + 0, g, col, b0); store_rows_relu(tb, A_H1 + 16, g, col, b1);
+        store_rows_relu(tb, A_H1 + 32, g, col, b2); store_rows_relu(tb, A_H1 + 48, g, col, b3);
+        store_rows_relu(tb, A_H2 + 0, g, col, c0); store_rows_relu(tb, A_H2 + 16, g, col, c1);
+        store_rows_relu(tb, A_H2 + 32, g, col, c2); store_rows_relu(tb, A_H2 + 48, g, col, c3);
+
+        // ---- backward.  dL/d(rgb output rows 0..2) and dL/dsigma from the loss (extract_rgb, add_density_gradient)
+        f4v d_o = zero;
+        float d_sigma = 0.0f;
+        if (valid && g == 0) {
+            const uint16_t* dl = b.dloss + (size_t)s * 4;
+            d_o[0] = h2f(dl[0]); d_o[1] = h2f(dl[1]); d_o[2] = h2f(dl[2]);
+            d_sigma = h2f(dl[3]);
+        }
+        store_rows(tb, D_O, g, col, d_o);
+        const h4v bo = to_h4(d_o);
+        // rgb W2: dh2 = W2^T d_o, masked by relu(c)
+        f4v e0 = relu_mask(mfma16k16(wfrag_t[(T_RGB2 + 0) * 64 + lane], bo, zero), c0);
+        f4v e1 = relu_mask(mfma16k16(wfrag_t[(T_RGB2 + 1) * 64 + lane], bo, zero), c1);
+        f4v e2 = relu_mask(mfma16k16(wfrag_t[(T_RGB2 + 2) * 64 + lane], bo, zero), c2);
+        f4v e3 = relu_mask(mfma16k16(wfrag_t[(T_RGB2 + 3) * 64 + lane], bo, zero), c3);
+        store_rows(tb, D_H2 + 0, g, col, e0); store_rows(tb, D_H2 + 16, g, col, e1);
+        store_rows(tb, D_H2 + 32, g, col, e2); store_rows(tb, D_H2 + 48, g, col, e3);
+        const h4v he[4] = {to_h4(e0), to_h4(e1), to_h4(e2), to_h4(e3)};
+        // rgb W1: dh1 = W1^T dh2, masked by relu(b)
+        f4v f[4];
+        const f4v bpre[4] = {b0, b1, b2, b3};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f4v acc = zero;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc = mfma16k16(wfrag_t[(T_RGB1 + 4 * i + q) * 64 + lane], he[q], acc);
+            f[i] = relu_mask(acc, bpre[i]);
+            store_rows(tb, D_H1 + 16 * i, g, col, f[i]);
+        }
+        const h4v hf[4] = {to_h4(f[0]), to_h4(f[1]), to_h4(f[2]), to_h4(f[3])};
+        // rgb W0: d(rgb input rows 0..15) = density-network output gradient; + dL/dsigma on row 0
+        f4v ddens = zero;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ddens = mfma16k16(wfrag_t[(T_RGB0 + q) * 64 + lane], hf[q], ddens);
+        {
+            // tcnn keeps dL/d(rgb network input) in fp16 before add_density_gradient
+            for (int k = 0; k < 4; ++k) ddens[k] = (float)(_Float16)ddens[k];
+            if (g == 0) ddens[0] = (float)(_Float16)(ddens[0] + d_sigma);
+        }
+        store_rows(tb, D_DENS, g, col, ddens);
+        const h4v hd = to_h4(ddens);
+        // density W1: dh0 = W1^T ddens, masked by relu(a)
+        f4v h[4];
+        const f4v apre[4] = {a0, a1, a2, a3};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            h[i] = relu_mask(mfma16k16(wfrag_t[(T_DEN1 + i) * 64 + lane], hd, zero), apre[i]);
+            store_rows(tb, D_H0 + 16 * i, g, col, h[i]);
+        }
+        const h4v hh[4] = {to_h4(h[0]), to_h4(h[1]), to_h4(h[2]), to_h4(h[3])};
+        // density W0: denc = W0^T dh0 (32 features = 2 blocks)
+        f4v de0 = zero, de1 = zero;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            de0 = mfma16k16(wfrag_t[(T_DEN0 + q) * 64 + lane], hh[q], de0);
+            de1 = mfma16k16(wfrag_t[(T_DEN0 + 4 + q) * 64 + lane], hh[q], de1);
+        }
+        if (!valid) continue;
+        // encoding gradient (fp16, as tcnn's dL_ddensity_network_input) -> grid; the lane holds
+        // features 4g..4g+3 and 16+4g..16+4g+3
+        float df0[4], df1[4];
+        for (int k = 0; k < 4; ++k) { df0[k] = (float)(_Float16)de0[k]; df1[k] = (float)(_Float16)de1[k]; }
+        if constexpr (F == 4) {
+            grid_backward_level<4>(levels[g], ggrad, x0, x1, x2, df0);
+            grid_backward_level<4>(levels[4 + g], ggrad, x0, x1, x2, df1);
+        } else {
+            grid_backward_level<2>(levels[2 * g], ggrad, x0, x1, x2, df0);
+            grid_backward_level<2>(levels[2 * g + 1], ggrad, x0, x1, x2, df0 + 2);
+            grid_backward_level<2>(levels[8 + 2 * g], ggrad, x0, x1, x2, df1);
+            grid_backward_level<2>(levels[8 + 2 * g + 1], ggrad, x0, x1, x2, df1 + 2);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradients: dW[out][in] = sum_s delta[out][s] * act[in][s] over the batch (K = samples),
+// v_mfma_f32_16x16x16f16 with both operands read straight from the tiled buffer (4 consecutive
+// samples of one feature = 8 B per lane).  Five waves per workgroup split the 40 16x16 blocks;
+// each workgroup covers a slab of tiles and adds its partial sums to the f32 gradient.
+// ---------------------------------------------------------------------------------------------
+struct DwJob { int dfeat, afeat, mb, nb, n_in, param_off; };
+__device__ __forceinline__ DwJob dw_job(int blk) {
+    // blocks: rgb W1 (16) | rgb W0 (8) | dens W0 (8) | rgb W2 (4) | dens W1 (4)
+    if (blk < 16) return {D_H2, A_H1, blk / 4, blk % 4, 64, 3072 + 64 * 32};
+    if (blk < 24) { const int b = blk - 16; return {D_H1, A_RIN, b / 2, b % 2, 32, 3072}; }
+    if (blk < 32) { const int b = blk - 24; return {D_H0, A_ENC, b / 2, b % 2, 32, 0}; }
+    if (blk < 36) { const int b = blk - 32; return {D_O, A_H2, 0, b, 64, 3072 + 64 * 32 + 64 * 64}; }
+    const int b = blk - 36;
+    return {D_DENS, A_H0, 0, b, 64, 64 * 32};
+}
+__global__ __launch_bounds__(320) void train_dw_kernel(TrainStepArgs a, const uint16_t* __restrict__ acts, uint32_t tiles_per_block, float* __restrict__ wgrad) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;   // 5 waves x 8 blocks
+    const uint32_t n_tiles = (a.target_batch + 15) >> 4;
+    const uint32_t t0 = blockIdx.x * tiles_per_block, t1 = min(n_tiles, t0 + tiles_per_block);
+    const int r = lane & 15, kq = lane >> 4;
+    f4v acc[8];
+    DwJob job[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { acc[j] = f4v{0.0f, 0.0f, 0.0f, 0.0f}; job[j] = dw_job(wv * 8 + j); }
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint16_t* tb = acts + (size_t)t * TRAIN_FEATS * 16;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const h4v A = *reinterpret_cast<const h4v*>(tb + (job[j].dfeat + 16 * job[j].mb + r) * 16 + 4 * kq);
+            const h4v B = *reinterpret_cast<const h4v*>(tb + (job[j].afeat + 16 * job[j].nb + r) * 16 + 4 * kq);
+            acc[j] = mfma16k16(A, B, acc[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const DwJob& jb = job[j];
+        for (int k = 0; k < 4; ++k) {
+            const int row = 16 * jb.mb + 4 * kq + k, cin = 16 * jb.nb + r;
+            atomicAdd(&wgrad[jb.param_off + row * jb.n_in + cin], acc[j][k]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// tcnn Ema(ExponentialDecay(Adam)) step (base.json:5-22).  Matrix params (the 10240 MLP weights)
+// get l2_reg; grid params with a zero gradient are skipped (sparse update, per-parameter step
+// counts for the bias correction).  Writes the fp32 master, the fp16 training copy and the EMA
+// (debiased) fp16 inference copy.
+// ---------------------------------------------------------------------------------------------
+__global__ void train_adam_kernel(AdamArgs o, uint64_t n, uint32_t n_matrix, float* __restrict__ master, const float* __restrict__ grads,
+                                  float* __restrict__ m1, float* __restrict__ m2, uint32_t* __restrict__ steps, float* __restrict__ ema,
+                                  uint16_t* __restrict__ p_train, uint16_t* __restrict__ p_infer) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float gradient = grads[i] / o.loss_scale;
+    const bool matrix = i < n_matrix;
+    float w = master[i];
+    if (!(matrix || gradient != 0.0f)) {
+        // untouched grid entry: weights unchanged, EMA still advances (tcnn EmaOptimizer steps every param)
+    } else {
+        const uint32_t step = ++steps[i];
+        if (matrix) gradient += o.l2_reg * w;
+        const float gsq = gradient * gradient;
+        const float fm = m1[i] = o.beta1 * m1[i] + (1.0f - o.beta1) * gradient;
+        const float sm = m2[i] = o.beta2 * m2[i] + (1.0f - o.beta2) * gsq;
+        const float lr = o.lr * sqrtf(1.0f - powf(o.beta2, (float)step)) / (1.0f - powf(o.beta1, (float)step));
+        const float eff = lr / (sqrtf(sm) + o.epsilon);
+        w = w - eff * fm;
+        master[i] = w;
+    }
+    p_train[i] = f2h(w);
+    // EMA with debiasing (tcnn EmaOptimizer)
+    const float deb_old = 1.0f - powf(o.ema_decay, (float)o.ema_step), deb_new = 1.0f - powf(o.ema_decay, (float)(o.ema_step + 1));
+    const float e = (ema[i] * o.ema_decay * deb_old + w * (1.0f - o.ema_decay)) / deb_new;
+    ema[i] = e;
+    p_infer[i] = f2h(e);
+}
+
+// ---------------------------------------------------------------------------------------------
+// density grid (update_density_grid_nerf, testbed_nerf.cu:3121-3210)
+// ---------------------------------------------------------------------------------------------
+// mark_untrained_density_grid (75-141): cells no training camera sees are -1
+__global__ void train_mark_untrained_kernel(uint32_t n_elements, float* __restrict__ grid, TrainImages im, int clear_visible) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_elements) return;
+    const uint32_t level = i / GRID_CELLS, pos_idx = i % GRID_CELLS;
+    const uint32_t x = morton3D_invert(pos_idx >> 0), y = morton3D_invert(pos_idx >> 1), z = morton3D_invert(pos_idx >> 2);
+    const float voxel_size = scalbnf(1.0f / (float)GRID_SIZE, (int)level);
+    const f3 pos = (mk((float)x, (float)y, (float)z) / (float)GRID_SIZE - 0.5f) * scalbnf(1.0f, (int)level) + 0.5f;
+    uint32_t count = 0;
+    for (uint32_t j = 0; j < (uint32_t)im.n && count < 1; ++j) {
+        const float* xf = im.xforms + 12 * j;
+        const f3 c0 = mk(xf[0], xf[1], xf[2]), c1 = mk(xf[3], xf[4], xf[5]), c2 = mk(xf[6], xf[7], xf[8]), c3 = mk(xf[9], xf[10], xf[11]);
+        const f2 focal = {im.focal[2 * j], im.focal[2 * j + 1]}, pp = {im.pp[2 * j], im.pp[2 * j + 1]};
+        for (uint32_t k = 0; k < 8; ++k) {
+            const f3 corner = pos + mk((k & 1) ? voxel_size : 0.0f, (k & 2) ? voxel_size : 0.0f, (k & 4) ? voxel_size : 0.0f);
+            const f3 dir = normalize(corner - c3);
+            if (dot(dir, c2) < 1e-4f) continue;
+            // pos_to_uv (pinhole): camera-space direction, project, then uv_to_ray round trip
+            const f3 v = corner - c3;
+            const f3 lc = mk(dot(v, c0), dot(v, c1), dot(v, c2));
+            const f2 uv = {lc.x / lc.z * focal.x / (float)im.w + pp.x, lc.y / lc.z * focal.y / (float)im.h + pp.y};
+            const f3 dl = mk((uv.x - pp.x) * (float)im.w / focal.x, (uv.y - pp.y) * (float)im.h / focal.y, 1.0f);
+            const f3 rd = normalize(c0 * dl.x + c1 * dl.y + c2 * dl.z);
+            if (length(rd - dir) < 1e-3f && uv.x > 0.0f && uv.y > 0.0f && uv.x < 1.0f && uv.y < 1.0f) { ++count; break; }
+        }
+    }
+    if (clear_visible || (grid[i] < 0) != (count < 1)) grid[i] = count >= 1 ? 0.0f : -1.0f;
+}
+
+// generate_grid_samples_nerf_nonuniform (186-215): NerfPosition written as a 7-float coordinate
+// (direction unused by the density output)
+__global__ void train_grid_samples_kernel(uint32_t n_elements, Pcg32 rng, uint32_t step, aabb box, const float* __restrict__ grid_in, float* __restrict__ coords,
+                                          uint32_t* __restrict__ indices, uint32_t n_cascades, float thresh) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_elements) return;
+    rng.advance((uint64_t)i * 4);
+    const uint32_t level = (uint32_t)(rng.next_float() * (float)n_cascades) % n_cascades;
+    uint32_t idx = 0;
+    for (uint32_t j = 0; j < 10; ++j) {
+        idx = ((i + step * n_elements) * 56924617u + j * 19349663u + 96925573u) % GRID_CELLS;
+        idx += level * GRID_CELLS;
+        if (grid_in[idx] > thresh) break;
+    }
+    const uint32_t pos_idx = idx % GRID_CELLS;
+    const uint32_t x = morton3D_invert(pos_idx >> 0), y = morton3D_invert(pos_idx >> 1), z = morton3D_invert(pos_idx >> 2);
+    const float rx = rng.next_float(), ry = rng.next_float(), rz = rng.next_float();
+    const f3 pos = ((mk((float)x, (float)y, (float)z) + mk(rx, ry, rz)) / (float)GRID_SIZE - 0.5f) * scalbnf(1.0f, (int)level) + 0.5f;
+    const f3 wp = (pos - box.lo) / (box.hi - box.lo);
+    float* c = coords + (size_t)i * 7;
+    c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(MIN_STEP); c[4] = 0.5f; c[5] = 0.5f; c[6] = 0.5f;
+    indices[i] = idx;
+}
+
+// splat_grid_samples_nerf_max_nearest_neighbor (217-233): optical thickness, atomic max on the bits
+__global__ void train_grid_splat_kernel(uint32_t n, const uint32_t* __restrict__ indices, const uint16_t* __restrict__ out4, float* __restrict__ tmp) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float mlp = sng_expf(h2f(out4[(size_t)i * 4 + 3]));
+    const float ot = mlp * MIN_STEP;
+    atomicMax(reinterpret_cast<uint32_t*>(&tmp[indices[i]]), __float_as_uint(ot));
+}
+
+// ema_grid_samples_nerf (254-275): max(prev * decay, new), negative (untrained) cells stay
+__global__ void train_grid_ema_kernel(uint32_t n, float decay, float* __restrict__ grid, const float* __restrict__ tmp) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float prev = grid[i];
+    grid[i] = prev < 0.0f ? prev : fmaxf(prev * decay, tmp[i]);
+}
+
+__global__ void train_clamp_count_kernel(const uint32_t* __restrict__ in, uint32_t cap, uint32_t* __restrict__ out) {
+    if (threadIdx.x == 0) *out = min(*in, cap);
+}
+
+// ---------------------------------------------------------------------------------------------
+void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(train_clamp_count_kernel, dim3(1), dim3(64), 0, s, in, cap, out);
+}
+void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, hipStream_t s) {
+    hipLaunchKernelGGL(train_generate_kernel, dim3((a.n_rays + 255) / 256), dim3(256), 0, s, a, im, b, rng);
+}
+void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
+    hipLaunchKernelGGL(train_loss_kernel, dim3((a.n_rays + 255) / 256), dim3(256), 0, s, a, im, b, rng, mean_density);
+    hipLaunchKernelGGL(train_rollover_kernel, dim3((a.target_batch + 255) / 256), dim3(256), 0, s, a, b);
+}
+void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s) {
+    hipLaunchKernelGGL(train_pack_kernel, dim3(56), dim3(64), 0, s, params, wfrag, wfrag_t);
+}
+void launch_train_field(const TrainStepArgs& a, const TrainBatch& b, const NetworkDev& net, const uint16_t* wfrag, const uint16_t* wfrag_t,
+                        const uint16_t* grid, float* ggrad, hipStream_t s) {
+    const uint32_t tiles = (a.target_batch + 15) / 16;
+    const uint32_t waves = std::min<uint32_t>(tiles, (uint32_t)net.n_cus * 8u);
+    const uint32_t blocks = (waves + 3) / 4;
+    const h8* w = reinterpret_cast<const h8*>(wfrag);
+    const h4v* wt = reinterpret_cast<const h4v*>(wfrag_t);
+    const _Float16* gr = reinterpret_cast<const _Float16*>(grid);
+    if (net.F == 4) hipLaunchKernelGGL((train_field_kernel<4>), dim3(blocks), dim3(256), 0, s, a, b, w, wt, gr, net.levels, ggrad);
+    else hipLaunchKernelGGL((train_field_kernel<2>), dim3(blocks), dim3(256), 0, s, a, b, w, wt, gr, net.levels, ggrad);
+}
+void launch_train_dw(const TrainStepArgs& a, const uint16_t* acts, float* wgrad, uint32_t n_cus, hipStream_t s) {
+    const uint32_t tiles = (a.target_batch + 15) / 16;
+    const uint32_t blocks_target = n_cus * 2;
+    const uint32_t per = std::max<uint32_t>(16, (tiles + blocks_target - 1) / blocks_target);
+    hipLaunchKernelGGL(train_dw_kernel, dim3((tiles + per - 1) / per), dim3(320), 0, s, a, acts, per, wgrad);
+}
+void launch_train_adam(const AdamArgs& o, uint64_t n, uint32_t n_matrix, float* master, const float* grads, float* m1, float* m2, uint32_t* steps, float* ema,
+                       uint16_t* p_train, uint16_t* p_infer, hipStream_t s) {
+    hipLaunchKernelGGL(train_adam_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, o, n, n_matrix, master, grads, m1, m2, steps, ema, p_train, p_infer);
+}
+void launch_train_mark_untrained(uint32_t n, float* grid, const TrainImages& im, int clear_visible, hipStream_t s) {
+    hipLaunchKernelGGL(train_mark_untrained_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, grid, im, clear_visible);
+}
+void launch_train_grid_samples(uint32_t n, Pcg32 rng, uint32_t step, const aabb& box, const float* grid, float* coords, uint32_t* indices, uint32_t n_cascades,
+                               float thresh, hipStream_t s) {
+    if (!n) return;
+    hipLaunchKernelGGL(train_grid_samples_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, rng, step, box, grid, coords, indices, n_cascades, thresh);
+}
+void launch_train_grid_splat_ema(uint32_t n_samples, const uint32_t* indices, const uint16_t* out4, float* tmp, uint32_t n_cells, float decay, float* grid,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(train_grid_splat_kernel, dim3((n_samples + 255) / 256), dim3(256), 0, s, n_samples, indices, out4, tmp);
+    hipLaunchKernelGGL(train_grid_ema_kernel, dim3((n_cells + 255) / 256), dim3(256), 0, s, n_cells, decay, grid, tmp);
+}
+
+}  // namespace sng

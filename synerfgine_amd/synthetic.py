@@ -224,3 +224,15 @@ def kitchen_like(seed=1337, ramp=0.2, a=2.6, b=2.3):
     cfg = dict(n_levels=L, n_features_per_level=F, log2_hashmap_size=LOG2T, base_resolution=NMIN,
                per_level_scale=KITCHEN_PER_LEVEL_SCALE, aabb_scale=KITCHEN_AABB_SCALE)
     return cfg, params, dg.astype(np.float16)
+
+
+def random_init(seed=1337, cfg=None):
+    """Freshly initialised base.json network (tcnn: hash-grid entries U(-1e-4, 1e-4), Xavier-uniform
+    MLP weights) -- the starting point of online training."""
+    rng = np.random.default_rng(seed)
+    mlp = np.concatenate([_xavier(rng, 64, 32).ravel(), _xavier(rng, 16, 64).ravel(), _xavier(rng, 64, 32).ravel(), _xavier(rng, 64, 64).ravel(),
+                          _xavier(rng, 16, 64).ravel()])
+    offsets, _ = level_table()
+    grid = rng.uniform(-1e-4, 1e-4, size=offsets[-1] * F)
+    cfg = cfg or dict(n_levels=L, n_features_per_level=F, log2_hashmap_size=LOG2T, base_resolution=NMIN, per_level_scale=PER_LEVEL_SCALE, aabb_scale=1)
+    return cfg, np.concatenate([mlp, grid]).astype(np.float16)
