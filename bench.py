@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""bench.py -- rendered frames/s at 1920x1080 (synthetic lego-like snapshot + armadillo scene, shadows both ways).
+"""bench.py -- rendered frames/s at 1920x1080 (lego .ingp snapshot + armadillo scene, shadows both ways).
 
 One step = one complete Engine::frame (raytrace + NeRF march/encode/MLP/composite +
 shadows on the NeRF + overlay) of BASELINE.json config C3.  With N ranks the frame
@@ -25,8 +25,8 @@ MFMA_F16_PEAK_TFLOPS = 2500.0                # dense fp16/bf16 MFMA
 
 
 WORKLOADS = {
-    "c2": "lego-like NeRF only (show_virtual_obj=0, shadows off)",
-    "c3": "lego-like NeRF + armadillo.json (light_samples 8, path_trace_depth 2, shadow_on_nerf + shadow_on_virtual_obj)",
+    "c2": "lego NeRF only (show_virtual_obj=0, shadows off)",
+    "c3": "lego NeRF + armadillo.json (light_samples 8, path_trace_depth 2, shadow_on_nerf + shadow_on_virtual_obj)",
     "c4": "kitchen-like NeRF (aabb_scale 16, 5 cascades, cone stepping) + kitchen-rocks.json (bunny/rock/box, light_samples 4, "
           "nerf_shadow_samples 4)",
 }
@@ -47,11 +47,15 @@ def parse():
                     help="N>1: step each band from its own alive count (no per-iteration count all-reduce; not bit-identical to N=1)")
     ap.add_argument("--balance-iters", type=int, default=8, help="untimed calibration frames for the band split")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="engine parameter override (sng_set_param)")
+    ap.add_argument("--model", default=None,
+                    help="lego (trained .ingp, data/lego.ingp; default for c2/c3 when present), synthetic, or an .ingp path")
     return ap.parse_args()
 
 
-def cpu_baseline(eng_cfg, config, scale):
-    """Time the CPU oracle (test infrastructure) on a bounded sample of the same workload."""
+def cpu_baseline(eng_cfg, config, scale, model_name, overrides):
+    """Time the CPU oracle (test infrastructure) on a bounded sample of the same workload, and compare the
+    GPU's frame of that same sample with it (the metric's "PSNR vs ref": the oracle is the reference
+    restatement).  Returns (cpu_baseline, psnr_vs_oracle)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle as O
@@ -60,21 +64,27 @@ def cpu_baseline(eng_cfg, config, scale):
     ncfg, params, grid = eng_cfg
     full = S.CONFIGS[config]
     w, h = int(round(full["width"] / scale)), int(round(full["height"] / scale))
-    tb, eng, _ = S.make_engine(config, width=w, height=h)
+    tb, eng, _ = S.make_engine(config, width=w, height=h, model=model_name, overrides=overrides)
     model = O.Model(ncfg, params)
     vol = O.volume_for(ncfg, grid)
-    r = eng.resolution()
-    nrng = O.xorwow_states(r["nerf"][0] * r["nerf"][1])
-    mrng = O.xorwow_states(r["mesh"][0] * r["mesh"][1])
+    nrng = eng.rng_states(0).copy()
+    mrng = eng.rng_states(1).copy()
+    gpu = eng.frame(spp=0, reset=True).download("final_rgba")
     t0 = time.perf_counter()
-    O.render_frame(model, vol, tb, eng, nrng, mrng)
+    ref = O.render_frame(model, vol, tb, eng, nrng, mrng)
     dt = time.perf_counter() - t0
     tb.close()
     frac = (w * h) / float(full["width"] * full["height"])
     fps_full = frac / dt   # pixel-count scaling to the full-resolution frame
-    return {"value": round(fps_full, 5), "unit": "frames/s", "cores": O.lib().orc_num_threads(), "kind": "port",
+    err = np.abs(np.clip(gpu[..., :3], 0, 1) - np.clip(ref["final"][..., :3], 0, 1))
+    mse = float(np.mean(err ** 2))
+    psnr = {"db": round(10 * np.log10(1.0 / max(mse, 1e-12)), 2), "max_abs": round(float(err.max()), 5),
+            "frac_within_2_255": round(float(np.mean(err.max(axis=-1) <= 2.0 / 255.0)), 5), "res": [w, h],
+            "against": "CPU oracle (line-by-line restatement of the reference path, oracle/), same inputs and RNG states; final sRGB RGB in [0,1]"}
+    base = {"value": round(fps_full, 5), "unit": "frames/s", "cores": O.lib().orc_num_threads(), "kind": "port",
             "sample": f"oracle (C++ OpenMP) Engine::frame of {config} at {w}x{h} ({frac:.3g} of the pixels) took "
                       f"{dt:.2f}s; extrapolated by pixel count to {full['width']}x{full['height']}"}
+    return base, psnr
 
 
 def main():
@@ -98,7 +108,9 @@ def main():
     for kv in args.set:
         k, v = kv.split("=", 1)
         overrides[k] = float(v)
-    tb, eng, eng_cfg = S.make_engine(args.config, device_id=dev_id, overrides=overrides)
+    if args.model is None:
+        args.model = "lego" if (args.config != "c4" and os.path.exists(S.LEGO_INGP)) else "synthetic"
+    tb, eng, eng_cfg = S.make_engine(args.config, device_id=dev_id, overrides=overrides, model=args.model)
     res = eng.resolution()
     MW, MH = res["mesh"]
     dev = torch.device("cuda", dev_id)
@@ -196,8 +208,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp16 (hash grid + MLP, MFMA f16->f32), fp32 (marching, compositing, shading)",
-            "data": "synthetic: random-init base.json NeRF (L=8,F=4,T=2^19) with an analytic density (synthetic.py); scene JSON + OBJ meshes "
-                    "from scenes/ and data/obj/",
+            "data": (f"snapshot {os.path.relpath(S.snapshot_path(args.config, args.model), REPO)}" +
+                     (" (base.json NeRF L=8,F=4,T=2^19 trained on-GPU by tools/train_lego.py from the reference's lego set, data/nerf/lego400)"
+                      if args.model == "lego" else "") if args.model != "synthetic" else
+                     "synthetic: random-init base.json NeRF (L=8,F=4,T=2^19) with an analytic density (synthetic.py)") +
+                    "; scene JSON + OBJ meshes from scenes/ and data/obj/; synthetic frames (fixed camera, accumulation reset every frame)",
             "config": {"workload": f"{args.config}: " + WORKLOADS[args.config],
                        "width": MW, "height": MH, "nerf_res": list(res["nerf"]), "tiles": f"{world} horizontal bands (rows {bounds}) + " + ("RCCL all_gather" if args.dist_backend == "nccl" else "gloo all_gather"),
                        "step_schedule": "band-local" if (world > 1 and args.local_schedule) else ("frame-wide (per-iteration alive-count all-reduce)" if world > 1 else "frame-wide"),
@@ -222,7 +237,7 @@ def main():
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:
             try:
-                result["cpu_baseline"] = cpu_baseline(eng_cfg, args.config, args.cpu_baseline_scale)
+                result["cpu_baseline"], result["psnr_vs_oracle"] = cpu_baseline(eng_cfg, args.config, args.cpu_baseline_scale, args.model, overrides)
             except Exception as e:   # the CPU leg must never hide the GPU number
                 result["cpu_baseline"] = {"value": None, "error": str(e)}
         print(json.dumps(result), flush=True)

@@ -50,6 +50,11 @@ class orc_material(ctypes.Structure):
                 ("rg", ctypes.c_float), ("spec_angle", ctypes.c_float), ("type", ctypes.c_int32)]
 
 
+class orc_train_images(ctypes.Structure):
+    _fields_ = [("rgba", ctypes.c_void_p), ("xforms", ctypes.c_void_p), ("focal", ctypes.c_void_p), ("pp", ctypes.c_void_p),
+                ("w", ctypes.c_int32), ("h", ctypes.c_int32), ("n", ctypes.c_int32)]
+
+
 class orc_nerf_stats(ctypes.Structure):
     _fields_ = [("n_iterations", ctypes.c_uint32), ("n_samples", ctypes.c_uint64), ("n_slots", ctypes.c_uint64),
                 ("n_hit", ctypes.c_uint32), ("alive_per_iter", ctypes.c_uint32 * 64), ("steps_per_iter", ctypes.c_uint32 * 64)]
@@ -97,6 +102,8 @@ def lib():
             "orc_overlay": (None, [vp, vp, vp, vp, vp, vp, vp]),
             "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
             "orc_num_threads": (i32, []),
+            "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
+            "orc_train_adam_ema": (None, [u64, u32, f32, f32, f32, f32, f32, f32, f32, u32, vp, vp, vp, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(_lib, name)
@@ -283,3 +290,28 @@ def render_frame(model, vol, tb, eng, nerf_rng, mesh_rng, spp=0, target=0):
                            len(objs), ctypes.addressof(ll), len(lights), ctypes.addressof(mm), len(mats), ptr(nerf_rng), ptr(mesh_rng), ptr(final), ptr(final_d), ptr(nrgba), ptr(ndepth),
                            ctypes.byref(st))
     return dict(final=final, final_depth=final_d, nerf_rgba=nrgba, nerf_depth=ndepth, stats=st)
+
+
+# ---- online training (config 5) ----------------------------------------------------
+def train_generate(vol, images, xforms, focal, pp, rng_state, rng_inc, n_rays, max_per_ray=1024):
+    """generate_training_samples_nerf for rays [0, n_rays): (numsteps [n], rays [n][6], coords [n][max_per_ray][7]).
+    images [n, h, w, 4] uint8; xforms [n, 3, 4] NGP camera (columns c0..c3)."""
+    im = np.ascontiguousarray(images, np.uint8)
+    xf = np.ascontiguousarray(np.asarray(xforms, np.float32).reshape(-1, 3, 4).transpose(0, 2, 1).reshape(-1, 12))
+    fo = np.ascontiguousarray(focal, np.float32)
+    p = np.ascontiguousarray(pp, np.float32)
+    desc = orc_train_images(im.ctypes.data, xf.ctypes.data, fo.ctypes.data, p.ctypes.data, im.shape[2], im.shape[1], im.shape[0])
+    ns = np.zeros(n_rays, np.uint32)
+    rays = np.zeros((n_rays, 6), np.float32)
+    co = np.zeros((n_rays, max_per_ray, 7), np.float32)
+    lib().orc_train_generate(ctypes.byref(vol), ctypes.byref(desc), rng_state, rng_inc, n_rays, max_per_ray, ptr(ns), ptr(rays), ptr(co))
+    return ns, rays, co
+
+
+def train_adam_ema(master, grads, m1, m2, steps, ema, n_matrix, lr=1e-2, beta1=0.9, beta2=0.99, eps=1e-15, l2_reg=1e-6, loss_scale=128.0,
+                   ema_decay=0.95, ema_step=0):
+    """One Ema(Adam) step in place on float32 / uint32 arrays."""
+    for a, dt in ((master, np.float32), (grads, np.float32), (m1, np.float32), (m2, np.float32), (steps, np.uint32), (ema, np.float32)):
+        assert a.dtype == dt and a.flags.c_contiguous
+    lib().orc_train_adam_ema(len(master), n_matrix, lr, beta1, beta2, eps, l2_reg, loss_scale, ema_decay, ema_step, ptr(master), ptr(grads),
+                             ptr(m1), ptr(m2), ptr(steps), ptr(ema))

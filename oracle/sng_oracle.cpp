@@ -1494,3 +1494,129 @@ void orc_render_nerf_ngp(const orc_model* m, const orc_volume* v, const orc_came
     std::vector<float> pos((size_t)W * H * 3), nrm((size_t)W * H * 3);
     render_nerf_impl(m, v, c, 1, render_mode, depth_scale, frame_rgba, frame_depth, pos.data(), nrm.data(), stats);
 }
+
+/* ---- online training ------------------------------------------------------- */
+namespace {
+/* tcnn pcg32 (random.h, after M. O'Neill's PCG32 / W. Jakob's pcg32.h) [tcnn, unvendored] */
+struct OrcPcg32 {
+    uint64_t state, inc;
+    uint32_t next_uint() {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+    }
+    float next_float() {
+        union { uint32_t u; float f; } x;
+        x.u = (next_uint() >> 9) | 0x3f800000u;
+        return x.f - 1.0f;
+    }
+    void advance(uint64_t delta) {
+        uint64_t cur_mult = 0x5851f42d4c957f2dULL, cur_plus = inc, acc_mult = 1u, acc_plus = 0u;
+        while (delta > 0) {
+            if (delta & 1) { acc_mult *= cur_mult; acc_plus = acc_plus * cur_mult + cur_plus; }
+            cur_plus = (cur_mult + 1) * cur_plus;
+            cur_mult *= cur_mult;
+            delta /= 2;
+        }
+        state = acc_mult * state + acc_plus;
+    }
+};
+/* mip_from_dt (nerf_device.cuh:450-460) */
+inline uint32_t mip_from_dt(float dt, V3 pos, uint32_t max_cascade) {
+    uint32_t mip = mip_from_pos(pos, max_cascade);
+    dt *= 2 * NERF_GRIDSIZE;
+    if (dt < 1.0f) return mip;
+    int exponent;
+    std::frexp(dt, &exponent);
+    return (uint32_t)std::min(std::max((int)mip, exponent), (int)max_cascade);
+}
+}  // namespace
+
+extern "C" {
+void orc_train_generate(const orc_volume* vdesc, const orc_train_images* im, uint64_t rng_state, uint64_t rng_inc, uint32_t n_rays,
+                        uint32_t max_per_ray, uint32_t* numsteps, float* rays, float* coords) {
+    const Volume vol = make_volume(vdesc);
+    const BBox aabb = vol.train_aabb;
+    for (uint32_t i = 0; i < n_rays; ++i) {
+        numsteps[i] = 0;
+        /* image_idx without a CDF (nerf_device.cuh:598) */
+        const uint32_t img = ((i * (uint32_t)im->n) / n_rays) % (uint32_t)im->n;
+        OrcPcg32 rng{rng_state, rng_inc};
+        rng.advance((uint64_t)i * 16);   /* N_MAX_RANDOM_SAMPLES_PER_RAY (nerf_device.cuh:40) */
+        /* nerf_random_image_pos_training with snap_to_pixel_centers (nerf_device.cuh:553-576; testbed.h:794) */
+        float ux = rng.next_float();
+        float uy = rng.next_float();
+        int px = std::min(std::max((int)(ux * (float)im->w), 0), im->w - 1), py = std::min(std::max((int)(uy * (float)im->h), 0), im->h - 1);
+        V2 uv = {((float)px + 0.5f) / (float)im->w, ((float)py + 0.5f) / (float)im->h};
+        /* read_rgba < 0: masked texel (common_device.cuh:803-835) */
+        int tx = std::min(std::max((int)(uv.x * (float)im->w), 0), im->w - 1), ty = std::min(std::max((int)(uv.y * (float)im->h), 0), im->h - 1);
+        const uint8_t* tex = im->rgba + (((size_t)img * im->h + ty) * im->w + tx) * 4;
+        if (tex[0] == 0xFF && tex[1] == 0x00 && tex[2] == 0xFF && tex[3] == 0x00) continue;
+        (void)rng.next_float();   /* motionblur_time */
+        /* get_xform_given_rolling_shutter (common_device.cuh:361-368), then uv_to_ray pinhole (403-470) */
+        const float* xf = im->xforms + 12 * (size_t)img;
+        const M43 cam = m43_load(xf);
+        const M3 rot = rolling_shutter_rotation(m3_of(cam));
+        const float* fo = im->focal + 2 * (size_t)img;
+        const float* pp = im->pp + 2 * (size_t)img;
+        V3 dir = v3((uv.x - pp[0]) * (float)im->w / fo[0], (uv.y - pp[1]) * (float)im->h / fo[1], 1.0f);
+        dir = mul(rot, dir);
+        const V3 o = cam.c[3];
+        const V3 dn = normalize(dir);
+        V2 tminmax = bb_ray_intersect(aabb, o, dn);
+        const float cone = vol.cone;   /* calc_cone_angle returns the constant (nerf_device.cuh:370-377) */
+        tminmax.x = std::fmax(tminmax.x, 0.0f);
+        const float startt = advance_n_steps(tminmax.x, cone, rng.next_float());
+        const V3 idir = v3(1.0f / dn.x, 1.0f / dn.y, 1.0f / dn.z);
+        uint32_t j = 0;
+        float t = startt;
+        V3 pos;
+        float* co = coords + (size_t)i * max_per_ray * 7;
+        const V3 wd = warp_direction(dn);
+        while (bb_contains(aabb, pos = o + t * dn) && j < NERF_STEPS) {
+            const float dt = calc_dt(t, cone);
+            const uint32_t mip = mip_from_dt(dt, pos, vol.max_mip);
+            if (density_grid_occupied_at(pos, vol.bitfield, mip)) {
+                if (j < max_per_ray) {
+                    const V3 wp = warp_position(pos, aabb);
+                    float* c = co + (size_t)j * 7;
+                    c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+                }
+                ++j;
+                t += dt;
+            } else {
+                t = advance_to_next_voxel(t, cone, pos, dn, idir, mip);
+            }
+        }
+        numsteps[i] = j;
+        float* r = rays + 6 * (size_t)i;
+        r[0] = o.x; r[1] = o.y; r[2] = o.z; r[3] = dir.x; r[4] = dir.y; r[5] = dir.z;
+    }
+}
+
+void orc_train_adam_ema(uint64_t n, uint32_t n_matrix, float lr, float beta1, float beta2, float eps, float l2_reg, float loss_scale,
+                        float ema_decay, uint32_t ema_step, float* master, const float* grads, float* m1, float* m2, uint32_t* steps,
+                        float* ema) {
+    const float deb_old = 1.0f - std::pow(ema_decay, (float)ema_step), deb_new = 1.0f - std::pow(ema_decay, (float)(ema_step + 1));
+    for (uint64_t i = 0; i < n; ++i) {
+        /* tcnn adam_step (optimizers/adam.h) [unvendored] */
+        float gradient = grads[i] / loss_scale;
+        if (i < n_matrix || gradient != 0.0f) {
+            const float w = master[i];
+            if (i < n_matrix) gradient += l2_reg * w;
+            const float gsq = gradient * gradient;
+            const float fm = m1[i] = beta1 * m1[i] + (1.0f - beta1) * gradient;
+            const float sm = m2[i] = beta2 * m2[i] + (1.0f - beta2) * gsq;
+            const uint32_t step = ++steps[i];
+            float l = lr;
+            l *= std::sqrt(1.0f - std::pow(beta2, (float)step)) / (1.0f - std::pow(beta1, (float)step));
+            const float eff = l / (std::sqrt(sm) + eps);
+            master[i] = w - eff * fm;
+        }
+        /* tcnn EmaOptimizer (optimizers/average.h): debiased exponential moving average of the weights */
+        ema[i] = (ema[i] * ema_decay * deb_old + master[i] * (1.0f - ema_decay)) / deb_new;
+    }
+}
+}  // extern "C"

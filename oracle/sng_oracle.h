@@ -162,6 +162,25 @@ void orc_render_frame(const orc_model* m, const orc_volume* v, const orc_camera*
                       float* final_rgba, float* final_depth,
                       float* nerf_rgba, float* nerf_depth, orc_nerf_stats* stats);
 
+/* ---- online training (BASELINE config 5, Testbed::train_nerf) --------------- */
+typedef struct {
+    const uint8_t* rgba;    /* n x h x w x 4 sRGB 8-bit (0x00FF00FF little-endian word = masked) */
+    const float* xforms;    /* n x 12: camera columns c0 c1 c2 c3 (mat4x3, NGP space) */
+    const float* focal;     /* n x 2 pixels */
+    const float* pp;        /* n x 2 principal point (uv) */
+    int32_t w, h, n;
+} orc_train_images;
+/* generate_training_samples_nerf (testbed_nerf.cu:838-998) for rays [0, n_rays) of a batch drawn from the
+ * tcnn pcg32 {rng_state, rng_inc}: per ray, numsteps (0 = masked pixel or no occupied sample), the
+ * unnormalised ray (o, d) and the first min(numsteps, max_per_ray) NerfCoordinates (7 floats). */
+void orc_train_generate(const orc_volume* v, const orc_train_images* im, uint64_t rng_state, uint64_t rng_inc, uint32_t n_rays,
+                        uint32_t max_per_ray, uint32_t* numsteps, float* rays /* n_rays x 6 */, float* coords /* n_rays x max_per_ray x 7 */);
+/* one tcnn Adam step (adam_step: l2_reg on the first n_matrix params, zero-gradient non-matrix params
+ * skipped, per-param step counts) followed by the EmaOptimizer's debiased EMA (ema_step) */
+void orc_train_adam_ema(uint64_t n, uint32_t n_matrix, float lr, float beta1, float beta2, float eps, float l2_reg, float loss_scale,
+                        float ema_decay, uint32_t ema_step, float* master, const float* grads, float* m1, float* m2, uint32_t* steps,
+                        float* ema);
+
 int32_t orc_num_threads(void);
 
 #ifdef __cplusplus

@@ -440,7 +440,7 @@ struct sng_ctx {
         uint32_t measured = 0, measured_before = 0;
         Pcg32 rng{}, grid_rng{};
         int w = 0, h = 0, n_images = 0;
-        DevBuf pixels, xforms, focal, pp;
+        DevBuf pixels, xforms, xforms_ray, focal, pp;
         DevBuf master, grads, m1, m2, steps, ema, p_train, p_infer, wfrag_train, wfrag_t;
         DevBuf grid, grid_tmp, grid_coords, grid_idx, grid_out;
         DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts;
@@ -1207,7 +1207,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
 // ================================================================================================
 TrainImages train_images(sng_ctx* c) {
     auto& t = c->tr;
-    return {t.pixels.as<uint32_t>(), t.xforms.as<float>(), t.focal.as<float>(), t.pp.as<float>(), t.w, t.h, t.n_images};
+    return {t.pixels.as<uint32_t>(), t.xforms.as<float>(), t.xforms_ray.as<float>(), t.focal.as<float>(), t.pp.as<float>(), t.w, t.h, t.n_images};
 }
 
 // Testbed::reset_network's training state: fp32 master weights from the current model, zeroed
@@ -1852,6 +1852,15 @@ int sng_train_set_dataset(sng_ctx* c, uint32_t n, uint32_t w, uint32_t h, const 
         auto& t = c->tr;
         upload(t.pixels, rgba, (size_t)n * w * h * 4);
         upload(t.xforms, xf, (size_t)n * 12 * 4);
+        // generate_training_samples_nerf builds rays from get_xform_given_rolling_shutter (common_device.cuh:
+        // 361-368): rotation through the glm quat round trip (start == end, no rolling shutter)
+        std::vector<float> xr(xf, xf + (size_t)n * 12);
+        for (uint32_t i = 0; i < n; ++i) {
+            float* q = xr.data() + 12 * (size_t)i;
+            const m3 r = rolling_shutter_rotation({mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), mk(q[6], q[7], q[8])});
+            q[0] = r.c0.x; q[1] = r.c0.y; q[2] = r.c0.z; q[3] = r.c1.x; q[4] = r.c1.y; q[5] = r.c1.z; q[6] = r.c2.x; q[7] = r.c2.y; q[8] = r.c2.z;
+        }
+        upload(t.xforms_ray, xr.data(), (size_t)n * 12 * 4);
         upload(t.focal, focal, (size_t)n * 2 * 4);
         upload(t.pp, pp, (size_t)n * 2 * 4);
         t.w = (int)w; t.h = (int)h; t.n_images = (int)n;
@@ -1896,7 +1905,8 @@ int sng_train_debug(sng_ctx* c, int stage, const char* name, void* out, uint64_t
         const std::string k = name;
         const std::map<std::string, DevBuf*> bufs = {{"ctrl", &t.ctrl}, {"ray_indices", &t.ray_indices}, {"rays", &t.rays}, {"numsteps", &t.numsteps},
                                                      {"coords", &t.coords}, {"mlp_out", &t.mlp_out}, {"coords_c", &t.coords_c}, {"dloss", &t.dloss},
-                                                     {"loss", &t.loss}, {"grads", &t.grads}, {"acts", &t.acts}, {"grid", &t.grid}, {"master", &t.master}};
+                                                     {"loss", &t.loss}, {"grads", &t.grads}, {"acts", &t.acts}, {"grid", &t.grid}, {"master", &t.master},
+                                                     {"m1", &t.m1}, {"m2", &t.m2}, {"steps", &t.steps}, {"ema", &t.ema}, {"p_infer", &t.p_infer}};
         auto it = bufs.find(k);
         if (it == bufs.end()) throw SngError(SNG_ERR_INVALID, "unknown training buffer " + k);
         const uint64_t n = it->second->bytes;

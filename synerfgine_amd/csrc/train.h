@@ -56,6 +56,7 @@ SNG_HD uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f);
 struct TrainImages {
     const uint32_t* pixels;   // [n][h][w] RGBA8 (0x00FF00FF = masked)
     const float* xforms;      // [n][12]: camera columns c0 c1 c2 c3 (mat4x3)
+    const float* xforms_ray;  // the same after get_xform_given_rolling_shutter's quat round trip (ray generation)
     const float* focal;       // [n][2] pixels
     const float* pp;          // [n][2] principal point (uv)
     int w, h, n;
@@ -85,7 +86,7 @@ SNG_HD f2 train_image_pos(Pcg32& rng, const TrainImages& im) {
 struct TrainRay { f3 o, d; };
 // uv_to_ray (common_device.cuh:403-470), pinhole, no parallax / aperture / near distance
 SNG_HD TrainRay train_ray(const TrainImages& im, uint32_t img, f2 uv) {
-    const float* xf = im.xforms + 12 * img;
+    const float* xf = im.xforms_ray + 12 * img;
     const m3 rot = {mk(xf[0], xf[1], xf[2]), mk(xf[3], xf[4], xf[5]), mk(xf[6], xf[7], xf[8])};
     const f3 dir = mk((uv.x - im.pp[2 * img]) * (float)im.w / im.focal[2 * img], (uv.y - im.pp[2 * img + 1]) * (float)im.h / im.focal[2 * img + 1], 1.0f);
     return {mk(xf[9], xf[10], xf[11]), mul(rot, dir)};

@@ -244,6 +244,7 @@ __global__ void train_pack_kernel(const uint16_t* __restrict__ p, uint16_t* __re
 }
 constexpr int T_RGB2 = 0, T_RGB1 = 4, T_RGB0 = 20, T_DEN1 = 24, T_DEN0 = 28;
 
+struct U16x8 { uint16_t v[8]; };
 __device__ __forceinline__ h4v to_h4(f4v v) { return {(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]}; }
 __device__ __forceinline__ f4v relu_mask(f4v d, f4v pre) {
     // ReLU backward on the post-activation value (tcnn: grad *= (y > 0)); y = relu(pre) > 0 <=> pre > 0
@@ -324,12 +325,15 @@ __global__ __launch_bounds__(256) void train_field_kernel(TrainStepArgs a, Train
         f4v c2 = mfma16(W[14], k0, zero); c2 = mfma16(W[15], k1, c2);
         f4v c3 = mfma16(W[16], k0, zero); c3 = mfma16(W[17], k1, c3);
         // activations for the weight gradients
-        for (int k = 0; k < 8; ++k) tb[(A_ENC + 8 * g + k) * 16 + col] = __builtin_bit_cast(uint16_t, enc[k]);
+        // whole-vector bit casts: element-wise __builtin_bit_cast(uint16_t, v[k]) of an ext_vector
+        // element stored v[0] for every k with this compiler (caught by tests/test_gpu_train.py)
+        const U16x8 eu = __builtin_bit_cast(U16x8, enc), ru = __builtin_bit_cast(U16x8, rin);
+        for (int k = 0; k < 8; ++k) tb[(A_ENC + 8 * g + k) * 16 + col] = eu.v[k];
         store_rows_relu(tb, A_H0 + 0, g, col, a0); store_rows_relu(tb, A_H0 + 16, g, col, a1);
         store_rows_relu(tb, A_H0 + 32, g, col, a2); store_rows_relu(tb, A_H0 + 48, g, col, a3);
         for (int k = 0; k < 4; ++k) {
-            tb[(A_RIN + 4 * g + k) * 16 + col] = __builtin_bit_cast(uint16_t, rin[k]);
-            tb[(A_RIN + 16 + 4 * g + k) * 16 + col] = __builtin_bit_cast(uint16_t, rin[4 + k]);
+            tb[(A_RIN + 4 * g + k) * 16 + col] = ru.v[k];
+            tb[(A_RIN + 16 + 4 * g + k) * 16 + col] = ru.v[4 + k];
         }
         store_rows_relu(tb, A_H1 + 0, g, col, b0); store_rows_relu(tb, A_H1 + 16, g, col, b1);
         store_rows_relu(tb, A_H1 + 32, g, col, b2); store_rows_relu(tb, A_H1 + 48, g, col, b3);
@@ -476,7 +480,8 @@ __global__ void train_adam_kernel(AdamArgs o, uint64_t n, uint32_t n_matrix, flo
         const float gsq = gradient * gradient;
         const float fm = m1[i] = o.beta1 * m1[i] + (1.0f - o.beta1) * gradient;
         const float sm = m2[i] = o.beta2 * m2[i] + (1.0f - o.beta2) * gsq;
-        const float lr = o.lr * sqrtf(1.0f - powf(o.beta2, (float)step)) / (1.0f - powf(o.beta1, (float)step));
+        // tcnn adam_step: learning_rate *= sqrtf(1 - beta2^t) / (1 - beta1^t) (the quotient first)
+        const float lr = o.lr * (sqrtf(1.0f - powf(o.beta2, (float)step)) / (1.0f - powf(o.beta1, (float)step)));
         const float eff = lr / (sqrtf(sm) + o.epsilon);
         w = w - eff * fm;
         master[i] = w;

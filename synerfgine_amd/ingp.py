@@ -40,3 +40,29 @@ def write_ingp(path, cfg, params_f16, grid_f16, camera=None, aabb_scale=None):
     }
     with open(path, "wb") as f:
         f.write(zlib.compress(msgpack.packb(root, use_bin_type=True), 6))
+
+
+def read_ingp(path):
+    """Host-side read of an .ingp (zlib(msgpack) or plain msgpack) -> (cfg, params fp16, density grid fp16).
+    Data only (msgpack decodes no code); the product's loader is sng_load_snapshot -- this reader feeds the
+    oracle and the tests the same model content."""
+    import msgpack
+    with open(path, "rb") as f:
+        raw = f.read()
+    try:
+        raw = zlib.decompress(raw)
+    except zlib.error:
+        pass
+    root = msgpack.unpackb(raw, raw=False, strict_map_key=False)
+    snap, enc = root["snapshot"], root["encoding"]
+    if snap.get("params_type", "__half") != "__half":
+        params = np.frombuffer(snap["params_binary"], np.float32).astype(np.float16)
+    else:
+        params = np.frombuffer(snap["params_binary"], np.float16).copy()
+    grid = np.frombuffer(snap["density_grid_binary"], np.float16).copy()
+    nerf = snap.get("nerf", {})
+    a = nerf.get("aabb_scale", nerf.get("dataset", {}).get("aabb_scale", 1))
+    cfg = dict(n_levels=int(enc["n_levels"]), n_features_per_level=int(enc["n_features_per_level"]),
+               log2_hashmap_size=int(enc["log2_hashmap_size"]), base_resolution=int(enc["base_resolution"]),
+               per_level_scale=float(enc["per_level_scale"]), aabb_scale=int(a))
+    return cfg, params, grid

@@ -4,7 +4,7 @@ import os
 import numpy as np
 
 from . import Engine, Testbed
-from . import synthetic
+from . import ingp, synthetic
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCENES = os.path.join(REPO, "scenes")
@@ -17,24 +17,49 @@ CONFIGS = {
     "c4": dict(scene="kitchen-rocks.json", width=1920, height=1080, overrides={"light_samples": 4}),
 }
 
+# the trained lego snapshot (tools/train_lego.py on data/nerf/lego400, the reference's lego set); configs
+# c2/c3 render it when model="lego" (bench.py's default), the tests default to the synthetic model
+LEGO_INGP = os.path.join(REPO, "data", "lego.ingp")
+
 _MODEL_CACHE = {}
 
 
-def model_for(config, seed=1337):
-    """Synthetic snapshot content of a config (cached per process): lego-like or kitchen-like."""
-    key = ("kitchen" if config == "c4" else "lego", seed)
+def snapshot_path(config, model):
+    """.ingp path a (config, model) pair renders, or None for the synthetic content."""
+    if model in (None, "synthetic"):
+        return None
+    if model == "lego":
+        if config == "c4":
+            raise ValueError("c4 renders the kitchen-like synthetic snapshot (no kitchen capture in the reference)")
+        return LEGO_INGP
+    return model
+
+
+def model_for(config, seed=1337, model="synthetic"):
+    """Snapshot content of a config (cached per process): the synthetic lego-like / kitchen-like model, or
+    (cfg, params, grid) read from an .ingp (model="lego" or a path)."""
+    path = snapshot_path(config, model)
+    key = (path,) if path else ("kitchen" if config == "c4" else "lego", seed)
     if key not in _MODEL_CACHE:
-        _MODEL_CACHE[key] = synthetic.kitchen_like(seed=seed) if config == "c4" else synthetic.lego_like(seed=seed)
+        if path:
+            _MODEL_CACHE[key] = ingp.read_ingp(path)
+        else:
+            _MODEL_CACHE[key] = synthetic.kitchen_like(seed=seed) if config == "c4" else synthetic.lego_like(seed=seed)
     return _MODEL_CACHE[key]
 
 
-def make_engine(config="c3", device_id=0, width=None, height=None, overrides=None, seed=1337):
-    """Testbed with the synthetic lego-like snapshot + Engine with the config's scene JSON."""
+def make_engine(config="c3", device_id=0, width=None, height=None, overrides=None, seed=1337, model="synthetic"):
+    """Testbed with the config's snapshot + Engine with the config's scene JSON.  model="synthetic" sets the
+    synthetic model from memory; model="lego" (or an .ingp path) goes through Testbed::load_snapshot."""
     cfg = CONFIGS[config]
     tb = Testbed(device_id)
-    ncfg, params, grid = model_for(config, seed)
-    tb.set_nerf_model(ncfg, params)
-    tb.set_density_grid(grid)
+    path = snapshot_path(config, model)
+    ncfg, params, grid = model_for(config, seed, model)
+    if path:
+        tb.load_snapshot(path)
+    else:
+        tb.set_nerf_model(ncfg, params)
+        tb.set_density_grid(grid)
     eng = Engine(tb)
     eng.set_virtual_world(os.path.join(SCENES, cfg["scene"]))
     for k, v in {**cfg["overrides"], **(overrides or {})}.items():
