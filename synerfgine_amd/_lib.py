@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libsng_hip.so")
+LIB_PATH = os.environ.get("SNG_LIB_PATH") or os.path.join(_HERE, "_build", "libsng_hip.so")   # override: A/B builds (tools/)
 
 SNG_OK = 0
 

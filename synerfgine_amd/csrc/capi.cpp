@@ -355,6 +355,8 @@ const std::map<std::string, double>& default_params() {
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"rt_staged", 0},                       // ... plus primary / shade / bounce stages over compacted queues
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
+        {"bvh_flat", 1},                        // BvhWide walk keeping the nearer child in a register (exact)
+        {"rt_tile", 8},                         // path-kernel tile edge: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
@@ -364,7 +366,8 @@ const std::map<std::string, double>& default_params() {
         {"train_random_bg", 1},
         {"train_debug", 0},                     // parity hook: generate writes per-ray step counts (sng_train_debug)                 // m_nerf.training.random_bg_color (testbed.h:790)                    // device-memory budget for the deferred-shadow queues
         {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
-        {"nerf_fused_after", 4},                // ... after this many whole-GPU wavefront iterations
+        {"nerf_fused_after", 1},                // ... after this many whole-GPU wavefront iterations (1: the one big
+                                                //   uncontended network launch, then the ray-local tail; measured best)
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
     };
     return d;
@@ -1044,6 +1047,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             ra.scene_f4 = c->scene_f4;
             // max stack use of the reference traversal is depth + 1; FixedStack<32> drops pushes at 31
             ra.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
+            ra.bvh_flat = c->p("bvh_flat") != 0.0 ? 1 : 0;
             ra.scene_in_lds = (c->p("scene_lds") != 0.0 && (uint64_t)c->scene_f4 * 16 + (uint64_t)ra.stack_depth * 512 * 4 <= 80u * 1024u) ? 1 : 0;
             // persistent raytracer grids leave `rt_reserved_cus` CUs' worth of room for the NeRF
             // wavefront running beside them on the other stream (concurrent mode only)
@@ -1051,9 +1055,10 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             ra.persistent_blocks = (uint32_t)std::max(1, c->n_cus - std::max(0, reserve));
             c->rt_work.ensure(16);
             ra.work = c->rt_work.as<uint32_t>();
+            ra.tile = (c->p("rt_tile") == 4.0 && c->p("rt_staged") == 0.0) ? 4 : 8;   // the staged kernels walk 8x8 tiles
             if (c->p("rt_tile_order") != 0.0) {
-                const uint32_t n_tiles = (uint32_t)((MW + 7) / 8) * (uint32_t)((y1 - y0 + 7) / 8);
-                const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1;
+                const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile - 1) / ra.tile);
+                const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60);
                 c->rt_tile_cost.ensure((size_t)n_tiles * 4);
                 c->rt_tile_order.ensure((size_t)n_tiles * 4);
                 if (key == c->rt_tile_key) {

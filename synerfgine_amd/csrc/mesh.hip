@@ -36,6 +36,7 @@ struct TraceCtx {
     int* stack;            // this thread's first stack slot
     int stride;
     const char* scene;     // LDS scene blob (LDS = true)
+    int flat;              // near child in a register (bvh_walk_near)
     __device__ __forceinline__ const BvhNode* nodes(const ObjectGpu& o) const {
         if constexpr (LDS) return reinterpret_cast<const BvhNode*>(scene + o.lds_nodes);
         else return o.nodes;
@@ -158,6 +159,56 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
     tri_out = shortest;
     return mint;
 }
+// The same traversal with the nearer child kept in a register instead of being pushed and popped
+// straight away (push far, continue near): one LDS store + load less per inner visit that descends.
+// The visiting sequence, `d < mint` culling at push time and triangle order are the reference's, so
+// the result is identical.  (The reference's FixedStack<32> overflow rule cannot fire: the stack
+// never holds more than max BVH depth + 2 <= 32 entries, capi.cpp upload_scene.)
+template <bool FAST>
+__device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const Tri* __restrict__ tris, int root_ref,
+                                               int* stack_lds, int stride, int& tri_out, float t_max) {
+    Stack st{stack_lds, stride, 0};
+    float mint = t_max;
+    int shortest = -1;
+    int cur = root_ref;          // next stack entry to process
+    bool have = true;            // cur is valid
+    while (true) {
+        if (!have) {
+            if (st.n == 0) break;
+            cur = st.pop();
+        }
+        have = false;
+        if (cur < 0) {
+            const uint32_t e = ~(uint32_t)cur;
+            const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
+            for (int i = b; i < end; ++i) {
+                float t;
+                if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
+            }
+            continue;
+        }
+        const BvhWide w = wide[cur];
+        const aabb b0 = {mk(w.lo0[0], w.lo0[1], w.lo0[2]), mk(w.hi0[0], w.hi0[1], w.hi0[2])};
+        const aabb b1 = {mk(w.lo1[0], w.lo1[1], w.lo1[2]), mk(w.hi1[0], w.hi1[1], w.hi1[2])};
+        float d0 = FAST ? aabb_entry_fast(b0, ro, rd, y) : aabb_entry(b0, ro, rd);
+        float d1 = FAST ? aabb_entry_fast(b1, ro, rd, y) : aabb_entry(b1, ro, rd);
+        int i0 = w.ref0, i1 = w.ref1;
+        if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = w.ref1; i1 = w.ref0; }
+        // reference: push(far) if d0 < mint, push(near) if d1 < mint, then pop
+        const bool far_in = d0 < mint, near_in = d1 < mint;
+        if (near_in) {
+            if (far_in) st.push(i0);
+            cur = i1;
+            have = true;
+        } else if (far_in) {
+            cur = i0;
+            have = true;
+        }
+    }
+    tri_out = shortest;
+    return mint;
+}
+
 // t_max < MAX_DEPTH culls everything at or beyond t_max (the result is then min(closest, t_max));
 // only the shadow kernel uses it, where any value >= full_dist yields the same mask.
 template <bool LDS>
@@ -165,6 +216,10 @@ __device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu&
     const f3 oro = mul(o.world_to_obj, ro - o.pos);
     const f3 ord = mul(o.world_to_obj, rd);
     const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
+    if (o.wide && cx.flat) {
+        if (fast) return bvh_walk_near<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
+        return bvh_walk_near<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
+    }
     if (o.wide) {
         if (fast) return bvh_walk_wide<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
         return bvh_walk_wide<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
@@ -269,7 +324,7 @@ __device__ __forceinline__ f3 light_sample(const LightGpu& l, Xorwow& r) {
 __global__ __launch_bounds__(TPB) void shade_shadow_kernel(ShadowArgs a, float4* __restrict__ rgba, const float* __restrict__ positions,
                                                             const float* __restrict__ normals, uint32_t* __restrict__ rng, uint32_t n_rng) {
     __shared__ int stack_lds[BVH_STACK * TPB];
-    const TraceCtx<false> cx{stack_lds + threadIdx.x, TPB, nullptr};
+    const TraceCtx<false> cx{stack_lds + threadIdx.x, TPB, nullptr, 1};
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (t >= n) return;
@@ -371,7 +426,7 @@ __device__ __forceinline__ TraceCtx<LDS> trace_ctx_setup(const RaytraceArgs& a) 
         __syncthreads();
     }
     int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
-    return TraceCtx<LDS>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4)};
+    return TraceCtx<LDS>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat};
 }
 
 template <bool DEFER, bool LDS>
@@ -386,6 +441,9 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
     f3 shade = splat(0.0f), next_pos = splat(0.0f);
     int prev_rec = -1;
     if (DEFER) q.head[i] = -1;
+#ifdef RT_PROFILE
+    uint64_t pc_trav0 = 0, pc_trav1 = 0, pc_shade = 0, pc_alloc = 0, pc_scatter = 0, pc_start = clock64(), pc_t = 0;
+#endif
     for (uint32_t spp = 0; spp < a.samples; ++spp) {
         const float longi = curand_uniform(r) * a.lens;
         const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
@@ -394,7 +452,14 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
         f3 shade_s = splat(0.0f);
         for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
             Hit h;
+#ifdef RT_PROFILE
+            pc_t = clock64();
+#endif
             const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h);
+#ifdef RT_PROFILE
+            if (bounce) pc_trav1 += clock64() - pc_t; else pc_trav0 += clock64() - pc_t;
+            pc_t = clock64();
+#endif
             if (!bounce) next_pos = next_pos + h.pos;
             if (hit_obj < 0) break;
             // shade_object (raytracer.cu:6-57)
@@ -403,7 +468,13 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
             uint32_t k = 0;
             float* lc_out = nullptr;
             if (DEFER) {
+#ifdef RT_PROFILE
+                const uint64_t pa = clock64();
+#endif
                 k = wave_alloc(q.count, lane);
+#ifdef RT_PROFILE
+                pc_alloc += clock64() - pa;
+#endif
                 float4* rk = q.rec + (size_t)k * q.rec_stride;
                 rk[0] = make_float4(__int_as_float(-1), __uint_as_float(spp), __int_as_float(h.mat), 0.0f);
                 rk[1] = make_float4(pdf, att, 0.0f, 0.0f);
@@ -451,6 +522,10 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                 color = color / (float)a.shadow_iters;
                 color = color + m.ka;
             }
+#ifdef RT_PROFILE
+            pc_shade += clock64() - pc_t;
+            pc_t = clock64();
+#endif
             // Material::scatter (material.cuh:112-123)
             const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
             const float lo = curand_uniform(r) * spec;
@@ -461,6 +536,9 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
             rd = ndir;
             pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
             att = 1.0f * m.rg;
+#ifdef RT_PROFILE
+            pc_scatter += clock64() - pc_t;
+#endif
         }
         if (!DEFER) shade = shade + shade_s;
     }
@@ -475,19 +553,31 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
         acc_rgba[i] = make_float4(shade.x, shade.y, shade.z, cur.w);
     }
     store_rng(rng, n_rng, i, r);
+#ifdef RT_PROFILE
+    const uint64_t tot = clock64() - pc_start;
+    if (lane == (int)(__ffsll((long long)__ballot(1)) - 1) && tot > 1500000ull)
+        printf("RTPROF pixel %u total %lu trav0 %lu trav1 %lu shade %lu (alloc %lu) scatter %lu\n", (uint32_t)i, (unsigned long)tot,
+               (unsigned long)pc_trav0, (unsigned long)pc_trav1, (unsigned long)pc_shade, (unsigned long)pc_alloc, (unsigned long)pc_scatter);
+#endif
 }
 
-// Persistent workgroups; each wave takes 8x8 pixel tiles from a device counter (dynamic balance:
+// Persistent workgroups; each wave takes T x T pixel tiles (T = 8, or 4 for thin bands: a tile is a
+// serial chain of 8 samples x 2 bounces whose divergent traversals cost the union of its lanes' paths,
+// so fewer pixels per wave shorten the chain when there are too few tiles to fill the GPU anyway)
+// from a device counter (dynamic balance:
 // only ~15 % of the pixels hit an object and those cost ~100x the others).  Square tiles keep a
 // wave's primary rays coherent (fewer hit/miss-divergent waves than 64-pixel row segments).
 template <bool DEFER, bool LDS>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void raytrace_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins,
+#ifndef RT_WAVES_PER_EU
+#define RT_WAVES_PER_EU 4
+#endif
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void raytrace_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins,
                                                         const float4* __restrict__ dirs, uint32_t* __restrict__ rng, uint32_t n_rng,
                                                         float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
     const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
     const int lane = threadIdx.x & 63;
     const uint32_t rows = (uint32_t)(a.row1 - a.row0);
-    const uint32_t tiles_x = ((uint32_t)a.W + 7) / 8, n_tiles = tiles_x * ((rows + 7) / 8);
+    const uint32_t T = (uint32_t)a.tile, tiles_x = ((uint32_t)a.W + T - 1) / T, n_tiles = tiles_x * ((rows + T - 1) / T);
     while (true) {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(work, 1u);
@@ -497,8 +587,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         // object tiles start first instead of being the latency tail of the launch
         const uint32_t tile = a.tile_order ? a.tile_order[k] : k;
         const uint64_t t0 = wall_clock64();
-        const uint32_t x = (tile % tiles_x) * 8 + (lane & 7), y = (tile / tiles_x) * 8 + (lane >> 3);
-        if (x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth);
+        const uint32_t x = (tile % tiles_x) * T + (uint32_t)lane % T, y = (tile / tiles_x) * T + (uint32_t)lane / T;
+        if ((uint32_t)lane < T * T && x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth);
         if (a.tile_cost && lane == 0) a.tile_cost[tile] = (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull);
     }
 }
@@ -879,7 +969,8 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     const uint32_t tp = 512, ts = 512;
     const bool lds = a.scene_in_lds != 0;
     const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
-    const uint32_t bp = std::min((n + tp - 1) / tp, a.persistent_blocks * 2);
+    const uint32_t n_tiles = (((uint32_t)a.W + a.tile - 1) / a.tile) * (((uint32_t)(a.row1 - a.row0) + a.tile - 1) / a.tile);
+    const uint32_t bp = std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * 2);
     (void)shadow_blocks;
     if (lds) {
         allow_lds(raytrace_kernel<true, true>, lp);

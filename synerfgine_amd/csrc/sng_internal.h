@@ -147,6 +147,8 @@ struct RaytraceArgs {
     uint32_t* work;             // 2 device work counters (pixel tiles, shadow-ray chunks)
     const uint32_t* tile_order; // 8x8 tile visiting order (nullptr: row-major)
     uint32_t* tile_cost;        // per-tile cycles of this frame (nullptr: not recorded)
+    int bvh_flat;               // BvhWide traversal with the nearer child in a register (bvh_walk_near)
+    int tile;                   // path-kernel tile edge in pixels (8: 64 lanes, 4: 16 lanes per wave)
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,

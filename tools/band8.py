@@ -11,7 +11,7 @@ from synerfgine_amd import scene as S
 from synerfgine_amd.tiling import balance_bounds, even_bounds
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-tb, eng, _ = S.make_engine("c3")
+tb, eng, _ = S.make_engine("c3", model="lego")
 H = eng.resolution()["mesh"][1]
 
 

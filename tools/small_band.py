@@ -9,7 +9,7 @@ from synerfgine_amd import scene as S
 
 r0, r1 = int(sys.argv[1]), int(sys.argv[2])
 serial = len(sys.argv) > 3 and sys.argv[3] == "serial"
-tb, eng, _ = S.make_engine("c3", overrides={"concurrent_streams": 0} if serial else None)
+tb, eng, _ = S.make_engine("c3", overrides={"concurrent_streams": 0} if serial else None, model="lego")
 for _ in range(3):
     eng.frame(rows=(r0, r1))
 torch.cuda.synchronize()
