@@ -160,7 +160,30 @@ int sng_get_focal_length(sng_ctx* ctx, int which /*0 nerf,1 mesh*/, float out[2]
 /* ---- frame: Engine::resize + Engine::frame (engine.cu:236-255, 352-433) ---- */
 int sng_set_window(sng_ctx* ctx, int32_t width, int32_t height);
 int sng_get_resolution(sng_ctx* ctx, sng_resolution_info* out);
+/* Each call first advances the scene animation exactly as Engine::frame does before rendering
+ * (engine.cu:365-372): the camera path when playing (CamPath::update, cam_path.cuh:117-135), then,
+ * when "animation_speed" > 0, every object (VirtualObject::next_frame, virtual_object.cuh:53-64)
+ * and light (Light::next_frame, light.cuh:39-49).  Animation parameters (sng_set_param):
+ * "animation_speed", "camera_path_playing" (Play/Pause), "camera_path_frame" (the frame slider);
+ * read-only "camera_path_total_frames". */
 int sng_render_frame(sng_ctx* ctx, const sng_frame_params* params, sng_frame_result* out);
+/* ---- headless display stage (Display::present / save_image, display.cu:265-322; main.frag:24-117) ----
+ * The last frame's final RGBA at mesh resolution, drawn to the window resolution through main.frag's
+ * FXAA (GL_LINEAR / GL_REPEAT sampling), blended over rendering.clear_color and read back as RGB8,
+ * top-down.  rgb_out: host buffer of width*height*3 bytes (window resolution), may be NULL. */
+int sng_display_frame(sng_ctx* ctx, uint8_t* rgb_out, uint64_t capacity);
+/* Display::save_image: display_frame, then <folder>/output-NNN.png (NNN = ++image count, 3 digits);
+ * *written = 0 once the count exceeds output.img_count (default: the camera path's frames).  folder
+ * NULL/"" = the scene JSON's output.folder.  Parameters "record", "img_count", "img_count_max". */
+int sng_save_image(sng_ctx* ctx, const char* folder, int32_t* written);
+/* host: 8-bit RGB (3) / RGBA (4) PNG writer (stbi_write_png) */
+int sng_image_write_png(const char* path, const uint8_t* pixels, int32_t width, int32_t height, int32_t channels);
+/* host-only: load a scene JSON and play n_frames of its animation without a device; per frame the
+ * camera (mat4x3, column-major), light positions [n_lights][3] and object positions [n_objects][3].
+ * playing / animation_speed < 0 keep the JSON's move_on_start / animation_speed. */
+int sng_animation_probe(const char* scene_json, uint32_t n_frames, int32_t playing, float animation_speed, float* cameras,
+                        float* light_pos, uint32_t light_cap, float* object_pos, uint32_t object_cap, uint32_t* n_lights,
+                        uint32_t* n_objects);
 /* Testbed::render_nerf (testbed_nerf.cu:2679-2837): the instant-NGP tracer (NerfTracer::trace 2279-2401,
  * composite_kernel_nerf 577-788, shade_kernel_nerf 1788-1828) into d_nerf_rgba / d_nerf_depth at NeRF
  * resolution; parameters "render_mode" (ERenderMode) and "depth_scale".  row_begin/row_end are NeRF rows. */

@@ -55,6 +55,20 @@ class orc_train_images(ctypes.Structure):
                 ("w", ctypes.c_int32), ("h", ctypes.c_int32), ("n", ctypes.c_int32)]
 
 
+class orc_keyframe(ctypes.Structure):
+    _fields_ = [("view", ctypes.c_float * 3), ("at", ctypes.c_float * 3), ("zoom", ctypes.c_float)]
+
+
+class orc_light_anim(ctypes.Structure):
+    _fields_ = [("on", ctypes.c_int32), ("start", ctypes.c_float * 3), ("end", ctypes.c_float * 3), ("ratio", ctypes.c_float),
+                ("step", ctypes.c_float)]
+
+
+class orc_object_anim(ctypes.Structure):
+    _fields_ = [("angle", ctypes.c_float), ("axis", ctypes.c_float * 3), ("centre", ctypes.c_float * 3), ("rot", ctypes.c_float * 9),
+                ("pos", ctypes.c_float * 3)]
+
+
 class orc_nerf_stats(ctypes.Structure):
     _fields_ = [("n_iterations", ctypes.c_uint32), ("n_samples", ctypes.c_uint64), ("n_slots", ctypes.c_uint64),
                 ("n_hit", ctypes.c_uint32), ("alive_per_iter", ctypes.c_uint32 * 64), ("steps_per_iter", ctypes.c_uint32 * 64)]
@@ -103,6 +117,9 @@ def lib():
             "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
             "orc_num_threads": (i32, []),
             "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
+            "orc_display": (None, [vp, i32, i32, i32, i32, vp, vp]),
+            "orc_camera_set_view": (None, [vp, vp, vp, vp, vp, f32]),
+            "orc_animation_play": (None, [vp, vp, vp, vp, u32, i32, i32, f32, vp, u32, vp, u32, u32, vp, vp, vp]),
             "orc_train_adam_ema": (None, [u64, u32, f32, f32, f32, f32, f32, f32, f32, u32, vp, vp, vp, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
@@ -315,3 +332,60 @@ def train_adam_ema(master, grads, m1, m2, steps, ema, n_matrix, lr=1e-2, beta1=0
         assert a.dtype == dt and a.flags.c_contiguous
     lib().orc_train_adam_ema(len(master), n_matrix, lr, beta1, beta2, eps, l2_reg, loss_scale, ema_decay, ema_step, ptr(master), ptr(grads),
                              ptr(m1), ptr(m2), ptr(steps), ptr(ema))
+
+
+# ---- scene animation (camera path, lights, objects) ---------------------------------
+TESTBED_DEFAULT_CAMERA = [1, 0, 0, 0, -1, 0, 0, 0, -1, 0.5, 0.5, 2.0]   # Testbed::reset_camera (testbed.cu:470-490)
+TESTBED_DEFAULT_SCALE = 1.5
+
+
+def animation_play(scene, n_frames, playing=None, anim_speed=None):
+    """Play a parsed scene JSON's animation: (cameras [n][12], light positions [n][L][3], object positions [n][O][3])."""
+    cam = np.array(TESTBED_DEFAULT_CAMERA, np.float32)
+    scale = ctypes.c_float(TESTBED_DEFAULT_SCALE)
+    up = np.array([0, 1, 0], np.float32)
+    cc = scene.get("camera", {})
+    view = np.array(cc.get("view", [0, 0, 0]), np.float32)
+    if np.dot(view, view) != 0:
+        lib().orc_camera_set_view(ptr(cam), ctypes.byref(scale), ptr(up), ptr(view), ptr(np.array(cc.get("at", [0, 0, 0]), np.float32)),
+                                  float(cc.get("zoom", 1.0)))
+    keys = []
+    if "path" in cc:
+        keys = list(cc.get("frames", [])) + list(cc["path"])
+    kk = (orc_keyframe * max(1, len(keys)))()
+    for i, k in enumerate(keys):
+        kk[i].view[:] = k["view"]; kk[i].at[:] = k["at"]; kk[i].zoom = k["zoom"]
+    total = int(cc.get("total_time_ms", 10000)) * int(cc.get("fps", 24)) // 1000
+    play = bool(cc.get("move_on_start", False)) if playing is None else bool(playing)
+    speed = float(cc.get("animation_speed", 0.0)) if anim_speed is None else float(anim_speed)
+    ls = scene.get("lights", [])
+    la = (orc_light_anim * max(1, len(ls)))()
+    for i, l in enumerate(ls):
+        la[i].start[:] = l["pos"]
+        if "anim" in l:
+            la[i].on = 1; la[i].end[:] = l["anim"]["end"]; la[i].step = l["anim"]["step"]
+    os_ = scene.get("objfile", [])
+    oa = (orc_object_anim * max(1, len(os_)))()
+    for i, o in enumerate(os_):
+        oa[i].rot[:] = o.get("rot", [1, 0, 0, 0, 1, 0, 0, 0, 1]); oa[i].pos[:] = o.get("pos", [0, 0, 0])
+        oa[i].axis[:] = [0, 1, 0]
+        if "anim" in o:
+            oa[i].angle = o["anim"]["rot_angle"]; oa[i].axis[:] = o["anim"]["rot_axis"]; oa[i].centre[:] = o["anim"]["rot_center"]
+    cams = np.zeros((n_frames, 12), np.float32)
+    lp = np.zeros((n_frames, len(ls), 3), np.float32)
+    op = np.zeros((n_frames, len(os_), 3), np.float32)
+    vp = ctypes.c_void_p
+    lib().orc_animation_play(ptr(cam), ctypes.byref(scale), ptr(up), ctypes.cast(kk, vp), len(keys), total, int(play), speed, ctypes.cast(la, vp),
+                             len(ls), ctypes.cast(oa, vp), len(os_), n_frames, ptr(cams), ptr(lp), ptr(op))
+    return cams, lp, op
+
+
+def display(rgba, out_w=None, out_h=None, clear=(0.0, 0.0, 0.0)):
+    """main.frag FXAA + blend + unorm8 of a final RGBA32F frame [h][w][4] -> RGB8 [oh][ow][3]."""
+    im = np.ascontiguousarray(rgba, np.float32)
+    h, w = im.shape[:2]
+    ow, oh = out_w or w, out_h or h
+    out = np.zeros((oh, ow, 3), np.uint8)
+    cl = np.asarray(clear, np.float32)
+    lib().orc_display(ptr(im), w, h, ow, oh, ptr(cl), ptr(out))
+    return out

@@ -1620,3 +1620,175 @@ void orc_train_adam_ema(uint64_t n, uint32_t n_matrix, float lr, float beta1, fl
     }
 }
 }  // extern "C"
+
+/* ---- scene animation ---------------------------------------------------------- */
+namespace {
+struct OrcCam { V3 c[4]; float scale; V3 up; };
+inline V3 orc_look_at(const OrcCam& k) { return k.c[3] + k.c[2] * k.scale; }                       /* testbed.cu:405-407 */
+inline void orc_set_look_at(OrcCam& k, V3 pos) { k.c[3] = k.c[3] + (pos - orc_look_at(k)); }     /* testbed.cu:409-411 */
+inline void orc_set_scale(OrcCam& k, float scale) {                                               /* testbed.cu:413-417 */
+    V3 prev = orc_look_at(k);
+    k.c[3] = (k.c[3] - prev) * (scale / k.scale) + prev;
+    k.scale = scale;
+}
+inline void orc_set_view_dir(OrcCam& k, V3 dir) {                                                 /* testbed.cu:419-425 */
+    V3 old = orc_look_at(k);
+    k.c[0] = normalize(cross(dir, k.up));
+    k.c[1] = normalize(cross(dir, k.c[0]));
+    k.c[2] = normalize(dir);
+    orc_set_look_at(k, old);
+}
+}  // namespace
+
+extern "C" {
+void orc_camera_set_view(float cam[12], float* scale, const float up[3], const float view[3], const float at[3], float zoom) {
+    OrcCam k;
+    for (int i = 0; i < 4; ++i) k.c[i] = v3(cam[3 * i], cam[3 * i + 1], cam[3 * i + 2]);
+    k.scale = *scale;
+    k.up = v3(up[0], up[1], up[2]);
+    orc_set_view_dir(k, v3(view[0], view[1], view[2]));
+    orc_set_look_at(k, v3(at[0], at[1], at[2]));
+    orc_set_scale(k, zoom);
+    for (int i = 0; i < 4; ++i) { cam[3 * i] = k.c[i].x; cam[3 * i + 1] = k.c[i].y; cam[3 * i + 2] = k.c[i].z; }
+    *scale = k.scale;
+}
+void orc_animation_play(float cam[12], float* scale, const float up[3], const orc_keyframe* keys, uint32_t n_keys, int32_t total_frames,
+                        int32_t playing, float anim_speed, orc_light_anim* lights, uint32_t n_lights, orc_object_anim* objs, uint32_t n_objs,
+                        uint32_t n_frames, float* cams_out, float* light_pos_out, float* obj_pos_out) {
+    OrcCam k;
+    for (int i = 0; i < 4; ++i) k.c[i] = v3(cam[3 * i], cam[3 * i + 1], cam[3 * i + 2]);
+    k.scale = *scale;
+    k.up = v3(up[0], up[1], up[2]);
+    /* CamPath(config) (cam_path.cuh:97-115): frames_between_keyframes = total_frames / max(n - 1, 1) */
+    int frames_between = total_frames / std::max((int)n_keys - 1, 1);
+    if (frames_between < 1) frames_between = 1;
+    int current_frame = 0;
+    const bool enable = anim_speed > 0.0f;   /* m_enable_animations (engine.cu:43-46) */
+    for (uint32_t f = 0; f < n_frames; ++f) {
+        /* CamPath::update -> advance_frame -> set_to_frame (cam_path.cuh:117-135) */
+        if (playing && n_keys >= 2) {
+            current_frame += 1;
+            int current_keyframe = current_frame / frames_between;
+            uint32_t next = (uint32_t)current_keyframe + 1;
+            if (next >= n_keys) { current_frame = 0; current_keyframe = 0; next = 1; }
+            const orc_keyframe& a = keys[current_keyframe];
+            const orc_keyframe& b = keys[next];
+            /* CamKeyframe::interpolate (cam_path.cuh:30-39) */
+            float t = (float)(current_frame % frames_between) / (float)frames_between;
+            float invk = (float)(1.0 - (double)t);
+            V3 view = invk * v3(a.view[0], a.view[1], a.view[2]) + t * v3(b.view[0], b.view[1], b.view[2]);
+            orc_set_view_dir(k, view);
+            V3 at = invk * v3(a.at[0], a.at[1], a.at[2]) + t * v3(b.at[0], b.at[1], b.at[2]);
+            orc_set_look_at(k, at);
+            orc_set_scale(k, invk * a.zoom + t * b.zoom);
+        }
+        if (enable) {
+            /* update_world_objects (engine.cu:87-98): VirtualObject::next_frame (virtual_object.cuh:53-64) */
+            for (uint32_t i = 0; i < n_objs; ++i) {
+                orc_object_anim& o = objs[i];
+                if (o.angle == 0.0f) continue;
+                const V3 ax = v3(o.axis[0], o.axis[1], o.axis[2]);
+                const float cost = std::cos(o.angle * anim_speed);
+                const float sint = std::sin(o.angle * anim_speed);
+                /* tcnn mat3 from 9 scalars: column-major, written as in the reference (3rd column uses ax.z*ax.y) */
+                const float m[9] = {cost + ax.x * ax.x * (1.0f - cost), ax.x * ax.y * (1.0f - cost) - ax.z * sint, ax.x * ax.z * (1.0f - cost) + ax.y * sint,
+                                    ax.x * ax.y * (1.0f - cost) + ax.z * sint, cost + ax.y * ax.y * (1.0f - cost), ax.y * ax.z * (1.0f - cost) - ax.x * sint,
+                                    ax.z * ax.y * (1.0f - cost) - ax.y * sint, ax.z * ax.y * (1.0f - cost) + ax.x * sint, cost + ax.z * ax.z * (1.0f - cost)};
+                const M3 next = m3_load(m);
+                const M3 rot = m3_load(o.rot);
+                V3 p = v3(o.pos[0], o.pos[1], o.pos[2]);
+                const V3 centre = v3(o.centre[0], o.centre[1], o.centre[2]);
+                p = mul(next, mul(rot, p - centre)) + centre;
+                o.pos[0] = p.x; o.pos[1] = p.y; o.pos[2] = p.z;
+            }
+            /* Light::next_frame (light.cuh:39-49) */
+            for (uint32_t i = 0; i < n_lights; ++i) {
+                orc_light_anim& l = lights[i];
+                if (!l.on || l.step == 0.0f) continue;
+                float nr = l.ratio + l.step;
+                if (nr > 1.0 || nr < 0.0) { l.step = -l.step; nr = l.ratio + l.step; }
+                l.ratio = nr;
+            }
+        }
+        for (int i = 0; i < 4; ++i) { cams_out[12 * f + 3 * i] = k.c[i].x; cams_out[12 * f + 3 * i + 1] = k.c[i].y; cams_out[12 * f + 3 * i + 2] = k.c[i].z; }
+        for (uint32_t i = 0; i < n_lights; ++i) {
+            const orc_light_anim& l = lights[i];
+            float* q = light_pos_out + 3 * ((size_t)f * n_lights + i);
+            if (l.on) {
+                const V3 p = (1.0f - l.ratio) * v3(l.start[0], l.start[1], l.start[2]) + l.ratio * v3(l.end[0], l.end[1], l.end[2]);
+                q[0] = p.x; q[1] = p.y; q[2] = p.z;
+            } else {
+                q[0] = l.start[0]; q[1] = l.start[1]; q[2] = l.start[2];
+            }
+        }
+        for (uint32_t i = 0; i < n_objs; ++i)
+            for (int d = 0; d < 3; ++d) obj_pos_out[3 * ((size_t)f * n_objs + i) + d] = objs[i].pos[d];
+    }
+    for (int i = 0; i < 4; ++i) { cam[3 * i] = k.c[i].x; cam[3 * i + 1] = k.c[i].y; cam[3 * i + 2] = k.c[i].z; }
+    *scale = k.scale;
+}
+}  // extern "C"
+
+/* ---- display stage (main.frag) ------------------------------------------------------ */
+namespace {
+struct Tex4 { float r, g, b, a; };
+/* texture(sampler2D, uv) with GL_LINEAR + GL_REPEAT; textureProjOffset adds the texel offset in texel space */
+Tex4 gl_texture(const float* img, int W, int H, float u, float v, int ox = 0, int oy = 0) {
+    const float x = u * (float)W - 0.5f + (float)ox, y = v * (float)H - 0.5f + (float)oy;
+    const float fx0 = std::floor(x), fy0 = std::floor(y);
+    const float ax = x - fx0, ay = y - fy0;
+    int x0 = (int)fx0 % W, y0 = (int)fy0 % H;
+    if (x0 < 0) x0 += W;
+    if (y0 < 0) y0 += H;
+    const int x1 = x0 + 1 == W ? 0 : x0 + 1, y1 = y0 + 1 == H ? 0 : y0 + 1;
+    const float* a = img + 4 * ((size_t)y0 * W + x0);
+    const float* b = img + 4 * ((size_t)y0 * W + x1);
+    const float* c = img + 4 * ((size_t)y1 * W + x0);
+    const float* d = img + 4 * ((size_t)y1 * W + x1);
+    const float w00 = (1.0f - ax) * (1.0f - ay), w10 = ax * (1.0f - ay), w01 = (1.0f - ax) * ay, w11 = ax * ay;
+    float o[4];
+    for (int k = 0; k < 4; ++k) o[k] = a[k] * w00 + b[k] * w10 + c[k] * w01 + d[k] * w11;
+    return {o[0], o[1], o[2], o[3]};
+}
+inline float gl_luma(float r, float g, float b) { return r * 0.299f + g * 0.587f + b * 0.114f; }   /* dot(rgb, vec3(0.299, 0.587, 0.114)) */
+}  // namespace
+
+extern "C" void orc_display(const float* rgba, int32_t W, int32_t H, int32_t OW, int32_t OH, const float clear[3], uint8_t* out) {
+#pragma omp parallel for schedule(static)
+    for (int row = 0; row < OH; ++row)
+        for (int x = 0; x < OW; ++x) {
+            /* main(): tex_coords = UVs, y flipped, unwarp = identity without foveation */
+            const int ygl = OH - 1 - row;
+            const float u = ((float)x + 0.5f) / (float)OW;
+            const float v = 1.0f - ((float)ygl + 0.5f) / (float)OH;
+            /* fxaa(tex, fragCoord, resolution) */
+            const float ivx = 1.0f / (float)OW, ivy = 1.0f / (float)OH;
+            const Tex4 nw = gl_texture(rgba, W, H, u, v, -1, 1), ne = gl_texture(rgba, W, H, u, v, 1, 1);
+            const Tex4 sw = gl_texture(rgba, W, H, u, v, -1, -1), se = gl_texture(rgba, W, H, u, v, 1, -1);
+            const Tex4 tc = gl_texture(rgba, W, H, u, v);
+            const float lNW = gl_luma(nw.r, nw.g, nw.b), lNE = gl_luma(ne.r, ne.g, ne.b), lSW = gl_luma(sw.r, sw.g, sw.b), lSE = gl_luma(se.r, se.g, se.b);
+            const float lM = gl_luma(tc.r, tc.g, tc.b);
+            const float lmin = std::fmin(lM, std::fmin(std::fmin(lNW, lNE), std::fmin(lSW, lSE)));
+            const float lmax = std::fmax(lM, std::fmax(std::fmax(lNW, lNE), std::fmax(lSW, lSE)));
+            float dx = -((lNW + lNE) - (lSW + lSE));
+            float dy = ((lNW + lSW) - (lNE + lSE));
+            const float reduce = std::fmax((lNW + lNE + lSW + lSE) * (0.25f * (1.0f / 8.0f)), 1.0f / 128.0f);   /* FXAA_REDUCE_MUL / _MIN */
+            const float rcp_min = 1.0f / (std::fmin(std::fabs(dx), std::fabs(dy)) + reduce);
+            dx = std::fmin(8.0f, std::fmax(-8.0f, dx * rcp_min)) * ivx;   /* FXAA_SPAN_MAX */
+            dy = std::fmin(8.0f, std::fmax(-8.0f, dy * rcp_min)) * ivy;
+            const float k1 = 1.0f / 3.0f - 0.5f, k2 = 2.0f / 3.0f - 0.5f;
+            const Tex4 a1 = gl_texture(rgba, W, H, u + dx * k1, v + dy * k1), a2 = gl_texture(rgba, W, H, u + dx * k2, v + dy * k2);
+            const float A[3] = {0.5f * (a1.r + a2.r), 0.5f * (a1.g + a2.g), 0.5f * (a1.b + a2.b)};
+            const Tex4 b1 = gl_texture(rgba, W, H, u + dx * -0.5f, v + dy * -0.5f), b2 = gl_texture(rgba, W, H, u + dx * 0.5f, v + dy * 0.5f);
+            const float B[3] = {A[0] * 0.5f + 0.25f * (b1.r + b2.r), A[1] * 0.5f + 0.25f * (b1.g + b2.g), A[2] * 0.5f + 0.25f * (b1.b + b2.b)};
+            const float lB = gl_luma(B[0], B[1], B[2]);
+            const float* C = (lB < lmin || lB > lmax) ? A : B;
+            const float ia = 1.0f - tc.a;
+            uint8_t* o = out + 3 * ((size_t)row * OW + x);
+            for (int k = 0; k < 3; ++k) {
+                float f = C[k] + clear[k] * ia;
+                f = std::fmin(std::fmax(f, 0.0f), 1.0f);
+                o[k] = (uint8_t)(int)(f * 255.0f + 0.5f);
+            }
+        }
+}

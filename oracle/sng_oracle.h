@@ -181,6 +181,24 @@ void orc_train_adam_ema(uint64_t n, uint32_t n_matrix, float lr, float beta1, fl
                         float ema_decay, uint32_t ema_step, float* master, const float* grads, float* m1, float* m2, uint32_t* steps,
                         float* ema);
 
+/* ---- scene animation: CamPath (cam_path.cuh:30-143) driving Testbed::set_view_dir /
+ * set_look_at / set_scale (testbed.cu:405-425), Light::next_frame (light.cuh:39-49), VirtualObject::next_frame
+ * (virtual_object.cuh:53-64), played in Engine::frame's order (engine.cu:365-372, 80-127). */
+typedef struct { float view[3], at[3], zoom; } orc_keyframe;
+typedef struct { int32_t on; float start[3], end[3], ratio, step; } orc_light_anim;
+typedef struct { float angle, axis[3], centre[3], rot[9] /* object rotation, column-major */, pos[3]; } orc_object_anim;
+/* Engine::init's camera from the scene JSON (engine.cu:148-152): set_view_dir(view), set_look_at(at), set_scale(zoom) */
+void orc_camera_set_view(float cam[12], float* scale, const float up[3], const float view[3], const float at[3], float zoom);
+void orc_animation_play(float cam[12] /* in/out */, float* scale /* in/out */, const float up[3], const orc_keyframe* keys, uint32_t n_keys,
+                        int32_t total_frames, int32_t playing, float anim_speed, orc_light_anim* lights, uint32_t n_lights,
+                        orc_object_anim* objs, uint32_t n_objs, uint32_t n_frames, float* cams_out /* n x 12 */,
+                        float* light_pos_out /* n x n_lights x 3 */, float* obj_pos_out /* n x n_objs x 3 */);
+
+/* headless display stage: main.frag (scripts/virtual_desc/main.frag:24-117) FXAA of the final RGBA32F
+ * frame (W x H texture, GL_LINEAR + GL_REPEAT) into an OW x OH window, blended GL_ONE /
+ * GL_ONE_MINUS_SRC_ALPHA over the clear colour (display.cu:265-281), unorm8 RGB, top-down rows */
+void orc_display(const float* rgba, int32_t W, int32_t H, int32_t OW, int32_t OH, const float clear[3], uint8_t* rgb_out);
+
 int32_t orc_num_threads(void);
 
 #ifdef __cplusplus

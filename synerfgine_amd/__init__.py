@@ -186,6 +186,7 @@ class Engine:
 
     def init(self, width, height):
         check(self._lib.sng_set_window(self.ctx, int(width), int(height)))
+        self._window = (int(width), int(height))
 
     def set_syn_samples(self, spp):      # --sshadows (engine.cuh:29)
         self.set_param("sshadows", spp)
@@ -262,6 +263,20 @@ class Engine:
         check(self._lib.sng_set_sched_reducer(self.ctx, None, None))
         self._reduce_cb = None
 
+    # ---- headless display stage (Display::present / save_image, display.cu:265-322) ----------
+    def display(self):
+        """The window image of the last frame: main.frag FXAA + clear-colour blend, RGB8 [h][w][3], top-down."""
+        w, h = self._window
+        out = np.zeros((h, w, 3), np.uint8)
+        check(self._lib.sng_display_frame(self.ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), out.nbytes))
+        return out
+
+    def save_image(self, folder=None):
+        """Display::save_image: <folder>/output-NNN.png; False once output.img_count is exceeded."""
+        w = ctypes.c_int32()
+        check(self._lib.sng_save_image(self.ctx, None if folder is None else str(folder).encode(), ctypes.byref(w)))
+        return bool(w.value)
+
     # ---- scene inspection (tests) --------------------------------------------------
     def scene(self):
         no, nl, nm = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
@@ -297,6 +312,30 @@ class Engine:
     def set_rng_states(self, which, states):
         states = np.ascontiguousarray(states, np.uint32)
         check(self._lib.sng_set_rng_states(self.ctx, which, states.ctypes.data_as(_lib.U32P), states.shape[0]))
+
+
+def write_png(path, image):
+    """uint8 [h][w][3|4] -> PNG (host; the recording's stbi_write_png)."""
+    im = np.ascontiguousarray(image, np.uint8)
+    check(_lib.load().sng_image_write_png(str(path).encode(), im.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), im.shape[1], im.shape[0],
+                                          im.shape[2]))
+
+
+def animation_probe(scene_json, n_frames, playing=None, animation_speed=None, max_lights=64, max_objects=64):
+    """Host-only (no device): play a scene JSON's animation for n_frames in Engine::frame's order --
+    (cameras [n][3][4], light positions [n][L][3], object positions [n][O][3])."""
+    lib = _lib.load()
+    cams = np.zeros((n_frames, 12), np.float32)
+    lp = np.zeros((n_frames, max_lights, 3), np.float32)
+    op = np.zeros((n_frames, max_objects, 3), np.float32)
+    nl, no = ctypes.c_uint32(), ctypes.c_uint32()
+    check(lib.sng_animation_probe(str(scene_json).encode(), n_frames, -1 if playing is None else int(bool(playing)),
+                                  -1.0 if animation_speed is None else float(animation_speed), _fptr(cams), _fptr(lp), max_lights, _fptr(op),
+                                  max_objects, ctypes.byref(nl), ctypes.byref(no)))
+    L, O = nl.value, no.value
+    lp = lp.reshape(-1)[: n_frames * L * 3].reshape(n_frames, L, 3)
+    op = op.reshape(-1)[: n_frames * O * 3].reshape(n_frames, O, 3)
+    return cams.reshape(n_frames, 4, 3).transpose(0, 2, 1), lp, op
 
 
 def bvh_build(tris, prims_per_leaf=4):

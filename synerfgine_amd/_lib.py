@@ -169,6 +169,11 @@ SIGNATURES = {
     "sng_get_resolution": (ctypes.c_int, [P, ctypes.POINTER(sng_resolution_info)]),
     "sng_render_frame": (ctypes.c_int, [P, ctypes.POINTER(sng_frame_params), ctypes.POINTER(sng_frame_result)]),
     "sng_render_nerf_ngp": (ctypes.c_int, [P, ctypes.POINTER(sng_frame_params), ctypes.POINTER(sng_frame_result)]),
+    "sng_display_frame": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint8), U64]),
+    "sng_save_image": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.POINTER(I32)]),
+    "sng_image_write_png": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), I32, I32, I32]),
+    "sng_animation_probe": (ctypes.c_int, [ctypes.c_char_p, U32, I32, ctypes.c_float, FP, FP, U32, FP, U32, ctypes.POINTER(U32),
+                                           ctypes.POINTER(U32)]),
     "sng_image_load_png": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), U64, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "sng_train_set_dataset": (ctypes.c_int, [P, U32, U32, U32, ctypes.POINTER(ctypes.c_uint8), FP, FP, FP]),
     "sng_train_reset": (ctypes.c_int, [P, U64]),

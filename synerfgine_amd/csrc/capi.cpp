@@ -24,6 +24,7 @@
 
 #include "json.h"
 #include "sng_internal.h"
+#include <array>
 #include "train.h"
 
 using namespace sng;
@@ -277,6 +278,16 @@ m3 rolling_shutter_rotation(const m3& M) {
             mk(2.0f * (qxz + qwy), 2.0f * (qyz - qwx), 1.0f - 2.0f * (qxx + qyy))};
 }
 
+// ---- animation: cam_path.cuh:30-143, light.cuh:39-49, virtual_object.cuh:53-64 ----
+struct CamKeyframe { f3 view, at; float zoom; };
+struct CamPathState {           // sng::CamPath
+    std::vector<CamKeyframe> keys;
+    int total_time_ms = 10000, fps = 24, total_frames = 0, frames_between = 1, current_frame = 0, current_keyframe = 0;
+    bool playing = false, present = false;
+};
+struct LightAnim { bool on = false; f3 start{}, end{}; float ratio = 0.0f, step = 0.0f; };
+struct ObjAnim { float angle = 0.0f; f3 axis{0.0f, 1.0f, 0.0f}, centre{0.0f, 0.0f, 0.0f}; };
+
 struct HostObject {
     std::string file;
     std::vector<Tri> tris;
@@ -287,6 +298,7 @@ struct HostObject {
     f3 pos;
     float scale = 1.0f;
     int mat = 0;
+    ObjAnim anim;
     DevBuf d_nodes, d_tris, d_wide;
 };
 
@@ -400,6 +412,19 @@ struct sng_ctx {
     // camera (Testbed)
     float cam[12] = {1, 0, 0, 0, -1, 0, 0, 0, -1, 0.5f, 0.5f, 2.0f};
     float m_scale = 1.5f;
+    // animation state (Engine::m_camera_path, m_anim_speed / m_enable_animations, per light / object)
+    CamPathState campath;
+    std::vector<LightAnim> light_anim;
+    std::vector<ObjAnim> obj_anim;
+    float anim_speed = 0.0f;
+    bool animations = false;
+    uint64_t anim_frames = 0;
+    // display stage (Display::present / save_image, display.cu:265-322)
+    f3 clear_color{0.0f, 0.0f, 0.0f};   // Engine::m_default_clear_color (rendering.clear_color, engine.cu:161-163)
+    std::string out_folder;             // output.folder (engine.cu:54-64)
+    bool record = false;                // output.record
+    int img_count = 0, img_count_max = 1;
+    DevBuf display_rgb;
     f3 up = {0.0f, 1.0f, 0.0f};
     float rel_focal[2] = {0, 0};
     int fov_axis = 1;
@@ -697,6 +722,32 @@ void load_scene(sng_ctx* c, const std::string& path) {
         if (cc.contains("at")) at = mk(cc["at"][0].as_float(), cc["at"][1].as_float(), cc["at"][2].as_float());
         if (cc.contains("zoom")) zoom = cc["zoom"].as_float();
         if (cc.contains("vo_scale")) c->params["vo_scale"] = cc["vo_scale"].as_num();
+        // Engine::set_virtual_world (engine.cu:43-49): animation_speed, CamPath(cam_conf) (cam_path.cuh:97-115)
+        c->anim_speed = 0.0f;
+        c->animations = false;
+        if (cc.contains("animation_speed")) {
+            c->anim_speed = cc["animation_speed"].as_float();
+            c->animations = c->anim_speed > 0.0f;
+        }
+        c->campath = CamPathState{};
+        if (cc.contains("path")) {
+            CamPathState& cp = c->campath;
+            auto key = [](const JValue& f) {
+                return CamKeyframe{mk(f["view"][0].as_float(), f["view"][1].as_float(), f["view"][2].as_float()),
+                                   mk(f["at"][0].as_float(), f["at"][1].as_float(), f["at"][2].as_float()), f["zoom"].as_float()};
+            };
+            if (cc.contains("frames"))
+                for (size_t i = 0; i < cc["frames"].size(); ++i) cp.keys.push_back(key(cc["frames"][i]));
+            if (!cc.contains("total_time_ms")) throw SngError(SNG_ERR_INVALID, "camera path without total_time_ms");
+            cp.total_time_ms = (int)cc["total_time_ms"].as_num();
+            if (cc.contains("fps")) cp.fps = (int)cc["fps"].as_num();
+            cp.total_frames = cp.total_time_ms * cp.fps / 1000;
+            if (cc.contains("move_on_start")) cp.playing = cc["move_on_start"].as_num() != 0.0;
+            for (size_t i = 0; i < cc["path"].size(); ++i) cp.keys.push_back(key(cc["path"][i]));
+            // total_frames / (keyframes - 1); the reference divides by zero in set_to_frame when that is 0
+            cp.frames_between = std::max(1, cp.total_frames / std::max((int)cp.keys.size() - 1, 1));
+            cp.present = true;
+        }
         if (dot(view, view) != 0.0f) {   // Engine::init (engine.cu:148-152)
             set_view_dir(c, view);
             set_look_at(c, at);
@@ -711,10 +762,24 @@ void load_scene(sng_ctx* c, const std::string& path) {
                                         "shadow_on_nerf", "show_virtual_obj", "show_nerf", "depth_offset"};
         for (const char* k : numeric)
             if (r.contains(k)) c->params[k] = r[k].as_num();
+        if (r.contains("clear_color")) c->clear_color = mk(r["clear_color"][0].as_float(), r["clear_color"][1].as_float(), r["clear_color"][2].as_float());
         if (r.contains("nerf_filter") && r["nerf_filter"].as_str() != "Shade")
             throw SngError(SNG_ERR_INVALID, "nerf_filter '" + r["nerf_filter"].as_str() + "' is not on the accelerated path (Shade only)");
         if (r.contains("syn_filter") && r["syn_filter"].as_str() != "Final")
             throw SngError(SNG_ERR_INVALID, "syn_filter '" + r["syn_filter"].as_str() + "' is not on the accelerated path (Final only)");
+    }
+    // output (engine.cu:52-65): recording folder, record flag, image budget (img_count or the camera path's frames)
+    c->img_count = 0;
+    c->record = false;
+    c->img_count_max = std::max(1, c->campath.present ? c->campath.total_frames : 0);
+    if (cfg.contains("output")) {
+        const JValue& oc = cfg["output"];
+        if (oc.contains("folder")) {
+            c->out_folder = oc["folder"].as_str();
+            if (!c->out_folder.empty() && c->out_folder[0] != '/') c->out_folder = dir + "/" + c->out_folder;
+        }
+        if (oc.contains("img_count")) c->img_count_max = (int)oc["img_count"].as_num();
+        if (oc.contains("record")) c->record = oc["record"].as_num() != 0.0;
     }
     std::vector<sng_material> mats;
     for (size_t i = 0; i < cfg["materials"].size(); ++i) {   // Material(id, json) (material.cuh:26-48)
@@ -749,12 +814,19 @@ void load_scene(sng_ctx* c, const std::string& path) {
                       mk(a[6].as_float(), a[7].as_float(), a[8].as_float())};
         }
         ho.mat = (int)o["material"].as_num();
+        if (o.contains("anim")) {   // virtual_object.cu:27-33
+            const JValue& an = o["anim"];
+            ho.anim.centre = mk(an["rot_center"][0].as_float(), an["rot_center"][1].as_float(), an["rot_center"][2].as_float());
+            ho.anim.axis = mk(an["rot_axis"][0].as_float(), an["rot_axis"][1].as_float(), an["rot_axis"][2].as_float());
+            ho.anim.angle = an["rot_angle"].as_float();
+        }
         ho.tris = load_obj(fp);
         if (ho.tris.empty()) throw SngError(SNG_ERR_IO, "mesh has no triangles: " + fp);
         ho.nodes = build_bvh(ho.tris, ppl);
         objs.push_back(std::move(ho));
     }
     std::vector<sng_light> lights;
+    std::vector<LightAnim> light_anims;
     for (size_t i = 0; i < cfg["lights"].size(); ++i) {   // Light(id, json) (light.cuh:17-37)
         const JValue& l = cfg["lights"][i];
         sng_light ll{};
@@ -768,6 +840,15 @@ void load_scene(sng_ctx* c, const std::string& path) {
             else if (t == "directional") ll.type = 1;
             else throw SngError(SNG_ERR_INVALID, t + " light not recognized");
         }
+        LightAnim la;
+        if (l.contains("anim")) {   // light.cuh:31-36
+            la.on = true;
+            la.start = mk(ll.pos[0], ll.pos[1], ll.pos[2]);
+            la.end = mk(l["anim"]["end"][0].as_float(), l["anim"]["end"][1].as_float(), l["anim"]["end"][2].as_float());
+            la.step = l["anim"]["step"].as_float();
+            la.ratio = 0.0f;
+        }
+        light_anims.push_back(la);
         lights.push_back(ll);
     }
     for (auto& o : objs)
@@ -776,8 +857,71 @@ void load_scene(sng_ctx* c, const std::string& path) {
     c->objs = std::move(objs);
     c->mats = mats;
     c->lights = lights;
+    c->light_anim = light_anims;
+    c->anim_frames = 0;
     c->scene_dirty = true;
     c->mesh_reset = true;
+}
+
+// ---- animation: Engine::frame's m_camera_path.update + update_world_objects (engine.cu:365-372, 80-127) ----
+// CamPath::set_to_frame (cam_path.cuh:121-130) + CamKeyframe::interpolate (cam_path.cuh:30-39)
+void campath_set_to_frame(sng_ctx* c) {
+    CamPathState& cp = c->campath;
+    if (cp.keys.size() < 2) return;   // the reference reads keyframes[1] past the end here
+    cp.current_keyframe = cp.current_frame / cp.frames_between;
+    uint32_t next = (uint32_t)cp.current_keyframe + 1;
+    if (next >= cp.keys.size()) {
+        cp.current_frame = 0;
+        cp.current_keyframe = 0;
+        next = 1;
+    }
+    const CamKeyframe& a = cp.keys[cp.current_keyframe];
+    const CamKeyframe& b = cp.keys[next];
+    const float k = (float)(cp.current_frame % cp.frames_between) / (float)cp.frames_between;
+    const float invk = 1.0f - k;
+    set_view_dir(c, invk * a.view + k * b.view);
+    set_look_at(c, invk * a.at + k * b.at);
+    set_scale(c, invk * a.zoom + k * b.zoom);
+}
+// Light::next_frame (light.cuh:39-49); lights without "anim" do not move (the reference leaves
+// their step uninitialised)
+void light_next_frame(sng_light& l, LightAnim& a) {
+    if (!a.on || a.step == 0.0f) return;
+    float next = a.ratio + a.step;
+    if (next > 1.0f || next < 0.0f) {
+        a.step = -a.step;
+        next = a.ratio + a.step;
+    }
+    a.ratio = next;
+    const f3 p = (1.0f - a.ratio) * a.start + a.ratio * a.end;
+    l.pos[0] = p.x; l.pos[1] = p.y; l.pos[2] = p.z;
+}
+// VirtualObject::next_frame (virtual_object.cuh:53-64), including its rotation matrix as written
+// (third column uses ax.z*ax.y) and pos = R_next * (rot * (pos - centre)) + centre
+void object_next_frame(HostObject& o, float speed) {
+    const ObjAnim& an = o.anim;
+    if (an.angle == 0.0f) return;
+    const f3 ax = an.axis;
+    const float cost = std::cos(an.angle * speed), sint = std::sin(an.angle * speed);
+    const m3 R = {mk(cost + ax.x * ax.x * (1.0f - cost), ax.x * ax.y * (1.0f - cost) - ax.z * sint, ax.x * ax.z * (1.0f - cost) + ax.y * sint),
+                  mk(ax.x * ax.y * (1.0f - cost) + ax.z * sint, cost + ax.y * ax.y * (1.0f - cost), ax.y * ax.z * (1.0f - cost) - ax.x * sint),
+                  mk(ax.z * ax.y * (1.0f - cost) - ax.y * sint, ax.z * ax.y * (1.0f - cost) + ax.x * sint, cost + ax.z * ax.z * (1.0f - cost))};
+    o.pos = mul(R, mul(o.rot, o.pos - an.centre)) + an.centre;
+}
+// one frame of animation, in the reference's order: camera path, then objects, then lights
+void animate(sng_ctx* c) {
+    if (c->campath.playing) {
+        c->campath.current_frame += 1;   // CamPath::advance_frame (cam_path.cuh:132-135)
+        campath_set_to_frame(c);
+        c->mesh_reset = true;
+    }
+    if (c->animations) {
+        for (auto& o : c->objs) object_next_frame(o, c->anim_speed);
+        for (size_t i = 0; i < c->lights.size() && i < c->light_anim.size(); ++i) light_next_frame(c->lights[i], c->light_anim[i]);
+        c->scene_dirty = true;
+        c->mesh_reset = true;
+    }
+    ++c->anim_frames;
 }
 
 // ---- resize: Engine::resize (engine.cu:236-255) --------------------------------------
@@ -982,6 +1126,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     if ((int)c->p("res_factor") != c->last_res_factor) resize(c);
     const bool show_nerf = c->p("show_nerf") != 0.0;
     if (show_nerf && !(c->has_model && c->has_bitfield)) throw SngError(SNG_ERR_STATE, "no NeRF model/density grid loaded");
+    animate(c);
     if (c->scene_dirty) upload_scene(c);
     sng_frame_params P{};
     if (fp) P = *fp;
@@ -1691,6 +1836,23 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
         std::string k = key;
         if (k == "sshadows") k = "syn_shadow_samples";       // Engine::set_syn_samples (engine.cuh:29)
         else if (k == "nshadows") k = "nerf_shadow_samples"; // Engine::set_nerf_samples (engine.cuh:30-33)
+        if (k == "animation_speed") {   // Engine::m_anim_speed / m_enable_animations (engine.cu:43-46)
+            c->anim_speed = (float)v;
+            c->animations = c->anim_speed > 0.0f;
+            return;
+        }
+        if (k == "camera_path_playing") {   // CamPath::is_playing (Play / Pause)
+            c->campath.playing = v != 0.0 && c->campath.keys.size() >= 2;
+            return;
+        }
+        if (k == "record") { c->record = v != 0.0; return; }
+        if (k == "img_count_max") { c->img_count_max = (int)v; return; }
+        if (k == "camera_path_frame") {   // CamPath "Current Frame" slider -> set_to_frame
+            c->campath.current_frame = std::max(0, (int)v);
+            campath_set_to_frame(c);
+            c->mesh_reset = true;
+            return;
+        }
         if (!default_params().count(k)) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
         c->params[k] = v;
         c->mesh_reset = true;
@@ -1702,6 +1864,13 @@ int sng_get_param(sng_ctx* c, const char* key, double* v) {
         std::string k = key;
         if (k == "sshadows") k = "syn_shadow_samples";
         else if (k == "nshadows") k = "nerf_shadow_samples";
+        if (k == "animation_speed") { *v = c->anim_speed; return; }
+        if (k == "camera_path_playing") { *v = c->campath.playing ? 1.0 : 0.0; return; }
+        if (k == "camera_path_frame") { *v = c->campath.current_frame; return; }
+        if (k == "camera_path_total_frames") { *v = c->campath.present ? c->campath.total_frames : 0; return; }
+        if (k == "record") { *v = c->record ? 1.0 : 0.0; return; }
+        if (k == "img_count") { *v = c->img_count; return; }
+        if (k == "img_count_max") { *v = c->img_count_max; return; }
         auto it = c->params.find(k);
         if (it == c->params.end()) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
         *v = it->second;
@@ -1783,6 +1952,105 @@ int sng_get_resolution(sng_ctx* c, sng_resolution_info* out) {
 }
 int sng_render_nerf_ngp(sng_ctx* c, const sng_frame_params* p, sng_frame_result* out) {
     return guarded([&] { HIPCHK(hipSetDevice(c->device)); render_nerf_ngp(c, p, out); });
+}
+// PNG (RGB8 / RGBA8, filter 0, zlib) -- the recording's stbi_write_png (display.cu:319)
+void write_png(const std::string& path, const uint8_t* px, int w, int h, int ch) {
+    if (w <= 0 || h <= 0 || (ch != 3 && ch != 4)) throw SngError(SNG_ERR_INVALID, "bad PNG image");
+    std::vector<uint8_t> raw((size_t)h * ((size_t)w * ch + 1));
+    for (int y = 0; y < h; ++y) {
+        raw[(size_t)y * ((size_t)w * ch + 1)] = 0;
+        std::memcpy(&raw[(size_t)y * ((size_t)w * ch + 1) + 1], px + (size_t)y * w * ch, (size_t)w * ch);
+    }
+    uLongf zlen = compressBound((uLong)raw.size());
+    std::vector<uint8_t> z(zlen);
+    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 6) != Z_OK) throw SngError(SNG_ERR_IO, "zlib compress failed");
+    z.resize(zlen);
+    std::ofstream f(path, std::ios::binary);
+    if (!f) throw SngError(SNG_ERR_IO, "cannot write " + path);
+    auto be32 = [](uint32_t v) { return std::array<uint8_t, 4>{(uint8_t)(v >> 24), (uint8_t)(v >> 16), (uint8_t)(v >> 8), (uint8_t)v}; };
+    auto chunk = [&](const char* type, const std::vector<uint8_t>& data) {
+        const auto len = be32((uint32_t)data.size());
+        f.write(reinterpret_cast<const char*>(len.data()), 4);
+        std::vector<uint8_t> td(type, type + 4);
+        td.insert(td.end(), data.begin(), data.end());
+        f.write(reinterpret_cast<const char*>(td.data()), (std::streamsize)td.size());
+        const auto crc = be32((uint32_t)crc32(0L, td.data(), (uInt)td.size()));
+        f.write(reinterpret_cast<const char*>(crc.data()), 4);
+    };
+    static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    f.write(reinterpret_cast<const char*>(sig), 8);
+    std::vector<uint8_t> ihdr(13);
+    const auto bw = be32((uint32_t)w), bh = be32((uint32_t)h);
+    std::copy(bw.begin(), bw.end(), ihdr.begin());
+    std::copy(bh.begin(), bh.end(), ihdr.begin() + 4);
+    ihdr[8] = 8; ihdr[9] = ch == 4 ? 6 : 2; ihdr[10] = 0; ihdr[11] = 0; ihdr[12] = 0;
+    chunk("IHDR", ihdr);
+    chunk("IDAT", z);
+    chunk("IEND", {});
+}
+
+// Display::present (display.cu:265-303) of the last frame: FXAA + blend + RGB8 readback (display.hip)
+void display_frame(sng_ctx* c, uint8_t* out, uint64_t cap) {
+    const int W = c->mesh_res[0], H = c->mesh_res[1], OW = c->win[0], OH = c->win[1];
+    if (W <= 0 || OW <= 0 || !c->final_rgba.p) throw SngError(SNG_ERR_STATE, "render a frame first");
+    const size_t n = (size_t)OW * OH * 3;
+    if (out && cap < n) throw SngError(SNG_ERR_INVALID, "display buffer too small");
+    c->display_rgb.ensure(n);
+    launch_display(c->final_rgba.as<float4>(), W, H, OW, OH, c->clear_color, c->display_rgb.as<uint8_t>(), c->s_nerf);
+    HIPCHK(hipGetLastError());
+    if (out) HIPCHK(hipMemcpyAsync(out, c->display_rgb.p, n, hipMemcpyDeviceToHost, c->s_nerf));
+    HIPCHK(hipStreamSynchronize(c->s_nerf));
+}
+
+int sng_image_write_png(const char* path, const uint8_t* pixels, int32_t width, int32_t height, int32_t channels) {
+    return guarded([&] {
+        if (!path || !pixels) throw SngError(SNG_ERR_INVALID, "null argument");
+        write_png(path, pixels, width, height, channels);
+    });
+}
+int sng_display_frame(sng_ctx* c, uint8_t* rgb_out, uint64_t capacity) {
+    return guarded([&] { HIPCHK(hipSetDevice(c->device)); display_frame(c, rgb_out, capacity); });
+}
+int sng_save_image(sng_ctx* c, const char* folder, int32_t* written) {
+    return guarded([&] {
+        HIPCHK(hipSetDevice(c->device));
+        if (written) *written = 0;
+        if (c->img_count > c->img_count_max) return;   // Display::save_image (display.cu:305-306)
+        const std::string dir = folder && *folder ? std::string(folder) : c->out_folder;
+        if (dir.empty()) throw SngError(SNG_ERR_INVALID, "no output folder");
+        std::vector<uint8_t> rgb((size_t)c->win[0] * c->win[1] * 3);
+        display_frame(c, rgb.data(), rgb.size());
+        char name[32];
+        std::snprintf(name, sizeof(name), "/output-%03d.png", ++c->img_count);
+        write_png(dir + name, rgb.data(), c->win[0], c->win[1], 3);
+        if (written) *written = 1;
+    });
+}
+int sng_animation_probe(const char* scene_json, uint32_t n_frames, int32_t playing, float animation_speed, float* cameras, float* light_pos,
+                        uint32_t light_cap, float* object_pos, uint32_t object_cap, uint32_t* n_lights, uint32_t* n_objects) {
+    return guarded([&] {
+        if (!scene_json) throw SngError(SNG_ERR_INVALID, "null path");
+        std::unique_ptr<sng_ctx> c(new sng_ctx());   // host state only: no device calls below
+        c->params = default_params();
+        load_scene(c.get(), scene_json);
+        if (playing >= 0) c->campath.playing = playing != 0 && c->campath.keys.size() >= 2;
+        if (animation_speed >= 0.0f) { c->anim_speed = animation_speed; c->animations = animation_speed > 0.0f; }
+        const uint32_t nl = (uint32_t)c->lights.size(), no = (uint32_t)c->objs.size();
+        if (n_lights) *n_lights = nl;
+        if (n_objects) *n_objects = no;
+        for (uint32_t f = 0; f < n_frames; ++f) {
+            animate(c.get());
+            if (cameras) std::memcpy(cameras + 12 * (size_t)f, c->cam, 12 * sizeof(float));
+            if (light_pos && nl <= light_cap)
+                for (uint32_t i = 0; i < nl; ++i) std::memcpy(light_pos + 3 * ((size_t)f * nl + i), c->lights[i].pos, 3 * sizeof(float));
+            if (object_pos && no <= object_cap)
+                for (uint32_t i = 0; i < no; ++i) {
+                    float* q = object_pos + 3 * ((size_t)f * no + i);
+                    q[0] = c->objs[i].pos.x; q[1] = c->objs[i].pos.y; q[2] = c->objs[i].pos.z;
+                }
+        }
+        c->objs.clear();
+    });
 }
 int sng_render_frame(sng_ctx* c, const sng_frame_params* p, sng_frame_result* out) {
     return guarded([&] { HIPCHK(hipSetDevice(c->device)); render_frame(c, p, out); });

@@ -199,6 +199,8 @@ void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st,
 void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, hipStream_t s);
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
                      hipStream_t s);
+// display.hip
+void launch_display(const float4* img, int W, int H, int OW, int OH, f3 clear, uint8_t* out, hipStream_t s);
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
                     const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s);
 void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s);
