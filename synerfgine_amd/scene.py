@@ -62,6 +62,9 @@ def make_engine(config="c3", device_id=0, width=None, height=None, overrides=Non
         tb.set_density_grid(grid)
     eng = Engine(tb)
     eng.set_virtual_world(os.path.join(SCENES, cfg["scene"]))
+    # the workloads render a fixed camera (the scene's initial view): kitchen-rocks.json's move_on_start
+    # would otherwise advance its camera path on every frame (set camera_path_playing=1 to play it)
+    eng.set_param("camera_path_playing", 0)
     for k, v in {**cfg["overrides"], **(overrides or {})}.items():
         eng.set_param(k, v)
     eng.init(width or cfg["width"], height or cfg["height"])

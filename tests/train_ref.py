@@ -132,7 +132,7 @@ def ray_loss_grad(out16, dt, target, bg, n_rays, loss_scale=128.0, eps=1e-4):
     acc = torch.zeros(3, dtype=torch.float64)
     cn = 0
     for j in range(o.shape[0]):
-        if float(T) < eps:
+        if float(T.detach()) < eps:
             break
         acc = acc + alpha[j] * T * rgb[j]
         T = T * (1.0 - alpha[j])
