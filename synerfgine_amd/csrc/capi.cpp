@@ -366,6 +366,8 @@ const std::map<std::string, double>& default_params() {
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"rt_staged", 0},                       // ... plus primary / shade / bounce stages over compacted queues
+        {"rt_defer_shade", 0},                  // ... and the light loop of every hit in its own kernel, off the path chain (exact;
+                                                //   3 % shorter thin-band chains, 6 % slower full frames: off)
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
         {"bvh_flat", 1},                        // BvhWide walk keeping the nearer child in a register (exact)
         {"rt_tile", 8},                         // path-kernel tile edge: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
@@ -1223,6 +1225,11 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             q.nls = (uint32_t)c->lights.size() * ra.shadow_iters;
             q.nps = n_point * ra.shadow_iters;
             q.rec_stride = 2 + (3 * q.nls + 3) / 4;
+            // deferred shading inputs after the light colours (not in staged mode, which shades per stage)
+            if (c->p("rt_defer_shade") != 0.0 && c->p("rt_staged") == 0.0) {
+                q.shade_in = q.rec_stride;
+                q.rec_stride += 5;
+            }
             const uint64_t bytes = cap * (16ull * q.rec_stride + 32ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
             const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
                                    bytes <= (uint64_t)(c->p("rt_queue_gb") * 1073741824.0);

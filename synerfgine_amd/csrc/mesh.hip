@@ -484,6 +484,18 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                 prev_rec = (int)k;
             }
             uint32_t jl = 0, jp = 0;
+            if (DEFER && q.shade_in) {
+                // shading off the chain: keep what rt_shade_records_kernel needs and skip the light
+                // samples' draws (3 per light and shadow iteration) -- same RNG position afterwards
+                float4* si = q.rec + (size_t)k * q.rec_stride + q.shade_in;
+                si[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, 0.0f);
+                si[1] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.0f);
+                si[2] = make_float4(rd.x, rd.y, rd.z, 0.0f);
+                si[3] = make_float4(__uint_as_float(r.v0), __uint_as_float(r.v1), __uint_as_float(r.v2), __uint_as_float(r.v3));
+                si[4] = make_float4(__uint_as_float(r.v4), __uint_as_float(r.d), 0.0f, 0.0f);
+                const uint32_t n_draws = 3u * (uint32_t)a.n_lights * a.shadow_iters;
+                for (uint32_t j = 0; j < n_draws; ++j) (void)xorwow_next(r);
+            } else
             for (int l = 0; l < a.n_lights; ++l) {
                 const LightGpu L = a.lights[l];
                 for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
@@ -788,6 +800,42 @@ __global__ __launch_bounds__(512) void rt_bounce_kernel(RaytraceArgs a, RtStage 
     }
 }
 
+// shade_object's light loop (raytracer.cu:24-50) for every hit record of the frame, off the path
+// chain: the light samples are redrawn from the XORWOW state the path kernel saved, so lc and the
+// shadow rays are bit-identical to computing them inline.
+__global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, RtQueue q) {
+    const uint32_t n = *q.count;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        float4* rk = q.rec + (size_t)k * q.rec_stride;
+        const float4* si = rk + q.shade_in;
+        const float4 s0 = si[0], s1 = si[1], s2 = si[2], s3 = si[3], s4 = si[4];
+        const f3 pos = mk(s0.x, s0.y, s0.z), normal = mk(s1.x, s1.y, s1.z), rd = mk(s2.x, s2.y, s2.z);
+        Xorwow r{__float_as_uint(s3.x), __float_as_uint(s3.y), __float_as_uint(s3.z), __float_as_uint(s3.w), __float_as_uint(s4.x), __float_as_uint(s4.y)};
+        const MaterialGpu m = a.mats[__float_as_int(rk[0].z)];
+        float* lc_out = reinterpret_cast<float*>(rk + 2);
+        uint32_t jl = 0, jp = 0;
+        for (int l = 0; l < a.n_lights; ++l) {
+            const LightGpu L = a.lights[l];
+            for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
+                const f3 lpos = light_sample(L, r);
+                f3 Lv = lpos - pos;
+                const float full_dist = length(Lv);
+                Lv = normalize(Lv);
+                const f3 R = reflect(Lv, normal);
+                const f3 V = normalize(-rd);
+                const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
+                if (L.type == 0) {
+                    float4* sr = q.srec + 2 * ((size_t)k * q.nps + jp);
+                    sr[0] = make_float4(pos.x, pos.y, pos.z, full_dist);
+                    sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
+                    ++jp;
+                }
+            }
+        }
+    }
+}
+
 // Shadow rays of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
@@ -976,11 +1024,13 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
         allow_lds(raytrace_kernel<true, true>, lp);
         allow_lds(shadow_rays_kernel<true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
+        if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
         hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
     } else {
         allow_lds(raytrace_kernel<true, false>, lp);
         allow_lds(shadow_rays_kernel<false>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
+        if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
         hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
     }
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);

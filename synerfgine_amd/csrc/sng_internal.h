@@ -165,6 +165,9 @@ struct RtQueue {
     uint32_t nls;         // n_lights * shadow_iters
     uint32_t nps;         // n_point_lights * shadow_iters
     uint32_t cap;
+    uint32_t shade_in;    // > 0: float4 offset of the deferred-shading inputs {pos} {normal} {rd} {rng v0-v3} {rng v4, d}
+                          // in each record; raytrace_kernel skips the light samples' draws and
+                          // rt_shade_records_kernel computes lc + shadow rays off the path chain
 };
 
 // nerf.hip

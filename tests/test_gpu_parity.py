@@ -236,7 +236,7 @@ def test_errors_are_loud(tb):
 
 
 @pytest.mark.parametrize("overrides", [{}, {"path_trace_depth": 3, "light_samples": 3}, {"fast_slab": 0}, {"scene_lds": 0}, {"rt_staged": 1},
-                                       {"rt_staged": 1, "path_trace_depth": 3, "light_samples": 3}, {"rt_staged": 1, "scene_lds": 0}])
+                                       {"rt_staged": 1, "path_trace_depth": 3, "light_samples": 3}, {"rt_staged": 1, "scene_lds": 0}, {"rt_defer_shade": 1}])
 def test_wavefront_raytracer_equals_megakernel(overrides):
     """Deferred shadow-ray queues (rt_wavefront=1) and the staged tracer (rt_staged=1) reproduce the one-kernel
     path tracer bit for bit."""
