@@ -24,6 +24,11 @@ OUT = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out", "le
 HOLD = 20
 
 imgs, xf, focal, pp = nerf_data.load_nerf_synthetic(os.path.join(REPO, "data", "nerf", "lego400"))
+if os.environ.get("FOCAL_FROM_ANGLE"):
+    # transforms.json carries fl_x = 1000 (@800 px) beside camera_angle_x = 0.6911 (-> 1111 px, the
+    # Blender render's focal); ngp's read_focal_length (nerf_loader.cu:243-270) prefers fl_x
+    angle = json.load(open(os.path.join(REPO, "data", "nerf", "lego400", "transforms.json")))["camera_angle_x"]
+    focal[:] = 0.5 * imgs.shape[2] / math.tan(0.5 * angle)
 n = len(imgs)
 test = list(range(0, n, HOLD))
 train = [i for i in range(n) if i not in test]
