@@ -375,13 +375,16 @@ const std::map<std::string, double>& default_params() {
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)
-        {"rt_queue_gb", 48},
+        {"rt_spec", 0},                         // sample-parallel path kernel (exact; mesh.hip raytrace_spec_kernel): 1 on, 0 off,
+                                                //   -1 for bands of < 25 % of the rows
+        {"rt_queue_gb", 48},                    // device-memory budget for the deferred-shadow queues
         {"train_batch", 262144},                // m_training_batch_size (testbed.h:1103)
-        {"train_random_bg", 1},
-        {"train_debug", 0},                     // parity hook: generate writes per-ray step counts (sng_train_debug)                 // m_nerf.training.random_bg_color (testbed.h:790)                    // device-memory budget for the deferred-shadow queues
+        {"train_random_bg", 1},                 // m_nerf.training.random_bg_color (testbed.h:790)
+        {"train_debug", 0},                     // parity hook: generate writes per-ray step counts (sng_train_debug)
         {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
         {"nerf_fused_after", 1},                // ... after this many whole-GPU wavefront iterations (1: the one big
                                                 //   uncontended network launch, then the ray-local tail; measured best)
+        {"nerf_fused_lanes", 64},               // rays per wave in the fused kernel
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
     };
     return d;
@@ -449,6 +452,7 @@ struct sng_ctx {
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
     DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
+    DevBuf rt_hint;                        // sample-parallel path kernel: per-pixel hit-depth sums of the previous frame (u8)
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf rt_hits, rt_rays, rt_next_pos, rt_tail, rt_counters;   // staged path tracer
     bool fused_last = false;               // the last trace finished in the fused kernel
@@ -1082,6 +1086,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             fa.wfrag = c->net.wfrag; fa.grid_params = c->net.grid; fa.levels = c->net.levels;
             fa.frame_rgba = c->nerf_rgba.as<float4>(); fa.frame_depth = c->nerf_depth.as<float>(); fa.positions = c->nerf_pos.as<float>();
             fa.work = c->fused_work.as<uint32_t>();
+            fa.lanes = (uint32_t)std::min(64.0, std::max(1.0, c->p("nerf_fused_lanes")));
             // concurrent frames: the tail runs beside the raytracer on the CUs its grids leave free
             double fb = c->p("nerf_fused_blocks");
             if (fb < 0) fb = (c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0) ? 2.0 * std::max(1.0, c->p("rt_reserved_cus")) : 0.0;
@@ -1202,7 +1207,12 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             ra.persistent_blocks = (uint32_t)std::max(1, c->n_cus - std::max(0, reserve));
             c->rt_work.ensure(16);
             ra.work = c->rt_work.as<uint32_t>();
-            ra.tile = (c->p("rt_tile") == 4.0 && c->p("rt_staged") == 0.0) ? 4 : 8;   // the staged kernels walk 8x8 tiles
+            // sample-parallel path kernel: 2..64 samples, <= 2 bounces, its own 8x8 tile pieces, not with the
+            // staged or deferred-shading variants
+            const double rs = c->p("rt_spec");
+            const bool spec = (rs > 0 || (rs < 0 && (y1 - y0) * 4 < MH)) && ra.samples >= 2 && ra.samples <= 64 && ra.bounces <= 2 &&
+                              c->p("rt_staged") == 0.0 && c->p("rt_defer_shade") == 0.0;
+            ra.tile = (c->p("rt_tile") == 4.0 && c->p("rt_staged") == 0.0 && !spec) ? 4 : 8;   // the staged and spec kernels walk 8x8 tiles
             if (c->p("rt_tile_order") != 0.0) {
                 const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile - 1) / ra.tile);
                 const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60);
@@ -1250,6 +1260,15 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                     RtStage st{c->rt_hits.as<float4>(), c->rt_rays.as<float4>(), nullptr, c->rt_next_pos.as<float4>(), q.head, c->rt_tail.as<int>()};
                     launch_raytrace_staged(ra, q, st, c->rt_counters.as<uint32_t>(), c->mesh_o.as<float4>(), c->mesh_d.as<float4>(),
                                            c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), c->s_rt);
+                } else if (spec) {
+                    if (c->rt_hint.bytes < (uint64_t)MW * MH) {
+                        c->rt_hint.ensure((uint64_t)MW * MH);
+                        HIPCHK(hipMemsetAsync(c->rt_hint.p, 0, c->rt_hint.bytes, c->s_rt));
+                    }
+                    ra.spec_group = 1;
+                    while ((uint32_t)ra.spec_group < ra.samples) ra.spec_group <<= 1;
+                    launch_raytrace_spec(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
+                                         c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), c->rt_hint.as<uint8_t>(), c->s_rt);
                 } else {
                     launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
                                               c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), (uint32_t)c->n_cus * 16, c->s_rt);

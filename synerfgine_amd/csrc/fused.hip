@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     while (true) {
         // ---- refill empty lanes from the ray queue (one atomic per wave)
         {
-            const unsigned long long need = __ballot(!has);
+            const unsigned long long need = __ballot(!has && (uint32_t)lane < a.lanes);
             if (need) {
                 const int leader = __ffsll((long long)need) - 1;
                 uint32_t base = 0;
@@ -271,7 +271,7 @@ __global__ void fused_prepare_kernel(MarchCtrl* ctrl, uint32_t* work) {
 
 void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s) {
     hipLaunchKernelGGL(fused_prepare_kernel, dim3(1), dim3(64), 0, s, a.ctrl, a.work);
-    const uint32_t waves_needed = (n_rays_hint + 63) / 64;
+    const uint32_t waves_needed = (n_rays_hint + a.lanes - 1) / a.lanes;
     const uint32_t cap = max_blocks ? max_blocks : (uint32_t)net.n_cus * 2;
     const uint32_t blocks = std::max(1u, std::min((waves_needed + FUSED_WAVES - 1) / FUSED_WAVES, cap));
     const bool lin = a.vol.linear != 0;

@@ -606,6 +606,209 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
 }
 
 // ===========================================================================================
+// Sample-parallel path tracer (rt_spec): raytrace_pixel<DEFER = true>'s records, shadow rays,
+// depth and final XORWOW state, bit for bit, with a pixel's samples on separate lanes instead of
+// one lane's serial chain.
+//
+// Sample s of a pixel starts at XORWOW offset off_s = sum_{j<s} d_j, where d_j = Dl + h_j * H is
+// sample j's draw count (Dl = 1 or 2 lens draws; H = 3 * n_lights * shadow_iters light draws + 2
+// scatter draws per bounce that hits; h_j = bounces hit before the first miss).  Every lane traces
+// its sample from a guessed offset (the pixel's mean hit depth of the previous frame), then the
+// offsets are re-formed by an exclusive scan of the d's and lanes whose offset changed trace again.
+// The fixed point is the serial sequence: after round r the first r offsets are final, so it ends
+// within `samples` + 1 rounds, and in practice in 2-3 (primary hits are nearly deterministic per
+// pixel; only the bounce hits vary).  A pixel's chain becomes (rounds x one sample) instead of
+// (samples x one sample).  Each lane keeps, per hit bounce, what shade_object needs (position,
+// normal, incoming direction, material, pdf, att and the XORWOW state before the light draws); the
+// converged lanes then write their hit records in (sample, bounce) order into one contiguous block
+// per pixel and draw the light samples from the saved states -- off any chain.
+// ===========================================================================================
+constexpr int SPEC_MAXB = 2;   // bounces kept per lane (path_trace_depth <= 2)
+#ifndef SPEC_WAVES_PER_EU
+#define SPEC_WAVES_PER_EU 2         // ~230 VGPRs without spills: one 512-thread workgroup per CU
+#endif
+
+struct SpecBounce {
+    Xorwow r;      // state before this bounce's light draws
+    f3 pos, normal, rd;
+    int mat;
+    float pdf, att;
+};
+
+__device__ __forceinline__ void xorwow_skip(Xorwow& r, uint32_t n) {
+#pragma unroll 1
+    for (uint32_t j = 0; j < n; ++j) (void)xorwow_next(r);
+}
+
+// One sample of raytrace_pixel's loop from XORWOW offset `off`: returns hit depth, fills the hit
+// bounces, the first-bounce position and the state after the sample's last draw.
+template <bool LDS>
+__device__ __forceinline__ uint32_t spec_sample(const RaytraceArgs& a, const TraceCtx<LDS>& cx, const Xorwow& base, uint32_t off, f3 src_p, f3 src_d,
+                                                uint32_t n_light_draws, SpecBounce (&bh)[SPEC_MAXB], f3& p0, Xorwow& r_end) {
+    Xorwow r = base;
+    xorwow_skip(r, off);
+    const float longi = curand_uniform(r) * a.lens;
+    const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+    f3 rp = src_p, rd = cone_random_up(src_d, a.up, longi, latid);
+    float pdf = 1.0f / (float)a.bounces, att = 1.0f;
+    uint32_t nh = 0;
+#pragma unroll
+    for (int b = 0; b < SPEC_MAXB; ++b) {
+        if ((uint32_t)b >= a.bounces) break;
+        Hit h;
+        const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h);
+        if (b == 0) p0 = h.pos;
+        if (hit_obj < 0) break;
+        bh[b].r = r;
+        bh[b].pos = h.pos; bh[b].normal = h.normal; bh[b].rd = rd;
+        bh[b].mat = h.mat; bh[b].pdf = pdf; bh[b].att = att;
+        xorwow_skip(r, n_light_draws);
+        // Material::scatter (material.cuh:112-123)
+        const MaterialGpu m = a.mats[h.mat];
+        const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
+        const float lo = curand_uniform(r) * spec;
+        const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+        const f3 ndir = cone_random_frame(h.normal, h.perturb, lo, la);
+        rp = h.pos;
+        rd = ndir;
+        pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
+        att = 1.0f * m.rg;
+        ++nh;
+    }
+    r_end = r;
+    return nh;
+}
+
+// segmented (width SG) inclusive sum over the wave
+__device__ __forceinline__ uint32_t seg_incl_scan(uint32_t v, int s, int SG) {
+    for (int o = 1; o < SG; o <<= 1) {
+        const uint32_t u = __shfl_up(v, (unsigned)o, SG);
+        if (s >= o) v += u;
+    }
+    return v;
+}
+
+// lanes: SG = a.spec_group lanes per pixel (power of two >= samples), 64 / SG pixels per wave; a
+// wave takes one 64/SG-pixel row piece of an 8x8 tile (tiles in the previous frame's cost order).
+template <bool LDS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SPEC_WAVES_PER_EU))) void raytrace_spec_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work,
+                                                             const float4* __restrict__ origins, const float4* __restrict__ dirs,
+                                                             uint32_t* __restrict__ rng, uint32_t n_rng, float* __restrict__ acc_depth,
+                                                             uint8_t* __restrict__ hint) {
+    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    const int lane = threadIdx.x & 63;
+    const int SG = a.spec_group, PPW = 64 / SG;
+    const int s = lane & (SG - 1), pw = lane / SG;
+    const uint32_t rows = (uint32_t)(a.row1 - a.row0);
+    const uint32_t tiles_x = ((uint32_t)a.W + 7u) / 8u, n_tiles = tiles_x * ((rows + 7u) / 8u);
+    const uint32_t units_per_tile = 64u / (uint32_t)PPW, n_units = n_tiles * units_per_tile;
+    const uint32_t n_light_draws = 3u * (uint32_t)a.n_lights * a.shadow_iters;
+    const uint32_t Dl = a.lens != 0.0f ? 1u : 2u, H = n_light_draws + 2u;
+    while (true) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(work, 1u);
+        k = __shfl(k, 0, 64);
+        if (k >= n_units) break;
+        const uint32_t tile = a.tile_order ? a.tile_order[k / units_per_tile] : k / units_per_tile;
+        const uint64_t t0 = wall_clock64();
+        const uint32_t j = (k % units_per_tile) * (uint32_t)PPW + (uint32_t)pw;   // pixel within the tile
+        const uint32_t x = (tile % tiles_x) * 8u + j % 8u, y = (tile / tiles_x) * 8u + j / 8u;
+        const bool px_ok = x < (uint32_t)a.W && y < rows;
+        const bool active = px_ok && (uint32_t)s < a.samples;
+        const size_t i = (size_t)a.row0 * a.W + (px_ok ? y * (uint32_t)a.W + x : 0u);
+
+        Xorwow base{0, 0, 0, 0, 0, 0};
+        f3 src_p = splat(0.0f), src_d = splat(0.0f);
+        uint32_t off = 0, d = 0, nh = 0;
+        if (px_ok) {
+            base = load_rng(rng, n_rng, i);
+            const float4 o4 = origins[i], d4 = dirs[i];
+            src_p = mk(o4.x, o4.y, o4.z);
+            src_d = mk(d4.x, d4.y, d4.z);
+            // guess: every sample hits as deep as this pixel's samples did on average last frame
+            const uint32_t g = ((uint32_t)hint[i] * 2u + a.samples) / (2u * a.samples);
+            off = (uint32_t)s * (Dl + min(g, a.bounces) * H);
+        }
+        SpecBounce bh[SPEC_MAXB];
+        f3 p0 = splat(0.0f);
+        Xorwow r_end = base;
+        bool need = active;
+        while (__ballot(need)) {
+            if (need) {
+                nh = spec_sample<LDS>(a, cx, base, off, src_p, src_d, n_light_draws, bh, p0, r_end);
+                d = Dl + nh * H;
+            }
+            const uint32_t incl = seg_incl_scan(active ? d : 0u, s, SG);
+            const uint32_t noff = incl - (active ? d : 0u);
+            need = active && noff != off;
+            off = noff;
+        }
+
+        // ---- hit records: lanes are pixel-major, sample-minor, so one wave-wide scan of the lanes'
+        // record counts lays out each pixel's records contiguously in (sample, bounce) order
+        const uint32_t my = active ? nh : 0u;
+        const uint32_t wincl = seg_incl_scan(my, lane, 64);
+        const uint32_t wexcl = wincl - my;
+        const uint32_t all = __shfl(wincl, 63, 64);
+        const uint32_t px_first = __shfl(wexcl, pw * SG, 64);
+        const uint32_t px_total = __shfl(wincl, pw * SG + SG - 1, 64) - px_first;
+        uint32_t wbase = 0;
+        if (lane == 0 && all) wbase = atomicAdd(q.count, all);
+        wbase = __shfl(wbase, 0, 64);
+        if (px_ok && s == 0) q.head[i] = px_total ? (int)(wbase + px_first) : -1;
+        if (active) {
+#pragma unroll
+            for (int b = 0; b < SPEC_MAXB; ++b) {
+                if ((uint32_t)b >= nh) break;
+                const uint32_t kr = wbase + wexcl + (uint32_t)b;
+                const bool last = wexcl + (uint32_t)b + 1u == px_first + px_total;
+                float4* rk = q.rec + (size_t)kr * q.rec_stride;
+                const SpecBounce& hb = bh[b];
+                rk[0] = make_float4(__int_as_float(last ? -1 : (int)kr + 1), __uint_as_float((uint32_t)s), __int_as_float(hb.mat), 0.0f);
+                rk[1] = make_float4(hb.pdf, hb.att, 0.0f, 0.0f);
+                float* lc_out = reinterpret_cast<float*>(rk + 2);
+                const MaterialGpu m = a.mats[hb.mat];
+                Xorwow r = hb.r;
+                uint32_t jl = 0, jp = 0;
+                for (int l = 0; l < a.n_lights; ++l) {
+                    const LightGpu L = a.lights[l];
+                    for (uint32_t si = 0; si < a.shadow_iters; ++si, ++jl) {
+                        const f3 lpos = light_sample(L, r);
+                        f3 Lv = lpos - hb.pos;
+                        const float full_dist = length(Lv);
+                        Lv = normalize(Lv);
+                        const f3 R = reflect(Lv, hb.normal);
+                        const f3 V = normalize(-hb.rd);
+                        const f3 lc = fmaxf(0.0f, dot(Lv, hb.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                        lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
+                        if (L.type == 0) {
+                            float4* sr = q.srec + 2 * ((size_t)kr * q.nps + jp);
+                            sr[0] = make_float4(hb.pos.x, hb.pos.y, hb.pos.z, full_dist);
+                            sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
+                            ++jp;
+                        }
+                    }
+                }
+            }
+        }
+        // ---- depth from the first-bounce positions summed in sample order; final XORWOW state
+        f3 next_pos = splat(0.0f);
+        for (uint32_t jj = 0; jj < a.samples; ++jj) {
+            const int src = pw * SG + (int)jj;
+            const f3 v = mk(__shfl(p0.x, src, 64), __shfl(p0.y, src, 64), __shfl(p0.z, src, 64));
+            next_pos = next_pos + v;
+        }
+        if (px_ok && s == 0) {
+            next_pos = next_pos / (float)a.samples;
+            acc_depth[i] = dot(src_d, next_pos - src_p);
+            hint[i] = (uint8_t)min(px_total, 255u);
+        }
+        if (active && (uint32_t)s == a.samples - 1u) store_rng(rng, n_rng, i, r_end);
+        if (a.tile_cost && lane == 0) atomicMax(&a.tile_cost[tile], (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull));
+    }
+}
+
+// ===========================================================================================
 // Staged path tracer (rt_mode 2): the same per-pixel path and RNG sequence as raytrace_pixel,
 // split into dense stages per sample -- primary traversal over all pixels, then for every
 // bounce: shade (light samples -> hit records + shadow queue, scatter) over the compacted hits
@@ -1031,6 +1234,37 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
         allow_lds(shadow_rays_kernel<false>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
         if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
+        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
+    }
+    hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
+}
+
+// sample-parallel mode: raytrace_spec_kernel replaces the path kernel; shadow and accumulate kernels
+// as in launch_raytrace_wavefront.  `hint`: per-pixel hit depth sums of the previous frame (u8).
+void launch_raytrace_spec(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
+                          float* accd, uint8_t* hint, hipStream_t s) {
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (!n) return;
+    (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);
+    (void)hipMemsetAsync(a.work, 0, 2 * sizeof(uint32_t), s);
+    const uint32_t tiles_x = ((uint32_t)a.W + 7u) / 8u, n_tiles = tiles_x * (((uint32_t)(a.row1 - a.row0) + 7u) / 8u);
+    if (a.tile_cost) (void)hipMemsetAsync(a.tile_cost, 0, (size_t)n_tiles * 4, s);   // atomicMax over a tile's row pieces
+    const uint32_t n_units = n_tiles * (uint32_t)a.spec_group;   // 64 / (64 / SG) pieces per tile
+    const uint32_t tp = 512, ts = 512;
+    const bool lds = a.scene_in_lds != 0;
+    const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
+    // one 512-thread workgroup per CU (2 waves/SIMD at ~230 VGPRs): a larger grid would spill onto the
+    // CUs left to the NeRF stream
+    const uint32_t bp = std::min((n_units + tp / 64 - 1) / (tp / 64), a.persistent_blocks * (SPEC_WAVES_PER_EU / 2u));
+    if (lds) {
+        allow_lds(raytrace_spec_kernel<true>, lp);
+        allow_lds(shadow_rays_kernel<true>, ls);
+        hipLaunchKernelGGL(raytrace_spec_kernel<true>, dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd, hint);
+        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
+    } else {
+        allow_lds(raytrace_spec_kernel<false>, lp);
+        allow_lds(shadow_rays_kernel<false>, ls);
+        hipLaunchKernelGGL(raytrace_spec_kernel<false>, dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd, hint);
         hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
     }
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);

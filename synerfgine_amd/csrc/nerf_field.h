@@ -121,8 +121,16 @@ __device__ __forceinline__ void sh_lane(int g, float dx, float dy, float dz, flo
 
 // One 16-sample tile: lane (g = lane>>4, col = lane&15) holds sample `col`'s coordinates; returns
 // the rgb accumulator rows 4g..4g+3 (o) and density rows 4g..4g+3 (dens) of that sample.
-template <int F>
-__device__ __forceinline__ void field_tile(const h8* W, const LevelInfo* __restrict__ levels, const _Float16* __restrict__ grid, int g, float x0,
+// Weights in LDS instead of VGPRs: W[f] reads this lane's 16-B slice of fragment f (20 KiB per
+// workgroup, conflict-free ds_read_b128), freeing 80 VGPRs per lane (nerf_network_kernel)
+struct LdsWeights {
+    const h8* base;   // LDS, [20][64]
+    int lane;
+    __device__ __forceinline__ h8 operator[](int f) const { return base[f * 64 + lane]; }
+};
+
+template <int F, typename WT = const h8*>
+__device__ __forceinline__ void field_tile(WT W, const LevelInfo* __restrict__ levels, const _Float16* __restrict__ grid, int g, float x0,
                                            float x1, float x2, float d0, float d1, float d2, f4v& o, f4v& dens) {
     const f4v zero = {0.0f, 0.0f, 0.0f, 0.0f};
     // ---- hash grid encoding -> B fragment of layer 0

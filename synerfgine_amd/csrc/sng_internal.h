@@ -110,6 +110,7 @@ struct FusedArgs {
     float* positions;
     uint32_t* work;               // ray-queue cursor (zeroed by the launcher)
     int p;                        // ping-pong buffer holding the alive rays (MarchCtrl::n_alive[p], i_step[p])
+    uint32_t lanes;               // rays per wave (64; fewer shorten a wave's per-iteration field chain for thin bands)
 };
 void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s);
 
@@ -149,6 +150,7 @@ struct RaytraceArgs {
     uint32_t* tile_cost;        // per-tile cycles of this frame (nullptr: not recorded)
     int bvh_flat;               // BvhWide traversal with the nearer child in a register (bvh_walk_near)
     int tile;                   // path-kernel tile edge in pixels (8: 64 lanes, 4: 16 lanes per wave)
+    int spec_group;             // > 0: sample-parallel path kernel (raytrace_spec_kernel), lanes per pixel
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
@@ -187,6 +189,8 @@ void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 fo
                       hipStream_t s);
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
                                float* accd, uint32_t shadow_blocks, hipStream_t s);
+void launch_raytrace_spec(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
+                          float* accd, uint8_t* hint, hipStream_t s);
 // staged path tracer buffers (mesh.hip, rt_staged): hit / ray queues of one stage (3 float4 per entry,
 // capacity = band pixels) and per-pixel state carried across stages
 struct RtStage {

@@ -262,6 +262,35 @@ def test_wavefront_raytracer_equals_megakernel(overrides):
         tb.close()
 
 
+@pytest.mark.parametrize("config,overrides,rows", [("c3", {}, None), ("c3", {}, (40, 71)), ("c3", {"light_samples": 3}, None),
+                                                    ("c3", {"path_trace_depth": 1}, None), ("c3", {"scene_lds": 0, "light_samples": 16}, None),
+                                                    ("c4", {}, None), ("c4", {}, (20, 52))])
+def test_sample_parallel_raytracer_equals_path_kernel(config, overrides, rows):
+    """The sample-parallel path kernel (rt_spec=1: a pixel's samples on separate lanes from guessed
+    XORWOW offsets, re-traced until the offsets are the serial ones) reproduces the serial path kernel
+    bit for bit -- colours, depths and the XORWOW states it leaves -- over three frames (frames 2-3 start
+    from the previous frame's hit-depth guesses), full frames and bands, 3 / 8 / 16 samples, 1-2 bounces."""
+    tb, eng, _ = _engine(192, 108, overrides, config=config)
+    try:
+        m0, n0 = eng.rng_states(1).copy(), eng.rng_states(0).copy()
+        out = {}
+        for spec in (0, 1):
+            eng.set_rng_states(0, n0)
+            eng.set_rng_states(1, m0)
+            eng.set_param("rt_spec", spec)
+            frames = []
+            for _ in range(3):
+                r = eng.frame(rows=rows)
+                frames.append((r.download("syn_rgba"), r.download("syn_depth"), r.download("final_rgba"), eng.rng_states(1).copy()))
+            out[spec] = frames
+        for fa, fb in zip(out[0], out[1]):
+            for a, b in zip(fa, fb):
+                assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert (out[1][0][1] < 100).mean() > 0.02    # objects are in view
+    finally:
+        tb.close()
+
+
 @pytest.mark.parametrize("config,overrides", [("c3", {}), ("c3", {"scene_lds": 0}), ("c3", {"rt_wavefront": 0}), ("c4", {})])
 def test_wide_bvh_layout_equals_node_walk(config, overrides):
     """The BvhWide traversal layout (bvh_wide=1) reproduces the TriangleBvhNode walk bit for bit."""
