@@ -18,8 +18,12 @@ def short(n):
     return re.sub(r"\(.*", "", n).replace("void ", "").replace("sng::", "")
 
 
-def load(d, counter):
-    f = glob.glob(f"{d}/{counter}/**/*counter_collection.csv", recursive=True)
+N_SIMD = 256 * 4
+N_XCD = 8
+
+
+def load(d, counter, sub=None):
+    f = glob.glob(f"{d}/{sub or counter}/**/*counter_collection.csv", recursive=True)
     if not f:
         raise SystemExit(f"no counter_collection.csv for {counter}")
     per = defaultdict(list)
@@ -47,6 +51,18 @@ def main():
            "calibration_half_to_float": dict(kernels.get("half_to_float_kernel", {}), expected_read_bytes=2 * 128 ** 3,
                                              expected_write_bytes=4 * 128 ** 3),
            "kernels": kernels}
+    # optional third pass: MFMA counters (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_F16, GRBM_GUI_ACTIVE)
+    if glob.glob(f"{d}/MFMA/**/*counter_collection.csv", recursive=True) and net:
+        busy, mops, gui = (load(d, c, "MFMA").get(net[0], []) for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16", "GRBM_GUI_ACTIVE"))
+        avg = lambda v: sum(v) / len(v) if v else None
+        b, m, g = avg(busy), avg(mops), avg(gui)
+        res["mfma"] = {"launches": len(busy), "busy_cycles_avg": b, "mops_f16_avg": m, "flop_per_launch": m * 512 if m else None,
+                       "gui_active_cycles_avg": g, "n_simd": N_SIMD, "n_xcd": N_XCD,
+                       "kernel_cycles": g / N_XCD if g else None,
+                       "mfma_busy_frac": b / (g / N_XCD * N_SIMD) if b and g else None,
+                       "note": "GRBM_GUI_ACTIVE is the sum over the 8 XCDs (137 K cycles = the 57 us launch at 2.4 GHz); "
+                               "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES (16 per v_mfma_f32_16x16x32_f16, summed over SIMDs) / "
+                               "(kernel cycles x 1024 SIMDs); flop = MOPS_F16 x 512 (= samples x 20,480, SURVEY 8d)"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * max(1, kv[1]["launches"]))[:12]:
