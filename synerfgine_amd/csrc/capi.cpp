@@ -1205,7 +1205,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             // wavefront running beside them on the other stream (concurrent mode only)
             const int reserve = concurrent && show_nerf ? (int)c->p("rt_reserved_cus") : 0;
             ra.persistent_blocks = (uint32_t)std::max(1, c->n_cus - std::max(0, reserve));
-            c->rt_work.ensure(16);
+            c->rt_work.ensure(RT_WORK_WORDS * sizeof(uint32_t));
             ra.work = c->rt_work.as<uint32_t>();
             // sample-parallel path kernel: 2..64 samples, <= 2 bounces, its own 8x8 tile pieces, not with the
             // staged or deferred-shading variants

@@ -509,7 +509,7 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                     if (DEFER) {
                         lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                         if (L.type == 0) {
-                            float4* sr = q.srec + 2 * ((size_t)k * q.nps + jp);
+                            float4* sr = q.shadow_ray(k, jp);
                             sr[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, full_dist);
                             sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
                             ++jp;
@@ -782,7 +782,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SPEC_WAVES_
                         const f3 lc = fmaxf(0.0f, dot(Lv, hb.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                         lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                         if (L.type == 0) {
-                            float4* sr = q.srec + 2 * ((size_t)kr * q.nps + jp);
+                            float4* sr = q.shadow_ray(kr, jp);
                             sr[0] = make_float4(hb.pos.x, hb.pos.y, hb.pos.z, full_dist);
                             sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
                             ++jp;
@@ -942,7 +942,7 @@ __global__ __launch_bounds__(256) void rt_shade_kernel(RaytraceArgs a, RtQueue q
                     const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                     lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                     if (L.type == 0) {
-                        float4* sr = q.srec + 2 * ((size_t)k * q.nps + jp);
+                        float4* sr = q.shadow_ray(k, jp);
                         sr[0] = make_float4(hpos.x, hpos.y, hpos.z, full_dist);
                         sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
                         ++jp;
@@ -1029,7 +1029,7 @@ __global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, R
                 const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                 lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                 if (L.type == 0) {
-                    float4* sr = q.srec + 2 * ((size_t)k * q.nps + jp);
+                    float4* sr = q.shadow_ray(k, jp);
                     sr[0] = make_float4(pos.x, pos.y, pos.z, full_dist);
                     sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
                     ++jp;
@@ -1046,23 +1046,45 @@ __global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, R
 template <bool LDS>
 __global__ __launch_bounds__(512) void shadow_rays_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work) {
     const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
-    const uint32_t total = *q.count * q.nps;
+    const uint32_t n_rec = *q.count, total = n_rec * q.nps;
     const int lane = threadIdx.x & 63;
-    while (true) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(work, 64u);
-        base = __shfl(base, 0, 64);
-        if (base >= total) break;
-        const uint32_t j = base + (uint32_t)lane;
+    // 64-ray chunks handed out by SHADOW_NCTR counters in separate memory channels: chunk c belongs to
+    // counter c % NCTR, a wave starts on the counter of its workgroup's XCD slot and moves on when that
+    // one runs dry.  One shared counter serialised ~200 K same-address atomics per frame (2.0 ms on
+    // their own, measured with the tracing removed); static round-robin dealing has no atomics but
+    // unbalances the waves (2.8 ms), because the expensive rays cluster in the queue.
+    const uint32_t n_chunks = (total + 63u) / 64u;
+    uint32_t x = blockIdx.x % SHADOW_NCTR, tried = 0;
+    while (tried < SHADOW_NCTR) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(work + x * SHADOW_CTR_STRIDE, 1u);
+        k = __shfl(k, 0, 64);
+        const uint32_t c = k * SHADOW_NCTR + x;
+        if (c >= n_chunks) {
+            x = (x + 1u) % SHADOW_NCTR;
+            ++tried;
+            continue;
+        }
+        const uint32_t j = c * 64u + (uint32_t)lane;
         if (j >= total) continue;
-        const float4 s0 = q.srec[2 * (size_t)j], s1 = q.srec[2 * (size_t)j + 1];
+        const uint32_t kr = j / q.nps, jp = j - kr * q.nps;   // record, shadow sample (RtQueue::shadow_ray)
+        const float4* sr = q.shadow_ray(kr, jp);
+        const float4 s0 = sr[0], s1 = sr[1];
         const f3 pos = mk(s0.x, s0.y, s0.z), Lv = mk(s1.x, s1.y, s1.z);
         const float full_dist = s0.w;
         int oh = -1;
+#ifdef SHADOW_TIMING_NO_BVH   // timing-only builds (not exact): which half of a shadow ray costs what
+        const float syn = MAX_DEPTH;
+#else
         const float syn = depth_test_world(pos, Lv, a.objs, a.n_objs, cx, oh, full_dist);
+#endif
+#ifdef SHADOW_TIMING_NO_NERF
+        const float nerf = MAX_DEPTH;
+#else
         const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip);
+#endif
         const float sh = fminf(fminf(nerf, syn), full_dist);
-        q.mask[j] = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
+        q.mask[q.mask_at(kr, jp)] = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
     }
 }
 
@@ -1082,14 +1104,13 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
             const float4 h0 = rk[0], h1 = rk[1];
             if (__float_as_uint(h0.y) != spp) break;
             const float* lc = reinterpret_cast<const float*>(rk + 2);
-            const float* mk_ = q.mask + (size_t)k * q.nps;
             f3 color = splat(0.0f);
             uint32_t jl = 0, jp = 0;
             for (int l = 0; l < a.n_lights; ++l) {
                 const bool point = a.lights[l].type == 0;
                 for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
                     const f3 c = mk(lc[3 * jl], lc[3 * jl + 1], lc[3 * jl + 2]);
-                    if (point) color = color + c * mk_[jp++];
+                    if (point) color = color + c * q.mask[q.mask_at((uint32_t)k, jp++)];
                     else color = color + c;
                 }
             }
@@ -1204,7 +1225,7 @@ void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, ui
     if (!n) return;
     const uint32_t tpb = 256, blocks = std::min((n + tpb - 1) / tpb, a.persistent_blocks * 3);
     const size_t lds = trace_lds_bytes(a, false, tpb);
-    (void)hipMemsetAsync(a.work, 0, 2 * sizeof(uint32_t), s);
+    (void)hipMemsetAsync(a.work, 0, RT_WORK_WORDS * sizeof(uint32_t), s);
     allow_lds(raytrace_kernel<false, false>, lds);
     hipLaunchKernelGGL((raytrace_kernel<false, false>), dim3(blocks), dim3(tpb), lds, s, a, RtQueue{}, a.work, o, d, rng, n_rng, acc, accd);
 }
@@ -1213,7 +1234,7 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
     (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);   // errors surface through hipGetLastError in the caller
-    (void)hipMemsetAsync(a.work, 0, 2 * sizeof(uint32_t), s);
+    (void)hipMemsetAsync(a.work, 0, RT_WORK_WORDS * sizeof(uint32_t), s);
     // path kernel: capped at 128 VGPRs (amdgpu_waves_per_eu(4), a few spills) -> 4 waves/SIMD = 2 x 512-thread workgroups;
     // measured faster than 3 waves/SIMD without spills
     // shadow kernel: ~100 VGPRs -> 5 waves/SIMD; LDS-bound at 2 x 512-thread workgroups
@@ -1228,13 +1249,13 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
         allow_lds(shadow_rays_kernel<true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
         if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
-        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
+        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     } else {
         allow_lds(raytrace_kernel<true, false>, lp);
         allow_lds(shadow_rays_kernel<false>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
         if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
-        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
+        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     }
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
 }
@@ -1246,7 +1267,7 @@ void launch_raytrace_spec(const RaytraceArgs& a, const RtQueue& q, const float4*
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
     (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);
-    (void)hipMemsetAsync(a.work, 0, 2 * sizeof(uint32_t), s);
+    (void)hipMemsetAsync(a.work, 0, RT_WORK_WORDS * sizeof(uint32_t), s);
     const uint32_t tiles_x = ((uint32_t)a.W + 7u) / 8u, n_tiles = tiles_x * (((uint32_t)(a.row1 - a.row0) + 7u) / 8u);
     if (a.tile_cost) (void)hipMemsetAsync(a.tile_cost, 0, (size_t)n_tiles * 4, s);   // atomicMax over a tile's row pieces
     const uint32_t n_units = n_tiles * (uint32_t)a.spec_group;   // 64 / (64 / SG) pieces per tile
@@ -1260,12 +1281,12 @@ void launch_raytrace_spec(const RaytraceArgs& a, const RtQueue& q, const float4*
         allow_lds(raytrace_spec_kernel<true>, lp);
         allow_lds(shadow_rays_kernel<true>, ls);
         hipLaunchKernelGGL(raytrace_spec_kernel<true>, dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd, hint);
-        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
+        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     } else {
         allow_lds(raytrace_spec_kernel<false>, lp);
         allow_lds(shadow_rays_kernel<false>, ls);
         hipLaunchKernelGGL(raytrace_spec_kernel<false>, dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd, hint);
-        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + 1);
+        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     }
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
 }
@@ -1304,9 +1325,9 @@ void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st,
             }
         }
     }
-    (void)hipMemsetAsync(a.work + 1, 0, sizeof(uint32_t), s);
-    if (lds) hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + 1);
-    else hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + 1);
+    (void)hipMemsetAsync(a.work + SHADOW_CTR0, 0, (RT_WORK_WORDS - SHADOW_CTR0) * sizeof(uint32_t), s);
+    if (lds) hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + SHADOW_CTR0);
+    else hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + SHADOW_CTR0);
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, qq, acc, st.next_pos, o, d, accd);
 }
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,

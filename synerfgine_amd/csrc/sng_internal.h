@@ -128,6 +128,15 @@ struct ShadowArgs {
     const LightGpu* lights; int n_lights;
 };
 
+// raytracer work counters (RaytraceArgs::work): [0] path-kernel tiles, [SHADOW_CTR0 + x * SHADOW_CTR_STRIDE]
+// the shadow-ray chunk counters, one per memory channel (mesh.hip shadow_rays_kernel)
+#ifndef SHADOW_NCTR
+#define SHADOW_NCTR 8u
+#endif
+constexpr uint32_t SHADOW_CTR_STRIDE = 256;   // u32 (1 KiB) between counters
+constexpr uint32_t SHADOW_CTR0 = 256;
+constexpr uint32_t RT_WORK_WORDS = SHADOW_CTR0 + SHADOW_NCTR * SHADOW_CTR_STRIDE;
+
 struct RaytraceArgs {
     Volume vol;
     int W, row0, row1;
@@ -145,7 +154,7 @@ struct RaytraceArgs {
     int scene_in_lds;           // copy the blob into LDS per workgroup
     uint32_t stack_depth;       // traversal stack entries per thread (max BVH depth + 2, <= 32)
     uint32_t persistent_blocks; // workgroups per launch unit (number of CUs)
-    uint32_t* work;             // 2 device work counters (pixel tiles, shadow-ray chunks)
+    uint32_t* work;             // RT_WORK_WORDS device work counters (pixel tiles, shadow-ray chunks)
     const uint32_t* tile_order; // 8x8 tile visiting order (nullptr: row-major)
     uint32_t* tile_cost;        // per-tile cycles of this frame (nullptr: not recorded)
     int bvh_flat;               // BvhWide traversal with the nearer child in a register (bvh_walk_near)
@@ -170,6 +179,11 @@ struct RtQueue {
     uint32_t shade_in;    // > 0: float4 offset of the deferred-shading inputs {pos} {normal} {rd} {rng v0-v3} {rng v4, d}
                           // in each record; raytrace_kernel skips the light samples' draws and
                           // rt_shade_records_kernel computes lc + shadow rays off the path chain
+    // shadow ray jp of hit record k, record-major ([k][jp]): a wave traces the nps shadow samples of 64 / nps
+    // consecutive records.  (Sample-major, [jp][k] -- 64 records towards one light sample per wave --
+    // measured 40 % slower: the rays of one hit point share their walk until they part towards the lights.)
+    __host__ __device__ float4* shadow_ray(uint32_t k, uint32_t jp) const { return srec + 2 * ((size_t)k * nps + jp); }
+    __host__ __device__ size_t mask_at(uint32_t k, uint32_t jp) const { return (size_t)k * nps + jp; }
 };
 
 // nerf.hip
