@@ -283,6 +283,43 @@ __device__ __forceinline__ void grid_backward_level(const LevelInfo& L, float* _
     }
 }
 
+// The same scatter with the atomics shaped for the memory-side atomic unit (F = 4): one atomic
+// wave-instruction covers 16 corner entries x 4 features = 16 aligned 16-B segments (lane 4q + f adds
+// feature f of the corner of source lane 16i + q) instead of 64 scattered dwords, so each instruction
+// leaves L2 as 16 requests rather than 64 (MI355X_MICROARCH.md "Global float atomics": scattered
+// lanes run ~17x below the contiguous rate).  Same products w * dfeat[f], same atomics, regrouped.
+// Source lanes 16i..16i+15 share lane group g = i, hence one level per instruction.
+__device__ __forceinline__ void grid_backward_level_coop4(const LevelInfo& L, float* __restrict__ ggrad, float x0, float x1, float x2,
+                                                          const float* dfeat, int lane) {
+    const float p0 = fmaf(L.scale, x0, 0.5f), p1 = fmaf(L.scale, x1, 0.5f), p2 = fmaf(L.scale, x2, 0.5f);
+    const float q0 = floorf(p0), q1 = floorf(p1), q2 = floorf(p2);
+    const uint32_t g0 = (uint32_t)(int)q0, g1 = (uint32_t)(int)q1, g2 = (uint32_t)(int)q2;
+    const float f0 = p0 - q0, f1 = p1 - q1, f2 = p2 - q2;
+    const int f = lane & 3, qd = lane >> 2;
+    float ds[4];   // dfeat[f] of source lane 16i + qd
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int src = 16 * i + qd;
+        const float v0 = __shfl(dfeat[0], src, 64), v1 = __shfl(dfeat[1], src, 64), v2 = __shfl(dfeat[2], src, 64), v3 = __shfl(dfeat[3], src, 64);
+        ds[i] = f == 0 ? v0 : (f == 1 ? v1 : (f == 2 ? v2 : v3));
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float w = 1.0f;
+        w *= (c & 1) ? f0 : 1.0f - f0;
+        w *= (c & 2) ? f1 : 1.0f - f1;
+        w *= (c & 4) ? f2 : 1.0f - f2;
+        const uint32_t at = L.offset * 4u + grid_index(L, g0 + (c & 1), g1 + ((c >> 1) & 1), g2 + ((c >> 2) & 1)) * 4u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int src = 16 * i + qd;
+            const float ws = __shfl(w, src, 64);
+            const uint32_t as = __shfl(at, src, 64);
+            if (ds[i] != 0.0f) atomicAdd(ggrad + as + f, ws * ds[i]);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // NerfNetwork forward + backward per 16-sample tile (nerf_network.h:144-268).  Activations
 // (post-ReLU, fp16) and pre-activation gradients (fp16) go to acts[tile][TRAIN_FEATS][16] for
@@ -397,15 +434,20 @@ __global__ __launch_bounds__(256) void train_field_kernel(TrainStepArgs a, Train
             de0 = mfma16k16(wfrag_t[(T_DEN0 + q) * 64 + lane], hh[q], de0);
             de1 = mfma16k16(wfrag_t[(T_DEN0 + 4 + q) * 64 + lane], hh[q], de1);
         }
-        if (!valid) continue;
         // encoding gradient (fp16, as tcnn's dL_ddensity_network_input) -> grid; the lane holds
-        // features 4g..4g+3 and 16+4g..16+4g+3
+        // features 4g..4g+3 and 16+4g..16+4g+3 (tail lanes of the last tile contribute nothing)
         float df0[4], df1[4];
-        for (int k = 0; k < 4; ++k) { df0[k] = (float)(_Float16)de0[k]; df1[k] = (float)(_Float16)de1[k]; }
+        for (int k = 0; k < 4; ++k) { df0[k] = valid ? (float)(_Float16)de0[k] : 0.0f; df1[k] = valid ? (float)(_Float16)de1[k] : 0.0f; }
         if constexpr (F == 4) {
+#ifndef TRAIN_GRID_SCATTERED
+            grid_backward_level_coop4(levels[g], ggrad, x0, x1, x2, df0, lane);
+            grid_backward_level_coop4(levels[4 + g], ggrad, x0, x1, x2, df1, lane);
+#else
             grid_backward_level<4>(levels[g], ggrad, x0, x1, x2, df0);
             grid_backward_level<4>(levels[4 + g], ggrad, x0, x1, x2, df1);
+#endif
         } else {
+            if (!valid) continue;
             grid_backward_level<2>(levels[2 * g], ggrad, x0, x1, x2, df0);
             grid_backward_level<2>(levels[2 * g + 1], ggrad, x0, x1, x2, df0 + 2);
             grid_backward_level<2>(levels[8 + 2 * g], ggrad, x0, x1, x2, df1);
