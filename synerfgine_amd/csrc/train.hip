@@ -96,8 +96,8 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
     if (i >= b.ctrl->ray_counter) return;
     const uint2 ns = b.numsteps[i];
     const uint32_t numsteps = ns.x, base = ns.y;
-    const float* cin = b.coords + (size_t)base * 7;
-    const uint16_t* nout = b.mlp_out + (size_t)base * 4;
+    const float* __restrict__ cin = b.coords + (size_t)base * 7;
+    const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
     const aabb box = a.vol.train_aabb;
     const f3 diag = box.hi - box.lo;
     const float4 ro4 = b.rays[2 * i];
@@ -106,17 +106,35 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
     const float EPSILON = 1e-4f;
     f3 rgb_ray = splat(0.0f);
     uint32_t cn = 0;
-    for (; cn < numsteps; ++cn) {
-        if (T < EPSILON) break;
-        const float* c = cin + (size_t)cn * 7;
-        const uint16_t* o = nout + (size_t)cn * 4;
-        const f3 rgb = mk(logistic(h2f(o[0])), logistic(h2f(o[1])), logistic(h2f(o[2])));
-        const float dt = unwarp_dt(c[3]);
-        const float density = sng_expf(h2f(o[3]));
-        const float alpha = 1.0f - sng_expf(-density * dt);
-        const float weight = alpha * T;
-        rgb_ray = rgb_ray + weight * rgb;
-        T *= (1.0f - alpha);
+    // the per-ray chain is serial in T; the loads of the next LOSS_AHEAD samples are independent of it
+    // and are issued as one batch (few rays per batch leave most of the GPU idle, so the chain's memory
+    // latency is the cost)
+    constexpr uint32_t LOSS_AHEAD = 4;
+    bool stop = false;
+    for (; cn < numsteps && !stop;) {
+        float dtw[LOSS_AHEAD];
+        uint2 ow[LOSS_AHEAD];
+#pragma unroll
+        for (uint32_t u = 0; u < LOSS_AHEAD; ++u) {
+            const uint32_t j = min(cn + u, numsteps - 1);
+            dtw[u] = cin[(size_t)j * 7 + 3];
+            ow[u] = *reinterpret_cast<const uint2*>(nout + (size_t)j * 4);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < LOSS_AHEAD; ++u) {
+            if (cn >= numsteps) break;
+            if (T < EPSILON) { stop = true; break; }
+            const float o0 = h2f((uint16_t)(ow[u].x & 0xffffu)), o1 = h2f((uint16_t)(ow[u].x >> 16));
+            const float o2 = h2f((uint16_t)(ow[u].y & 0xffffu)), o3 = h2f((uint16_t)(ow[u].y >> 16));
+            const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
+            const float dt = unwarp_dt(dtw[u]);
+            const float density = sng_expf(o3);
+            const float alpha = 1.0f - sng_expf(-density * dt);
+            const float weight = alpha * T;
+            rgb_ray = rgb_ray + weight * rgb;
+            T *= (1.0f - alpha);
+            ++cn;
+        }
     }
     // same RNG draws as train_generate_kernel for this ray: uv, (max_level off), motionblur, then bg
     const uint32_t ray_idx = b.ray_indices[i];
@@ -162,8 +180,9 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
     const float l1_reg_density = *mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
     f3 rgb_ray2 = splat(0.0f);
     T = 1.0f;
-    float* cout = b.coords_c + (size_t)cbase * 7;
-    uint16_t* dout = b.dloss + (size_t)cbase * 4;
+    float* __restrict__ cout = b.coords_c + (size_t)cbase * 7;
+    uint16_t* __restrict__ dout = b.dloss + (size_t)cbase * 4;
+#pragma unroll 4
     for (uint32_t j = 0; j < ccount; ++j) {
         const float* c = cin + (size_t)j * 7;
         for (int k = 0; k < 7; ++k) cout[(size_t)j * 7 + k] = c[k];
