@@ -50,11 +50,15 @@ __global__ __launch_bounds__(256) void train_generate_kernel(TrainStepArgs a, Tr
     uint32_t j = 0;
     float t = startt;
     f3 pos;
+    // unit-cube scenes (cone 0, one cascade): the exact linear specialisation of the occupancy test and
+    // of advance_to_next_voxel that the render marcher uses (sng_math.h, tests/test_host_fastpaths.py)
+    const bool lin = a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_linear != nullptr;
+    const f3 hs = half_sign(dn);
     while (aabb_contains(box, pos = ray.o + t * dn) && j < NERF_STEPS) {
         const float dt = calc_dt(t, cone);
         const uint32_t mip = mip_from_dt(dt, pos, a.vol.max_mip);
-        if (occupied_at(pos, a.vol.bitfield, mip)) { ++j; t += dt; }
-        else t = advance_to_next_voxel(t, cone, pos, dn, idir, mip);
+        if (lin ? occupied_linear(pos, a.vol.occ_linear) : occupied_at(pos, a.vol.bitfield, mip)) { ++j; t += dt; }
+        else t = lin ? dda_step_linear(t, pos, idir, hs) : advance_to_next_voxel(t, cone, pos, dn, idir, mip);
     }
     if (a.debug) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
     if (j == 0) return;
@@ -74,14 +78,14 @@ __global__ __launch_bounds__(256) void train_generate_kernel(TrainStepArgs a, Tr
     while (aabb_contains(box, pos = ray.o + t * dn) && j < numsteps) {
         const float dt = calc_dt(t, cone);
         const uint32_t mip = mip_from_dt(dt, pos, a.vol.max_mip);
-        if (occupied_at(pos, a.vol.bitfield, mip)) {
+        if (lin ? occupied_linear(pos, a.vol.occ_linear) : occupied_at(pos, a.vol.bitfield, mip)) {
             const f3 wp = (pos - box.lo) / diag;   // warp_position = aabb.relative_pos
             float* c = co + (size_t)j * 7;
             c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
             ++j;
             t += dt;
         } else {
-            t = advance_to_next_voxel(t, cone, pos, dn, idir, mip);
+            t = lin ? dda_step_linear(t, pos, idir, hs) : advance_to_next_voxel(t, cone, pos, dn, idir, mip);
         }
     }
 }
