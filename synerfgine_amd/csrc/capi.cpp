@@ -477,7 +477,7 @@ struct sng_ctx {
         DevBuf pixels, xforms, xforms_ray, focal, pp;
         DevBuf master, grads, m1, m2, steps, ema, p_train, p_infer, wfrag_train, wfrag_t;
         DevBuf grid, grid_tmp, grid_coords, grid_idx, grid_out;
-        DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts;
+        DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts, partial, rayrec;
         uint32_t target = 1u << 18;                    // m_training_batch_size (testbed.h:1103)
         float last_loss = 0.0f;
     } tr;
@@ -1418,6 +1418,7 @@ void train_reset(sng_ctx* c, uint64_t seed) {
     t.coords.ensure((size_t)max_samples * 28); t.mlp_out.ensure((size_t)max_samples * 8);
     t.coords_c.ensure((size_t)target * 28); t.dloss.ensure((size_t)target * 8); t.loss.ensure(max_rays * 4);
     t.acts.ensure((size_t)((target + 15) / 16) * TRAIN_FEATS * 16 * 2);
+    t.partial.ensure((size_t)max_samples * 16); t.rayrec.ensure(max_rays * 48);
     // the bitfield the training marcher reads (density grid -> bitfield after every update)
     c->d_grid_f32.ensure((size_t)n_cells * 4);
     c->d_partial.ensure(1024 * sizeof(double));
@@ -1481,7 +1482,7 @@ TrainStepArgs train_args(sng_ctx* c) {
 TrainBatch train_batch(sng_ctx* c) {
     auto& t = c->tr;
     return {t.ctrl.as<TrainCtrl>(), t.ray_indices.as<uint32_t>(), t.rays.as<float4>(), t.numsteps.as<uint2>(), t.coords.as<float>(), t.mlp_out.as<uint16_t>(),
-            t.coords_c.as<float>(), t.dloss.as<uint16_t>(), t.loss.as<float>(), t.acts.as<uint16_t>()};
+            t.coords_c.as<float>(), t.dloss.as<uint16_t>(), t.loss.as<float>(), t.acts.as<uint16_t>(), t.partial.as<float4>(), t.rayrec.as<float4>()};
 }
 
 // train_nerf_step (3532-3780) up to the gradients; stage > 0 stops early (parity hooks):

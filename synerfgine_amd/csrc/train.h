@@ -134,6 +134,8 @@ struct TrainBatch {
     uint16_t* dloss;         // [target][4] fp16
     float* loss;             // [n_rays]
     uint16_t* acts;          // [target/16][TRAIN_FEATS][16] fp16
+    float4* partial;         // [max_samples] {T before the sample, running rgb after it} (train_loss_kernel)
+    float4* rayrec;          // [n_rays][3] {cbase, ccount, base, -} {grad, loss_scale} {rgb_ray, l1_reg} (train_dloss_kernel)
 };
 
 // feature rows of the tiled activation / gradient buffer

@@ -136,6 +136,7 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
             const float alpha = 1.0f - sng_expf(-density * dt);
             const float weight = alpha * T;
             rgb_ray = rgb_ray + weight * rgb;
+            b.partial[base + cn] = make_float4(T, rgb_ray.x, rgb_ray.y, rgb_ray.z);   // train_dloss_kernel replays from here
             T *= (1.0f - alpha);
             ++cn;
         }
@@ -182,12 +183,34 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
     b.loss[i] = (loss_sum / 3.0f) / (float)a.n_rays;
     const float loss_scale = a.loss_scale / (float)a.n_rays;
     const float l1_reg_density = *mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
-    f3 rgb_ray2 = splat(0.0f);
-    T = 1.0f;
+    // the per-sample gradients need only this ray's constants and the forward partials: they are
+    // written by train_dloss_kernel with one wave per ray instead of this lane's serial loop
+    b.rayrec[3 * i] = make_float4(__uint_as_float(cbase), __uint_as_float(ccount), __uint_as_float(base), 0.0f);
+    b.rayrec[3 * i + 1] = make_float4(grad.x, grad.y, grad.z, loss_scale);
+    b.rayrec[3 * i + 2] = make_float4(rgb_ray.x, rgb_ray.y, rgb_ray.z, l1_reg_density);
+}
+
+// compute_loss_kernel_train_nerf's gradient loop (testbed_nerf.cu:1209-1275) for the ray's first
+// ccount samples, one wave per ray, lanes over the samples: T and the running rgb come from the
+// forward pass's partials (the same float sequence), so every value is the serial loop's.
+__global__ __launch_bounds__(256) void train_dloss_kernel(TrainStepArgs a, TrainBatch b) {
+    const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (i >= b.ctrl->ray_counter) return;
+    const float4 r0 = b.rayrec[3 * i], r1 = b.rayrec[3 * i + 1], r2 = b.rayrec[3 * i + 2];
+    if (r0.x == 0.0f && r0.y == 0.0f && r0.z == 0.0f && r0.w == 0.0f) return;   // ray returned before its record (ccount 0)
+    const uint32_t cbase = __float_as_uint(r0.x), ccount = __float_as_uint(r0.y), base = __float_as_uint(r0.z);
+    const f3 grad = mk(r1.x, r1.y, r1.z), rgb_ray = mk(r2.x, r2.y, r2.z);
+    const float loss_scale = r1.w, l1_reg_density = r2.w;
+    const aabb box = a.vol.train_aabb;
+    const f3 diag = box.hi - box.lo;
+    const float4 ro4 = b.rays[2 * i];
+    const f3 ray_o = mk(ro4.x, ro4.y, ro4.z);
+    const float* __restrict__ cin = b.coords + (size_t)base * 7;
+    const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
     float* __restrict__ cout = b.coords_c + (size_t)cbase * 7;
     uint16_t* __restrict__ dout = b.dloss + (size_t)cbase * 4;
-#pragma unroll 4
-    for (uint32_t j = 0; j < ccount; ++j) {
+    for (uint32_t j = lane; j < ccount; j += 64) {
         const float* c = cin + (size_t)j * 7;
         for (int k = 0; k < 7; ++k) cout[(size_t)j * 7 + k] = c[k];
         const f3 pos = box.lo + mk(c[0], c[1], c[2]) * diag;   // unwarp_position
@@ -198,9 +221,10 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
         const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
         const float density = sng_expf(o3);
         const float alpha = 1.0f - sng_expf(-density * dt);
-        const float weight = alpha * T;
-        rgb_ray2 = rgb_ray2 + weight * rgb;
-        T *= (1.0f - alpha);
+        const float4 pt = b.partial[base + j];
+        const float weight = alpha * pt.x;
+        const f3 rgb_ray2 = mk(pt.y, pt.z, pt.w);
+        const float T = pt.x * (1.0f - alpha);
         const f3 suffix = rgb_ray - rgb_ray2;
         const f3 dl_drgb = weight * grad;
         const float d0 = loss_scale * (dl_drgb.x * (rgb.x * (1.0f - rgb.x)));
@@ -644,7 +668,9 @@ void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const 
     hipLaunchKernelGGL(train_generate_kernel, dim3((a.n_rays + 255) / 256), dim3(256), 0, s, a, im, b, rng);
 }
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
+    (void)hipMemsetAsync(b.rayrec, 0, (size_t)a.n_rays * 48, s);
     hipLaunchKernelGGL(train_loss_kernel, dim3((a.n_rays + 255) / 256), dim3(256), 0, s, a, im, b, rng, mean_density);
+    hipLaunchKernelGGL(train_dloss_kernel, dim3((a.n_rays + 3) / 4), dim3(256), 0, s, a, b);
     hipLaunchKernelGGL(train_rollover_kernel, dim3((a.target_batch + 255) / 256), dim3(256), 0, s, a, b);
 }
 void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s) {
