@@ -362,7 +362,24 @@ __device__ __forceinline__ void grid_backward_level_coop4(const LevelInfo& L, fl
             const int src = 16 * i + qd;
             const float ws = __shfl(w, src, 64);
             const uint32_t as = __shfl(at, src, 64);
+#ifndef TRAIN_GRID_NO_RUNS
+            // consecutive samples of a ray that share this corner entry (the coarse levels: a 16^3 cell
+            // holds ~37 samples of a ray) form runs over qd; a segmented scan sums each run and only
+            // its last lane adds to memory, instead of up to 16 adds to one address in one instruction
+            float v = ws * ds[i];
+            const uint32_t a_prev = __shfl_up(as, 4u, 64), a_next = __shfl_down(as, 4u, 64);
+            bool head = qd == 0 || a_prev != as;
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) {
+                const float u = __shfl_up(v, 4u * (unsigned)d, 64);
+                const bool hu = __shfl_up(head, 4u * (unsigned)d, 64);
+                if (qd >= d && !head) { v += u; head = hu; }
+            }
+            const bool tail = qd == 15 || a_next != as;
+            if (tail && v != 0.0f) atomicAdd(ggrad + as + f, v);
+#else
             if (ds[i] != 0.0f) atomicAdd(ggrad + as + f, ws * ds[i]);
+#endif
         }
     }
 }
