@@ -1106,6 +1106,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             }
             launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf);
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->net_events[2 * net_launches + 1], c->s_nerf));
+            HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));   // render_frame starts the raytracer after the head's network
             ++net_launches;
             launch_composite(vol, cam, mode, a.sched, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
                              c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf);
@@ -1168,13 +1169,15 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     const bool concurrent = c->p("concurrent_streams") != 0.0;
     int rt_start_chunk = (concurrent && show_nerf) ? (int)c->p("rt_start_chunk") : 0;
     if (rt_start_chunk < 0) rt_start_chunk = (y1 - y0) * 10 >= MH * 6 ? 1 : 0;
-    bool rt_enqueued = false;
-    auto enqueue_raytracer = [&](hipEvent_t after) {
-        HIPCHK(hipStreamWaitEvent(c->s_rt, after, 0));
+    bool rt_enqueued = false, rt_sorted = false;
+    // phase 0: everything after `after`; 1 (concurrent frames, at frame start): the work that does not
+    // wait for the NeRF head -- mesh rays and the tile-order sort -- so it overlaps init_rays; 2: the
+    // rest, gated on `after`
+    auto enqueue_raytracer = [&](hipEvent_t after, int phase) {
         // ---- raytracer (RayTracer::render, raytracer.cu:312-370) on its own stream
-        // ---- raytracer (RayTracer::render, raytracer.cu:312-370) on its own stream
-        HIPCHK(hipEventRecord(c->ev_rt0, c->s_rt));
-        if (c->mesh_reset || P.reset_accumulation) {
+        if (phase == 0) HIPCHK(hipStreamWaitEvent(c->s_rt, after, 0));
+        if (phase != 2) HIPCHK(hipEventRecord(c->ev_rt0, c->s_rt));
+        if (phase != 2 && (c->mesh_reset || P.reset_accumulation)) {
             const int mres[2] = {MW, MH};
             launch_mesh_rays(MW, MH, y0, y1, cam, focal_for(c, mres), sc, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->acc_rgba.as<float4>(),
                              c->acc_depth.as<float>(), c->s_rt);
@@ -1216,15 +1219,18 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             if (c->p("rt_tile_order") != 0.0) {
                 const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile - 1) / ra.tile);
                 const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60);
-                c->rt_tile_cost.ensure((size_t)n_tiles * 4);
-                c->rt_tile_order.ensure((size_t)n_tiles * 4);
-                if (key == c->rt_tile_key) {
-                    launch_tile_sort(c->rt_tile_cost.as<uint32_t>(), n_tiles, c->rt_tile_order.as<uint32_t>(), c->s_rt);
-                    ra.tile_order = c->rt_tile_order.as<uint32_t>();
+                if (phase != 2) {
+                    c->rt_tile_cost.ensure((size_t)n_tiles * 4);
+                    c->rt_tile_order.ensure((size_t)n_tiles * 4);
+                    rt_sorted = key == c->rt_tile_key;
+                    if (rt_sorted) launch_tile_sort(c->rt_tile_cost.as<uint32_t>(), n_tiles, c->rt_tile_order.as<uint32_t>(), c->s_rt);
+                    c->rt_tile_key = key;
                 }
+                if (rt_sorted) ra.tile_order = c->rt_tile_order.as<uint32_t>();
                 ra.tile_cost = c->rt_tile_cost.as<uint32_t>();
-                c->rt_tile_key = key;
             }
+            if (phase == 1) return;
+            if (phase == 2) HIPCHK(hipStreamWaitEvent(c->s_rt, after, 0));
             // deferred shadow rays (wavefront) whenever the path has point-light shadow tests and the
             // worst-case queues (every pixel hits on every sample and bounce) fit the budget
             uint32_t n_point = 0;
@@ -1278,12 +1284,13 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                                 c->acc_depth.as<float>(), c->s_rt);
             }
         }
+        if (phase == 1) return;
+        if (phase == 2 && !(c->p("show_virtual_obj") != 0.0 && !c->objs.empty())) HIPCHK(hipStreamWaitEvent(c->s_rt, after, 0));
         HIPCHK(hipEventRecord(c->ev_rt1, c->s_rt));
-
-
         rt_enqueued = true;
     };
-    if (rt_start_chunk <= 0) enqueue_raytracer(c->ev_start);
+    if (rt_start_chunk <= 0) enqueue_raytracer(c->ev_start, 0);
+    else enqueue_raytracer(nullptr, 1);
     if (!concurrent) HIPCHK(hipStreamWaitEvent(c->s_nerf, c->ev_rt1, 0));
 
     // ---- NeRF (Testbed::render SyNeRFgine overload, testbed.cu:4353-4404)
@@ -1292,13 +1299,14 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     if (show_nerf) {
         TraceMode mode{0, 1, 1.0f};
         net_launches = trace_nerf(c, P, vol, cam, sc, tr0, tr1, own0, own1, mode, target, [&](int chunk) {
-            if (!rt_enqueued && chunk == rt_start_chunk) enqueue_raytracer(c->ev_nerf1);
+            // gated on the last network launch of the head (ev_rt_go, trace_nerf), not the chunk's end
+            if (!rt_enqueued && chunk == rt_start_chunk) enqueue_raytracer(c->ev_rt_go, 2);
         });
         launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
     }
     if (!rt_enqueued) {
         HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));
-        enqueue_raytracer(c->ev_rt_go);
+        enqueue_raytracer(c->ev_rt_go, rt_start_chunk <= 0 ? 0 : 2);
     }
     HIPCHK(hipEventRecord(c->ev_shadow1, c->s_nerf));   // end of the trace
     if (shadows && !c->objs.empty()) {
