@@ -1121,6 +1121,13 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             HIPCHK(hipEventSynchronize(c->ev_nerf1));
             const uint32_t* h = &c->h_alive[2 * ((chunk - 1) & 1)];
             if (h[0] == 0 && h[1] == 0) done = true;
+            // once the alive count (it only shrinks) allows 8 steps per iteration, the rest of the march is
+            // ray-local: hand it to the fused tail (the count read here is a chunk old, so it bounds the
+            // count at `iter` from above)
+            else if (!fuse && c->p("nerf_fused") != 0.0 && (uint64_t)std::max(h[0], h[1]) * MAX_STEPS_BETWEEN_COMPACTION <= target) {
+                fuse = true;
+                fuse_after = iter;
+            }
         }
         HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
         ++chunk;

@@ -45,6 +45,33 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred, in
     return base + below;
 }
 
+// Block-aggregated append for 256-thread blocks: ONE returning atomic on `counter` per
+// workgroup trip instead of one per wave (same-address atomics serialise at ~10 ns each, so a
+// 2M-ray iteration with per-wave atomics spends ~0.3 ms on them alone).  Returns each lane's
+// exclusive slot for its `v` entries; `a`/`b` are count-only flags summed into cnt_a/cnt_b
+// (null: skipped).  Must be reached by every thread of the block.
+__device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t v, uint32_t* cnt_a, bool a, uint32_t* cnt_b, bool b,
+                                                 uint32_t* sh, int lane) {
+    const int wave = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v, lane);
+    const uint32_t na = (uint32_t)__popcll(__ballot(a)), nb = (uint32_t)__popcll(__ballot(b));
+    if (lane == 63) sh[wave] = incl;
+    if (lane == 0) { sh[4 + wave] = na; sh[8 + wave] = nb; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t sv = 0, sa = 0, sb = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) { const uint32_t t = sh[w]; sh[w] = sv; sv += t; sa += sh[4 + w]; sb += sh[8 + w]; }
+        sh[12] = sv ? atomicAdd(counter, sv) : 0u;
+        if (cnt_a && sa) atomicAdd(cnt_a, sa);
+        if (cnt_b && sb) atomicAdd(cnt_b, sb);
+    }
+    __syncthreads();
+    const uint32_t r = sh[12] + sh[wave] + incl - v;
+    __syncthreads();   // sh is reused by the next trip
+    return r;
+}
+
 __device__ __forceinline__ uint32_t steps_for(uint32_t n_alive, uint32_t target) {
     uint32_t s = target / n_alive;
     return s < 1 ? 1 : (s > MAX_STEPS_BETWEEN_COMPACTION ? MAX_STEPS_BETWEEN_COMPACTION : s);
@@ -131,12 +158,12 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
     }
     if (!active) return;
     const int lane = threadIdx.x & 63;
-    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
     const float cone = LIN ? 0.0f : vol.cone;
-    for (uint32_t base_i = gw * 64; base_i < n_alive; base_i += n_waves * 64) {
-        const uint32_t i = base_i + lane;
+    __shared__ uint32_t sh_app[16];
+    // block-uniform trips (block_append syncs the block)
+    for (uint32_t blk = blockIdx.x * blockDim.x; blk < n_alive; blk += gridDim.x * blockDim.x) {
+        const uint32_t i = blk + threadIdx.x;
         uint32_t cnt = 0;
         float ts[LIN ? 1 : MAX_STEPS_BETWEEN_COMPACTION];
         f3 o = splat(0.0f), d = splat(1.0f);
@@ -180,10 +207,7 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
             // trace_alt overwrites it in the compositor
             if (store_t && cnt == n_steps) reinterpret_cast<float*>(rays.o_t + i)[3] = t;
         }
-        const uint32_t incl = wave_incl_scan(cnt, lane);
-        uint32_t base = 0;
-        if (lane == 63 && incl) base = atomicAdd(&ctrl->n_samples[p], incl);
-        base = __shfl(base, 63, 64) + incl - cnt;
+        const uint32_t base = block_append(&ctrl->n_samples[p], cnt, nullptr, false, nullptr, false, sh_app, lane);
         if (i < n_alive) {
             samp[i] = make_uint2(base, cnt);
             const f3 wd = (d + 1.0f) * 0.5f;
@@ -236,11 +260,10 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
     // the reference leaves the loop without another compaction once i >= MARCH_ITER
     const bool last = i_step + n_steps >= MARCH_ITER;
     const int lane = threadIdx.x & 63;
-    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
     const f3 diag = vol.train_aabb.hi - vol.train_aabb.lo;
-    for (uint32_t base_i = gw * 64; base_i < n_alive; base_i += n_waves * 64) {
-        const uint32_t i = base_i + lane;
+    __shared__ uint32_t sh_app[16];
+    for (uint32_t blk = blockIdx.x * blockDim.x; blk < n_alive; blk += gridDim.x * blockDim.x) {
+        const uint32_t i = blk + threadIdx.x;
         bool survive = false, hit = false;
         float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
         float depth = 0.0f, mw = 0.0f;
@@ -292,11 +315,10 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
             if (j < n_steps) { hit = !last && rgba.w > 0.001f; death_step = j + i_step; }
             else survive = !last;
         }
-        const uint32_t slot = wave_append(&ctrl->n_alive[p ^ 1], survive, lane);
-        if (sched.global) {
-            const uint32_t idx = __float_as_uint(di.w);
-            (void)wave_append(&ctrl->n_owned[p ^ 1], survive && idx >= sched.own_lo && idx < sched.own_hi, lane);
-        }
+        const uint32_t own_idx = __float_as_uint(di.w);
+        const uint32_t slot = block_append(&ctrl->n_alive[p ^ 1], survive ? 1u : 0u, &ctrl->n_hit, hit,
+                                           sched.global ? &ctrl->n_owned[p ^ 1] : nullptr, survive && own_idx >= sched.own_lo && own_idx < sched.own_hi,
+                                           sh_app, lane);
         if (survive) {
             out.o_t[slot] = ot;
             out.d_idx[slot] = di;
@@ -326,8 +348,6 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
             positions[3 * idx + 0] = orig.x; positions[3 * idx + 1] = orig.y; positions[3 * idx + 2] = orig.z;
             if (ta > 0.2f) frame_depth[idx] = depth;
         }
-        const uint32_t nh = (uint32_t)__popcll(__ballot(hit));
-        if (lane == 0 && nh) atomicAdd(&ctrl->n_hit, nh);
     }
 }
 
