@@ -33,18 +33,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
-// Append `pred` lanes to a buffer; returns each lane's slot (wave-aggregated atomic).
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred, int lane) {
-    unsigned long long mask = __ballot(pred);
-    uint32_t total = (uint32_t)__popcll(mask);
-    uint32_t base = 0;
-    int leader = mask ? (int)(__ffsll((long long)mask) - 1) : 0;
-    if (total && lane == leader) base = atomicAdd(counter, total);
-    base = __shfl(base, leader, 64);
-    uint32_t below = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-    return base + below;
-}
-
 // Block-aggregated append for 256-thread blocks: ONE returning atomic on `counter` per
 // workgroup trip instead of one per wave (same-address atomics serialise at ~10 ns each, so a
 // 2M-ray iteration with per-wave atomics spends ~0.3 ms on them alone).  Returns each lane's
@@ -116,8 +104,9 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
             if (t1 < MAX_DEPTH) { alive = true; tt = t1; }
         }
     }
-    uint32_t slot = wave_append(&ctrl->n_alive[0], alive, lane);
-    if (a.sched.global) (void)wave_append(&ctrl->n_owned[0], alive && idx >= a.sched.own_lo && idx < a.sched.own_hi, lane);
+    __shared__ uint32_t sh_app[16];
+    const uint32_t slot = block_append(&ctrl->n_alive[0], alive ? 1u : 0u, a.sched.global ? &ctrl->n_owned[0] : nullptr,
+                                       alive && idx >= a.sched.own_lo && idx < a.sched.own_hi, nullptr, false, sh_app, lane);
     if (alive) {
         out.o_t[slot] = make_float4(origin.x, origin.y, origin.z, tt);
         out.d_idx[slot] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(idx));
