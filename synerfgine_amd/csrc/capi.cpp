@@ -1109,7 +1109,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));   // render_frame starts the raytracer after the head's network
             ++net_launches;
             launch_composite(vol, cam, mode, a.sched, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
-                             c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf);
+                             c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf, !fuse);
             reduce_sched(p ^ 1);
             p ^= 1;
         }

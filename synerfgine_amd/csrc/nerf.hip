@@ -33,29 +33,30 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
-// Block-aggregated append for 256-thread blocks: ONE returning atomic on `counter` per
+// Block-aggregated append for blocks of NW waves: ONE returning atomic on `counter` per
 // workgroup trip instead of one per wave (same-address atomics serialise at ~10 ns each, so a
 // 2M-ray iteration with per-wave atomics spends ~0.3 ms on them alone).  Returns each lane's
 // exclusive slot for its `v` entries; `a`/`b` are count-only flags summed into cnt_a/cnt_b
 // (null: skipped).  Must be reached by every thread of the block.
+template <int NW = 4>
 __device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t v, uint32_t* cnt_a, bool a, uint32_t* cnt_b, bool b,
                                                  uint32_t* sh, int lane) {
     const int wave = threadIdx.x >> 6;
     const uint32_t incl = wave_incl_scan(v, lane);
     const uint32_t na = (uint32_t)__popcll(__ballot(a)), nb = (uint32_t)__popcll(__ballot(b));
     if (lane == 63) sh[wave] = incl;
-    if (lane == 0) { sh[4 + wave] = na; sh[8 + wave] = nb; }
+    if (lane == 0) { sh[NW + wave] = na; sh[2 * NW + wave] = nb; }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t sv = 0, sa = 0, sb = 0;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) { const uint32_t t = sh[w]; sh[w] = sv; sv += t; sa += sh[4 + w]; sb += sh[8 + w]; }
-        sh[12] = sv ? atomicAdd(counter, sv) : 0u;
+        for (int w = 0; w < NW; ++w) { const uint32_t t = sh[w]; sh[w] = sv; sv += t; sa += sh[NW + w]; sb += sh[2 * NW + w]; }
+        sh[3 * NW] = sv ? atomicAdd(counter, sv) : 0u;
         if (cnt_a && sa) atomicAdd(cnt_a, sa);
         if (cnt_b && sb) atomicAdd(cnt_b, sb);
     }
     __syncthreads();
-    const uint32_t r = sh[12] + sh[wave] + incl - v;
+    const uint32_t r = sh[3 * NW] + sh[wave] + incl - v;
     __syncthreads();   // sh is reused by the next trip
     return r;
 }
@@ -229,7 +230,8 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
 // composite_kernel_nerf_alt (476-575) + compaction into the next buffer
 // (compact_kernel_nerf 1830-1853) + extract_from_payload (1578-1612)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, TraceMode mode, Sched sched, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p,
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev cam, TraceMode mode, Sched sched, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p,
                                                         uint32_t target, uint32_t iter, const float* __restrict__ coords, const uint2* __restrict__ samp,
                                                         const uint2* __restrict__ net_out, float4* __restrict__ frame_rgba,
                                                         float* __restrict__ frame_depth, float* __restrict__ positions) {
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
     const bool last = i_step + n_steps >= MARCH_ITER;
     const int lane = threadIdx.x & 63;
     const f3 diag = vol.train_aabb.hi - vol.train_aabb.lo;
-    __shared__ uint32_t sh_app[16];
+    __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
     for (uint32_t blk = blockIdx.x * blockDim.x; blk < n_alive; blk += gridDim.x * blockDim.x) {
         const uint32_t i = blk + threadIdx.x;
         bool survive = false, hit = false;
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(256) void composite_kernel(Volume vol, CamDev cam, 
             else survive = !last;
         }
         const uint32_t own_idx = __float_as_uint(di.w);
-        const uint32_t slot = block_append(&ctrl->n_alive[p ^ 1], survive ? 1u : 0u, &ctrl->n_hit, hit,
+        const uint32_t slot = block_append<THREADS / 64>(&ctrl->n_alive[p ^ 1], survive ? 1u : 0u, &ctrl->n_hit, hit,
                                            sched.global ? &ctrl->n_owned[p ^ 1] : nullptr, survive && own_idx >= sched.own_lo && own_idx < sched.own_hi,
                                            sh_app, lane);
         if (survive) {
@@ -466,8 +468,11 @@ void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p
 }
 void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const Sched& sched, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p,
                       uint32_t target, uint32_t iter, const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos,
-                      uint32_t blocks, hipStream_t s) {
-    hipLaunchKernelGGL(composite_kernel, dim3(blocks), dim3(256), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
+                      uint32_t blocks, hipStream_t s, bool wide) {
+    // long one-step marches (no fused tail): 1024-thread workgroups, 4x fewer append atomics;
+    // the short head of the hybrid schedule keeps 256 (more, smaller blocks beside the raytracer)
+    if (wide) hipLaunchKernelGGL(composite_kernel<1024>, dim3(std::max(1u, blocks / 4u)), dim3(1024), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
+    else hipLaunchKernelGGL(composite_kernel<256>, dim3(blocks), dim3(256), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
 }
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;

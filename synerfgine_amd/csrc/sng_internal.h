@@ -192,7 +192,7 @@ void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p
                      uint32_t blocks, int store_t, int global_sched, hipStream_t s);
 void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const Sched& sched, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p,
                       uint32_t target, uint32_t iter, const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
-                      hipStream_t s);
+                      hipStream_t s, bool wide = false);
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s);
 void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, uint32_t* occ_linear,
                      hipStream_t s);
