@@ -1099,7 +1099,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             break;
         }
         for (int k = 0; k < CHUNK && !(fuse && iter >= fuse_after); ++k, ++iter) {
-            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, mode.ngp, a.sched.global, c->s_nerf);
+            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, mode.ngp, a.sched.global, c->s_nerf, !fuse);
             if (P.collect_kernel_times) {
                 while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
                 HIPCHK(hipEventRecord(c->net_events[2 * net_launches], c->s_nerf));

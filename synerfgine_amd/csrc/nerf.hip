@@ -127,8 +127,8 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
 // distances of a ray go to LDS instead of 8 live registers, which keeps the kernel small
 // and at high occupancy (the DDA walk is latency bound: many waves in flight hide the
 // bitfield gathers).  The general path (cascades / cone stepping) keeps the unrolled form.
-template <bool LIN>
-__global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
+template <bool LIN, int THREADS = 256>
+__global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                                                        float* __restrict__ coords, uint2* __restrict__ samp, int store_t, int global_sched) {
     __shared__ float ts_lds[LIN ? MAX_STEPS_BETWEEN_COMPACTION * 256 : 1];
     const uint32_t n_alive = ctrl->n_alive[p];
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
     const int lane = threadIdx.x & 63;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
     const float cone = LIN ? 0.0f : vol.cone;
-    __shared__ uint32_t sh_app[16];
+    __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
     // block-uniform trips (block_append syncs the block)
     for (uint32_t blk = blockIdx.x * blockDim.x; blk < n_alive; blk += gridDim.x * blockDim.x) {
         const uint32_t i = blk + threadIdx.x;
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void generate_kernel(Volume vol, RayBuf rays, 
             // trace_alt overwrites it in the compositor
             if (store_t && cnt == n_steps) reinterpret_cast<float*>(rays.o_t + i)[3] = t;
         }
-        const uint32_t base = block_append(&ctrl->n_samples[p], cnt, nullptr, false, nullptr, false, sh_app, lane);
+        const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], cnt, nullptr, false, nullptr, false, sh_app, lane);
         if (i < n_alive) {
             samp[i] = make_uint2(base, cnt);
             const f3 wd = (d + 1.0f) * 0.5f;
@@ -462,8 +462,9 @@ void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl
     hipLaunchKernelGGL(init_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, out, ctrl, fb, depth, pos, nrm);
 }
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
-                     uint32_t blocks, int store_t, int global_sched, hipStream_t s) {
+                     uint32_t blocks, int store_t, int global_sched, hipStream_t s, bool wide) {
     if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
+    else if (wide) hipLaunchKernelGGL(HIP_KERNEL_NAME(generate_kernel<false, 1024>), dim3(std::max(1u, blocks / 4u)), dim3(1024), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
     else hipLaunchKernelGGL(generate_kernel<false>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
 }
 void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const Sched& sched, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p,
