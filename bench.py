@@ -4,14 +4,22 @@
 One step = one complete Engine::frame (raytrace + NeRF march/encode/MLP/composite +
 shadows on the NeRF + overlay) of BASELINE.json config C3.  With N ranks the frame
 is split into N horizontal bands (one per GPU, halo rows recomputed) and the final
-RGBA tiles are all-gathered over RCCL, so the whole job still produces one frame
+bands are all-gathered as RGBA8 over RCCL, so the whole job still produces one frame
 per step (strong scaling).
+
+`python bench.py --gpus N` without a torch.distributed environment starts the N ranks itself
+(torch.distributed.run, one process per GPU) before anything touches the GPU; under torchrun
+(WORLD_SIZE set) it runs as one of the ranks and checks that WORLD_SIZE == N.
 
 Prints ONE JSON line on rank 0 (driver contract).
 """
 import argparse
 import json
 import os
+import platform
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -22,13 +30,18 @@ BYTES_PER_SAMPLE = 28 + 8 * 8 * 4 * 2 + 8   # NerfCoordinate read + 8 levels x 8
 FLOPS_PER_SAMPLE = 20480                     # 2*(32*64+64*16) + 2*(32*64+64*64+64*16)
 HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F16_PEAK_TFLOPS = 2500.0                # dense fp16/bf16 MFMA
-
+ROUND = "r02"
 
 WORKLOADS = {
     "c2": "lego NeRF only (show_virtual_obj=0, shadows off)",
     "c3": "lego NeRF + armadillo.json (light_samples 8, path_trace_depth 2, shadow_on_nerf + shadow_on_virtual_obj)",
     "c4": "kitchen-like NeRF (aabb_scale 16, 5 cascades, cone stepping) + kitchen-rocks.json (bunny/rock/box, light_samples 4, "
           "nerf_shadow_samples 4)",
+}
+METRICS = {
+    "c2": "rendered frames/sec at 800x800 (lego .ingp, NeRF only); PSNR vs ref",
+    "c3": "rendered frames/sec at 1920x1080 (lego .ingp + 1 mesh); PSNR vs ref",
+    "c4": "rendered frames/sec at 1920x1080 (kitchen-like .ingp + 3 meshes, light_samples 4); PSNR vs ref",
 }
 
 
@@ -39,9 +52,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="timed oracle runs per CPU-baseline leg (median reported)")
     ap.add_argument("--serial-streams", action="store_true", help="run raytracer and NeRF back to back (profiling)")
-    ap.add_argument("--cpu-baseline-scale", type=float, default=1.5, help="oracle renders the frame at 1/scale linear resolution")
+    ap.add_argument("--cpu-baseline-scale", type=float, default=1.5, help="the C3-sample leg renders the frame at 1/scale linear resolution")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help="gloo: CPU-side gather (rehearsal on one GPU)")
+    ap.add_argument("--dry-run", action="store_true", help="form the ranks and exchange the world size only (no GPU; CPU tests)")
     ap.add_argument("--even-bands", action="store_true", help="equal-height bands instead of cost-balanced ones")
     ap.add_argument("--local-schedule", action="store_true",
                     help="N>1: step each band from its own alive count (no per-iteration count all-reduce; not bit-identical to N=1)")
@@ -52,10 +67,78 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(eng_cfg, config, scale, model_name, overrides):
-    """Time the CPU oracle (test infrastructure) on a bounded sample of the same workload, and compare the
-    GPU's frame of that same sample with it (the metric's "PSNR vs ref": the oracle is the reference
-    restatement).  Returns (cpu_baseline, psnr_vs_oracle)."""
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """--gpus N outside torch.distributed: start N ranks, one process per GPU, with torch.distributed.run as
+    a child process.  This parent never initialises the GPU (no torch.cuda / HIP call happens before the
+    children exist), and it exits with the launcher's status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_info():
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model}
+
+
+def cpu_baseline_c1(model_name, runs):
+    """the reference has no CPU inference path, so the baseline is the oracle (C++ OpenMP,
+    -O2, IEEE fp32 -- the CPU restatement of the render path) rendering config C1: one Engine::frame of the
+    lego snapshot at 256x256, NeRF only, no virtual objects.  1 warm-up, then the median of `runs` timed
+    frames, on all the OpenMP threads the process has and on 1 thread."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    from synerfgine_amd import scene as S
+
+    tb, eng, (ncfg, params, grid) = S.make_engine("c2", width=256, height=256, model=model_name)
+    try:
+        model = O.Model(ncfg, params)
+        vol = O.volume_for(ncfg, grid)
+        nrng, mrng = eng.rng_states(0).copy(), eng.rng_states(1).copy()
+        lib = O.lib()
+        all_threads = lib.orc_num_threads()
+        legs = {}
+        for threads in (all_threads, 1):
+            lib.orc_set_num_threads(threads)
+            O.render_frame(model, vol, tb, eng, nrng.copy(), mrng.copy())
+            ts = []
+            for _ in range(runs):
+                t0 = time.perf_counter()
+                out = O.render_frame(model, vol, tb, eng, nrng.copy(), mrng.copy())
+                ts.append(time.perf_counter() - t0)
+            med = statistics.median(ts)
+            n = int(out["stats"].n_samples)
+            legs[threads] = {"threads": threads, "median_s": round(med, 4), "runs_s": [round(t, 4) for t in ts],
+                             "frames_per_s": round(1.0 / med, 3), "samples": n, "samples_per_s": round(n / med, 1),
+                             "algorithmic_GB_per_s": round(n * BYTES_PER_SAMPLE / med / 1e9, 3)}
+        lib.orc_set_num_threads(all_threads)
+    finally:
+        tb.close()
+    return legs, all_threads
+
+
+def cpu_sample_c3(eng_cfg, config, scale, model_name, overrides):
+    """Time the CPU oracle (test infrastructure) on a bounded sample of the benchmarked workload, and compare
+    the GPU's frame of that same sample with it (the metric's "PSNR vs ref": the oracle is the reference
+    restatement).  Returns (sample, psnr_vs_oracle)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle as O
@@ -75,23 +158,55 @@ def cpu_baseline(eng_cfg, config, scale, model_name, overrides):
     dt = time.perf_counter() - t0
     tb.close()
     frac = (w * h) / float(full["width"] * full["height"])
-    fps_full = frac / dt   # pixel-count scaling to the full-resolution frame
     err = np.abs(np.clip(gpu[..., :3], 0, 1) - np.clip(ref["final"][..., :3], 0, 1))
     mse = float(np.mean(err ** 2))
     psnr = {"db": round(10 * np.log10(1.0 / max(mse, 1e-12)), 2), "max_abs": round(float(err.max()), 5),
             "frac_within_2_255": round(float(np.mean(err.max(axis=-1) <= 2.0 / 255.0)), 5), "res": [w, h],
             "against": "CPU oracle (line-by-line restatement of the reference path, oracle/), same inputs and RNG states; final sRGB RGB in [0,1]"}
-    base = {"value": round(fps_full, 5), "unit": "frames/s", "cores": O.lib().orc_num_threads(), "kind": "port",
-            "sample": f"oracle (C++ OpenMP) Engine::frame of {config} at {w}x{h} ({frac:.3g} of the pixels) took "
-                      f"{dt:.2f}s; extrapolated by pixel count to {full['width']}x{full['height']}"}
-    return base, psnr
+    sample = {"frames_per_s": round(frac / dt, 5), "threads": O.lib().orc_num_threads(), "seconds": round(dt, 3),
+              "what": f"one oracle Engine::frame of {config} at {w}x{h} ({frac:.3g} of the pixels), extrapolated by pixel count to "
+                      f"{full['width']}x{full['height']}"}
+    return sample, psnr
+
+
+def traffic_profile(config):
+    """HBM bytes per launch of the roofline kernels from this round's PMC passes for this config
+    (tools/gpu_pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 FETCH correction), labelled
+    with the file they came from; None when no profile of this config exists."""
+    path = os.path.join(REPO, "profiles", f"pmc_traffic_{ROUND}_{config}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return {"file": os.path.relpath(path, REPO), "config": d.get("config"), "kernels": d.get("roofline_kernels", {})}
+
+
+def dry_run(args, rank, world):
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([1], dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_formed": int(t.item()), "world_size": dist.get_world_size(),
+                          "requested_gpus": args.gpus}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        return dry_run(args, rank, world)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -101,6 +216,7 @@ def main():
     if world > 1:
         torch.cuda.set_device(dev_id)
         dist.init_process_group(args.dist_backend)
+        assert dist.get_world_size() == args.gpus, "process group does not span --gpus ranks"
     from synerfgine_amd import scene as S
     from synerfgine_amd import tiling as T
 
@@ -116,17 +232,20 @@ def main():
     dev = torch.device("cuda", dev_id)
     stream = torch.cuda.current_stream(dev)
     bounds = T.even_bounds(MH, world)
+    comm = {"backend": args.dist_backend if world > 1 else None, "world_size": dist.get_world_size() if world > 1 else 1}
     if world > 1 and not args.local_schedule:
         # frame-wide step schedule: one uint32 all-reduce per wavefront iteration
         # keeps every band bit-identical to the single-GPU frame
         if args.dist_backend == "nccl":
             eng.attach_comm()
+            comm["sched_comm"] = f"RCCL communicator of {world} ranks (sng_set_comm)"
         else:
             def _reduce(vals):
                 t = torch.tensor(vals, dtype=torch.int64)
                 dist.all_reduce(t)
                 return t.tolist()
             eng.attach_host_reducer(_reduce)
+            comm["sched_comm"] = f"gloo host reducer over {world} ranks"
 
     if world > 1 and not args.even_bands:
         # untimed calibration: re-split the rows until every band costs the same device time
@@ -140,16 +259,16 @@ def main():
     rows = (bounds[rank], bounds[rank + 1])
     band = max(bounds[k + 1] - bounds[k] for k in range(world))
     on_dev = args.dist_backend == "nccl"
-    tile = torch.zeros((band, MW, 4), dtype=torch.float32, device=dev if on_dev else "cpu")
-    frame = torch.empty((world * band, MW, 4), dtype=torch.float32, device=dev if on_dev else "cpu") if world > 1 else None
-    tile_dev = tile if on_dev else torch.zeros((band, MW, 4), dtype=torch.float32, device=dev)
+    # composition tiles: RGBA8 (4 B/px), written by sng_final_rgba8 on the device
+    tile_dev = torch.zeros((band, MW), dtype=torch.int32, device=dev)
+    tile = tile_dev if on_dev else torch.zeros((band, MW), dtype=torch.int32)
+    frame = torch.empty((world * band, MW), dtype=torch.int32, device=dev if on_dev else "cpu") if world > 1 else None
 
     def step(collect):
         r = eng.frame(spp=0, reset=True, rows=rows if world > 1 else None, collect_kernel_times=collect)
         if world > 1:
-            n = (rows[1] - rows[0]) * MW * 16
-            if n:
-                tb._lib.sng_copy_device(tb.ctx, r.raw.d_final_rgba + rows[0] * MW * 16, tile_dev.data_ptr(), n, stream.cuda_stream)
+            if rows[1] > rows[0]:
+                tb._lib.sng_final_rgba8(tb.ctx, rows[0], rows[1], tile_dev.data_ptr(), stream.cuda_stream)
             if not on_dev:
                 tile.copy_(tile_dev)
             T.gather_bands(tile, frame)
@@ -173,31 +292,34 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel: fused hash-grid + MLP, timed with hipEvents on its own stream over the timed region
+    # dominant kernel: fused hash-grid + MLP, timed with hipEvents on its own stream over the timed region.
+    # Samples per launch come from the device counter of the network launches (MarchCtrl::net_samples);
+    # the ray-local fused tail (fused.hip) evaluates the rest of the frame's samples inside its own kernel.
     ms_net = sum(s.ms_network for s in stats)
     launches = sum(s.network_launches for s in stats)
-    # samples evaluated by the network kernel: one launch per wavefront iteration; the ray-local
-    # tail (fused.hip) evaluates the remaining iterations' samples inside its own kernel
-    samples = sum(sum(s.samples_per_iter[: s.network_launches]) for s in stats)
-    tail_samples = sum(s.n_samples for s in stats) - samples
+    samples = sum(s.n_samples_network for s in stats)
+    total_samples = sum(s.n_samples for s in stats)
+    tail_samples = total_samples - samples
+    ms_tail = sum(s.ms_fused_tail for s in stats)
     avg_launch_ms = ms_net / max(1, launches)
     bytes_per_launch = samples * BYTES_PER_SAMPLE / max(1, launches)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     tflops = samples * FLOPS_PER_SAMPLE / (ms_net * 1e-3) / 1e12 if ms_net > 0 else 0.0
+    tail_gbs = tail_samples * BYTES_PER_SAMPLE / (ms_tail * 1e-3) / 1e9 if ms_tail > 0 else 0.0
+    field_ms = ms_net + ms_tail
+    field_gbs = total_samples * BYTES_PER_SAMPLE / (field_ms * 1e-3) / 1e9 if field_ms > 0 else 0.0
+    prof = traffic_profile(args.config)
     traffic = None
-    pmc_file = os.path.join(REPO, "profiles", "pmc_network_r01.json")
-    if os.path.exists(pmc_file):
-        try:
-            traffic = json.load(open(pmc_file)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    if prof:
+        net_prof = prof["kernels"].get("nerf_network_kernel")
+        traffic = net_prof.get("hbm_bytes_per_launch") if net_prof else None
 
     result = None
     if rank == 0:
         fps = args.steps / elapsed
         s0 = stats[-1]
         result = {
-            "metric": "rendered frames/sec at 1920x1080 (lego .ingp + 1 mesh); PSNR vs ref",
+            "metric": METRICS[args.config],
             "value": round(fps, 3),
             "unit": "frames/s",
             "n_gpus": world,
@@ -214,10 +336,14 @@ def main():
                      "synthetic: random-init base.json NeRF (L=8,F=4,T=2^19) with an analytic density (synthetic.py)") +
                     "; scene JSON + OBJ meshes from scenes/ and data/obj/; synthetic frames (fixed camera, accumulation reset every frame)",
             "config": {"workload": f"{args.config}: " + WORKLOADS[args.config],
-                       "width": MW, "height": MH, "nerf_res": list(res["nerf"]), "tiles": f"{world} horizontal bands (rows {bounds}) + " + ("RCCL all_gather" if args.dist_backend == "nccl" else "gloo all_gather"),
+                       "width": MW, "height": MH, "nerf_res": list(res["nerf"]),
+                       "tiles": f"{world} horizontal bands (rows {bounds}) + " +
+                                (("RCCL" if on_dev else "gloo") + " all_gather of RGBA8 tiles" if world > 1 else "no gather"),
                        "step_schedule": "band-local" if (world > 1 and args.local_schedule) else ("frame-wide (per-iteration alive-count all-reduce)" if world > 1 else "frame-wide"),
                        "samples_per_frame": int(s0.n_samples), "reference_slots_per_frame": int(s0.n_reference_slots),
-                       "wavefront_iterations": int(s0.n_iterations), "hit_rays": int(s0.n_hit)},
+                       "wavefront_iterations": int(s0.n_iterations), "fused_tail_from_iteration": int(s0.fused_from_iter),
+                       "hit_rays": int(s0.n_hit)},
+            "comm": comm,
             "streams": "serialized (raytracer then NeRF)" if args.serial_streams else
                        "concurrent (NeRF head alone, then raytracer || NeRF tail; NeRF stream high priority)",
             "overrides": overrides,
@@ -225,21 +351,40 @@ def main():
                                      "shadow": round(s0.ms_shadow, 3), "overlay": round(s0.ms_overlay, 3)},
             "roofline": {"kernel": "nerf_network_kernel<4,1> (fused hash grid + SH + density/rgb MLP)", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
-                         "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
-                         "samples_in_launches": int(samples), "samples_in_fused_tail": int(tail_samples),
+                         "traffic": traffic, "traffic_source": prof["file"] if prof else None,
+                         "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
+                         "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches, "samples_in_launches": int(samples),
                          "timing": "hipEvents around every launch on the NeRF stream over the timed region" +
                                    ("" if args.serial_streams else "; the kernel shares the GPU with the raytracer stream, so this is the "
                                     "contended duration (uncontended: --serial-streams)"),
-                         "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / MFMA_F16_PEAK_TFLOPS, 4)},
+                         "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / MFMA_F16_PEAK_TFLOPS, 4),
+                         "fused_tail": {"kernel": "nerf_fused_kernel (march + field + composite, ray-local)", "samples": int(tail_samples),
+                                        "ms": round(ms_tail, 4), "achieved": round(tail_gbs, 1), "frac": round(tail_gbs / HBM_PEAK_GBS, 4),
+                                        "timing": "hipEvents around the tail launch (it runs beside the raytracer on reserved CUs in the "
+                                                  "concurrent schedule, so its duration is latency, not throughput)"},
+                         "field_sample_weighted": {"samples": int(total_samples), "ms": round(field_ms, 4), "achieved": round(field_gbs, 1),
+                                                   "frac": round(field_gbs / HBM_PEAK_GBS, 4)}},
         }
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        try:
+            legs, threads = cpu_baseline_c1(args.model if args.config != "c4" else "lego", args.cpu_runs)
+            best = legs[threads]
+            result["cpu_baseline"] = {
+                "value": best["frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
+                "sample": "BASELINE config C1: the oracle (C++ OpenMP restatement of the render path; the reference has no CPU "
+                          "path) renders the lego snapshot at 256x256, NeRF only; median of "
+                          f"{args.cpu_runs} after 1 warm-up",
+                "legs": {"all_threads": best, "one_thread": legs[1]}, **cpu_info()}
+        except Exception as e:   # the CPU leg must never hide the GPU number
+            result["cpu_baseline"] = {"value": None, "error": repr(e)}
     tb.close()
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:
             try:
-                result["cpu_baseline"], result["psnr_vs_oracle"] = cpu_baseline(eng_cfg, args.config, args.cpu_baseline_scale, args.model, overrides)
-            except Exception as e:   # the CPU leg must never hide the GPU number
-                result["cpu_baseline"] = {"value": None, "error": str(e)}
+                sample, result["psnr_vs_oracle"] = cpu_sample_c3(eng_cfg, args.config, args.cpu_baseline_scale, args.model, overrides)
+                result["cpu_baseline"]["benchmarked_workload_sample"] = sample
+            except Exception as e:
+                result["psnr_vs_oracle"] = {"error": repr(e)}
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -89,7 +89,11 @@ typedef struct {
     uint32_t alive_per_iter[64];
     uint32_t steps_per_iter[64];
     uint32_t samples_per_iter[64];
-    int32_t reserved[8];
+    uint32_t fused_from_iter;   /* first iteration marched by the ray-local fused tail (n_iterations: none) */
+    uint64_t n_samples_network; /* samples of the whole-GPU network launches (device counter); the other
+                                   n_samples - n_samples_network were evaluated inside the fused tail */
+    float ms_fused_tail;        /* device time of the fused tail launch (collect_kernel_times) */
+    int32_t reserved[3];
 } sng_frame_result;
 
 typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;
@@ -167,6 +171,11 @@ int sng_get_resolution(sng_ctx* ctx, sng_resolution_info* out);
  * "animation_speed", "camera_path_playing" (Play/Pause), "camera_path_frame" (the frame slider);
  * read-only "camera_path_total_frames". */
 int sng_render_frame(sng_ctx* ctx, const sng_frame_params* params, sng_frame_result* out);
+/* Band composition for tiled multi-GPU frames (the reference has no multi-GPU render): the
+ * last frame's final RGBA rows [row_begin, row_end) at mesh resolution as RGBA8 (unorm8 =
+ * round(clamp(c, 0, 1) * 255), one uint32 per px, R in the low byte) into the device buffer d_out,
+ * enqueued on hip_stream -- the 4 B/px tile each rank contributes to the RCCL gather. */
+int sng_final_rgba8(sng_ctx* ctx, int32_t row_begin, int32_t row_end, uint32_t* d_out, void* hip_stream);
 /* ---- headless display stage (Display::present / save_image, display.cu:265-322; main.frag:24-117) ----
  * The last frame's final RGBA at mesh resolution, drawn to the window resolution through main.frag's
  * FXAA (GL_LINEAR / GL_REPEAT sampling), blended over rendering.clear_color and read back as RGB8,

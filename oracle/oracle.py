@@ -115,7 +115,7 @@ def lib():
             "orc_raytrace": (None, [vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, u32, vp, vp, vp]),
             "orc_overlay": (None, [vp, vp, vp, vp, vp, vp, vp]),
             "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
-            "orc_num_threads": (i32, []),
+            "orc_num_threads": (i32, []), "orc_set_num_threads": (None, [i32]), "orc_set_mlp_accum": (None, [i32, i32]),
             "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
             "orc_display": (None, [vp, i32, i32, i32, i32, vp, vp]),
             "orc_camera_set_view": (None, [vp, vp, vp, vp, vp, f32]),
@@ -127,6 +127,20 @@ def lib():
             fn.restype = res
             fn.argtypes = args
     return _lib
+
+
+class mlp_accum:
+    """Context manager: run the oracle MLP with tcnn's fp16 WMMA accumulators (mode 1) or fp32 (mode 0)."""
+    def __init__(self, mode, chunk=16):
+        self.mode, self.chunk = mode, chunk
+
+    def __enter__(self):
+        lib().orc_set_mlp_accum(self.mode, self.chunk)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_mlp_accum(0, 16)
+        return False
 
 
 def ptr(a):

@@ -593,12 +593,28 @@ void sh_one(float dx, float dy, float dz, uint16_t* o) {
     o[14] = f2h(1.4453057213202769f * z * (x2 - y2));
     o[15] = f2h(0.59004358992664352f * x * (-x2 + 3.0f * y2));
 }
-/* dense layer y = W x (W row-major [n_out][n_in], fp16), fp32 accumulation,
- * optional ReLU, result rounded to fp16 [tcnn FullyFusedMLP, unvendored] */
+/* dense layer y = W x (W row-major [n_out][n_in], fp16), optional ReLU, result rounded to fp16
+ * [tcnn FullyFusedMLP, unvendored].  Two accumulation models (orc_set_mlp_accum):
+ *   mode 0 (default): one fp32 accumulator over the whole K, rounded to fp16 once -- what this repository's
+ *     MFMA kernel computes (v_mfma_f32_16x16x32_f16 keeps an f32 accumulator);
+ *   mode 1: tcnn's FullyFusedMLP on sm >= 70 (nerf_network.h:120,130 -> fully_fused_mlp.cu): WMMA fragments
+ *     with __half accumulators (wmma::fragment<accumulator,16,16,16,__half>), so the running sum is
+ *     rounded to fp16 after every k-chunk of `chunk` products (16 = one wmma::mma_sync; the products of
+ *     a chunk summed in fp32).  The tensor core's internal alignment/truncation inside a chunk is not
+ *     modelled (unpublished; parity unpinned). */
+static int g_mlp_accum = 0, g_mlp_chunk = 16;
 void dense(const uint16_t* W, uint32_t n_out, uint32_t n_in, const uint16_t* x, uint16_t* y, bool relu) {
     for (uint32_t o = 0; o < n_out; ++o) {
         float acc = 0.0f;
-        for (uint32_t k = 0; k < n_in; ++k) acc += h2f(W[o * n_in + k]) * h2f(x[k]);
+        if (g_mlp_accum == 0) {
+            for (uint32_t k = 0; k < n_in; ++k) acc += h2f(W[o * n_in + k]) * h2f(x[k]);
+        } else {
+            for (uint32_t k0 = 0; k0 < n_in; k0 += (uint32_t)g_mlp_chunk) {
+                float part = 0.0f;
+                for (uint32_t k = k0; k < std::min(n_in, k0 + (uint32_t)g_mlp_chunk); ++k) part += h2f(W[o * n_in + k]) * h2f(x[k]);
+                acc = h2f(f2h(acc + part));
+            }
+        }
         if (relu && acc < 0.0f) acc = 0.0f;
         y[o] = f2h(acc);
     }
@@ -1472,6 +1488,19 @@ void orc_render_frame(const orc_model* m, const orc_volume* v, const orc_camera*
                                    P->nerf_shadow_intensity, P->nerf_on_nerf_shadow_threshold, P->nerf_kernel_size);
     }
     orc_overlay(P, acc.data(), accd.data(), nerf_rgba, nerf_depth, final_rgba, final_depth);
+}
+
+void orc_set_mlp_accum(int32_t mode, int32_t chunk) {
+    g_mlp_accum = mode;
+    g_mlp_chunk = chunk > 0 ? chunk : 16;
+}
+
+void orc_set_num_threads(int32_t n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
 }
 
 int32_t orc_num_threads(void) {

@@ -200,6 +200,10 @@ void orc_animation_play(float cam[12] /* in/out */, float* scale /* in/out */, c
 void orc_display(const float* rgba, int32_t W, int32_t H, int32_t OW, int32_t OH, const float clear[3], uint8_t* rgb_out);
 
 int32_t orc_num_threads(void);
+void orc_set_num_threads(int32_t n);
+/* MLP accumulation model (sng_oracle.cpp dense()): 0 = fp32 over K (default), 1 = tcnn WMMA __half
+ * accumulators, rounded to fp16 after every `chunk` (16) products */
+void orc_set_mlp_accum(int32_t mode, int32_t chunk);   /* OpenMP threads of the later calls (bench CPU baseline) */
 
 #ifdef __cplusplus
 }

@@ -78,7 +78,10 @@ class sng_frame_result(ctypes.Structure):
         ("alive_per_iter", ctypes.c_uint32 * 64),
         ("steps_per_iter", ctypes.c_uint32 * 64),
         ("samples_per_iter", ctypes.c_uint32 * 64),
-        ("reserved", ctypes.c_int32 * 8),
+        ("fused_from_iter", ctypes.c_uint32),
+        ("n_samples_network", ctypes.c_uint64),
+        ("ms_fused_tail", ctypes.c_float),
+        ("reserved", ctypes.c_int32 * 3),
     ]
 
 
@@ -186,6 +189,7 @@ SIGNATURES = {
     "sng_synchronize": (ctypes.c_int, [P]),
     "sng_copy_to_host": (ctypes.c_int, [P, P, P, U64]),
     "sng_copy_device": (ctypes.c_int, [P, P, P, U64, P]),
+    "sng_final_rgba8": (ctypes.c_int, [P, ctypes.c_int32, ctypes.c_int32, P, P]),
     "sng_get_rng_states": (ctypes.c_int, [P, ctypes.c_int, U32P, U64]),
     "sng_set_rng_states": (ctypes.c_int, [P, ctypes.c_int, U32P, U64]),
     "sng_bvh_build": (ctypes.c_int, [FP, U32, U32, FP, U32, U32P]),

@@ -396,7 +396,7 @@ struct sng_ctx {
     int device = 0;
     int n_cus = 256;
     hipStream_t s_nerf = nullptr, s_rt = nullptr;
-    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr;
+    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr, ev_fused0 = nullptr, ev_fused1 = nullptr;
     std::vector<hipEvent_t> net_events;
 
     // model
@@ -1087,11 +1087,16 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             fa.frame_rgba = c->nerf_rgba.as<float4>(); fa.frame_depth = c->nerf_depth.as<float>(); fa.positions = c->nerf_pos.as<float>();
             fa.work = c->fused_work.as<uint32_t>();
             fa.lanes = (uint32_t)std::min(64.0, std::max(1.0, c->p("nerf_fused_lanes")));
-            // concurrent frames: the tail runs beside the raytracer on the CUs its grids leave free
+            // concurrent frames: the tail runs beside the raytracer on the CUs its grids leave free.  A
+            // mid-frame switch (a long march, e.g. C4) happens long after the raytracer has finished: the
+            // tail then gets the whole-GPU grid
             double fb = c->p("nerf_fused_blocks");
-            if (fb < 0) fb = (c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0) ? 2.0 * std::max(1.0, c->p("rt_reserved_cus")) : 0.0;
+            const bool beside_rt = iter <= (uint32_t)std::max(0.0, c->p("nerf_fused_after"));
+            if (fb < 0) fb = (beside_rt && c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0) ? 2.0 * std::max(1.0, c->p("rt_reserved_cus")) : 0.0;
+            if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused0, c->s_nerf));
             launch_nerf_fused(fa, c->net, iter == 0 ? std::min(c->h_alive[0], n_band) : n_band, (uint32_t)fb, c->s_nerf);
             HIPCHK(hipGetLastError());
+            if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused1, c->s_nerf));
             HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
             c->fused_last = true;
             c->fused_k0 = iter;
@@ -1134,6 +1139,33 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         on_chunk(chunk);
     }
     return net_launches;
+}
+
+// march statistics of the last trace (MarchCtrl read back at the end of the frame)
+void march_stats(const sng_ctx* c, const sng_frame_params& P, sng_frame_result* out) {
+    out->n_iterations = c->h_ctrl->n_iter;
+    out->n_hit = c->h_ctrl->n_hit;
+    out->n_samples = c->h_ctrl->total_samples;
+    out->n_samples_network = c->h_ctrl->net_samples;
+    out->fused_from_iter = c->fused_last ? c->fused_k0 : c->h_ctrl->n_iter;
+    out->n_reference_slots = ref_slots_of(c);
+    std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
+    std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
+    std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
+}
+
+// hipEvent durations of the network launches and of the fused tail (collect_kernel_times)
+void network_times(sng_ctx* c, const sng_frame_params& P, uint32_t net_launches, sng_frame_result* out) {
+    out->network_launches = net_launches;
+    if (!P.collect_kernel_times) return;
+    float tot = 0.0f;
+    for (uint32_t k = 0; k < net_launches; ++k) {
+        float ms = 0.0f;
+        HIPCHK(hipEventElapsedTime(&ms, c->net_events[2 * k], c->net_events[2 * k + 1]));
+        tot += ms;
+    }
+    out->ms_network = tot;
+    if (c->fused_last) HIPCHK(hipEventElapsedTime(&out->ms_fused_tail, c->ev_fused0, c->ev_fused1));
 }
 
 void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out) {
@@ -1360,15 +1392,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         out->d_nerf_normals = c->nerf_nrm.as<float>();
         out->d_syn_rgba = c->acc_rgba.as<float>();
         out->d_syn_depth = c->acc_depth.as<float>();
-        if (show_nerf) {
-            out->n_iterations = c->h_ctrl->n_iter;
-            out->n_hit = c->h_ctrl->n_hit;
-            out->n_samples = c->h_ctrl->total_samples;
-            out->n_reference_slots = ref_slots_of(c);
-            std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
-            std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
-            std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
-        }
+        if (show_nerf) march_stats(c, P, out);
         HIPCHK(hipEventElapsedTime(&out->ms_frame, c->ev_start, c->ev_end));
         HIPCHK(hipEventElapsedTime(&out->ms_raytrace, c->ev_rt0, c->ev_rt1));
         HIPCHK(hipEventElapsedTime(&out->ms_nerf, c->ev_nerf0, c->ev_shadow1));
@@ -1376,16 +1400,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         float ov = 0.0f;
         HIPCHK(hipEventElapsedTime(&ov, c->ev_nerf1, c->ev_end));
         out->ms_overlay = ov;
-        if (P.collect_kernel_times) {
-            float tot = 0.0f;
-            for (uint32_t k = 0; k < net_launches; ++k) {
-                float ms = 0.0f;
-                HIPCHK(hipEventElapsedTime(&ms, c->net_events[2 * k], c->net_events[2 * k + 1]));
-                tot += ms;
-            }
-            out->ms_network = tot;
-        }
-        out->network_launches = net_launches;
+        network_times(c, P, net_launches, out);
     }
 }
 
@@ -1615,25 +1630,10 @@ void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* o
         std::memset(out, 0, sizeof(*out));
         out->d_nerf_rgba = c->nerf_rgba.as<float>();
         out->d_nerf_depth = c->nerf_depth.as<float>();
-        out->n_iterations = c->h_ctrl->n_iter;
-        out->n_hit = c->h_ctrl->n_hit;
-        out->n_samples = c->h_ctrl->total_samples;
-        out->n_reference_slots = ref_slots_of(c);
-        std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
-        std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
-        std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
+        march_stats(c, P, out);
         HIPCHK(hipEventElapsedTime(&out->ms_frame, c->ev_start, c->ev_end));
         out->ms_nerf = out->ms_frame;
-        if (P.collect_kernel_times) {
-            float tot = 0.0f;
-            for (uint32_t k = 0; k < net_launches; ++k) {
-                float ms = 0.0f;
-                HIPCHK(hipEventElapsedTime(&ms, c->net_events[2 * k], c->net_events[2 * k + 1]));
-                tot += ms;
-            }
-            out->ms_network = tot;
-        }
-        out->network_launches = net_launches;
+        network_times(c, P, net_launches, out);
     }
 }
 
@@ -1654,7 +1654,7 @@ void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_nerf, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_rt, hipStreamNonBlocking, prio_lo));
-    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go}) HIPCHK(hipEventCreate(e));
+    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go, &c->ev_fused0, &c->ev_fused1}) HIPCHK(hipEventCreate(e));
     HIPCHK(hipHostMalloc((void**)&c->h_ctrl, sizeof(MarchCtrl), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&c->h_alive, 8 * sizeof(uint32_t), hipHostMallocDefault));
     float rf = fov_to_focal(50.625f);   // Testbed::reset_camera -> set_fov(50.625) (testbed.cu:480)
@@ -1678,7 +1678,7 @@ void ctx_destroy(sng_ctx* c) {
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); }
-    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go}) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);
@@ -2262,6 +2262,15 @@ int sng_copy_device(sng_ctx* c, const void* src, void* dst, uint64_t n, void* st
     return guarded([&] {
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    });
+}
+int sng_final_rgba8(sng_ctx* c, int32_t row_begin, int32_t row_end, uint32_t* d_out, void* stream) {
+    return guarded([&] {
+        HIPCHK(hipSetDevice(c->device));
+        const int W = c->mesh_res[0], H = c->mesh_res[1];
+        if (!d_out || row_begin < 0 || row_end > H || row_begin > row_end) throw SngError(SNG_ERR_INVALID, "bad row band");
+        launch_rgba8_band(c->final_rgba.as<float4>() + (size_t)row_begin * W, (uint32_t)((row_end - row_begin) * W), d_out, (hipStream_t)stream);
+        HIPCHK(hipGetLastError());
     });
 }
 int sng_get_rng_states(sng_ctx* c, int which, uint32_t* out, uint64_t n) {

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
 template <bool LIN, int THREADS = 256>
 __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                                                        float* __restrict__ coords, uint2* __restrict__ samp, int store_t, int global_sched) {
-    __shared__ float ts_lds[LIN ? MAX_STEPS_BETWEEN_COMPACTION * 256 : 1];
+    __shared__ float ts_lds[LIN ? MAX_STEPS_BETWEEN_COMPACTION * THREADS : 1];
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t n_sched = global_sched ? ctrl->sched_alive[p] : n_alive;   // Sched
     const uint32_t i_step = ctrl->i_step[p];
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
                     const f3 pos = o + d * t;
                     if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
                     if (occupied_linear(pos, vol.occ_linear)) {
-                        ts_lds[cnt * 256 + threadIdx.x] = t;
+                        ts_lds[cnt * THREADS + threadIdx.x] = t;
                         t += calc_dt(t, 0.0f);
                         ++cnt;
                     } else {
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
             if constexpr (LIN) {
 #pragma unroll 1
                 for (uint32_t j = 0; j < cnt; ++j) {
-                    const float t = ts_lds[j * 256 + threadIdx.x];
+                    const float t = ts_lds[j * THREADS + threadIdx.x];
                     const float dt = calc_dt(t, 0.0f);
                     const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
                     float* c = coords + (size_t)(base + j) * 7;
@@ -242,6 +242,7 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (active) {
             ctrl->total_samples += ctrl->n_samples[p];
+            ctrl->net_samples += ctrl->n_samples[p];
             if (iter < 64) ctrl->samples_hist[iter] = ctrl->n_samples[p];
         }
         ctrl->n_samples[p ^ 1] = 0;
@@ -447,7 +448,7 @@ __global__ void ctrl_init_kernel(MarchCtrl* c) {
         c->n_samples[0] = 0; c->n_samples[1] = 0;
         c->i_step[0] = 1; c->i_step[1] = 1;   // trace_alt: uint32_t i = 1 (2163)
         c->n_hit = 0; c->n_iter = 0;
-        c->total_samples = 0; c->ref_slots = 0;
+        c->total_samples = 0; c->net_samples = 0; c->ref_slots = 0;
     }
 }
 

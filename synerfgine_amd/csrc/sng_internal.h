@@ -42,6 +42,7 @@ struct MarchCtrl {
     uint32_t n_hit;
     uint32_t n_iter;
     unsigned long long total_samples;
+    unsigned long long net_samples;   // samples of the whole-GPU network launches (the rest ran in the fused tail)
     unsigned long long ref_slots;
     uint32_t alive_hist[64];
     uint32_t steps_hist[64];
@@ -222,6 +223,7 @@ void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, ui
                      hipStream_t s);
 // display.hip
 void launch_display(const float4* img, int W, int H, int OW, int OH, f3 clear, uint8_t* out, hipStream_t s);
+void launch_rgba8_band(const float4* img, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
                     const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s);
 void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s);

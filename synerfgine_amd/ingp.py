@@ -50,7 +50,7 @@ def read_ingp(path):
     with open(path, "rb") as f:
         raw = f.read()
     try:
-        raw = zlib.decompress(raw)
+        raw = zlib.decompress(raw, 47)   # 32 + 15: zlib or gzip wrapper (zstr writes gzip), as the C++ loader's inflateInit2(15 + 32)
     except zlib.error:
         pass
     root = msgpack.unpackb(raw, raw=False, strict_map_key=False)

@@ -15,6 +15,9 @@ CONFIGS = {
                                                                             "shadow_on_virtual_obj": 0}),
     "c3": dict(scene="armadillo.json", width=1920, height=1080, overrides={}),
     "c4": dict(scene="kitchen-rocks.json", width=1920, height=1080, overrides={"light_samples": 4}),
+    # the scene of every reference measurement in BASELINE.md (scripts/render/profiling.sh:12-18): lego +
+    # armadillo/bunny/monkey at 1280x720, swept over --sshadows/--nshadows in {1,2,4,8}
+    "abm": dict(scene="dmrf-compare-abm.json", width=1280, height=720, overrides={}),
 }
 
 # the trained lego snapshot (tools/train_lego.py on data/nerf/lego400, the reference's lego set); configs

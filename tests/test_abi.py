@@ -146,3 +146,28 @@ def test_ingp_probe_errors_are_loud(lib, tmp_path):
     assert lib.sng_last_error()
     rc = lib.sng_snapshot_probe(str(tmp_path / "missing.ingp").encode(), None, None, None, None, 0, None, 0)
     assert rc != 0
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """The ctypes mirrors in synerfgine_amd/_lib.py have the C layout of include/sng.h (sizes and every
+    field offset), compiled here with gcc."""
+    from synerfgine_amd import _lib
+    structs = [n for n in dir(_lib) if n.startswith("sng_") and isinstance(getattr(_lib, n), type)
+               and issubclass(getattr(_lib, n), ctypes.Structure)]
+    assert "sng_frame_result" in structs
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for s in structs:
+        lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
+        for f in getattr(_lib, s)._fields_:
+            lines.append(f'printf("{s}.{f[0]} %zu\\n", offsetof({s}, {f[0]}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines())
+    for s in structs:
+        cls = getattr(_lib, s)
+        assert int(got[s]) == ctypes.sizeof(cls), s
+        for f in cls._fields_:
+            assert int(got[f"{s}.{f[0]}"]) == getattr(cls, f[0]).offset, f"{s}.{f[0]}"

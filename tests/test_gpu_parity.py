@@ -410,3 +410,33 @@ def test_fused_nerf_kernel_equals_wavefront(config, ngp_mode):
         assert out[0][1:] == out[1][1:]
     finally:
         tb.close()
+
+
+@pytest.mark.parametrize("config,target", [("c3", 3000), ("c4", 100000)])
+def test_mid_frame_switch_to_fused_tail_is_exact(config, target):
+    """With a small query target the march starts with short iterations and hands over to the fused tail in
+    the middle of the frame (capi.cpp trace_nerf: at a chunk boundary, once n_alive * 8 <= target); the
+    result, statistics and per-iteration histograms equal the pure wavefront's bit for bit -- for the linear
+    lego-like generate and the cascaded kitchen-like one, with shadows and the mesh on (RNG streams rewound
+    between the two renders)."""
+    tb, eng, _ = _engine(160, 90, {}, config)
+    try:
+        n0, m0 = eng.rng_states(0).copy(), eng.rng_states(1).copy()
+        out = {}
+        for fused in (0, 1):
+            eng.set_rng_states(0, n0)
+            eng.set_rng_states(1, m0)
+            eng.set_param("nerf_fused", fused)
+            r = eng.frame(target_n_queries=target)
+            if fused:
+                assert 1 < r.fused_from_iter < r.n_iterations, (r.fused_from_iter, r.n_iterations)
+            else:
+                assert r.fused_from_iter == r.n_iterations
+            out[fused] = ([r.download(b) for b in ("final_rgba", "nerf_rgba", "nerf_depth", "nerf_positions")],
+                          (r.n_samples, r.n_hit, r.n_iterations, r.n_reference_slots), list(r.alive_per_iter), list(r.steps_per_iter),
+                          list(r.samples_per_iter))
+        for a, b in zip(out[0][0], out[1][0]):
+            assert np.array_equal(a, b)
+        assert out[0][1:] == out[1][1:]
+    finally:
+        tb.close()
