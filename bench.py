@@ -298,8 +298,10 @@ def main():
     ms_net = sum(s.ms_network for s in stats)
     launches = sum(s.network_launches for s in stats)
     samples = sum(s.n_samples_network for s in stats)
-    total_samples = sum(s.n_samples for s in stats)
-    tail_samples = total_samples - samples
+    total_samples = sum(s.n_samples for s in stats)          # march samples composited
+    reused = sum(s.n_samples_reused for s in stats)         # of which taken from the boundary-sample cache
+    evaluated = total_samples - reused                      # network evaluations (launches + fused tail)
+    tail_samples = evaluated - samples
     ms_tail = sum(s.ms_fused_tail for s in stats)
     avg_launch_ms = ms_net / max(1, launches)
     bytes_per_launch = samples * BYTES_PER_SAMPLE / max(1, launches)
@@ -307,7 +309,7 @@ def main():
     tflops = samples * FLOPS_PER_SAMPLE / (ms_net * 1e-3) / 1e12 if ms_net > 0 else 0.0
     tail_gbs = tail_samples * BYTES_PER_SAMPLE / (ms_tail * 1e-3) / 1e9 if ms_tail > 0 else 0.0
     field_ms = ms_net + ms_tail
-    field_gbs = total_samples * BYTES_PER_SAMPLE / (field_ms * 1e-3) / 1e9 if field_ms > 0 else 0.0
+    field_gbs = evaluated * BYTES_PER_SAMPLE / (field_ms * 1e-3) / 1e9 if field_ms > 0 else 0.0
     prof = traffic_profile(args.config)
     traffic = None
     if prof:
@@ -340,7 +342,8 @@ def main():
                        "tiles": f"{world} horizontal bands (rows {bounds}) + " +
                                 (("RCCL" if on_dev else "gloo") + " all_gather of RGBA8 tiles" if world > 1 else "no gather"),
                        "step_schedule": "band-local" if (world > 1 and args.local_schedule) else ("frame-wide (per-iteration alive-count all-reduce)" if world > 1 else "frame-wide"),
-                       "samples_per_frame": int(s0.n_samples), "reference_slots_per_frame": int(s0.n_reference_slots),
+                       "samples_per_frame": int(s0.n_samples), "samples_reused_per_frame": int(s0.n_samples_reused),
+                       "reference_slots_per_frame": int(s0.n_reference_slots),
                        "wavefront_iterations": int(s0.n_iterations), "fused_tail_from_iteration": int(s0.fused_from_iter),
                        "hit_rays": int(s0.n_hit)},
             "comm": comm,
@@ -362,7 +365,7 @@ def main():
                                         "ms": round(ms_tail, 4), "achieved": round(tail_gbs, 1), "frac": round(tail_gbs / HBM_PEAK_GBS, 4),
                                         "timing": "hipEvents around the tail launch (it runs beside the raytracer on reserved CUs in the "
                                                   "concurrent schedule, so its duration is latency, not throughput)"},
-                         "field_sample_weighted": {"samples": int(total_samples), "ms": round(field_ms, 4), "achieved": round(field_gbs, 1),
+                         "field_sample_weighted": {"samples": int(evaluated), "ms": round(field_ms, 4), "achieved": round(field_gbs, 1),
                                                    "frac": round(field_gbs / HBM_PEAK_GBS, 4)}},
         }
     if rank == 0 and not args.no_cpu_baseline and world == 1:

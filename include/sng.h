@@ -80,7 +80,7 @@ typedef struct {
     /* statistics */
     uint32_t n_iterations;    /* wavefront iterations of trace_alt */
     uint32_t n_hit;           /* rays that reached the hit list */
-    uint64_t n_samples;       /* network samples evaluated (real, compacted) */
+    uint64_t n_samples;       /* march samples composited (real, compacted; equals the reference's real samples) */
     uint64_t n_reference_slots; /* slots the reference would evaluate (incl. stale + padding) */
     float ms_frame;           /* device time of the whole frame (hipEvents) */
     float ms_raytrace, ms_nerf, ms_shadow, ms_overlay;
@@ -93,7 +93,9 @@ typedef struct {
     uint64_t n_samples_network; /* samples of the whole-GPU network launches (device counter); the other
                                    n_samples - n_samples_network were evaluated inside the fused tail */
     float ms_fused_tail;        /* device time of the fused tail launch (collect_kernel_times) */
-    int32_t reserved[3];
+    uint64_t n_samples_reused;  /* march samples whose network output was reused, not evaluated: trace_alt's t reset
+                                   (testbed_nerf.cu:574) makes an iteration's first sample the previous one's last */
+    int32_t reserved[2];
 } sng_frame_result;
 
 typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;

@@ -152,7 +152,7 @@ class FrameResult:
         self.raw = r
         for name in ("n_iterations", "n_hit", "n_samples", "n_reference_slots", "ms_frame", "ms_raytrace", "ms_nerf", "ms_shadow",
                      "ms_overlay", "ms_network", "network_launches",
-                     "fused_from_iter", "n_samples_network", "ms_fused_tail"):
+                     "fused_from_iter", "n_samples_network", "ms_fused_tail", "n_samples_reused"):
             setattr(self, name, getattr(r, name))
         self.alive_per_iter = list(r.alive_per_iter)[: min(64, r.n_iterations)]
         self.steps_per_iter = list(r.steps_per_iter)[: min(64, r.n_iterations)]

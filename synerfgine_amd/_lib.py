@@ -81,7 +81,8 @@ class sng_frame_result(ctypes.Structure):
         ("fused_from_iter", ctypes.c_uint32),
         ("n_samples_network", ctypes.c_uint64),
         ("ms_fused_tail", ctypes.c_float),
-        ("reserved", ctypes.c_int32 * 3),
+        ("n_samples_reused", ctypes.c_uint64),
+        ("reserved", ctypes.c_int32 * 2),
     ]
 
 

@@ -446,7 +446,7 @@ struct sng_ctx {
 
     // buffers
     DevBuf nerf_rgba, nerf_depth, nerf_pos, nerf_nrm;
-    DevBuf ray_ot[2], ray_di[2], ray_rgba[2], ray_depth[2], ray_mw[2];
+    DevBuf ray_ot[2], ray_di[2], ray_rgba[2], ray_depth[2], ray_mw[2], ray_lt[2], ray_lo[2];
     DevBuf samp, coords, net_out, ctrl;
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
@@ -957,6 +957,8 @@ void resize(sng_ctx* c) {
         c->ray_rgba[b].ensure(nn * 16);
         c->ray_depth[b].ensure(nn * 4);
         c->ray_mw[b].ensure(nn * 4);
+        c->ray_lt[b].ensure(nn * 8);
+        c->ray_lo[b].ensure(nn * 8);
     }
     c->samp.ensure(nn * 8);
     c->ray_cap = nn;
@@ -1053,7 +1055,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     uint32_t* const sched_src = gsched ? &ctrl->sched_alive[0] : &ctrl->n_alive[0];   // counts the host loop reads
     RayBuf rb[2];
     for (int b = 0; b < 2; ++b)
-        rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>()};
+        rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>(),
+                 c->ray_lt[b].as<float2>(), c->ray_lo[b].as<uint2>()};
     launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
     reduce_sched(0);
     const uint32_t n_band = (uint32_t)(tr1 - tr0) * (uint32_t)NW;
@@ -1147,6 +1150,7 @@ void march_stats(const sng_ctx* c, const sng_frame_params& P, sng_frame_result* 
     out->n_hit = c->h_ctrl->n_hit;
     out->n_samples = c->h_ctrl->total_samples;
     out->n_samples_network = c->h_ctrl->net_samples;
+    out->n_samples_reused = c->h_ctrl->reused_samples;
     out->fused_from_iter = c->fused_last ? c->fused_k0 : c->h_ctrl->n_iter;
     out->n_reference_slots = ref_slots_of(c);
     std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
@@ -1677,7 +1681,7 @@ void ctx_destroy(sng_ctx* c) {
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
-    for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); }
+    for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);

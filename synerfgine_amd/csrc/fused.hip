@@ -47,12 +47,12 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     __shared__ uint2 out_lds[FUSED_WAVES][64 * MAX_STEPS_BETWEEN_COMPACTION];
     __shared__ uint32_t hist_alive[64], hist_samples[64];
     __shared__ uint32_t blk_hit, blk_iter;
-    __shared__ unsigned long long blk_samples;
+    __shared__ unsigned long long blk_samples, blk_reused;
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int g = lane >> 4, col = lane & 15;
     if (threadIdx.x < 64) { hist_alive[threadIdx.x] = 0; hist_samples[threadIdx.x] = 0; }
-    if (threadIdx.x == 0) { blk_hit = 0; blk_iter = 0; blk_samples = 0; }
+    if (threadIdx.x == 0) { blk_hit = 0; blk_iter = 0; blk_samples = 0; blk_reused = 0; }
     __syncthreads();
 
     const Volume& vol = a.vol;
@@ -76,7 +76,10 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     float4 rgba = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     uint32_t idx = 0, k = 0, istep = 0;
     uint32_t my_hits = 0, my_iter = 0;
-    unsigned long long my_samples = 0;
+    unsigned long long my_samples = 0, my_reused = 0;
+    // trace_alt boundary-sample cache (RayBuf::lt/lo): the previous iteration's last sample t and output
+    float lt = 0.0f;
+    uint2 lo = make_uint2(0u, 0u);
 
     while (true) {
         // ---- refill empty lanes from the ray queue (one atomic per wave)
@@ -98,6 +101,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
                         rgba = a.rays.rgba[r];
                         depth = a.rays.depth[r];
                         mw = a.mode.ngp ? a.rays.mw[r] : 0.0f;
+                        if (!a.mode.ngp) { lt = a.rays.lt[r].x; lo = a.rays.lo[r]; }
                         k = k0;
                         istep = i_step0;
                         has = true;
@@ -109,6 +113,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
 
         // ---- generate: up to 8 samples (generate_next_nerf_network_inputs, testbed_nerf.cu:790-837)
         uint32_t cnt = 0;
+        bool reuse = false;
         const uint32_t n_steps = MAX_STEPS_BETWEEN_COMPACTION;
         if (has) {
             const f3 idir = inv(d);
@@ -118,6 +123,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
                     const f3 pos = o + d * t;
                     if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
                     if (occupied_linear(pos, vol.occ_linear)) {
+                        if (cnt == 0 && !a.mode.ngp && t == lt) reuse = true;
                         ts_lds[wv][cnt][lane] = t;
                         t += calc_dt(t, 0.0f);
                         ++cnt;
@@ -133,18 +139,23 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
                     ts_lds[wv][cnt][lane] = t;
                     t += calc_dt(t, cone);
                 }
+                reuse = cnt > 0 && !a.mode.ngp && ts_lds[wv][0][lane] == lt;
             }
             ray_lds[wv][lane][0] = make_float4(o.x, o.y, o.z, 0.0f);
             ray_lds[wv][lane][1] = make_float4(d.x, d.y, d.z, 0.0f);
             if (k < 64) atomicAdd(&hist_alive[k], 1u);
             if (istep >= MARCH_ITER) cnt = 0;   // unreachable: `last` retires rays first
         }
-        const uint32_t incl = wave_incl_scan_u(cnt, lane);
+        // the network evaluates only the samples not taken from the boundary cache
+        const uint32_t ru = reuse ? 1u : 0u;
+        const uint32_t ncnt = cnt - ru;
+        const uint32_t incl = wave_incl_scan_u(ncnt, lane);
         const uint32_t total = __shfl(incl, 63, 64);
-        const uint32_t sbase = incl - cnt;
-        for (uint32_t j = 0; j < cnt; ++j) own_lds[wv][sbase + j] = (uint16_t)((lane << 3) | j);
+        const uint32_t sbase = incl - ncnt;
+        for (uint32_t j = ru; j < cnt; ++j) own_lds[wv][sbase + j - ru] = (uint16_t)((lane << 3) | j);
         if (has && k < 64 && cnt) atomicAdd(&hist_samples[k], cnt);
         my_samples += cnt;
+        my_reused += ru;
         wave_sync();
 
         // ---- field on the wave's samples, 16 per tile
@@ -172,8 +183,10 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
         if (has) {
             const bool last = istep + n_steps >= MARCH_ITER;
             uint32_t j = 0;
+            uint2 last_raw = lo;
             for (; j < cnt; ++j) {
-                const uint2 raw = out_lds[wv][sbase + j];
+                const uint2 raw = (reuse && j == 0) ? lo : out_lds[wv][sbase + j - ru];
+                last_raw = raw;
                 const float ts = ts_lds[wv][j][lane];
                 const f3 wp = ((o + d * ts) - vol.train_aabb.lo) / wdiag;
                 const float cdt = warp_dt(calc_dt(ts, cone));
@@ -210,7 +223,10 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
             }
             // trace_alt resets t to the last sample (574); trace keeps generate's t (836) -- in
             // the flattened march t already is generate's end value when all 8 steps were taken
-            if (!a.mode.ngp) t = depth / dot(cam.c2, d);
+            if (!a.mode.ngp) {
+                t = depth / dot(cam.c2, d);
+                if (cnt) { lt = ts_lds[wv][cnt - 1][lane]; lo = last_raw; }   // survivors composited all cnt samples
+            }
             bool hit = false;
             if (j < n_steps) {
                 hit = !last && rgba.w > 0.001f;
@@ -251,6 +267,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     atomicAdd(&blk_hit, my_hits);
     atomicMax(&blk_iter, my_iter);
     atomicAdd(&blk_samples, my_samples);
+    if (my_reused) atomicAdd(&blk_reused, my_reused);
     __syncthreads();
     if (threadIdx.x < 64) {
         if (hist_alive[threadIdx.x]) atomicAdd(&a.ctrl->alive_hist[threadIdx.x], hist_alive[threadIdx.x]);
@@ -260,6 +277,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
         atomicAdd(&a.ctrl->n_hit, blk_hit);
         atomicMax(&a.ctrl->n_iter, blk_iter);
         atomicAdd(&a.ctrl->total_samples, blk_samples);
+        if (blk_reused) atomicAdd(&a.ctrl->reused_samples, blk_reused);
     }
 }
 

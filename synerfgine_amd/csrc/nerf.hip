@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
         out.rgba[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // memset(m_rays[0].rgba) 2102
         out.depth[slot] = 0.0f;                                // memset(m_rays[0].depth) 2103
         if (a.mode.ngp) out.mw[slot] = 0.0f;                   // payload.max_weight = 0 (1964)
+        else out.lt[slot] = make_float2(__int_as_float(0x7fc00000), 0.0f);   // no cached boundary sample yet
     }
 }
 
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
     for (uint32_t blk = blockIdx.x * blockDim.x; blk < n_alive; blk += gridDim.x * blockDim.x) {
         const uint32_t i = blk + threadIdx.x;
         uint32_t cnt = 0;
+        bool reuse = false;
         float ts[LIN ? 1 : MAX_STEPS_BETWEEN_COMPACTION];
         f3 o = splat(0.0f), d = splat(1.0f);
         if (i < n_alive) {
@@ -163,6 +165,10 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
             d = mk(di.x, di.y, di.z);
             const f3 idir = inv(d);
             float t = ot.w;
+            // trace_alt: the previous iteration's last sample (t and output) -- if this iteration's first
+            // sample lands on the same t, its NerfCoordinate is bit-identical and so is the network output
+            const float lt0 = store_t ? __int_as_float(0x7fc00000) : rays.lt[i].x;
+            float tl = 0.0f;
             if constexpr (LIN) {
                 // advance_to_occupied_linear + sample, flattened into ONE loop: each trip either
                 // records a sample (occupied voxel) or takes one DDA step, so a lane's cost is its
@@ -173,7 +179,9 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
                     const f3 pos = o + d * t;
                     if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
                     if (occupied_linear(pos, vol.occ_linear)) {
+                        if (cnt == 0 && t == lt0) reuse = true;
                         ts_lds[cnt * THREADS + threadIdx.x] = t;
+                        tl = t;
                         t += calc_dt(t, 0.0f);
                         ++cnt;
                     } else {
@@ -187,37 +195,41 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
                         t = advance_to_occupied(t, cone, o, d, idir, 0, vol.max_mip, vol);
                         if (t < MAX_DEPTH) {
                             ts[j] = t;
+                            tl = t;
                             t += calc_dt(t, cone);
                             ++cnt;
                         }
                     }
                 }
+                reuse = cnt > 0 && ts[0] == lt0;
             }
             // NerfTracer::trace keeps generate's t (payload.t = t after n_steps samples, 836);
             // trace_alt overwrites it in the compositor
             if (store_t && cnt == n_steps) reinterpret_cast<float*>(rays.o_t + i)[3] = t;
+            if (!store_t && cnt) rays.lt[i] = make_float2(lt0, tl);
         }
-        const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], cnt, nullptr, false, nullptr, false, sh_app, lane);
+        const uint32_t ru = reuse ? 1u : 0u;
+        const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], cnt - ru, &ctrl->n_reused[p], reuse, nullptr, false, sh_app, lane);
         if (i < n_alive) {
-            samp[i] = make_uint2(base, cnt);
+            samp[i] = make_uint2(base, cnt | (ru << 31));
             const f3 wd = (d + 1.0f) * 0.5f;
             if constexpr (LIN) {
 #pragma unroll 1
-                for (uint32_t j = 0; j < cnt; ++j) {
+                for (uint32_t j = ru; j < cnt; ++j) {
                     const float t = ts_lds[j * THREADS + threadIdx.x];
                     const float dt = calc_dt(t, 0.0f);
                     const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
-                    float* c = coords + (size_t)(base + j) * 7;
+                    float* c = coords + (size_t)(base + j - ru) * 7;
                     c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
                 }
             } else {
 #pragma unroll
                 for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
-                    if (j < cnt) {
+                    if (j < cnt && j >= ru) {
                         const float t = ts[j];
                         const float dt = calc_dt(t, cone);
                         const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
-                        float* c = coords + (size_t)(base + j) * 7;
+                        float* c = coords + (size_t)(base + j - ru) * 7;
                         c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
                     }
                 }
@@ -241,11 +253,13 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
     const bool active = n_sched > 0 && i_step < MARCH_ITER;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (active) {
-            ctrl->total_samples += ctrl->n_samples[p];
+            ctrl->total_samples += ctrl->n_samples[p] + ctrl->n_reused[p];
             ctrl->net_samples += ctrl->n_samples[p];
-            if (iter < 64) ctrl->samples_hist[iter] = ctrl->n_samples[p];
+            ctrl->reused_samples += ctrl->n_reused[p];
+            if (iter < 64) ctrl->samples_hist[iter] = ctrl->n_samples[p] + ctrl->n_reused[p];
         }
         ctrl->n_samples[p ^ 1] = 0;
+        ctrl->n_reused[p ^ 1] = 0;
     }
     if (!active) return;
     const uint32_t n_steps = steps_for(n_sched, target);
@@ -259,6 +273,8 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
         bool survive = false, hit = false;
         float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
         float depth = 0.0f, mw = 0.0f;
+        float2 lt = make_float2(0.0f, 0.0f);
+        uint2 last_raw = make_uint2(0u, 0u);
         uint32_t death_step = 0;
         if (i < n_alive) {
             rgba = in.rgba[i];
@@ -266,14 +282,28 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
             ot = in.o_t[i];
             di = in.d_idx[i];
             if (mode.ngp) mw = in.mw[i];
+            else lt = in.lt[i];
             const uint2 sc = samp[i];
+            const uint32_t cnt = sc.y & 0x7fffffffu, ru = sc.y >> 31;
             uint32_t j = 0;
-            for (; j < sc.y; ++j) {
-                const uint2 raw = net_out[sc.x + j];
-                const float* c = coords + (size_t)(sc.x + j) * 7;
-                const f3 pos = vol.train_aabb.lo + mk(c[0], c[1], c[2]) * diag;
+            for (; j < cnt; ++j) {
+                uint2 raw;
+                f3 pos;
+                float dt;
+                const bool cached = ru && j == 0;
+                const float* c = coords + (cached ? (size_t)0 : (size_t)sc.x + j - ru) * 7;   // c unused when cached (trace_alt)
+                if (cached) {   // the cached boundary sample: generate_kernel's expressions on its t
+                    raw = in.lo[i];
+                    const f3 wp = ((mk(ot.x, ot.y, ot.z) + mk(di.x, di.y, di.z) * lt.x) - vol.train_aabb.lo) / diag;
+                    pos = vol.train_aabb.lo + wp * diag;
+                    dt = unwarp_dt(warp_dt(calc_dt(lt.x, vol.cone)));
+                } else {
+                    raw = net_out[sc.x + j - ru];
+                    pos = vol.train_aabb.lo + mk(c[0], c[1], c[2]) * diag;
+                    dt = unwarp_dt(c[3]);
+                }
+                last_raw = raw;
                 const float T = 1.f - rgba.w;
-                const float dt = unwarp_dt(c[3]);
                 const float r = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x & 0xffffu));
                 const float g = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x >> 16));
                 const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y & 0xffffu));
@@ -317,6 +347,7 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
             out.rgba[slot] = rgba;
             out.depth[slot] = depth;
             if (mode.ngp) out.mw[slot] = mw;
+            else { out.lt[slot] = make_float2(lt.y, 0.0f); out.lo[slot] = last_raw; }
         }
         if (hit && mode.ngp) {
             // shade_kernel_nerf (1788-1828), gbuffer_hard_edges = false, train_in_linear_colors = false
@@ -446,9 +477,10 @@ __global__ void ctrl_init_kernel(MarchCtrl* c) {
         c->n_owned[0] = 0; c->n_owned[1] = 0;
         c->sched_alive[0] = 0; c->sched_alive[1] = 0;
         c->n_samples[0] = 0; c->n_samples[1] = 0;
+        c->n_reused[0] = 0; c->n_reused[1] = 0;
         c->i_step[0] = 1; c->i_step[1] = 1;   // trace_alt: uint32_t i = 1 (2163)
         c->n_hit = 0; c->n_iter = 0;
-        c->total_samples = 0; c->net_samples = 0; c->ref_slots = 0;
+        c->total_samples = 0; c->net_samples = 0; c->ref_slots = 0; c->reused_samples = 0;
     }
 }
 

@@ -37,13 +37,15 @@ struct MarchCtrl {
     uint32_t n_alive[2];
     uint32_t n_owned[2];      // alive rays of the band's own rows (Sched::own_lo/hi), counted when Sched::global
     uint32_t sched_alive[2];  // frame-wide alive count (sum of n_owned over ranks) the step schedule uses
-    uint32_t n_samples[2];
+    uint32_t n_samples[2];    // network samples of the iteration (appended by generate)
+    uint32_t n_reused[2];     // boundary samples of the iteration that reuse the previous iteration's output
     uint32_t i_step[2];
     uint32_t n_hit;
     uint32_t n_iter;
     unsigned long long total_samples;
     unsigned long long net_samples;   // samples of the whole-GPU network launches (the rest ran in the fused tail)
     unsigned long long ref_slots;
+    unsigned long long reused_samples;   // march samples taken from the ray's cached output (no network evaluation)
     uint32_t alive_hist[64];
     uint32_t steps_hist[64];
     uint32_t samples_hist[64];
@@ -56,6 +58,10 @@ struct RayBuf {
     float4* rgba;
     float* depth;
     float* mw;         // payload.max_weight (instant-NGP trace path only)
+    // trace_alt boundary-sample cache: the t reset (composite_kernel_nerf_alt:574) makes the next
+    // iteration's first sample the previous iteration's last one, bit for bit in the common case.
+    float2* lt;        // x: t of the previous iteration's last sample (NaN: none); y: this iteration's (generate)
+    uint2* lo;         // raw fp16 (r, g, b, density) network output of that sample
 };
 
 // Which NeRF tracer runs: SyNeRFgine's trace_alt (ngp = 0: depth of the last sample,
