@@ -345,6 +345,7 @@ def main():
                        "samples_per_frame": int(s0.n_samples), "samples_reused_per_frame": int(s0.n_samples_reused),
                        "reference_slots_per_frame": int(s0.n_reference_slots),
                        "wavefront_iterations": int(s0.n_iterations), "fused_tail_from_iteration": int(s0.fused_from_iter),
+                       "onestep_regime": [int(s0.onestep_from_iter), int(s0.onestep_iterations)],
                        "hit_rays": int(s0.n_hit)},
             "comm": comm,
             "streams": "serialized (raytracer then NeRF)" if args.serial_streams else

@@ -95,7 +95,9 @@ typedef struct {
     float ms_fused_tail;        /* device time of the fused tail launch (collect_kernel_times) */
     uint64_t n_samples_reused;  /* march samples whose network output was reused, not evaluated: trace_alt's t reset
                                    (testbed_nerf.cu:574) makes an iteration's first sample the previous one's last */
-    int32_t reserved[2];
+    uint32_t onestep_from_iter; /* trace_alt's one-step regime (n_alive > target/2) marched ray-locally from this
+                                   iteration (n_iterations: none) ... */
+    uint32_t onestep_iterations;/* ... for this many iterations */
 } sng_frame_result;
 
 typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;

@@ -82,7 +82,8 @@ class sng_frame_result(ctypes.Structure):
         ("n_samples_network", ctypes.c_uint64),
         ("ms_fused_tail", ctypes.c_float),
         ("n_samples_reused", ctypes.c_uint64),
-        ("reserved", ctypes.c_int32 * 2),
+        ("onestep_from_iter", ctypes.c_uint32),
+        ("onestep_iterations", ctypes.c_uint32),
     ]
 
 

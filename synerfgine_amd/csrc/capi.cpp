@@ -386,6 +386,7 @@ const std::map<std::string, double>& default_params() {
                                                 //   uncontended network launch, then the ray-local tail; measured best)
         {"nerf_fused_lanes", 64},               // rays per wave in the fused kernel
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
+        {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
     };
     return d;
 }
@@ -396,7 +397,7 @@ struct sng_ctx {
     int device = 0;
     int n_cus = 256;
     hipStream_t s_nerf = nullptr, s_rt = nullptr;
-    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr, ev_fused0 = nullptr, ev_fused1 = nullptr;
+    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr, ev_fused0 = nullptr, ev_fused1 = nullptr, ev_os0 = nullptr, ev_os1 = nullptr;
     std::vector<hipEvent_t> net_events;
 
     // model
@@ -457,6 +458,9 @@ struct sng_ctx {
     DevBuf rt_hits, rt_rays, rt_next_pos, rt_tail, rt_counters;   // staged path tracer
     bool fused_last = false;               // the last trace finished in the fused kernel
     uint32_t fused_k0 = 0;                 // ... from this iteration on
+    DevBuf os_hist, os_state;              // one-step regime: death / no-sample histograms, OnestepState
+    OnestepState* h_os = nullptr;          // pinned readback of the regime's length
+    bool os_ran = false;                   // the last trace ran a one-step regime (ev_os0 .. ev_os1)
     uint64_t rt_tile_key = 0;             // band geometry the costs belong to
     DevBuf rng_nerf, rng_mesh;
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
@@ -1081,7 +1085,61 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     uint32_t iter = 0;
     int chunk = 0;
     bool done = false;
+    // trace_alt's one-step regime (fused.hip): tried at the first chunk boundary at which the alive
+    // count may still exceed target / 2 (the boundary-sample caches are warm by then)
+    bool os_open = !mode.ngp && c->p("nerf_onestep") != 0.0;
+    c->os_ran = false;
+    // an upper bound of the current (schedule) alive count from the chunk readbacks; unknown before the first.
+    // Every input of the decision is frame-wide, so all ranks of a banded frame take the same branch.
+    uint32_t known_alive = UINT32_MAX;
     while (!done && iter < MARCH_ITER) {
+        if (os_open && chunk >= 1 && !fuse && 2ull * known_alive > target) {
+            os_open = false;   // the count only shrinks: once the regime is over (or never was) it stays over
+            HIPCHK(hipMemcpyAsync(c->h_ctrl, ctrl, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
+            HIPCHK(hipStreamSynchronize(c->s_nerf));
+            const MarchCtrl& hc = *c->h_ctrl;
+            const uint32_t ns = gsched ? hc.sched_alive[p] : hc.n_alive[p];
+            if (ns > 0 && hc.i_step[p] < MARCH_ITER && steps_for(ns, target) == 1) {
+                c->os_hist.ensure((size_t)3 * ONESTEP_HIST * 4);
+                c->os_state.ensure(sizeof(OnestepState));
+                OnestepArgs oa{};
+                oa.vol = vol; oa.cam = cam; oa.sched = a.sched; oa.in = rb[p]; oa.out = rb[p ^ 1]; oa.ctrl = ctrl;
+                oa.os = c->os_state.as<OnestepState>();
+                oa.deaths_local = c->os_hist.as<uint32_t>();
+                oa.deaths_sched = oa.deaths_local + ONESTEP_HIST;
+                oa.nosample = oa.deaths_local + 2 * ONESTEP_HIST;
+                oa.wfrag = c->net.wfrag; oa.grid_params = c->net.grid; oa.levels = c->net.levels;
+                oa.frame_rgba = c->nerf_rgba.as<float4>(); oa.frame_depth = c->nerf_depth.as<float>(); oa.positions = c->nerf_pos.as<float>();
+                oa.p = p; oa.target = target;
+                if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_os0, c->s_nerf));
+                launch_onestep_begin(oa, iter, c->s_nerf);
+                launch_onestep_pass(oa, c->net, 0, hc.n_alive[p], c->s_nerf);
+                HIPCHK(hipGetLastError());
+                if (gsched) {   // the frame-wide schedule: own-row deaths summed over the ranks
+                    if (c->sched_comm.comm) {
+                        comm_allreduce_u32(c->sched_comm, oa.deaths_sched, ONESTEP_HIST, c->s_nerf);
+                    } else {
+                        std::vector<uint32_t> h(ONESTEP_HIST);
+                        HIPCHK(hipMemcpyAsync(h.data(), oa.deaths_sched, ONESTEP_HIST * 4, hipMemcpyDeviceToHost, c->s_nerf));
+                        HIPCHK(hipStreamSynchronize(c->s_nerf));
+                        if (c->sched_comm.host_fn(h.data(), ONESTEP_HIST, c->sched_comm.host_user) != 0) throw SngError(SNG_ERR_STATE, "schedule reducer failed");
+                        HIPCHK(hipMemcpyAsync(oa.deaths_sched, h.data(), ONESTEP_HIST * 4, hipMemcpyHostToDevice, c->s_nerf));
+                    }
+                }
+                launch_onestep_schedule(oa, c->s_nerf);
+                HIPCHK(hipMemcpyAsync(c->h_os, oa.os, sizeof(OnestepState), hipMemcpyDeviceToHost, c->s_nerf));
+                HIPCHK(hipStreamSynchronize(c->s_nerf));
+                const uint32_t J = c->h_os->J;
+                launch_onestep_pass(oa, c->net, 1, hc.n_alive[p], c->s_nerf);
+                HIPCHK(hipGetLastError());
+                if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_os1, c->s_nerf));
+                c->os_ran = true;
+                reduce_sched(p ^ 1);
+                p ^= 1;
+                iter += J;
+                if (iter >= MARCH_ITER || c->h_os->istep0 + J >= MARCH_ITER) break;
+            }
+        }
         if (fuse && iter >= fuse_after) {
             c->fused_work.ensure(16);
             FusedArgs fa{};
@@ -1128,6 +1186,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // wait for the previous chunk's readback (the current chunk stays queued behind it)
             HIPCHK(hipEventSynchronize(c->ev_nerf1));
             const uint32_t* h = &c->h_alive[2 * ((chunk - 1) & 1)];
+            known_alive = std::max(h[0], h[1]);
             if (h[0] == 0 && h[1] == 0) done = true;
             // once the alive count (it only shrinks) allows 8 steps per iteration, the rest of the march is
             // ray-local: hand it to the fused tail (the count read here is a chunk old, so it bounds the
@@ -1152,6 +1211,8 @@ void march_stats(const sng_ctx* c, const sng_frame_params& P, sng_frame_result* 
     out->n_samples_network = c->h_ctrl->net_samples;
     out->n_samples_reused = c->h_ctrl->reused_samples;
     out->fused_from_iter = c->fused_last ? c->fused_k0 : c->h_ctrl->n_iter;
+    out->onestep_from_iter = c->os_ran ? c->h_os->k : c->h_ctrl->n_iter;
+    out->onestep_iterations = c->os_ran ? c->h_os->J : 0u;
     out->n_reference_slots = ref_slots_of(c);
     std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
     std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
@@ -1170,6 +1231,11 @@ void network_times(sng_ctx* c, const sng_frame_params& P, uint32_t net_launches,
     }
     out->ms_network = tot;
     if (c->fused_last) HIPCHK(hipEventElapsedTime(&out->ms_fused_tail, c->ev_fused0, c->ev_fused1));
+    if (c->os_ran) {   // the one-step regime's ray-local passes count with the fused tail (field evaluations inside a march kernel)
+        float ms = 0.0f;
+        HIPCHK(hipEventElapsedTime(&ms, c->ev_os0, c->ev_os1));
+        out->ms_fused_tail += ms;
+    }
 }
 
 void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out) {
@@ -1658,9 +1724,10 @@ void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_nerf, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_rt, hipStreamNonBlocking, prio_lo));
-    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go, &c->ev_fused0, &c->ev_fused1}) HIPCHK(hipEventCreate(e));
+    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go, &c->ev_fused0, &c->ev_fused1, &c->ev_os0, &c->ev_os1}) HIPCHK(hipEventCreate(e));
     HIPCHK(hipHostMalloc((void**)&c->h_ctrl, sizeof(MarchCtrl), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&c->h_alive, 8 * sizeof(uint32_t), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c->h_os, sizeof(OnestepState), hipHostMallocDefault));
     float rf = fov_to_focal(50.625f);   // Testbed::reset_camera -> set_fov(50.625) (testbed.cu:480)
     c->rel_focal[0] = c->rel_focal[1] = rf;
     // reset_camera matrix: transpose(mat3x4{1,0,0,0.5; 0,-1,0,0.5; 0,0,-1,0.5}), then pos -= scale*dir
@@ -1682,10 +1749,11 @@ void ctx_destroy(sng_ctx* c) {
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); }
-    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1}) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);
+    (void)hipHostFree(c->h_os);
     (void)hipStreamDestroy(c->s_nerf);
     (void)hipStreamDestroy(c->s_rt);
     delete c;

@@ -281,6 +281,447 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     }
 }
 
+// =============================================================================================
+// trace_alt's one-step regime (OnestepArgs, sng_internal.h)
+// =============================================================================================
+//
+// While the frame-wide alive count n exceeds target / 2, trace_alt takes n_steps = 1 per
+// iteration (testbed_nerf.cu:2189-2190) and its t reset (574) sends every ray back to the point it
+// has just sampled: iteration m samples s_m = adv(t_m) (if_unoccupied_advance_to_next_occupied_voxel,
+// 824) and the compositor sets t_{m+1} = g(s_m) = depth(s_m) / dot(fwd, dir).  t -> g(adv(t)) is a
+// fixed float map, so once a ray's start t repeats (t_m == t_{m-P}) its samples -- and their network
+// outputs -- repeat with period P: the ray composites the same P (sample, output) pairs again and
+// again until its opacity passes 1 - min_transmittance.  In C4 (2 M rays alive for ~1100 one-step
+// iterations) nearly every ray is periodic after an iteration or two, with P = 1.
+//
+// Exactness needs the schedule, and under n_steps = 1 a ray's fate does not depend on the others:
+//   pass 0 (speculative): each lane simulates its ray alone under n_steps = 1 until it leaves --
+//          dies, finds no occupied sample, or reaches MARCH_ITER -- evaluating the field only for
+//          samples the ray has not seen in its last 4 iterations; periodic rays finish in a closed
+//          loop over their opacity alone.  The iteration each ray leaves at is histogrammed;
+//   schedule: alive(k + m) = n_k - prefix(deaths); the regime lasts J iterations, J = the first m
+//          whose alive count allows 2 steps (or 0 alive, or MARCH_ITER); the per-iteration statistics
+//          are those the wavefront records;
+//   pass 1 (final): the same simulation stopped at k + J with full compositing; rays leaving before
+//          k + J are extracted exactly as composite_kernel does, survivors are appended to the next
+//          ray buffer with their boundary-sample cache.
+constexpr int OS_P = 4;   // longest orbit closed (start t's remembered)
+
+template <int F, bool FINAL>
+__global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
+    __shared__ float4 ray_lds[FUSED_WAVES][64][2];
+    __shared__ float s_lds[FUSED_WAVES][64];
+    __shared__ uint8_t own_lds[FUSED_WAVES][64];
+    __shared__ uint2 out_lds[FUSED_WAVES][64];
+    __shared__ float4 cyc_lds[FUSED_WAVES][OS_P][64];   // orbit entry: logistic rgb, alpha
+    __shared__ float4 cycd_lds[FUSED_WAVES][OS_P][64];  // orbit entry: depth, sample t, raw output (2 x u32)
+
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int g = lane >> 4, col = lane & 15;
+    const Volume& vol = a.vol;
+    const CamDev& cam = a.cam;
+    OnestepState* os = a.os;
+    const uint32_t n_rays = os->n_local;
+    const uint32_t istep0 = os->istep0;
+    const uint32_t limit = FINAL ? os->J : os->H;   // iterations simulated (relative to k)
+    const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
+    const float cone = vol.cone;
+    const float opaque = 1.0f - vol.min_transmittance;
+    const h8* wfrag = reinterpret_cast<const h8*>(a.wfrag);
+    const _Float16* grid = reinterpret_cast<const _Float16*>(a.grid_params);
+    h8 W[20];
+#pragma unroll
+    for (int f = 0; f < 20; ++f) W[f] = wfrag[f * 64 + lane];
+    const float qnan = __int_as_float(0x7fc00000);
+
+    bool has = false, own = true;
+    f3 o = splat(0.0f), d = splat(1.0f);
+    float t = 0.0f, depth = 0.0f;
+    float4 rgba = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    uint32_t idx = 0, m = 0;
+    float th0 = qnan, th1 = qnan, th2 = qnan, th3 = qnan;   // start t of iterations m-1 .. m-4
+    float sc0 = qnan, sc1 = qnan, sc2 = qnan, sc3 = qnan;   // their samples
+    uint2 oc0 = make_uint2(0u, 0u), oc1 = oc0, oc2 = oc0, oc3 = oc0;   // and raw outputs
+    uint32_t my_evals = 0, my_hits = 0;
+
+    // a ray leaves at relative iteration mm (it is not alive at k + mm + 1)
+    auto record = [&](uint32_t mm, bool nos) {
+        atomicAdd(&a.deaths_local[mm], 1u);
+        if (a.sched.global && own) atomicAdd(&a.deaths_sched[mm], 1u);
+        if (nos) atomicAdd(&a.nosample[mm], 1u);
+    };
+    // composite_kernel's hit path for trace_alt (extract_from_payload, testbed_nerf.cu:1578-1612)
+    auto extract = [&]() {
+        const f3 orig = cam.c3 + d * t;
+        float4 fb = a.frame_rgba[idx];
+        const float ta = rgba.w;
+        const float sr = srgb_to_linear(rgba.x), sg = srgb_to_linear(rgba.y), sb = srgb_to_linear(rgba.z);
+        fb = make_float4(sr + fb.x * (1.0f - ta), sg + fb.y * (1.0f - ta), sb + fb.z * (1.0f - ta), ta + fb.w * (1.0f - ta));
+        a.frame_rgba[idx] = fb;
+        a.positions[3 * idx + 0] = orig.x; a.positions[3 * idx + 1] = orig.y; a.positions[3 * idx + 2] = orig.z;
+        if (ta > 0.2f) a.frame_depth[idx] = depth;
+        ++my_hits;
+    };
+
+    while (true) {
+        // ---- refill empty lanes from the ray queue (one atomic per wave)
+        {
+            const unsigned long long need = __ballot(!has);
+            if (need) {
+                const int leader = __ffsll((long long)need) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&os->work[FINAL ? 1 : 0], (uint32_t)__popcll(need));
+                base = __shfl(base, leader, 64);
+                if (!has) {
+                    const uint32_t r = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+                    if (r < n_rays) {
+                        const float4 ot = a.in.o_t[r], di = a.in.d_idx[r];
+                        o = mk(ot.x, ot.y, ot.z);
+                        t = ot.w;
+                        d = mk(di.x, di.y, di.z);
+                        idx = __float_as_uint(di.w);
+                        own = !a.sched.global || (idx >= a.sched.own_lo && idx < a.sched.own_hi);
+                        rgba = a.in.rgba[r];
+                        depth = a.in.depth[r];
+                        th0 = th1 = th2 = th3 = qnan;
+                        sc0 = a.in.lt[r].x; sc1 = sc2 = sc3 = qnan;   // the wavefront's boundary-sample cache
+                        oc0 = a.in.lo[r];
+                        m = 0;
+                        has = true;
+                    }
+                }
+            }
+        }
+        if (!__ballot(has)) break;
+
+        bool survivor = false;   // FINAL: alive at k + J -> next ray buffer
+        // ---- rays at the end of the span, and periodic rays (closed loop, no field evaluations)
+        if (has) {
+            if (m >= limit) {   // pass 0: unreachable (m = H - 1 is MARCH_ITER's last iteration)
+                survivor = FINAL;
+                has = false;
+            } else {
+                const int P = t == th0 ? 1 : t == th1 ? 2 : t == th2 ? 3 : t == th3 ? 4 : 0;
+                if (P) {
+                    // orbit entry q (0..P-1) = the sample of iteration m - P + q, used at m + q, m + q + P, ...
+                    bool all_zero = true;
+#pragma unroll
+                    for (int q = 0; q < OS_P; ++q) {
+                        if (q < P) {
+                            const int src = P - 1 - q;
+                            const float sq = src == 0 ? sc0 : src == 1 ? sc1 : src == 2 ? sc2 : sc3;
+                            const uint2 raw = src == 0 ? oc0 : src == 1 ? oc1 : src == 2 ? oc2 : oc3;
+                            const float dt = unwarp_dt(warp_dt(calc_dt(sq, cone)));
+                            const f3 wp = ((o + d * sq) - vol.train_aabb.lo) / wdiag;
+                            const f3 pos = vol.train_aabb.lo + wp * wdiag;
+                            const float r = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x & 0xffffu));
+                            const float gg = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x >> 16));
+                            const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y & 0xffffu));
+                            const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
+                            const float alpha = 1.f - sng_expf(-sng_expf(s) * dt);
+                            all_zero = all_zero && alpha == 0.0f;
+                            cyc_lds[wv][q][lane] = make_float4(logistic(r), logistic(gg), logistic(b), alpha);
+                            cycd_lds[wv][q][lane] = make_float4(dot(cam.c2, pos - cam.c3), sq, __uint_as_float(raw.x), __uint_as_float(raw.y));
+                        }
+                    }
+                    const float dfw = dot(cam.c2, d);
+                    uint32_t q = 0;
+                    if (all_zero) {
+                        // weights are exactly 0: rgba never changes, depth is the last composited sample's
+                        if (FINAL) {
+                            q = (limit - 1u - m) % (uint32_t)P;
+                            depth = cycd_lds[wv][q][lane].x;
+                            t = depth / dfw;
+                            survivor = istep0 + limit < MARCH_ITER;   // else dropped in MARCH_ITER's last iteration
+                        }
+                        // pass 0: never opaque; dropped at MARCH_ITER's last iteration, past every schedule decision
+                    } else {
+                        float wprev = rgba.w;
+                        for (uint32_t x = m;; ++x) {
+                            if (x >= limit) {   // FINAL: alive at k + J
+                                survivor = FINAL;
+                                break;
+                            }
+                            const float4 cq = cyc_lds[wv][q][lane];
+                            const bool last = istep0 + x + 1u >= MARCH_ITER;
+                            const float T = 1.f - rgba.w;
+                            const float weight = cq.w * T;
+                            if (FINAL) {
+                                rgba.x += cq.x * weight;
+                                rgba.y += cq.y * weight;
+                                rgba.z += cq.z * weight;
+                            }
+                            rgba.w += weight;
+                            if (rgba.w > opaque) {
+                                if (FINAL) {
+                                    const float aa = rgba.w;
+                                    rgba.x /= aa; rgba.y /= aa; rgba.z /= aa; rgba.w /= aa;
+                                    depth = cycd_lds[wv][q][lane].x;
+                                    t = depth / dfw;
+                                    if (!last) extract();
+                                } else {
+                                    record(x, false);
+                                }
+                                break;
+                            }
+                            if (last) {   // survives its composite but the march ends: dropped
+                                if (!FINAL) record(x, false);
+                                break;
+                            }
+                            if (++q == (uint32_t)P) {
+                                q = 0;
+                                if (!FINAL) {   // opacity unchanged over a whole orbit: it never changes again
+                                    if (rgba.w == wprev) break;
+                                    wprev = rgba.w;
+                                }
+                            }
+                        }
+                        if (FINAL && survivor) {
+                            // alive at k + J: the last composited sample is the orbit entry before q
+                            const uint32_t ql = q == 0 ? (uint32_t)P - 1u : q - 1u;
+                            depth = cycd_lds[wv][ql][lane].x;
+                            t = depth / dfw;
+                        }
+                    }
+                    if (FINAL && survivor) {
+                        const uint32_t ql = (limit - 1u - m) % (uint32_t)P;
+                        const float4 e = cycd_lds[wv][ql][lane];
+                        sc0 = e.y;
+                        oc0 = make_uint2(__float_as_uint(e.z), __float_as_uint(e.w));
+                    }
+                    has = false;
+                }
+            }
+        }
+
+        // ---- stepping rays: one iteration (generate one sample, field if unseen, composite)
+        bool need = false;
+        float s = 0.0f;
+        uint2 out = make_uint2(0u, 0u);
+        if (has) {
+            const f3 idir = inv(d);
+            s = advance_to_occupied(t, cone, o, d, idir, 0, vol.max_mip, vol);
+            if (s >= MAX_DEPTH) {
+                // no occupied sample: the compositor sees cnt = 0 < n_steps and retires the ray
+                const bool last = istep0 + m + 1u >= MARCH_ITER;
+                if (FINAL) {
+                    if (!last && rgba.w > 0.001f) extract();
+                } else {
+                    record(m, true);
+                }
+                has = false;
+            } else if (s == sc0) out = oc0;
+            else if (s == sc1) out = oc1;
+            else if (s == sc2) out = oc2;
+            else if (s == sc3) out = oc3;
+            else need = true;
+        }
+        // ---- field on the wave's unseen samples, 16 per tile (generate_kernel's coordinate expressions)
+        const unsigned long long nb = __ballot(need);
+        if (nb) {
+            const uint32_t total = (uint32_t)__popcll(nb);
+            const uint32_t slot = (uint32_t)__popcll(nb & ((1ull << lane) - 1ull));
+            if (need) {
+                own_lds[wv][slot] = (uint8_t)lane;
+                s_lds[wv][lane] = s;
+                ray_lds[wv][lane][0] = make_float4(o.x, o.y, o.z, 0.0f);
+                ray_lds[wv][lane][1] = make_float4(d.x, d.y, d.z, 0.0f);
+            }
+            wave_sync();
+            for (uint32_t tile = 0; tile * 16 < total; ++tile) {
+                const uint32_t q = tile * 16 + (uint32_t)col;
+                const bool valid = q < total;
+                const uint32_t ol = own_lds[wv][valid ? q : 0];
+                const float4 ro = ray_lds[wv][ol][0], rd = ray_lds[wv][ol][1];
+                const float ts = s_lds[wv][ol];
+                const f3 so = mk(ro.x, ro.y, ro.z), sd = mk(rd.x, rd.y, rd.z);
+                const f3 wp = ((so + sd * ts) - vol.train_aabb.lo) / wdiag;
+                const f3 wd = (sd + 1.0f) * 0.5f;
+                f4v fo, dens;
+                field_tile<F>(W, a.levels, grid, g, wp.x, wp.y, wp.z, wd.x, wd.y, wd.z, fo, dens);
+                if (valid && g == 0) {
+                    const _Float16 r = (_Float16)fo[0], gg = (_Float16)fo[1], b = (_Float16)fo[2], sg = (_Float16)dens[0];
+                    out_lds[wv][q] = make_uint2((uint32_t)__builtin_bit_cast(uint16_t, r) | ((uint32_t)__builtin_bit_cast(uint16_t, gg) << 16),
+                                                (uint32_t)__builtin_bit_cast(uint16_t, b) | ((uint32_t)__builtin_bit_cast(uint16_t, sg) << 16));
+                }
+            }
+            wave_sync();
+            if (need) { out = out_lds[wv][slot]; ++my_evals; }
+            wave_sync();
+        }
+        // ---- composite the stepped sample (composite_kernel_nerf_alt 535-574 with n_steps = 1)
+        if (has) {
+            const bool last = istep0 + m + 1u >= MARCH_ITER;
+            const float dt = unwarp_dt(warp_dt(calc_dt(s, cone)));
+            const f3 wp = ((o + d * s) - vol.train_aabb.lo) / wdiag;
+            const f3 pos = vol.train_aabb.lo + wp * wdiag;
+            const float r = (float)__builtin_bit_cast(_Float16, (uint16_t)(out.x & 0xffffu));
+            const float gg = (float)__builtin_bit_cast(_Float16, (uint16_t)(out.x >> 16));
+            const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(out.y & 0xffffu));
+            const float sg = (float)__builtin_bit_cast(_Float16, (uint16_t)(out.y >> 16));
+            const float T = 1.f - rgba.w;
+            const float alpha = 1.f - sng_expf(-sng_expf(sg) * dt);
+            const float weight = alpha * T;
+            rgba.x += logistic(r) * weight;
+            rgba.y += logistic(gg) * weight;
+            rgba.z += logistic(b) * weight;
+            rgba.w += weight;
+            depth = dot(cam.c2, pos - cam.c3);
+            const float t_start = t;
+            t = depth / dot(cam.c2, d);
+            if (rgba.w > opaque) {
+                if (FINAL) {
+                    const float aa = rgba.w;
+                    rgba.x /= aa; rgba.y /= aa; rgba.z /= aa; rgba.w /= aa;
+                    if (!last) extract();
+                } else {
+                    record(m, false);
+                }
+                has = false;
+            } else if (last) {
+                if (!FINAL) record(m, false);
+                has = false;
+            } else {
+                th3 = th2; th2 = th1; th1 = th0; th0 = t_start;
+                sc3 = sc2; sc2 = sc1; sc1 = sc0; sc0 = s;
+                oc3 = oc2; oc2 = oc1; oc1 = oc0; oc0 = out;
+                ++m;
+            }
+        }
+
+        // ---- FINAL: survivors to the next ray buffer (one atomic per wave)
+        if (FINAL) {
+            const unsigned long long sv = __ballot(survivor);
+            if (sv) {
+                const int leader = __ffsll((long long)sv) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&a.ctrl->n_alive[a.p ^ 1], (uint32_t)__popcll(sv));
+                base = __shfl(base, leader, 64);
+                if (a.sched.global) {
+                    const unsigned long long so = __ballot(survivor && own);
+                    if (so && lane == leader) atomicAdd(&a.ctrl->n_owned[a.p ^ 1], (uint32_t)__popcll(so));
+                }
+                if (survivor) {
+                    const uint32_t slot = base + (uint32_t)__popcll(sv & ((1ull << lane) - 1ull));
+                    a.out.o_t[slot] = make_float4(o.x, o.y, o.z, t);
+                    a.out.d_idx[slot] = make_float4(d.x, d.y, d.z, __uint_as_float(idx));
+                    a.out.rgba[slot] = rgba;
+                    a.out.depth[slot] = depth;
+                    a.out.lt[slot] = make_float2(sc0, 0.0f);
+                    a.out.lo[slot] = oc0;
+                }
+            }
+        }
+    }
+
+    // ---- statistics
+    if (my_evals) atomicAdd(&os->evals[FINAL ? 1 : 0], (unsigned long long)my_evals);
+    if (FINAL) {
+        if (my_hits) atomicAdd(&a.ctrl->n_hit, my_hits);
+        // the schedule counted every regime sample as reused; the final pass's evaluations were not
+        if (my_evals) atomicAdd(&a.ctrl->reused_samples, (unsigned long long)(-(long long)my_evals));
+    }
+}
+
+__global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ONESTEP_HIST; i += gridDim.x * blockDim.x) {
+        a.deaths_local[i] = 0;
+        a.deaths_sched[i] = 0;
+        a.nosample[i] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const MarchCtrl* c = a.ctrl;
+        OnestepState* os = a.os;
+        os->k = k;
+        os->istep0 = c->i_step[a.p];
+        os->n_local = c->n_alive[a.p];
+        os->n_sched = a.sched.global ? c->sched_alive[a.p] : c->n_alive[a.p];
+        os->H = c->i_step[a.p] < MARCH_ITER ? MARCH_ITER - c->i_step[a.p] : 0u;
+        os->J = 0;
+        os->work[0] = 0; os->work[1] = 0;
+        os->evals[0] = 0; os->evals[1] = 0;
+    }
+}
+
+// alive(k + m) = n_k - sum_{x < m} deaths[x]; J = first m in [0, H) whose alive count is 0 or allows
+// more than one step (H: MARCH_ITER).  Statistics as generate/composite record them per iteration.
+__global__ __launch_bounds__(1024) void onestep_schedule_kernel(OnestepArgs a) {
+    constexpr uint32_t CH = ONESTEP_HIST / 1024;
+    __shared__ uint32_t ps[1024], pl[1024];
+    __shared__ uint32_t J_sh;
+    __shared__ unsigned long long slots_sh, samp_sh;
+    OnestepState* os = a.os;
+    MarchCtrl* c = a.ctrl;
+    const uint32_t H = os->H, k = os->k, tid = threadIdx.x;
+    const uint32_t* ds = a.sched.global ? a.deaths_sched : a.deaths_local;
+    const uint32_t b0 = tid * CH;
+    uint32_t ss = 0, sl = 0;
+    for (uint32_t x = 0; x < CH; ++x)
+        if (b0 + x < H) { ss += ds[b0 + x]; sl += a.deaths_local[b0 + x]; }
+    ps[tid] = ss; pl[tid] = sl;
+    if (tid == 0) { J_sh = H; slots_sh = 0; samp_sh = 0; }
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {   // inclusive Hillis-Steele scans
+        const uint32_t vs = tid >= off ? ps[tid - off] : 0u, vl = tid >= off ? pl[tid - off] : 0u;
+        __syncthreads();
+        ps[tid] += vs; pl[tid] += vl;
+        __syncthreads();
+    }
+    uint32_t alive_s = os->n_sched - (ps[tid] - ss);
+    for (uint32_t x = 0; x < CH; ++x) {
+        const uint32_t mm = b0 + x;
+        if (mm >= H) break;
+        if (alive_s == 0 || steps_for(alive_s, a.target) > 1) { atomicMin(&J_sh, mm); break; }
+        alive_s -= ds[mm];
+    }
+    __syncthreads();
+    const uint32_t J = J_sh;
+    uint32_t alive_l = os->n_local - (pl[tid] - sl);
+    unsigned long long slots = 0, samp = 0;
+    for (uint32_t x = 0; x < CH; ++x) {
+        const uint32_t mm = b0 + x;
+        if (mm >= J) break;
+        const uint32_t sm = alive_l - a.nosample[mm];
+        slots += ((unsigned long long)alive_l + 255ull) / 256ull * 256ull;
+        samp += sm;
+        if (k + mm < 64) { c->alive_hist[k + mm] = alive_l; c->steps_hist[k + mm] = 1; c->samples_hist[k + mm] = sm; }
+        alive_l -= a.deaths_local[mm];
+    }
+    if (slots) atomicAdd(&slots_sh, slots);
+    if (samp) atomicAdd(&samp_sh, samp);
+    __syncthreads();
+    if (tid == 0) {
+        c->ref_slots += slots_sh;
+        c->total_samples += samp_sh;
+        c->reused_samples += samp_sh;   // the final pass subtracts its field evaluations
+        c->n_iter = k + J;
+        c->i_step[a.p ^ 1] = os->istep0 + J;
+        c->n_alive[a.p ^ 1] = 0;
+        c->n_owned[a.p ^ 1] = 0;
+        c->n_samples[a.p ^ 1] = 0;
+        c->n_reused[a.p ^ 1] = 0;
+        os->J = J;
+    }
+}
+
+void launch_onestep_begin(const OnestepArgs& a, uint32_t k, hipStream_t s) {
+    hipLaunchKernelGGL(onestep_begin_kernel, dim3((ONESTEP_HIST + 255) / 256), dim3(256), 0, s, a, k);
+}
+void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(onestep_schedule_kernel, dim3(1), dim3(1024), 0, s, a);
+}
+void launch_onestep_pass(const OnestepArgs& a, const NetworkDev& net, int final_pass, uint32_t n_rays_hint, hipStream_t s) {
+    const uint32_t waves = (n_rays_hint + 63) / 64;
+    const uint32_t blocks = std::max(1u, std::min((waves + FUSED_WAVES - 1) / FUSED_WAVES, (uint32_t)net.n_cus * 8));
+    if (net.F == 4) {
+        if (final_pass) hipLaunchKernelGGL((nerf_onestep_kernel<4, true>), dim3(blocks), dim3(64 * FUSED_WAVES), 0, s, a);
+        else hipLaunchKernelGGL((nerf_onestep_kernel<4, false>), dim3(blocks), dim3(64 * FUSED_WAVES), 0, s, a);
+    } else {
+        if (final_pass) hipLaunchKernelGGL((nerf_onestep_kernel<2, true>), dim3(blocks), dim3(64 * FUSED_WAVES), 0, s, a);
+        else hipLaunchKernelGGL((nerf_onestep_kernel<2, false>), dim3(blocks), dim3(64 * FUSED_WAVES), 0, s, a);
+    }
+}
+
 __global__ void fused_prepare_kernel(MarchCtrl* ctrl, uint32_t* work) {
     // iterations from n_iter on take 8 steps each (the fused kernel's precondition)
     if (threadIdx.x < 64 && threadIdx.x >= ctrl->n_iter) ctrl->steps_hist[threadIdx.x] = MAX_STEPS_BETWEEN_COMPACTION;

@@ -61,11 +61,6 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t v, 
     return r;
 }
 
-__device__ __forceinline__ uint32_t steps_for(uint32_t n_alive, uint32_t target) {
-    uint32_t s = target / n_alive;
-    return s < 1 ? 1 : (s > MAX_STEPS_BETWEEN_COMPACTION ? MAX_STEPS_BETWEEN_COMPACTION : s);
-}
-
 // ---------------------------------------------------------------------------
 // init_rays_with_payload_kernel_nerf + advance_pos_nerf + first compaction
 // ---------------------------------------------------------------------------

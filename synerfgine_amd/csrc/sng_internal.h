@@ -64,6 +64,12 @@ struct RayBuf {
     uint2* lo;         // raw fp16 (r, g, b, density) network output of that sample
 };
 
+// n_steps_between_compaction = clamp(target / n_alive, 1, 8) (testbed_nerf.cu:2189-2190)
+SNG_HD uint32_t steps_for(uint32_t n_alive, uint32_t target) {
+    const uint32_t s = target / n_alive;
+    return s < 1 ? 1 : (s > MAX_STEPS_BETWEEN_COMPACTION ? MAX_STEPS_BETWEEN_COMPACTION : s);
+}
+
 // Which NeRF tracer runs: SyNeRFgine's trace_alt (ngp = 0: depth of the last sample,
 // payload.t reset to it, extract_from_payload) or instant-NGP's trace (ngp = 1: depth of the
 // max-weight sample, no t reset, shade_kernel_nerf with ERenderMode render_mode).
@@ -120,6 +126,45 @@ struct FusedArgs {
     uint32_t lanes;               // rays per wave (64; fewer shorten a wave's per-iteration field chain for thin bands)
 };
 void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s);
+
+// fused.hip: trace_alt's one-step regime (n_alive > target / 2, so every iteration takes ONE step).
+// A speculative ray-local pass simulates each ray on its own under n_steps = 1 and histograms the
+// iteration at which it leaves; the schedule kernel finds the first iteration k + J whose frame-wide
+// alive count allows more steps; the final pass re-simulates every ray to k + J and writes the
+// survivors to the other ray buffer (dying rays are extracted on the way).
+constexpr uint32_t ONESTEP_HIST = 10240;   // >= MARCH_ITER: iterations a regime can span
+struct OnestepState {
+    uint32_t k;             // first iteration of the regime
+    uint32_t istep0;        // trace_alt's i at k
+    uint32_t n_local;       // rays of this band alive at k
+    uint32_t n_sched;       // frame-wide alive count at k (the schedule's)
+    uint32_t H;             // iterations the histograms span (MARCH_ITER - istep0)
+    uint32_t J;             // iterations the regime lasts (schedule kernel)
+    uint32_t work[2];       // ray-queue cursors of the two passes
+    unsigned long long evals[2];   // field evaluations of the two passes
+};
+struct OnestepArgs {
+    Volume vol;
+    CamDev cam;
+    Sched sched;
+    RayBuf in, out;               // rays alive at k (buffer p) -> rays alive at k + J (buffer p ^ 1)
+    MarchCtrl* ctrl;
+    OnestepState* os;
+    uint32_t* deaths_local;       // [ONESTEP_HIST] rays alive at k + m but not at k + m + 1
+    uint32_t* deaths_sched;       // the same, own rows only (summed over ranks for a banded frame)
+    uint32_t* nosample;           // [ONESTEP_HIST] rays that found no occupied sample at k + m
+    const void* wfrag;
+    const void* grid_params;
+    const LevelInfo* levels;
+    float4* frame_rgba;
+    float* frame_depth;
+    float* positions;
+    int p;
+    uint32_t target;
+};
+void launch_onestep_begin(const OnestepArgs& a, uint32_t k, hipStream_t s);
+void launch_onestep_pass(const OnestepArgs& a, const NetworkDev& net, int final_pass, uint32_t n_rays_hint, hipStream_t s);
+void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s);
 
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
                    uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream);

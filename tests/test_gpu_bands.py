@@ -32,7 +32,7 @@ def _free_port():
     return p
 
 
-def _band_worker(rank, world, port, bounds, overrides, out_dir):
+def _band_worker(rank, world, port, bounds, overrides, out_dir, config="c3", target=TARGET):
     import sys
     sys.path.insert(0, os.path.dirname(HERE))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -41,7 +41,7 @@ def _band_worker(rank, world, port, bounds, overrides, out_dir):
     from synerfgine_amd import scene as S
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        tb, eng, _ = S.make_engine("c3", overrides=overrides)
+        tb, eng, _ = S.make_engine(config, overrides=overrides)
 
         def reduce_fn(vals):
             t = torch.tensor(vals, dtype=torch.int64)
@@ -58,18 +58,20 @@ def _band_worker(rank, world, port, bounds, overrides, out_dir):
         res = {}
         # independent bands (local schedule) first, then the frame-wide schedule
         fresh()
-        r = eng.frame(rows=(r0, r1), target_n_queries=TARGET)
+        r = eng.frame(rows=(r0, r1), target_n_queries=target)
         res["local_steps"] = np.array(r.steps_per_iter, np.int64)
         eng.attach_host_reducer(reduce_fn)
         fresh()
-        r = eng.frame(rows=(r0, r1), target_n_queries=TARGET)
+        r = eng.frame(rows=(r0, r1), target_n_queries=target)
         res["global_steps"] = np.array(r.steps_per_iter, np.int64)
+        res["global_onestep"] = np.array([r.onestep_from_iter, r.onestep_iterations], np.int64)
         res["band"] = r.download("final_rgba")[r0:r1]
         eng.detach_comm()
         if rank == 0:   # the single-GPU frame
             fresh()
-            r = eng.frame(target_n_queries=TARGET)
+            r = eng.frame(target_n_queries=target)
             res["full_steps"] = np.array(r.steps_per_iter, np.int64)
+            res["full_onestep"] = np.array([r.onestep_from_iter, r.onestep_iterations], np.int64)
             res["full"] = r.download("final_rgba")
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
         tb.close()
@@ -77,18 +79,21 @@ def _band_worker(rank, world, port, bounds, overrides, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bounds,overrides", [
-    ([0, 540, 1080], {}),
-    ([0, 301, 777, 1080], {}),
-    ([0, 301, 1080], {"res_factor": 16}),   # NeRF at half resolution: bands split NeRF rows by ceil(y / 2)
-], ids=["even2", "uneven3", "halfres2"])
-def test_bands_with_global_schedule_equal_single_gpu(bounds, overrides):
+@pytest.mark.parametrize("bounds,overrides,config,target", [
+    ([0, 540, 1080], {}, "c3", TARGET),
+    ([0, 301, 777, 1080], {}, "c3", TARGET),
+    ([0, 301, 1080], {"res_factor": 16}, "c3", TARGET),   # NeRF at half resolution: bands split NeRF rows by ceil(y / 2)
+    # C4 at the reference's 2^21 target: ~1100 one-step iterations, marched by the ray-local one-step regime
+    # (fused.hip) whose length comes from the death histograms summed over the ranks
+    ([0, 500, 1080], {"show_virtual_obj": 0, "shadow_on_nerf": 0}, "c4", 0),
+], ids=["even2", "uneven3", "halfres2", "c4_onestep2"])
+def test_bands_with_global_schedule_equal_single_gpu(bounds, overrides, config, target):
     import torch.multiprocessing as mp
     world = len(bounds) - 1
     ctx = mp.get_context("spawn")
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
-        procs = [ctx.Process(target=_band_worker, args=(r, world, port, bounds, overrides, d)) for r in range(world)]
+        procs = [ctx.Process(target=_band_worker, args=(r, world, port, bounds, overrides, d, config, target)) for r in range(world)]
         for p in procs:
             p.start()
         for p in procs:
@@ -106,16 +111,20 @@ def test_bands_with_global_schedule_equal_single_gpu(bounds, overrides):
         assert _prefix_equal(res[r]["global_steps"], res[0]["full_steps"])
         # ... and the band equals the single-GPU frame's rows bit for bit
         assert np.array_equal(res[r]["band"].view(np.uint32), full[r0:r1].view(np.uint32)), f"rank {r}"
+        if config == "c4":   # the regime ran, with the single-GPU frame's length
+            assert res[r]["global_onestep"][1] > 100 and np.array_equal(res[r]["global_onestep"], res[0]["full_onestep"])
     # without the exchange the bands step differently (the check above is not vacuous)
     assert any(not _prefix_equal(res[r]["local_steps"], res[0]["full_steps"]) for r in range(world))
 
 
-def test_rccl_schedule_world1_matches_local():
-    """sng_set_comm at world size 1: RCCL all-reduce of the count on the NeRF stream."""
+@pytest.mark.parametrize("config,target", [("c3", TARGET), ("c4", 0)])
+def test_rccl_schedule_world1_matches_local(config, target):
+    """sng_set_comm at world size 1: RCCL all-reduce of the count on the NeRF stream (C4: and of the one-step
+    regime's death histogram)."""
     import ctypes
     from synerfgine_amd import _lib
     from synerfgine_amd import scene as S
-    tb, eng, _ = S.make_engine("c3")
+    tb, eng, _ = S.make_engine(config)
     try:
         rng = [eng.rng_states(0), eng.rng_states(1)]
 
@@ -124,14 +133,16 @@ def test_rccl_schedule_world1_matches_local():
             eng.set_rng_states(1, rng[1])
 
         fresh()
-        a = eng.frame(target_n_queries=TARGET)
+        a = eng.frame(target_n_queries=target)
+        if config == "c4":
+            assert a.onestep_iterations > 100
         ref = a.download("final_rgba")
         lib = eng._lib
         uid = (ctypes.c_uint8 * _lib.SNG_COMM_ID_BYTES)()
         _lib.check(lib.sng_comm_unique_id(uid))
         _lib.check(lib.sng_set_comm(eng.ctx, uid, 0, 1))
         fresh()
-        b = eng.frame(target_n_queries=TARGET)
+        b = eng.frame(target_n_queries=target)
         got = b.download("final_rgba")
         assert list(b.steps_per_iter) == list(a.steps_per_iter)
         assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
@@ -140,7 +151,7 @@ def test_rccl_schedule_world1_matches_local():
             eng.attach_host_reducer(lambda v: v)
         eng.detach_comm()
         fresh()
-        c = eng.frame(target_n_queries=TARGET)
+        c = eng.frame(target_n_queries=target)
         assert np.array_equal(c.download("final_rgba").view(np.uint32), ref.view(np.uint32))
     finally:
         tb.close()

@@ -440,3 +440,33 @@ def test_mid_frame_switch_to_fused_tail_is_exact(config, target):
         assert out[0][1:] == out[1][1:]
     finally:
         tb.close()
+
+
+@pytest.mark.parametrize("config,w,h,target,shade", [("c4", 160, 90, 8192, False), ("c4", 96, 54, 4096, True), ("c4", 1920, 1080, 0, False),
+                                                     ("c3", 160, 90, 1024, True)])
+def test_onestep_regime_equals_wavefront(config, w, h, target, shade):
+    """fused.hip's one-step regime (while n_alive > target / 2: speculative ray-local march, death histograms,
+    schedule, final ray-local pass) reproduces the per-iteration wavefront bit for bit: frame buffers, hit
+    and sample counts, reference slots and the per-iteration histograms (RNG streams rewound in between)."""
+    ov = {} if shade else {"show_virtual_obj": 0, "shadow_on_nerf": 0}
+    tb, eng, _ = _engine(w, h, ov, config)
+    try:
+        n0, m0 = eng.rng_states(0).copy(), eng.rng_states(1).copy()
+        out = {}
+        for on in (0, 1):
+            eng.set_rng_states(0, n0)
+            eng.set_rng_states(1, m0)
+            eng.set_param("nerf_onestep", on)
+            r = eng.frame(target_n_queries=target)
+            if on:
+                assert r.onestep_iterations >= 1 and r.onestep_from_iter >= 4, (r.onestep_from_iter, r.onestep_iterations)
+            else:
+                assert r.onestep_iterations == 0
+            out[on] = ([r.download(b) for b in ("final_rgba", "nerf_rgba", "nerf_depth", "nerf_positions")],
+                       (r.n_samples, r.n_hit, r.n_iterations, r.n_reference_slots), list(r.alive_per_iter), list(r.steps_per_iter),
+                       list(r.samples_per_iter))
+        for a, b in zip(out[0][0], out[1][0]):
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert out[0][1:] == out[1][1:]
+    finally:
+        tb.close()
