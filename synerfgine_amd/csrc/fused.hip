@@ -133,11 +133,13 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
                 }
             } else {
 #pragma unroll 1
-                for (; cnt < n_steps; ++cnt) {
-                    t = advance_to_occupied(t, cone, o, d, idir, 0, vol.max_mip, vol);
-                    if (t >= MAX_DEPTH) break;
-                    ts_lds[wv][cnt][lane] = t;
-                    t += calc_dt(t, cone);
+                while (cnt < n_steps) {   // flattened occ_step trips (generate_kernel)
+                    if (occ_step(t, cone, o, d, idir, 0, vol.max_mip, vol)) {
+                        if (t >= MAX_DEPTH) break;
+                        ts_lds[wv][cnt][lane] = t;
+                        t += calc_dt(t, cone);
+                        ++cnt;
+                    }
                 }
                 reuse = cnt > 0 && !a.mode.ngp && ts_lds[wv][0][lane] == lt;
             }

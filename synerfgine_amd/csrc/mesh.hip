@@ -298,10 +298,14 @@ __device__ float depth_test_nerf(float full_d, uint32_t n_steps, const Volume& v
         }
         return s;
     }
-    for (uint32_t j = 0; j < n_steps; ++j) {
-        s = advance_to_occupied(s, vol.cone, src, L, invL, min_mip, max_mip, vol);
-        if (s >= full_d) { s = full_d; break; }
-        s += calc_dt(s, vol.cone);
+    // general path, flattened the same way (occ_step: one DDA step or one sample per trip)
+    uint32_t j = 0;
+    while (j < n_steps) {
+        if (occ_step(s, vol.cone, src, L, invL, min_mip, max_mip, vol)) {
+            if (s >= full_d) { s = full_d; break; }
+            s += calc_dt(s, vol.cone);
+            ++j;
+        }
     }
     return s;
 }
@@ -348,13 +352,21 @@ __global__ __launch_bounds__(TPB) void shade_shadow_kernel(ShadowArgs a, float4*
                     const f3 l = normalize(lpos - pos);
                     const float full_d = length(lpos - pos);
                     int hit = -1;
+#ifdef SHADOW_NO_BVH   // timing-only builds (tools/gpu_shadow_c4.sh)
+                    const float syn_depth = full_d + (float)(hit + 1);
+#else
                     const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, cx, hit);
+#endif
                     overall = fminf(overall, powf(syn_depth / full_d, a.intensity));
                     const f3 fract_offset = full_d * a.threshold * lpos;
                     const f3 src = pos + fract_offset;
                     const float fd = length(lpos - src);
                     const f3 Ld = normalize(lpos - src);
+#ifdef SHADOW_NO_NERF
+                    const float nd = fminf(full_d, fd + Ld.x);
+#else
                     const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip));
+#endif
                     const double mask = (double)(nd * (1.0f - fminf(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)a.threshold));
                     overall = (float)fmin((double)overall, mask);
                 } else {

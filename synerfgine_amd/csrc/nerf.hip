@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
 template <bool LIN, int THREADS = 256>
 __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                                                        float* __restrict__ coords, uint2* __restrict__ samp, int store_t, int global_sched) {
-    __shared__ float ts_lds[LIN ? MAX_STEPS_BETWEEN_COMPACTION * THREADS : 1];
+    __shared__ float ts_lds[MAX_STEPS_BETWEEN_COMPACTION * THREADS];
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t n_sched = global_sched ? ctrl->sched_alive[p] : n_alive;   // Sched
     const uint32_t i_step = ctrl->i_step[p];
@@ -152,7 +152,6 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
         const uint32_t i = blk + threadIdx.x;
         uint32_t cnt = 0;
         bool reuse = false;
-        float ts[LIN ? 1 : MAX_STEPS_BETWEEN_COMPACTION];
         f3 o = splat(0.0f), d = splat(1.0f);
         if (i < n_alive) {
             float4 ot = rays.o_t[i], di = rays.d_idx[i];
@@ -184,19 +183,18 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
                     }
                 }
             } else {
-#pragma unroll
-                for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
-                    if (j < n_steps && cnt == j) {
-                        t = advance_to_occupied(t, cone, o, d, idir, 0, vol.max_mip, vol);
-                        if (t < MAX_DEPTH) {
-                            ts[j] = t;
-                            tl = t;
-                            t += calc_dt(t, cone);
-                            ++cnt;
-                        }
+                // cascades / cone stepping: the same flattened loop over occ_step trips
+#pragma unroll 1
+                while (cnt < n_steps) {
+                    if (occ_step(t, cone, o, d, idir, 0, vol.max_mip, vol)) {
+                        if (t >= MAX_DEPTH) break;
+                        if (cnt == 0 && t == lt0) reuse = true;
+                        ts_lds[cnt * THREADS + threadIdx.x] = t;
+                        tl = t;
+                        t += calc_dt(t, cone);
+                        ++cnt;
                     }
                 }
-                reuse = cnt > 0 && ts[0] == lt0;
             }
             // NerfTracer::trace keeps generate's t (payload.t = t after n_steps samples, 836);
             // trace_alt overwrites it in the compositor
@@ -208,26 +206,13 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
         if (i < n_alive) {
             samp[i] = make_uint2(base, cnt | (ru << 31));
             const f3 wd = (d + 1.0f) * 0.5f;
-            if constexpr (LIN) {
 #pragma unroll 1
-                for (uint32_t j = ru; j < cnt; ++j) {
-                    const float t = ts_lds[j * THREADS + threadIdx.x];
-                    const float dt = calc_dt(t, 0.0f);
-                    const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
-                    float* c = coords + (size_t)(base + j - ru) * 7;
-                    c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
-                }
-            } else {
-#pragma unroll
-                for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
-                    if (j < cnt && j >= ru) {
-                        const float t = ts[j];
-                        const float dt = calc_dt(t, cone);
-                        const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
-                        float* c = coords + (size_t)(base + j - ru) * 7;
-                        c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
-                    }
-                }
+            for (uint32_t j = ru; j < cnt; ++j) {
+                const float t = ts_lds[j * THREADS + threadIdx.x];
+                const float dt = calc_dt(t, cone);
+                const f3 wp = ((o + d * t) - vol.train_aabb.lo) / wdiag;
+                float* c = coords + (size_t)(base + j - ru) * 7;
+                c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
             }
         }
     }

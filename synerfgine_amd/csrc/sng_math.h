@@ -326,6 +326,22 @@ SNG_HD float advance_to_occupied(float t, float cone, f3 o, f3 d, f3 idir, uint3
     }
 }
 
+// ONE trip of the general advance_to_occupied loop above: returns true when t is final (an occupied
+// voxel, or MAX_DEPTH when the ray left the render aabb), else t moved to the next voxel boundary.
+// Marchers that take several samples loop over it "flattened" (each trip one DDA step or one
+// sample), so a lane costs its own trips instead of the wave's slowest walk per sample.
+SNG_HD bool occ_step(float& t, float cone, f3 o, f3 d, f3 idir, uint32_t min_mip, uint32_t max_mip, const Volume& vol) {
+    const f3 pos = o + d * t;
+    if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) { t = MAX_DEPTH; return true; }
+    uint32_t mip = mip_from_pos(pos, N_CASCADES - 1);
+    mip = mip < min_mip ? min_mip : mip;
+    mip = mip > max_mip ? max_mip : mip;
+    if (!vol.bitfield || occupied_at(pos, vol.bitfield, mip)) return true;
+    while (mip < max_mip && !occupied_at(pos, vol.bitfield, mip + 1)) ++mip;
+    t = advance_to_next_voxel(t, cone, pos, d, idir, mip);
+    return false;
+}
+
 // ---- scrambled Sobol: random_val.cuh:162-325 ---------------------------------
 SNG_HD uint32_t reverse_bits(uint32_t x) {
     x = (((x & 0xaaaaaaaau) >> 1) | ((x & 0x55555555u) << 1));
