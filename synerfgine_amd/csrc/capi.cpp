@@ -386,7 +386,10 @@ const std::map<std::string, double>& default_params() {
                                                 //   uncontended network launch, then the ray-local tail; measured best)
         {"nerf_fused_lanes", 64},               // rays per wave in the fused kernel
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
+        {"nerf_gen_wide", 0},                   // cascaded generate with 1024-thread workgroups while no fused tail runs
+        {"nerf_gen_blocks", -1},                 // generate grid (256-thread units): 0 = min(rays, 8 per CU); -1 = all rays in one trip
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
+        {"nerf_onestep_horizon", 2048},         // iterations one speculative segment of the regime spans
     };
     return d;
 }
@@ -461,6 +464,7 @@ struct sng_ctx {
     DevBuf os_hist, os_state;              // one-step regime: death / no-sample histograms, OnestepState
     OnestepState* h_os = nullptr;          // pinned readback of the regime's length
     bool os_ran = false;                   // the last trace ran a one-step regime (ev_os0 .. ev_os1)
+    uint32_t os_k = 0, os_J = 0;           // ... from iteration os_k for os_J iterations (all segments)
     uint64_t rt_tile_key = 0;             // band geometry the costs belong to
     DevBuf rng_nerf, rng_mesh;
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
@@ -615,6 +619,7 @@ Volume make_volume(const sng_ctx* c) {
     v.to_local = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)};
     v.to_local_identity = 1;
     v.cone = c->cone;
+    v.ss = step_space(c->cone);
     v.max_mip = c->max_cascade;
     v.min_transmittance = (float)c->p("min_transmittance");
     v.bitfield = c->d_bitfield.as<uint8_t>();
@@ -1080,6 +1085,10 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     }
     const uint32_t blocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
     const uint32_t max_tiles = (uint32_t)((c->sample_cap + 15) / 16);
+    // generate's grid: the marcher's DDA chains are long and uneven, so one trip over all rays (each
+    // block waits for its slowest lane once) can beat the grid-stride cap
+    const double gb = c->p("nerf_gen_blocks");
+    const uint32_t gen_blocks = gb > 0 ? (uint32_t)gb : gb < 0 ? std::max(1u, (n_band + 255) / 256) : blocks;
     const int CHUNK = 4;
     int p = 0;
     uint32_t iter = 0;
@@ -1088,12 +1097,16 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     // trace_alt's one-step regime (fused.hip): tried at the first chunk boundary at which the alive
     // count may still exceed target / 2 (the boundary-sample caches are warm by then)
     bool os_open = !mode.ngp && c->p("nerf_onestep") != 0.0;
+    uint32_t& os_k = c->os_k;
+    uint32_t& os_J = c->os_J;
     c->os_ran = false;
     // an upper bound of the current (schedule) alive count from the chunk readbacks; unknown before the first.
     // Every input of the decision is frame-wide, so all ranks of a banded frame take the same branch.
     uint32_t known_alive = UINT32_MAX;
     while (!done && iter < MARCH_ITER) {
-        if (os_open && chunk >= 1 && !fuse && 2ull * known_alive > target) {
+        // a regime that reaches the speculative horizon continues with the next segment at once
+        for (bool again = true; again && os_open && chunk >= 1 && !fuse && 2ull * known_alive > target;) {
+            again = false;
             os_open = false;   // the count only shrinks: once the regime is over (or never was) it stays over
             HIPCHK(hipMemcpyAsync(c->h_ctrl, ctrl, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
             HIPCHK(hipStreamSynchronize(c->s_nerf));
@@ -1111,8 +1124,9 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 oa.wfrag = c->net.wfrag; oa.grid_params = c->net.grid; oa.levels = c->net.levels;
                 oa.frame_rgba = c->nerf_rgba.as<float4>(); oa.frame_depth = c->nerf_depth.as<float>(); oa.positions = c->nerf_pos.as<float>();
                 oa.p = p; oa.target = target;
-                if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_os0, c->s_nerf));
-                launch_onestep_begin(oa, iter, c->s_nerf);
+                if (!c->os_ran && P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_os0, c->s_nerf));
+                const uint32_t horizon = (uint32_t)std::max(1.0, c->p("nerf_onestep_horizon"));
+                launch_onestep_begin(oa, iter, horizon, c->s_nerf);
                 launch_onestep_pass(oa, c->net, 0, hc.n_alive[p], c->s_nerf);
                 HIPCHK(hipGetLastError());
                 if (gsched) {   // the frame-wide schedule: own-row deaths summed over the ranks
@@ -1133,13 +1147,17 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 launch_onestep_pass(oa, c->net, 1, hc.n_alive[p], c->s_nerf);
                 HIPCHK(hipGetLastError());
                 if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_os1, c->s_nerf));
+                if (!c->os_ran) { os_k = c->h_os->k; os_J = 0; }
                 c->os_ran = true;
+                os_J += J;
                 reduce_sched(p ^ 1);
                 p ^= 1;
                 iter += J;
-                if (iter >= MARCH_ITER || c->h_os->istep0 + J >= MARCH_ITER) break;
+                if (c->h_os->istep0 + J >= MARCH_ITER) break;
+                if (J == c->h_os->H) { os_open = true; again = true; }   // horizon reached: n_steps may still be 1
             }
         }
+        if (c->os_ran && c->h_os->istep0 + c->h_os->J >= MARCH_ITER) break;
         if (fuse && iter >= fuse_after) {
             c->fused_work.ensure(16);
             FusedArgs fa{};
@@ -1165,7 +1183,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             break;
         }
         for (int k = 0; k < CHUNK && !(fuse && iter >= fuse_after); ++k, ++iter) {
-            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), blocks, mode.ngp, a.sched.global, c->s_nerf, !fuse);
+            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), gen_blocks, mode.ngp, a.sched.global, c->s_nerf,
+                            !fuse && c->p("nerf_gen_wide") != 0.0);
             if (P.collect_kernel_times) {
                 while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
                 HIPCHK(hipEventRecord(c->net_events[2 * net_launches], c->s_nerf));
@@ -1211,8 +1230,8 @@ void march_stats(const sng_ctx* c, const sng_frame_params& P, sng_frame_result* 
     out->n_samples_network = c->h_ctrl->net_samples;
     out->n_samples_reused = c->h_ctrl->reused_samples;
     out->fused_from_iter = c->fused_last ? c->fused_k0 : c->h_ctrl->n_iter;
-    out->onestep_from_iter = c->os_ran ? c->h_os->k : c->h_ctrl->n_iter;
-    out->onestep_iterations = c->os_ran ? c->h_os->J : 0u;
+    out->onestep_from_iter = c->os_ran ? c->os_k : c->h_ctrl->n_iter;
+    out->onestep_iterations = c->os_ran ? c->os_J : 0u;
     out->n_reference_slots = ref_slots_of(c);
     std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
     std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));

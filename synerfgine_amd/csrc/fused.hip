@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     const uint32_t i_step0 = a.ctrl->i_step[a.p];
     const uint32_t k0 = a.ctrl->n_iter;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
-    const float cone = LIN ? 0.0f : vol.cone;
+    const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
     const h8* wfrag = reinterpret_cast<const h8*>(a.wfrag);
     const _Float16* grid = reinterpret_cast<const _Float16*>(a.grid_params);
     h8 W[20];
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
     const uint32_t istep0 = os->istep0;
     const uint32_t limit = FINAL ? os->J : os->H;   // iterations simulated (relative to k)
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
-    const float cone = vol.cone;
+    const StepSpace cone = vol.ss;
     const float opaque = 1.0f - vol.min_transmittance;
     const h8* wfrag = reinterpret_cast<const h8*>(a.wfrag);
     const _Float16* grid = reinterpret_cast<const _Float16*>(a.grid_params);
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
         bool survivor = false;   // FINAL: alive at k + J -> next ray buffer
         // ---- rays at the end of the span, and periodic rays (closed loop, no field evaluations)
         if (has) {
-            if (m >= limit) {   // pass 0: unreachable (m = H - 1 is MARCH_ITER's last iteration)
+            if (m >= limit) {   // pass 0: alive at the horizon (the schedule's span ends there)
                 survivor = FINAL;
                 has = false;
             } else {
@@ -502,7 +502,12 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
         uint2 out = make_uint2(0u, 0u);
         if (has) {
             const f3 idir = inv(d);
-            s = advance_to_occupied(t, cone, o, d, idir, 0, vol.max_mip, vol);
+            if (vol.linear) {
+                s = advance_to_occupied(t, vol.cone, o, d, idir, 0, vol.max_mip, vol);
+            } else {
+                s = t;
+                while (!occ_step(s, cone, o, d, idir, 0, vol.max_mip, vol)) {}
+            }
             if (s >= MAX_DEPTH) {
                 // no occupied sample: the compositor sees cnt = 0 < n_steps and retires the ray
                 const bool last = istep0 + m + 1u >= MARCH_ITER;
@@ -625,7 +630,7 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
     }
 }
 
-__global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k) {
+__global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k, uint32_t horizon) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ONESTEP_HIST; i += gridDim.x * blockDim.x) {
         a.deaths_local[i] = 0;
         a.deaths_sched[i] = 0;
@@ -638,7 +643,8 @@ __global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k) {
         os->istep0 = c->i_step[a.p];
         os->n_local = c->n_alive[a.p];
         os->n_sched = a.sched.global ? c->sched_alive[a.p] : c->n_alive[a.p];
-        os->H = c->i_step[a.p] < MARCH_ITER ? MARCH_ITER - c->i_step[a.p] : 0u;
+        const uint32_t left = c->i_step[a.p] < MARCH_ITER ? MARCH_ITER - c->i_step[a.p] : 0u;
+        os->H = left < horizon ? left : horizon;   // a regime longer than the horizon continues in a new segment
         os->J = 0;
         os->work[0] = 0; os->work[1] = 0;
         os->evals[0] = 0; os->evals[1] = 0;
@@ -706,8 +712,8 @@ __global__ __launch_bounds__(1024) void onestep_schedule_kernel(OnestepArgs a) {
     }
 }
 
-void launch_onestep_begin(const OnestepArgs& a, uint32_t k, hipStream_t s) {
-    hipLaunchKernelGGL(onestep_begin_kernel, dim3((ONESTEP_HIST + 255) / 256), dim3(256), 0, s, a, k);
+void launch_onestep_begin(const OnestepArgs& a, uint32_t k, uint32_t horizon, hipStream_t s) {
+    hipLaunchKernelGGL(onestep_begin_kernel, dim3((ONESTEP_HIST + 255) / 256), dim3(256), 0, s, a, k, horizon);
 }
 void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(onestep_schedule_kernel, dim3(1), dim3(1024), 0, s, a);

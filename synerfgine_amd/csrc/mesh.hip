@@ -301,9 +301,9 @@ __device__ float depth_test_nerf(float full_d, uint32_t n_steps, const Volume& v
     // general path, flattened the same way (occ_step: one DDA step or one sample per trip)
     uint32_t j = 0;
     while (j < n_steps) {
-        if (occ_step(s, vol.cone, src, L, invL, min_mip, max_mip, vol)) {
+        if (occ_step(s, vol.ss, src, L, invL, min_mip, max_mip, vol)) {
             if (s >= full_d) { s = full_d; break; }
-            s += calc_dt(s, vol.cone);
+            s += calc_dt(s, vol.ss);
             ++j;
         }
     }

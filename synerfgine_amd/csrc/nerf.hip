@@ -145,7 +145,7 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
     if (!active) return;
     const int lane = threadIdx.x & 63;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
-    const float cone = LIN ? 0.0f : vol.cone;
+    const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
     __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
     // block-uniform trips (block_append syncs the block)
     for (uint32_t blk = blockIdx.x * blockDim.x; blk < n_alive; blk += gridDim.x * blockDim.x) {
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
                     raw = in.lo[i];
                     const f3 wp = ((mk(ot.x, ot.y, ot.z) + mk(di.x, di.y, di.z) * lt.x) - vol.train_aabb.lo) / diag;
                     pos = vol.train_aabb.lo + wp * diag;
-                    dt = unwarp_dt(warp_dt(calc_dt(lt.x, vol.cone)));
+                    dt = unwarp_dt(warp_dt(calc_dt(lt.x, vol.ss)));
                 } else {
                     raw = net_out[sc.x + j - ru];
                     pos = vol.train_aabb.lo + mk(c[0], c[1], c[2]) * diag;

@@ -138,7 +138,7 @@ struct OnestepState {
     uint32_t istep0;        // trace_alt's i at k
     uint32_t n_local;       // rays of this band alive at k
     uint32_t n_sched;       // frame-wide alive count at k (the schedule's)
-    uint32_t H;             // iterations the histograms span (MARCH_ITER - istep0)
+    uint32_t H;             // iterations the histograms span (MARCH_ITER - istep0, capped at the horizon)
     uint32_t J;             // iterations the regime lasts (schedule kernel)
     uint32_t work[2];       // ray-queue cursors of the two passes
     unsigned long long evals[2];   // field evaluations of the two passes
@@ -162,7 +162,7 @@ struct OnestepArgs {
     int p;
     uint32_t target;
 };
-void launch_onestep_begin(const OnestepArgs& a, uint32_t k, hipStream_t s);
+void launch_onestep_begin(const OnestepArgs& a, uint32_t k, uint32_t horizon, hipStream_t s);
 void launch_onestep_pass(const OnestepArgs& a, const NetworkDev& net, int final_pass, uint32_t n_rays_hint, hipStream_t s);
 void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s);
 

@@ -222,6 +222,37 @@ SNG_HD float from_stepping_space(float n, float cone) {
     else return (n - b) * MAX_STEP + bt;
 }
 SNG_HD float advance_n_steps(float t, float cone, float n) { return from_stepping_space(to_stepping_space(t, cone) + n, cone); }
+// The same three functions with their cone-only constants (log1p(c), a, b, e^a, e^b) computed once per
+// frame by step_space() -- identical float expressions, so identical bits; the marchers' inner loops
+// then spend one log or exp per conversion instead of seven.
+struct StepSpace {
+    float cone, log1p_c, a, b, at, bt;
+};
+SNG_HD StepSpace step_space(float cone) {
+    StepSpace k{};
+    k.cone = cone;
+    if (cone <= 1e-5f) return k;
+    k.log1p_c = sng_logf(1.0f + cone);
+    k.a = (sng_logf(MIN_STEP) - sng_logf(k.log1p_c)) / k.log1p_c;
+    k.b = (sng_logf(MAX_STEP) - sng_logf(k.log1p_c)) / k.log1p_c;
+    k.at = sng_expf(k.a * k.log1p_c);
+    k.bt = sng_expf(k.b * k.log1p_c);
+    return k;
+}
+SNG_HD float to_stepping_space(float t, const StepSpace& k) {
+    if (k.cone <= 1e-5f) return div_by(t, MIN_STEP, INV_MIN_STEP);
+    if (t <= k.at) return (t - k.at) / MIN_STEP + k.a;
+    else if (t <= k.bt) return sng_logf(t) / k.log1p_c;
+    else return (t - k.bt) / MAX_STEP + k.b;
+}
+SNG_HD float from_stepping_space(float n, const StepSpace& k) {
+    if (k.cone <= 1e-5f) return n * MIN_STEP;
+    if (n <= k.a) return (n - k.a) * MIN_STEP + k.at;
+    else if (n <= k.b) return sng_expf(n * k.log1p_c);
+    else return (n - k.b) * MAX_STEP + k.bt;
+}
+SNG_HD float advance_n_steps(float t, const StepSpace& k, float n) { return from_stepping_space(to_stepping_space(t, k) + n, k); }
+SNG_HD float calc_dt(float t, const StepSpace& k) { return advance_n_steps(t, k, 1.0f) - t; }
 SNG_HD float calc_dt(float t, float cone) { return advance_n_steps(t, cone, 1.0f) - t; }
 
 SNG_HD float distance_to_next_voxel(f3 pos, f3 dir, f3 idir, float res) {
@@ -238,6 +269,13 @@ SNG_HD float advance_to_next_voxel(float t, float cone, f3 pos, f3 dir, f3 idir,
     t = to_stepping_space(t, cone);
     t_target = to_stepping_space(t_target, cone);
     return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), cone);
+}
+SNG_HD float advance_to_next_voxel(float t, const StepSpace& k, f3 pos, f3 dir, f3 idir, uint32_t mip) {
+    float res = scalbnf((float)GRID_SIZE, -(int)mip);
+    float t_target = t + distance_to_next_voxel(pos, dir, idir, res);
+    t = to_stepping_space(t, k);
+    t_target = to_stepping_space(t_target, k);
+    return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), k);
 }
 SNG_HD uint32_t mip_from_pos(f3 pos, uint32_t max_cascade) {
     int exponent;
@@ -276,6 +314,7 @@ struct Volume {
     const uint8_t* bitfield;
     const uint32_t* occ_linear;  // mip-0 occupancy as x-fastest bit rows (same bits as the Morton bitfield)
     int linear;                  // cone == 0 && max_mip == 0: the exact fast marcher applies
+    StepSpace ss;                // step_space(cone)
 };
 SNG_HD f3 to_local(const Volume& v, f3 p) { return v.to_local_identity ? p : mul(v.to_local, p); }
 
@@ -330,7 +369,7 @@ SNG_HD float advance_to_occupied(float t, float cone, f3 o, f3 d, f3 idir, uint3
 // voxel, or MAX_DEPTH when the ray left the render aabb), else t moved to the next voxel boundary.
 // Marchers that take several samples loop over it "flattened" (each trip one DDA step or one
 // sample), so a lane costs its own trips instead of the wave's slowest walk per sample.
-SNG_HD bool occ_step(float& t, float cone, f3 o, f3 d, f3 idir, uint32_t min_mip, uint32_t max_mip, const Volume& vol) {
+SNG_HD bool occ_step(float& t, const StepSpace& cone, f3 o, f3 d, f3 idir, uint32_t min_mip, uint32_t max_mip, const Volume& vol) {
     const f3 pos = o + d * t;
     if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) { t = MAX_DEPTH; return true; }
     uint32_t mip = mip_from_pos(pos, N_CASCADES - 1);

@@ -442,13 +442,16 @@ def test_mid_frame_switch_to_fused_tail_is_exact(config, target):
         tb.close()
 
 
-@pytest.mark.parametrize("config,w,h,target,shade", [("c4", 160, 90, 8192, False), ("c4", 96, 54, 4096, True), ("c4", 1920, 1080, 0, False),
-                                                     ("c3", 160, 90, 1024, True)])
-def test_onestep_regime_equals_wavefront(config, w, h, target, shade):
+@pytest.mark.parametrize("config,w,h,target,shade,horizon", [("c4", 160, 90, 8192, False, 2048), ("c4", 160, 90, 8192, False, 7),
+                                                             ("c4", 96, 54, 4096, True, 2048), ("c4", 1920, 1080, 0, False, 2048),
+                                                             ("c4", 1920, 1080, 0, False, 100), ("c3", 160, 90, 1024, True, 2048)])
+def test_onestep_regime_equals_wavefront(config, w, h, target, shade, horizon):
     """fused.hip's one-step regime (while n_alive > target / 2: speculative ray-local march, death histograms,
-    schedule, final ray-local pass) reproduces the per-iteration wavefront bit for bit: frame buffers, hit
-    and sample counts, reference slots and the per-iteration histograms (RNG streams rewound in between)."""
+    schedule, final ray-local pass; a regime longer than the speculative horizon runs as several segments)
+    reproduces the per-iteration wavefront bit for bit: frame buffers, hit and sample counts, reference
+    slots and the per-iteration histograms (RNG streams rewound in between)."""
     ov = {} if shade else {"show_virtual_obj": 0, "shadow_on_nerf": 0}
+    ov["nerf_onestep_horizon"] = horizon
     tb, eng, _ = _engine(w, h, ov, config)
     try:
         n0, m0 = eng.rng_states(0).copy(), eng.rng_states(1).copy()
