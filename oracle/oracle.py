@@ -116,6 +116,7 @@ def lib():
             "orc_overlay": (None, [vp, vp, vp, vp, vp, vp, vp]),
             "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
             "orc_num_threads": (i32, []), "orc_set_num_threads": (None, [i32]), "orc_set_mlp_accum": (None, [i32, i32]),
+            "orc_set_visualization": (None, [i32, i32]),
             "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
             "orc_display": (None, [vp, i32, i32, i32, i32, vp, vp]),
             "orc_camera_set_view": (None, [vp, vp, vp, vp, vp, f32]),
@@ -278,12 +279,13 @@ def render_nerf(model, vol, cam):
     return rgba, depth, pos, nrm, st
 
 
-def render_nerf_ngp(model, vol, cam, render_mode=1, depth_scale=1.0):
+def render_nerf_ngp(model, vol, cam, render_mode=1, depth_scale=1.0, vis_layer=0, vis_dim=0):
     """instant-NGP render path (A22): returns rgba [H,W,4], depth [H,W], stats."""
     W, H = cam.res[0], cam.res[1]
     rgba = np.zeros((H, W, 4), np.float32)
     depth = np.zeros((H, W), np.float32)
     st = orc_nerf_stats()
+    lib().orc_set_visualization(vis_layer, vis_dim)
     lib().orc_render_nerf_ngp(model.ref(), ctypes.byref(vol), ctypes.byref(cam), render_mode, depth_scale, ptr(rgba), ptr(depth), ctypes.byref(st))
     return rgba, depth, st
 

@@ -619,6 +619,82 @@ void dense(const uint16_t* W, uint32_t n_out, uint32_t n_in, const uint16_t* x, 
         y[o] = f2h(acc);
     }
 }
+/* Testbed::render_nerf's extra network passes (testbed_nerf.cu:2363-2366) [tcnn, unvendored]: tcnn gets the
+ * network input matrix as its own output, so the NerfCoordinate is rewritten in place.
+ *   Normals (2): NerfNetwork::input_gradient(dim 3) -- backward_impl (nerf_network.h:189-268) with dL/doutput
+ *     one-hot at the density row: the rgb branch carries zero gradient, so rows 4-6 (direction) become 0;
+ *     the density MLP backward (ReLU mask from the forward activation) gives dL/d(encoding); GridEncoding's
+ *     input gradient sums, per level and axis, the 4 edges along the axis weighted by the other two axes'
+ *     linear weights times the level scale (kernel_grid dy_dx).  Row 3 (dt) is not an input: untouched.
+ *     Computed in float (tcnn: fp16 backprop with loss scale 128).
+ *   EncodingVis (10): visualize_activation(layer, dim) -> extract_dimension_pos_neg_kernel over the 7-row
+ *     output: (max(-v, 0), max(v, 0), 0, 1, 1, 1, 1). */
+static int g_vis_layer = 0, g_vis_dim = 0;
+void probe_one(const orc_model* m, const Grid& g, float* cc, int mode) {
+    const uint16_t* dW0 = m->params;
+    const uint16_t* dW1 = dW0 + 64 * 32;
+    const uint16_t* rW0 = m->params + 3072;
+    const uint16_t* rW1 = rW0 + 64 * 32;
+    uint16_t enc[32], h[64];
+    encode_one(g, cc, enc);
+    dense(dW0, 64, 32, enc, h, true);
+    if (mode == 2) {
+        float gh[64], gx[3] = {0.0f, 0.0f, 0.0f};
+        for (int j = 0; j < 64; ++j) gh[j] = h2f(h[j]) > 0.0f ? h2f(dW1[j]) : 0.0f;
+        for (uint32_t level = 0; level < g.L; ++level) {
+            float ge[4] = {0, 0, 0, 0};
+            for (uint32_t f = 0; f < g.F; ++f)
+                for (int j = 0; j < 64; ++j) ge[f] = std::fma(h2f(dW0[j * 32 + level * g.F + f]), gh[j], ge[f]);
+            const uint16_t* grid = g.params + (size_t)g.offsets[level] * g.F;
+            uint32_t hashmap_size = g.offsets[level + 1] - g.offsets[level];
+            float scale = g.scale[level];
+            uint32_t res = g.res[level];
+            float pos[3];
+            uint32_t pg[3];
+            for (int d = 0; d < 3; ++d) {
+                float p = std::fma(scale, cc[d], 0.5f);
+                float tmp = std::floor(p);
+                pg[d] = (uint32_t)(int)tmp;
+                pos[d] = p - tmp;
+            }
+            for (uint32_t gd = 0; gd < 3; ++gd) {
+                for (uint32_t idx = 0; idx < 4; ++idx) {
+                    float w = scale;
+                    uint32_t pl[3];
+                    for (uint32_t ng = 0; ng < 2; ++ng) {
+                        const uint32_t dim = ng >= gd ? ng + 1 : ng;
+                        if ((idx & (1u << ng)) == 0) { w *= 1.0f - pos[dim]; pl[dim] = pg[dim]; }
+                        else { w *= pos[dim]; pl[dim] = pg[dim] + 1; }
+                    }
+                    pl[gd] = pg[gd];
+                    const uint32_t il = grid_index(hashmap_size, res, pl) * g.F;
+                    pl[gd] = pg[gd] + 1;
+                    const uint32_t ir = grid_index(hashmap_size, res, pl) * g.F;
+                    for (uint32_t f = 0; f < g.F; ++f) gx[gd] += ge[f] * (w * (h2f(grid[ir + f]) - h2f(grid[il + f])));
+                }
+            }
+        }
+        cc[0] = gx[0]; cc[1] = gx[1]; cc[2] = gx[2];
+        cc[4] = 0.0f; cc[5] = 0.0f; cc[6] = 0.0f;
+        return;
+    }
+    float v;
+    if (g_vis_layer == 0) v = h2f(enc[g_vis_dim]);
+    else if (g_vis_layer == 1) v = h2f(h[g_vis_dim]);
+    else {
+        uint16_t rin[32], h1[64], h2o[64];
+        dense(dW1, 16, 64, h, rin, false);
+        sh_one(cc[4], cc[5], cc[6], rin + 16);
+        if (g_vis_layer == 2) v = h2f(rin[g_vis_dim]);
+        else {
+            dense(rW0, 64, 32, rin, h1, true);
+            if (g_vis_layer == 3) v = h2f(h1[g_vis_dim]);
+            else { dense(rW1, 64, 64, h1, h2o, true); v = h2f(h2o[g_vis_dim]); }
+        }
+    }
+    cc[0] = std::max(-v, 0.0f); cc[1] = std::max(v, 0.0f); cc[2] = 0.0f;
+    cc[3] = 1.0f; cc[4] = 1.0f; cc[5] = 1.0f; cc[6] = 1.0f;
+}
 /* one sample; coords = NerfCoordinate {pos(3), dt, dir(3)} (nerf_device.cuh:176-202);
  * out16 = the 16 fp16 outputs of the rgb network with row 3 replaced by density (extract_density) */
 void network_one(const orc_model* m, const Grid& g, const float* coord, uint16_t* out16) {
@@ -1039,6 +1115,7 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
             uint16_t o16[16];
             network_one(m, g, &coords[(size_t)s * 7], o16);
             std::memcpy(&outs[(size_t)s * 4], o16, 8);
+            if (ngp && (render_mode == 2 || render_mode == 10)) probe_one(m, g, &coords[(size_t)s * 7], render_mode);
         }
         /* composite_kernel_nerf_alt 476-575 */
 #pragma omp parallel for schedule(static)
@@ -1058,7 +1135,10 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
                 float weight = alpha * T;
                 V3 rgb = v3(logistic(h2f(o[0])), logistic(h2f(o[1])), logistic(h2f(o[2])));
                 if (ngp) {
-                    if (render_mode == 3) rgb = (pos - 0.5f) / 2.0f + 0.5f;                                /* Positions */
+                    if (render_mode == 2) {                                                                /* Normals */
+                        const float dd = det_expf(std::min(std::max(h2f(o[3]), -15.0f), 15.0f));  /* network_to_density_derivative */
+                        rgb = normalize(v3(cc[0], cc[1], cc[2]) * -dd);
+                    } else if (render_mode == 3) rgb = (pos - 0.5f) / 2.0f + 0.5f;                         /* Positions */
                     else if (render_mode == 10) rgb = v3(cc[0], cc[1], cc[2]);                             /* EncodingVis */
                     else if (render_mode == 4) rgb = v3s(dot(cam_fwd, pos - p.origin) * depth_scale);      /* Depth */
                     else if (render_mode == 0) rgb = v3s(alpha);                                           /* AO */
@@ -1490,6 +1570,10 @@ void orc_render_frame(const orc_model* m, const orc_volume* v, const orc_camera*
     orc_overlay(P, acc.data(), accd.data(), nerf_rgba, nerf_depth, final_rgba, final_depth);
 }
 
+void orc_set_visualization(int32_t layer, int32_t dim) {
+    g_vis_layer = layer;
+    g_vis_dim = dim;
+}
 void orc_set_mlp_accum(int32_t mode, int32_t chunk) {
     g_mlp_accum = mode;
     g_mlp_chunk = chunk > 0 ? chunk : 16;

@@ -203,7 +203,9 @@ int32_t orc_num_threads(void);
 void orc_set_num_threads(int32_t n);
 /* MLP accumulation model (sng_oracle.cpp dense()): 0 = fp32 over K (default), 1 = tcnn WMMA __half
  * accumulators, rounded to fp16 after every `chunk` (16) products */
-void orc_set_mlp_accum(int32_t mode, int32_t chunk);   /* OpenMP threads of the later calls (bench CPU baseline) */
+void orc_set_mlp_accum(int32_t mode, int32_t chunk);
+/* EncodingVis: Testbed::m_visualized_layer / m_visualized_dimension for orc_render_nerf_ngp(render_mode 10) */
+void orc_set_visualization(int32_t layer, int32_t dim);   /* OpenMP threads of the later calls (bench CPU baseline) */
 
 #ifdef __cplusplus
 }

@@ -374,6 +374,8 @@ const std::map<std::string, double>& default_params() {
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
+        {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
+        {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
         {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)
         {"rt_spec", 0},                         // sample-parallel path kernel (exact; mesh.hip raytrace_spec_kernel): 1 on, 0 off,
                                                 //   -1 for bands of < 25 % of the rows
@@ -1077,7 +1079,9 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     // initial alive count satisfies n_alive * 8 <= target (it only shrinks).
     bool fuse = false;
     uint32_t fuse_after = 0;
-    if (c->p("nerf_fused") != 0.0) {
+    // Normals / EncodingVis rewrite the network input between the network and the compositor: wavefront only
+    const bool probe = mode.ngp && (mode.render_mode == 2 || mode.render_mode == 10);
+    if (c->p("nerf_fused") != 0.0 && !probe) {
         HIPCHK(hipMemcpyAsync(c->h_alive, sched_src, 4, hipMemcpyDeviceToHost, c->s_nerf));
         HIPCHK(hipStreamSynchronize(c->s_nerf));
         fuse = (uint64_t)c->h_alive[0] * MAX_STEPS_BETWEEN_COMPACTION <= target;
@@ -1190,6 +1194,9 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 HIPCHK(hipEventRecord(c->net_events[2 * net_launches], c->s_nerf));
             }
             launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf);
+            if (probe)   // Normals / EncodingVis: input gradient or activation into the coordinates (testbed_nerf.cu:2363-2366)
+                launch_field_probe(c->net, c->d_params.as<uint16_t>(), c->coords.as<float>(), &ctrl->n_samples[p], mode.render_mode,
+                                   (int)c->p("visualized_layer"), (int)c->p("visualized_dimension"), c->s_nerf);
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->net_events[2 * net_launches + 1], c->s_nerf));
             HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));   // render_frame starts the raytracer after the head's network
             ++net_launches;
@@ -1210,7 +1217,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // once the alive count (it only shrinks) allows 8 steps per iteration, the rest of the march is
             // ray-local: hand it to the fused tail (the count read here is a chunk old, so it bounds the
             // count at `iter` from above)
-            else if (!fuse && c->p("nerf_fused") != 0.0 && (uint64_t)std::max(h[0], h[1]) * MAX_STEPS_BETWEEN_COMPACTION <= target) {
+            else if (!fuse && !probe && c->p("nerf_fused") != 0.0 && (uint64_t)std::max(h[0], h[1]) * MAX_STEPS_BETWEEN_COMPACTION <= target) {
                 fuse = true;
                 fuse_after = iter;
             }
@@ -1693,9 +1700,15 @@ void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* o
     if (c->win[0] <= 0) throw SngError(SNG_ERR_STATE, "sng_set_window first");
     if ((int)c->p("res_factor") != c->last_res_factor) resize(c);
     if (!(c->has_model && c->has_bitfield)) throw SngError(SNG_ERR_STATE, "no NeRF model/density grid loaded");
-    const int rm = (int)c->p("render_mode");
-    if (!(rm == 0 || rm == 1 || rm == 3 || rm == 4 || rm == 6 || rm == 10))
-        throw SngError(SNG_ERR_INVALID, "render_mode " + std::to_string(rm) + " is not supported by the instant-NGP path (AO, Shade, Positions, Depth, Cost, EncodingVis)");
+    const int vdim = (int)c->p("visualized_dimension"), vlayer = (int)c->p("visualized_layer");
+    const int rm = vdim > -1 ? 10 : (int)c->p("render_mode");   // testbed_nerf.cu:2491
+    if (!(rm == 0 || rm == 1 || rm == 2 || rm == 3 || rm == 4 || rm == 6 || rm == 10))
+        throw SngError(SNG_ERR_INVALID, "render_mode " + std::to_string(rm) + " is not supported by the instant-NGP path (AO, Shade, Normals, Positions, Depth, Cost, EncodingVis)");
+    if (rm == 10) {   // tcnn visualize_activation's range checks (NerfNetwork::width, base.json: 1 density + 2 rgb hidden layers)
+        static const int width[5] = {32, 64, 32, 64, 64};
+        if (vlayer < 0 || vlayer > 4 || vdim < 0 || vdim >= width[vlayer])
+            throw SngError(SNG_ERR_INVALID, "EncodingVis: visualized layer " + std::to_string(vlayer) + " / dimension " + std::to_string(vdim) + " out of range");
+    }
     sng_frame_params P{};
     if (fp) P = *fp;
     const uint32_t target = P.target_n_queries ? P.target_n_queries : 2u * 1024u * 1024u;

@@ -292,7 +292,10 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
                 const float weight = alpha * T;
                 f3 rgb = mk(logistic(r), logistic(g), logistic(b));
                 if (mode.ngp) {   // composite_kernel_nerf render modes (testbed_nerf.cu:709-723)
-                    if (mode.render_mode == 3) rgb = (pos - 0.5f) / 2.0f + 0.5f;
+                    if (mode.render_mode == 2) {   // network_to_density_derivative (Exponential) x the density gradient
+                        const float dd = sng_expf(fminf(fmaxf(s, -15.0f), 15.0f));
+                        rgb = normalize(-dd * mk(c[0], c[1], c[2]));
+                    } else if (mode.render_mode == 3) rgb = (pos - 0.5f) / 2.0f + 0.5f;
                     else if (mode.render_mode == 10) rgb = mk(c[0], c[1], c[2]);
                     else if (mode.render_mode == 4) rgb = splat(dot(cam.c2, pos - mk(ot.x, ot.y, ot.z)) * mode.depth_scale);
                     else if (mode.render_mode == 0) rgb = splat(alpha);

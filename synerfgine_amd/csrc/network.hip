@@ -141,6 +141,133 @@ int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, 
     return 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Testbed::render_nerf's extra network passes (testbed_nerf.cu:2363-2366).  tcnn is called with the
+// network input matrix as its own output, so the samples' NerfCoordinates are rewritten in place and
+// composite_kernel_nerf then reads the result as "warped_pos" (and dt):
+//   Normals     (2): NerfNetwork::input_gradient(dim 3): rows 0-2 = d(raw density)/d(warped position)
+//                    (density MLP backward -> GridEncoding input gradient, kernel_grid's dy_dx with
+//                    linear interpolation), rows 4-6 = 0 (the direction feeds only rgb), row 3 untouched;
+//   EncodingVis (10): visualize_activation(layer, dim) (tcnn extract_dimension_pos_neg_kernel over a
+//                    7-row output): (max(-v, 0), max(v, 0), 0, 1, 1, 1, 1), v = activation `dim` of
+//                    NerfNetwork layer `layer` (0 encoding, 1 density hidden, 2 rgb-network input,
+//                    3-4 rgb hidden).
+// One thread per sample with plain f32 arithmetic (the oracle's dense() accumulation order) (tcnn backpropagates in fp16 with a 128 loss scale;
+// after normalize() the direction differs by O(1e-3)); activations are the fp16 values tcnn keeps.
+// Not a hot path: only these two render modes run it.
+template <int F>
+__global__ __launch_bounds__(128) void field_probe_kernel(float* __restrict__ coords, const uint32_t* __restrict__ n_dev,
+                                                          const uint16_t* __restrict__ mlp, const _Float16* __restrict__ grid,
+                                                          const LevelInfo* __restrict__ levels, int n_levels, int mode, int layer, int dim) {
+    const uint32_t n = *n_dev;
+    const _Float16* W = reinterpret_cast<const _Float16*>(mlp);
+    const _Float16* dW0 = W;                 // density [64][32]
+    const _Float16* dW1 = W + 64 * 32;       // density [16][64]
+    const _Float16* cW0 = dW1 + 16 * 64;     // rgb [64][32]
+    const _Float16* cW1 = cW0 + 64 * 32;     // rgb [64][64]
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n; s += gridDim.x * blockDim.x) {
+        float* c = coords + (size_t)s * 7;
+        const float x0 = c[0], x1 = c[1], x2 = c[2];
+        _Float16 enc[32];
+        for (int l = 0; l < n_levels; ++l) encode_level<F>(levels[l], grid, x0, x1, x2, enc + l * F);
+        _Float16 hid[64];
+        float gh[64];
+        for (int j = 0; j < 64; ++j) {
+            float a = 0.0f;
+            for (int i = 0; i < 32; ++i) a += (float)dW0[j * 32 + i] * (float)enc[i];
+            hid[j] = (_Float16)fmaxf(a, 0.0f);
+        }
+        if (mode == 2) {
+            // d(raw density) / d(hidden) = W1[0][j] where the ReLU passed, then / d(encoding) = W0^T
+            for (int j = 0; j < 64; ++j) gh[j] = (float)hid[j] > 0.0f ? (float)dW1[j] : 0.0f;
+            float g[3] = {0.0f, 0.0f, 0.0f};
+            for (int l = 0; l < n_levels; ++l) {
+                float ge[F];
+                for (int f = 0; f < F; ++f) {
+                    float a = 0.0f;
+                    for (int j = 0; j < 64; ++j) a = fmaf((float)dW0[j * 32 + l * F + f], gh[j], a);
+                    ge[f] = a;
+                }
+                const LevelInfo L = levels[l];
+                const float xs[3] = {x0, x1, x2};
+                float fr[3];
+                uint32_t gi[3];
+                for (int d = 0; d < 3; ++d) {
+                    const float p = fmaf(L.scale, xs[d], 0.5f);
+                    const float q = floorf(p);
+                    gi[d] = (uint32_t)(int)q;
+                    fr[d] = p - q;
+                }
+                const _Float16* tbl = grid + (size_t)L.offset * F;
+                // kernel_grid dy_dx: for each axis, the 4 edges along it weighted by the other two axes
+                for (int gd = 0; gd < 3; ++gd) {
+                    const int da = gd == 0 ? 1 : 0, db = gd == 2 ? 1 : 2;
+                    for (int e = 0; e < 4; ++e) {
+                        float w = L.scale;
+                        uint32_t cc[3];
+                        cc[da] = gi[da] + (e & 1); w *= (e & 1) ? fr[da] : 1.0f - fr[da];
+                        cc[db] = gi[db] + ((e >> 1) & 1); w *= (e & 2) ? fr[db] : 1.0f - fr[db];
+                        cc[gd] = gi[gd];
+                        const uint32_t il = grid_index(L, cc[0], cc[1], cc[2]) * F;
+                        cc[gd] = gi[gd] + 1;
+                        const uint32_t ir = grid_index(L, cc[0], cc[1], cc[2]) * F;
+                        for (int f = 0; f < F; ++f) g[gd] += ge[f] * (w * ((float)tbl[ir + f] - (float)tbl[il + f]));
+                    }
+                }
+            }
+            c[0] = g[0]; c[1] = g[1]; c[2] = g[2];
+            c[4] = 0.0f; c[5] = 0.0f; c[6] = 0.0f;
+        } else {
+            float v = 0.0f;
+            if (layer == 0) {
+                v = (float)enc[dim];
+            } else if (layer == 1) {
+                v = (float)hid[dim];
+            } else {
+                // rgb-network input: the density MLP's 16 outputs (no output activation), then SH degree 4
+                _Float16 rin[32];
+                for (int k = 0; k < 16; ++k) {
+                    float a = 0.0f;
+                    for (int j = 0; j < 64; ++j) a += (float)dW1[k * 64 + j] * (float)hid[j];
+                    rin[k] = (_Float16)a;
+                }
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    float o[4];
+                    sh_lane(g4, c[4], c[5], c[6], o);
+                    for (int q = 0; q < 4; ++q) rin[16 + 4 * g4 + q] = (_Float16)o[q];
+                }
+                if (layer == 2) {
+                    v = (float)rin[dim];
+                } else {
+                    _Float16 h1[64];
+                    for (int j = 0; j < 64; ++j) {
+                        float a = 0.0f;
+                        for (int i = 0; i < 32; ++i) a += (float)cW0[j * 32 + i] * (float)rin[i];
+                        h1[j] = (_Float16)fmaxf(a, 0.0f);
+                    }
+                    if (layer == 3) {
+                        v = (float)h1[dim];
+                    } else {
+                        float a = 0.0f;
+                        for (int i = 0; i < 64; ++i) a += (float)cW1[dim * 64 + i] * (float)h1[i];
+                        v = (float)(_Float16)fmaxf(a, 0.0f);
+                    }
+                }
+            }
+            c[0] = fmaxf(-v, 0.0f); c[1] = fmaxf(v, 0.0f); c[2] = 0.0f;
+            c[3] = 1.0f; c[4] = 1.0f; c[5] = 1.0f; c[6] = 1.0f;
+        }
+    }
+}
+
+void launch_field_probe(const NetworkDev& net, const uint16_t* mlp_params, float* coords, const uint32_t* n_dev, int mode, int layer, int dim,
+                        hipStream_t stream) {
+    const uint32_t blocks = (uint32_t)net.n_cus * 8;
+    const _Float16* gr = reinterpret_cast<const _Float16*>(net.grid);
+    if (net.F == 4) hipLaunchKernelGGL((field_probe_kernel<4>), dim3(blocks), dim3(128), 0, stream, coords, n_dev, mlp_params, gr, net.levels, net.L, mode, layer, dim);
+    else hipLaunchKernelGGL((field_probe_kernel<2>), dim3(blocks), dim3(128), 0, stream, coords, n_dev, mlp_params, gr, net.levels, net.L, mode, layer, dim);
+}
+
 int launch_encode(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n, uint16_t* out, hipStream_t stream) {
     if (n == 0) return 0;
     uint32_t blocks = (n * 4 + 255) / 256;

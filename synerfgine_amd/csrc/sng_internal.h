@@ -168,6 +168,9 @@ void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s);
 
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
                    uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream);
+// Normals (mode 2) input gradient / EncodingVis (mode 10) activation, rewriting the samples' coordinates in place
+void launch_field_probe(const NetworkDev& net, const uint16_t* mlp_params, float* coords, const uint32_t* n_dev, int mode, int layer, int dim,
+                        hipStream_t stream);
 int launch_encode(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n, uint16_t* out, hipStream_t stream);
 
 struct ShadowArgs {

@@ -359,27 +359,39 @@ def test_load_snapshot_equals_direct_model(tmp_path):
         tb.close()
 
 
-@pytest.mark.parametrize("render_mode", [1, 0, 3, 4, 6, 10])
-def test_instant_ngp_render_path_matches_oracle(render_mode):
-    """SURVEY A22: Testbed::render_nerf (NerfTracer::trace + composite_kernel_nerf + shade_kernel_nerf) per ERenderMode."""
+@pytest.mark.parametrize("render_mode,vis", [(1, None), (0, None), (3, None), (4, None), (6, None), (2, None),
+                                              (10, (0, 5)), (10, (1, 17)), (10, (2, 0)), (10, (2, 20)), (10, (4, 3))])
+def test_instant_ngp_render_path_matches_oracle(render_mode, vis):
+    """SURVEY A22: Testbed::render_nerf (NerfTracer::trace + composite_kernel_nerf + shade_kernel_nerf) per ERenderMode.
+    Normals (2): the network's input gradient (density MLP + hash-grid backward, testbed_nerf.cu:2363, 736-741);
+    EncodingVis (10, selected by visualized_dimension > -1, testbed_nerf.cu:2491): visualize_activation of
+    (layer, dimension) written over the samples' coordinates (2365-2366)."""
     import oracle as O
     tb, eng, (cfg, params, grid) = _engine(128, 72, {"show_virtual_obj": 0, "shadow_on_nerf": 0})
     try:
         eng.set_param("depth_scale", 3.0)
-        r = eng.render_nerf(render_mode=render_mode)
+        layer, dim = vis if vis else (0, -1)
+        eng.set_param("visualized_layer", layer)
+        eng.set_param("visualized_dimension", dim)
+        r = eng.render_nerf(render_mode=1 if vis else render_mode)
         got = r.download("nerf_rgba")
         gd = r.download("nerf_depth")[..., 0]
         res = eng.resolution()["nerf"]
         cam = O.make_camera(tb.camera_matrix, tb.focal_length(0), res)
-        ref, rd, st = O.render_nerf_ngp(O.Model(cfg, params), O.volume_for(cfg, grid), cam, render_mode, 3.0)
+        ref, rd, st = O.render_nerf_ngp(O.Model(cfg, params), O.volume_for(cfg, grid), cam, render_mode, 3.0, vis_layer=layer, vis_dim=max(dim, 0))
         assert r.n_iterations == st.n_iterations
         assert list(r.alive_per_iter) == list(st.alive_per_iter)[: st.n_iterations]
         assert r.n_samples == st.n_samples and r.n_hit == st.n_hit
-        err = np.abs(got - ref).max(axis=-1)
+        fin = np.isfinite(ref).all(axis=-1) & np.isfinite(got).all(axis=-1)
+        assert (fin == np.isfinite(ref).all(axis=-1)).all()
+        err = np.abs(got - ref).max(axis=-1)[fin]
         assert (err <= 2e-3).mean() >= 0.995, f"max err {err.max()}"
         dmask = (rd < 1e4) & (gd < 1e4)
         assert (np.abs(gd - rd)[dmask] <= 1e-3 * np.maximum(1.0, rd[dmask])).mean() >= 0.995
+        if render_mode == 2:   # shaded normals are unit vectors where a ray stopped on the surface
+            assert (got[..., 3] > 0.5).mean() > 0.05
     finally:
+        eng.set_param("visualized_dimension", -1)
         tb.close()
 
 
@@ -388,7 +400,12 @@ def test_instant_ngp_rejects_unsupported_modes():
     tb, eng, _ = _engine(32, 18, {"show_virtual_obj": 0})
     try:
         with pytest.raises(SngError):
-            eng.render_nerf(render_mode=2)   # Normals needs network input gradients
+            eng.render_nerf(render_mode=5)   # Slice: an SDF/volume mode, not a NeRF one
+        with pytest.raises(SngError):
+            eng.render_nerf(render_mode=10)  # EncodingVis needs visualized_dimension >= 0 (tcnn range check)
+        eng.set_param("visualized_dimension", 64)
+        with pytest.raises(SngError):
+            eng.render_nerf()                # layer 0 (the encoding) has 32 dimensions
     finally:
         tb.close()
 
