@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the extra legs (C3 nerf_shadow_samples r=2, the reference's "
+                                                            "dmrf-compare-abm --sshadows/--nshadows sweep)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed oracle runs per CPU-baseline leg (median reported)")
     ap.add_argument("--serial-streams", action="store_true", help="run raytracer and NeRF back to back (profiling)")
     ap.add_argument("--cpu-baseline-scale", type=float, default=1.5, help="the C3-sample leg renders the frame at 1/scale linear resolution")
@@ -181,6 +183,47 @@ def traffic_profile(config):
     except (OSError, ValueError):
         return None
     return {"file": os.path.relpath(path, REPO), "config": d.get("config"), "kernels": d.get("roofline_kernels", {})}
+
+
+def frame_cells(eng, cells, frames, warmup, px):
+    """Render `frames` timed frames (after `warmup`) per parameter cell; frames/s (host wall clock around the
+    synchronous sng_render_frame calls), samples per NeRF pixel and the network launches' roofline fraction."""
+    import torch
+    out = []
+    for cell in cells:
+        for k, v in cell.items():
+            eng.set_param(k, v)
+        for _ in range(warmup):
+            eng.frame(spp=0, reset=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = [eng.frame(spp=0, reset=True, collect_kernel_times=True) for _ in range(frames)]
+        el = time.perf_counter() - t0
+        net_ms = sum(r.ms_network for r in st)
+        net_samples = sum(r.n_samples_network for r in st)
+        gbs = net_samples * BYTES_PER_SAMPLE / (net_ms * 1e-3) / 1e9 if net_ms > 0 else 0.0
+        r = st[-1]
+        out.append({**cell, "frames_per_s": round(frames / el, 2), "ms_frame_device": round(r.ms_frame, 3),
+                    "samples_per_px": round(r.n_samples / px, 3), "reference_slots_per_px": round(r.n_reference_slots / px, 3),
+                    "network_roofline_frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "stages_ms": {"raytrace": round(r.ms_raytrace, 3), "nerf": round(r.ms_nerf, 3), "shadow": round(r.ms_shadow, 3)}})
+    return out
+
+
+def abm_sweep(model, frames, warmup):
+    """The reference's own perf sweep (scripts/render/profiling.sh:12-18; every number in BASELINE.md): the lego
+    snapshot + dmrf-compare-abm.json (armadillo, bunny, monkey, 2 lights) at 1280x720, --sshadows x --nshadows
+    in {1,2,4,8}^2 (Engine::set_syn_samples / set_nerf_samples)."""
+    from synerfgine_amd import scene as S
+    tb, eng, _ = S.make_engine("abm", model=model)
+    try:
+        NW, NH = eng.resolution()["nerf"]
+        cells = [{"sshadows": a, "nshadows": b} for a in (1, 2, 4, 8) for b in (1, 2, 4, 8)]
+        return {"scene": "scenes/dmrf-compare-abm.json (scripts/virtual_desc/dmrf-compare-abm.json)", "model": model,
+                "width": 1280, "height": 720, "frames_per_cell": frames,
+                "cells": frame_cells(eng, cells, frames, warmup, NW * NH)}
+    finally:
+        tb.close()
 
 
 def dry_run(args, rank, world):
@@ -369,6 +412,20 @@ def main():
                          "field_sample_weighted": {"samples": int(evaluated), "ms": round(field_ms, 4), "achieved": round(field_gbs, 1),
                                                    "frac": round(field_gbs / HBM_PEAK_GBS, 4)}},
         }
+    if rank == 0 and world == 1 and not args.no_sweep:
+        # extra legs, after the timed region: C3 with NeRF shadows r = 2 (SURVEY §8d reports r = 0 and r = 2), and
+        # the reference's own sweep (BASELINE.md's scene)
+        try:
+            if args.config == "c3":
+                NW, NH = res["nerf"]
+                result["c3_nerf_shadow_r"] = frame_cells(eng, [{"nerf_shadow_samples": 1}, {"nerf_shadow_samples": 4}], 5, 1, NW * NH)
+                eng.set_param("nerf_shadow_samples", 1)
+        except Exception as e:
+            result["c3_nerf_shadow_r"] = {"error": repr(e)}
+        try:
+            result["abm_sweep"] = abm_sweep(args.model if args.config != "c4" else "lego", 3, 1)
+        except Exception as e:
+            result["abm_sweep"] = {"error": repr(e)}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
             legs, threads = cpu_baseline_c1(args.model if args.config != "c4" else "lego", args.cpu_runs)

@@ -120,6 +120,12 @@ int sng_ctx_destroy(sng_ctx* ctx);
 
 /* ---- model: Testbed::load_snapshot (testbed.cu:4878-5015, 4994) ---------- */
 int sng_load_snapshot(sng_ctx* ctx, const char* ingp_path);
+/* Testbed::save_snapshot(path, include_optimizer_state, compress) (testbed.cu:4812-4876): the network
+ * config + tcnn Trainer::serialize (inference params; with the optimizer state: EMA weights, Adam
+ * moments / param steps / step) + the Testbed fields (density grid fp16, aabbs, camera, dataset
+ * metadata, batch counters).  ".ingp": gzip(msgpack), else msgpack.  sng_load_snapshot restores the
+ * optimizer state when present (training continues from it). */
+int sng_save_snapshot(sng_ctx* ctx, const char* path, int32_t include_optimizer_state, int32_t compress);
 /* host-only parse of the same file (no device): config, sizes, and optionally the fp16 params and
  * density grid copied out (buffers may be NULL) -- the load_snapshot parse step (testbed.cu:4880-4931) */
 int sng_snapshot_probe(const char* ingp_path, sng_nerf_config* cfg, uint64_t* n_params, uint64_t* n_grid_cells,

@@ -57,6 +57,10 @@ class Testbed:
     def load_snapshot(self, path):
         check(self._lib.sng_load_snapshot(self.ctx, str(path).encode()))
 
+    def save_snapshot(self, path, include_optimizer_state=False, compress=True):
+        """Testbed::save_snapshot (testbed.cu:4812-4876): .ingp = gzip(msgpack), any other suffix = msgpack."""
+        check(self._lib.sng_save_snapshot(self.ctx, str(path).encode(), 1 if include_optimizer_state else 0, 1 if compress else 0))
+
     def set_nerf_model(self, cfg, params):
         params = np.ascontiguousarray(params, dtype=np.float16)
         c = _lib.sng_nerf_config(**cfg)

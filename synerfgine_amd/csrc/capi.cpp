@@ -1866,6 +1866,70 @@ ParsedSnapshot parse_snapshot(const std::string& path) {
     return ps;
 }
 
+// The optimizer state of a snapshot saved with include_optimizer_state (save_snapshot below; tcnn
+// Trainer::deserialize): Adam moments and per-parameter steps, EMA weights, the step counter and the
+// batch counters.  With snapshot.sng (this library's extension) also the fp32 master weights, the fp32
+// density grid and the pcg32 states, so training resumes exactly; without it the master weights are
+// the fp16 params and the grid the fp16 density grid (what a reference snapshot carries).
+template <typename T>
+std::vector<T> download(const DevBuf& b, size_t n) {
+    std::vector<T> h(n);
+    if (n) HIPCHK(hipMemcpy(h.data(), b.p, n * sizeof(T), hipMemcpyDeviceToHost));
+    return h;
+}
+void restore_training_state(sng_ctx* c, const JValue& snap) {
+    const uint64_t n = c->n_params;
+    const uint32_t n_cells = GRID_CELLS * (c->max_cascade + 1);
+    auto bin = [](const JValue& v, size_t bytes) -> const void* {
+        if (v.type != JValue::Binary || v.str.size() != bytes) throw SngError(SNG_ERR_IO, "snapshot optimizer state has the wrong size");
+        return v.str.data();
+    };
+    const JValue& opt = snap["optimizer"];
+    const JValue& adam = opt["nested"]["nested"];
+    train_reset(c, 1337);   // allocations; master = ema = float(params), zero moments
+    auto& t = c->tr;
+    HIPCHK(hipMemcpy(t.ema.p, bin(opt["weights_ema_binary"], n * 4), n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.m1.p, bin(adam["first_moments_binary"], n * 4), n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.m2.p, bin(adam["second_moments_binary"], n * 4), n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.steps.p, bin(adam["param_steps_binary"], n * 4), n * 4, hipMemcpyHostToDevice));
+    t.step = (uint32_t)adam["current_step"].as_num();
+    if (snap.contains("nerf") && snap["nerf"].contains("rgb")) {
+        const JValue& r = snap["nerf"]["rgb"];
+        t.rays_per_batch = (uint32_t)r["rays_per_batch"].as_num();
+        t.measured = (uint32_t)r["measured_batch_size"].as_num();
+        t.measured_before = (uint32_t)r["measured_batch_size_before_compaction"].as_num();
+    }
+    if (snap.contains("loss")) t.last_loss = snap["loss"].as_float();
+    std::vector<float> master(n), grid(n_cells);
+    if (snap.contains("sng")) {
+        const JValue& x = snap["sng"];
+        std::memcpy(master.data(), bin(x["master_binary"], n * 4), n * 4);
+        std::memcpy(grid.data(), bin(x["density_grid_f32_binary"], (size_t)n_cells * 4), (size_t)n_cells * 4);
+        uint64_t rng[4];
+        std::memcpy(rng, bin(x["rng_binary"], sizeof(rng)), sizeof(rng));
+        t.rng.state = rng[0]; t.rng.inc = rng[1]; t.grid_rng.state = rng[2]; t.grid_rng.inc = rng[3];
+        t.grid_ema_step = (uint32_t)x["grid_ema_step"].as_num();
+    } else {
+        HIPCHK(hipMemcpy(master.data(), t.master.p, n * 4, hipMemcpyDeviceToHost));
+        const std::vector<uint16_t> g16 = download<uint16_t>(c->d_grid_f16, n_cells);
+        for (uint32_t i = 0; i < n_cells; ++i) grid[i] = h2f(g16[i]);
+        t.grid_ema_step = t.step;
+    }
+    std::vector<uint16_t> p_train(n);
+    for (uint64_t i = 0; i < n; ++i) p_train[i] = f2h_host(master[i]);
+    HIPCHK(hipMemcpy(t.master.p, master.data(), n * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.p_train.p, p_train.data(), n * 2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.p_infer.p, c->d_params.p, n * 2, hipMemcpyDeviceToDevice));
+    HIPCHK(hipMemcpy(t.grid.p, grid.data(), (size_t)n_cells * 4, hipMemcpyHostToDevice));
+    // the training marcher's bitfield and density mean from the f32 grid (train_density_update's tail)
+    HIPCHK(hipMemcpy(c->d_grid_f32.p, t.grid.p, (size_t)n_cells * 4, hipMemcpyDeviceToDevice));
+    launch_bitfield(nullptr, c->max_cascade, c->d_grid_f32.as<float>(), c->d_partial.as<double>(), c->d_mean.as<float>(), c->d_bitfield.as<uint8_t>(),
+                    c->d_occ_linear.as<uint32_t>(), c->s_nerf);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->s_nerf));
+    c->has_bitfield = true;
+}
+
 void load_snapshot(sng_ctx* c, const std::string& path) {
     ParsedSnapshot ps = parse_snapshot(path);
     const JValue& snap = ps.root["snapshot"];
@@ -1886,6 +1950,181 @@ void load_snapshot(sng_ctx* c, const std::string& path) {
         if (cam.contains("scale")) c->m_scale = cam["scale"].as_float();
     }
     if (snap.contains("exposure")) c->params["exposure"] = snap["exposure"].as_num();
+    if (snap.contains("optimizer")) restore_training_state(c, snap);
+}
+
+// ---- Testbed::save_snapshot (testbed.cu:4812-4876) ------------------------------------------------
+// m_network_config (base.json, with the model's encoding) + "snapshot": tcnn Trainer::serialize (n_params,
+// params_type, params_binary = the inference (EMA) params; with include_optimizer_state the optimizer
+// chain Ema -> ExponentialDecay -> Adam: weights_ema / first_moments / second_moments / param_steps /
+// current_step [tcnn, unvendored: key names restated from its source, parity unpinned]) and the Testbed
+// fields the reference writes.  Extension (ignored by the reference's loader): snapshot.sng holds what an
+// exact resume needs beyond those -- the fp32 master weights, the fp32 density grid and both pcg32 states.
+// .ingp: gzip-wrapped deflate (zstr::ostream; Z_NO_COMPRESSION when compress = 0); else plain msgpack.
+void put_vec3(MsgpackWriter& w, f3 v) { const float a[3] = {v.x, v.y, v.z}; w.nums(a, 3); }
+void put_mat43(MsgpackWriter& w, const float m[12]) {   // tcnn mat json: an array of the 4 columns
+    w.arr(4);
+    for (int i = 0; i < 4; ++i) w.nums(m + 3 * i, 3);
+}
+void put_aabb(MsgpackWriter& w, const aabb& b) { w.map(2); w.key("min"); put_vec3(w, b.lo); w.key("max"); put_vec3(w, b.hi); }
+void put_network_config(MsgpackWriter& w, const sng_nerf_config& g) {
+    w.key("loss"); w.map(1); w.key("otype"); w.str("Huber");
+    w.key("optimizer"); w.map(3); w.key("otype"); w.str("Ema"); w.key("decay"); w.num(0.95);
+    w.key("nested"); w.map(5); w.key("otype"); w.str("ExponentialDecay"); w.key("decay_start"); w.uint(20000); w.key("decay_interval"); w.uint(10000);
+    w.key("decay_base"); w.num(0.33);
+    w.key("nested"); w.map(6); w.key("otype"); w.str("Adam"); w.key("learning_rate"); w.num(1e-2); w.key("beta1"); w.num(0.9); w.key("beta2"); w.num(0.99);
+    w.key("epsilon"); w.num(1e-15); w.key("l2_reg"); w.num(1e-6);
+    w.key("encoding"); w.map(6); w.key("otype"); w.str("HashGrid"); w.key("n_levels"); w.uint(g.n_levels); w.key("n_features_per_level"); w.uint(g.n_features_per_level);
+    w.key("log2_hashmap_size"); w.uint(g.log2_hashmap_size); w.key("base_resolution"); w.uint(g.base_resolution);
+    w.key("per_level_scale"); w.num(g.per_level_scale);   // testbed.cu:3740 writes it back into the config
+    for (const char* name : {"network", "rgb_network"}) {
+        w.key(name); w.map(5); w.key("otype"); w.str("FullyFusedMLP"); w.key("activation"); w.str("ReLU"); w.key("output_activation"); w.str("None");
+        w.key("n_neurons"); w.uint(64); w.key("n_hidden_layers"); w.uint(name[0] == 'n' ? 1 : 2);
+    }
+    w.key("dir_encoding"); w.map(2); w.key("otype"); w.str("Composite");
+    w.key("nested"); w.arr(2); w.map(3); w.key("n_dims_to_encode"); w.uint(3); w.key("otype"); w.str("SphericalHarmonics"); w.key("degree"); w.uint(4);
+    w.map(1); w.key("otype"); w.str("Identity");
+}
+void save_snapshot(sng_ctx* c, const std::string& path, bool include_opt, bool compress) {
+    if (!c->has_model) throw SngError(SNG_ERR_STATE, "no model to save");
+    HIPCHK(hipStreamSynchronize(c->s_nerf));
+    const uint64_t n = c->n_params;
+    auto& t = c->tr;
+    const uint32_t n_cells = GRID_CELLS * (c->max_cascade + 1);
+    const std::vector<uint16_t> params = download<uint16_t>(c->d_params, n);
+    // m_nerf.density_grid (f32) -> fp16: the trained grid when training ran, else the loaded one
+    std::vector<float> grid32;
+    std::vector<uint16_t> grid16(n_cells, 0);
+    if (t.ready && t.grid.p) {
+        grid32 = download<float>(t.grid, n_cells);
+        for (uint32_t i = 0; i < n_cells; ++i) grid16[i] = f2h_host(grid32[i]);
+    } else if (c->has_bitfield && c->d_grid_f16.p) {
+        grid16 = download<uint16_t>(c->d_grid_f16, n_cells);
+    }
+    const bool opt = include_opt && t.ready;
+    MsgpackWriter w;
+    w.map(7);
+    put_network_config(w, c->cfg);
+    w.key("snapshot");
+    w.map(opt ? 21 : 19);
+    w.key("n_params"); w.uint(n);
+    w.key("params_type"); w.str("__half");
+    w.key("params_binary"); w.bin(params.data(), n * 2);
+    if (opt) {
+        const std::vector<float> ema = download<float>(t.ema, n), m1 = download<float>(t.m1, n), m2 = download<float>(t.m2, n);
+        const std::vector<uint32_t> ps = download<uint32_t>(t.steps, n);
+        w.key("optimizer"); w.map(2);
+        w.key("weights_ema_binary"); w.bin(ema.data(), n * 4);
+        w.key("nested"); w.map(1); w.key("nested"); w.map(5);
+        w.key("current_step"); w.uint(t.step);
+        w.key("base_learning_rate"); w.num(1e-2);
+        w.key("first_moments_binary"); w.bin(m1.data(), n * 4);
+        w.key("second_moments_binary"); w.bin(m2.data(), n * 4);
+        w.key("param_steps_binary"); w.bin(ps.data(), n * 4);
+        const std::vector<float> master = download<float>(t.master, n);
+        w.key("sng"); w.map(5);
+        w.key("master_binary"); w.bin(master.data(), n * 4);
+        w.key("density_grid_f32_binary"); w.bin(grid32.data(), grid32.size() * 4);
+        const uint64_t rng[4] = {t.rng.state, t.rng.inc, t.grid_rng.state, t.grid_rng.inc};
+        w.key("rng_binary"); w.bin(rng, sizeof(rng));
+        w.key("grid_ema_step"); w.uint(t.grid_ema_step);
+        w.key("loss_scalar"); w.num(t.last_loss);
+    }
+    w.key("version"); w.uint(1);   // SNAPSHOT_FORMAT_VERSION
+    w.key("mode"); w.str("Nerf");
+    w.key("density_grid_size"); w.uint(GRID_SIZE);
+    w.key("density_grid_binary"); w.bin(grid16.data(), grid16.size() * 2);
+    const float ident[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    w.key("nerf"); w.map(6);
+    w.key("aabb_scale"); w.uint(c->cfg.aabb_scale);
+    w.key("cam_pos_offset"); w.arr(0);
+    w.key("cam_rot_offset"); w.arr(0);
+    w.key("extra_dims_opt"); w.arr(0);
+    w.key("rgb"); w.map(3);
+    w.key("rays_per_batch"); w.uint(t.rays_per_batch);
+    w.key("measured_batch_size"); w.uint(t.measured);
+    w.key("measured_batch_size_before_compaction"); w.uint(t.measured_before);
+    w.key("dataset");
+    {   // NerfDataset to_json (json_binding.h:108-132); images are not part of a snapshot
+        const int ni = t.n_images;
+        std::vector<float> xf = ni ? download<float>(t.xforms, (size_t)ni * 12) : std::vector<float>();
+        std::vector<float> fo = ni ? download<float>(t.focal, (size_t)ni * 2) : std::vector<float>();
+        std::vector<float> pp = ni ? download<float>(t.pp, (size_t)ni * 2) : std::vector<float>();
+        w.map(ni ? 15 : 13);
+        w.key("n_images"); w.uint((uint64_t)ni);
+        w.key("paths"); w.arr((uint32_t)ni); for (int i = 0; i < ni; ++i) w.str("");
+        if (ni) {
+            w.key("metadata"); w.arr((uint32_t)ni);
+            for (int i = 0; i < ni; ++i) {
+                w.map(5);
+                w.key("focal_length"); w.nums(&fo[2 * i], 2);
+                w.key("lens"); w.map(0);
+                w.key("principal_point"); w.nums(&pp[2 * i], 2);
+                const float rs[4] = {0, 0, 0, 0};
+                w.key("rolling_shutter"); w.nums(rs, 4);
+                w.key("resolution"); w.arr(2); w.uint((uint64_t)t.w); w.uint((uint64_t)t.h);
+            }
+            w.key("xforms"); w.arr((uint32_t)ni);
+            for (int i = 0; i < ni; ++i) { w.map(2); w.key("start"); put_mat43(w, &xf[12 * i]); w.key("end"); put_mat43(w, &xf[12 * i]); }
+        }
+        w.key("render_aabb"); put_aabb(w, c->box);
+        w.key("render_aabb_to_local"); w.arr(3); for (int i = 0; i < 3; ++i) w.nums(ident + 3 * i, 3);
+        w.key("up"); put_vec3(w, c->up);
+        w.key("offset"); put_vec3(w, mk(0.5f, 0.5f, 0.5f));
+        w.key("envmap_resolution"); w.arr(2); w.uint(0); w.uint(0);
+        w.key("scale"); w.num(0.33);
+        w.key("aabb_scale"); w.uint(c->cfg.aabb_scale);
+        w.key("from_mitsuba"); w.boolean(false);
+        w.key("is_hdr"); w.boolean(false);
+        w.key("wants_importance_sampling"); w.boolean(true);
+        w.key("n_extra_learnable_dims"); w.uint(0);
+    }
+    w.key("training_step"); w.uint(t.step);
+    w.key("loss"); w.num(t.last_loss);
+    w.key("aabb"); put_aabb(w, c->box);
+    w.key("bounding_radius"); w.num(1.0);
+    w.key("render_aabb_to_local"); w.arr(3); for (int i = 0; i < 3; ++i) w.nums(ident + 3 * i, 3);
+    w.key("render_aabb"); put_aabb(w, c->box);
+    w.key("up_dir"); put_vec3(w, c->up);
+    w.key("sun_dir"); put_vec3(w, normalize(mk(1.0f, 1.0f, 1.0f)));
+    w.key("exposure"); w.num(c->p("exposure"));
+    const float bg[4] = {0, 0, 0, 0};
+    w.key("background_color"); w.nums(bg, 4);
+    w.key("camera"); w.map(10);
+    w.key("matrix"); put_mat43(w, c->cam);
+    w.key("fov_axis"); w.sint(c->fov_axis);
+    w.key("relative_focal_length"); w.nums(c->rel_focal, 2);
+    w.key("screen_center"); w.nums(c->screen_center, 2);
+    w.key("zoom"); w.num(c->zoom);
+    w.key("scale"); w.num(c->m_scale);
+    w.key("aperture_size"); w.num(0.0);
+    w.key("autofocus"); w.boolean(false);
+    const float af[3] = {0.5f, 0.5f, 0.5f};
+    w.key("autofocus_target"); w.nums(af, 3);
+    w.key("autofocus_depth"); w.num(0.0);
+    std::ofstream f(path, std::ios::binary);
+    if (!f) throw SngError(SNG_ERR_IO, "cannot write '" + path + "'");
+    const bool ingp = path.size() >= 5 && path.substr(path.size() - 5) == ".ingp";
+    if (!ingp) {
+        f.write(reinterpret_cast<const char*>(w.out.data()), (std::streamsize)w.out.size());
+    } else {
+        z_stream zs{};
+        if (deflateInit2(&zs, compress ? Z_DEFAULT_COMPRESSION : Z_NO_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+            throw SngError(SNG_ERR_IO, "zlib init failed");
+        std::vector<uint8_t> buf(1 << 20);
+        zs.next_in = w.out.data();
+        zs.avail_in = (uInt)w.out.size();
+        int r;
+        do {
+            zs.next_out = buf.data();
+            zs.avail_out = (uInt)buf.size();
+            r = deflate(&zs, Z_FINISH);
+            if (r == Z_STREAM_ERROR) { deflateEnd(&zs); throw SngError(SNG_ERR_IO, "zlib deflate failed"); }
+            f.write(reinterpret_cast<const char*>(buf.data()), (std::streamsize)(buf.size() - zs.avail_out));
+        } while (r != Z_STREAM_END);
+        deflateEnd(&zs);
+    }
+    if (!f) throw SngError(SNG_ERR_IO, "write failed '" + path + "'");
 }
 
 }  // namespace
@@ -1908,6 +2147,13 @@ int sng_ctx_create(const sng_ctx_desc* desc, sng_ctx** out) { return guarded([&]
 int sng_ctx_destroy(sng_ctx* ctx) { return guarded([&] { ctx_destroy(ctx); }); }
 
 int sng_load_snapshot(sng_ctx* c, const char* path) { return guarded([&] { HIPCHK(hipSetDevice(c->device)); load_snapshot(c, path); }); }
+int sng_save_snapshot(sng_ctx* c, const char* path, int32_t include_optimizer_state, int32_t compress) {
+    return guarded([&] {
+        if (!c || !path) throw SngError(SNG_ERR_INVALID, "null context or path");
+        HIPCHK(hipSetDevice(c->device));
+        save_snapshot(c, path, include_optimizer_state != 0, compress != 0);
+    });
+}
 int sng_snapshot_probe(const char* path, sng_nerf_config* cfg, uint64_t* n_params, uint64_t* n_grid_cells, uint16_t* params_out,
                        uint64_t params_cap, uint16_t* grid_out, uint64_t grid_cap) {
     return guarded([&] {

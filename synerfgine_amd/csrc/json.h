@@ -224,4 +224,56 @@ private:
     }
 };
 
+// JValue-free msgpack emitter (nlohmann::json::to_msgpack's encodings: the smallest int/str/bin/map
+// form; floats as float32 when exact, else float64), for Testbed::save_snapshot (testbed.cu:4812-4876).
+class MsgpackWriter {
+public:
+    std::vector<uint8_t> out;
+    void map(uint32_t n) { if (n < 16) u8(0x80 | n); else if (n < 65536) { u8(0xde); be(n, 2); } else { u8(0xdf); be(n, 4); } }
+    void arr(uint32_t n) { if (n < 16) u8(0x90 | n); else if (n < 65536) { u8(0xdc); be(n, 2); } else { u8(0xdd); be(n, 4); } }
+    void str(const std::string& v) {
+        const size_t n = v.size();
+        if (n < 32) u8(0xa0 | (uint8_t)n);
+        else if (n < 256) { u8(0xd9); be(n, 1); }
+        else if (n < 65536) { u8(0xda); be(n, 2); }
+        else { u8(0xdb); be(n, 4); }
+        out.insert(out.end(), v.begin(), v.end());
+    }
+    void bin(const void* p, size_t n) {
+        if (n < 256) { u8(0xc4); be(n, 1); }
+        else if (n < 65536) { u8(0xc5); be(n, 2); }
+        else { u8(0xc6); be(n, 4); }
+        const uint8_t* b = static_cast<const uint8_t*>(p);
+        out.insert(out.end(), b, b + n);
+    }
+    void uint(uint64_t v) {
+        if (v < 128) u8((uint8_t)v);
+        else if (v < 256) { u8(0xcc); be(v, 1); }
+        else if (v < 65536) { u8(0xcd); be(v, 2); }
+        else if (v <= 0xffffffffull) { u8(0xce); be(v, 4); }
+        else { u8(0xcf); be(v, 8); }
+    }
+    void sint(int64_t v) {
+        if (v >= 0) { uint((uint64_t)v); return; }
+        if (v >= -32) u8((uint8_t)(int8_t)v);
+        else if (v >= -128) { u8(0xd0); be((uint64_t)(uint8_t)(int8_t)v, 1); }
+        else if (v >= -32768) { u8(0xd1); be((uint64_t)(uint16_t)(int16_t)v, 2); }
+        else if (v >= INT32_MIN) { u8(0xd2); be((uint64_t)(uint32_t)(int32_t)v, 4); }
+        else { u8(0xd3); be((uint64_t)v, 8); }
+    }
+    void num(double v) {
+        const float f = (float)v;
+        if ((double)f == v) { uint32_t b; std::memcpy(&b, &f, 4); u8(0xca); be(b, 4); }
+        else { uint64_t b; std::memcpy(&b, &v, 8); u8(0xcb); be(b, 8); }
+    }
+    void boolean(bool v) { u8(v ? 0xc3 : 0xc2); }
+    void nil() { u8(0xc0); }
+    void key(const char* k) { str(k); }
+    void nums(const float* v, int n) { arr((uint32_t)n); for (int i = 0; i < n; ++i) num(v[i]); }
+
+private:
+    void u8(uint8_t v) { out.push_back(v); }
+    void be(uint64_t v, int bytes) { for (int k = bytes - 1; k >= 0; --k) out.push_back((uint8_t)(v >> (8 * k))); }
+};
+
 }  // namespace sng

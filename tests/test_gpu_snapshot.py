@@ -1,0 +1,128 @@
+"""`.ingp` writer: sng_save_snapshot = Testbed::save_snapshot (testbed.cu:4812-4876),
+including the optimizer state, and its round trip through sng_load_snapshot.
+
+Parity status: the keys and their encodings restate testbed.cu:4812-4864 and json_binding.h:108-132; the
+tcnn Trainer / optimizer serialisation (params_binary, weights_ema_binary, *_moments_binary,
+param_steps_binary, current_step) and zstr's gzip wrapper are unvendored (tiny-cuda-nn, zstr) -- parity
+unpinned; no reference-written .ingp exists in the container, so the files checked here are this
+library's own.
+"""
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+msgpack = pytest.importorskip("msgpack")
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BATCH = 1 << 14
+STEPS = 40
+
+# Testbed::save_snapshot's keys (testbed.cu:4813-4862) and Trainer::serialize's
+SNAPSHOT_KEYS = {"n_params", "params_type", "params_binary", "version", "mode", "density_grid_size", "density_grid_binary", "nerf",
+                 "training_step", "loss", "aabb", "bounding_radius", "render_aabb_to_local", "render_aabb", "up_dir", "sun_dir",
+                 "exposure", "background_color", "camera"}
+NERF_KEYS = {"aabb_scale", "cam_pos_offset", "cam_rot_offset", "extra_dims_opt", "rgb", "dataset"}
+CAMERA_KEYS = {"matrix", "fov_axis", "relative_focal_length", "screen_center", "zoom", "scale", "aperture_size", "autofocus",
+               "autofocus_target", "autofocus_depth"}
+DATASET_KEYS = {"n_images", "paths", "metadata", "xforms", "render_aabb", "render_aabb_to_local", "up", "offset", "envmap_resolution",
+                "scale", "aabb_scale", "from_mitsuba", "is_hdr", "wants_importance_sampling", "n_extra_learnable_dims"}
+
+
+def _decode(path):
+    with open(path, "rb") as f:
+        raw = f.read()
+    assert raw[:2] == b"\x1f\x8b"   # gzip member, as zstr::ostream writes
+    return msgpack.unpackb(zlib.decompress(raw, 47), raw=False, strict_map_key=False)
+
+
+@pytest.fixture(scope="module")
+def data():
+    from synerfgine_amd import nerf_data
+    return nerf_data.load_nerf_synthetic(os.path.join(REPO, "data", "nerf", "lego400"), max_images=8)
+
+
+def _testbed(data, cfg=None, params=None):
+    from synerfgine_amd import Engine, Testbed
+    tb = Testbed(0)
+    if cfg is not None:
+        tb.set_nerf_model(cfg, params)
+    eng = Engine(tb)
+    eng.set_param("train_batch", BATCH)
+    return tb, eng
+
+
+def _state(tb):
+    return {k: tb.train_debug(0, k, dt).copy() for k, dt in (("master", np.float32), ("m1", np.float32), ("m2", np.float32),
+                                                            ("steps", np.uint32), ("ema", np.float32), ("grid", np.float32))}
+
+
+def test_snapshot_round_trip_and_training_resume(data, tmp_path):
+    from synerfgine_amd import synthetic
+    imgs, xf, focal, pp = data
+    cfg, params = synthetic.random_init(1337)
+    a, ea = _testbed(data, cfg, params)
+    b = c = None
+    try:
+        a.set_training_dataset(imgs, xf, focal, pp)
+        a.train_reset(1337)
+        a.train(STEPS)
+        p_opt, p_plain = tmp_path / "a_opt.ingp", tmp_path / "a.ingp"
+        a.save_snapshot(p_opt, include_optimizer_state=True)
+        a.save_snapshot(p_plain)
+        # the reference's fields, the tcnn serialisation and the optimizer chain Ema -> ExponentialDecay -> Adam
+        root = _decode(p_opt)
+        snap = root["snapshot"]
+        assert SNAPSHOT_KEYS <= set(snap) and NERF_KEYS <= set(snap["nerf"]) and CAMERA_KEYS <= set(snap["camera"])
+        assert DATASET_KEYS <= set(snap["nerf"]["dataset"]) and snap["nerf"]["dataset"]["n_images"] == len(imgs)
+        assert snap["training_step"] == STEPS and snap["version"] == 1 and snap["params_type"] == "__half"
+        assert root["encoding"]["per_level_scale"] == pytest.approx(cfg["per_level_scale"])
+        adam = snap["optimizer"]["nested"]["nested"]
+        assert adam["current_step"] == STEPS and len(adam["first_moments_binary"]) == 4 * snap["n_params"]
+        assert "optimizer" not in _decode(p_plain)["snapshot"]
+        sa = _state(a)
+
+        # load into a fresh context: model, density grid and the whole training state
+        b, eb = _testbed(data)
+        b.load_snapshot(p_opt)
+        b.set_training_dataset(imgs, xf, focal, pp)
+        sb = _state(b)
+        for k in sa:
+            assert np.array_equal(sa[k].view(np.uint32), sb[k].view(np.uint32)), k
+        assert np.array_equal(a.density_grid_bitfield(), b.density_grid_bitfield())
+        for e in (ea, eb):
+            e.set_param("show_virtual_obj", 0)
+            e.set_param("res_factor", 8)
+            e.init(96, 54)
+        fa, fb = ea.frame().download("nerf_rgba"), eb.frame().download("nerf_rgba")
+        assert np.array_equal(fa, fb)
+        # saving the loaded state again gives the same content
+        b.save_snapshot(tmp_path / "b_opt.ingp", include_optimizer_state=True)
+        snap2 = _decode(tmp_path / "b_opt.ingp")["snapshot"]
+        for k in ("params_binary", "density_grid_binary"):
+            assert snap2[k] == snap[k], k
+        assert snap2["optimizer"]["weights_ema_binary"] == snap["optimizer"]["weights_ema_binary"]
+        assert snap2["camera"]["matrix"] == snap["camera"]["matrix"]
+
+        # the next step from the restored state follows the uninterrupted run (gradients are f32 atomics, so
+        # not bit-reproducible run to run); a reload without the optimizer state restarts Adam and lands elsewhere
+        c, _ = _testbed(data)
+        c.load_snapshot(p_plain)
+        c.set_training_dataset(imgs, xf, focal, pp)
+        for tb in (a, b, c):
+            tb.train(1)
+        m0 = sa["master"].astype(np.float64)
+        ua, ub, uc = ((tb.train_debug(0, "master", np.float32).astype(np.float64) - m0) for tb in (a, b, c))
+        rel_ab = np.linalg.norm(ua - ub) / np.linalg.norm(ua)
+        rel_ac = np.linalg.norm(ua - uc) / np.linalg.norm(ua)
+        mlp = slice(0, 3072 + 7168)   # the MLP weights: gradients summed over the whole batch
+        rel_ab_mlp = np.linalg.norm(ua[mlp] - ub[mlp]) / np.linalg.norm(ua[mlp])
+        print("resume: update rel. difference", rel_ab, "(MLP", rel_ab_mlp, ") vs without optimizer state", rel_ac)
+        # measured: 2e-8 (MLP 3e-7) resumed vs 5.4 restarted
+        assert rel_ab_mlp < 1e-4 and rel_ab < 1e-4 and rel_ac > 0.5, (rel_ab, rel_ab_mlp, rel_ac)
+    finally:
+        for tb in (a, b, c):
+            if tb is not None:
+                tb.close()
