@@ -423,6 +423,27 @@ def main():
         except Exception as e:
             result["c3_nerf_shadow_r"] = {"error": repr(e)}
         try:
+            if args.config in ("c3", "c4"):
+                # one counting frame (rt_count: the path / shadow kernels' counting instantiations, untimed) -> BVH
+                # work per frame; rates over the raytracer stage of the last timed frame
+                eng.set_param("rt_count", 1)
+                eng.frame(spp=0, reset=True)
+                eng.set_param("rt_count", 0)
+                cnt = eng.rt_counters()
+                rt_s = s0.ms_raytrace * 1e-3
+                q = cnt["path"]["queries"] + cnt["shadow"]["queries"]
+                boxes = cnt["path"]["box_tests"] + cnt["shadow"]["box_tests"]
+                tris = cnt["path"]["tri_tests"] + cnt["shadow"]["tri_tests"]
+                result["bvh"] = {"per_frame": cnt, "rays_per_s": round(q / rt_s, 1) if rt_s > 0 else None,
+                                 "box_tests_per_s": round(boxes / rt_s, 1) if rt_s > 0 else None,
+                                 "tri_tests_per_s": round(tris / rt_s, 1) if rt_s > 0 else None,
+                                 "raytrace_stage_ms": round(s0.ms_raytrace, 3),
+                                 "note": "rays = BVH world queries (camera + bounce rays of the path kernel, deferred shadow rays); rates "
+                                         "over the raytracer stream's device time of the last timed frame (path + shadow + accumulate "
+                                         "kernels; in the concurrent schedule the NeRF tail shares the GPU)"}
+        except Exception as e:
+            result["bvh"] = {"error": repr(e)}
+        try:
             result["abm_sweep"] = abm_sweep(args.model if args.config != "c4" else "lego", 3, 1)
         except Exception as e:
             result["abm_sweep"] = {"error": repr(e)}

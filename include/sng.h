@@ -181,6 +181,11 @@ int sng_get_resolution(sng_ctx* ctx, sng_resolution_info* out);
  * "animation_speed", "camera_path_playing" (Play/Pause), "camera_path_frame" (the frame slider);
  * read-only "camera_path_total_frames". */
 int sng_render_frame(sng_ctx* ctx, const sng_frame_params* params, sng_frame_result* out);
+/* Traversal counts of the last frame rendered with parameter rt_count = 1 (the deferred path tracer's
+ * counting instantiation; the timed kernels carry no counters): out[6] = path kernel {world queries
+ * (camera + bounce rays), box tests, triangle tests}, shadow-ray kernel {queries, box tests, triangle
+ * tests}.  Zeros when no counting frame ran. */
+int sng_rt_counters(sng_ctx* ctx, uint64_t* out);
 /* Band composition for tiled multi-GPU frames (the reference has no multi-GPU render): the
  * last frame's final RGBA rows [row_begin, row_end) at mesh resolution as RGBA8 (unorm8 =
  * round(clamp(c, 0, 1) * 255), one uint32 per px, R in the low byte) into the device buffer d_out,

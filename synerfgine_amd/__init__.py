@@ -222,6 +222,13 @@ class Engine:
         check(self._lib.sng_render_frame(self.ctx, ctypes.byref(p), ctypes.byref(r)))
         return FrameResult(self, r)
 
+    def rt_counters(self):
+        """Traversal counts of the last rt_count = 1 frame: {path, shadow} x {queries, box_tests, tri_tests}."""
+        out = (ctypes.c_uint64 * 6)()
+        check(self._lib.sng_rt_counters(self.ctx, out))
+        keys = ("queries", "box_tests", "tri_tests")
+        return {"path": dict(zip(keys, out[0:3])), "shadow": dict(zip(keys, out[3:6]))}
+
     def render_nerf(self, spp=0, reset=True, rows=None, render_mode=None, collect_kernel_times=False, target_n_queries=0):
         """Testbed::render_nerf: the instant-NGP tracer (composite_kernel_nerf + shade_kernel_nerf), NeRF only."""
         if render_mode is not None:

@@ -148,6 +148,7 @@ SIGNATURES = {
     "sng_ctx_destroy": (ctypes.c_int, [P]),
     "sng_load_snapshot": (ctypes.c_int, [P, ctypes.c_char_p]),
     "sng_save_snapshot": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32]),
+    "sng_rt_counters": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
     "sng_snapshot_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(sng_nerf_config), ctypes.POINTER(U64), ctypes.POINTER(U64), U16P, U64,
                                           U16P, U64]),
     "sng_set_nerf_model": (ctypes.c_int, [P, ctypes.POINTER(sng_nerf_config), U16P, U64]),

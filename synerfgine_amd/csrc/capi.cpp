@@ -390,6 +390,7 @@ const std::map<std::string, double>& default_params() {
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
         {"nerf_gen_wide", 0},                   // cascaded generate with 1024-thread workgroups while no fused tail runs
         {"nerf_gen_blocks", -1},                 // generate grid (256-thread units): 0 = min(rays, 8 per CU); -1 = all rays in one trip
+        {"rt_count", 0},                        // count BVH queries / box / triangle tests of the deferred raytracer (sng_rt_counters)
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
         {"nerf_onestep_horizon", 2048},         // iterations one speculative segment of the regime spans
     };
@@ -460,6 +461,7 @@ struct sng_ctx {
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf rt_hint;                        // sample-parallel path kernel: per-pixel hit-depth sums of the previous frame (u8)
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
+    DevBuf rt_counts;                      // rt_count frames: path / shadow kernel {queries, box tests, triangle tests}
     DevBuf rt_hits, rt_rays, rt_next_pos, rt_tail, rt_counters;   // staged path tracer
     bool fused_last = false;               // the last trace finished in the fused kernel
     uint32_t fused_k0 = 0;                 // ... from this iteration on
@@ -1345,6 +1347,11 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             ra.persistent_blocks = (uint32_t)std::max(1, c->n_cus - std::max(0, reserve));
             c->rt_work.ensure(RT_WORK_WORDS * sizeof(uint32_t));
             ra.work = c->rt_work.as<uint32_t>();
+            if (c->p("rt_count") != 0.0 && phase != 1) {   // counting frame: traversal counters (sng_rt_counters)
+                c->rt_counts.ensure(8 * sizeof(unsigned long long));
+                HIPCHK(hipMemsetAsync(c->rt_counts.p, 0, 8 * sizeof(unsigned long long), c->s_rt));
+                ra.counts = c->rt_counts.as<unsigned long long>();
+            }
             // sample-parallel path kernel: 2..64 samples, <= 2 bounces, its own 8x8 tile pieces, not with the
             // staged or deferred-shading variants
             const double rs = c->p("rt_spec");
@@ -2147,6 +2154,16 @@ int sng_ctx_create(const sng_ctx_desc* desc, sng_ctx** out) { return guarded([&]
 int sng_ctx_destroy(sng_ctx* ctx) { return guarded([&] { ctx_destroy(ctx); }); }
 
 int sng_load_snapshot(sng_ctx* c, const char* path) { return guarded([&] { HIPCHK(hipSetDevice(c->device)); load_snapshot(c, path); }); }
+int sng_rt_counters(sng_ctx* c, uint64_t* out) {
+    return guarded([&] {
+        if (!c || !out) throw SngError(SNG_ERR_INVALID, "null context or output");
+        HIPCHK(hipSetDevice(c->device));
+        std::memset(out, 0, 6 * sizeof(uint64_t));
+        if (!c->rt_counts.p) return;
+        HIPCHK(hipStreamSynchronize(c->s_rt));
+        HIPCHK(hipMemcpy(out, c->rt_counts.p, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    });
+}
 int sng_save_snapshot(sng_ctx* c, const char* path, int32_t include_optimizer_state, int32_t compress) {
     return guarded([&] {
         if (!c || !path) throw SngError(SNG_ERR_INVALID, "null context or path");

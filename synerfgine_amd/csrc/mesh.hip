@@ -31,12 +31,15 @@ struct Stack {
 // triangles were copied once per workgroup into LDS (scene blob, capi.cpp upload_scene) and the
 // stack is only as deep as the deepest BVH needs (max depth + 2 <= 32, so the reference's
 // FixedStack<32> overflow rule can never trigger differently).
-template <bool LDS>
+// CNT = true (bench's counting frames only, sng_rt_counters): cnt -> this thread's {world queries,
+// box tests, triangle tests}; the timed kernels are the CNT = false instantiations (no counting code).
+template <bool LDS, bool CNT = false>
 struct TraceCtx {
     int* stack;            // this thread's first stack slot
     int stride;
     const char* scene;     // LDS scene blob (LDS = true)
     int flat;              // near child in a register (bvh_walk_near)
+    uint32_t* cnt = nullptr;
     __device__ __forceinline__ const BvhNode* nodes(const ObjectGpu& o) const {
         if constexpr (LDS) return reinterpret_cast<const BvhNode*>(scene + o.lds_nodes);
         else return o.nodes;
@@ -72,6 +75,17 @@ __device__ __forceinline__ uint32_t wave_alloc(uint32_t* counter, int lane) {
     return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
 }
 
+// counting frames: the wave's {queries, box tests, triangle tests} into dst[0..2] (one atomic each per wave)
+__device__ __forceinline__ void flush_counts(unsigned long long* dst, const uint32_t (&c)[3], int lane) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        unsigned long long v = c[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+        if (lane == 0 && v) atomicAdd(dst + k, v);
+    }
+}
+
 // Triangle::ray_intersect (triangle.cuh:45-59) fused with the caller's `t < mint` test: t is
 // formed first and u, v only when t can win.  The accept set is unchanged: the reference replaces
 // a rejected t by FLT_MAX, which never passes `t < mint` (mint <= MAX_DEPTH), and a NaN t fails
@@ -95,7 +109,7 @@ __device__ __forceinline__ bool tri_hit(const Tri& tr, f3 ro, f3 rd, float mint,
 // object allow it, which removes 12 IEEE divisions per interior node without changing a bit.
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __restrict__ nodes, const Tri* __restrict__ tris, int* stack_lds,
-                                          int stride, int& tri_out, float t_max) {
+                                          int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
     Stack st{stack_lds, stride, 0};
     st.push(0);
     float mint = t_max;
@@ -105,6 +119,7 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
         const BvhNode node = nodes[idx];
         if (node.left < 0) {
             const int end = -node.right - 1;
+            if (cnt) cnt[2] += (uint32_t)(end + node.left + 1);
             for (int i = -node.left - 1; i < end; ++i) {
                 float t;
                 if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
@@ -114,6 +129,7 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
             const BvhNode n0 = nodes[c0], n1 = nodes[c1];
             const aabb b0 = {mk(n0.lo[0], n0.lo[1], n0.lo[2]), mk(n0.hi[0], n0.hi[1], n0.hi[2])};
             const aabb b1 = {mk(n1.lo[0], n1.lo[1], n1.lo[2]), mk(n1.hi[0], n1.hi[1], n1.hi[2])};
+            if (cnt) cnt[1] += 2u;
             float d0 = FAST ? aabb_entry_fast(b0, ro, rd, y) : aabb_entry(b0, ro, rd);
             float d1 = FAST ? aabb_entry_fast(b1, ro, rd, y) : aabb_entry(b1, ro, rd);
             // sorting_network<2>: descending, so the nearer child is pushed last
@@ -130,7 +146,7 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
 // triangle order, so identical results; one record load per inner node, none per leaf.
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const Tri* __restrict__ tris, int root_ref,
-                                               int* stack_lds, int stride, int& tri_out, float t_max) {
+                                               int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
     Stack st{stack_lds, stride, 0};
     st.push(root_ref);
     float mint = t_max;
@@ -140,6 +156,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
         if (ref < 0) {
             const uint32_t e = ~(uint32_t)ref;
             const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
+            if (cnt) cnt[2] += (uint32_t)(end - b);
             for (int i = b; i < end; ++i) {
                 float t;
                 if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
@@ -148,6 +165,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
             const BvhWide w = wide[ref];
             const aabb b0 = {mk(w.lo0[0], w.lo0[1], w.lo0[2]), mk(w.hi0[0], w.hi0[1], w.hi0[2])};
             const aabb b1 = {mk(w.lo1[0], w.lo1[1], w.lo1[2]), mk(w.hi1[0], w.hi1[1], w.hi1[2])};
+            if (cnt) cnt[1] += 2u;
             float d0 = FAST ? aabb_entry_fast(b0, ro, rd, y) : aabb_entry(b0, ro, rd);
             float d1 = FAST ? aabb_entry_fast(b1, ro, rd, y) : aabb_entry(b1, ro, rd);
             int i0 = w.ref0, i1 = w.ref1;
@@ -166,7 +184,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
 // never holds more than max BVH depth + 2 <= 32 entries, capi.cpp upload_scene.)
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const Tri* __restrict__ tris, int root_ref,
-                                               int* stack_lds, int stride, int& tri_out, float t_max) {
+                                               int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
     Stack st{stack_lds, stride, 0};
     float mint = t_max;
     int shortest = -1;
@@ -181,6 +199,7 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
         if (cur < 0) {
             const uint32_t e = ~(uint32_t)cur;
             const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
+            if (cnt) cnt[2] += (uint32_t)(end - b);
             for (int i = b; i < end; ++i) {
                 float t;
                 if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
@@ -190,6 +209,7 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
         const BvhWide w = wide[cur];
         const aabb b0 = {mk(w.lo0[0], w.lo0[1], w.lo0[2]), mk(w.hi0[0], w.hi0[1], w.hi0[2])};
         const aabb b1 = {mk(w.lo1[0], w.lo1[1], w.lo1[2]), mk(w.hi1[0], w.hi1[1], w.hi1[2])};
+        if (cnt) cnt[1] += 2u;
         float d0 = FAST ? aabb_entry_fast(b0, ro, rd, y) : aabb_entry(b0, ro, rd);
         float d1 = FAST ? aabb_entry_fast(b1, ro, rd, y) : aabb_entry(b1, ro, rd);
         int i0 = w.ref0, i1 = w.ref1;
@@ -211,29 +231,30 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
 
 // t_max < MAX_DEPTH culls everything at or beyond t_max (the result is then min(closest, t_max));
 // only the shadow kernel uses it, where any value >= full_dist yields the same mask.
-template <bool LDS>
-__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, const TraceCtx<LDS>& cx, int& tri, float t_max = MAX_DEPTH) {
+template <bool LDS, bool CNT = false>
+__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, const TraceCtx<LDS, CNT>& cx, int& tri, float t_max = MAX_DEPTH) {
     const f3 oro = mul(o.world_to_obj, ro - o.pos);
     const f3 ord = mul(o.world_to_obj, rd);
     const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
     if (o.wide && cx.flat) {
-        if (fast) return bvh_walk_near<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
-        return bvh_walk_near<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
+        if (fast) return bvh_walk_near<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+        return bvh_walk_near<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
     }
     if (o.wide) {
-        if (fast) return bvh_walk_wide<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
-        return bvh_walk_wide<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max);
+        if (fast) return bvh_walk_wide<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+        return bvh_walk_wide<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
     }
-    if (fast) return bvh_walk<true>(oro, ord, inv(ord), cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max);
-    return bvh_walk<false>(oro, ord, ord, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max);
+    if (fast) return bvh_walk<true>(oro, ord, inv(ord), cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+    return bvh_walk<false>(oro, ord, ord, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
 }
 
 // sng::depth_test_world (common.cu:36-48)
-template <bool LDS>
-__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS>& cx, int& out_obj,
+template <bool LDS, bool CNT = false>
+__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, int& out_obj,
                                   float t_max = MAX_DEPTH) {
     float depth = MAX_DEPTH;
     const f3 off = origin + dir * MIN_DEPTH;
+    if constexpr (CNT) cx.cnt[0] += 1u;
     for (int c = 0; c < n_objs; ++c) {
         int tri;
         const float t = object_intersect(off, dir, objs[c], cx, tri, t_max);
@@ -250,9 +271,10 @@ struct Hit {
 };
 __device__ __forceinline__ f3 tri_normal(const Tri& t) { return normalize(cross(t.b - t.a, t.c - t.a)); }
 // sng::depth_test_world(+HitRecord) (common.cu:50-67)
-template <bool LDS>
-__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS>& cx, Hit& h) {
+template <bool LDS, bool CNT = false>
+__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, Hit& h) {
     const f3 off = origin + dir * MIN_DEPTH;
+    if constexpr (CNT) cx.cnt[0] += 1u;
     int out_obj = -1;
     h.t = MAX_DEPTH;
     h.normal = splat(0.0f);
@@ -430,19 +452,19 @@ __device__ __forceinline__ f3 cone_random_frame(f3 orig, const m3& frame, float 
 //                colour sums in the original order.  Bit-identical to DEFER = false.
 // Dynamic LDS of the traversal kernels: [scene blob (LDS = true)][stack: stack_depth x blockDim ints].
 // Workgroups are persistent (grid-stride), so each copies the scene blob once.
-template <bool LDS>
-__device__ __forceinline__ TraceCtx<LDS> trace_ctx_setup(const RaytraceArgs& a) {
+template <bool LDS, bool CNT = false>
+__device__ __forceinline__ TraceCtx<LDS, CNT> trace_ctx_setup(const RaytraceArgs& a, uint32_t* cnt = nullptr) {
     extern __shared__ float4 smem4[];
     if constexpr (LDS) {
         for (uint32_t k = threadIdx.x; k < a.scene_f4; k += blockDim.x) smem4[k] = a.scene_blob[k];
         __syncthreads();
     }
     int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
-    return TraceCtx<LDS>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat};
+    return TraceCtx<LDS, CNT>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt};
 }
 
-template <bool DEFER, bool LDS>
-__device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS>& cx, uint32_t t,
+template <bool DEFER, bool LDS, bool CNT = false>
+__device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t t,
                                                const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
                                                uint32_t n_rng, float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
     const size_t i = (size_t)a.row0 * a.W + t;
@@ -591,14 +613,15 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
 // from a device counter (dynamic balance:
 // only ~15 % of the pixels hit an object and those cost ~100x the others).  Square tiles keep a
 // wave's primary rays coherent (fewer hit/miss-divergent waves than 64-pixel row segments).
-template <bool DEFER, bool LDS>
+template <bool DEFER, bool LDS, bool CNT = false>
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 4
 #endif
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void raytrace_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins,
                                                         const float4* __restrict__ dirs, uint32_t* __restrict__ rng, uint32_t n_rng,
                                                         float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
-    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    uint32_t counts[3] = {0u, 0u, 0u};
+    const TraceCtx<LDS, CNT> cx = trace_ctx_setup<LDS, CNT>(a, counts);
     const int lane = threadIdx.x & 63;
     const uint32_t rows = (uint32_t)(a.row1 - a.row0);
     const uint32_t T = (uint32_t)a.tile, tiles_x = ((uint32_t)a.W + T - 1) / T, n_tiles = tiles_x * ((rows + T - 1) / T);
@@ -615,6 +638,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PE
         if ((uint32_t)lane < T * T && x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth);
         if (a.tile_cost && lane == 0) a.tile_cost[tile] = (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull);
     }
+    if constexpr (CNT) flush_counts(a.counts, counts, lane);
 }
 
 // ===========================================================================================
@@ -654,8 +678,8 @@ __device__ __forceinline__ void xorwow_skip(Xorwow& r, uint32_t n) {
 
 // One sample of raytrace_pixel's loop from XORWOW offset `off`: returns hit depth, fills the hit
 // bounces, the first-bounce position and the state after the sample's last draw.
-template <bool LDS>
-__device__ __forceinline__ uint32_t spec_sample(const RaytraceArgs& a, const TraceCtx<LDS>& cx, const Xorwow& base, uint32_t off, f3 src_p, f3 src_d,
+template <bool LDS, bool CNT = false>
+__device__ __forceinline__ uint32_t spec_sample(const RaytraceArgs& a, const TraceCtx<LDS, CNT>& cx, const Xorwow& base, uint32_t off, f3 src_p, f3 src_d,
                                                 uint32_t n_light_draws, SpecBounce (&bh)[SPEC_MAXB], f3& p0, Xorwow& r_end) {
     Xorwow r = base;
     xorwow_skip(r, off);
@@ -707,7 +731,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SPEC_WAVES_
                                                              const float4* __restrict__ origins, const float4* __restrict__ dirs,
                                                              uint32_t* __restrict__ rng, uint32_t n_rng, float* __restrict__ acc_depth,
                                                              uint8_t* __restrict__ hint) {
-    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    const TraceCtx<LDS> cx = trace_ctx_setup<LDS, false>(a);
     const int lane = threadIdx.x & 63;
     const int SG = a.spec_group, PPW = 64 / SG;
     const int s = lane & (SG - 1), pw = lane / SG;
@@ -832,8 +856,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SPEC_WAVES_
 
 // depth_test_world(+HitRecord) (common.cu:50-67) without the normal/perturb (the shade stage
 // derives them from (obj, tri) with the same expressions)
-template <bool LDS>
-__device__ __forceinline__ int nearest_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS>& cx, float& t_out,
+template <bool LDS, bool CNT = false>
+__device__ __forceinline__ int nearest_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, float& t_out,
                                            int& tri_out) {
     const f3 off = origin + dir * MIN_DEPTH;
     int out_obj = -1, out_tri = -1;
@@ -858,7 +882,7 @@ template <bool LDS>
 __global__ __launch_bounds__(512) void rt_primary_kernel(RaytraceArgs a, RtStage st, uint32_t spp, uint32_t* __restrict__ work,
                                                           const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
                                                           uint32_t n_rng) {
-    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    const TraceCtx<LDS> cx = trace_ctx_setup<LDS, false>(a);
     const int lane = threadIdx.x & 63;
     const uint32_t rows = (uint32_t)(a.row1 - a.row0);
     const uint32_t tiles_x = ((uint32_t)a.W + 7) / 8, n_tiles = tiles_x * ((rows + 7) / 8);
@@ -985,7 +1009,7 @@ __global__ __launch_bounds__(256) void rt_shade_kernel(RaytraceArgs a, RtQueue q
 template <bool LDS>
 __global__ __launch_bounds__(512) void rt_bounce_kernel(RaytraceArgs a, RtStage st, const float4* __restrict__ rays_in, const uint32_t* __restrict__ n_rays_dev,
                                                          uint32_t* __restrict__ work) {
-    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    const TraceCtx<LDS> cx = trace_ctx_setup<LDS, false>(a);
     const int lane = threadIdx.x & 63;
     const uint32_t n_rays = *n_rays_dev;
     while (true) {
@@ -1055,9 +1079,10 @@ __global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, R
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
 // depend on its cap syn + 1 >= full_dist), so the result is bit-identical.
-template <bool LDS>
+template <bool LDS, bool CNT = false>
 __global__ __launch_bounds__(512) void shadow_rays_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work) {
-    const TraceCtx<LDS> cx = trace_ctx_setup<LDS>(a);
+    uint32_t counts[3] = {0u, 0u, 0u};
+    const TraceCtx<LDS, CNT> cx = trace_ctx_setup<LDS, CNT>(a, counts);
     const uint32_t n_rec = *q.count, total = n_rec * q.nps;
     const int lane = threadIdx.x & 63;
     // 64-ray chunks handed out by SHADOW_NCTR counters in separate memory channels: chunk c belongs to
@@ -1098,6 +1123,7 @@ __global__ __launch_bounds__(512) void shadow_rays_kernel(RaytraceArgs a, RtQueu
         const float sh = fminf(fminf(nerf, syn), full_dist);
         q.mask[q.mask_at(kr, jp)] = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
     }
+    if constexpr (CNT) flush_counts(a.counts + 3, counts, lane);
 }
 
 // Colour replay of the deferred raytracer, in raytrace_kernel's exact float order.
@@ -1256,7 +1282,13 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     const uint32_t n_tiles = (((uint32_t)a.W + a.tile - 1) / a.tile) * (((uint32_t)(a.row1 - a.row0) + a.tile - 1) / a.tile);
     const uint32_t bp = std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * 2);
     (void)shadow_blocks;
-    if (lds) {
+    if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in
+        allow_lds(raytrace_kernel<true, true, true>, lp);
+        allow_lds(shadow_rays_kernel<true, true>, ls);
+        hipLaunchKernelGGL((raytrace_kernel<true, true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
+        if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
+        hipLaunchKernelGGL((shadow_rays_kernel<true, true>), dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+    } else if (lds) {
         allow_lds(raytrace_kernel<true, true>, lp);
         allow_lds(shadow_rays_kernel<true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);

@@ -215,6 +215,7 @@ struct RaytraceArgs {
     int bvh_flat;               // BvhWide traversal with the nearer child in a register (bvh_walk_near)
     int tile;                   // path-kernel tile edge in pixels (8: 64 lanes, 4: 16 lanes per wave)
     int spec_group;             // > 0: sample-parallel path kernel (raytrace_spec_kernel), lanes per pixel
+    unsigned long long* counts; // counting frames (rt_count): path kernel {queries, box, tri}, shadow kernel {queries, box, tri}
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,

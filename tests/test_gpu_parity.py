@@ -490,3 +490,23 @@ def test_onestep_regime_equals_wavefront(config, w, h, target, shade, horizon):
         assert out[0][1:] == out[1][1:]
     finally:
         tb.close()
+
+
+def test_rt_counting_frame_is_exact():
+    """rt_count = 1 renders with the counting instantiations of the path and shadow-ray kernels: the frame is
+    bit-identical to the timed kernels' and the traversal counters are filled (sng_rt_counters)."""
+    tb, eng, _ = _engine(160, 90, {}, "c3")
+    try:
+        n0, m0 = eng.rng_states(0).copy(), eng.rng_states(1).copy()
+        out = []
+        for cnt in (0, 1):
+            eng.set_rng_states(0, n0)
+            eng.set_rng_states(1, m0)
+            eng.set_param("rt_count", cnt)
+            out.append(eng.frame().download("final_rgba"))
+        assert np.array_equal(out[0].view(np.uint32), out[1].view(np.uint32))
+        c = eng.rt_counters()
+        assert c["path"]["queries"] >= 160 * 90 and c["path"]["box_tests"] > c["path"]["queries"] and c["path"]["tri_tests"] > 0
+        assert c["shadow"]["queries"] > 0 and c["shadow"]["box_tests"] > 0
+    finally:
+        tb.close()

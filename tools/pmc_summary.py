@@ -44,13 +44,24 @@ def main():
         wa = sum(w) / len(w) if w else 0.0
         kernels[k] = {"launches": len(f), "fetch_kib_raw_avg": fa, "write_kib_avg": wa,
                       "hbm_bytes_per_launch": 2.0 * fa * 1024 + wa * 1024}
+    # per-launch HBM bytes of the kernels bench.py reports, keyed by plain name (launch-weighted over variants)
+    roof = {}
+    for key in ("nerf_network_kernel", "nerf_fused_kernel", "nerf_onestep_kernel", "generate_kernel", "composite_kernel", "raytrace_kernel",
+                "shadow_rays_kernel", "rt_accumulate_kernel", "shade_shadow_kernel", "init_rays_kernel"):
+        ks = [k for k in kernels if key in k]
+        n = sum(kernels[k]["launches"] for k in ks)
+        if not n:
+            continue
+        fetch = sum(2.0 * kernels[k]["fetch_kib_raw_avg"] * 1024 * kernels[k]["launches"] for k in ks) / n
+        wr = sum(kernels[k]["write_kib_avg"] * 1024 * kernels[k]["launches"] for k in ks) / n
+        roof[key] = {"launches": n, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": wr, "hbm_bytes_per_launch": fetch + wr}
     net = [k for k in kernels if "nerf_network_kernel" in k]
     res = {"note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes; averages over all launches of bench.py --steps 3 --warmup 1 --serial-streams",
            "kernel": net[0] if net else None,
            "hbm_bytes_per_launch": kernels[net[0]]["hbm_bytes_per_launch"] if net else None,
            "calibration_half_to_float": dict(kernels.get("half_to_float_kernel", {}), expected_read_bytes=2 * 128 ** 3,
                                              expected_write_bytes=4 * 128 ** 3),
-           "kernels": kernels}
+           "kernels": kernels, "roofline_kernels": roof, "config": sys.argv[3] if len(sys.argv) > 3 else None}
     # optional third pass: MFMA counters (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_F16, GRBM_GUI_ACTIVE)
     if glob.glob(f"{d}/MFMA/**/*counter_collection.csv", recursive=True) and net:
         busy, mops, gui = (load(d, c, "MFMA").get(net[0], []) for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16", "GRBM_GUI_ACTIVE"))
