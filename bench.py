@@ -346,6 +346,9 @@ def main():
     evaluated = total_samples - reused                      # network evaluations (launches + fused tail)
     tail_samples = evaluated - samples
     ms_tail = sum(s.ms_fused_tail for s in stats)
+    os_evals = sum(s.onestep_field_evals for s in stats)   # field evaluations inside the one-step regime's final pass
+    ms_os = sum(s.ms_onestep for s in stats)
+    tail_samples -= os_evals
     avg_launch_ms = ms_net / max(1, launches)
     bytes_per_launch = samples * BYTES_PER_SAMPLE / max(1, launches)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
@@ -409,8 +412,12 @@ def main():
                                         "ms": round(ms_tail, 4), "achieved": round(tail_gbs, 1), "frac": round(tail_gbs / HBM_PEAK_GBS, 4),
                                         "timing": "hipEvents around the tail launch (it runs beside the raytracer on reserved CUs in the "
                                                   "concurrent schedule, so its duration is latency, not throughput)"},
-                         "field_sample_weighted": {"samples": int(evaluated), "ms": round(field_ms, 4), "achieved": round(field_gbs, 1),
-                                                   "frac": round(field_gbs / HBM_PEAK_GBS, 4)}},
+                         "onestep_regime": {"kernels": "nerf_onestep_kernel x2 + schedule (trace_alt while n_alive > target/2; ray-local, "
+                                                       "periodic rays composited in a closed loop)", "field_evals": int(os_evals),
+                                            "ms": round(ms_os, 4)},
+                         "field_sample_weighted": {"samples": int(evaluated), "ms": round(field_ms + ms_os, 4),
+                                                   "achieved": round(evaluated * BYTES_PER_SAMPLE / ((field_ms + ms_os) * 1e-3) / 1e9, 1) if field_ms + ms_os > 0 else 0.0,
+                                                   "frac": round(evaluated * BYTES_PER_SAMPLE / ((field_ms + ms_os) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if field_ms + ms_os > 0 else 0.0}},
         }
     if rank == 0 and world == 1 and not args.no_sweep:
         # extra legs, after the timed region: C3 with NeRF shadows r = 2 (SURVEY §8d reports r = 0 and r = 2), and

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 1
+#define SNG_ABI_VERSION 2
 
 enum {
     SNG_OK = 0,
@@ -98,6 +98,9 @@ typedef struct {
     uint32_t onestep_from_iter; /* trace_alt's one-step regime (n_alive > target/2) marched ray-locally from this
                                    iteration (n_iterations: none) ... */
     uint32_t onestep_iterations;/* ... for this many iterations */
+    float ms_onestep;           /* device time of the one-step regime's kernels (collect_kernel_times) */
+    uint32_t onestep_field_evals; /* field evaluations of the regime's final pass (its samples are otherwise cached) */
+    uint32_t reserved2[6];
 } sng_frame_result;
 
 typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;
@@ -186,6 +189,9 @@ int sng_render_frame(sng_ctx* ctx, const sng_frame_params* params, sng_frame_res
  * (camera + bounce rays), box tests, triangle tests}, shadow-ray kernel {queries, box tests, triangle
  * tests}.  Zeros when no counting frame ran. */
 int sng_rt_counters(sng_ctx* ctx, uint64_t* out);
+/* Debug hook: copy a wavefront buffer of the last frame to the host -- "coords" (the last network
+ * launch's NerfCoordinates), "net_out" ([n][4] fp16 outputs), "samp" (per-ray {first, count}). */
+int sng_frame_buffer(sng_ctx* ctx, const char* name, void* out, uint64_t capacity_bytes, uint64_t* size_bytes);
 /* Band composition for tiled multi-GPU frames (the reference has no multi-GPU render): the
  * last frame's final RGBA rows [row_begin, row_end) at mesh resolution as RGBA8 (unorm8 =
  * round(clamp(c, 0, 1) * 255), one uint32 per px, R in the low byte) into the device buffer d_out,

@@ -157,7 +157,7 @@ class FrameResult:
         for name in ("n_iterations", "n_hit", "n_samples", "n_reference_slots", "ms_frame", "ms_raytrace", "ms_nerf", "ms_shadow",
                      "ms_overlay", "ms_network", "network_launches",
                      "fused_from_iter", "n_samples_network", "ms_fused_tail", "n_samples_reused",
-                     "onestep_from_iter", "onestep_iterations"):
+                     "onestep_from_iter", "onestep_iterations", "ms_onestep", "onestep_field_evals"):
             setattr(self, name, getattr(r, name))
         self.alive_per_iter = list(r.alive_per_iter)[: min(64, r.n_iterations)]
         self.steps_per_iter = list(r.steps_per_iter)[: min(64, r.n_iterations)]
@@ -221,6 +221,14 @@ class Engine:
         r = _lib.sng_frame_result()
         check(self._lib.sng_render_frame(self.ctx, ctypes.byref(p), ctypes.byref(r)))
         return FrameResult(self, r)
+
+    def frame_buffer(self, name, dtype=np.float32):
+        """Debug hook (sng_frame_buffer): a wavefront buffer of the last frame, e.g. "coords"."""
+        size = ctypes.c_uint64(0)
+        check(self._lib.sng_frame_buffer(self.ctx, name.encode(), None, 0, ctypes.byref(size)))
+        out = np.empty(size.value // np.dtype(dtype).itemsize, dtype)
+        check(self._lib.sng_frame_buffer(self.ctx, name.encode(), out.ctypes.data_as(ctypes.c_void_p), out.nbytes, None))
+        return out
 
     def rt_counters(self):
         """Traversal counts of the last rt_count = 1 frame: {path, shadow} x {queries, box_tests, tri_tests}."""

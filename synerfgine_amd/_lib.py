@@ -84,6 +84,9 @@ class sng_frame_result(ctypes.Structure):
         ("n_samples_reused", ctypes.c_uint64),
         ("onestep_from_iter", ctypes.c_uint32),
         ("onestep_iterations", ctypes.c_uint32),
+        ("ms_onestep", ctypes.c_float),
+        ("onestep_field_evals", ctypes.c_uint32),
+        ("reserved2", ctypes.c_uint32 * 6),
     ]
 
 
@@ -149,6 +152,7 @@ SIGNATURES = {
     "sng_load_snapshot": (ctypes.c_int, [P, ctypes.c_char_p]),
     "sng_save_snapshot": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32]),
     "sng_rt_counters": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
+    "sng_frame_buffer": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "sng_snapshot_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(sng_nerf_config), ctypes.POINTER(U64), ctypes.POINTER(U64), U16P, U64,
                                           U16P, U64]),
     "sng_set_nerf_model": (ctypes.c_int, [P, ctypes.POINTER(sng_nerf_config), U16P, U64]),
@@ -202,6 +206,9 @@ SIGNATURES = {
 _lib = None
 
 
+ABI_VERSION = 2   # SNG_ABI_VERSION of include/sng.h
+
+
 def load():
     """Load libsng_hip.so; raises if it has not been built (no silent fallback)."""
     global _lib
@@ -214,6 +221,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.sng_abi_version() != ABI_VERSION:   # the struct mirrors below follow include/sng.h of this version
+        raise ImportError(f"libsng_hip.so ABI {lib.sng_abi_version()} != {ABI_VERSION}; rebuild it")
     _lib = lib
     return lib
 

@@ -390,6 +390,7 @@ const std::map<std::string, double>& default_params() {
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
         {"nerf_gen_wide", 0},                   // cascaded generate with 1024-thread workgroups while no fused tail runs
         {"nerf_gen_blocks", -1},                 // generate grid (256-thread units): 0 = min(rays, 8 per CU); -1 = all rays in one trip
+        {"nerf_ray_tile", 0},                   // > 0: NeRF rays enter the wavefront in tiles of this many pixels squared
         {"rt_count", 0},                        // count BVH queries / box / triangle tests of the deferred raytracer (sng_rt_counters)
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
         {"nerf_onestep_horizon", 2048},         // iterations one speculative segment of the regime spans
@@ -1047,6 +1048,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     a.spp = P.spp;
     a.snap = 0;
     a.reset = P.reset_accumulation ? 1 : 0;
+    a.ray_tile = (int)std::max(0.0, c->p("nerf_ray_tile"));
     a.target_n_queries = target;
     a.mode = mode;
     const bool gsched = c->sched_comm.active();
@@ -1132,7 +1134,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 oa.p = p; oa.target = target;
                 if (!c->os_ran && P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_os0, c->s_nerf));
                 const uint32_t horizon = (uint32_t)std::max(1.0, c->p("nerf_onestep_horizon"));
-                launch_onestep_begin(oa, iter, horizon, c->s_nerf);
+                launch_onestep_begin(oa, iter, horizon, c->os_ran ? 0 : 1, c->s_nerf);
                 launch_onestep_pass(oa, c->net, 0, hc.n_alive[p], c->s_nerf);
                 HIPCHK(hipGetLastError());
                 if (gsched) {   // the frame-wide schedule: own-row deaths summed over the ranks
@@ -1241,6 +1243,10 @@ void march_stats(const sng_ctx* c, const sng_frame_params& P, sng_frame_result* 
     out->fused_from_iter = c->fused_last ? c->fused_k0 : c->h_ctrl->n_iter;
     out->onestep_from_iter = c->os_ran ? c->os_k : c->h_ctrl->n_iter;
     out->onestep_iterations = c->os_ran ? c->os_J : 0u;
+    if (c->os_ran) {
+        HIPCHK(hipMemcpy(c->h_os, c->os_state.p, sizeof(OnestepState), hipMemcpyDeviceToHost));
+        out->onestep_field_evals = (uint32_t)c->h_os->evals[1];
+    }
     out->n_reference_slots = ref_slots_of(c);
     std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
     std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
@@ -1259,11 +1265,7 @@ void network_times(sng_ctx* c, const sng_frame_params& P, uint32_t net_launches,
     }
     out->ms_network = tot;
     if (c->fused_last) HIPCHK(hipEventElapsedTime(&out->ms_fused_tail, c->ev_fused0, c->ev_fused1));
-    if (c->os_ran) {   // the one-step regime's ray-local passes count with the fused tail (field evaluations inside a march kernel)
-        float ms = 0.0f;
-        HIPCHK(hipEventElapsedTime(&ms, c->ev_os0, c->ev_os1));
-        out->ms_fused_tail += ms;
-    }
+    if (c->os_ran) HIPCHK(hipEventElapsedTime(&out->ms_onestep, c->ev_os0, c->ev_os1));
 }
 
 void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out) {
@@ -2154,6 +2156,18 @@ int sng_ctx_create(const sng_ctx_desc* desc, sng_ctx** out) { return guarded([&]
 int sng_ctx_destroy(sng_ctx* ctx) { return guarded([&] { ctx_destroy(ctx); }); }
 
 int sng_load_snapshot(sng_ctx* c, const char* path) { return guarded([&] { HIPCHK(hipSetDevice(c->device)); load_snapshot(c, path); }); }
+int sng_frame_buffer(sng_ctx* c, const char* name, void* out, uint64_t cap, uint64_t* size) {
+    return guarded([&] {
+        if (!c || !name) throw SngError(SNG_ERR_INVALID, "null context or name");
+        HIPCHK(hipSetDevice(c->device));
+        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}};
+        auto it = bufs.find(name);
+        if (it == bufs.end()) throw SngError(SNG_ERR_INVALID, std::string("unknown frame buffer ") + name);
+        HIPCHK(hipDeviceSynchronize());
+        if (size) *size = it->second->bytes;
+        if (out) HIPCHK(hipMemcpy(out, it->second->p, std::min<uint64_t>(cap, it->second->bytes), hipMemcpyDeviceToHost));
+    });
+}
 int sng_rt_counters(sng_ctx* c, uint64_t* out) {
     return guarded([&] {
         if (!c || !out) throw SngError(SNG_ERR_INVALID, "null context or output");

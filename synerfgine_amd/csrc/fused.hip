@@ -630,7 +630,7 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
     }
 }
 
-__global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k, uint32_t horizon) {
+__global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k, uint32_t horizon, int first) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ONESTEP_HIST; i += gridDim.x * blockDim.x) {
         a.deaths_local[i] = 0;
         a.deaths_sched[i] = 0;
@@ -647,7 +647,7 @@ __global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k, uint32_t horizon
         os->H = left < horizon ? left : horizon;   // a regime longer than the horizon continues in a new segment
         os->J = 0;
         os->work[0] = 0; os->work[1] = 0;
-        os->evals[0] = 0; os->evals[1] = 0;
+        if (first) { os->evals[0] = 0; os->evals[1] = 0; }   // accumulated over the segments of a frame
     }
 }
 
@@ -712,8 +712,8 @@ __global__ __launch_bounds__(1024) void onestep_schedule_kernel(OnestepArgs a) {
     }
 }
 
-void launch_onestep_begin(const OnestepArgs& a, uint32_t k, uint32_t horizon, hipStream_t s) {
-    hipLaunchKernelGGL(onestep_begin_kernel, dim3((ONESTEP_HIST + 255) / 256), dim3(256), 0, s, a, k, horizon);
+void launch_onestep_begin(const OnestepArgs& a, uint32_t k, uint32_t horizon, int first, hipStream_t s) {
+    hipLaunchKernelGGL(onestep_begin_kernel, dim3((ONESTEP_HIST + 255) / 256), dim3(256), 0, s, a, k, horizon, first);
 }
 void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(onestep_schedule_kernel, dim3(1), dim3(1024), 0, s, a);

@@ -74,8 +74,19 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
     f3 origin = a.cam.c3, dir = splat(0.0f);
     float tt = 0.0f;
     uint32_t idx = 0;
-    if (t < n_band) {
-        const int x = (int)(t % (uint32_t)a.W), y = a.row0 + (int)(t / (uint32_t)a.W);
+    int x, y;
+    bool in_band;
+    if (a.ray_tile > 0) {   // thread -> pixel in T x T tiles, tiles row-major over the band
+        const uint32_t T = (uint32_t)a.ray_tile, tiles_x = ((uint32_t)a.W + T - 1) / T, tile = t / (T * T), w = t % (T * T);
+        x = (int)((tile % tiles_x) * T + w % T);
+        y = a.row0 + (int)((tile / tiles_x) * T + w / T);
+        in_band = x < a.W && y < a.row1;
+    } else {
+        x = (int)(t % (uint32_t)a.W);
+        y = a.row0 + (int)(t / (uint32_t)a.W);
+        in_band = t < n_band;
+    }
+    if (in_band) {
         idx = (uint32_t)x + (uint32_t)a.W * (uint32_t)y;
         f2 off = ld_random_pixel_offset(a.snap ? 0u : a.spp);
         f2 uv = {((float)x + off.x) / (float)a.W, ((float)y + off.y) / (float)a.H};
@@ -473,8 +484,12 @@ void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s) { hipLaunchKernelGGL(ctrl_
 // ---------------------------------------------------------------------------
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm,
                       hipStream_t s) {
-    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
+    if (a.ray_tile > 0) {
+        const uint32_t T = (uint32_t)a.ray_tile;
+        n = (((uint32_t)a.W + T - 1) / T) * (((uint32_t)(a.row1 - a.row0) + T - 1) / T) * T * T;
+    }
     hipLaunchKernelGGL(init_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, out, ctrl, fb, depth, pos, nrm);
 }
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,

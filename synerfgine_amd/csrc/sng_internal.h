@@ -103,6 +103,8 @@ struct NerfFrameArgs {
     uint32_t spp;
     int snap;
     int reset;           // clear alpha of the frame buffer (camera moved)
+    int ray_tile;        // > 0: rays enter the buffer in ray_tile x ray_tile pixel tiles (2-D locality of the
+                         //      network launches' samples); 0: row-major.  Per-ray results do not depend on it
     uint32_t target_n_queries;
     TraceMode mode;
     Sched sched;
@@ -162,7 +164,7 @@ struct OnestepArgs {
     int p;
     uint32_t target;
 };
-void launch_onestep_begin(const OnestepArgs& a, uint32_t k, uint32_t horizon, hipStream_t s);
+void launch_onestep_begin(const OnestepArgs& a, uint32_t k, uint32_t horizon, int first, hipStream_t s);
 void launch_onestep_pass(const OnestepArgs& a, const NetworkDev& net, int final_pass, uint32_t n_rays_hint, hipStream_t s);
 void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s);
 
