@@ -117,6 +117,7 @@ def lib():
             "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
             "orc_num_threads": (i32, []), "orc_set_num_threads": (None, [i32]), "orc_set_mlp_accum": (None, [i32, i32]),
             "orc_set_visualization": (None, [i32, i32]),
+            "orc_set_gbuffer_out": (None, [vp, vp]),
             "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
             "orc_display": (None, [vp, i32, i32, i32, i32, vp, vp]),
             "orc_camera_set_view": (None, [vp, vp, vp, vp, vp, f32]),
@@ -306,7 +307,7 @@ def frame_params_from_engine(eng):
     return p
 
 
-def render_frame(model, vol, tb, eng, nerf_rng, mesh_rng, spp=0, target=0):
+def render_frame(model, vol, tb, eng, nerf_rng, mesh_rng, spp=0, target=0, gbuffer=False):
     """Whole Engine::frame on the CPU with the product's camera/scene/RNG inputs (rng arrays are advanced in place)."""
     r = eng.resolution()
     cam = tb.camera_matrix
@@ -319,10 +320,16 @@ def render_frame(model, vol, tb, eng, nerf_rng, mesh_rng, spp=0, target=0):
     final = np.zeros((mh, mw, 4), np.float32); final_d = np.zeros((mh, mw), np.float32)
     nrgba = np.zeros((nh, nw, 4), np.float32); ndepth = np.zeros((nh, nw), np.float32)
     st = orc_nerf_stats()
+    gpos = gnrm = None
+    if gbuffer:
+        gpos, gnrm = np.zeros((nh, nw, 3), np.float32), np.zeros((nh, nw, 3), np.float32)
+        lib().orc_set_gbuffer_out(ptr(gpos), ptr(gnrm))
     lib().orc_render_frame(model.ref(), ctypes.byref(vol), ctypes.byref(ncam), ctypes.byref(mcam), ctypes.byref(p), ctypes.addressof(oo),
                            len(objs), ctypes.addressof(ll), len(lights), ctypes.addressof(mm), len(mats), ptr(nerf_rng), ptr(mesh_rng), ptr(final), ptr(final_d), ptr(nrgba), ptr(ndepth),
                            ctypes.byref(st))
-    return dict(final=final, final_depth=final_d, nerf_rgba=nrgba, nerf_depth=ndepth, stats=st)
+    if gbuffer:
+        lib().orc_set_gbuffer_out(None, None)
+    return dict(final=final, final_depth=final_d, nerf_rgba=nrgba, nerf_depth=ndepth, stats=st, positions=gpos, normals=gnrm)
 
 
 # ---- online training (config 5) ----------------------------------------------------

@@ -1550,6 +1550,11 @@ void orc_overlay(const orc_frame_params* P, const float* syn_rgba, const float* 
 
 /* Engine::frame (synerfgine/engine.cu:352-433): raytrace -> NeRF render (+ shadows) -> overlay.
  * The mesh layer is re-initialised (camera reset semantics, raytracer.cu:327-336). */
+static float *g_gbuf_pos = nullptr, *g_gbuf_nrm = nullptr;
+void orc_set_gbuffer_out(float* positions, float* normals) {
+    g_gbuf_pos = positions;
+    g_gbuf_nrm = normals;
+}
 void orc_render_frame(const orc_model* m, const orc_volume* v, const orc_camera* nerf_cam, const orc_camera* mesh_cam,
                       const orc_frame_params* P, const orc_object* objs, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
                       const orc_material* mats, uint32_t n_mats, uint32_t* nerf_rng, uint32_t* mesh_rng,
@@ -1563,6 +1568,8 @@ void orc_render_frame(const orc_model* m, const orc_volume* v, const orc_camera*
     if (P->show_nerf) {
         std::vector<float> pos(3 * n_nerf), nrm(3 * n_nerf);
         orc_render_nerf(m, v, nerf_cam, nerf_rgba, nerf_depth, pos.data(), nrm.data(), stats);
+        if (g_gbuf_pos) std::memcpy(g_gbuf_pos, pos.data(), pos.size() * sizeof(float));   /* the NeRF G-buffer (A10c) */
+        if (g_gbuf_nrm) std::memcpy(g_gbuf_nrm, nrm.data(), nrm.size() * sizeof(float));
         if (P->shadow_on_nerf)
             orc_shade_nerf_shadows(v, nerf_cam->res, nerf_rgba, pos.data(), nrm.data(), objs, n_objs, lights, n_lights, nerf_rng,
                                    P->nerf_shadow_intensity, P->nerf_on_nerf_shadow_threshold, P->nerf_kernel_size);

@@ -205,7 +205,10 @@ void orc_set_num_threads(int32_t n);
  * accumulators, rounded to fp16 after every `chunk` (16) products */
 void orc_set_mlp_accum(int32_t mode, int32_t chunk);
 /* EncodingVis: Testbed::m_visualized_layer / m_visualized_dimension for orc_render_nerf_ngp(render_mode 10) */
-void orc_set_visualization(int32_t layer, int32_t dim);   /* OpenMP threads of the later calls (bench CPU baseline) */
+void orc_set_visualization(int32_t layer, int32_t dim);
+/* orc_render_frame also copies the NeRF G-buffer (positions, normals: 3 floats per NeRF pixel, before the
+ * shadow pass) into these host buffers when set (NULL: off) */
+void orc_set_gbuffer_out(float* positions, float* normals);   /* OpenMP threads of the later calls (bench CPU baseline) */
 
 #ifdef __cplusplus
 }

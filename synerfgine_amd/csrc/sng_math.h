@@ -376,6 +376,8 @@ SNG_HD bool occ_step(float& t, const StepSpace& cone, f3 o, f3 d, f3 idir, uint3
     mip = mip < min_mip ? min_mip : mip;
     mip = mip > max_mip ? max_mip : mip;
     if (!vol.bitfield || occupied_at(pos, vol.bitfield, mip)) return true;
+    // (loading every cascade's byte up front, to save the escalation's dependent loads, measured slower:
+    // C4 14.7 -> 13.7 frames/s -- empty-space trips rarely escalate more than once)
     while (mip < max_mip && !occupied_at(pos, vol.bitfield, mip + 1)) ++mip;
     t = advance_to_next_voxel(t, cone, pos, d, idir, mip);
     return false;

@@ -510,3 +510,31 @@ def test_rt_counting_frame_is_exact():
         assert c["shadow"]["queries"] > 0 and c["shadow"]["box_tests"] > 0
     finally:
         tb.close()
+
+
+def test_nerf_gbuffer_matches_oracle():
+    """the NeRF G-buffer the shadow pass reads -- extract_from_payload's positions and
+    write_normals_to_buffer's normals (testbed_nerf.cu:1523-1612) -- vs the oracle on the same frame."""
+    import oracle as O
+    tb, eng, (cfg, params, grid) = _engine(160, 90, {"show_virtual_obj": 0})
+    try:
+        nrng, mrng = eng.rng_states(0).copy(), eng.rng_states(1).copy()
+        r = eng.frame(spp=0, reset=True)
+        pos, nrm = r.download("nerf_positions"), r.download("nerf_normals")
+        ref = O.render_frame(O.Model(cfg, params), O.volume_for(cfg, grid), tb, eng, nrng, mrng, gbuffer=True)
+        rp, rn = ref["positions"], ref["normals"]
+        hit = np.abs(rp).sum(axis=-1) > 0
+        assert hit.mean() > 0.05
+        pos_ok = np.abs(pos - rp).max(axis=-1) <= 1e-5
+        assert pos_ok.mean() >= 0.99, pos_ok.mean()
+        # normals are finite differences of +-2 px neighbours: compare where the whole 5x5 neighbourhood agrees
+        from numpy.lib.stride_tricks import sliding_window_view
+        ok5 = np.zeros_like(pos_ok)
+        ok5[2:-2, 2:-2] = sliding_window_view(pos_ok, (5, 5)).all(axis=(-1, -2))
+        fin = np.isfinite(nrm).all(axis=-1)
+        assert np.array_equal(fin, np.isfinite(rn).all(axis=-1))   # background normalize(0) cases agree
+        m = ok5 & fin & hit
+        assert m.sum() > 100
+        assert (np.abs(nrm - rn).max(axis=-1)[m] <= 1e-4).mean() >= 0.995
+    finally:
+        tb.close()
