@@ -40,7 +40,7 @@ WORKLOADS = {
 }
 METRICS = {
     "c2": "rendered frames/sec at 800x800 (lego .ingp, NeRF only); PSNR vs ref",
-    "c3": "rendered frames/sec at 1920x1080 (lego .ingp + 1 mesh); PSNR vs ref",
+    "c3": "rendered frames/sec at 1920\u00d71080 (lego .ingp + 1 mesh); PSNR vs ref",   # BASELINE.json's metric, verbatim
     "c4": "rendered frames/sec at 1920x1080 (kitchen-like .ingp + 3 meshes, light_samples 4); PSNR vs ref",
 }
 

@@ -391,6 +391,7 @@ const std::map<std::string, double>& default_params() {
         {"nerf_gen_wide", 0},                   // cascaded generate with 1024-thread workgroups while no fused tail runs
         {"nerf_gen_blocks", -1},                 // generate grid (256-thread units): 0 = min(rays, 8 per CU); -1 = all rays in one trip
         {"nerf_ray_tile", 0},                   // > 0: NeRF rays enter the wavefront in tiles of this many pixels squared
+        {"rt_shadow_all_cus", 1},               // shadow-ray kernel on every CU: the NeRF tail has mostly finished by then (C3 +2 %; 0: the path kernel grid)
         {"rt_count", 0},                        // count BVH queries / box / triangle tests of the deferred raytracer (sng_rt_counters)
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
         {"nerf_onestep_horizon", 2048},         // iterations one speculative segment of the regime spans
@@ -1420,8 +1421,11 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                     launch_raytrace_spec(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
                                          c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), c->rt_hint.as<uint8_t>(), c->s_rt);
                 } else {
+                    // shadow-ray grid: the CUs the path kernel leaves to the NeRF tail too when rt_shadow_all_cus
+                    // (by then the tail has mostly finished)
+                    const uint32_t sb = c->p("rt_shadow_all_cus") != 0.0 ? (uint32_t)c->n_cus * 2 : 0u;
                     launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
-                                              c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), (uint32_t)c->n_cus * 16, c->s_rt);
+                                              c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt);
                 }
             } else {
                 launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),

@@ -1281,25 +1281,25 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
     const uint32_t n_tiles = (((uint32_t)a.W + a.tile - 1) / a.tile) * (((uint32_t)(a.row1 - a.row0) + a.tile - 1) / a.tile);
     const uint32_t bp = std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * 2);
-    (void)shadow_blocks;
+    const uint32_t sb = shadow_blocks ? shadow_blocks : a.persistent_blocks * 2;
     if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in
         allow_lds(raytrace_kernel<true, true, true>, lp);
         allow_lds(shadow_rays_kernel<true, true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
         if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
-        hipLaunchKernelGGL((shadow_rays_kernel<true, true>), dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+        hipLaunchKernelGGL((shadow_rays_kernel<true, true>), dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     } else if (lds) {
         allow_lds(raytrace_kernel<true, true>, lp);
         allow_lds(shadow_rays_kernel<true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
         if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
-        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     } else {
         allow_lds(raytrace_kernel<true, false>, lp);
         allow_lds(shadow_rays_kernel<false>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
         if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
-        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     }
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
 }
