@@ -324,7 +324,7 @@ bool wide_bvh(const std::vector<BvhNode>& nodes, std::vector<BvhWide>& wide, int
         if ((size_t)n.left + 1 >= nodes.size()) return false;
         BvhWide& w = wide[id[i]];
         const BvhNode &c0 = nodes[n.left], &c1 = nodes[n.left + 1];
-        for (int k = 0; k < 3; ++k) { w.lo0[k] = c0.lo[k]; w.hi0[k] = c0.hi[k]; w.lo1[k] = c1.lo[k]; w.hi1[k] = c1.hi[k]; }
+        for (int k = 0; k < 3; ++k) { w.s0[2 * k] = c0.lo[k]; w.s0[2 * k + 1] = c0.hi[k]; w.s1[2 * k] = c1.lo[k]; w.s1[2 * k + 1] = c1.hi[k]; }
         w.ref0 = ref_of(n.left);
         w.ref1 = ref_of(n.left + 1);
     }

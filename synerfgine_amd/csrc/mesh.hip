@@ -54,6 +54,23 @@ struct TraceCtx {
     }
 };
 
+// One BvhWide record: four 16-B loads (ds_read_b128 from the LDS scene blob).  d0, d1: the entry
+// distances of its two child boxes, exactly as aabb_entry(_fast) gives them.
+template <bool FAST>
+__device__ __forceinline__ void wide_visit(const BvhWide* __restrict__ rec, f3 ro, f3 rd, f3 y, float& d0, float& d1, int& ref0, int& ref1) {
+    const float4* r = reinterpret_cast<const float4*>(rec);
+    const float4 a = r[0], b = r[1], c = r[2], e = r[3];
+    if constexpr (FAST) {
+        d0 = slab_entry_fast(pf2{a.x, a.y}, pf2{a.z, a.w}, pf2{b.x, b.y}, ro, rd, y);
+        d1 = slab_entry_fast(pf2{b.z, b.w}, pf2{c.x, c.y}, pf2{c.z, c.w}, ro, rd, y);
+    } else {
+        d0 = aabb_entry(aabb{mk(a.x, a.z, b.x), mk(a.y, a.w, b.y)}, ro, rd);
+        d1 = aabb_entry(aabb{mk(b.z, c.x, c.z), mk(b.w, c.y, c.w)}, ro, rd);
+    }
+    ref0 = __float_as_int(e.x);
+    ref1 = __float_as_int(e.y);
+}
+
 // slot per lane with pred set, one atomic per wave
 __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred, int lane) {
     const unsigned long long mask = __ballot(pred);
@@ -162,14 +179,12 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
                 if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
             }
         } else {
-            const BvhWide w = wide[ref];
-            const aabb b0 = {mk(w.lo0[0], w.lo0[1], w.lo0[2]), mk(w.hi0[0], w.hi0[1], w.hi0[2])};
-            const aabb b1 = {mk(w.lo1[0], w.lo1[1], w.lo1[2]), mk(w.hi1[0], w.hi1[1], w.hi1[2])};
             if (cnt) cnt[1] += 2u;
-            float d0 = FAST ? aabb_entry_fast(b0, ro, rd, y) : aabb_entry(b0, ro, rd);
-            float d1 = FAST ? aabb_entry_fast(b1, ro, rd, y) : aabb_entry(b1, ro, rd);
-            int i0 = w.ref0, i1 = w.ref1;
-            if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = w.ref1; i1 = w.ref0; }
+            float d0, d1;
+            int r0, r1;
+            wide_visit<FAST>(wide + ref, ro, rd, y, d0, d1, r0, r1);
+            int i0 = r0, i1 = r1;
+            if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = r1; i1 = r0; }
             if (d0 < mint) { if (st.n >= BVH_STACK - 1) { } else st.push(i0); }
             if (d1 < mint) { if (st.n >= BVH_STACK - 1) { } else st.push(i1); }
         }
@@ -206,14 +221,12 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
             }
             continue;
         }
-        const BvhWide w = wide[cur];
-        const aabb b0 = {mk(w.lo0[0], w.lo0[1], w.lo0[2]), mk(w.hi0[0], w.hi0[1], w.hi0[2])};
-        const aabb b1 = {mk(w.lo1[0], w.lo1[1], w.lo1[2]), mk(w.hi1[0], w.hi1[1], w.hi1[2])};
         if (cnt) cnt[1] += 2u;
-        float d0 = FAST ? aabb_entry_fast(b0, ro, rd, y) : aabb_entry(b0, ro, rd);
-        float d1 = FAST ? aabb_entry_fast(b1, ro, rd, y) : aabb_entry(b1, ro, rd);
-        int i0 = w.ref0, i1 = w.ref1;
-        if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = w.ref1; i1 = w.ref0; }
+        float d0, d1;
+        int r0, r1;
+        wide_visit<FAST>(wide + cur, ro, rd, y, d0, d1, r0, r1);
+        int i0 = r0, i1 = r1;
+        if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = r1; i1 = r0; }
         // reference: push(far) if d0 < mint, push(near) if d1 < mint, then pop
         const bool far_in = d0 < mint, near_in = d1 < mint;
         if (near_in) {

@@ -161,23 +161,30 @@ SNG_HD float aabb_entry(const aabb& b, f3 pos, f3 dir) {
 // aabb_entry with each division x / dir_i evaluated as div_by(x, dir_i, 1/dir_i) -- bit-identical
 // to aabb_entry (Markstein correction, see div_by) provided no intermediate over/underflows, which
 // slab_fast_ok() guarantees for the ray and the host guarantees for the boxes (|coord| < 2^40).
-SNG_HD float aabb_entry_fast(const aabb& b, f3 pos, f3 dir, f3 y) {
+// Branch-free: with no NaN or infinity in play (slab_fast_ok), aabb_entry's swaps are min/max and
+// its two early-outs together test every pair (a_min > b_max, a != b), i.e. max(mins) > min(maxes);
+// the value returned otherwise is max(mins).  Only the sign of a zero result can differ, which no
+// caller observes (the result is only compared).
+// The (lo, hi) pair of each axis is one packed-f32 operand (v_pk_add/mul/fma: two lanes per op).
+typedef float pf2 __attribute__((ext_vector_type(2)));
+SNG_HD pf2 div_by2(pf2 x, float d, float y) {
+    const pf2 dd = {d, d}, yy = {y, y};
+    const pf2 q0 = x * yy;
+    const pf2 r = __builtin_elementwise_fma(-q0, dd, x);
+    return __builtin_elementwise_fma(r, yy, q0);
+}
+// sx, sy, sz: the box's (lo, hi) slab of each axis
+SNG_HD float slab_entry_fast(pf2 sx, pf2 sy, pf2 sz, f3 pos, f3 dir, f3 y) {
     const float FMAX = 3.402823466e+38f;
-    float tmin = div_by(b.lo.x - pos.x, dir.x, y.x);
-    float tmax = div_by(b.hi.x - pos.x, dir.x, y.x);
-    if (tmin > tmax) fswap(tmin, tmax);
-    float tymin = div_by(b.lo.y - pos.y, dir.y, y.y);
-    float tymax = div_by(b.hi.y - pos.y, dir.y, y.y);
-    if (tymin > tymax) fswap(tymin, tymax);
-    if (tmin > tymax || tymin > tmax) return FMAX;
-    if (tymin > tmin) tmin = tymin;
-    if (tymax < tmax) tmax = tymax;
-    float tzmin = div_by(b.lo.z - pos.z, dir.z, y.z);
-    float tzmax = div_by(b.hi.z - pos.z, dir.z, y.z);
-    if (tzmin > tzmax) fswap(tzmin, tzmax);
-    if (tmin > tzmax || tzmin > tmax) return FMAX;
-    if (tzmin > tmin) tmin = tzmin;
-    return tmin;
+    const pf2 tx = div_by2(sx - pos.x, dir.x, y.x);
+    const pf2 ty = div_by2(sy - pos.y, dir.y, y.y);
+    const pf2 tz = div_by2(sz - pos.z, dir.z, y.z);
+    const float tmin = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
+    const float tmax = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+    return tmin > tmax ? FMAX : tmin;
+}
+SNG_HD float aabb_entry_fast(const aabb& b, f3 pos, f3 dir, f3 y) {
+    return slab_entry_fast(pf2{b.lo.x, b.hi.x}, pf2{b.lo.y, b.hi.y}, pf2{b.lo.z, b.hi.z}, pos, dir, y);
 }
 constexpr float SLAB_FAST_MAX_COORD = 1099511627776.0f;   // 2^40
 SNG_HD bool slab_fast_ok(f3 pos, f3 dir) {
@@ -446,10 +453,11 @@ SNG_HD float curand_uniform(Xorwow& s) {
 struct BvhNode { float lo[3], hi[3]; int left, right; };   // TriangleBvhNode (32 B)
 struct Tri { f3 a, b, c; };                                 // Triangle (36 B)
 // Traversal layout of the same BVH (capi.cpp wide_bvh): one 64-B record per INNER node holding
-// both children's boxes and references, so visiting a node is one load and a leaf needs none
-// (its triangle range travels in the stack entry).  ref >= 0: inner record index;
-// ref < 0: leaf, ~ref = first_triangle | triangle_count << 24.
-struct BvhWide { float lo0[3], hi0[3], lo1[3], hi1[3]; int ref0, ref1, pad0, pad1; };
+// both children's boxes and references, so visiting a node is four 16-B loads and a leaf needs none
+// (its triangle range travels in the stack entry).  Each box is stored slab by slab
+// (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z) so that an axis is one packed-f32 register pair.
+// ref >= 0: inner record index; ref < 0: leaf, ~ref = first_triangle | triangle_count << 24.
+struct alignas(16) BvhWide { float s0[6], s1[6]; int ref0, ref1, pad0, pad1; };
 constexpr uint32_t WIDE_MAX_BEGIN = 1u << 24, WIDE_MAX_COUNT = 127u;
 struct ObjectGpu {                                           // ObjectTransform + hoisted inverse
     const BvhNode* nodes;

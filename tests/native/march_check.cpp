@@ -3,7 +3,7 @@
 //   1. div_by(x, d, RN(1/d)) == x / d bit for bit (random pairs + a sweep of t / MIN_STEP);
 //   2. advance_to_occupied_linear == the general advance_to_occupied (nerf_device.cuh:462-495) on
 //      cone == 0, max_mip == 0 volumes for random rays through a random occupancy grid;
-//   3. aabb_entry_fast == aabb_entry for random boxes and rays.
+//   3. aabb_entry_fast == aabb_entry for random boxes and rays, and for degenerate boxes / on-plane origins.
 #include "sng_math.h"
 #include <cstdio>
 #include <cstring>
@@ -84,7 +84,25 @@ int main() {
         if (it % 7 == 0) d = d * 37.5f;
         if (!slab_fast_ok(o, d)) continue;
         ++n_slab;
-        if (!same(aabb_entry_fast(box, o, d, inv(d)), aabb_entry(box, o, d))) ++bad_slab;
+        // equal up to the sign of a zero result (aabb_entry_fast's min/max form; callers only compare it)
+        const float fa = aabb_entry_fast(box, o, d, inv(d)), fb = aabb_entry(box, o, d);
+        if (!(same(fa, fb) || (fa == 0.0f && fb == 0.0f))) ++bad_slab;
+    }
+    // degenerate slabs and origins on a slab plane: the equal-value cases of the swaps and early-outs
+    for (int it = 0; it < 2000000; ++it) {
+        const float q[5] = {-0.5f, 0.0f, 0.25f, 0.5f, 1.0f};
+        f3 lo = mk(q[g() % 5], q[g() % 5], q[g() % 5]), hi = lo;
+        if (g() & 1) hi.x = fmaxf(hi.x, q[g() % 5]);
+        if (g() & 1) hi.y = fmaxf(hi.y, q[g() % 5]);
+        if (g() & 1) hi.z = fmaxf(hi.z, q[g() % 5]);
+        aabb box = {lo, hi};
+        f3 o = mk(q[g() % 5], q[g() % 5], q[g() % 5]);
+        if (g() & 1) o.x += U(g);
+        f3 d = mk(q[g() % 5] + 0.125f * (float)(g() % 3), q[g() % 5] - 0.0625f, q[g() % 5] + 0.375f);
+        if (d.x == 0.0f || d.y == 0.0f || d.z == 0.0f || !slab_fast_ok(o, d)) continue;
+        ++n_slab;
+        const float fa = aabb_entry_fast(box, o, d, inv(d)), fb = aabb_entry(box, o, d);
+        if (!(same(fa, fb) || (fa == 0.0f && fb == 0.0f))) ++bad_slab;
     }
     std::printf("{\"div\": [%ld, %ld], \"march\": [%ld, %ld, %ld], \"slab\": [%ld, %ld]}\n", n_div, bad_div, n_march, n_samples, bad_march,
                 n_slab, bad_slab);
