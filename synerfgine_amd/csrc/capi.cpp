@@ -299,7 +299,7 @@ struct HostObject {
     float scale = 1.0f;
     int mat = 0;
     ObjAnim anim;
-    DevBuf d_nodes, d_tris, d_wide;
+    DevBuf d_nodes, d_tris, d_trit, d_wide;
 };
 
 // BvhWide records of the inner nodes of a TriangleBvhNode array (children at left, left + 1).
@@ -678,7 +678,7 @@ uint32_t bvh_depth(const std::vector<BvhNode>& nodes) {
 
 void upload_scene(sng_ctx* c) {
     std::vector<ObjectGpu> og;
-    // scene blob: per object [nodes][triangles], each array 16-B aligned
+    // scene blob: per object [nodes or wide records][traversal triangles], each array 16-B aligned
     std::vector<uint8_t> blob;
     auto append = [&](const void* p, size_t bytes) {
         const size_t off = blob.size();
@@ -690,9 +690,13 @@ void upload_scene(sng_ctx* c) {
     for (auto& o : c->objs) {
         upload(o.d_nodes, o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
         upload(o.d_tris, o.tris.data(), o.tris.size() * sizeof(Tri));
+        std::vector<TriT> trit(o.tris.size());
+        for (size_t i = 0; i < o.tris.size(); ++i) trit[i] = make_trit(o.tris[i]);
+        upload(o.d_trit, trit.data(), trit.size() * sizeof(TriT));
         ObjectGpu g{};
         g.nodes = o.d_nodes.as<BvhNode>();
         g.tris = o.d_tris.as<Tri>();
+        g.trit = o.d_trit.as<TriT>();
         g.rot = o.rot;
         g.pos = o.pos;
         g.scale = o.scale;
@@ -714,7 +718,7 @@ void upload_scene(sng_ctx* c) {
         } else {
             g.lds_nodes = append(o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
         }
-        g.lds_tris = append(o.tris.data(), o.tris.size() * sizeof(Tri));
+        g.lds_trit = append(trit.data(), trit.size() * sizeof(TriT));
         c->bvh_depth = std::max(c->bvh_depth, bvh_depth(o.nodes));
         og.push_back(g);
     }
@@ -1343,7 +1347,14 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             // max stack use of the reference traversal is depth + 1; FixedStack<32> drops pushes at 31
             ra.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
             ra.bvh_flat = c->p("bvh_flat") != 0.0 ? 1 : 0;
-            ra.scene_in_lds = (c->p("scene_lds") != 0.0 && (uint64_t)c->scene_f4 * 16 + (uint64_t)ra.stack_depth * 512 * 4 <= 80u * 1024u) ? 1 : 0;
+            // blob + stacks in LDS: two 512-thread workgroups per CU (80 KB each), else one of 1024 threads
+            // (one blob copy per CU, 160 KB); both give 16 waves per CU
+            const uint64_t blob_b = (uint64_t)c->scene_f4 * 16;
+            const bool lds_ok = c->p("scene_lds") != 0.0;
+            ra.lds_tpb = 512;
+            ra.scene_in_lds = 0;
+            if (lds_ok && blob_b + (uint64_t)ra.stack_depth * 512 * 4 <= 80u * 1024u) ra.scene_in_lds = 1;
+            else if (lds_ok && blob_b + (uint64_t)ra.stack_depth * 1024 * 4 <= 160u * 1024u) { ra.scene_in_lds = 1; ra.lds_tpb = 1024; }
             // persistent raytracer grids leave `rt_reserved_cus` CUs' worth of room for the NeRF
             // wavefront running beside them on the other stream (concurrent mode only)
             const int reserve = concurrent && show_nerf ? (int)c->p("rt_reserved_cus") : 0;
@@ -1423,7 +1434,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 } else {
                     // shadow-ray grid: the CUs the path kernel leaves to the NeRF tail too when rt_shadow_all_cus
                     // (by then the tail has mostly finished)
-                    const uint32_t sb = c->p("rt_shadow_all_cus") != 0.0 ? (uint32_t)c->n_cus * 2 : 0u;
+                    const uint32_t sb = c->p("rt_shadow_all_cus") != 0.0 ? (uint32_t)c->n_cus * 1024u / ra.lds_tpb : 0u;
                     launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
                                               c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt);
                 }

@@ -26,6 +26,15 @@ struct Stack {
     __device__ __forceinline__ void push(int v) { base[n * stride] = v; ++n; }
     __device__ __forceinline__ int pop() { --n; return base[n * stride]; }
 };
+// The same LDS stack addressed by a moving pointer (no per-access depth x stride multiply).
+struct PStack {
+    int* base;
+    int* top;    // next free slot
+    int stride;
+    __device__ __forceinline__ void push(int v) { *top = v; top += stride; }
+    __device__ __forceinline__ int pop() { top -= stride; return *top; }
+    __device__ __forceinline__ bool empty() const { return top == base; }
+};
 
 // Where a traversal finds its stack and the BVH arrays.  LDS = true: every object's nodes and
 // triangles were copied once per workgroup into LDS (scene blob, capi.cpp upload_scene) and the
@@ -48,9 +57,9 @@ struct TraceCtx {
         if constexpr (LDS) return reinterpret_cast<const BvhWide*>(scene + o.lds_wide);
         else return o.wide;
     }
-    __device__ __forceinline__ const Tri* tris(const ObjectGpu& o) const {
-        if constexpr (LDS) return reinterpret_cast<const Tri*>(scene + o.lds_tris);
-        else return o.tris;
+    __device__ __forceinline__ const TriT* tris(const ObjectGpu& o) const {
+        if constexpr (LDS) return reinterpret_cast<const TriT*>(scene + o.lds_trit);
+        else return o.trit;
     }
 };
 
@@ -107,10 +116,23 @@ __device__ __forceinline__ void flush_counts(unsigned long long* dst, const uint
 // formed first and u, v only when t can win.  The accept set is unchanged: the reference replaces
 // a rejected t by FLT_MAX, which never passes `t < mint` (mint <= MAX_DEPTH), and a NaN t fails
 // both forms; u, v are evaluated with the reference's expressions and comparisons.
-__device__ __forceinline__ bool tri_hit(const Tri& tr, f3 ro, f3 rd, float mint, float& t_out) {
-    const f3 v1v0 = tr.b - tr.a, v2v0 = tr.c - tr.a, rov0 = ro - tr.a;
-    const f3 n = cross(v1v0, v2v0);
-    const float d = 1.0f / dot(rd, n);
+// 1.0f / x correctly rounded: v_rcp_f32 plus one FMA correction equals IEEE 1.0f / x for every x with
+// 2^-126 <= |x| < 2^126 (tools/rcp_check.hip: all 2^32 inputs on gfx950); the rest (zero,
+// denormals, results that would be denormal, inf, NaN) take the IEEE division.
+__device__ __forceinline__ float rcp_exact(float x) {
+    const float ax = fabsf(x);
+    if (ax >= 0x1p-126f && ax < 0x1p126f) {
+        const float y = __builtin_amdgcn_rcpf(x);
+        return fmaf(fmaf(-x, y, 1.0f), y, y);
+    }
+    return 1.0f / x;
+}
+__device__ __forceinline__ bool tri_hit(const TriT* tp, f3 ro, f3 rd, float mint, float& t_out) {
+    const float4* p4 = reinterpret_cast<const float4*>(tp);
+    const float4 w0 = p4[0], w1 = p4[1], w2 = p4[2];
+    const f3 v1v0 = mk(w0.w, w1.x, w1.y), v2v0 = mk(w1.z, w1.w, w2.x), n = mk(w2.y, w2.z, w2.w);
+    const f3 rov0 = ro - mk(w0.x, w0.y, w0.z);
+    const float d = rcp_exact(dot(rd, n));
     const float t = d * -dot(n, rov0);
     if (!(t >= 0.0f && t < mint)) return false;
     const f3 q = cross(rov0, rd);
@@ -125,7 +147,7 @@ __device__ __forceinline__ bool tri_hit(const Tri& tr, f3 ro, f3 rd, float mint,
 // The box tests use the exact reciprocal-multiply form (aabb_entry_fast) when the ray and the
 // object allow it, which removes 12 IEEE divisions per interior node without changing a bit.
 template <bool FAST>
-__device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __restrict__ nodes, const Tri* __restrict__ tris, int* stack_lds,
+__device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __restrict__ nodes, const TriT* __restrict__ tris, int* stack_lds,
                                           int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
     Stack st{stack_lds, stride, 0};
     st.push(0);
@@ -139,7 +161,7 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
             if (cnt) cnt[2] += (uint32_t)(end + node.left + 1);
             for (int i = -node.left - 1; i < end; ++i) {
                 float t;
-                if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
+                if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
             }
         } else {
             const int c0 = node.left, c1 = node.left + 1;
@@ -162,7 +184,7 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
 // The same traversal over the BvhWide layout: identical box tests, push order, overflow rule and
 // triangle order, so identical results; one record load per inner node, none per leaf.
 template <bool FAST>
-__device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const Tri* __restrict__ tris, int root_ref,
+__device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const TriT* __restrict__ tris, int root_ref,
                                                int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
     Stack st{stack_lds, stride, 0};
     st.push(root_ref);
@@ -176,7 +198,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
             if (cnt) cnt[2] += (uint32_t)(end - b);
             for (int i = b; i < end; ++i) {
                 float t;
-                if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
+                if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
             }
         } else {
             if (cnt) cnt[1] += 2u;
@@ -198,16 +220,16 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
 // the result is identical.  (The reference's FixedStack<32> overflow rule cannot fire: the stack
 // never holds more than max BVH depth + 2 <= 32 entries, capi.cpp upload_scene.)
 template <bool FAST>
-__device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const Tri* __restrict__ tris, int root_ref,
+__device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const TriT* __restrict__ tris, int root_ref,
                                                int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
-    Stack st{stack_lds, stride, 0};
+    PStack st{stack_lds, stack_lds, stride};
     float mint = t_max;
     int shortest = -1;
     int cur = root_ref;          // next stack entry to process
     bool have = true;            // cur is valid
     while (true) {
         if (!have) {
-            if (st.n == 0) break;
+            if (st.empty()) break;
             cur = st.pop();
         }
         have = false;
@@ -217,7 +239,7 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
             if (cnt) cnt[2] += (uint32_t)(end - b);
             for (int i = b; i < end; ++i) {
                 float t;
-                if (tri_hit(tris[i], ro, rd, mint, t)) { mint = t; shortest = i; }
+                if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
             }
             continue;
         }
@@ -301,7 +323,7 @@ __device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restri
             out_obj = c;
             h.t = t;
             h.mat = o.mat_id;
-            const Tri tr = cx.tris(o)[tri];
+            const Tri tr = o.tris[tri];
             const f3 N = tri_normal(tr);
             h.normal = mul(o.rot, N);
             const f3 T = normalize((tr.a + tr.b + tr.c) / 3.0f - tr.a);   // Triangle::get_perturb_matrix (triangle.cuh:164-170)
@@ -630,7 +652,7 @@ template <bool DEFER, bool LDS, bool CNT = false>
 #ifndef RT_WAVES_PER_EU
 #define RT_WAVES_PER_EU 4
 #endif
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void raytrace_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void raytrace_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins,
                                                         const float4* __restrict__ dirs, uint32_t* __restrict__ rng, uint32_t n_rng,
                                                         float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
     uint32_t counts[3] = {0u, 0u, 0u};
@@ -1093,7 +1115,7 @@ __global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, R
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
 // depend on its cap syn + 1 >= full_dist), so the result is bit-identical.
 template <bool LDS, bool CNT = false>
-__global__ __launch_bounds__(512) void shadow_rays_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work) {
+__global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work) {
     uint32_t counts[3] = {0u, 0u, 0u};
     const TraceCtx<LDS, CNT> cx = trace_ctx_setup<LDS, CNT>(a, counts);
     const uint32_t n_rec = *q.count, total = n_rec * q.nps;
@@ -1288,13 +1310,13 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     (void)hipMemsetAsync(a.work, 0, RT_WORK_WORDS * sizeof(uint32_t), s);
     // path kernel: capped at 128 VGPRs (amdgpu_waves_per_eu(4), a few spills) -> 4 waves/SIMD = 2 x 512-thread workgroups;
     // measured faster than 3 waves/SIMD without spills
-    // shadow kernel: ~100 VGPRs -> 5 waves/SIMD; LDS-bound at 2 x 512-thread workgroups
-    const uint32_t tp = 512, ts = 512;
+    // shadow kernel: ~100 VGPRs -> 5 waves/SIMD; LDS-bound at 16 waves per CU (2 x 512 or 1 x 1024 threads, lds_tpb)
     const bool lds = a.scene_in_lds != 0;
+    const uint32_t tp = lds ? a.lds_tpb : 512u, ts = tp, per_cu = 1024u / tp;   // 16 waves per CU either way
     const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
     const uint32_t n_tiles = (((uint32_t)a.W + a.tile - 1) / a.tile) * (((uint32_t)(a.row1 - a.row0) + a.tile - 1) / a.tile);
-    const uint32_t bp = std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * 2);
-    const uint32_t sb = shadow_blocks ? shadow_blocks : a.persistent_blocks * 2;
+    const uint32_t bp = std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * per_cu);
+    const uint32_t sb = shadow_blocks ? shadow_blocks : a.persistent_blocks * per_cu;
     if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in
         allow_lds(raytrace_kernel<true, true, true>, lp);
         allow_lds(shadow_rays_kernel<true, true>, ls);
@@ -1328,8 +1350,8 @@ void launch_raytrace_spec(const RaytraceArgs& a, const RtQueue& q, const float4*
     const uint32_t tiles_x = ((uint32_t)a.W + 7u) / 8u, n_tiles = tiles_x * (((uint32_t)(a.row1 - a.row0) + 7u) / 8u);
     if (a.tile_cost) (void)hipMemsetAsync(a.tile_cost, 0, (size_t)n_tiles * 4, s);   // atomicMax over a tile's row pieces
     const uint32_t n_units = n_tiles * (uint32_t)a.spec_group;   // 64 / (64 / SG) pieces per tile
-    const uint32_t tp = 512, ts = 512;
     const bool lds = a.scene_in_lds != 0;
+    const uint32_t tp = 512, ts = lds ? a.lds_tpb : 512u;
     const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
     // one 512-thread workgroup per CU (2 waves/SIMD at ~230 VGPRs): a larger grid would spill onto the
     // CUs left to the NeRF stream
@@ -1338,7 +1360,7 @@ void launch_raytrace_spec(const RaytraceArgs& a, const RtQueue& q, const float4*
         allow_lds(raytrace_spec_kernel<true>, lp);
         allow_lds(shadow_rays_kernel<true>, ls);
         hipLaunchKernelGGL(raytrace_spec_kernel<true>, dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd, hint);
-        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 1024u / ts), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     } else {
         allow_lds(raytrace_spec_kernel<false>, lp);
         allow_lds(shadow_rays_kernel<false>, ls);
@@ -1358,8 +1380,8 @@ void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st,
     (void)hipMemsetAsync(counters, 0, n_counters * sizeof(uint32_t), s);
     RtQueue qq = q;
     qq.count = counters;
-    const uint32_t tp = 512, ts = 512;
     const bool lds = a.scene_in_lds != 0;
+    const uint32_t tp = 512, ts = lds ? a.lds_tpb : 512u;
     const size_t lp = trace_lds_bytes(a, lds, tp);
     const uint32_t bp = std::min((n + tp - 1) / tp, a.persistent_blocks * 2);
     if (lds) { allow_lds(rt_primary_kernel<true>, lp); allow_lds(rt_bounce_kernel<true>, lp); allow_lds(shadow_rays_kernel<true>, trace_lds_bytes(a, lds, ts)); }
@@ -1383,7 +1405,7 @@ void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st,
         }
     }
     (void)hipMemsetAsync(a.work + SHADOW_CTR0, 0, (RT_WORK_WORDS - SHADOW_CTR0) * sizeof(uint32_t), s);
-    if (lds) hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + SHADOW_CTR0);
+    if (lds) hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 1024u / ts), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + SHADOW_CTR0);
     else hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + SHADOW_CTR0);
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, qq, acc, st.next_pos, o, d, accd);
 }

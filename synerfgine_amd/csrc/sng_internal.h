@@ -206,9 +206,10 @@ struct RaytraceArgs {
     int show_nerf_shadow;
     float syn_shadow_factor;
     // traversal resources (capi.cpp upload_scene / render_frame)
-    const float4* scene_blob;   // all objects' BVH nodes + triangles, 16-B aligned (ObjectGpu::lds_nodes/lds_tris)
+    const float4* scene_blob;   // all objects' BVH nodes + triangles, 16-B aligned (ObjectGpu::lds_nodes or lds_wide, lds_trit)
     uint32_t scene_f4;          // blob size in float4
     int scene_in_lds;           // copy the blob into LDS per workgroup
+    uint32_t lds_tpb;           // threads per traversal workgroup (512, or 1024 when only one blob copy per CU fits)
     uint32_t stack_depth;       // traversal stack entries per thread (max BVH depth + 2, <= 32)
     uint32_t persistent_blocks; // workgroups per launch unit (number of CUs)
     uint32_t* work;             // RT_WORK_WORDS device work counters (pixel tiles, shadow-ray chunks)

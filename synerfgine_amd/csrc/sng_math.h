@@ -459,16 +459,26 @@ struct Tri { f3 a, b, c; };                                 // Triangle (36 B)
 // ref >= 0: inner record index; ref < 0: leaf, ~ref = first_triangle | triangle_count << 24.
 struct alignas(16) BvhWide { float s0[6], s1[6]; int ref0, ref1, pad0, pad1; };
 constexpr uint32_t WIDE_MAX_BEGIN = 1u << 24, WIDE_MAX_COUNT = 127u;
+// Traversal copy of a triangle (capi.cpp upload_scene): a, e1 = b - a, e2 = c - a and n = cross(e1, e2),
+// the values Triangle::ray_intersect (triangle.cuh:45-59) forms first, evaluated once on the host with
+// the same float operations, so the test reads them instead of recomputing them per ray.  48 B, three
+// 16-B loads: v = {a.x a.y a.z e1.x | e1.y e1.z e2.x e2.y | e2.z n.x n.y n.z}.
+struct alignas(16) TriT { float v[12]; };
+SNG_HD TriT make_trit(const Tri& t) {
+    const f3 e1 = t.b - t.a, e2 = t.c - t.a, n = cross(e1, e2);
+    return TriT{{t.a.x, t.a.y, t.a.z, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z, n.x, n.y, n.z}};
+}
 struct ObjectGpu {                                           // ObjectTransform + hoisted inverse
     const BvhNode* nodes;
-    const Tri* tris;
+    const Tri* tris;                // the mesh's triangles (hit normals and perturb frames)
+    const TriT* trit;               // their traversal copies
     m3 rot;
     f3 pos;
     float scale;
     int mat_id;
     m3 world_to_obj;   // (I/scale) * inverse(rot), triangle_bvh.cu:313-319
     int fast_slab;     // every BVH box coordinate < 2^40 in magnitude: aabb_entry_fast is exact
-    uint32_t lds_nodes, lds_tris;   // byte offsets of this object's arrays in the scene blob
+    uint32_t lds_nodes, lds_trit;   // byte offsets of this object's arrays in the scene blob
     const BvhWide* wide;            // traversal layout (nullptr: walk the TriangleBvhNode array)
     uint32_t lds_wide;              // its byte offset in the scene blob
     int root_ref;                   // stack entry of the root
