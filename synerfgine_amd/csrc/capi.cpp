@@ -315,6 +315,7 @@ bool wide_bvh(const std::vector<BvhNode>& nodes, std::vector<BvhWide>& wide, int
         if (n.left >= 0) return id[i];
         const int b = -n.left - 1, e = -n.right - 1;
         if (b < 0 || e < b || (uint32_t)b >= WIDE_MAX_BEGIN || (uint32_t)(e - b) > WIDE_MAX_COUNT) { ok = false; return 0; }
+        if (((uint32_t)b | ((uint32_t)(e - b) << 24)) == 0x7FFFFFFFu) { ok = false; return 0; }   // would collide with WIDE_DONE
         return (int)~((uint32_t)b | ((uint32_t)(e - b) << 24));
     };
     wide.assign(n_inner, BvhWide{});

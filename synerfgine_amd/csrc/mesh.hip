@@ -26,10 +26,12 @@ struct Stack {
     __device__ __forceinline__ void push(int v) { base[n * stride] = v; ++n; }
     __device__ __forceinline__ int pop() { --n; return base[n * stride]; }
 };
-// The same LDS stack addressed by a moving pointer (no per-access depth x stride multiply).
+// The same LDS stack addressed by a moving LDS-typed pointer (no per-access depth x stride multiply,
+// and always ds_read / ds_write, never a flat access).
+typedef __attribute__((address_space(3))) int lds_int;
 struct PStack {
-    int* base;
-    int* top;    // next free slot
+    lds_int* base;
+    lds_int* top;    // next free slot
     int stride;
     __device__ __forceinline__ void push(int v) { *top = v; top += stride; }
     __device__ __forceinline__ int pop() { top -= stride; return *top; }
@@ -222,43 +224,40 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const TriT* __restrict__ tris, int root_ref,
                                                int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
-    PStack st{stack_lds, stack_lds, stride};
+    PStack st{(lds_int*)stack_lds, (lds_int*)stack_lds, stride};
     float mint = t_max;
     int shortest = -1;
     int cur = root_ref;          // next stack entry to process
-    bool have = true;            // cur is valid
     while (true) {
-        if (!have) {
-            if (st.empty()) break;
-            cur = st.pop();
-        }
-        have = false;
-        if (cur < 0) {
-            const uint32_t e = ~(uint32_t)cur;
-            const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
-            if (cnt) cnt[2] += (uint32_t)(end - b);
-            for (int i = b; i < end; ++i) {
-                float t;
-                if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
+        // inner records until this lane holds a leaf or has nothing left (WIDE_DONE)
+        while (cur >= 0) {
+            if (cnt) cnt[1] += 2u;
+            float d0, d1;
+            int r0, r1;
+            wide_visit<FAST>(wide + cur, ro, rd, y, d0, d1, r0, r1);
+            int i0 = r0, i1 = r1;
+            if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = r1; i1 = r0; }
+            // reference: push(far) if d0 < mint, push(near) if d1 < mint, then pop
+            const bool far_in = d0 < mint, near_in = d1 < mint;
+            if (near_in) {
+                if (far_in) st.push(i0);
+                cur = i1;
+            } else if (far_in) {
+                cur = i0;
+            } else {
+                cur = st.empty() ? WIDE_DONE : st.pop();
             }
-            continue;
         }
-        if (cnt) cnt[1] += 2u;
-        float d0, d1;
-        int r0, r1;
-        wide_visit<FAST>(wide + cur, ro, rd, y, d0, d1, r0, r1);
-        int i0 = r0, i1 = r1;
-        if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = r1; i1 = r0; }
-        // reference: push(far) if d0 < mint, push(near) if d1 < mint, then pop
-        const bool far_in = d0 < mint, near_in = d1 < mint;
-        if (near_in) {
-            if (far_in) st.push(i0);
-            cur = i1;
-            have = true;
-        } else if (far_in) {
-            cur = i0;
-            have = true;
+        if (cur == WIDE_DONE) break;
+        const uint32_t e = ~(uint32_t)cur;
+        const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
+        if (cnt) cnt[2] += (uint32_t)(end - b);
+        for (int i = b; i < end; ++i) {
+            float t;
+            if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
         }
+        if (st.empty()) break;
+        cur = st.pop();
     }
     tri_out = shortest;
     return mint;

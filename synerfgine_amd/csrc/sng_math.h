@@ -459,6 +459,7 @@ struct Tri { f3 a, b, c; };                                 // Triangle (36 B)
 // ref >= 0: inner record index; ref < 0: leaf, ~ref = first_triangle | triangle_count << 24.
 struct alignas(16) BvhWide { float s0[6], s1[6]; int ref0, ref1, pad0, pad1; };
 constexpr uint32_t WIDE_MAX_BEGIN = 1u << 24, WIDE_MAX_COUNT = 127u;
+constexpr int WIDE_DONE = (int)0x80000000;   // traversal sentinel; wide_bvh never encodes a leaf as ~0x7FFFFFFF
 // Traversal copy of a triangle (capi.cpp upload_scene): a, e1 = b - a, e2 = c - a and n = cross(e1, e2),
 // the values Triangle::ray_intersect (triangle.cuh:45-59) forms first, evaluated once on the host with
 // the same float operations, so the test reads them instead of recomputing them per ray.  48 B, three
