@@ -393,7 +393,7 @@ const std::map<std::string, double>& default_params() {
         {"nerf_gen_blocks", -1},                 // generate grid (256-thread units): 0 = min(rays, 8 per CU); -1 = all rays in one trip
         {"nerf_ray_tile", 0},                   // > 0: NeRF rays enter the wavefront in tiles of this many pixels squared
         {"rt_shadow_all_cus", 1},               // shadow-ray kernel on every CU: the NeRF tail has mostly finished by then (C3 +2 %; 0: the path kernel grid)
-        {"rt_count", 0},                        // count BVH queries / box / triangle tests of the deferred raytracer (sng_rt_counters)
+        {"rt_count", 0},                        // count BVH queries / box / triangle tests of the deferred raytracer (sng_rt_counters); 2: wave iterations
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
         {"nerf_onestep_horizon", 2048},         // iterations one speculative segment of the regime spans
     };
@@ -473,6 +473,7 @@ struct sng_ctx {
     bool os_ran = false;                   // the last trace ran a one-step regime (ev_os0 .. ev_os1)
     uint32_t os_k = 0, os_J = 0;           // ... from iteration os_k for os_J iterations (all segments)
     uint64_t rt_tile_key = 0;             // band geometry the costs belong to
+
     DevBuf rng_nerf, rng_mesh;
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
     DevBuf d_seq;
@@ -1366,6 +1367,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 c->rt_counts.ensure(8 * sizeof(unsigned long long));
                 HIPCHK(hipMemsetAsync(c->rt_counts.p, 0, 8 * sizeof(unsigned long long), c->s_rt));
                 ra.counts = c->rt_counts.as<unsigned long long>();
+                ra.count_waves = c->p("rt_count") == 2.0 ? 1 : 0;
             }
             // sample-parallel path kernel: 2..64 samples, <= 2 bounces, its own 8x8 tile pieces, not with the
             // staged or deferred-shading variants

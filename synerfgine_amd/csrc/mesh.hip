@@ -51,6 +51,7 @@ struct TraceCtx {
     const char* scene;     // LDS scene blob (LDS = true)
     int flat;              // near child in a register (bvh_walk_near)
     uint32_t* cnt = nullptr;
+    int cnt_waves = 0;     // rt_count = 2: cnt[1], cnt[2] count wave iterations of the record / triangle loops instead
     __device__ __forceinline__ const BvhNode* nodes(const ObjectGpu& o) const {
         if constexpr (LDS) return reinterpret_cast<const BvhNode*>(scene + o.lds_nodes);
         else return o.nodes;
@@ -223,7 +224,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
 // never holds more than max BVH depth + 2 <= 32 entries, capi.cpp upload_scene.)
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const TriT* __restrict__ tris, int root_ref,
-                                               int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
+                                               int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr, bool cw = false) {
     PStack st{(lds_int*)stack_lds, (lds_int*)stack_lds, stride};
     float mint = t_max;
     int shortest = -1;
@@ -231,7 +232,7 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
     while (true) {
         // inner records until this lane holds a leaf or has nothing left (WIDE_DONE)
         while (cur >= 0) {
-            if (cnt) cnt[1] += 2u;
+            if (cnt) cnt[1] += cw ? (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id()) : 2u;
             float d0, d1;
             int r0, r1;
             wide_visit<FAST>(wide + cur, ro, rd, y, d0, d1, r0, r1);
@@ -251,8 +252,9 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
         if (cur == WIDE_DONE) break;
         const uint32_t e = ~(uint32_t)cur;
         const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
-        if (cnt) cnt[2] += (uint32_t)(end - b);
+        if (cnt && !cw) cnt[2] += (uint32_t)(end - b);
         for (int i = b; i < end; ++i) {
+            if (cnt && cw) cnt[2] += (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id());
             float t;
             if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
         }
@@ -271,8 +273,8 @@ __device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu&
     const f3 ord = mul(o.world_to_obj, rd);
     const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
     if (o.wide && cx.flat) {
-        if (fast) return bvh_walk_near<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
-        return bvh_walk_near<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+        if (fast) return bvh_walk_near<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
+        return bvh_walk_near<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
     }
     if (o.wide) {
         if (fast) return bvh_walk_wide<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
@@ -494,7 +496,7 @@ __device__ __forceinline__ TraceCtx<LDS, CNT> trace_ctx_setup(const RaytraceArgs
         __syncthreads();
     }
     int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
-    return TraceCtx<LDS, CNT>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt};
+    return TraceCtx<LDS, CNT>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt, a.count_waves};
 }
 
 template <bool DEFER, bool LDS, bool CNT = false>

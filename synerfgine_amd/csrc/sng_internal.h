@@ -219,6 +219,7 @@ struct RaytraceArgs {
     int tile;                   // path-kernel tile edge in pixels (8: 64 lanes, 4: 16 lanes per wave)
     int spec_group;             // > 0: sample-parallel path kernel (raytrace_spec_kernel), lanes per pixel
     unsigned long long* counts; // counting frames (rt_count): path kernel {queries, box, tri}, shadow kernel {queries, box, tri}
+    int count_waves;            // rt_count = 2: box / tri entries count wave iterations of those loops (SIMD efficiency)
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
@@ -277,6 +278,7 @@ struct RtStage {
 void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st, uint32_t* counters, const float4* o, const float4* d, uint32_t* rng,
                             uint32_t n_rng, float4* acc, float* accd, hipStream_t s);
 void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, hipStream_t s);
+
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
                      hipStream_t s);
 // display.hip
