@@ -374,6 +374,7 @@ const std::map<std::string, double>& default_params() {
         {"rt_tile", 8},                         // path-kernel tile edge: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
+        {"rt_plist", 1},                        // per-pixel hit-record lists for the colour replay (rt_accumulate_kernel)
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
@@ -461,6 +462,7 @@ struct sng_ctx {
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
     DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
+    DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf rt_hint;                        // sample-parallel path kernel: per-pixel hit-depth sums of the previous frame (u8)
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
@@ -880,7 +882,7 @@ void load_scene(sng_ctx* c, const std::string& path) {
     }
     for (auto& o : objs)
         if (o.mat < 0 || (size_t)o.mat >= mats.size()) throw SngError(SNG_ERR_INVALID, "object material index out of range");
-    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_wide.release(); }
+    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_trit.release(); o.d_wide.release(); }
     c->objs = std::move(objs);
     c->mats = mats;
     c->lights = lights;
@@ -1438,6 +1440,19 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                     // shadow-ray grid: the CUs the path kernel leaves to the NeRF tail too when rt_shadow_all_cus
                     // (by then the tail has mostly finished)
                     const uint32_t sb = c->p("rt_shadow_all_cus") != 0.0 ? (uint32_t)c->n_cus * 1024u / ra.lds_tpb : 0u;
+                    const uint64_t max_hits = (uint64_t)ra.samples * ra.bounces;
+                    const uint64_t stage_b = 16ull * (64ull * q.rec_stride + (64ull * q.nps + 3) / 4);   // rt_record_colour_kernel's LDS per wave
+                    if (c->p("rt_plist") != 0.0 && max_hits <= 255 && stage_b <= 64ull * 1024) {
+                        // per-pixel record lists: the colour replay reads each pixel's records directly instead of
+                        // walking their chain (one dependent load per record)
+                        c->rt_plist.ensure(n_px * max_hits * 4);
+                        c->rt_pcount.ensure(n_px);
+                        c->rt_rval.ensure(cap * 16);
+                        q.plist = c->rt_plist.as<int>();
+                        q.pcount = c->rt_pcount.as<uint8_t>();
+                        q.rval = c->rt_rval.as<float4>();
+                        q.max_hits = (uint32_t)max_hits;
+                    }
                     launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
                                               c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt);
                 }
@@ -1802,10 +1817,10 @@ void ctx_destroy(sng_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     comm_destroy(c->sched_comm);
-    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_wide.release(); }
+    for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_trit.release(); o.d_wide.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1}) (void)hipEventDestroy(e);
@@ -2267,7 +2282,7 @@ int sng_hashgrid_encode(sng_ctx* c, const float* coords, uint32_t stride, uint32
 int sng_load_virtual_scene(sng_ctx* c, const char* path) { return guarded([&] { load_scene(c, path); }); }
 int sng_clear_virtual_scene(sng_ctx* c) {
     return guarded([&] {
-        for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_wide.release(); }
+        for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_trit.release(); o.d_wide.release(); }
         c->objs.clear(); c->lights.clear(); c->mats.clear();
         c->scene_dirty = true;
     });

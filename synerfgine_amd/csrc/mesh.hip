@@ -499,6 +499,70 @@ __device__ __forceinline__ TraceCtx<LDS, CNT> trace_ctx_setup(const RaytraceArgs
     return TraceCtx<LDS, CNT>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt, a.count_waves};
 }
 
+// shade_object + Material::scatter of one hit, deferred form (raytracer.cu:6-57, material.cuh:112-123):
+// the hit record (linked after prev_rec, or as the pixel's head), its light colours and point-light
+// shadow rays go to q; rp / rd / pdf / att become the scattered ray's.
+__device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& q, int lane, size_t i, uint32_t t, uint32_t spp, const Hit& h,
+                                          int& prev_rec, uint32_t& n_hits, Xorwow& r, f3& rp, f3& rd, float& pdf, float& att) {
+    const MaterialGpu m = a.mats[h.mat];
+    const uint32_t k = wave_alloc(q.count, lane);
+    if (q.plist) q.plist[(size_t)t * q.max_hits + n_hits] = (int)k;
+    ++n_hits;
+    float4* rk = q.rec + (size_t)k * q.rec_stride;
+    rk[0] = make_float4(__int_as_float(-1), __uint_as_float(spp), __int_as_float(h.mat), 0.0f);
+    rk[1] = make_float4(pdf, att, 0.0f, 0.0f);
+    float* lc_out = reinterpret_cast<float*>(rk + 2);
+    if (prev_rec < 0) q.head[i] = (int)k;
+    else reinterpret_cast<int*>(q.rec + (size_t)prev_rec * q.rec_stride)[0] = (int)k;
+    prev_rec = (int)k;
+    uint32_t jl = 0, jp = 0;
+    if (q.shade_in) {
+        // shading off the chain: keep what rt_shade_records_kernel needs and skip the light
+        // samples' draws (3 per light and shadow iteration) -- same RNG position afterwards
+        float4* si = q.rec + (size_t)k * q.rec_stride + q.shade_in;
+        si[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, 0.0f);
+        si[1] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.0f);
+        si[2] = make_float4(rd.x, rd.y, rd.z, 0.0f);
+        si[3] = make_float4(__uint_as_float(r.v0), __uint_as_float(r.v1), __uint_as_float(r.v2), __uint_as_float(r.v3));
+        si[4] = make_float4(__uint_as_float(r.v4), __uint_as_float(r.d), 0.0f, 0.0f);
+        const uint32_t n_draws = 3u * (uint32_t)a.n_lights * a.shadow_iters;
+        for (uint32_t j = 0; j < n_draws; ++j) (void)xorwow_next(r);
+    } else {
+        for (int l = 0; l < a.n_lights; ++l) {
+            const LightGpu L = a.lights[l];
+            for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
+                const f3 lpos = light_sample(L, r);
+#ifdef RT_TIMING_NO_SHADE   // timing-only builds (not exact): the cost of shade_object's per-sample lighting
+                const float full_dist = 1.0f;
+                const f3 Lv = lpos, lc = lpos;
+#else
+                f3 Lv = lpos - h.pos;
+                const float full_dist = length(Lv);
+                Lv = normalize(Lv);
+                const f3 R = reflect(Lv, h.normal);
+                const f3 V = normalize(-rd);
+                const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+#endif
+                lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
+                if (L.type == 0) {
+                    float4* sr = q.shadow_ray(k, jp);
+                    sr[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, full_dist);
+                    sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
+                    ++jp;
+                }
+            }
+        }
+    }
+    const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
+    const float lo = curand_uniform(r) * spec;
+    const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+    const f3 ndir = cone_random_frame(h.normal, h.perturb, lo, la);
+    rp = h.pos;
+    rd = ndir;
+    pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
+    att = 1.0f * m.rg;
+}
+
 template <bool DEFER, bool LDS, bool CNT = false>
 __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t t,
                                                const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
@@ -510,10 +574,8 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
     const f3 src_p = mk(o4.x, o4.y, o4.z), src_d = mk(d4.x, d4.y, d4.z);
     f3 shade = splat(0.0f), next_pos = splat(0.0f);
     int prev_rec = -1;
+    uint32_t n_hits = 0;
     if (DEFER) q.head[i] = -1;
-#ifdef RT_PROFILE
-    uint64_t pc_trav0 = 0, pc_trav1 = 0, pc_shade = 0, pc_alloc = 0, pc_scatter = 0, pc_start = clock64(), pc_t = 0;
-#endif
     for (uint32_t spp = 0; spp < a.samples; ++spp) {
         const float longi = curand_uniform(r) * a.lens;
         const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
@@ -522,53 +584,19 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
         f3 shade_s = splat(0.0f);
         for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
             Hit h;
-#ifdef RT_PROFILE
-            pc_t = clock64();
-#endif
             const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h);
-#ifdef RT_PROFILE
-            if (bounce) pc_trav1 += clock64() - pc_t; else pc_trav0 += clock64() - pc_t;
-            pc_t = clock64();
-#endif
             if (!bounce) next_pos = next_pos + h.pos;
             if (hit_obj < 0) break;
+            if (DEFER) {
+                defer_hit(a, q, lane, i, t, spp, h, prev_rec, n_hits, r, rp, rd, pdf, att);
+                continue;
+            }
             // shade_object (raytracer.cu:6-57)
             const MaterialGpu m = a.mats[h.mat];
             f3 color = splat(0.0f);
-            uint32_t k = 0;
-            float* lc_out = nullptr;
-            if (DEFER) {
-#ifdef RT_PROFILE
-                const uint64_t pa = clock64();
-#endif
-                k = wave_alloc(q.count, lane);
-#ifdef RT_PROFILE
-                pc_alloc += clock64() - pa;
-#endif
-                float4* rk = q.rec + (size_t)k * q.rec_stride;
-                rk[0] = make_float4(__int_as_float(-1), __uint_as_float(spp), __int_as_float(h.mat), 0.0f);
-                rk[1] = make_float4(pdf, att, 0.0f, 0.0f);
-                lc_out = reinterpret_cast<float*>(rk + 2);
-                if (prev_rec < 0) q.head[i] = (int)k;
-                else reinterpret_cast<int*>(q.rec + (size_t)prev_rec * q.rec_stride)[0] = (int)k;
-                prev_rec = (int)k;
-            }
-            uint32_t jl = 0, jp = 0;
-            if (DEFER && q.shade_in) {
-                // shading off the chain: keep what rt_shade_records_kernel needs and skip the light
-                // samples' draws (3 per light and shadow iteration) -- same RNG position afterwards
-                float4* si = q.rec + (size_t)k * q.rec_stride + q.shade_in;
-                si[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, 0.0f);
-                si[1] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.0f);
-                si[2] = make_float4(rd.x, rd.y, rd.z, 0.0f);
-                si[3] = make_float4(__uint_as_float(r.v0), __uint_as_float(r.v1), __uint_as_float(r.v2), __uint_as_float(r.v3));
-                si[4] = make_float4(__uint_as_float(r.v4), __uint_as_float(r.d), 0.0f, 0.0f);
-                const uint32_t n_draws = 3u * (uint32_t)a.n_lights * a.shadow_iters;
-                for (uint32_t j = 0; j < n_draws; ++j) (void)xorwow_next(r);
-            } else
             for (int l = 0; l < a.n_lights; ++l) {
                 const LightGpu L = a.lights[l];
-                for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
+                for (uint32_t s = 0; s < a.shadow_iters; ++s) {
                     const f3 lpos = light_sample(L, r);
                     f3 Lv = lpos - h.pos;
                     const float full_dist = length(Lv);
@@ -576,16 +604,7 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                     const f3 R = reflect(Lv, h.normal);
                     const f3 V = normalize(-rd);
                     const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
-                    if (DEFER) {
-                        lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
-                        if (L.type == 0) {
-                            float4* sr = q.shadow_ray(k, jp);
-                            sr[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, full_dist);
-                            sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
-                            ++jp;
-                        }
-                    } else if (L.type == 0) {
-                        float mask = 1.0f;
+                    if (L.type == 0) {
                         const f3 invL = inv(Lv);
                         int oh = -1;
                         const float syn = a.show_nerf_shadow ? depth_test_world(h.pos, Lv, a.objs, a.n_objs, cx, oh) : 1.0f;
@@ -593,34 +612,25 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                                                ? depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, h.pos, Lv, invL, 0, a.vol.max_mip)
                                                : 1.0f;
                         const float sh = fminf(fminf(nerf, syn), full_dist);
-                        mask = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
+                        const float mask = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
                         color = color + lc * mask;
                     } else {
                         color = color + lc;
                     }
                 }
             }
-            if (!DEFER) {
-                color = color / (float)a.shadow_iters;
-                color = color + m.ka;
-            }
-#ifdef RT_PROFILE
-            pc_shade += clock64() - pc_t;
-            pc_t = clock64();
-#endif
+            color = color / (float)a.shadow_iters;
+            color = color + m.ka;
             // Material::scatter (material.cuh:112-123)
             const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
             const float lo = curand_uniform(r) * spec;
             const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
             const f3 ndir = cone_random_frame(h.normal, h.perturb, lo, la);
-            if (!DEFER) shade_s = shade_s + color * pdf * att;
+            shade_s = shade_s + color * pdf * att;
             rp = h.pos;
             rd = ndir;
             pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
             att = 1.0f * m.rg;
-#ifdef RT_PROFILE
-            pc_scatter += clock64() - pc_t;
-#endif
         }
         if (!DEFER) shade = shade + shade_s;
     }
@@ -634,13 +644,8 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
         if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
         acc_rgba[i] = make_float4(shade.x, shade.y, shade.z, cur.w);
     }
+    if (DEFER && q.pcount) q.pcount[t] = (uint8_t)n_hits;
     store_rng(rng, n_rng, i, r);
-#ifdef RT_PROFILE
-    const uint64_t tot = clock64() - pc_start;
-    if (lane == (int)(__ffsll((long long)__ballot(1)) - 1) && tot > 1500000ull)
-        printf("RTPROF pixel %u total %lu trav0 %lu trav1 %lu shade %lu (alloc %lu) scatter %lu\n", (uint32_t)i, (unsigned long)tot,
-               (unsigned long)pc_trav0, (unsigned long)pc_trav1, (unsigned long)pc_shade, (unsigned long)pc_alloc, (unsigned long)pc_scatter);
-#endif
 }
 
 // Persistent workgroups; each wave takes T x T pixel tiles (T = 8, or 4 for thin bands: a tile is a
@@ -1162,6 +1167,50 @@ __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQue
     if constexpr (CNT) flush_counts(a.counts + 3, counts, lane);
 }
 
+// One hit record's term of the colour replay: shade_object's colour (raytracer.cu:6-57) times pdf * att,
+// evaluated exactly as rt_accumulate_kernel's chain walk does; .w = the record's sample index.  A wave
+// stages its 64 consecutive records and their masks in LDS with coalesced 16-B loads, then each lane
+// sums its own record.  Dynamic LDS: waves per block x 64 x (rec_stride float4 + nps floats).
+__global__ __launch_bounds__(256) void rt_record_colour_kernel(RaytraceArgs a, RtQueue q) {
+    extern __shared__ float4 rc_lds[];
+    const uint32_t n = min(*q.count, q.cap);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t rs = q.rec_stride, wave_f4 = 64u * rs + (64u * q.nps + 3u) / 4u;
+    float4* recs = rc_lds + wave * wave_f4;
+    float* masks = reinterpret_cast<float*>(recs + 64u * rs);
+    for (uint32_t k0 = (blockIdx.x * (blockDim.x >> 6) + wave) * 64u; k0 < n; k0 += gridDim.x * blockDim.x) {
+        const uint32_t nk = min(64u, n - k0);
+        const float4* src = q.rec + (size_t)k0 * rs;
+        for (uint32_t e = lane; e < nk * rs; e += 64u) recs[e] = src[e];
+        const float* msrc = q.mask + q.mask_at(k0, 0);
+        for (uint32_t e = lane; e < nk * q.nps; e += 64u) masks[e] = msrc[e];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < nk) {
+            const float4* rk = recs + lane * rs;
+            const float4 h0 = rk[0], h1 = rk[1];
+            const float* lc = reinterpret_cast<const float*>(rk + 2);
+            const float* mk_ = masks + lane * q.nps;
+            f3 color = splat(0.0f);
+            uint32_t jl = 0, jp = 0;
+            for (int l = 0; l < a.n_lights; ++l) {
+                const bool point = a.lights[l].type == 0;
+                for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
+                    const f3 c = mk(lc[3 * jl], lc[3 * jl + 1], lc[3 * jl + 2]);
+                    if (point) color = color + c * mk_[jp++];
+                    else color = color + c;
+                }
+            }
+            color = color / (float)a.shadow_iters;
+            color = color + a.mats[__float_as_int(h0.z)].ka;
+            const f3 v = color * h1.x * h1.y;
+            q.rval[k0 + lane] = make_float4(v.x, v.y, v.z, h0.y);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // Colour replay of the deferred raytracer, in raytrace_kernel's exact float order.
 __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQueue q, float4* __restrict__ acc_rgba, const float4* __restrict__ next_pos,
                                                             const float4* __restrict__ origins, const float4* __restrict__ dirs, float* __restrict__ acc_depth) {
@@ -1169,8 +1218,35 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (t >= n) return;
     const size_t i = (size_t)a.row0 * a.W + t;
-    int k = q.head[i];
     f3 shade = splat(0.0f);
+    if (q.plist) {
+        // list mode: the pixel's records in allocation order, their terms from rt_record_colour_kernel; the
+        // first 16 are loaded up front (independent loads), so the sum waits for memory once, not per record
+        constexpr uint32_t PRE = 16;
+        const uint32_t cnt = q.pcount[t];
+        const int* L = q.plist + (size_t)t * q.max_hits;
+        float4 v[PRE];
+#pragma unroll
+        for (uint32_t h = 0; h < PRE; ++h) v[h] = h < cnt ? q.rval[L[h]] : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0xFFFFFFFFu));
+        uint32_t h = 0;
+        for (uint32_t spp = 0; spp < a.samples; ++spp) {
+            f3 shade_s = splat(0.0f);
+            while (h < cnt) {
+                float4 w;
+                if (h < PRE) {
+#pragma unroll
+                    for (uint32_t u = 0; u < PRE; ++u) if (u == h) w = v[u];
+                } else {
+                    w = q.rval[L[h]];
+                }
+                if (__float_as_uint(w.w) != spp) break;
+                shade_s = shade_s + mk(w.x, w.y, w.z);
+                ++h;
+            }
+            shade = shade + shade_s;
+        }
+    } else {
+    int k = q.head[i];
     for (uint32_t spp = 0; spp < a.samples; ++spp) {
         f3 shade_s = splat(0.0f);
         while (k >= 0) {
@@ -1194,6 +1270,7 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
             k = __float_as_int(h0.x);
         }
         shade = shade + shade_s;
+    }
     }
     shade = shade / (float)a.samples;
     if (next_pos) {   // staged mode: raytrace_pixel's depth from the summed first hits
@@ -1336,6 +1413,12 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
         hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
         if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
         hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+    }
+    if (q.plist) {   // capi.cpp enables the lists only when one wave's staging fits 64 KB
+        const size_t per_wave = 16u * (64u * q.rec_stride + (64u * q.nps + 3u) / 4u);
+        const uint32_t waves = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160u * 1024u) / per_wave));
+        allow_lds(rt_record_colour_kernel, waves * per_wave);
+        hipLaunchKernelGGL(rt_record_colour_kernel, dim3(a.persistent_blocks * 16 / waves), dim3(64 * waves), waves * per_wave, s, a, q);
     }
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
 }

@@ -239,6 +239,13 @@ struct RtQueue {
     uint32_t shade_in;    // > 0: float4 offset of the deferred-shading inputs {pos} {normal} {rd} {rng v0-v3} {rng v4, d}
                           // in each record; raytrace_kernel skips the light samples' draws and
                           // rt_shade_records_kernel computes lc + shadow rays off the path chain
+    // per-pixel record lists (tile path kernel): plist[t * max_hits + h] = the pixel's h-th hit record, pcount[t]
+    // = its hits; rt_record_colour_kernel writes each record's colour term to rval and rt_accumulate_kernel
+    // sums them in list order without walking the record chain.  nullptr: chain walk.
+    int* plist;
+    uint8_t* pcount;
+    float4* rval;         // {colour * pdf * att, spp bits}
+    uint32_t max_hits;    // samples * bounces (<= 255)
     // shadow ray jp of hit record k, record-major ([k][jp]): a wave traces the nps shadow samples of 64 / nps
     // consecutive records.  (Sample-major, [jp][k] -- 64 records towards one light sample per wave --
     // measured 40 % slower: the rays of one hit point share their walk until they part towards the lights.)

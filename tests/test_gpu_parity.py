@@ -291,6 +291,32 @@ def test_sample_parallel_raytracer_equals_path_kernel(config, overrides, rows):
         tb.close()
 
 
+@pytest.mark.parametrize("config,overrides,rows", [("c3", {}, None), ("c3", {}, (37, 90)), ("c3", {"rt_defer_shade": 1}, None),
+                                                    ("c3", {"path_trace_depth": 3, "light_samples": 3}, None), ("c4", {}, (20, 52))])
+def test_record_lists_equal_chain_walk(config, overrides, rows):
+    """The colour replay over per-pixel record lists + per-record colour terms (rt_plist=1) equals the walk of
+    each pixel's record chain (rt_plist=0) bit for bit."""
+    tb, eng, _ = _engine(192, 108, overrides, config=config)
+    try:
+        m0, n0 = eng.rng_states(1).copy(), eng.rng_states(0).copy()
+        out = {}
+        for mode in (0, 1):
+            eng.set_rng_states(0, n0)
+            eng.set_rng_states(1, m0)
+            eng.set_param("rt_plist", mode)
+            frames = []
+            for _ in range(2):
+                r = eng.frame(rows=rows)
+                frames.append((r.download("syn_rgba"), r.download("syn_depth"), r.download("final_rgba")))
+            out[mode] = frames
+        for fa, fb in zip(out[0], out[1]):
+            for a, b in zip(fa, fb):
+                assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert (out[1][0][1] < 100).mean() > 0.02    # objects are in view
+    finally:
+        tb.close()
+
+
 @pytest.mark.parametrize("config,overrides", [("c3", {}), ("c3", {"scene_lds": 0}), ("c3", {"rt_wavefront": 0}), ("c4", {})])
 def test_wide_bvh_layout_equals_node_walk(config, overrides):
     """The BvhWide traversal layout (bvh_wide=1) reproduces the TriangleBvhNode walk bit for bit."""

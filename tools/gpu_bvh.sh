@@ -5,7 +5,7 @@ tag=${1:-bvh}
 mkdir -p gpurun_out/$tag
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread \
-  -k "full_frame or raytracer or wide_bvh or rt_counting or band_rendering or pixel_cost" > gpurun_out/$tag/pytest.log 2>&1 || { tail -30 gpurun_out/$tag/pytest.log; exit 1; }
+  -k "full_frame or raytracer or wide_bvh or rt_counting or band_rendering or record_lists" > gpurun_out/$tag/pytest.log 2>&1 || { tail -30 gpurun_out/$tag/pytest.log; exit 1; }
 tail -2 gpurun_out/$tag/pytest.log
 for rep in 1 2; do
   timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-sweep > gpurun_out/$tag/c3.json 2>/dev/null || exit 1
