@@ -362,7 +362,7 @@ const std::map<std::string, double>& default_params() {
         {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
         {"rt_start_chunk", -1},                 // concurrent mode: raytracer starts after this many 4-iteration NeRF chunks (-1: 1 for
                                                 //   bands of >= 60 % of the rows, else 0 -- thin bands are latency bound)
-        {"rt_reserved_cus", 16},                // concurrent mode: CUs (2 per XCD) the persistent raytracer grids leave to the NeRF stream
+        {"rt_reserved_cus", 32},                // concurrent mode: CUs (4 per XCD) the persistent raytracer grids leave to the NeRF stream
         {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer

@@ -380,9 +380,64 @@ __device__ __forceinline__ f3 light_sample(const LightGpu& l, Xorwow& r) {
     return l.pos + mk(x, y, z) * l.size * 1.0f;
 }
 
+__device__ __forceinline__ void xorwow_skip(Xorwow& r, uint32_t n) {
+#pragma unroll 1
+    for (uint32_t j = 0; j < n; ++j) (void)xorwow_next(r);
+}
+
 // ---------------------------------------------------------------------------
 // shade_with_shadow (testbed_nerf.cu:1702-1786) / shadow_for_px (1614-1700)
 // ---------------------------------------------------------------------------
+// One neighbour's term of shade_with_shadow: shadow_for_px at (pos, nrm) with the pixel's XORWOW
+// state r (3 draws per point light).
+template <bool LDS>
+__device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx<LDS>& cx, f3 pos, f3 nrm, Xorwow& r) {
+    float overall = 1.0f;
+    for (int li = 0; li < a.n_lights; ++li) {
+        const LightGpu L = a.lights[li];
+        if (L.type == 0) {
+            const f3 lpos = light_sample(L, r);
+            const f3 l = normalize(lpos - pos);
+            const float full_d = length(lpos - pos);
+            int hit = -1;
+#ifdef SHADOW_NO_BVH   // timing-only builds (tools/gpu_shadow_c4.sh)
+            const float syn_depth = full_d + (float)(hit + 1);
+#else
+            const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, cx, hit);
+#endif
+            overall = fminf(overall, powf(syn_depth / full_d, a.intensity));
+            const f3 fract_offset = full_d * a.threshold * lpos;
+            const f3 src = pos + fract_offset;
+            const float fd = length(lpos - src);
+            const f3 Ld = normalize(lpos - src);
+#ifdef SHADOW_NO_NERF
+            const float nd = fminf(full_d, fd + Ld.x);
+#else
+            const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip));
+#endif
+            const double mask = (double)(nd * (1.0f - fminf(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)a.threshold));
+            overall = (float)fmin((double)overall, mask);
+        } else {
+            const f3 l = normalize(L.pos - pos);
+            const double v = (double)overall + fmin(0.0, (double)dot(l, nrm)) * (double)L.intensity;
+            overall = (float)fmin(1.0, v);
+        }
+    }
+    return overall;
+}
+__device__ __forceinline__ void shadow_apply(const ShadowArgs& a, float4* __restrict__ rgba, size_t idx, float sum) {
+    sum = powf(sum, a.intensity);
+    float4 c = rgba[idx];
+    c.x = srgb_to_linear(c.x) * sum;
+    c.y = srgb_to_linear(c.y) * sum;
+    c.z = srgb_to_linear(c.z) * sum;
+    rgba[idx] = c;
+}
+__device__ __forceinline__ f3 load_f3(const float* __restrict__ p, size_t i) { return mk(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
+
+// One lane per pixel, the neighbours in loop order.  (A form with a pixel's (2r+1)^2 neighbour terms on
+// separate lanes -- each lane skipping the pixel's XORWOW stream to its neighbour's draws -- was exact but
+// 16 % slower at C4's r = 2: the pass is VALU-bound, not latency-bound.)
 __global__ __launch_bounds__(TPB) void shade_shadow_kernel(ShadowArgs a, float4* __restrict__ rgba, const float* __restrict__ positions,
                                                             const float* __restrict__ normals, uint32_t* __restrict__ rng, uint32_t n_rng) {
     __shared__ int stack_lds[BVH_STACK * TPB];
@@ -400,49 +455,11 @@ __global__ __launch_bounds__(TPB) void shade_shadow_kernel(ShadowArgs a, float4*
             const int fx = x + i, fy = y + j;
             if (fx < 0 || fy < 0 || fx >= a.W || fy >= a.H) continue;
             const size_t tid = (size_t)fy * a.W + fx;
-            const f3 pos = mk(positions[3 * tid], positions[3 * tid + 1], positions[3 * tid + 2]);
-            const f3 nrm = mk(normals[3 * tid], normals[3 * tid + 1], normals[3 * tid + 2]);
-            float overall = 1.0f;
-            for (int li = 0; li < a.n_lights; ++li) {
-                const LightGpu L = a.lights[li];
-                if (L.type == 0) {
-                    const f3 lpos = light_sample(L, r);
-                    const f3 l = normalize(lpos - pos);
-                    const float full_d = length(lpos - pos);
-                    int hit = -1;
-#ifdef SHADOW_NO_BVH   // timing-only builds (tools/gpu_shadow_c4.sh)
-                    const float syn_depth = full_d + (float)(hit + 1);
-#else
-                    const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, cx, hit);
-#endif
-                    overall = fminf(overall, powf(syn_depth / full_d, a.intensity));
-                    const f3 fract_offset = full_d * a.threshold * lpos;
-                    const f3 src = pos + fract_offset;
-                    const float fd = length(lpos - src);
-                    const f3 Ld = normalize(lpos - src);
-#ifdef SHADOW_NO_NERF
-                    const float nd = fminf(full_d, fd + Ld.x);
-#else
-                    const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip));
-#endif
-                    const double mask = (double)(nd * (1.0f - fminf(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)a.threshold));
-                    overall = (float)fmin((double)overall, mask);
-                } else {
-                    const f3 l = normalize(L.pos - pos);
-                    const double v = (double)overall + fmin(0.0, (double)dot(l, nrm)) * (double)L.intensity;
-                    overall = (float)fmin(1.0, v);
-                }
-            }
-            sum += overall;
+            sum += shadow_term(a, cx, load_f3(positions, tid), load_f3(normals, tid), r);
             ++blend;
         }
     sum /= (float)blend;
-    sum = powf(sum, a.intensity);
-    float4 c = rgba[idx];
-    c.x = srgb_to_linear(c.x) * sum;
-    c.y = srgb_to_linear(c.y) * sum;
-    c.z = srgb_to_linear(c.z) * sum;
-    rgba[idx] = c;
+    shadow_apply(a, rgba, idx, sum);
     store_rng(rng, n_rng, idx, r);
 }
 
@@ -712,10 +729,6 @@ struct SpecBounce {
     float pdf, att;
 };
 
-__device__ __forceinline__ void xorwow_skip(Xorwow& r, uint32_t n) {
-#pragma unroll 1
-    for (uint32_t j = 0; j < n; ++j) (void)xorwow_next(r);
-}
 
 // One sample of raytrace_pixel's loop from XORWOW offset `off`: returns hit depth, fills the hit
 // bounces, the first-bounce position and the state after the sample's last draw.

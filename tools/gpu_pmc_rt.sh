@@ -1,11 +1,11 @@
 #!/bin/bash
 # Issue/stall breakdown of the traversal kernels (C3, serialized streams): one SQ pass, kernel trace only.
-# usage: tools/gpu_pmc_rt.sh [tag]
+# usage: tools/gpu_pmc_rt.sh [tag] [config]
 tag=${1:-pmc_rt}
 export TMPDIR=/tmp
 d=gpurun_out/$tag
 mkdir -p $d
-args="--steps 3 --warmup 1 --no-cpu-baseline --no-sweep --serial-streams"
+args="--config ${2:-c3} --steps 3 --warmup 1 --no-cpu-baseline --no-sweep --serial-streams"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS \
   -d $d/sq -o run --output-format csv -- python3 bench.py $args > $d/sq.log 2>&1 || { tail -20 $d/sq.log; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE \
@@ -19,7 +19,7 @@ n = defaultdict(int)
 for f in glob.glob(d + "/sq*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if not any(s in k for s in ("shadow_rays_kernel", "raytrace_kernel", "nerf_fused_kernel", "rt_accumulate")):
+        if not any(s in k for s in ("shadow_rays_kernel", "raytrace_kernel", "nerf_fused_kernel", "rt_accumulate", "shade_shadow", "onestep_kernel", "generate_kernel")):
             continue
         acc[k[:60]][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, c in acc.items():
