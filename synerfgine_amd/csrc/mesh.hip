@@ -335,14 +335,23 @@ __device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restri
     return out_obj;
 }
 
-// sng::depth_test_nerf (common.cu:69-83)
-__device__ float depth_test_nerf(float full_d, uint32_t n_steps, const Volume& vol, f3 src, f3 L, f3 invL, uint32_t min_mip, uint32_t max_mip) {
+// sng::depth_test_nerf (common.cu:69-83), with two exact early exits.  The march's distance s never
+// decreases, and once s >= full_d at the start of a trip the result is full_d (the next sample or
+// exit trip clamps to it, DDA trips in between change nothing), so it returns full_d there.  And a
+// caller that only uses min(result, cap) with cap <= full_d lets the walk stop once s >= cap: both
+// results are then >= cap.
+__device__ float depth_test_nerf(float full_d, uint32_t n_steps, const Volume& vol, f3 src, f3 L, f3 invL, uint32_t min_mip, uint32_t max_mip,
+                                 float cap) {
     float s = 0.0f;
     if (vol.linear && vol.bitfield && min_mip == 0 && max_mip == 0 && vol.cone <= 1e-5f) {
         // the same march flattened into one loop (one DDA step or one sample per trip), see generate_kernel
         const f3 hs = half_sign(L);
         uint32_t j = 0;
         while (j < n_steps) {
+#ifndef SHADOW_MARCH_NO_EARLY_EXIT   // A/B builds (tools/frame_dump.py): the early exits must not change a bit
+            if (s >= cap) return s;
+            if (s >= full_d) return full_d;
+#endif
             const f3 pos = src + L * s;
             const bool out = s >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos));
             if (out || occupied_linear(pos, vol.occ_linear)) {
@@ -359,6 +368,10 @@ __device__ float depth_test_nerf(float full_d, uint32_t n_steps, const Volume& v
     // general path, flattened the same way (occ_step: one DDA step or one sample per trip)
     uint32_t j = 0;
     while (j < n_steps) {
+#ifndef SHADOW_MARCH_NO_EARLY_EXIT   // A/B builds (tools/frame_dump.py): the early exits must not change a bit
+        if (s >= cap) return s;
+        if (s >= full_d) return full_d;
+#endif
         if (occ_step(s, vol.ss, src, L, invL, min_mip, max_mip, vol)) {
             if (s >= full_d) { s = full_d; break; }
             s += calc_dt(s, vol.ss);
@@ -413,7 +426,8 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
 #ifdef SHADOW_NO_NERF
             const float nd = fminf(full_d, fd + Ld.x);
 #else
-            const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip));
+            const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip,
+                                                                   full_d <= fd ? full_d : __builtin_huge_valf()));
 #endif
             const double mask = (double)(nd * (1.0f - fminf(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)a.threshold));
             overall = (float)fmin((double)overall, mask);
@@ -626,7 +640,8 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                         int oh = -1;
                         const float syn = a.show_nerf_shadow ? depth_test_world(h.pos, Lv, a.objs, a.n_objs, cx, oh) : 1.0f;
                         const float nerf = a.show_nerf_shadow
-                                               ? depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, h.pos, Lv, invL, 0, a.vol.max_mip)
+                                               ? depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, h.pos, Lv, invL, 0, a.vol.max_mip,
+                                                                 fminf(syn, full_dist))
                                                : 1.0f;
                         const float sh = fminf(fminf(nerf, syn), full_dist);
                         const float mask = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
@@ -1172,7 +1187,7 @@ __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQue
 #ifdef SHADOW_TIMING_NO_NERF
         const float nerf = MAX_DEPTH;
 #else
-        const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip);
+        const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip, fminf(syn, full_dist));
 #endif
         const float sh = fminf(fminf(nerf, syn), full_dist);
         q.mask[q.mask_at(kr, jp)] = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
