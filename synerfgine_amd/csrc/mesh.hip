@@ -387,6 +387,23 @@ __device__ __forceinline__ Xorwow load_rng(const uint32_t* __restrict__ st, size
 __device__ __forceinline__ void store_rng(uint32_t* __restrict__ st, size_t n, size_t i, const Xorwow& s) {
     st[i] = s.v0; st[n + i] = s.v1; st[2 * n + i] = s.v2; st[3 * n + i] = s.v3; st[4 * n + i] = s.v4; st[5 * n + i] = s.d;
 }
+// pow(x, n) of the Phong term (material.cuh, shade_object): an integer exponent in [0, 4096] -- every
+// material of the reference's scenes -- by binary exponentiation (a few ulps; the reference's build,
+// --use_fast_math, evaluates __powf = exp2(n * log2(x)), which is coarser), otherwise powf.  Every
+// kernel that forms a light colour calls this, so the path-tracer variants stay bit-identical.
+__device__ __forceinline__ float spec_pow(float x, float n) {
+    if (floorf(n) == n && n >= 0.0f && n <= 4096.0f) {
+        uint32_t e = (uint32_t)n;
+        float r = 1.0f, b = x;
+        while (e) {
+            if (e & 1u) r *= b;
+            b *= b;
+            e >>= 1;
+        }
+        return r;
+    }
+    return powf(x, n);
+}
 // Light::sample(rand_state) (light.cuh:71-77)
 __device__ __forceinline__ f3 light_sample(const LightGpu& l, Xorwow& r) {
     const float x = fractf_(curand_uniform(r)), y = fractf_(curand_uniform(r)), z = fractf_(curand_uniform(r));
@@ -572,7 +589,7 @@ __device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& 
                 Lv = normalize(Lv);
                 const f3 R = reflect(Lv, h.normal);
                 const f3 V = normalize(-rd);
-                const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
 #endif
                 lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                 if (L.type == 0) {
@@ -634,7 +651,7 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                     Lv = normalize(Lv);
                     const f3 R = reflect(Lv, h.normal);
                     const f3 V = normalize(-rd);
-                    const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                    const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                     if (L.type == 0) {
                         const f3 invL = inv(Lv);
                         int oh = -1;
@@ -884,7 +901,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SPEC_WAVES_
                         Lv = normalize(Lv);
                         const f3 R = reflect(Lv, hb.normal);
                         const f3 V = normalize(-hb.rd);
-                        const f3 lc = fmaxf(0.0f, dot(Lv, hb.normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                        const f3 lc = fmaxf(0.0f, dot(Lv, hb.normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                         lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                         if (L.type == 0) {
                             float4* sr = q.shadow_ray(kr, jp);
@@ -1044,7 +1061,7 @@ __global__ __launch_bounds__(256) void rt_shade_kernel(RaytraceArgs a, RtQueue q
                     Lv = normalize(Lv);
                     const f3 R = reflect(Lv, normal);
                     const f3 V = normalize(-rd);
-                    const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                    const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                     lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                     if (L.type == 0) {
                         float4* sr = q.shadow_ray(k, jp);
@@ -1131,7 +1148,7 @@ __global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, R
                 Lv = normalize(Lv);
                 const f3 R = reflect(Lv, normal);
                 const f3 V = normalize(-rd);
-                const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + powf(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                 lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                 if (L.type == 0) {
                     float4* sr = q.shadow_ray(k, jp);
