@@ -387,11 +387,12 @@ __device__ __forceinline__ Xorwow load_rng(const uint32_t* __restrict__ st, size
 __device__ __forceinline__ void store_rng(uint32_t* __restrict__ st, size_t n, size_t i, const Xorwow& s) {
     st[i] = s.v0; st[n + i] = s.v1; st[2 * n + i] = s.v2; st[3 * n + i] = s.v3; st[4 * n + i] = s.v4; st[5 * n + i] = s.d;
 }
-// pow(x, n) of the Phong term (material.cuh, shade_object): an integer exponent in [0, 4096] -- every
-// material of the reference's scenes -- by binary exponentiation (a few ulps; the reference's build,
-// --use_fast_math, evaluates __powf = exp2(n * log2(x)), which is coarser), otherwise powf.  Every
-// kernel that forms a light colour calls this, so the path-tracer variants stay bit-identical.
-__device__ __forceinline__ float spec_pow(float x, float n) {
+// pow(x, n) with the exponents of the render path (the Phong exponent of every reference material, the
+// shadow intensities, all small integers): an integer n in [0, 4096] by binary exponentiation (exact for
+// n = 0, 1, 2, a few ulps above; the reference's build, --use_fast_math, evaluates __powf =
+// exp2(n * log2(x)), which is coarser), otherwise powf.  Every kernel computing the same quantity calls
+// it, so the path-tracer variants stay bit-identical to each other.
+__device__ __forceinline__ float pow_small_int(float x, float n) {
     if (floorf(n) == n && n >= 0.0f && n <= 4096.0f) {
         uint32_t e = (uint32_t)n;
         float r = 1.0f, b = x;
@@ -435,7 +436,7 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
 #else
             const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, cx, hit);
 #endif
-            overall = fminf(overall, powf(syn_depth / full_d, a.intensity));
+            overall = fminf(overall, pow_small_int(syn_depth / full_d, a.intensity));
             const f3 fract_offset = full_d * a.threshold * lpos;
             const f3 src = pos + fract_offset;
             const float fd = length(lpos - src);
@@ -457,7 +458,7 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
     return overall;
 }
 __device__ __forceinline__ void shadow_apply(const ShadowArgs& a, float4* __restrict__ rgba, size_t idx, float sum) {
-    sum = powf(sum, a.intensity);
+    sum = pow_small_int(sum, a.intensity);
     float4 c = rgba[idx];
     c.x = srgb_to_linear(c.x) * sum;
     c.y = srgb_to_linear(c.y) * sum;
@@ -589,7 +590,7 @@ __device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& 
                 Lv = normalize(Lv);
                 const f3 R = reflect(Lv, h.normal);
                 const f3 V = normalize(-rd);
-                const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
 #endif
                 lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                 if (L.type == 0) {
@@ -651,7 +652,7 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                     Lv = normalize(Lv);
                     const f3 R = reflect(Lv, h.normal);
                     const f3 V = normalize(-rd);
-                    const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                    const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                     if (L.type == 0) {
                         const f3 invL = inv(Lv);
                         int oh = -1;
@@ -661,7 +662,7 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                                                                  fminf(syn, full_dist))
                                                : 1.0f;
                         const float sh = fminf(fminf(nerf, syn), full_dist);
-                        const float mask = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
+                        const float mask = pow_small_int(smoothstep(sh / full_dist), a.syn_shadow_factor);
                         color = color + lc * mask;
                     } else {
                         color = color + lc;
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SPEC_WAVES_
                         Lv = normalize(Lv);
                         const f3 R = reflect(Lv, hb.normal);
                         const f3 V = normalize(-hb.rd);
-                        const f3 lc = fmaxf(0.0f, dot(Lv, hb.normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                        const f3 lc = fmaxf(0.0f, dot(Lv, hb.normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                         lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                         if (L.type == 0) {
                             float4* sr = q.shadow_ray(kr, jp);
@@ -1061,7 +1062,7 @@ __global__ __launch_bounds__(256) void rt_shade_kernel(RaytraceArgs a, RtQueue q
                     Lv = normalize(Lv);
                     const f3 R = reflect(Lv, normal);
                     const f3 V = normalize(-rd);
-                    const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                    const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                     lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                     if (L.type == 0) {
                         float4* sr = q.shadow_ray(k, jp);
@@ -1148,7 +1149,7 @@ __global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, R
                 Lv = normalize(Lv);
                 const f3 R = reflect(Lv, normal);
                 const f3 V = normalize(-rd);
-                const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + spec_pow(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+                const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
                 lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
                 if (L.type == 0) {
                     float4* sr = q.shadow_ray(k, jp);
@@ -1207,7 +1208,7 @@ __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQue
         const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip, fminf(syn, full_dist));
 #endif
         const float sh = fminf(fminf(nerf, syn), full_dist);
-        q.mask[q.mask_at(kr, jp)] = powf(smoothstep(sh / full_dist), a.syn_shadow_factor);
+        q.mask[q.mask_at(kr, jp)] = pow_small_int(smoothstep(sh / full_dist), a.syn_shadow_factor);
     }
     if constexpr (CNT) flush_counts(a.counts + 3, counts, lane);
 }
