@@ -246,12 +246,16 @@ SNG_HD StepSpace step_space(float cone) {
     k.bt = sng_expf(k.b * k.log1p_c);
     return k;
 }
+// The two constant divisions as exact reciprocal forms: x / MIN_STEP is div_by (see above), and since
+// MAX_STEP == MIN_STEP * 2^10 exactly, x / MAX_STEP == (x / MIN_STEP) * 2^-10 (power-of-two scaling
+// commutes with rounding in the normal range).
 SNG_HD float to_stepping_space(float t, const StepSpace& k) {
     if (k.cone <= 1e-5f) return div_by(t, MIN_STEP, INV_MIN_STEP);
-    if (t <= k.at) return (t - k.at) / MIN_STEP + k.a;
+    if (t <= k.at) return div_by(t - k.at, MIN_STEP, INV_MIN_STEP) + k.a;
     else if (t <= k.bt) return sng_logf(t) / k.log1p_c;
-    else return (t - k.bt) / MAX_STEP + k.b;
+    else return div_by(t - k.bt, MIN_STEP, INV_MIN_STEP) * (1.0f / 1024.0f) + k.b;
 }
+static_assert(MAX_STEP == MIN_STEP * 1024.0f, "MAX_STEP / MIN_STEP must be 2^10");
 SNG_HD float from_stepping_space(float n, const StepSpace& k) {
     if (k.cone <= 1e-5f) return n * MIN_STEP;
     if (n <= k.a) return (n - k.a) * MIN_STEP + k.at;
@@ -277,9 +281,19 @@ SNG_HD float advance_to_next_voxel(float t, float cone, f3 pos, f3 dir, f3 idir,
     t_target = to_stepping_space(t_target, cone);
     return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), cone);
 }
+// distance_to_next_voxel with res = 128 * 2^-mip; its final t / res is the exact power-of-two scaling
+// t * 2^(mip - 7)
+SNG_HD float distance_to_next_voxel_mip(f3 pos, f3 dir, f3 idir, uint32_t mip) {
+    const float res = scalbnf((float)GRID_SIZE, -(int)mip);
+    f3 p = res * (pos - 0.5f);
+    float tx = (floorf(p.x + 0.5f + 0.5f * sgnf(dir.x)) - p.x) * idir.x;
+    float ty = (floorf(p.y + 0.5f + 0.5f * sgnf(dir.y)) - p.y) * idir.y;
+    float tz = (floorf(p.z + 0.5f + 0.5f * sgnf(dir.z)) - p.z) * idir.z;
+    float t = fminf(fminf(tx, ty), tz);
+    return fmaxf(t * scalbnf(1.0f / (float)GRID_SIZE, (int)mip), 0.0f);
+}
 SNG_HD float advance_to_next_voxel(float t, const StepSpace& k, f3 pos, f3 dir, f3 idir, uint32_t mip) {
-    float res = scalbnf((float)GRID_SIZE, -(int)mip);
-    float t_target = t + distance_to_next_voxel(pos, dir, idir, res);
+    float t_target = t + distance_to_next_voxel_mip(pos, dir, idir, mip);
     t = to_stepping_space(t, k);
     t_target = to_stepping_space(t_target, k);
     return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), k);
