@@ -119,15 +119,11 @@ __device__ __forceinline__ void flush_counts(unsigned long long* dst, const uint
 // formed first and u, v only when t can win.  The accept set is unchanged: the reference replaces
 // a rejected t by FLT_MAX, which never passes `t < mint` (mint <= MAX_DEPTH), and a NaN t fails
 // both forms; u, v are evaluated with the reference's expressions and comparisons.
-// 1.0f / x correctly rounded: v_rcp_f32 plus one FMA correction equals IEEE 1.0f / x for every x with
-// 2^-126 <= |x| < 2^126 (tools/rcp_check.hip: all 2^32 inputs on gfx950); the rest (zero,
-// denormals, results that would be denormal, inf, NaN) take the IEEE division.
+// 1.0f / x correctly rounded for every x: recip_rn (sng_math.h) in its range 2^-126 <= |x| < 2^126, the
+// IEEE division for the rest (zero, denormals, results that would be denormal, inf, NaN).
 __device__ __forceinline__ float rcp_exact(float x) {
     const float ax = fabsf(x);
-    if (ax >= 0x1p-126f && ax < 0x1p126f) {
-        const float y = __builtin_amdgcn_rcpf(x);
-        return fmaf(fmaf(-x, y, 1.0f), y, y);
-    }
+    if (ax >= 0x1p-126f && ax < 0x1p126f) return recip_rn(x);
     return 1.0f / x;
 }
 __device__ __forceinline__ bool tri_hit(const TriT* tp, f3 ro, f3 rd, float mint, float& t_out) {

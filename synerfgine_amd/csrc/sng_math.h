@@ -57,6 +57,25 @@ SNG_HD float sgnf(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f);
 // IEEE basic operations and fmaf only (<= ~1 ulp), so the CPU oracle (its own copy in
 // oracle/sng_oracle.cpp) and the GPU produce identical bits wherever a marching or termination
 // DECISION depends on them (cone stepping, compositing alpha).
+// x / d, correctly rounded, from y = RN(1/d): q0 = RN(x*y) plus one FMA remainder correction
+// (Markstein).  Verified bit-identical to IEEE division for every float t in [1e-9, 4e4] with
+// d = MIN_STEP and for 4e8 random (x, d) pairs (tools/divtest: 0 mismatches).
+SNG_HD float div_by(float x, float d, float y) {
+    const float q0 = x * y;
+    const float r = fmaf(-q0, d, x);
+    return fmaf(r, y, q0);
+}
+// RN(1/d) for 2^-126 <= |d| < 2^126: on the device v_rcp_f32 plus one FMA correction, which equals IEEE
+// 1.0f / d for every such d (tools/rcp_check.hip: all 2^32 inputs on gfx950, profiles/rcp_check_r02.txt);
+// the host divides.
+SNG_HD float recip_rn(float d) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const float y = __builtin_amdgcn_rcpf(d);
+    return fmaf(fmaf(-d, y, 1.0f), y, y);
+#else
+    return 1.0f / d;
+#endif
+}
 SNG_HD float sng_expf(float x) {
     if (x != x) return x;
     if (x > 88.72283935f) return __builtin_huge_valf();
@@ -82,7 +101,9 @@ SNG_HD float sng_logf(float x) {
     float m = frexpf(x, &e);                      // [0.5, 1)
     if (m < 0.707106769f) { m = m * 2.0f; e -= 1; }
     const float f = m - 1.0f;                     // exact (Sterbenz)
-    const float s = f / (2.0f + f);
+    // f / (2 + f) as div_by with the exact reciprocal: equal to the IEEE division for every f this
+    // function forms (all 2^24 mantissas, tests/native/march_check.cpp)
+    const float s = div_by(f, 2.0f + f, recip_rn(2.0f + f));
     const float z = s * s;
     const float R = z * fmaf(z, fmaf(z, fmaf(z, 0.222222224f, 0.285714298f), 0.400000006f), 0.666666687f);
     const float hf = 0.5f * f * f;
@@ -128,14 +149,6 @@ SNG_HD uint32_t morton3D_invert(uint32_t x) {
 
 // ---- AABB slab test: bounding_box.cuh:163-211 ---------------------------------
 struct aabb { f3 lo, hi; };
-// x / d, correctly rounded, from y = RN(1/d): q0 = RN(x*y) plus one FMA remainder correction
-// (Markstein).  Verified bit-identical to IEEE division for every float t in [1e-9, 4e4] with
-// d = MIN_STEP and for 4e8 random (x, d) pairs (tools/divtest: 0 mismatches).
-SNG_HD float div_by(float x, float d, float y) {
-    const float q0 = x * y;
-    const float r = fmaf(-q0, d, x);
-    return fmaf(r, y, q0);
-}
 constexpr float INV_MIN_STEP = 1.0f / MIN_STEP;   // RN(1/MIN_STEP), folded at compile time
 
 struct f2 { float x, y; };

@@ -104,7 +104,19 @@ int main() {
         const float fa = aabb_entry_fast(box, o, d, inv(d)), fb = aabb_entry(box, o, d);
         if (!(same(fa, fb) || (fa == 0.0f && fb == 0.0f))) ++bad_slab;
     }
-    std::printf("{\"div\": [%ld, %ld], \"march\": [%ld, %ld, %ld], \"slab\": [%ld, %ld]}\n", n_div, bad_div, n_march, n_samples, bad_march,
-                n_slab, bad_slab);
-    return (bad_div || bad_march || bad_slab) ? 1 : 0;
+    // sng_logf's f / (2 + f) as div_by(f, d, RN(1/d)): every f it can form (m in [0.5, 1), doubled below
+    // 0.7071, f = m - 1), i.e. all 2^23 mantissas.  recip_rn is 1.0f / d on the host and bit-identical to
+    // it on the device (tools/rcp_check.hip), so this covers the device form too.
+    long bad_log = 0, n_log = 0;
+    for (uint32_t u = 0x3F000000u; u < 0x3F800000u; ++u) {
+        float m;
+        std::memcpy(&m, &u, 4);
+        if (m < 0.707106769f) m = m * 2.0f;
+        const float f = m - 1.0f, den = 2.0f + f;
+        ++n_log;
+        if (!same(div_by(f, den, recip_rn(den)), f / den)) ++bad_log;
+    }
+    std::printf("{\"div\": [%ld, %ld], \"march\": [%ld, %ld, %ld], \"slab\": [%ld, %ld], \"logdiv\": [%ld, %ld]}\n", n_div, bad_div, n_march,
+                n_samples, bad_march, n_slab, bad_slab, n_log, bad_log);
+    return (bad_div || bad_march || bad_slab || bad_log) ? 1 : 0;
 }
