@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
             const f3 wp = ((so + sd * ts) - vol.train_aabb.lo) / wdiag;   // generate_kernel's expressions
             const f3 wd = (sd + 1.0f) * 0.5f;
             f4v out, dens;
-            field_tile<F>(W, a.levels, grid, g, wp.x, wp.y, wp.z, wd.x, wd.y, wd.z, out, dens);
+            field_tile<F, true>(W, a.levels, grid, g, wp.x, wp.y, wp.z, wd.x, wd.y, wd.z, out, dens);
             if (valid && g == 0) {
                 const _Float16 r = (_Float16)out[0], gg = (_Float16)out[1], b = (_Float16)out[2], s = (_Float16)dens[0];
                 out_lds[wv][q] = make_uint2((uint32_t)__builtin_bit_cast(uint16_t, r) | ((uint32_t)__builtin_bit_cast(uint16_t, gg) << 16),

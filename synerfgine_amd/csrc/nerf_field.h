@@ -2,6 +2,7 @@
 // shared by the standalone network kernel (network.hip) and the fused marcher (fused.hip).
 // See network.hip for the lane/fragment mapping.  [tcnn semantics restated -- DESIGN.md]
 #pragma once
+#include <type_traits>
 #include "sng_math.h"
 #include "sng_internal.h"
 
@@ -24,9 +25,16 @@ __device__ __forceinline__ h8 pack_relu(f4v lo, f4v hi) {
     return r;
 }
 
+// tcnn grid_index: the dense or hashed index modulo the level size.  FAST_MOD: for a dense level
+// res^3 <= size, so a corner inside the grid (x, y, z <= res) has idx <= res + res^2 + res^3 < 2 * size
+// and the modulo is one conditional subtraction; the full `%` runs only for corners outside (same value).
+// (The network kernel keeps the plain form: 2 more VGPRs would cost it a wave per SIMD.)
+template <bool FAST_MOD = false>
 __device__ __forceinline__ uint32_t grid_index(const LevelInfo& L, uint32_t x, uint32_t y, uint32_t z) {
     uint32_t idx = L.dense ? (x + y * L.res + z * L.res2) : ((x * 1u) ^ (y * 2654435761u) ^ (z * 805459861u));
-    return L.pow2_mask ? (idx & L.pow2_mask) : (idx % L.size);
+    if (L.pow2_mask) return idx & L.pow2_mask;
+    if (FAST_MOD && L.dense && idx < 2u * L.size) return idx >= L.size ? idx - L.size : idx;
+    return idx % L.size;
 }
 
 // Interpolate one level for one sample: tcnn kernel_grid N-linear path,
@@ -82,7 +90,8 @@ __device__ __forceinline__ void encode_level(const LevelInfo& L, const _Float16*
     }
 }
 
-// The lane's 8 features: levels [lpl*g, lpl*g + lpl) (lpl = 8/F levels per lane)
+// The lane's 8 features: levels [lpl*g, lpl*g + lpl) (lpl = 8/F levels per lane), one level at a time
+// (the standalone network kernel: 72 VGPRs and 7 waves per SIMD hide the gathers best this way).
 template <int F>
 __device__ __forceinline__ h8 encode_lane(const LevelInfo* __restrict__ levels, const _Float16* __restrict__ grid, int g, float x0,
                                           float x1, float x2) {
@@ -96,6 +105,66 @@ __device__ __forceinline__ h8 encode_lane(const LevelInfo* __restrict__ levels, 
     h8 r;
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] = e[j];
+    return r;
+}
+// The same features with the gathers of ALL the lane's levels issued before any corner is blended, so
+// a sample waits for memory once instead of once per level (encode_level's arithmetic; the fused tail,
+// whose waves each walk their own samples: 0.85 -> 0.75 ms in C3; the network kernel lost occupancy
+// with the 8 extra VGPRs and ran 12 % slower, so it keeps encode_lane).
+template <int F>
+__device__ __forceinline__ h8 encode_lane_all(const LevelInfo* __restrict__ levels, const _Float16* __restrict__ grid, int g, float x0,
+                                              float x1, float x2) {
+    constexpr int LPL = 8 / F;
+    typedef typename std::conditional<F == 4, uint2, uint32_t>::type V;
+    V v[LPL][8];
+    float fr[LPL][3];
+#pragma unroll
+    for (int l = 0; l < LPL; ++l) {
+        const LevelInfo L = levels[g * LPL + l];
+        const float p0 = fmaf(L.scale, x0, 0.5f), p1 = fmaf(L.scale, x1, 0.5f), p2 = fmaf(L.scale, x2, 0.5f);
+        const float q0 = floorf(p0), q1 = floorf(p1), q2 = floorf(p2);
+        const uint32_t g0 = (uint32_t)(int)q0, g1 = (uint32_t)(int)q1, g2 = (uint32_t)(int)q2;
+        fr[l][0] = p0 - q0; fr[l][1] = p1 - q1; fr[l][2] = p2 - q2;
+        const _Float16* tbl = grid + (size_t)L.offset * F;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            v[l][c] = *reinterpret_cast<const V*>(tbl + grid_index<true>(L, g0 + (c & 1), g1 + ((c >> 1) & 1), g2 + ((c >> 2) & 1)) * F);
+    }
+    h8 r;
+#pragma unroll
+    for (int l = 0; l < LPL; ++l) {
+        const float f0 = fr[l][0], f1 = fr[l][1], f2 = fr[l][2];
+        if constexpr (F == 4) {
+            h2 r01 = {(_Float16)0.0f, (_Float16)0.0f}, r23 = r01;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                float w = 1.0f;
+                w *= (c & 1) ? f0 : 1.0f - f0;
+                w *= (c & 2) ? f1 : 1.0f - f1;
+                w *= (c & 4) ? f2 : 1.0f - f2;
+                asm volatile("" : "+v"(w));   // keep the f32 product rounded before the f16 cast (no v_fma_mix fusion): tcnn (T)weight
+                const _Float16 wh = (_Float16)w;
+                const h2 w2 = {wh, wh};
+                r01 = __builtin_elementwise_fma(w2, __builtin_bit_cast(h2, v[l][c].x), r01);
+                r23 = __builtin_elementwise_fma(w2, __builtin_bit_cast(h2, v[l][c].y), r23);
+            }
+            r[l * 4 + 0] = r01[0]; r[l * 4 + 1] = r01[1]; r[l * 4 + 2] = r23[0]; r[l * 4 + 3] = r23[1];
+        } else {
+            h2 acc = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                float w = 1.0f;
+                w *= (c & 1) ? f0 : 1.0f - f0;
+                w *= (c & 2) ? f1 : 1.0f - f1;
+                w *= (c & 4) ? f2 : 1.0f - f2;
+                asm volatile("" : "+v"(w));   // keep the f32 product rounded before the f16 cast (no v_fma_mix fusion): tcnn (T)weight
+                const _Float16 wh = (_Float16)w;
+                const h2 w2 = {wh, wh};
+                acc = __builtin_elementwise_fma(w2, __builtin_bit_cast(h2, v[l][c]), acc);
+            }
+            r[l * 2 + 0] = acc[0]; r[l * 2 + 1] = acc[1];
+        }
+    }
     return r;
 }
 
@@ -129,12 +198,12 @@ struct LdsWeights {
     __device__ __forceinline__ h8 operator[](int f) const { return base[f * 64 + lane]; }
 };
 
-template <int F, typename WT = const h8*>
+template <int F, bool GATHER_ALL = false, typename WT = const h8*>
 __device__ __forceinline__ void field_tile(WT W, const LevelInfo* __restrict__ levels, const _Float16* __restrict__ grid, int g, float x0,
                                            float x1, float x2, float d0, float d1, float d2, f4v& o, f4v& dens) {
     const f4v zero = {0.0f, 0.0f, 0.0f, 0.0f};
     // ---- hash grid encoding -> B fragment of layer 0
-    h8 enc = encode_lane<F>(levels, grid, g, x0, x1, x2);
+    h8 enc = GATHER_ALL ? encode_lane_all<F>(levels, grid, g, x0, x1, x2) : encode_lane<F>(levels, grid, g, x0, x1, x2);
     // ---- density MLP: H^T = relu(W0 E^T) (64 rows = 4 blocks), O^T = W1 H^T (16 rows)
     f4v a0 = mfma16(W[0], enc, zero), a1 = mfma16(W[1], enc, zero), a2 = mfma16(W[2], enc, zero), a3 = mfma16(W[3], enc, zero);
     dens = mfma16(W[4], pack_relu(a0, a1), zero);
