@@ -1,9 +1,9 @@
 #!/bin/bash
 export TMPDIR=/tmp
 mkdir -p gpurun_out/band
-timeout -k 10 200 python tools/small_band.py 463 521 serial 2>&1 | grep -v amdgpu.ids
-timeout -k 10 200 python tools/small_band.py 463 521 2>&1 | grep -v amdgpu.ids
-timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/band -o run --output-format csv -- python3 tools/small_band.py 463 521 serial > gpurun_out/band/log 2>&1; echo "prof rc=$?"
+timeout -k 10 200 python tools/small_band.py 907 1080 serial 2>&1 | grep -v amdgpu.ids
+timeout -k 10 200 python tools/small_band.py 907 1080 2>&1 | grep -v amdgpu.ids
+timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/band -o run --output-format csv -- python3 tools/small_band.py 907 1080 serial > gpurun_out/band/log 2>&1; echo "prof rc=$?"
 python3 - <<'PY'
 import csv, glob, re
 f = glob.glob("gpurun_out/band/**/*kernel_trace.csv", recursive=True)[0]
