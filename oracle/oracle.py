@@ -117,6 +117,7 @@ def lib():
             "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
             "orc_num_threads": (i32, []), "orc_set_num_threads": (None, [i32]), "orc_set_mlp_accum": (None, [i32, i32]),
             "orc_set_visualization": (None, [i32, i32]),
+            "orc_set_motion_blur": (None, [vp, vp]), "orc_set_glow": (None, [i32, f32]),
             "orc_set_gbuffer_out": (None, [vp, vp]),
             "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
             "orc_display": (None, [vp, i32, i32, i32, i32, vp, vp]),
@@ -147,6 +148,21 @@ class mlp_accum:
 
 def ptr(a):
     return ctypes.c_void_p(a.ctypes.data)
+
+
+class motion_blur:
+    """Context manager: NeRF camera rays with View::camera1 / rolling_shutter (testbed_nerf.cu:1895)."""
+    def __init__(self, camera1=None, rolling_shutter=None):
+        self.c1 = None if camera1 is None else np.ascontiguousarray(np.asarray(camera1, np.float32).ravel())
+        self.rs = None if rolling_shutter is None else np.ascontiguousarray(rolling_shutter, np.float32)
+
+    def __enter__(self):
+        lib().orc_set_motion_blur(None if self.c1 is None else ptr(self.c1), None if self.rs is None else ptr(self.rs))
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_motion_blur(None, None)
+        return False
 
 
 # ---- convenience wrappers -----------------------------------------------------------
@@ -280,14 +296,18 @@ def render_nerf(model, vol, cam):
     return rgba, depth, pos, nrm, st
 
 
-def render_nerf_ngp(model, vol, cam, render_mode=1, depth_scale=1.0, vis_layer=0, vis_dim=0):
+def render_nerf_ngp(model, vol, cam, render_mode=1, depth_scale=1.0, vis_layer=0, vis_dim=0, glow_mode=0, glow_y_cutoff=0.0):
     """instant-NGP render path (A22): returns rgba [H,W,4], depth [H,W], stats."""
     W, H = cam.res[0], cam.res[1]
     rgba = np.zeros((H, W, 4), np.float32)
     depth = np.zeros((H, W), np.float32)
     st = orc_nerf_stats()
     lib().orc_set_visualization(vis_layer, vis_dim)
-    lib().orc_render_nerf_ngp(model.ref(), ctypes.byref(vol), ctypes.byref(cam), render_mode, depth_scale, ptr(rgba), ptr(depth), ctypes.byref(st))
+    lib().orc_set_glow(glow_mode, glow_y_cutoff)
+    try:
+        lib().orc_render_nerf_ngp(model.ref(), ctypes.byref(vol), ctypes.byref(cam), render_mode, depth_scale, ptr(rgba), ptr(depth), ctypes.byref(st))
+    finally:
+        lib().orc_set_glow(0, 0.0)
     return rgba, depth, st
 
 

@@ -916,6 +916,84 @@ M3 rolling_shutter_rotation(const M3& rot) {
     return r;
 }
 
+/* get_xform_given_rolling_shutter (common_device.cuh:361-368) for start != end: slerp(q0, q1, t) with
+ * the short-way negation and the mix branch near cos 1, normalize, to_mat3 [tcnn quat, unvendored] */
+M3 shutter_rotation(Quat a, Quat b, float t) {
+    float cos_theta = a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+    if (cos_theta < 0.0f) { b = {-b.x, -b.y, -b.z, -b.w}; cos_theta = -cos_theta; }
+    Quat s;
+    if (cos_theta > 1.0f - std::numeric_limits<float>::epsilon()) {
+        s = {a.x * (1.0f - t) + b.x * t, a.y * (1.0f - t) + b.y * t, a.z * (1.0f - t) + b.z * t, a.w * (1.0f - t) + b.w * t};
+    } else {
+        float angle = std::acos(cos_theta);
+        float s0 = std::sin((1.0f - t) * angle), s1 = std::sin(t * angle), sa = std::sin(angle);
+        s = {(s0 * a.x + s1 * b.x) / sa, (s0 * a.y + s1 * b.y) / sa, (s0 * a.z + s1 * b.z) / sa, (s0 * a.w + s1 * b.w) / sa};
+    }
+    float len = std::sqrt(s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w);
+    s = {s.x / len, s.y / len, s.z / len, s.w / len};
+    float qxx = s.x * s.x, qyy = s.y * s.y, qzz = s.z * s.z, qxz = s.x * s.z, qxy = s.x * s.y, qyz = s.y * s.z;
+    float qwx = s.w * s.x, qwy = s.w * s.y, qwz = s.w * s.z;
+    M3 r;
+    r.c[0][0] = 1.0f - 2.0f * (qyy + qzz); r.c[0][1] = 2.0f * (qxy + qwz); r.c[0][2] = 2.0f * (qxz - qwy);
+    r.c[1][0] = 2.0f * (qxy - qwz); r.c[1][1] = 1.0f - 2.0f * (qxx + qzz); r.c[1][2] = 2.0f * (qyz + qwx);
+    r.c[2][0] = 2.0f * (qxz + qwy); r.c[2][1] = 2.0f * (qyz - qwx); r.c[2][2] = 1.0f - 2.0f * (qxx + qyy);
+    return r;
+}
+
+/* View::camera1 / rolling_shutter (testbed.h:1032,1042): orc_set_motion_blur */
+static bool g_has_cam1 = false;
+static float g_cam1[12], g_rs[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+/* Testbed::Nerf::glow_mode / glow_y_cutoff (testbed.h:870-871): orc_set_glow */
+static int g_glow_mode = 0;
+static float g_glow_y_cutoff = 0.0f;
+
+/* composite_kernel_nerf's glow visualisation (testbed_nerf.cu:638-734): adds to rgb, may scale weight */
+static void glow_term(V3 pos, V3 cam_pos, V3& rgb, float& weight) {
+    const int glow_mode = g_glow_mode;
+    const float glow_y_cutoff = g_glow_y_cutoff;
+    float glow = 0.f;
+    const bool green_grid = glow_mode & 1, green_cutline = glow_mode & 2, mask_to_alpha = glow_mode & 4;
+    const bool radial_mode = glow_mode & 8, grid_mode = glow_mode & 16;
+    float dist;
+    if (radial_mode) {
+        dist = length(pos - cam_pos);
+        dist = std::min(dist, (4.5f - pos.y) * 0.333f);
+    } else {
+        dist = pos.y;
+    }
+    if (grid_mode) {
+        glow = 1.f / std::max(1.f, dist);
+    } else {
+        float y = glow_y_cutoff - dist;
+        float mask = 0.f;
+        if (y > 0.f) {
+            y *= 80.f;
+            mask = std::min(1.f, y);
+            if (green_cutline) glow += std::max(0.f, 1.f - std::fabs(1.f - y)) * 4.f;
+            if (y > 1.f) y = 1.f - (y - 1.f) * 0.05f;
+            if (green_grid) glow += std::max(0.f, y / std::max(1.f, dist));
+        }
+        if (mask_to_alpha) weight *= mask;
+    }
+    if (glow > 0.f) {
+        float line = 0.f;
+        const float sc[4] = {1.f, 2.f, 4.f, 8.f};
+        for (int q = 0; q < 4; ++q) {   /* pos.y, pos.x, pos.z at frequencies 2, 4, 8, 16 (in the reference's order) */
+            const float m = 2.f * sc[q];
+            line += std::max(0.f, std::cos(pos.y * m * 3.141592653589793f * 16.f) - 0.975f);
+            line += std::max(0.f, std::cos(pos.x * m * 3.141592653589793f * 16.f) - 0.975f);
+            line += std::max(0.f, std::cos(pos.z * m * 3.141592653589793f * 16.f) - 0.975f);
+        }
+        if (grid_mode) {
+            glow = glow * line * 15.f;
+            rgb.y = glow; rgb.z = glow * 0.5f; rgb.x = glow * 0.25f;
+        } else {
+            glow = glow * glow * 0.25f + glow * line * 15.f;
+            rgb.y += glow; rgb.z += glow * 0.5f; rgb.x += glow * 0.25f;
+        }
+    }
+}
+
 struct Payload { V3 origin, dir; float t, max_weight; uint32_t idx; uint16_t n_steps; bool alive; };
 struct RayState { V4 rgba; float depth; Payload p; };
 
@@ -1022,7 +1100,11 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
     const int W = c->res[0], H = c->res[1];
     const uint32_t n_px = (uint32_t)W * H;
     M43 cam = m43_load(c->camera);
-    M3 rs_rot = rolling_shutter_rotation(m3_of(cam));
+    /* get_xform_given_rolling_shutter({camera0, camera1}, rolling_shutter, uv, motionblur_time), testbed_nerf.cu:1895 */
+    const Quat q0 = quat_from_m3(m3_of(cam));
+    M43 cam1 = g_has_cam1 ? m43_load(g_cam1) : cam;
+    const Quat q1 = quat_from_m3(m3_of(cam1));
+    const V3 pos1 = cam1.c[3];
     V2 focal = {c->focal[0], c->focal[1]};
     V2 sc = {c->screen_center[0], c->screen_center[1]};
     V3 cam_fwd = cam.c[2], cam_pos = cam.c[3];
@@ -1043,8 +1125,9 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
         V2 uv = {((float)x + pixel_offset.x) / (float)W, ((float)y + pixel_offset.y) / (float)H};
         /* uv_to_ray (common_device.cuh:403-470) with identity foveation, no lens, no parallax, aperture 0, near 0 */
         V3 dir = v3((uv.x - sc.x) * (float)W / focal.x, (uv.y - sc.y) * (float)H / focal.y, 1.0f);
-        dir = mul(rs_rot, dir);
-        V3 origin = cam_pos;
+        const float pixel_t = g_rs[0] + g_rs[1] * uv.x + g_rs[2] * uv.y + g_rs[3] * ld_random_val(c->spp, (uint32_t)idx * 72239731u);
+        dir = mul(shutter_rotation(q0, q1, pixel_t), dir);
+        V3 origin = cam_pos + (pos1 - cam_pos) * pixel_t;
         frame_rgba[4 * idx + 0] = 0.0f; frame_rgba[4 * idx + 1] = 0.0f; frame_rgba[4 * idx + 2] = 0.0f; /* rgb only */
         dir = normalize(dir);
         float t = std::fmax(bb_ray_intersect(vol.render_aabb, to_local(vol, origin), to_local(vol, dir)).x, 0.0f) + 1e-6f;
@@ -1134,6 +1217,7 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
                 float alpha = 1.f - det_expf(-det_expf(h2f(o[3])) * dt);
                 float weight = alpha * T;
                 V3 rgb = v3(logistic(h2f(o[0])), logistic(h2f(o[1])), logistic(h2f(o[2])));
+                if (ngp && g_glow_mode) glow_term(pos, cam_pos, rgb, weight);
                 if (ngp) {
                     if (render_mode == 2) {                                                                /* Normals */
                         const float dd = det_expf(std::min(std::max(h2f(o[3]), -15.0f), 15.0f));  /* network_to_density_derivative */
@@ -1580,6 +1664,16 @@ void orc_render_frame(const orc_model* m, const orc_volume* v, const orc_camera*
 void orc_set_visualization(int32_t layer, int32_t dim) {
     g_vis_layer = layer;
     g_vis_dim = dim;
+}
+void orc_set_motion_blur(const float* camera1, const float* rolling_shutter) {
+    g_has_cam1 = camera1 != nullptr;
+    if (camera1) std::memcpy(g_cam1, camera1, sizeof(g_cam1));
+    const float rs0[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    std::memcpy(g_rs, rolling_shutter ? rolling_shutter : rs0, sizeof(g_rs));
+}
+void orc_set_glow(int32_t mode, float y_cutoff) {
+    g_glow_mode = mode;
+    g_glow_y_cutoff = y_cutoff;
 }
 void orc_set_mlp_accum(int32_t mode, int32_t chunk) {
     g_mlp_accum = mode;

@@ -131,6 +131,11 @@ void orc_render_nerf(const orc_model* m, const orc_volume* v, const orc_camera* 
 /* instant-NGP render path (A22): NerfTracer::trace + composite_kernel_nerf + shade_kernel_nerf
  * (testbed_nerf.cu:2279-2401, 577-788, 1788-1828).  render_mode: ERenderMode (0 AO, 1 Shade,
  * 3 Positions, 4 Depth, 6 Cost, 10 EncodingVis); depth_scale = 1 / dataset.scale. */
+/* View::camera1 / rolling_shutter (testbed.h:1032,1042) for the NeRF camera rays (testbed_nerf.cu:1895);
+ * camera1 NULL: camera0, rolling_shutter NULL: (0, 0, 0, 1) */
+void orc_set_motion_blur(const float* camera1, const float* rolling_shutter);
+/* Testbed::Nerf::glow_mode / glow_y_cutoff (testbed.h:870-871) for orc_render_nerf_ngp (testbed_nerf.cu:638-734) */
+void orc_set_glow(int32_t mode, float y_cutoff);
 void orc_render_nerf_ngp(const orc_model* m, const orc_volume* v, const orc_camera* c, int32_t render_mode, float depth_scale,
                          float* frame_rgba /* W*H*4 */, float* frame_depth /* W*H */, orc_nerf_stats* stats);
 void orc_shade_nerf_shadows(const orc_volume* v, const int32_t res[2],

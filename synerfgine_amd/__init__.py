@@ -141,6 +141,12 @@ class Testbed:
         m = np.ascontiguousarray(m, np.float32).ravel()
         check(self._lib.sng_set_camera_matrix(self.ctx, _fptr(m)))
 
+    def set_motion_blur(self, camera1=None, rolling_shutter=None):
+        """View::camera1 / rolling_shutter for the NeRF rays (testbed_nerf.cu:1895); None restores the defaults."""
+        c1 = None if camera1 is None else np.ascontiguousarray(camera1, np.float32).ravel()
+        rs = None if rolling_shutter is None else np.ascontiguousarray(rolling_shutter, np.float32).ravel()
+        check(self._lib.sng_set_motion_blur(self.ctx, None if c1 is None else _fptr(c1), None if rs is None else _fptr(rs)))
+
     def set_fov(self, degrees):
         check(self._lib.sng_set_fov(self.ctx, float(degrees)))
 

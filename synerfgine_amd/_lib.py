@@ -174,6 +174,7 @@ SIGNATURES = {
     "sng_set_camera_view": (ctypes.c_int, [P, FP, FP, F32]),
     "sng_set_camera_matrix": (ctypes.c_int, [P, FP]),
     "sng_get_camera_matrix": (ctypes.c_int, [P, FP]),
+    "sng_set_motion_blur": (ctypes.c_int, [P, FP, FP]),
     "sng_set_fov": (ctypes.c_int, [P, F32]),
     "sng_get_focal_length": (ctypes.c_int, [P, ctypes.c_int, FP]),
     "sng_set_window": (ctypes.c_int, [P, I32, I32]),

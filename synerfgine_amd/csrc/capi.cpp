@@ -245,37 +245,8 @@ m3 inverse3(const m3& M) {
 // get_xform_given_rolling_shutter(start == end, t = 0) rotation: glm quat round trip
 // (common_device.cuh:361-368) [tcnn quat, unvendored]
 m3 rolling_shutter_rotation(const m3& M) {
-    auto e = [&](int i, int j) { const f3& c = i == 0 ? M.c0 : (i == 1 ? M.c1 : M.c2); return j == 0 ? c.x : (j == 1 ? c.y : c.z); };
-    float fx = e(0, 0) - e(1, 1) - e(2, 2), fy = e(1, 1) - e(0, 0) - e(2, 2), fz = e(2, 2) - e(0, 0) - e(1, 1), fw = e(0, 0) + e(1, 1) + e(2, 2);
-    int bi = 0;
-    float fb = fw;
-    if (fx > fb) { fb = fx; bi = 1; }
-    if (fy > fb) { fb = fy; bi = 2; }
-    if (fz > fb) { fb = fz; bi = 3; }
-    float bv = std::sqrt(fb + 1.0f) * 0.5f, mult = 0.25f / bv;
-    float q[4];  // x y z w
-    switch (bi) {
-        case 0: q[0] = (e(1, 2) - e(2, 1)) * mult; q[1] = (e(2, 0) - e(0, 2)) * mult; q[2] = (e(0, 1) - e(1, 0)) * mult; q[3] = bv; break;
-        case 1: q[0] = bv; q[1] = (e(0, 1) + e(1, 0)) * mult; q[2] = (e(2, 0) + e(0, 2)) * mult; q[3] = (e(1, 2) - e(2, 1)) * mult; break;
-        case 2: q[0] = (e(0, 1) + e(1, 0)) * mult; q[1] = bv; q[2] = (e(1, 2) + e(2, 1)) * mult; q[3] = (e(2, 0) - e(0, 2)) * mult; break;
-        default: q[0] = (e(2, 0) + e(0, 2)) * mult; q[1] = (e(1, 2) + e(2, 1)) * mult; q[2] = bv; q[3] = (e(0, 1) - e(1, 0)) * mult; break;
-    }
-    float cos_theta = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
-    float s[4];
-    if (cos_theta > 1.0f - 1.1920929e-7f) {
-        for (int k = 0; k < 4; ++k) s[k] = q[k] * (1.0f - 0.0f) + q[k] * 0.0f;
-    } else {
-        float angle = std::acos(cos_theta);
-        float s0 = std::sin((1.0f - 0.0f) * angle), s1 = std::sin(0.0f * angle), sa = std::sin(angle);
-        for (int k = 0; k < 4; ++k) s[k] = (s0 * q[k] + s1 * q[k]) / sa;
-    }
-    float len = std::sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2] + s[3] * s[3]);
-    for (int k = 0; k < 4; ++k) s[k] = s[k] / len;
-    float qxx = s[0] * s[0], qyy = s[1] * s[1], qzz = s[2] * s[2], qxz = s[0] * s[2], qxy = s[0] * s[1], qyz = s[1] * s[2];
-    float qwx = s[3] * s[0], qwy = s[3] * s[1], qwz = s[3] * s[2];
-    return {mk(1.0f - 2.0f * (qyy + qzz), 2.0f * (qxy + qwz), 2.0f * (qxz - qwy)),
-            mk(2.0f * (qxy - qwz), 1.0f - 2.0f * (qxx + qzz), 2.0f * (qyz + qwx)),
-            mk(2.0f * (qxz + qwy), 2.0f * (qyz - qwx), 1.0f - 2.0f * (qxx + qyy))};
+    const q4 q = quat_from_m3(M);
+    return shutter_rotation(q, q, 0.0f);
 }
 
 // ---- animation: cam_path.cuh:30-143, light.cuh:39-49, virtual_object.cuh:53-64 ----
@@ -375,6 +346,9 @@ const std::map<std::string, double>& default_params() {
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"rt_plist", 1},                        // per-pixel hit-record lists for the colour replay (rt_accumulate_kernel)
+        {"glow_mode", 0},                       // Testbed::Nerf::glow_mode (testbed.h:871): bits 1 green grid, 2 cut line, 4 mask to alpha,
+                                                // 8 radial, 16 grid mode -- instant-NGP path only (testbed_nerf.cu:638-734)
+        {"glow_y_cutoff", 0},                   // Testbed::Nerf::glow_y_cutoff (testbed.h:870)
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
@@ -427,6 +401,11 @@ struct sng_ctx {
 
     // camera (Testbed)
     float cam[12] = {1, 0, 0, 0, -1, 0, 0, 0, -1, 0.5f, 0.5f, 2.0f};
+    // View::camera1 / rolling_shutter (testbed.h:1032,1042; Engine: camera1 = camera0 unless a camera
+    // path renders with a shutter, testbed.cu:2849-2850): sng_set_motion_blur
+    bool has_cam1 = false;
+    float cam1[12] = {};
+    float rolling_shutter[4] = {0.0f, 0.0f, 0.0f, 1.0f};
     float m_scale = 1.5f;
     // animation state (Engine::m_camera_path, m_anim_speed / m_enable_animations, per light / object)
     CamPathState campath;
@@ -1048,8 +1027,18 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     NerfFrameArgs a{};
     a.vol = vol;
     a.cam = cam;
-    m3 rot = {cam.c0, cam.c1, cam.c2};
-    a.ray_rot = rolling_shutter_rotation(rot);
+    // get_xform_given_rolling_shutter({camera0, camera1}, rolling_shutter, uv, motionblur_time) per pixel
+    // (testbed_nerf.cu:1895): the quats of both cameras here, slerp / lerp in init_rays_kernel
+    a.q0 = quat_from_m3({cam.c0, cam.c1, cam.c2});
+    if (c->has_cam1) {
+        const float* m = c->cam1;
+        a.q1 = quat_from_m3({mk(m[0], m[1], m[2]), mk(m[3], m[4], m[5]), mk(m[6], m[7], m[8])});
+        a.pos1 = mk(m[9], m[10], m[11]);
+    } else {
+        a.q1 = a.q0;
+        a.pos1 = cam.c3;
+    }
+    for (int k = 0; k < 4; ++k) a.rolling_shutter[k] = c->rolling_shutter[k];
     const int nres[2] = {NW, NH};
     a.focal = focal_for(c, nres);
     a.screen_center = sc;
@@ -1093,7 +1082,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     bool fuse = false;
     uint32_t fuse_after = 0;
     // Normals / EncodingVis rewrite the network input between the network and the compositor: wavefront only
-    const bool probe = mode.ngp && (mode.render_mode == 2 || mode.render_mode == 10);
+    // (and the glow visualisation is a compositor-only term)
+    const bool probe = mode.ngp && (mode.render_mode == 2 || mode.render_mode == 10 || mode.glow_mode != 0);
     if (c->p("nerf_fused") != 0.0 && !probe) {
         HIPCHK(hipMemcpyAsync(c->h_alive, sched_src, 4, hipMemcpyDeviceToHost, c->s_nerf));
         HIPCHK(hipStreamSynchronize(c->s_nerf));
@@ -1762,7 +1752,7 @@ void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* o
     const Volume vol = make_volume(c);
     const CamDev cam = cam_dev(c);
     const f2 sc = render_screen_center(c);
-    const TraceMode mode{1, rm, (float)c->p("depth_scale")};
+    const TraceMode mode{1, rm, (float)c->p("depth_scale"), (int)c->p("glow_mode"), (float)c->p("glow_y_cutoff")};
     HIPCHK(hipEventRecord(c->ev_start, c->s_nerf));
     HIPCHK(hipEventRecord(c->ev_nerf0, c->s_nerf));
     const uint32_t net_launches = trace_nerf(c, P, vol, cam, sc, r0, r1, r0, r1, mode, target, [](int) {});
@@ -2376,6 +2366,14 @@ int sng_set_camera_view(sng_ctx* c, const float v[3], const float at[3], float s
     });
 }
 int sng_set_camera_matrix(sng_ctx* c, const float m[12]) { return guarded([&] { std::memcpy(c->cam, m, 48); c->mesh_reset = true; }); }
+int sng_set_motion_blur(sng_ctx* c, const float camera1[12], const float rolling_shutter[4]) {
+    return guarded([&] {
+        c->has_cam1 = camera1 != nullptr;
+        if (camera1) std::memcpy(c->cam1, camera1, 48);
+        const float rs0[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+        std::memcpy(c->rolling_shutter, rolling_shutter ? rolling_shutter : rs0, 16);
+    });
+}
 int sng_get_camera_matrix(sng_ctx* c, float m[12]) { return guarded([&] { std::memcpy(m, c->cam, 48); }); }
 int sng_set_fov(sng_ctx* c, float deg) { return guarded([&] { c->rel_focal[0] = c->rel_focal[1] = fov_to_focal(deg); c->mesh_reset = true; }); }
 int sng_get_focal_length(sng_ctx* c, int which, float out[2]) {

@@ -90,9 +90,13 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
         idx = (uint32_t)x + (uint32_t)a.W * (uint32_t)y;
         f2 off = ld_random_pixel_offset(a.snap ? 0u : a.spp);
         f2 uv = {((float)x + off.x) / (float)a.W, ((float)y + off.y) / (float)a.H};
+        // get_xform_given_rolling_shutter (testbed_nerf.cu:1895, common_device.cuh:361-368)
+        const float* rs = a.rolling_shutter;
+        const float pixel_t = rs[0] + rs[1] * uv.x + rs[2] * uv.y + rs[3] * ld_random_val0(a.spp, idx * 72239731u);
+        origin = a.cam.c3 + (a.pos1 - a.cam.c3) * pixel_t;
         // uv_to_ray (common_device.cuh:403-470): pinhole, no lens/foveation/parallax/aperture
         f3 d = mk((uv.x - a.screen_center.x) * (float)a.W / a.focal.x, (uv.y - a.screen_center.y) * (float)a.H / a.focal.y, 1.0f);
-        d = mul(a.ray_rot, d);
+        d = mul(shutter_rotation(a.q0, a.q1, pixel_t), d);
         float4 fb = frame_rgba[idx];
         fb.x = 0.0f; fb.y = 0.0f; fb.z = 0.0f;
         if (a.reset) fb.w = 0.0f;
@@ -233,6 +237,51 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
 // composite_kernel_nerf_alt (476-575) + compaction into the next buffer
 // (compact_kernel_nerf 1830-1853) + extract_from_payload (1578-1612)
 // ---------------------------------------------------------------------------
+// composite_kernel_nerf's glow visualisation (testbed_nerf.cu:638-734): green grid lines / cut line
+// below glow_y_cutoff; adds to rgb (grid_mode replaces it) and may scale the sample weight
+__device__ __forceinline__ void glow_term(int glow_mode, float glow_y_cutoff, f3 pos, f3 cam_pos, f3& rgb, float& weight) {
+    float glow = 0.f;
+    const bool green_grid = glow_mode & 1, green_cutline = glow_mode & 2, mask_to_alpha = glow_mode & 4;
+    const bool radial_mode = glow_mode & 8, grid_mode = glow_mode & 16;
+    float dist;
+    if (radial_mode) {
+        dist = length(pos - cam_pos);
+        dist = fminf(dist, (4.5f - pos.y) * 0.333f);
+    } else {
+        dist = pos.y;
+    }
+    if (grid_mode) {
+        glow = 1.f / fmaxf(1.f, dist);
+    } else {
+        float y = glow_y_cutoff - dist;
+        float mask = 0.f;
+        if (y > 0.f) {
+            y *= 80.f;
+            mask = fminf(1.f, y);
+            if (green_cutline) glow += fmaxf(0.f, 1.f - fabsf(1.f - y)) * 4.f;
+            if (y > 1.f) y = 1.f - (y - 1.f) * 0.05f;
+            if (green_grid) glow += fmaxf(0.f, y / fmaxf(1.f, dist));
+        }
+        if (mask_to_alpha) weight *= mask;
+    }
+    if (glow > 0.f) {
+        float line = 0.f;
+        for (int q = 0; q < 4; ++q) {   // y, x, z lines at 2, 4, 8, 16 x 16 periods per unit
+            const float m = 2.f * (float)(1 << q);
+            line += fmaxf(0.f, cosf(pos.y * m * 3.141592653589793f * 16.f) - 0.975f);
+            line += fmaxf(0.f, cosf(pos.x * m * 3.141592653589793f * 16.f) - 0.975f);
+            line += fmaxf(0.f, cosf(pos.z * m * 3.141592653589793f * 16.f) - 0.975f);
+        }
+        if (grid_mode) {
+            glow = glow * line * 15.f;
+            rgb.y = glow; rgb.z = glow * 0.5f; rgb.x = glow * 0.25f;
+        } else {
+            glow = glow * glow * 0.25f + glow * line * 15.f;
+            rgb.y += glow; rgb.z += glow * 0.5f; rgb.x += glow * 0.25f;
+        }
+    }
+}
+
 template <int THREADS>
 __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev cam, TraceMode mode, Sched sched, RayBuf in, RayBuf out, MarchCtrl* ctrl, int p,
                                                         uint32_t target, uint32_t iter, const float* __restrict__ coords, const uint2* __restrict__ samp,
@@ -300,8 +349,9 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
                 const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y & 0xffffu));
                 const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
                 const float alpha = 1.f - sng_expf(-sng_expf(s) * dt);
-                const float weight = alpha * T;
+                float weight = alpha * T;
                 f3 rgb = mk(logistic(r), logistic(g), logistic(b));
+                if (mode.ngp && mode.glow_mode) glow_term(mode.glow_mode, mode.glow_y_cutoff, pos, cam.c3, rgb, weight);
                 if (mode.ngp) {   // composite_kernel_nerf render modes (testbed_nerf.cu:709-723)
                     if (mode.render_mode == 2) {   // network_to_density_derivative (Exponential) x the density gradient
                         const float dd = sng_expf(fminf(fmaxf(s, -15.0f), 15.0f));

@@ -77,6 +77,8 @@ struct TraceMode {
     int ngp;
     int render_mode;     // ERenderMode: 0 AO, 1 Shade, 3 Positions, 4 Depth, 6 Cost, 10 EncodingVis
     float depth_scale;   // 1 / dataset.scale
+    int glow_mode;       // Testbed::Nerf::glow_mode / glow_y_cutoff (testbed.h:870-871), instant-NGP path only
+    float glow_y_cutoff;
 };
 
 struct CamDev {
@@ -95,7 +97,9 @@ struct Sched {
 struct NerfFrameArgs {
     Volume vol;
     CamDev cam;          // camera0 (composite/extract)
-    m3 ray_rot;          // rotation after the rolling-shutter quat round trip (common_device.cuh:361-368)
+    q4 q0, q1;           // quat_cast of camera0 / camera1 (get_xform_given_rolling_shutter, common_device.cuh:361-368)
+    f3 pos1;             // camera1 position (camera0's: cam.c3)
+    float rolling_shutter[4];
     f2 focal;
     f2 screen_center;
     int W, H;            // full NeRF resolution (pixel indices are global)

@@ -125,6 +125,44 @@ SNG_HD f3 mul(const m3& m, f3 v) {
 }
 SNG_HD m3 mulm(const m3& a, const m3& b) { return {mul(a, b.c0), mul(a, b.c1), mul(a, b.c2)}; }
 
+// get_xform_given_rolling_shutter's rotation (common_device.cuh:361-368): glm-style quat_cast of
+// both cameras, slerp(q0, q1, t), normalize, to_mat3 [tcnn quat, unvendored: parity unpinned]
+struct q4 { float x, y, z, w; };
+SNG_HD q4 quat_from_m3(const m3& M) {
+    auto e = [&](int i, int j) { const f3& c = i == 0 ? M.c0 : (i == 1 ? M.c1 : M.c2); return j == 0 ? c.x : (j == 1 ? c.y : c.z); };
+    const float fx = e(0, 0) - e(1, 1) - e(2, 2), fy = e(1, 1) - e(0, 0) - e(2, 2), fz = e(2, 2) - e(0, 0) - e(1, 1), fw = e(0, 0) + e(1, 1) + e(2, 2);
+    int bi = 0;
+    float fb = fw;
+    if (fx > fb) { fb = fx; bi = 1; }
+    if (fy > fb) { fb = fy; bi = 2; }
+    if (fz > fb) { fb = fz; bi = 3; }
+    const float bv = sqrtf(fb + 1.0f) * 0.5f, mult = 0.25f / bv;
+    switch (bi) {
+        case 0: return {(e(1, 2) - e(2, 1)) * mult, (e(2, 0) - e(0, 2)) * mult, (e(0, 1) - e(1, 0)) * mult, bv};
+        case 1: return {bv, (e(0, 1) + e(1, 0)) * mult, (e(2, 0) + e(0, 2)) * mult, (e(1, 2) - e(2, 1)) * mult};
+        case 2: return {(e(0, 1) + e(1, 0)) * mult, bv, (e(1, 2) + e(2, 1)) * mult, (e(2, 0) - e(0, 2)) * mult};
+        default: return {(e(2, 0) + e(0, 2)) * mult, (e(1, 2) + e(2, 1)) * mult, bv, (e(0, 1) - e(1, 0)) * mult};
+    }
+}
+SNG_HD m3 shutter_rotation(q4 a, q4 b, float t) {
+    float cos_theta = a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+    if (cos_theta < 0.0f) { b = {-b.x, -b.y, -b.z, -b.w}; cos_theta = -cos_theta; }   // the short way round
+    q4 s;
+    if (cos_theta > 1.0f - 1.1920929e-7f) {   // mix(a, b, t)
+        s = {a.x * (1.0f - t) + b.x * t, a.y * (1.0f - t) + b.y * t, a.z * (1.0f - t) + b.z * t, a.w * (1.0f - t) + b.w * t};
+    } else {
+        const float angle = acosf(cos_theta), s0 = sinf((1.0f - t) * angle), s1 = sinf(t * angle), sa = sinf(angle);
+        s = {(s0 * a.x + s1 * b.x) / sa, (s0 * a.y + s1 * b.y) / sa, (s0 * a.z + s1 * b.z) / sa, (s0 * a.w + s1 * b.w) / sa};
+    }
+    const float len = sqrtf(s.x * s.x + s.y * s.y + s.z * s.z + s.w * s.w);
+    s = {s.x / len, s.y / len, s.z / len, s.w / len};
+    const float qxx = s.x * s.x, qyy = s.y * s.y, qzz = s.z * s.z, qxz = s.x * s.z, qxy = s.x * s.y, qyz = s.y * s.z;
+    const float qwx = s.w * s.x, qwy = s.w * s.y, qwz = s.w * s.z;
+    return {mk(1.0f - 2.0f * (qyy + qzz), 2.0f * (qxy + qwz), 2.0f * (qxz - qwy)),
+            mk(2.0f * (qxy - qwz), 1.0f - 2.0f * (qxx + qzz), 2.0f * (qyz + qwx)),
+            mk(2.0f * (qxz + qwy), 2.0f * (qyz - qwx), 1.0f - 2.0f * (qxx + qyy))};
+}
+
 // sRGB: common_device.cuh:35-70
 SNG_HD float srgb_to_linear(float s) { return s <= 0.04045f ? s / 12.92f : powf((s + 0.055f) / 1.055f, 2.4f); }
 SNG_HD float linear_to_srgb(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * powf(l, 0.41666f) - 0.055f; }

@@ -421,6 +421,65 @@ def test_instant_ngp_render_path_matches_oracle(render_mode, vis):
         tb.close()
 
 
+def _ngp_frame_vs_oracle(eng, tb, cfg, params, grid, min_exact=0.995, exact_schedule=True, **oracle_kw):
+    import oracle as O
+    r = eng.render_nerf(render_mode=1)
+    got = r.download("nerf_rgba")
+    res = eng.resolution()["nerf"]
+    cam = O.make_camera(tb.camera_matrix, tb.focal_length(0), res)
+    ref, rd, st = O.render_nerf_ngp(O.Model(cfg, params), O.volume_for(cfg, grid), cam, 1, 1.0, **oracle_kw)
+    if exact_schedule:
+        assert r.n_iterations == st.n_iterations
+        assert list(r.alive_per_iter) == list(st.alive_per_iter)[: st.n_iterations]
+        assert r.n_samples == st.n_samples
+    else:   # transcendental ulps (acos / sin of the slerp) may move a ray across an occupancy boundary
+        assert abs(int(r.n_samples) - int(st.n_samples)) <= 1e-3 * st.n_samples
+    err = np.abs(got - ref).max(axis=-1)
+    assert (err <= 2e-3).mean() >= min_exact, f"max err {err.max()}, within: {(err <= 2e-3).mean()}"
+    return got, ref
+
+
+@pytest.mark.parametrize("glow_mode,cutoff", [(1, 0.5), (2, 0.55), (7, 0.5), (9, 0.6), (16, 0.5), (15, 0.45)])
+def test_instant_ngp_glow_matches_oracle(glow_mode, cutoff):
+    """composite_kernel_nerf's glow visualisation (testbed_nerf.cu:638-734): green grid, cut line,
+    mask to alpha, radial distance and grid mode, vs the oracle (cosf of the grid lines: ulp-level differences)."""
+    tb, eng, (cfg, params, grid) = _engine(128, 72, {"show_virtual_obj": 0, "shadow_on_nerf": 0})
+    try:
+        base = eng.render_nerf(render_mode=1).download("nerf_rgba")
+        eng.set_param("glow_mode", glow_mode)
+        eng.set_param("glow_y_cutoff", cutoff)
+        got, _ = _ngp_frame_vs_oracle(eng, tb, cfg, params, grid, glow_mode=glow_mode, glow_y_cutoff=cutoff)
+        assert np.abs(got - base).max() > 0.05   # the glow changed the frame
+    finally:
+        eng.set_param("glow_mode", 0)
+        tb.close()
+
+
+@pytest.mark.parametrize("rolling_shutter", [None, (0.1, 0.3, 0.2, 0.4)])
+def test_motion_blur_camera1_matches_oracle(rolling_shutter):
+    """View::camera1 + rolling_shutter: every NeRF ray's camera is get_xform_given_rolling_shutter({camera0,
+    camera1}, rolling_shutter, uv, ld_random_val(spp, idx * 72239731)) (testbed_nerf.cu:1895) -- position lerp,
+    quat slerp (acos / sin branch for a 3-degree turn). The default (camera1 = camera0) runs in every frame test."""
+    import oracle as O
+    tb, eng, (cfg, params, grid) = _engine(128, 72, {"show_virtual_obj": 0, "shadow_on_nerf": 0})
+    try:
+        base = eng.render_nerf(render_mode=1).download("nerf_rgba")
+        m = np.asarray(tb.camera_matrix, np.float32).reshape(4, 3)
+        a = np.deg2rad(3.0)
+        R = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]], np.float32)
+        m1 = m.copy()
+        m1[:3] = (R @ m[:3].T).T
+        m1[3] += np.float32([0.02, -0.01, 0.0])
+        tb.set_motion_blur(m1, rolling_shutter)
+        with O.motion_blur(m1, rolling_shutter):
+            got, _ = _ngp_frame_vs_oracle(eng, tb, cfg, params, grid, min_exact=0.99, exact_schedule=False)
+        assert np.abs(got - base).max() > 0.05   # the shutter moved the rays
+        tb.set_motion_blur(None, None)
+        assert np.array_equal(eng.render_nerf(render_mode=1).download("nerf_rgba"), base)
+    finally:
+        tb.close()
+
+
 def test_instant_ngp_rejects_unsupported_modes():
     from synerfgine_amd import SngError
     tb, eng, _ = _engine(32, 18, {"show_virtual_obj": 0})
