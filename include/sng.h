@@ -150,6 +150,9 @@ int sng_nerf_inference(sng_ctx* ctx, const float* d_coords, uint32_t stride_floa
                        uint16_t* d_out, int32_t out_layout, void* hip_stream);
 /* pos encoding only (tcnn GridEncoding forward), out [n][L*F] fp16 -- parity hook */
 int sng_hashgrid_encode(sng_ctx* ctx, const float* d_coords, uint32_t stride_floats, uint32_t n, uint16_t* d_out, void* hip_stream);
+/* NerfNetwork::m_dir_encoding->inference_mixed_precision (nerf_network.h:84,122-127): SphericalHarmonics
+ * degree 4 of the direction at d_coords[i * stride + dir_offset .. +2] (warped to [0,1]^3), d_out [n][16] fp16 */
+int sng_sh_encode(sng_ctx* ctx, const float* d_coords, uint32_t stride_floats, uint32_t dir_offset, uint32_t n, uint16_t* d_out, void* hip_stream);
 
 /* ---- virtual scene: Engine::set_virtual_world + Engine::init keys (engine.cu:21-78, 129-234) */
 int sng_load_virtual_scene(sng_ctx* ctx, const char* json_path);

@@ -124,6 +124,10 @@ class Testbed:
         check(self._lib.sng_hashgrid_encode(self.ctx, ctypes.c_void_p(d_coords), stride_floats, n, ctypes.c_void_p(d_out),
                                             ctypes.c_void_p(stream)))
 
+    def sh_encode(self, d_coords, stride_floats, dir_offset, n, d_out, stream=0):
+        check(self._lib.sng_sh_encode(self.ctx, ctypes.c_void_p(d_coords), stride_floats, dir_offset, n, ctypes.c_void_p(d_out),
+                                      ctypes.c_void_p(stream)))
+
     # ---- camera (testbed.cu:405-425) ---------------------------------------------
     def set_camera_view(self, view_dir, look_at, scale):
         v = np.asarray(view_dir, np.float32)

@@ -162,6 +162,7 @@ SIGNATURES = {
     "sng_get_density_mean": (ctypes.c_int, [P, FP]),
     "sng_nerf_inference": (ctypes.c_int, [P, P, U32, U32, P, I32, P]),
     "sng_hashgrid_encode": (ctypes.c_int, [P, P, U32, U32, P, P]),
+    "sng_sh_encode": (ctypes.c_int, [P, P, U32, U32, U32, P, P]),
     "sng_load_virtual_scene": (ctypes.c_int, [P, ctypes.c_char_p]),
     "sng_clear_virtual_scene": (ctypes.c_int, [P]),
     "sng_set_param": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.c_double]),

@@ -2269,6 +2269,15 @@ int sng_hashgrid_encode(sng_ctx* c, const float* coords, uint32_t stride, uint32
     });
 }
 
+int sng_sh_encode(sng_ctx* c, const float* coords, uint32_t stride, uint32_t dir_offset, uint32_t n, uint16_t* out, void* stream) {
+    return guarded([&] {
+        if (stride < dir_offset + 3) throw SngError(SNG_ERR_INVALID, "stride must cover dir_offset + 3 floats");
+        HIPCHK(hipSetDevice(c->device));
+        launch_sh_encode(coords, stride, dir_offset, n, out, (hipStream_t)stream);
+        HIPCHK(hipGetLastError());
+    });
+}
+
 int sng_load_virtual_scene(sng_ctx* c, const char* path) { return guarded([&] { load_scene(c, path); }); }
 int sng_clear_virtual_scene(sng_ctx* c) {
     return guarded([&] {

@@ -110,6 +110,26 @@ __global__ __launch_bounds__(256) void hashgrid_encode_kernel(const float* __res
     *reinterpret_cast<h8*>(out + (size_t)s * 32 + g * 8) = e;   // 16-B store of the lane's 8 features
 }
 
+// Standalone direction encoding (parity hook): out [n][16] fp16, the SH degree-4 rows the network
+// feeds its rgb MLP (sh_lane, one lane per 4 coefficients as in field_tile)
+__global__ __launch_bounds__(256) void sh_encode_kernel(const float* __restrict__ coords, uint32_t stride, uint32_t dir_offset, uint32_t n,
+                                                        uint16_t* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t s = t >> 2;
+    const int g = t & 3;
+    if (s >= n) return;
+    const float* d = coords + (size_t)s * stride + dir_offset;
+    float sh[4];
+    sh_lane(g, d[0], d[1], d[2], sh);
+    _Float16 h[4] = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3]};
+    *reinterpret_cast<uint2*>(out + (size_t)s * 16 + g * 4) = *reinterpret_cast<const uint2*>(h);   // 8-B store
+}
+
+void launch_sh_encode(const float* coords, uint32_t stride, uint32_t dir_offset, uint32_t n, uint16_t* out, hipStream_t stream) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(sh_encode_kernel, dim3((uint32_t)(((uint64_t)n * 4 + 255) / 256)), dim3(256), 0, stream, coords, stride, dir_offset, n, out);
+}
+
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
                    uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream) {
     uint32_t tiles = n_dev ? max_tiles_hint : (n_static + 15) / 16;

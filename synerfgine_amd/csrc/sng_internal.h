@@ -172,6 +172,7 @@ void launch_onestep_begin(const OnestepArgs& a, uint32_t k, uint32_t horizon, in
 void launch_onestep_pass(const OnestepArgs& a, const NetworkDev& net, int final_pass, uint32_t n_rays_hint, hipStream_t s);
 void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s);
 
+void launch_sh_encode(const float* coords, uint32_t stride, uint32_t dir_offset, uint32_t n, uint16_t* out, hipStream_t stream);
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
                    uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream);
 // Normals (mode 2) input gradient / EncodingVis (mode 10) activation, rewriting the samples' coordinates in place

@@ -97,6 +97,23 @@ def test_network_matches_oracle(tb, model, oracle_lib, n):
     assert not bad.any(), f"{bad.sum()} of {bad.size} outputs off; max err {np.abs(got - exp).max()}"
 
 
+@pytest.mark.parametrize("n", [1, 4099])
+def test_sh_encode_bit_exact(tb, oracle_lib, n):
+    """the direction encoding (SphericalHarmonics degree 4, nerf_network.h:84,122-127) that the fused
+    network feeds its rgb MLP, standalone through sng_sh_encode, vs the oracle's restatement: bit-exact fp16."""
+    c = _coords(n, seed=200 + n, edge=False)
+    c[: min(n, 6), 4:7] = np.float32([[0, 0, 0], [1, 1, 1], [0.5, 0.5, 0.5], [1, 0, 0.5], [0, 1, 0], [0.5, 0, 1]])[: min(n, 6)]
+    ref = np.zeros((n, 16), np.uint16)
+    oracle_lib.lib().orc_sh_encode(oracle_lib.ptr(c), 7, 4, n, oracle_lib.ptr(ref))
+    dc = torch.from_numpy(c).cuda()
+    out = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
+    tb.sh_encode(dc.data_ptr(), 7, 4, n, out.data_ptr())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint16)
+    bad = np.argwhere(got != ref)
+    assert len(bad) == 0, f"{len(bad)} mismatching coefficients, first {bad[:4].tolist()}"
+
+
 def test_network_tcnn_layout(tb, model, oracle_lib):
     n = 1024
     c = _coords(n, seed=7)
