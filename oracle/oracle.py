@@ -117,7 +117,7 @@ def lib():
             "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
             "orc_num_threads": (i32, []), "orc_set_num_threads": (None, [i32]), "orc_set_mlp_accum": (None, [i32, i32]),
             "orc_set_visualization": (None, [i32, i32]),
-            "orc_set_motion_blur": (None, [vp, vp]), "orc_set_glow": (None, [i32, f32]),
+            "orc_set_motion_blur": (None, [vp, vp]), "orc_set_glow": (None, [i32, f32]), "orc_set_shadow_rng_mode": (None, [i32]),
             "orc_set_gbuffer_out": (None, [vp, vp]),
             "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
             "orc_display": (None, [vp, i32, i32, i32, i32, vp, vp]),

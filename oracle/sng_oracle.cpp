@@ -1311,6 +1311,10 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
  * -> shadow_for_px (1614-1700).  The neighbourhood's light samples draw from the
  * centre pixel's own RNG stream (the reference shares neighbour states racily,
  * SURVEY Appendix A.5); identical to the reference for kernel_size/2 == 0. */
+/* 1: shadow_for_px's light samples advance the NEIGHBOUR's XORWOW state, as the reference's rand_state[idx]
+ * does (testbed_nerf.cu:1635,1649: idx is the neighbour's pixel), with the pixels serialised in index order --
+ * one race-free interleaving of what the reference's threads do concurrently (orc_set_shadow_rng_mode) */
+static int g_shadow_rng_neighbour = 0;
 void orc_shade_nerf_shadows(const orc_volume* vdesc, const int32_t res[2], float* frame_rgba, const float* positions, const float* normals,
                             const orc_object* objd, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
                             uint32_t* rng, float nerf_shadow_intensity, float thr, int32_t kernel_size) {
@@ -1320,17 +1324,19 @@ void orc_shade_nerf_shadows(const orc_volume* vdesc, const int32_t res[2], float
     const int W = res[0], H = res[1];
     const int r = kernel_size / 2;
     const uint32_t n_steps = MAX_STEPS_INBETWEEN_COMPACTION;
-#pragma omp parallel for schedule(dynamic, 64)
+    const int neighbour_rng = g_shadow_rng_neighbour;
+#pragma omp parallel for schedule(dynamic, 64) if (!neighbour_rng)
     for (int64_t idx = 0; idx < (int64_t)W * H; ++idx) {
         int x = (int)(idx % W), y = (int)(idx / W);
         float sum = 0.0f;
         int blend = 0;
-        uint32_t* st = rng + 6 * idx;
+        uint32_t* const st_centre = rng + 6 * idx;
         for (int i = -r; i <= r; ++i)
             for (int j = -r; j <= r; ++j) {
                 int fx = x + i, fy = y + j;
                 if (fx < 0 || fy < 0 || fx >= W || fy >= H) continue;
                 size_t t = (size_t)fy * W + fx;
+                uint32_t* st = neighbour_rng ? rng + 6 * t : st_centre;
                 V3 pos = v3(positions[3 * t], positions[3 * t + 1], positions[3 * t + 2]);
                 V3 nrm = v3(normals[3 * t], normals[3 * t + 1], normals[3 * t + 2]);
                 float overall = 1.0f;
@@ -1671,6 +1677,7 @@ void orc_set_motion_blur(const float* camera1, const float* rolling_shutter) {
     const float rs0[4] = {0.0f, 0.0f, 0.0f, 1.0f};
     std::memcpy(g_rs, rolling_shutter ? rolling_shutter : rs0, sizeof(g_rs));
 }
+void orc_set_shadow_rng_mode(int32_t neighbour) { g_shadow_rng_neighbour = neighbour; }
 void orc_set_glow(int32_t mode, float y_cutoff) {
     g_glow_mode = mode;
     g_glow_y_cutoff = y_cutoff;

@@ -136,6 +136,9 @@ void orc_render_nerf(const orc_model* m, const orc_volume* v, const orc_camera* 
 void orc_set_motion_blur(const float* camera1, const float* rolling_shutter);
 /* Testbed::Nerf::glow_mode / glow_y_cutoff (testbed.h:870-871) for orc_render_nerf_ngp (testbed_nerf.cu:638-734) */
 void orc_set_glow(int32_t mode, float y_cutoff);
+/* shade_nerf_shadows' light-sample RNG for nerf_shadow_samples > 0: 0 = the centre pixel's stream (this
+ * library's kernels), 1 = the neighbour's stream as the reference's racy rand_state[idx] (serialised) */
+void orc_set_shadow_rng_mode(int32_t neighbour);
 void orc_render_nerf_ngp(const orc_model* m, const orc_volume* v, const orc_camera* c, int32_t render_mode, float depth_scale,
                          float* frame_rgba /* W*H*4 */, float* frame_depth /* W*H */, orc_nerf_stats* stats);
 void orc_shade_nerf_shadows(const orc_volume* v, const int32_t res[2],
