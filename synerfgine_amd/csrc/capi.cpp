@@ -1082,9 +1082,10 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     bool fuse = false;
     uint32_t fuse_after = 0;
     // Normals / EncodingVis rewrite the network input between the network and the compositor: wavefront only
-    // (and the glow visualisation is a compositor-only term)
-    const bool probe = mode.ngp && (mode.render_mode == 2 || mode.render_mode == 10 || mode.glow_mode != 0);
-    if (c->p("nerf_fused") != 0.0 && !probe) {
+    const bool probe = mode.ngp && (mode.render_mode == 2 || mode.render_mode == 10);
+    // the glow visualisation is a wavefront-compositor term as well (the fused tail does not carry it)
+    const bool wavefront_only = probe || (mode.ngp && mode.glow_mode != 0);
+    if (c->p("nerf_fused") != 0.0 && !wavefront_only) {
         HIPCHK(hipMemcpyAsync(c->h_alive, sched_src, 4, hipMemcpyDeviceToHost, c->s_nerf));
         HIPCHK(hipStreamSynchronize(c->s_nerf));
         fuse = (uint64_t)c->h_alive[0] * MAX_STEPS_BETWEEN_COMPACTION <= target;
@@ -1220,7 +1221,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // once the alive count (it only shrinks) allows 8 steps per iteration, the rest of the march is
             // ray-local: hand it to the fused tail (the count read here is a chunk old, so it bounds the
             // count at `iter` from above)
-            else if (!fuse && !probe && c->p("nerf_fused") != 0.0 && (uint64_t)std::max(h[0], h[1]) * MAX_STEPS_BETWEEN_COMPACTION <= target) {
+            else if (!fuse && !wavefront_only && c->p("nerf_fused") != 0.0 && (uint64_t)std::max(h[0], h[1]) * MAX_STEPS_BETWEEN_COMPACTION <= target) {
                 fuse = true;
                 fuse_after = iter;
             }
