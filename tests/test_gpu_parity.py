@@ -466,8 +466,10 @@ def test_instant_ngp_glow_matches_oracle(glow_mode, cutoff):
         r0 = eng.render_nerf(render_mode=1)
         base = r0.download("nerf_rgba")
         if cutoff is None:
+            # dist = min(distance to the camera, (4.5 - pos.y) / 3) (testbed_nerf.cu:670-672): the glow band sits
+            # just below the cutoff, so put it 0.1 above the smaller of the two at the frame's median depth
             d = r0.download("nerf_depth")[..., 0]
-            cutoff = float(np.median(d[d < 1e4])) + 0.1
+            cutoff = min(float(np.median(d[d < 1e4])), (4.5 - 0.5) * 0.333) + 0.1
         eng.set_param("glow_mode", glow_mode)
         eng.set_param("glow_y_cutoff", cutoff)
         got, _ = _ngp_frame_vs_oracle(eng, tb, cfg, params, grid, glow_mode=glow_mode, glow_y_cutoff=cutoff)
