@@ -404,7 +404,7 @@ def main():
                          "traffic": traffic, "traffic_source": prof["file"] if prof else None,
                          "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
                          "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches, "samples_in_launches": int(samples),
-                         "timing": "hipEvents around every launch on the NeRF stream over the timed region" +
+                         "timing": "HIP events recorded by each launch's own dispatch (hipExtLaunchKernelGGL start/stop events) on the NeRF stream over the timed region" +
                                    ("" if args.serial_streams else "; the kernel shares the GPU with the raytracer stream, so this is the "
                                     "contended duration (uncontended: --serial-streams)"),
                          "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / MFMA_F16_PEAK_TFLOPS, 4),

@@ -1195,13 +1195,14 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                             !fuse && c->p("nerf_gen_wide") != 0.0);
             if (P.collect_kernel_times) {
                 while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
-                HIPCHK(hipEventRecord(c->net_events[2 * net_launches], c->s_nerf));
             }
-            launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf);
+            // timing events recorded by the network kernel's own dispatch (hipExtLaunchKernelGGL)
+            launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf,
+                           P.collect_kernel_times ? c->net_events[2 * net_launches] : nullptr,
+                           P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr);
             if (probe)   // Normals / EncodingVis: input gradient or activation into the coordinates (testbed_nerf.cu:2363-2366)
                 launch_field_probe(c->net, c->d_params.as<uint16_t>(), c->coords.as<float>(), &ctrl->n_samples[p], mode.render_mode,
                                    (int)c->p("visualized_layer"), (int)c->p("visualized_dimension"), c->s_nerf);
-            if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->net_events[2 * net_launches + 1], c->s_nerf));
             HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));   // render_frame starts the raytracer after the head's network
             ++net_launches;
             launch_composite(vol, cam, mode, a.sched, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),

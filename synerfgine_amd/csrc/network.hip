@@ -19,6 +19,8 @@
 // The 20 weight fragments (20 KiB) are staged once per workgroup in LDS and read per layer with
 // conflict-free ds_read_b128 (72 VGPRs, 7 waves/SIMD); -DNET_W_REGS keeps them resident in 80 VGPRs
 // per wave instead (149 VGPRs, 3 waves/SIMD), measured 1.5-2 % slower per launch.
+#include <hip/hip_ext.h>
+
 #include "nerf_field.h"
 
 namespace sng {
@@ -131,7 +133,7 @@ void launch_sh_encode(const float* coords, uint32_t stride, uint32_t dir_offset,
 }
 
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
-                   uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream) {
+                   uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
     uint32_t tiles = n_dev ? max_tiles_hint : (n_static + 15) / 16;
     if (tiles == 0) return 0;
     // persistent-style grid: one occupancy's worth of waves (3/SIMD with register weights, 7/SIMD with
@@ -151,12 +153,18 @@ int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, 
 #endif
     const h8* w = reinterpret_cast<const h8*>(net.wfrag);
     const _Float16* gr = reinterpret_cast<const _Float16*>(net.grid);
+    auto go = [&](auto kernel) {
+        if (ev0 || ev1)
+            hipExtLaunchKernelGGL(kernel, dim3(blocks), dim3(256), 0, stream, ev0, ev1, 0u, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static);
+        else
+            hipLaunchKernelGGL(kernel, dim3(blocks), dim3(256), 0, stream, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static);
+    };
     if (net.F == 4) {
-        if (layout == 1) hipLaunchKernelGGL((nerf_network_kernel<4, 1>), dim3(blocks), dim3(256), 0, stream, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static);
-        else hipLaunchKernelGGL((nerf_network_kernel<4, 0>), dim3(blocks), dim3(256), 0, stream, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static);
+        if (layout == 1) go(nerf_network_kernel<4, 1>);
+        else go(nerf_network_kernel<4, 0>);
     } else {
-        if (layout == 1) hipLaunchKernelGGL((nerf_network_kernel<2, 1>), dim3(blocks), dim3(256), 0, stream, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static);
-        else hipLaunchKernelGGL((nerf_network_kernel<2, 0>), dim3(blocks), dim3(256), 0, stream, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static);
+        if (layout == 1) go(nerf_network_kernel<2, 1>);
+        else go(nerf_network_kernel<2, 0>);
     }
     return 0;
 }

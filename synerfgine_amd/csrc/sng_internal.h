@@ -173,8 +173,11 @@ void launch_onestep_pass(const OnestepArgs& a, const NetworkDev& net, int final_
 void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s);
 
 void launch_sh_encode(const float* coords, uint32_t stride, uint32_t dir_offset, uint32_t n, uint16_t* out, hipStream_t stream);
+// ev0 / ev1: optional timing events recorded by the kernel's own dispatch (hipExtLaunchKernelGGL), so
+// the measured interval is the kernel's execution, as rocprofv3 reports it
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
-                   uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream);
+                   uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream, hipEvent_t ev0 = nullptr,
+                   hipEvent_t ev1 = nullptr);
 // Normals (mode 2) input gradient / EncodingVis (mode 10) activation, rewriting the samples' coordinates in place
 void launch_field_probe(const NetworkDev& net, const uint16_t* mlp_params, float* coords, const uint32_t* n_dev, int mode, int layer, int dim,
                         hipStream_t stream);
