@@ -344,7 +344,9 @@ def main():
     total_samples = sum(s.n_samples for s in stats)          # march samples composited
     reused = sum(s.n_samples_reused for s in stats)         # of which taken from the boundary-sample cache
     evaluated = total_samples - reused                      # network evaluations (launches + fused tail)
-    tail_samples = evaluated - samples
+    spec_evals = sum(s.spec_evals for s in stats)           # speculative tail rounds: samples their network launches evaluated
+    spec_exec = sum(s.spec_exec for s in stats)             # ... of which composited (the rest: look-ahead past a ray's end)
+    tail_samples = evaluated - (samples - (spec_evals - spec_exec))
     ms_tail = sum(s.ms_fused_tail for s in stats)
     os_evals = sum(s.onestep_field_evals for s in stats)   # field evaluations inside the one-step regime's final pass
     ms_os = sum(s.ms_onestep for s in stats)
@@ -412,6 +414,10 @@ def main():
                                         "ms": round(ms_tail, 4), "achieved": round(tail_gbs, 1), "frac": round(tail_gbs / HBM_PEAK_GBS, 4),
                                         "timing": "hipEvents around the tail launch (it runs beside the raytracer on reserved CUs in the "
                                                   "concurrent schedule, so its duration is latency, not throughput)"},
+                         "spec_tail": {"kernels": "spec_generate (K iterations marched ahead per ray) + nerf_network_kernel + spec_composite "
+                                                  "(exact replay), per round", "rounds_per_frame": int(s0.spec_rounds),
+                                       "samples_evaluated": int(spec_evals), "samples_composited": int(spec_exec),
+                                       "lookahead_discarded_frac": round(1.0 - spec_exec / spec_evals, 4) if spec_evals else 0.0},
                          "onestep_regime": {"kernels": "nerf_onestep_kernel x2 + schedule (trace_alt while n_alive > target/2; ray-local, "
                                                        "periodic rays composited in a closed loop)", "field_evals": int(os_evals),
                                             "ms": round(ms_os, 4)},

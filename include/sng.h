@@ -100,7 +100,10 @@ typedef struct {
     uint32_t onestep_iterations;/* ... for this many iterations */
     float ms_onestep;           /* device time of the one-step regime's kernels (collect_kernel_times) */
     uint32_t onestep_field_evals; /* field evaluations of the regime's final pass (its samples are otherwise cached) */
-    uint32_t reserved2[6];
+    uint32_t spec_rounds;       /* speculative tail rounds enqueued (nerf_spec_rounds; 0: none) */
+    uint32_t spec_evals;        /* samples their network launches evaluated, incl. those past a ray's end */
+    uint32_t spec_exec;         /* ... of which composited (the rest is the rounds' discarded look-ahead) */
+    uint32_t reserved2[3];
 } sng_frame_result;
 
 typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;

@@ -86,7 +86,10 @@ class sng_frame_result(ctypes.Structure):
         ("onestep_iterations", ctypes.c_uint32),
         ("ms_onestep", ctypes.c_float),
         ("onestep_field_evals", ctypes.c_uint32),
-        ("reserved2", ctypes.c_uint32 * 6),
+        ("spec_rounds", ctypes.c_uint32),
+        ("spec_evals", ctypes.c_uint32),
+        ("spec_exec", ctypes.c_uint32),
+        ("reserved2", ctypes.c_uint32 * 3),
     ]
 
 

@@ -362,6 +362,10 @@ const std::map<std::string, double>& default_params() {
         {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
         {"nerf_fused_after", 1},                // ... after this many whole-GPU wavefront iterations (1: the one big
                                                 //   uncontended network launch, then the ray-local tail; measured best)
+        {"nerf_spec_rounds", 4},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
+        {"nerf_spec_budget", 1048576},          // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax))
+        {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
+        {"nerf_spec_rt_gate", 1},               // 1: the raytracer starts after the speculative rounds (they get the whole GPU)
         {"nerf_fused_lanes", 64},               // rays per wave in the fused kernel
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
         {"nerf_gen_wide", 0},                   // cascaded generate with 1024-thread workgroups while no fused tail runs
@@ -445,6 +449,8 @@ struct sng_ctx {
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf rt_hint;                        // sample-parallel path kernel: per-pixel hit-depth sums of the previous frame (u8)
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
+    DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
+    uint32_t spec_rounds = 0;              // rounds enqueued by the last trace
     DevBuf rt_counts;                      // rt_count frames: path / shadow kernel {queries, box tests, triangle tests}
     DevBuf rt_hits, rt_rays, rt_next_pos, rt_tail, rt_counters;   // staged path tracer
     bool fused_last = false;               // the last trace finished in the fused kernel
@@ -1168,6 +1174,44 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         if (c->os_ran && c->h_os->istep0 + c->h_os->J >= MARCH_ITER) break;
         if (fuse && iter >= fuse_after) {
             c->fused_work.ensure(16);
+            c->fused_last = true;
+            c->fused_k0 = iter;
+            // speculative tail rounds (nerf.hip): each marches every alive ray K iterations ahead, one
+            // whole-GPU network launch evaluates them, the compositor replays them exactly; the fused
+            // kernel below then finishes whatever is still alive
+            const uint32_t rounds = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds"));
+            c->spec_rounds = rounds;
+            launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), c->s_nerf);
+            if (rounds) {
+                c->spec_t.ensure(c->sample_cap * 4);
+                SpecArgs sa{};
+                sa.vol = vol; sa.cam = cam; sa.mode = mode; sa.ctrl = ctrl;
+                sa.budget = (uint32_t)std::min<double>((double)c->sample_cap, std::max(1.0, c->p("nerf_spec_budget")));
+                sa.kmax = (uint32_t)std::min<double>(SPEC_KMAX, std::max(1.0, c->p("nerf_spec_kmax")));
+                sa.coords = c->coords.as<float>(); sa.samp = c->samp.as<uint2>(); sa.tbuf = c->spec_t.as<float>();
+                sa.net_out = c->net_out.as<uint2>();
+                sa.frame_rgba = c->nerf_rgba.as<float4>(); sa.frame_depth = c->nerf_depth.as<float>(); sa.positions = c->nerf_pos.as<float>();
+                // rays alive after the head: at most the band's pixels (grid-stride over the device count)
+                const uint32_t sblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 4));
+                for (uint32_t r = 0; r < rounds; ++r) {
+                    sa.in = rb[p]; sa.out = rb[p ^ 1]; sa.p = p;
+                    launch_spec_generate(sa, sblocks, c->s_nerf);
+                    if (P.collect_kernel_times) {
+                        while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
+                    }
+                    launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf,
+                                   P.collect_kernel_times ? c->net_events[2 * net_launches] : nullptr,
+                                   P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr);
+                    ++net_launches;
+                    launch_spec_composite(sa, sblocks, c->s_nerf);
+                    p ^= 1;
+                }
+                HIPCHK(hipGetLastError());
+                if (c->p("nerf_spec_rt_gate") != 0.0) {   // the raytracer waits for the rounds, not for the head
+                    HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));
+                    on_chunk(-1);
+                }
+            }
             FusedArgs fa{};
             fa.vol = vol; fa.cam = cam; fa.mode = mode; fa.rays = rb[p]; fa.ctrl = ctrl; fa.p = p;
             fa.wfrag = c->net.wfrag; fa.grid_params = c->net.grid; fa.levels = c->net.levels;
@@ -1181,12 +1225,10 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             const bool beside_rt = iter <= (uint32_t)std::max(0.0, c->p("nerf_fused_after"));
             if (fb < 0) fb = (beside_rt && c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0) ? 2.0 * std::max(1.0, c->p("rt_reserved_cus")) : 0.0;
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused0, c->s_nerf));
-            launch_nerf_fused(fa, c->net, iter == 0 ? std::min(c->h_alive[0], n_band) : n_band, (uint32_t)fb, c->s_nerf);
+            launch_nerf_fused(fa, c->net, iter == 0 && !rounds ? std::min(c->h_alive[0], n_band) : n_band, (uint32_t)fb, c->s_nerf);
             HIPCHK(hipGetLastError());
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused1, c->s_nerf));
             HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
-            c->fused_last = true;
-            c->fused_k0 = iter;
             on_chunk(chunk + 1);
             break;
         }
@@ -1229,7 +1271,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         }
         HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
         ++chunk;
-        on_chunk(chunk);
+        // with speculative rounds next, the raytracer is started after them (on_chunk(-1) above)
+        if (!(fuse && iter >= fuse_after && c->p("nerf_spec_rounds") > 0 && c->p("nerf_spec_rt_gate") != 0.0)) on_chunk(chunk);
     }
     return net_launches;
 }
@@ -1249,6 +1292,9 @@ void march_stats(const sng_ctx* c, const sng_frame_params& P, sng_frame_result* 
         out->onestep_field_evals = (uint32_t)c->h_os->evals[1];
     }
     out->n_reference_slots = ref_slots_of(c);
+    out->spec_rounds = c->fused_last ? c->spec_rounds : 0u;
+    out->spec_evals = (uint32_t)c->h_ctrl->spec_evals;
+    out->spec_exec = (uint32_t)c->h_ctrl->spec_exec;
     std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
     std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
     std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
@@ -1469,7 +1515,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         TraceMode mode{0, 1, 1.0f};
         net_launches = trace_nerf(c, P, vol, cam, sc, tr0, tr1, own0, own1, mode, target, [&](int chunk) {
             // gated on the last network launch of the head (ev_rt_go, trace_nerf), not the chunk's end
-            if (!rt_enqueued && chunk == rt_start_chunk) enqueue_raytracer(c->ev_rt_go, 2);
+            if (!rt_enqueued && (chunk == rt_start_chunk || (chunk < 0 && rt_start_chunk > 0))) enqueue_raytracer(c->ev_rt_go, 2);
         });
         launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
     }

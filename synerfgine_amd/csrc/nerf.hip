@@ -418,6 +418,312 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
     }
 }
 
+// ---------------------------------------------------------------------------
+// Speculative tail rounds (SpecArgs, sng_internal.h)
+// ---------------------------------------------------------------------------
+// Once n_alive * 8 <= target, every later iteration of trace_alt / trace takes exactly 8 steps
+// (testbed_nerf.cu:2189-2190).  A ray that survives an iteration starts the next one at
+// t = depth(last sample) / dot(fwd, dir) (composite_kernel_nerf_alt:574; trace keeps generate's t,
+// 836), and generate_next_nerf_network_inputs advances from there through occupancy alone (821-835):
+// the positions of a ray's next K iterations do not depend on any network output.  Only the
+// termination test (A > 1 - min_transmittance, 561) and the end of the march (cnt < n_steps, 567) do.
+//   spec_generate : each lane marches its ray K iterations ahead (K * 8 samples, the t reset applied
+//                   between iterations with the compositor's float expressions), writes every sample's t
+//                   to tbuf and the samples that are not an iteration's cached boundary sample as
+//                   NerfCoordinates for ONE whole-GPU network launch;
+//   network       : nerf_network_kernel over the round's samples;
+//   spec_composite: replays the K iterations in order with composite_kernel's arithmetic, stops the ray
+//                   where the wavefront would (extract / shade, or the MARCH_ITER drop) and appends the
+//                   survivors with their boundary-sample cache.  Samples past a ray's end are discarded.
+// K = clamp(budget / (8 n_alive), 1, kmax) from the device alive count bounds the discarded work.
+
+// composite_kernel's per-sample step (476-565 / 577-742) on a sample at march distance ts
+__device__ __forceinline__ bool spec_composite_sample(const Volume& vol, const CamDev& cam, const TraceMode& mode, f3 o, f3 d, f3 diag, float ts, uint2 raw,
+                                                      float4& rgba, float& depth, float& mw) {
+    const f3 wp = ((o + d * ts) - vol.train_aabb.lo) / diag;   // generate_kernel's coordinate
+    const f3 pos = vol.train_aabb.lo + wp * diag;
+    const float dt = unwarp_dt(warp_dt(calc_dt(ts, vol.ss)));
+    const float T = 1.f - rgba.w;
+    const float r = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x & 0xffffu));
+    const float g = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x >> 16));
+    const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y & 0xffffu));
+    const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
+    const float alpha = 1.f - sng_expf(-sng_expf(s) * dt);
+    const float weight = alpha * T;
+    f3 rgb = mk(logistic(r), logistic(g), logistic(b));
+    if (mode.ngp) {
+        if (mode.render_mode == 3) rgb = (pos - 0.5f) / 2.0f + 0.5f;
+        else if (mode.render_mode == 4) rgb = splat(dot(cam.c2, pos - o) * mode.depth_scale);
+        else if (mode.render_mode == 0) rgb = splat(alpha);
+    }
+    rgba.x += rgb.x * weight;
+    rgba.y += rgb.y * weight;
+    rgba.z += rgb.z * weight;
+    rgba.w += weight;
+    if (mode.ngp) {
+        if (weight > mw) { mw = weight; depth = dot(cam.c2, pos - cam.c3); }
+    } else {
+        depth = dot(cam.c2, pos - cam.c3);
+    }
+    if (rgba.w > (1.0f - vol.min_transmittance)) {
+        const float aa = rgba.w;
+        rgba.x /= aa; rgba.y /= aa; rgba.z /= aa; rgba.w /= aa;
+        return true;
+    }
+    return false;
+}
+
+template <bool LIN, int THREADS = 256>
+__global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
+    MarchCtrl* ctrl = a.ctrl;
+    const int p = a.p;
+    const uint32_t n_alive = ctrl->n_alive[p];
+    const uint32_t istep0 = ctrl->i_step[p];
+    uint32_t K = 0;
+    if (n_alive > 0 && istep0 < MARCH_ITER) {
+        K = a.budget / (MAX_STEPS_BETWEEN_COMPACTION * n_alive);
+        K = K < 1u ? 1u : (K > a.kmax ? a.kmax : K);
+        const uint32_t left = (MARCH_ITER - istep0 + MAX_STEPS_BETWEEN_COMPACTION - 1) / MAX_STEPS_BETWEEN_COMPACTION;   // incl. the last
+        K = K < left ? K : left;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctrl->spec_K[p] = K;
+        ctrl->spec_k0[p] = ctrl->n_iter;
+        ctrl->n_alive[p ^ 1] = 0;
+        ctrl->i_step[p ^ 1] = istep0 + MAX_STEPS_BETWEEN_COMPACTION * K;
+    }
+    if (K == 0) return;
+    const Volume& vol = a.vol;
+    const int lane = threadIdx.x & 63;
+    const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
+    const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
+    const float qnan = __int_as_float(0x7fc00000);
+    __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
+    for (uint32_t blk = blockIdx.x * THREADS; blk < n_alive; blk += gridDim.x * THREADS) {
+        const uint32_t i = blk + threadIdx.x;
+        uint32_t tot = 0, nnet = 0, n_it = 0, cnt_last = 0, rbits = 0;
+        f3 o = splat(0.0f), d = splat(1.0f);
+        if (i < n_alive) {
+            const float4 ot = a.in.o_t[i], di = a.in.d_idx[i];
+            o = mk(ot.x, ot.y, ot.z);
+            d = mk(di.x, di.y, di.z);
+            const f3 idir = inv(d);
+            const float dfw = dot(a.cam.c2, d);
+            float t = ot.w;
+            float prev = a.mode.ngp ? qnan : a.in.lt[i].x;   // the previous iteration's last sample
+            for (uint32_t it = 0; it < K; ++it) {
+                uint32_t cnt = 0;
+                float first = qnan, tl = 0.0f;
+                if constexpr (LIN) {
+                    const f3 hs = half_sign(d);
+#pragma unroll 1
+                    while (cnt < MAX_STEPS_BETWEEN_COMPACTION) {   // generate_kernel's flattened loop
+                        const f3 pos = o + d * t;
+                        if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
+                        if (occupied_linear(pos, vol.occ_linear)) {
+                            a.tbuf[(size_t)(tot + cnt) * n_alive + i] = t;
+                            if (cnt == 0) first = t;
+                            tl = t;
+                            t += calc_dt(t, 0.0f);
+                            ++cnt;
+                        } else {
+                            t = dda_step_linear(t, pos, idir, hs);
+                        }
+                    }
+                } else {
+#pragma unroll 1
+                    while (cnt < MAX_STEPS_BETWEEN_COMPACTION) {
+                        if (occ_step(t, cone, o, d, idir, 0, vol.max_mip, vol)) {
+                            if (t >= MAX_DEPTH) break;
+                            a.tbuf[(size_t)(tot + cnt) * n_alive + i] = t;
+                            if (cnt == 0) first = t;
+                            tl = t;
+                            t += calc_dt(t, cone);
+                            ++cnt;
+                        }
+                    }
+                }
+                const uint32_t ru = (!a.mode.ngp && cnt > 0 && first == prev) ? 1u : 0u;
+                rbits |= ru << it;
+                tot += cnt;
+                nnet += cnt - ru;
+                ++n_it;
+                cnt_last = cnt;
+                if (cnt < MAX_STEPS_BETWEEN_COMPACTION) break;   // the ray ends in this iteration
+                prev = tl;
+                if (!a.mode.ngp) {   // the compositor's t reset (574) on the iteration's last sample
+                    const f3 wp = ((o + d * tl) - vol.train_aabb.lo) / wdiag;
+                    const f3 pos = vol.train_aabb.lo + wp * wdiag;
+                    t = dot(a.cam.c2, pos - a.cam.c3) / dfw;
+                }
+            }
+            // trace keeps generate's t (836): the survivors' next start
+            if (a.mode.ngp && n_it == K && cnt_last == MAX_STEPS_BETWEEN_COMPACTION) reinterpret_cast<float*>(a.in.o_t + i)[3] = t;
+        }
+        const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], nnet, nullptr, false, nullptr, false, sh_app, lane);
+        if (i < n_alive) {
+            a.samp[i] = make_uint2(base, n_it | (cnt_last << 5) | (rbits << 9));
+            const f3 wd = (d + 1.0f) * 0.5f;
+            uint32_t q = base;
+#pragma unroll 1
+            for (uint32_t s = 0; s < tot; ++s) {
+                if ((s & 7u) == 0 && ((rbits >> (s >> 3)) & 1u)) continue;   // cached boundary sample: no evaluation
+                const float ts = a.tbuf[(size_t)s * n_alive + i];
+                const f3 wp = ((o + d * ts) - vol.train_aabb.lo) / wdiag;
+                float* c = a.coords + (size_t)q * 7;
+                c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(calc_dt(ts, cone)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+                ++q;
+            }
+        }
+    }
+}
+
+template <int THREADS = 256>
+__global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
+    __shared__ uint32_t hist_alive[64], hist_samples[64];
+    __shared__ uint32_t blk_hit, blk_iter;
+    __shared__ unsigned long long blk_samples, blk_reused;
+    __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
+    MarchCtrl* ctrl = a.ctrl;
+    const int p = a.p;
+    const uint32_t n_alive = ctrl->n_alive[p];
+    const uint32_t K = ctrl->spec_K[p];
+    const uint32_t k0 = ctrl->spec_k0[p];
+    const uint32_t istep0 = ctrl->i_step[p];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (K) {
+            ctrl->net_samples += ctrl->n_samples[p];
+            ctrl->spec_evals += ctrl->n_samples[p];
+        }
+        ctrl->n_samples[p ^ 1] = 0;
+        ctrl->n_reused[p ^ 1] = 0;
+    }
+    if (K == 0) return;
+    if (threadIdx.x < 64) { hist_alive[threadIdx.x] = 0; hist_samples[threadIdx.x] = 0; }
+    if (threadIdx.x == 0) { blk_hit = 0; blk_iter = 0; blk_samples = 0; blk_reused = 0; }
+    __syncthreads();
+    const Volume& vol = a.vol;
+    const CamDev& cam = a.cam;
+    const TraceMode& mode = a.mode;
+    const int lane = threadIdx.x & 63;
+    const f3 diag = vol.train_aabb.hi - vol.train_aabb.lo;
+    uint32_t my_hits = 0, my_iter = 0;
+    unsigned long long my_samples = 0, my_reused = 0;
+    for (uint32_t blk = blockIdx.x * THREADS; blk < n_alive; blk += gridDim.x * THREADS) {
+        const uint32_t i = blk + threadIdx.x;
+        bool survive = false, hit = false;
+        float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
+        float depth = 0.0f, mw = 0.0f, lt = 0.0f;
+        uint2 lraw = make_uint2(0u, 0u);
+        uint32_t death_step = 0;
+        if (i < n_alive) {
+            rgba = a.in.rgba[i];
+            depth = a.in.depth[i];
+            ot = a.in.o_t[i];
+            di = a.in.d_idx[i];
+            if (mode.ngp) mw = a.in.mw[i];
+            else { lt = a.in.lt[i].x; lraw = a.in.lo[i]; }
+            const f3 o = mk(ot.x, ot.y, ot.z), d = mk(di.x, di.y, di.z);
+            const uint2 sc = a.samp[i];
+            const uint32_t n_it = sc.y & 31u, cnt_last = (sc.y >> 5) & 15u, rbits = sc.y >> 9;
+            uint32_t ob = sc.x, s = 0;
+            bool ended = false;
+            for (uint32_t it = 0; it < n_it && !ended; ++it) {
+                const uint32_t cnt = it + 1 == n_it ? cnt_last : MAX_STEPS_BETWEEN_COMPACTION;
+                const uint32_t ru = (rbits >> it) & 1u;
+                const uint32_t istep = istep0 + MAX_STEPS_BETWEEN_COMPACTION * it;
+                const bool last = istep + MAX_STEPS_BETWEEN_COMPACTION >= MARCH_ITER;
+                if (k0 + it < 64) {
+                    atomicAdd(&hist_alive[k0 + it], 1u);
+                    if (cnt) atomicAdd(&hist_samples[k0 + it], cnt);
+                }
+                my_samples += cnt;
+                my_reused += ru;
+                my_iter = max(my_iter, k0 + it + 1);
+                uint32_t j = 0;
+                uint2 last_raw = lraw;
+                float ts = 0.0f;
+                for (; j < cnt; ++j) {
+                    ts = a.tbuf[(size_t)(s + j) * n_alive + i];
+                    const uint2 raw = (ru && j == 0) ? lraw : a.net_out[ob++];
+                    last_raw = raw;
+                    if (spec_composite_sample(vol, cam, mode, o, d, diag, ts, raw, rgba, depth, mw)) break;
+                }
+                if (!mode.ngp) ot.w = depth / dot(cam.c2, d);   // payload.t reset (574)
+                if (j < MAX_STEPS_BETWEEN_COMPACTION) {
+                    hit = !last && rgba.w > 0.001f;
+                    death_step = j + istep;
+                    ended = true;
+                } else if (last) {
+                    ended = true;
+                } else {
+                    lt = ts;            // the boundary-sample cache of the next iteration
+                    lraw = last_raw;
+                    s += cnt;
+                }
+            }
+            survive = !ended;
+        }
+        const uint32_t slot = block_append<THREADS / 64>(&ctrl->n_alive[p ^ 1], survive ? 1u : 0u, nullptr, false, nullptr, false, sh_app, lane);
+        if (survive) {
+            a.out.o_t[slot] = ot;
+            a.out.d_idx[slot] = di;
+            a.out.rgba[slot] = rgba;
+            a.out.depth[slot] = depth;
+            if (mode.ngp) a.out.mw[slot] = mw;
+            else { a.out.lt[slot] = make_float2(lt, 0.0f); a.out.lo[slot] = lraw; }
+        }
+        if (hit) {
+            ++my_hits;
+            const uint32_t idx = __float_as_uint(di.w);
+            if (mode.ngp) {   // shade_kernel_nerf (1788-1828)
+                float4 tmp = rgba;
+                if (mode.render_mode == 6) { const float col = (float)death_step / 128; tmp = make_float4(col, col, col, 1.0f); }
+                if (mode.render_mode == 1) { tmp.x = srgb_to_linear(tmp.x); tmp.y = srgb_to_linear(tmp.y); tmp.z = srgb_to_linear(tmp.z); }
+                float4 fb = a.frame_rgba[idx];
+                fb = make_float4(tmp.x + fb.x * (1.0f - tmp.w), tmp.y + fb.y * (1.0f - tmp.w), tmp.z + fb.z * (1.0f - tmp.w), tmp.w + fb.w * (1.0f - tmp.w));
+                a.frame_rgba[idx] = fb;
+                if (tmp.w > 0.2f) a.frame_depth[idx] = depth;
+            } else {          // extract_from_payload (1578-1612)
+                const f3 dir = mk(di.x, di.y, di.z);
+                const f3 orig = cam.c3 + dir * ot.w;
+                float4 fb = a.frame_rgba[idx];
+                const float ta = rgba.w;
+                const float r = srgb_to_linear(rgba.x), g = srgb_to_linear(rgba.y), b = srgb_to_linear(rgba.z);
+                fb = make_float4(r + fb.x * (1.0f - ta), g + fb.y * (1.0f - ta), b + fb.z * (1.0f - ta), ta + fb.w * (1.0f - ta));
+                a.frame_rgba[idx] = fb;
+                a.positions[3 * idx + 0] = orig.x; a.positions[3 * idx + 1] = orig.y; a.positions[3 * idx + 2] = orig.z;
+                if (ta > 0.2f) a.frame_depth[idx] = depth;
+            }
+        }
+    }
+    // statistics (the wavefront's per-iteration histograms, hits, composited / reused samples)
+    atomicAdd(&blk_hit, my_hits);
+    atomicMax(&blk_iter, my_iter);
+    atomicAdd(&blk_samples, my_samples);
+    if (my_reused) atomicAdd(&blk_reused, my_reused);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        if (hist_alive[threadIdx.x]) atomicAdd(&ctrl->alive_hist[threadIdx.x], hist_alive[threadIdx.x]);
+        if (hist_samples[threadIdx.x]) atomicAdd(&ctrl->samples_hist[threadIdx.x], hist_samples[threadIdx.x]);
+    }
+    if (threadIdx.x == 0) {
+        if (blk_hit) atomicAdd(&ctrl->n_hit, blk_hit);
+        if (blk_iter) atomicMax(&ctrl->n_iter, blk_iter);
+        if (blk_samples) {
+            atomicAdd(&ctrl->total_samples, blk_samples);
+            atomicAdd(&ctrl->spec_exec, blk_samples - blk_reused);
+        }
+        if (blk_reused) atomicAdd(&ctrl->reused_samples, blk_reused);
+    }
+}
+
+// the tail's per-iteration statistics: iterations from n_iter on take 8 steps each
+__global__ void tail_prepare_kernel(MarchCtrl* ctrl, uint32_t* work) {
+    if (threadIdx.x < 64 && threadIdx.x >= ctrl->n_iter) ctrl->steps_hist[threadIdx.x] = MAX_STEPS_BETWEEN_COMPACTION;
+    if (threadIdx.x == 0 && work) *work = 0;
+}
+
 // write_normals_to_buffer (1523-1576) for rows [row0,row1)
 __global__ __launch_bounds__(256) void normals_kernel(int W, int H, int row0, int row1, const float* __restrict__ positions,
                                                       float* __restrict__ normals) {
@@ -525,6 +831,8 @@ __global__ void ctrl_init_kernel(MarchCtrl* c) {
         c->i_step[0] = 1; c->i_step[1] = 1;   // trace_alt: uint32_t i = 1 (2163)
         c->n_hit = 0; c->n_iter = 0;
         c->total_samples = 0; c->net_samples = 0; c->ref_slots = 0; c->reused_samples = 0;
+        c->spec_K[0] = 0; c->spec_K[1] = 0; c->spec_k0[0] = 0; c->spec_k0[1] = 0;
+        c->spec_evals = 0; c->spec_exec = 0;
     }
 }
 
@@ -556,6 +864,14 @@ void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode,
     if (wide) hipLaunchKernelGGL(composite_kernel<1024>, dim3(std::max(1u, blocks / 4u)), dim3(1024), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
     else hipLaunchKernelGGL(composite_kernel<256>, dim3(blocks), dim3(256), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
 }
+void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
+    if (a.vol.linear) hipLaunchKernelGGL(spec_generate_kernel<true>, dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(spec_generate_kernel<false>, dim3(blocks), dim3(256), 0, s, a);
+}
+void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL(spec_composite_kernel<256>, dim3(blocks), dim3(256), 0, s, a);
+}
+void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, hipStream_t s) { hipLaunchKernelGGL(tail_prepare_kernel, dim3(1), dim3(64), 0, s, ctrl, work); }
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
     if (!n) return;

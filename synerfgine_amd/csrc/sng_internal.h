@@ -49,6 +49,11 @@ struct MarchCtrl {
     uint32_t alive_hist[64];
     uint32_t steps_hist[64];
     uint32_t samples_hist[64];
+    // speculative tail rounds (nerf.hip spec_generate / spec_composite), per ping-pong buffer
+    uint32_t spec_K[2];       // iterations the round marched ahead
+    uint32_t spec_k0[2];      // iteration index of the round's first iteration
+    unsigned long long spec_evals;   // samples the rounds' network launches evaluated (incl. those past a ray's end)
+    unsigned long long spec_exec;    // ... of which composited
 };
 
 // Alive-ray SoA buffer (NerfPayload + rgba + depth, nerf_device.cuh:145-153; nerf.h:22-42)
@@ -260,6 +265,32 @@ struct RtQueue {
     __host__ __device__ float4* shadow_ray(uint32_t k, uint32_t jp) const { return srec + 2 * ((size_t)k * nps + jp); }
     __host__ __device__ size_t mask_at(uint32_t k, uint32_t jp) const { return (size_t)k * nps + jp; }
 };
+
+// nerf.hip: speculative tail rounds.  Once every iteration takes 8 steps a surviving ray's next
+// samples depend only on the march and the t reset, so a round marches each alive ray K iterations
+// ahead, ONE whole-GPU network launch evaluates them, and the compositor replays the iterations in
+// order, stopping each ray where the wavefront would (samples past that point are discarded).
+struct SpecArgs {
+    Volume vol;
+    CamDev cam;
+    TraceMode mode;
+    RayBuf in, out;               // alive rays (buffer p) -> survivors of the round (buffer p ^ 1)
+    MarchCtrl* ctrl;
+    int p;
+    uint32_t budget;              // samples one round may generate: K = clamp(budget / (8 n_alive), 1, kmax)
+    uint32_t kmax;                // <= SPEC_KMAX
+    float* coords;                // NerfCoordinate AoS of the network samples
+    uint2* samp;                  // per ray: {first network sample, n_it | cnt_last << 5 | reuse bits << 9}
+    float* tbuf;                  // [sample j of the ray][ray] march t of every sample (incl. reused boundary samples)
+    const uint2* net_out;         // [n][4] fp16
+    float4* frame_rgba;
+    float* frame_depth;
+    float* positions;
+};
+constexpr uint32_t SPEC_KMAX = 16;
+void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s);
+void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s);
+void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, hipStream_t s);
 
 // nerf.hip
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, hipStream_t s);

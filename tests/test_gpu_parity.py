@@ -538,6 +538,40 @@ def test_fused_nerf_kernel_equals_wavefront(config, ngp_mode):
         tb.close()
 
 
+@pytest.mark.parametrize("config,ngp_mode,spec", [
+    ("c3", None, {"nerf_spec_rounds": 0}),                                   # fused kernel only
+    ("c3", None, {"nerf_spec_rounds": 1, "nerf_spec_kmax": 2}),              # one short round, the fused kernel finishes
+    ("c3", None, {"nerf_spec_rounds": 8, "nerf_spec_kmax": 1}),              # one iteration per round
+    ("c3", None, {"nerf_spec_rounds": 3, "nerf_spec_budget": 4096}),         # K = 1 from the budget
+    ("c3", None, {"nerf_spec_rounds": 2, "nerf_spec_budget": 1 << 22}),      # K = 16: look-ahead past most rays' end
+    ("c3", 1, {"nerf_spec_rounds": 4}), ("c3", 6, {"nerf_spec_rounds": 4}), ("c3", 4, {"nerf_spec_rounds": 2, "nerf_spec_kmax": 3}),
+    ("c4", None, {"nerf_spec_rounds": 4}), ("c4", None, {"nerf_spec_rounds": 2, "nerf_spec_budget": 1 << 22}),
+])
+def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
+    """nerf.hip's speculative tail rounds (each alive ray marched K iterations ahead, one whole-GPU network
+    launch, the iterations replayed in order with the wavefront's termination) reproduce the per-iteration
+    wavefront bit for bit: frame buffers, sample / hit / iteration counts, reference slots and per-iteration
+    histograms, for every round / look-ahead shape, both tracers and the cascaded marcher."""
+    tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, config)
+    try:
+        out = {}
+        for fused in (0, 1):
+            eng.set_param("nerf_fused", fused)
+            for k, v in spec.items():
+                eng.set_param(k, v)
+            r = eng.frame() if ngp_mode is None else eng.render_nerf(render_mode=ngp_mode)
+            if fused and spec.get("nerf_spec_rounds", 0):
+                assert r.spec_rounds == spec["nerf_spec_rounds"] and r.spec_exec > 0 and r.spec_evals >= r.spec_exec
+            bufs = ["nerf_rgba", "nerf_depth"] + (["nerf_positions"] if ngp_mode is None else [])
+            out[fused] = ([r.download(b) for b in bufs], (r.n_samples, r.n_samples_reused, r.n_hit, r.n_iterations, r.n_reference_slots),
+                          list(r.alive_per_iter), list(r.steps_per_iter), list(r.samples_per_iter))
+        for a, b in zip(out[0][0], out[1][0]):
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert out[0][1:] == out[1][1:]
+    finally:
+        tb.close()
+
+
 @pytest.mark.parametrize("config,target", [("c3", 3000), ("c4", 100000)])
 def test_mid_frame_switch_to_fused_tail_is_exact(config, target):
     """With a small query target the march starts with short iterations and hands over to the fused tail in

@@ -1,0 +1,69 @@
+#!/bin/bash
+# tools/gpu.sh -- the one GPU-box runner (replaces the one-off tools/gpu_*.sh scripts of rounds 1-2).
+#
+# usage (inside gpurun):  TAG=name tools/gpu.sh STEP [STEP ...]
+# Steps run in order, each under its own time limit; the first failing step ends the call (no retries).
+#   test[:EXPR]            pytest -m gpu over tests/ (-k EXPR when given)
+#   bench[:CFG[:ARGS]]     bench.py --config CFG --no-cpu-baseline --no-sweep ARGS   (ARGS: ',' for spaces)
+#   driver                 bench.py with no flags (the driver's own line, incl. CPU baseline and extra legs)
+#   prof[:CFG[:ARGS]]      rocprofv3 --kernel-trace --stats of a short bench.py run (ARGS as for bench)
+#   pmc[:CFG[:ARGS]]       FETCH_SIZE / WRITE_SIZE / MFMA PMC passes (one rocprofv3 run each) + tools/pmc_summary.py
+#   py:SCRIPT[:ARGS]       python3 tools/SCRIPT ARGS
+# Output goes to gpurun_out/$TAG/ (TAG defaults to "run"), one log per step.
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${TAG:-run}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%:*}
+  rest=""
+  [[ "$step" == *:* ]] && rest=${step#*:}
+  cfg=${rest%%:*}
+  args=""
+  [[ "$rest" == *:* ]] && args=${rest#*:}
+  args=${args//,/ }
+  log=$OUT/$n.$kind.log
+  echo "[gpu.sh] step $n: $step -> $log"
+  case $kind in
+    test)
+      k=()
+      [ -n "$rest" ] && k=(-k "$rest")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread "${k[@]}" > $log 2>&1
+      rc=$?; tail -5 $log ;;
+    bench)
+      timeout -k 10 600 python3 -u bench.py --config ${cfg:-c3} --no-cpu-baseline --no-sweep $args > $log 2>&1
+      rc=$?; tail -c 3000 $log; echo ;;
+    driver)
+      timeout -k 10 900 python3 -u bench.py > $log 2>&1
+      rc=$?; tail -c 4000 $log; echo ;;
+    prof)
+      d=$OUT/prof$n
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- python3 bench.py --config ${cfg:-c3} --steps 10 --warmup 2 --no-cpu-baseline --no-sweep $args > $log 2>&1
+      rc=$?
+      [ $rc -eq 0 ] && python3 tools/kernel_table.py $(find $d -name "*kernel_trace.csv" | head -1) > $d/kernel_table.txt 2>&1 && head -30 $d/kernel_table.txt ;;
+    pmc)
+      d=$OUT/pmc$n
+      a="--config ${cfg:-c3} --steps 3 --warmup 1 --no-cpu-baseline --no-sweep $args"
+      rc=0
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 300 rocprofv3 --pmc $c -d $d/$c -o run --output-format csv -- python3 bench.py $a > $d.$c.log 2>&1
+        rc=$?; echo "$c rc=$rc"; [ $rc -ne 0 ] && break
+      done
+      if [ $rc -eq 0 ]; then
+        timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE -d $d/MFMA -o run --output-format csv -- python3 bench.py $a > $d.MFMA.log 2>&1
+        rc=$?; echo "MFMA rc=$rc"
+      fi
+      [ $rc -eq 0 ] && python3 tools/pmc_summary.py $d $OUT/pmc_traffic_${cfg:-c3}.json ${cfg:-c3} > $log 2>&1; rc=$? ;;
+    py)
+      timeout -k 10 600 python3 -u tools/$cfg $args > $log 2>&1
+      rc=$?; tail -c 3000 $log; echo ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+  echo "[gpu.sh] step $n rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0
