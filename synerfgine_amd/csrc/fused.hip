@@ -119,10 +119,11 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
             const f3 idir = inv(d);
             if constexpr (LIN) {
                 const f3 hs = half_sign(d);
+                OccCache oc;
                 while (cnt < n_steps) {
                     const f3 pos = o + d * t;
                     if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
-                    if (occupied_linear(pos, vol.occ_linear)) {
+                    if (occupied_linear_c(pos, vol.occ_linear, oc)) {
                         if (cnt == 0 && !a.mode.ngp && t == lt) reuse = true;
                         ts_lds[wv][cnt][lane] = t;
                         t += calc_dt(t, 0.0f);

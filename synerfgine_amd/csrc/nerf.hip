@@ -183,11 +183,12 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
                 // records a sample (occupied voxel) or takes one DDA step, so a lane's cost is its
                 // own total step count instead of the wave's worst walk summed over all 8 samples.
                 const f3 hs = half_sign(d);
+                OccCache oc;
 #pragma unroll 1
                 while (cnt < n_steps) {
                     const f3 pos = o + d * t;
                     if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
-                    if (occupied_linear(pos, vol.occ_linear)) {
+                    if (occupied_linear_c(pos, vol.occ_linear, oc)) {
                         if (cnt == 0 && t == lt0) reuse = true;
                         ts_lds[cnt * THREADS + threadIdx.x] = t;
                         tl = t;
@@ -473,8 +474,12 @@ __device__ __forceinline__ bool spec_composite_sample(const Volume& vol, const C
     return false;
 }
 
-template <bool LIN, int THREADS = 256>
-__global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
+// One wave per workgroup: a lane keeps all K * 8 sample t's of its ray in LDS (32 KiB per wave), so the
+// march loop issues no global stores (on gfx9-class counters a store would sit in front of every occupancy
+// load's wait); the t's and NerfCoordinates are written after the march.
+template <bool LIN>
+__global__ __launch_bounds__(64) void spec_generate_kernel(SpecArgs a) {
+    __shared__ float ts_lds[SPEC_KMAX * MAX_STEPS_BETWEEN_COMPACTION][64];
     MarchCtrl* ctrl = a.ctrl;
     const int p = a.p;
     const uint32_t n_alive = ctrl->n_alive[p];
@@ -494,15 +499,15 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
     }
     if (K == 0) return;
     const Volume& vol = a.vol;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
     const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
     const float qnan = __int_as_float(0x7fc00000);
-    __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
-    for (uint32_t blk = blockIdx.x * THREADS; blk < n_alive; blk += gridDim.x * THREADS) {
-        const uint32_t i = blk + threadIdx.x;
+    for (uint32_t blk = blockIdx.x * 64u; blk < n_alive; blk += gridDim.x * 64u) {
+        const uint32_t i = blk + lane;
         uint32_t tot = 0, nnet = 0, n_it = 0, cnt_last = 0, rbits = 0;
         f3 o = splat(0.0f), d = splat(1.0f);
+        float tl = 0.0f;
         if (i < n_alive) {
             const float4 ot = a.in.o_t[i], di = a.in.d_idx[i];
             o = mk(ot.x, ot.y, ot.z);
@@ -511,17 +516,18 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             const float dfw = dot(a.cam.c2, d);
             float t = ot.w;
             float prev = a.mode.ngp ? qnan : a.in.lt[i].x;   // the previous iteration's last sample
+            OccCache oc;
             for (uint32_t it = 0; it < K; ++it) {
                 uint32_t cnt = 0;
-                float first = qnan, tl = 0.0f;
+                float first = qnan;
                 if constexpr (LIN) {
                     const f3 hs = half_sign(d);
 #pragma unroll 1
                     while (cnt < MAX_STEPS_BETWEEN_COMPACTION) {   // generate_kernel's flattened loop
                         const f3 pos = o + d * t;
                         if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
-                        if (occupied_linear(pos, vol.occ_linear)) {
-                            a.tbuf[(size_t)(tot + cnt) * n_alive + i] = t;
+                        if (occupied_linear_c(pos, vol.occ_linear, oc)) {
+                            ts_lds[tot + cnt][lane] = t;
                             if (cnt == 0) first = t;
                             tl = t;
                             t += calc_dt(t, 0.0f);
@@ -535,7 +541,7 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
                     while (cnt < MAX_STEPS_BETWEEN_COMPACTION) {
                         if (occ_step(t, cone, o, d, idir, 0, vol.max_mip, vol)) {
                             if (t >= MAX_DEPTH) break;
-                            a.tbuf[(size_t)(tot + cnt) * n_alive + i] = t;
+                            ts_lds[tot + cnt][lane] = t;
                             if (cnt == 0) first = t;
                             tl = t;
                             t += calc_dt(t, cone);
@@ -560,15 +566,20 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             // trace keeps generate's t (836): the survivors' next start
             if (a.mode.ngp && n_it == K && cnt_last == MAX_STEPS_BETWEEN_COMPACTION) reinterpret_cast<float*>(a.in.o_t + i)[3] = t;
         }
-        const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], nnet, nullptr, false, nullptr, false, sh_app, lane);
+        // one atomic per wave for the round's network samples
+        const uint32_t incl = wave_incl_scan(nnet, lane);
+        uint32_t base = 0;
+        if (lane == 63 && incl) base = atomicAdd(&ctrl->n_samples[p], incl);
+        base = __shfl(base, 63, 64) + incl - nnet;
         if (i < n_alive) {
             a.samp[i] = make_uint2(base, n_it | (cnt_last << 5) | (rbits << 9));
             const f3 wd = (d + 1.0f) * 0.5f;
             uint32_t q = base;
 #pragma unroll 1
             for (uint32_t s = 0; s < tot; ++s) {
+                const float ts = ts_lds[s][lane];
+                a.tbuf[(size_t)s * n_alive + i] = ts;
                 if ((s & 7u) == 0 && ((rbits >> (s >> 3)) & 1u)) continue;   // cached boundary sample: no evaluation
-                const float ts = a.tbuf[(size_t)s * n_alive + i];
                 const f3 wp = ((o + d * ts) - vol.train_aabb.lo) / wdiag;
                 float* c = a.coords + (size_t)q * 7;
                 c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(calc_dt(ts, cone)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
@@ -640,14 +651,25 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                 my_samples += cnt;
                 my_reused += ru;
                 my_iter = max(my_iter, k0 + it + 1);
+                // the iteration's t's and outputs are loaded together, ahead of the compositing chain
+                float tv[MAX_STEPS_BETWEEN_COMPACTION];
+                uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
+#pragma unroll
+                for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
+                    if (q < cnt) {
+                        tv[q] = a.tbuf[(size_t)(s + q) * n_alive + i];
+                        rv[q] = (ru && q == 0) ? lraw : a.net_out[ob + q - ru];
+                    }
+                }
+                ob += cnt - ru;
                 uint32_t j = 0;
                 uint2 last_raw = lraw;
-                float ts = 0.0f;
-                for (; j < cnt; ++j) {
-                    ts = a.tbuf[(size_t)(s + j) * n_alive + i];
-                    const uint2 raw = (ru && j == 0) ? lraw : a.net_out[ob++];
-                    last_raw = raw;
-                    if (spec_composite_sample(vol, cam, mode, o, d, diag, ts, raw, rgba, depth, mw)) break;
+#pragma unroll
+                for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
+                    if (q >= cnt) break;
+                    last_raw = rv[q];
+                    j = q + 1;
+                    if (spec_composite_sample(vol, cam, mode, o, d, diag, tv[q], rv[q], rgba, depth, mw)) { j = q; break; }
                 }
                 if (!mode.ngp) ot.w = depth / dot(cam.c2, d);   // payload.t reset (574)
                 if (j < MAX_STEPS_BETWEEN_COMPACTION) {
@@ -657,7 +679,7 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                 } else if (last) {
                     ended = true;
                 } else {
-                    lt = ts;            // the boundary-sample cache of the next iteration
+                    lt = tv[MAX_STEPS_BETWEEN_COMPACTION - 1];   // the boundary-sample cache of the next iteration
                     lraw = last_raw;
                     s += cnt;
                 }
@@ -865,8 +887,8 @@ void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode,
     else hipLaunchKernelGGL(composite_kernel<256>, dim3(blocks), dim3(256), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
 }
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
-    if (a.vol.linear) hipLaunchKernelGGL(spec_generate_kernel<true>, dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(spec_generate_kernel<false>, dim3(blocks), dim3(256), 0, s, a);
+    if (a.vol.linear) hipLaunchKernelGGL(spec_generate_kernel<true>, dim3(blocks * 4), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(spec_generate_kernel<false>, dim3(blocks * 4), dim3(64), 0, s, a);
 }
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_composite_kernel<256>, dim3(blocks), dim3(256), 0, s, a);
