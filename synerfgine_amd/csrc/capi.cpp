@@ -365,7 +365,9 @@ const std::map<std::string, double>& default_params() {
         {"nerf_spec_rounds", 4},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
         {"nerf_spec_budget", 1048576},          // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax))
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
-        {"nerf_spec_rt_gate", 1},               // 1: the raytracer starts after the speculative rounds (they get the whole GPU)
+        {"nerf_spec_rt_gate", 1},
+        {"nerf_spec_debug", 0},
+        {"occ_lds_kb", 64},                     // LDS budget for the occupancy bricks in the linear marchers (0: global loads)                 // 1: spec_generate records per-ray march trips / cycles (sng_frame_buffer "spec_dbg")               // 1: the raytracer starts after the speculative rounds (they get the whole GPU)
         {"nerf_fused_lanes", 64},               // rays per wave in the fused kernel
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
         {"nerf_gen_wide", 0},                   // cascaded generate with 1024-thread workgroups while no fused tail runs
@@ -402,6 +404,9 @@ struct sng_ctx {
     // occupancy
     bool has_bitfield = false;
     DevBuf d_bitfield, d_occ_linear, d_grid_f16, d_grid_f32, d_partial, d_mean;
+    DevBuf d_occ_brick, d_occ_brick_aux;   // OccBrick blob (sng_math.h) + {4096 flags, n_bricks}
+    uint32_t occ_brick_n = 0;              // occupied bricks (host copy, read back lazily)
+    bool occ_brick_dirty = false;
 
     // camera (Testbed)
     float cam[12] = {1, 0, 0, 0, -1, 0, 0, 0, -1, 0.5f, 0.5f, 2.0f};
@@ -450,6 +455,7 @@ struct sng_ctx {
     DevBuf rt_hint;                        // sample-parallel path kernel: per-pixel hit-depth sums of the previous frame (u8)
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
+    DevBuf spec_dbg;                       // nerf_spec_debug: per round and ray {trips, samples, cycles, K}
     uint32_t spec_rounds = 0;              // rounds enqueued by the last trace
     DevBuf rt_counts;                      // rt_count frames: path / shadow kernel {queries, box tests, triangle tests}
     DevBuf rt_hits, rt_rays, rt_next_pos, rt_tail, rt_counters;   // staged path tracer
@@ -590,6 +596,7 @@ void set_model(sng_ctx* c, const sng_nerf_config* cfg, const uint16_t* params, u
     c->has_bitfield = false;
 }
 
+void build_occ_brick(sng_ctx* c, hipStream_t s);
 void set_density_grid(sng_ctx* c, const uint16_t* grid, uint64_t n_cells) {
     if (!c->has_model) throw SngError(SNG_ERR_STATE, "set the model before the density grid");
     if (n_cells != (uint64_t)GRID_CELLS * (c->max_cascade + 1))
@@ -602,9 +609,19 @@ void set_density_grid(sng_ctx* c, const uint16_t* grid, uint64_t n_cells) {
     c->d_occ_linear.ensure((size_t)GRID_CELLS / 8);
     launch_bitfield(c->d_grid_f16.as<uint16_t>(), c->max_cascade, c->d_grid_f32.as<float>(), c->d_partial.as<double>(), c->d_mean.as<float>(),
                     c->d_bitfield.as<uint8_t>(), c->d_occ_linear.as<uint32_t>(), c->s_nerf);
+    build_occ_brick(c, c->s_nerf);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->s_nerf));
     c->has_bitfield = true;
+}
+
+// OccBrick blob of the current linear occupancy (render_frame reads the brick count back lazily)
+void build_occ_brick(sng_ctx* c, hipStream_t s) {
+    c->d_occ_brick.ensure((size_t)OCC_BRICK_CAP_WORDS * 4);
+    c->d_occ_brick_aux.ensure((4096 + 4) * 4);
+    launch_occ_brick(c->d_occ_linear.as<uint32_t>(), c->d_occ_brick_aux.as<uint32_t>(), c->d_occ_brick.as<uint32_t>(),
+                     c->d_occ_brick_aux.as<uint32_t>() + 4096, s);
+    c->occ_brick_dirty = true;
 }
 
 Volume make_volume(const sng_ctx* c) {
@@ -620,6 +637,12 @@ Volume make_volume(const sng_ctx* c) {
     v.bitfield = c->d_bitfield.as<uint8_t>();
     v.occ_linear = c->d_occ_linear.as<uint32_t>();
     v.linear = (c->max_cascade == 0 && c->cone <= 1e-5f && c->p("linear_marcher") != 0.0) ? 1 : 0;
+    // the bricks in LDS when they fit the budget (lego: 521 bricks, 41 KiB)
+    const uint32_t words = (OCC_BRICK_TABLE_WORDS + 16u * c->occ_brick_n + 3u) & ~3u;
+    if (v.linear && c->d_occ_brick.p && !c->occ_brick_dirty && c->p("occ_lds_kb") * 1024.0 >= 4.0 * words) {
+        v.occ_brick = c->d_occ_brick.as<uint32_t>();
+        v.occ_brick_words = words;
+    }
     return v;
 }
 
@@ -1193,8 +1216,15 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 sa.frame_rgba = c->nerf_rgba.as<float4>(); sa.frame_depth = c->nerf_depth.as<float>(); sa.positions = c->nerf_pos.as<float>();
                 // rays alive after the head: at most the band's pixels (grid-stride over the device count)
                 const uint32_t sblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 4));
+                const bool dbg = c->p("nerf_spec_debug") != 0.0;
+                if (dbg) {
+                    c->spec_dbg.ensure((size_t)rounds * n_band * 16);
+                    HIPCHK(hipMemsetAsync(c->spec_dbg.p, 0, (size_t)rounds * n_band * 16, c->s_nerf));
+                }
                 for (uint32_t r = 0; r < rounds; ++r) {
                     sa.in = rb[p]; sa.out = rb[p ^ 1]; sa.p = p;
+                    sa.dbg = dbg ? c->spec_dbg.as<uint4>() + (size_t)r * n_band : nullptr;
+                    sa.dbg_stride = n_band;
                     launch_spec_generate(sa, sblocks, c->s_nerf);
                     if (P.collect_kernel_times) {
                         while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
@@ -1342,6 +1372,11 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     // the raytracer's NeRF shadow test uses the density bitfield whether or not the NeRF is shown
     // (engine.cu:386-397 passes m_nerf.density_grid_bitfield unconditionally)
     Volume vol{};
+    if (c->occ_brick_dirty && c->d_occ_brick_aux.p) {   // the brick count of the last occupancy rebuild
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(&c->occ_brick_n, c->d_occ_brick_aux.as<uint32_t>() + 4096, 4, hipMemcpyDeviceToHost));
+        c->occ_brick_dirty = false;
+    }
     if (c->has_model && c->has_bitfield) vol = make_volume(c);
     else { vol.render_aabb = c->box; vol.train_aabb = c->box; vol.to_local = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)}; vol.to_local_identity = 1; }
     const CamDev cam = cam_dev(c);
@@ -1666,6 +1701,7 @@ void train_density_update(sng_ctx* c, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(c->d_grid_f32.p, t.grid.p, (size_t)n_cells * 4, hipMemcpyDeviceToDevice, s));
     launch_bitfield(nullptr, c->max_cascade, c->d_grid_f32.as<float>(), c->d_partial.as<double>(), c->d_mean.as<float>(), c->d_bitfield.as<uint8_t>(),
                     c->d_occ_linear.as<uint32_t>(), s);
+    build_occ_brick(c, s);
     c->has_bitfield = true;
 }
 
@@ -1858,7 +1894,8 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_trit.release(); o.d_wide.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob})
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
+                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1}) (void)hipEventDestroy(e);
@@ -2005,6 +2042,7 @@ void restore_training_state(sng_ctx* c, const JValue& snap) {
     HIPCHK(hipMemcpy(c->d_grid_f32.p, t.grid.p, (size_t)n_cells * 4, hipMemcpyDeviceToDevice));
     launch_bitfield(nullptr, c->max_cascade, c->d_grid_f32.as<float>(), c->d_partial.as<double>(), c->d_mean.as<float>(), c->d_bitfield.as<uint8_t>(),
                     c->d_occ_linear.as<uint32_t>(), c->s_nerf);
+    build_occ_brick(c, c->s_nerf);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->s_nerf));
     c->has_bitfield = true;
@@ -2231,7 +2269,7 @@ int sng_frame_buffer(sng_ctx* c, const char* name, void* out, uint64_t cap, uint
     return guarded([&] {
         if (!c || !name) throw SngError(SNG_ERR_INVALID, "null context or name");
         HIPCHK(hipSetDevice(c->device));
-        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}};
+        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}, {"spec_dbg", &c->spec_dbg}};
         auto it = bufs.find(name);
         if (it == bufs.end()) throw SngError(SNG_ERR_INVALID, std::string("unknown frame buffer ") + name);
         HIPCHK(hipDeviceSynchronize());

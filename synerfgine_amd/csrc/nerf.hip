@@ -474,12 +474,13 @@ __device__ __forceinline__ bool spec_composite_sample(const Volume& vol, const C
     return false;
 }
 
-// One wave per workgroup: a lane keeps all K * 8 sample t's of its ray in LDS (32 KiB per wave), so the
-// march loop issues no global stores (on gfx9-class counters a store would sit in front of every occupancy
-// load's wait); the t's and NerfCoordinates are written after the march.
-template <bool LIN>
-__global__ __launch_bounds__(64) void spec_generate_kernel(SpecArgs a) {
-    __shared__ float ts_lds[SPEC_KMAX * MAX_STEPS_BETWEEN_COMPACTION][64];
+// BRICK: the occupancy bricks are staged in LDS (dynamic shared memory) and the march loop makes no global
+// load, so its per-sample t stores to tbuf are fire-and-forget (no load waits behind them).  Without the
+// bricks (too many for the LDS budget) the loop reads the linear occupancy through a register word cache.
+template <bool LIN, bool BRICK, int THREADS = 256>
+__global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
+    extern __shared__ uint32_t occ_lds[];
+    __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
     MarchCtrl* ctrl = a.ctrl;
     const int p = a.p;
     const uint32_t n_alive = ctrl->n_alive[p];
@@ -497,17 +498,17 @@ __global__ __launch_bounds__(64) void spec_generate_kernel(SpecArgs a) {
         ctrl->n_alive[p ^ 1] = 0;
         ctrl->i_step[p ^ 1] = istep0 + MAX_STEPS_BETWEEN_COMPACTION * K;
     }
-    if (K == 0) return;
+    if (K == 0 || blockIdx.x * THREADS >= n_alive) return;
     const Volume& vol = a.vol;
-    const int lane = threadIdx.x;
+    if constexpr (BRICK) stage_occ_brick(occ_lds, vol.occ_brick, vol.occ_brick_words);
+    const int lane = threadIdx.x & 63;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
     const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
     const float qnan = __int_as_float(0x7fc00000);
-    for (uint32_t blk = blockIdx.x * 64u; blk < n_alive; blk += gridDim.x * 64u) {
-        const uint32_t i = blk + lane;
+    for (uint32_t blk = blockIdx.x * THREADS; blk < n_alive; blk += gridDim.x * THREADS) {
+        const uint32_t i = blk + threadIdx.x;
         uint32_t tot = 0, nnet = 0, n_it = 0, cnt_last = 0, rbits = 0;
         f3 o = splat(0.0f), d = splat(1.0f);
-        float tl = 0.0f;
         if (i < n_alive) {
             const float4 ot = a.in.o_t[i], di = a.in.d_idx[i];
             o = mk(ot.x, ot.y, ot.z);
@@ -517,17 +518,24 @@ __global__ __launch_bounds__(64) void spec_generate_kernel(SpecArgs a) {
             float t = ot.w;
             float prev = a.mode.ngp ? qnan : a.in.lt[i].x;   // the previous iteration's last sample
             OccCache oc;
+            uint32_t trips = 0;
+            const uint64_t c0 = a.dbg ? (uint64_t)clock64() : 0ull;
+            float* tb = a.tbuf + i;
             for (uint32_t it = 0; it < K; ++it) {
                 uint32_t cnt = 0;
-                float first = qnan;
+                float first = qnan, tl = 0.0f;
                 if constexpr (LIN) {
                     const f3 hs = half_sign(d);
 #pragma unroll 1
                     while (cnt < MAX_STEPS_BETWEEN_COMPACTION) {   // generate_kernel's flattened loop
                         const f3 pos = o + d * t;
+                        ++trips;
                         if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
-                        if (occupied_linear_c(pos, vol.occ_linear, oc)) {
-                            ts_lds[tot + cnt][lane] = t;
+                        bool occ;
+                        if constexpr (BRICK) occ = occupied_brick_c(pos, occ_lds, oc);
+                        else occ = occupied_linear_c(pos, vol.occ_linear, oc);
+                        if (occ) {
+                            tb[(size_t)(tot + cnt) * n_alive] = t;
                             if (cnt == 0) first = t;
                             tl = t;
                             t += calc_dt(t, 0.0f);
@@ -539,9 +547,10 @@ __global__ __launch_bounds__(64) void spec_generate_kernel(SpecArgs a) {
                 } else {
 #pragma unroll 1
                     while (cnt < MAX_STEPS_BETWEEN_COMPACTION) {
+                        ++trips;
                         if (occ_step(t, cone, o, d, idir, 0, vol.max_mip, vol)) {
                             if (t >= MAX_DEPTH) break;
-                            ts_lds[tot + cnt][lane] = t;
+                            tb[(size_t)(tot + cnt) * n_alive] = t;
                             if (cnt == 0) first = t;
                             tl = t;
                             t += calc_dt(t, cone);
@@ -565,25 +574,35 @@ __global__ __launch_bounds__(64) void spec_generate_kernel(SpecArgs a) {
             }
             // trace keeps generate's t (836): the survivors' next start
             if (a.mode.ngp && n_it == K && cnt_last == MAX_STEPS_BETWEEN_COMPACTION) reinterpret_cast<float*>(a.in.o_t + i)[3] = t;
+#ifdef SNG_OCC_COUNT
+            const uint32_t loads = oc.loads;
+#else
+            const uint32_t loads = 0u;
+#endif
+            if (a.dbg && i < a.dbg_stride) a.dbg[i] = make_uint4(trips, tot | (loads << 16), (uint32_t)((uint64_t)clock64() - c0), K);
         }
-        // one atomic per wave for the round's network samples
-        const uint32_t incl = wave_incl_scan(nnet, lane);
-        uint32_t base = 0;
-        if (lane == 63 && incl) base = atomicAdd(&ctrl->n_samples[p], incl);
-        base = __shfl(base, 63, 64) + incl - nnet;
+        const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], nnet, nullptr, false, nullptr, false, sh_app, lane);
         if (i < n_alive) {
             a.samp[i] = make_uint2(base, n_it | (cnt_last << 5) | (rbits << 9));
             const f3 wd = (d + 1.0f) * 0.5f;
             uint32_t q = base;
+            // the iteration's t's read back together, then its NerfCoordinates written
 #pragma unroll 1
-            for (uint32_t s = 0; s < tot; ++s) {
-                const float ts = ts_lds[s][lane];
-                a.tbuf[(size_t)s * n_alive + i] = ts;
-                if ((s & 7u) == 0 && ((rbits >> (s >> 3)) & 1u)) continue;   // cached boundary sample: no evaluation
-                const f3 wp = ((o + d * ts) - vol.train_aabb.lo) / wdiag;
-                float* c = a.coords + (size_t)q * 7;
-                c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(calc_dt(ts, cone)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
-                ++q;
+            for (uint32_t s0 = 0; s0 < tot; s0 += MAX_STEPS_BETWEEN_COMPACTION) {
+                float tv[MAX_STEPS_BETWEEN_COMPACTION];
+#pragma unroll
+                for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j)
+                    if (s0 + j < tot) tv[j] = a.tbuf[(size_t)(s0 + j) * n_alive + i];
+                const uint32_t j0 = ((rbits >> (s0 >> 3)) & 1u) ? 1u : 0u;   // cached boundary sample: no evaluation
+#pragma unroll
+                for (uint32_t j = 0; j < MAX_STEPS_BETWEEN_COMPACTION; ++j) {
+                    if (j < j0 || s0 + j >= tot) continue;
+                    const float ts = tv[j];
+                    const f3 wp = ((o + d * ts) - vol.train_aabb.lo) / wdiag;
+                    float* c = a.coords + (size_t)q * 7;
+                    c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(calc_dt(ts, cone)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+                    ++q;
+                }
             }
         }
     }
@@ -840,6 +859,51 @@ __global__ void bitfield_linear_kernel(const uint8_t* __restrict__ bf, uint32_t*
     occ[w] = bits;
 }
 
+// OccBrick blob (sng_math.h) from the linear mip-0 occupancy: flags, one-block scan, fill
+__global__ void occ_brick_flag_kernel(const uint32_t* __restrict__ occ, uint32_t* __restrict__ flags) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= 4096) return;
+    const uint32_t bz = b >> 8, by = (b >> 4) & 15u, bx = b & 15u;
+    uint32_t any = 0;
+    for (uint32_t z = 0; z < 8; ++z)
+        for (uint32_t y = 0; y < 8; ++y) any |= (occ[((bz * 8 + z) * GRID_SIZE + by * 8 + y) * (GRID_SIZE / 32) + (bx >> 2)] >> ((bx & 3u) * 8u)) & 0xffu;
+    flags[b] = any ? 1u : 0u;
+}
+__global__ __launch_bounds__(1024) void occ_brick_scan_kernel(const uint32_t* __restrict__ flags, uint32_t* __restrict__ blob, uint32_t* __restrict__ n_out) {
+    __shared__ uint32_t ps[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t f0 = flags[4 * t], f1 = flags[4 * t + 1], f2 = flags[4 * t + 2], f3v = flags[4 * t + 3];
+    const uint32_t sum = f0 + f1 + f2 + f3v;
+    ps[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? ps[t - off] : 0u;
+        __syncthreads();
+        ps[t] += v;
+        __syncthreads();
+    }
+    uint32_t slot = ps[t] - sum;
+    uint16_t* tab = reinterpret_cast<uint16_t*>(blob);
+    const uint32_t fl[4] = {f0, f1, f2, f3v};
+    for (int k = 0; k < 4; ++k) {
+        tab[4 * t + k] = fl[k] ? (uint16_t)slot : (uint16_t)0xffffu;
+        slot += fl[k];
+    }
+    if (t == 1023) *n_out = ps[t];
+}
+__global__ void occ_brick_fill_kernel(const uint32_t* __restrict__ occ, uint32_t* __restrict__ blob) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= 4096 * 16) return;
+    const uint32_t b = g >> 4, k = g & 15u;
+    const uint32_t slot = reinterpret_cast<const uint16_t*>(blob)[b];
+    if (slot == 0xffffu) return;
+    const uint32_t bz = b >> 8, by = (b >> 4) & 15u, bx = b & 15u;
+    const uint32_t z = bz * 8 + (k >> 1), y0 = by * 8 + (k & 1u) * 4;
+    uint32_t w = 0;
+    for (uint32_t yy = 0; yy < 4; ++yy) w |= ((occ[(z * GRID_SIZE + y0 + yy) * (GRID_SIZE / 32) + (bx >> 2)] >> ((bx & 3u) * 8u)) & 0xffu) << (yy * 8u);
+    blob[OCC_BRICK_TABLE_WORDS + slot * 16u + k] = w;
+}
+
 __global__ void ctrl_init_kernel(MarchCtrl* c) {
     if (threadIdx.x < 64) {   // the fused tail kernel accumulates into the histograms
         c->alive_hist[threadIdx.x] = 0; c->steps_hist[threadIdx.x] = 0; c->samples_hist[threadIdx.x] = 0;
@@ -887,8 +951,10 @@ void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode,
     else hipLaunchKernelGGL(composite_kernel<256>, dim3(blocks), dim3(256), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
 }
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
-    if (a.vol.linear) hipLaunchKernelGGL(spec_generate_kernel<true>, dim3(blocks * 4), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(spec_generate_kernel<false>, dim3(blocks * 4), dim3(64), 0, s, a);
+    if (a.vol.linear && a.vol.occ_brick_words)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(spec_generate_kernel<true, true>), dim3(blocks), dim3(256), a.vol.occ_brick_words * 4, s, a);
+    else if (a.vol.linear) hipLaunchKernelGGL(HIP_KERNEL_NAME(spec_generate_kernel<true, false>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(spec_generate_kernel<false, false>), dim3(blocks), dim3(256), 0, s, a);
 }
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_composite_kernel<256>, dim3(blocks), dim3(256), 0, s, a);
@@ -912,6 +978,11 @@ void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid
         hipLaunchKernelGGL(bitfield_max_pool_kernel, dim3((N / 64 + 255) / 256), dim3(256), 0, s, N / 64, bf + (size_t)N / 8 * (level - 1),
                            bf + (size_t)N / 8 * level);
     hipLaunchKernelGGL(bitfield_linear_kernel, dim3(N / 32 / 256), dim3(256), 0, s, bf, occ_linear);
+}
+void launch_occ_brick(const uint32_t* occ_linear, uint32_t* flags, uint32_t* blob, uint32_t* n_bricks, hipStream_t s) {
+    hipLaunchKernelGGL(occ_brick_flag_kernel, dim3(16), dim3(256), 0, s, occ_linear, flags);
+    hipLaunchKernelGGL(occ_brick_scan_kernel, dim3(1), dim3(1024), 0, s, flags, blob, n_bricks);
+    hipLaunchKernelGGL(occ_brick_fill_kernel, dim3(4096 * 16 / 256), dim3(256), 0, s, occ_linear, blob);
 }
 
 }  // namespace sng

@@ -286,6 +286,8 @@ struct SpecArgs {
     float4* frame_rgba;
     float* frame_depth;
     float* positions;
+    uint4* dbg;                   // nerf_spec_debug: per round and ray {march trips, samples, shader cycles, K} (nullptr: off)
+    uint32_t dbg_stride;          // rays per round in dbg
 };
 constexpr uint32_t SPEC_KMAX = 16;
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s);
@@ -303,6 +305,8 @@ void launch_normals(int W, int H, int row0, int row1, const float* pos, float* n
 void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, uint32_t* occ_linear,
                      hipStream_t s);
 void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s);
+// OccBrick blob (sng_math.h) of the linear occupancy; flags: 4096 u32 scratch, blob: OCC_BRICK_CAP_WORDS, n_bricks: 1 u32
+void launch_occ_brick(const uint32_t* occ_linear, uint32_t* flags, uint32_t* blob, uint32_t* n_bricks, hipStream_t s);
 // mesh.hip
 void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, hipStream_t s);
 void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,

@@ -387,7 +387,15 @@ struct Volume {
     const uint32_t* occ_linear;  // mip-0 occupancy as x-fastest bit rows (same bits as the Morton bitfield)
     int linear;                  // cone == 0 && max_mip == 0: the exact fast marcher applies
     StepSpace ss;                // step_space(cone)
+    // mip-0 occupancy as 8^3-cell bricks (same bits, OccBrick layout below), small enough to stage in LDS:
+    // the linear marchers' loops then make no global load.  occ_brick_words == 0: not available.
+    const uint32_t* occ_brick;
+    uint32_t occ_brick_words;
 };
+// OccBrick layout (u32 words): [0, 2048) = u16 slot per brick b = (iz/8)*256 + (iy/8)*16 + ix/8 (0xffff:
+// no occupied cell), then 16 words per occupied brick: word (iz%8)*2 + (iy%8)/4, bit (iy%4)*8 + ix%8.
+constexpr uint32_t OCC_BRICK_TABLE_WORDS = 2048;
+constexpr uint32_t OCC_BRICK_CAP_WORDS = OCC_BRICK_TABLE_WORDS + 4096 * 16;
 SNG_HD f3 to_local(const Volume& v, f3 p) { return v.to_local_identity ? p : mul(v.to_local, p); }
 
 // Exact specialisation of if_unoccupied_advance_to_next_occupied_voxel<false> for unit-cube
@@ -405,15 +413,46 @@ SNG_HD bool occupied_linear(f3 pos, const uint32_t* occ) {
 // the march's dependent chain.  Same bits as occupied_linear.
 struct OccCache {
     uint32_t w = 0xffffffffu, bits = 0u;
+#ifdef SNG_OCC_COUNT
+    uint32_t loads = 0u;
+#endif
 };
 SNG_HD bool occupied_linear_c(f3 pos, const uint32_t* occ, OccCache& c) {
     f3 q = ((pos - splat(0.5f)) + splat(0.5f)) * (float)GRID_SIZE;   // cascaded_grid_idx_at, mip 0
     int ix = (int)q.x, iy = (int)q.y, iz = (int)q.z;
     if (ix < 0 || ix >= (int)GRID_SIZE || iy < 0 || iy >= (int)GRID_SIZE || iz < 0 || iz >= (int)GRID_SIZE) return false;
     const uint32_t w = ((uint32_t)iz * GRID_SIZE + (uint32_t)iy) * (GRID_SIZE / 32) + ((uint32_t)ix >> 5);
-    if (w != c.w) { c.w = w; c.bits = occ[w]; }
+    if (w != c.w) {
+        c.w = w;
+        c.bits = occ[w];
+#ifdef SNG_OCC_COUNT
+        ++c.loads;
+#endif
+    }
     return (c.bits >> (ix & 31)) & 1u;
 }
+#if defined(__HIP__)
+// occupied_linear through the LDS copy of the OccBrick blob, with the last 32-cell group in registers
+__device__ __forceinline__ bool occupied_brick_c(f3 pos, const uint32_t* lds, OccCache& c) {
+    f3 q = ((pos - splat(0.5f)) + splat(0.5f)) * (float)GRID_SIZE;   // cascaded_grid_idx_at, mip 0
+    int ix = (int)q.x, iy = (int)q.y, iz = (int)q.z;
+    if (ix < 0 || ix >= (int)GRID_SIZE || iy < 0 || iy >= (int)GRID_SIZE || iz < 0 || iz >= (int)GRID_SIZE) return false;
+    const uint32_t b = ((uint32_t)iz >> 3) * 256u + ((uint32_t)iy >> 3) * 16u + ((uint32_t)ix >> 3);
+    const uint32_t sub = ((uint32_t)iz & 7u) * 2u + (((uint32_t)iy & 7u) >> 2);
+    const uint32_t key = (b << 4) | sub;
+    if (key != c.w) {
+        c.w = key;
+        const uint32_t slot = reinterpret_cast<const uint16_t*>(lds)[b];
+        c.bits = slot == 0xffffu ? 0u : lds[OCC_BRICK_TABLE_WORDS + slot * 16u + sub];
+    }
+    return (c.bits >> ((((uint32_t)iy & 3u) << 3) | ((uint32_t)ix & 7u))) & 1u;
+}
+// copy the OccBrick blob into LDS (every thread of the block; words padded to a multiple of 4)
+__device__ __forceinline__ void stage_occ_brick(uint32_t* lds, const uint32_t* g, uint32_t words) {
+    for (uint32_t k = threadIdx.x * 4u; k < words; k += blockDim.x * 4u) *reinterpret_cast<uint4*>(lds + k) = *reinterpret_cast<const uint4*>(g + k);
+    __syncthreads();
+}
+#endif
 // advance_to_next_voxel(mip 0) with distance_to_next_voxel(res = 128), cone == 0
 SNG_HD float dda_step_linear(float t, f3 pos, f3 idir, f3 hs /* 0.5*sign(d) */) {
     const f3 p = (float)GRID_SIZE * (pos - 0.5f);

@@ -1,7 +1,7 @@
 """Tail diagnostics: per-iteration alive / sample histograms and the speculative rounds' statistics for a config,
 and the frame time for a list of parameter sets.
 
-usage: python tools/tail_diag.py CONFIG [key=value,key=value ...]   (one parameter set per argument; none: defaults)
+usage: python tools/tail_diag.py CONFIG [key=value+key=value ...]   (one parameter set per argument; none: defaults)
 """
 import json
 import sys
@@ -13,7 +13,7 @@ import torch
 from synerfgine_amd import scene as S
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
-sets = [dict((kv.split("=")[0], float(kv.split("=")[1])) for kv in a.split(",") if kv) for a in sys.argv[2:]] or [{}]
+sets = [dict((kv.split("=")[0], float(kv.split("=")[1])) for kv in a.split("+") if kv) for a in sys.argv[2:]] or [{}]
 tb, eng, _ = S.make_engine(cfg, model="lego" if cfg != "c4" else "synthetic")
 first = True
 for ov in sets:
@@ -36,4 +36,21 @@ for ov in sets:
                       "raytrace": round(r.ms_raytrace, 3), "net_ms": round(r.ms_network, 4), "launches": r.network_launches,
                       "tail_ms": round(r.ms_fused_tail, 4), "spec_evals": r.spec_evals, "spec_exec": r.spec_exec,
                       "iters": r.n_iterations, "samples": r.n_samples}), flush=True)
+if any(ov.get("nerf_spec_debug") for ov in sets):
+    import numpy as np
+    W, H = eng.resolution()["nerf"]
+    dbg = eng.frame_buffer("spec_dbg", np.uint32).reshape(-1, W * H, 4)
+    for r, d in enumerate(dbg):
+        d = d[d[:, 3] > 0]
+        if len(d) == 0:
+            continue
+        cyc = d[:, 2].astype(np.float64)
+        tr = d[:, 0].astype(np.float64)
+        ld = (d[:, 1] >> 16).astype(np.float64)
+        am = int(np.argmax(tr))
+        print(json.dumps({"round": r, "rays": int(len(d)), "K": int(d[0, 3]), "trips_max": int(tr.max()), "trips_mean": round(tr.mean(), 1),
+                          "loads_of_max": int(ld[am]), "loads_mean": round(ld.mean(), 1),
+                          "trips_p99": float(np.percentile(tr, 99)), "samples_max": int((d[:, 1] & 0xffff).max()), "cycles_max": int(cyc.max()),
+                          "cycles_per_trip_median": round(float(np.median(cyc / np.maximum(tr, 1))), 1),
+                          "cycles_per_trip_of_max": round(float(cyc[np.argmax(tr)] / tr.max()), 1)}))
 tb.close()
