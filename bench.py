@@ -302,19 +302,29 @@ def main():
     rows = (bounds[rank], bounds[rank + 1])
     band = max(bounds[k + 1] - bounds[k] for k in range(world))
     on_dev = args.dist_backend == "nccl"
-    # composition tiles: RGBA8 (4 B/px), written by sng_final_rgba8 on the device
+    # composition: RGBA8 (4 B/px).  RCCL: every band goes to rank 0 only, received straight
+    # into its rows of the frame (sng_gather_rgba8: grouped ncclSend / ncclRecv).  gloo (CPU rehearsal):
+    # sng_final_rgba8 tiles all-gathered on the host.
     tile_dev = torch.zeros((band, MW), dtype=torch.int32, device=dev)
-    tile = tile_dev if on_dev else torch.zeros((band, MW), dtype=torch.int32)
-    frame = torch.empty((world * band, MW), dtype=torch.int32, device=dev if on_dev else "cpu") if world > 1 else None
+    tile = torch.zeros((band, MW), dtype=torch.int32)
+    root_gather = world > 1 and on_dev and not args.local_schedule   # the communicator sng_set_comm attached
+    if root_gather:
+        frame = torch.empty((MH, MW), dtype=torch.int32, device=dev) if rank == 0 else None
+    else:
+        frame = torch.empty((world * band, MW), dtype=torch.int32, device=dev if on_dev else "cpu") if world > 1 else None
 
     def step(collect):
         r = eng.frame(spp=0, reset=True, rows=rows if world > 1 else None, collect_kernel_times=collect)
-        if world > 1:
+        if root_gather:
+            eng.gather_rgba8(bounds, frame.data_ptr() if rank == 0 else 0)
+        elif world > 1:
             if rows[1] > rows[0]:
                 tb._lib.sng_final_rgba8(tb.ctx, rows[0], rows[1], tile_dev.data_ptr(), stream.cuda_stream)
-            if not on_dev:
+            if on_dev:
+                T.gather_bands(tile_dev, frame)
+            else:
                 tile.copy_(tile_dev)
-            T.gather_bands(tile, frame)
+                T.gather_bands(tile, frame)
         return r
 
     for _ in range(args.warmup):
@@ -388,7 +398,9 @@ def main():
             "config": {"workload": f"{args.config}: " + WORKLOADS[args.config],
                        "width": MW, "height": MH, "nerf_res": list(res["nerf"]),
                        "tiles": f"{world} horizontal bands (rows {bounds}) + " +
-                                (("RCCL" if on_dev else "gloo") + " all_gather of RGBA8 tiles" if world > 1 else "no gather"),
+                                (("RCCL gather of the RGBA8 bands to rank 0 (sng_gather_rgba8)" if root_gather else
+                                  ("RCCL" if on_dev else "gloo") + " all_gather of RGBA8 tiles")
+                                 if world > 1 else "no gather"),
                        "step_schedule": "band-local" if (world > 1 and args.local_schedule) else ("frame-wide (per-iteration alive-count all-reduce)" if world > 1 else "frame-wide"),
                        "samples_per_frame": int(s0.n_samples), "samples_reused_per_frame": int(s0.n_samples_reused),
                        "reference_slots_per_frame": int(s0.n_reference_slots),

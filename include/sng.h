@@ -276,6 +276,16 @@ int sng_set_comm(sng_ctx* ctx, const uint8_t* unique_id, int rank, int world);
  * success; called once per wavefront iteration after a stream sync.  fn NULL detaches. */
 typedef int (*sng_sched_reduce_fn)(uint32_t* values, uint32_t n, void* user);
 int sng_set_sched_reducer(sng_ctx* ctx, sng_sched_reduce_fn fn, void* user);
+/* Final composition of a banded frame ("a final RCCL gather to GPU 0 of RGBA8"): rank r's
+ * final rows [bounds[r], bounds[r+1]) as RGBA8 (the sng_final_rgba8 encoding) go to rank 0 over the
+ * attached communicator -- grouped ncclSend / ncclRecv, each band received straight into its rows of
+ * d_frame (rank 0: device buffer of width x height uint32; ignored on other ranks).  bounds: world + 1
+ * row boundaries, the same on every rank.  Enqueued on hip_stream (NULL: the context's stream); every
+ * rank calls it once per frame.  The reference renders on one GPU; its per-view copy-back is
+ * testbed.cu:5126-5127. */
+int sng_gather_rgba8(sng_ctx* ctx, const int32_t* bounds, uint32_t* d_frame, void* hip_stream);
+/* in-place sum of n uint32 on the device over the attached communicator (band balancing: per-rank times) */
+int sng_comm_allreduce_u32(sng_ctx* ctx, uint32_t* d_values, uint64_t n, void* hip_stream);
 
 int sng_synchronize(sng_ctx* ctx);
 int sng_copy_to_host(sng_ctx* ctx, const void* d_src, void* h_dst, uint64_t n_bytes);

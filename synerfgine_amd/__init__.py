@@ -290,6 +290,13 @@ class Engine:
         self._reduce_cb = _lib.SCHED_REDUCE_FN(cb)   # keep alive while attached
         check(self._lib.sng_set_sched_reducer(self.ctx, ctypes.cast(self._reduce_cb, ctypes.c_void_p), None))
 
+    def gather_rgba8(self, bounds, d_frame=0, stream=0):
+        """Final composition over the attached RCCL communicator (sng_gather_rgba8): this rank's final rows
+        [bounds[rank], bounds[rank+1]) as RGBA8 go to rank 0, straight into d_frame (rank 0: device pointer of
+        a height x width uint32 buffer).  Enqueued on `stream` (0: the context's)."""
+        b = (ctypes.c_int32 * len(bounds))(*[int(x) for x in bounds])
+        check(self._lib.sng_gather_rgba8(self.ctx, b, ctypes.c_void_p(int(d_frame) or None), ctypes.c_void_p(int(stream) or None)))
+
     def detach_comm(self):
         check(self._lib.sng_set_comm(self.ctx, None, 0, 0))
         check(self._lib.sng_set_sched_reducer(self.ctx, None, None))

@@ -155,6 +155,8 @@ SIGNATURES = {
     "sng_load_snapshot": (ctypes.c_int, [P, ctypes.c_char_p]),
     "sng_save_snapshot": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32]),
     "sng_rt_counters": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
+    "sng_gather_rgba8": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_int32), P, P]),
+    "sng_comm_allreduce_u32": (ctypes.c_int, [P, P, ctypes.c_uint64, P]),
     "sng_frame_buffer": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "sng_snapshot_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(sng_nerf_config), ctypes.POINTER(U64), ctypes.POINTER(U64), U16P, U64,
                                           U16P, U64]),

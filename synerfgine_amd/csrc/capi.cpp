@@ -367,7 +367,9 @@ const std::map<std::string, double>& default_params() {
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
         {"nerf_spec_rt_gate", 1},
         {"nerf_spec_debug", 0},
-        {"occ_lds_kb", 64},                     // LDS budget for the occupancy bricks in the linear marchers (0: global loads)                 // 1: spec_generate records per-ray march trips / cycles (sng_frame_buffer "spec_dbg")               // 1: the raytracer starts after the speculative rounds (they get the whole GPU)
+        {"occ_lds_kb", 64},
+        {"load_optimizer_state", 1},            // sng_load_snapshot restores a snapshot's optimizer state (0: inference model only)
+        {"optimizer_state_loaded", -1},         // set by sng_load_snapshot: 1 restored, 0 skipped / malformed, -1 none in the file                     // LDS budget for the occupancy bricks in the linear marchers (0: global loads)                 // 1: spec_generate records per-ray march trips / cycles (sng_frame_buffer "spec_dbg")               // 1: the raytracer starts after the speculative rounds (they get the whole GPU)
         {"nerf_fused_lanes", 64},               // rays per wave in the fused kernel
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
         {"nerf_gen_wide", 0},                   // cascaded generate with 1024-thread workgroups while no fused tail runs
@@ -456,6 +458,7 @@ struct sng_ctx {
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
     DevBuf spec_dbg;                       // nerf_spec_debug: per round and ray {trips, samples, cycles, K}
+    DevBuf band_rgba8;                     // sng_gather_rgba8: this rank's band as RGBA8
     uint32_t spec_rounds = 0;              // rounds enqueued by the last trace
     DevBuf rt_counts;                      // rt_count frames: path / shadow kernel {queries, box tests, triangle tests}
     DevBuf rt_hits, rt_rays, rt_next_pos, rt_tail, rt_counters;   // staged path tracer
@@ -1895,7 +1898,7 @@ void ctx_destroy(sng_ctx* c) {
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
-                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->display_rgb})
+                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->band_rgba8, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1}) (void)hipEventDestroy(e);
@@ -1994,6 +1997,33 @@ std::vector<T> download(const DevBuf& b, size_t n) {
     if (n) HIPCHK(hipMemcpy(h.data(), b.p, n * sizeof(T), hipMemcpyDeviceToHost));
     return h;
 }
+// whether the snapshot's optimizer block has every key and size restore_training_state reads (the tcnn key
+// names are restated, not pinned; a block written by another tcnn version must not break a render-only load)
+bool training_state_usable(const sng_ctx* c, const JValue& snap, std::string& why) {
+    const uint64_t n = c->n_params;
+    const uint64_t n_cells = (uint64_t)GRID_CELLS * (c->max_cascade + 1);
+    auto bin_ok = [&](const JValue& parent, const char* key, uint64_t bytes) {
+        if (!parent.contains(key)) { why = std::string("missing ") + key; return false; }
+        const JValue& v = parent[key];
+        if (v.type != JValue::Binary || v.str.size() != bytes) { why = std::string(key) + " has the wrong type or size"; return false; }
+        return true;
+    };
+    const JValue& opt = snap["optimizer"];
+    if (opt.type != JValue::Object) { why = "optimizer is not a map"; return false; }
+    if (!bin_ok(opt, "weights_ema_binary", n * 4)) return false;
+    if (!opt.contains("nested") || !opt["nested"].contains("nested")) { why = "missing optimizer.nested.nested (Adam)"; return false; }
+    const JValue& adam = opt["nested"]["nested"];
+    if (!bin_ok(adam, "first_moments_binary", n * 4) || !bin_ok(adam, "second_moments_binary", n * 4) || !bin_ok(adam, "param_steps_binary", n * 4))
+        return false;
+    if (!adam.contains("current_step") || adam["current_step"].type == JValue::Binary) { why = "missing current_step"; return false; }
+    if (snap.contains("sng")) {
+        const JValue& x = snap["sng"];
+        if (!bin_ok(x, "master_binary", n * 4) || !bin_ok(x, "density_grid_f32_binary", n_cells * 4) || !bin_ok(x, "rng_binary", 32)) return false;
+        if (!x.contains("grid_ema_step")) { why = "missing sng.grid_ema_step"; return false; }
+    }
+    return true;
+}
+
 void restore_training_state(sng_ctx* c, const JValue& snap) {
     const uint64_t n = c->n_params;
     const uint32_t n_cells = GRID_CELLS * (c->max_cascade + 1);
@@ -2068,7 +2098,20 @@ void load_snapshot(sng_ctx* c, const std::string& path) {
         if (cam.contains("scale")) c->m_scale = cam["scale"].as_float();
     }
     if (snap.contains("exposure")) c->params["exposure"] = snap["exposure"].as_num();
-    if (snap.contains("optimizer")) restore_training_state(c, snap);
+    // the optimizer chain's state (include_optimizer_state): restored for training when every key and size is
+    // as written; otherwise the inference model stays loaded and the training state is not touched
+    // (optimizer_state_loaded: 1 restored, 0 skipped or malformed, -1 none in the file)
+    c->params["optimizer_state_loaded"] = -1.0;
+    if (snap.contains("optimizer")) {
+        std::string why;
+        if (c->p("load_optimizer_state") != 0.0 && training_state_usable(c, snap, why)) {
+            restore_training_state(c, snap);
+            c->params["optimizer_state_loaded"] = 1.0;
+        } else {
+            c->params["optimizer_state_loaded"] = 0.0;
+            if (!why.empty()) std::fprintf(stderr, "sng_load_snapshot: optimizer state not restored (%s); inference model loaded\n", why.c_str());
+        }
+    }
 }
 
 // ---- Testbed::save_snapshot (testbed.cu:4812-4876) ------------------------------------------------
@@ -2769,6 +2812,36 @@ int sng_copy_device(sng_ctx* c, const void* src, void* dst, uint64_t n, void* st
     return guarded([&] {
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    });
+}
+int sng_gather_rgba8(sng_ctx* c, const int32_t* bounds, uint32_t* d_frame, void* stream) {
+    return guarded([&] {
+        if (!c || !bounds) throw SngError(SNG_ERR_INVALID, "null context or bounds");
+        HIPCHK(hipSetDevice(c->device));
+        if (!c->sched_comm.comm) throw SngError(SNG_ERR_STATE, "no communicator attached (sng_set_comm)");
+        const int world = c->sched_comm.world, rank = c->sched_comm.rank;
+        const int W = c->mesh_res[0], H = c->mesh_res[1];
+        std::vector<size_t> off(world), size(world);
+        for (int k = 0; k < world; ++k) {
+            if (bounds[k] < 0 || bounds[k + 1] > H || bounds[k] > bounds[k + 1] || (k == 0 && bounds[0] != 0) || (k == world - 1 && bounds[world] != H))
+                throw SngError(SNG_ERR_INVALID, "bounds must tile [0, height)");
+            off[k] = (size_t)bounds[k] * W * 4;
+            size[k] = (size_t)(bounds[k + 1] - bounds[k]) * W * 4;
+        }
+        if (rank == 0 && !d_frame) throw SngError(SNG_ERR_INVALID, "rank 0 needs the frame buffer");
+        hipStream_t s = stream ? (hipStream_t)stream : c->s_nerf;
+        c->band_rgba8.ensure(std::max<size_t>(4, size[rank]));
+        if (size[rank]) launch_rgba8_band(c->final_rgba.as<float4>() + (size_t)bounds[rank] * W, (uint32_t)(size[rank] / 4), c->band_rgba8.as<uint32_t>(), s);
+        HIPCHK(hipGetLastError());
+        comm_gather_to_root(c->sched_comm, c->band_rgba8.p, d_frame, off.data(), size.data(), s);
+    });
+}
+int sng_comm_allreduce_u32(sng_ctx* c, uint32_t* d, uint64_t n, void* stream) {
+    return guarded([&] {
+        if (!c || !d) throw SngError(SNG_ERR_INVALID, "null context or buffer");
+        HIPCHK(hipSetDevice(c->device));
+        if (!c->sched_comm.comm) throw SngError(SNG_ERR_STATE, "no communicator attached (sng_set_comm)");
+        comm_allreduce_u32(c->sched_comm, d, (size_t)n, stream ? (hipStream_t)stream : c->s_nerf);
     });
 }
 int sng_final_rgba8(sng_ctx* c, int32_t row_begin, int32_t row_end, uint32_t* d_out, void* stream) {

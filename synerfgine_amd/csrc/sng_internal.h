@@ -357,5 +357,6 @@ void comm_unique_id(uint8_t out[SNG_COMM_ID_BYTES]);
 void comm_init(SchedComm& c, const uint8_t* id, int rank, int world);
 void comm_destroy(SchedComm& c);
 void comm_allreduce_u32(SchedComm& c, uint32_t* dev, size_t n, hipStream_t s);
+void comm_gather_to_root(SchedComm& c, const void* d_band, void* d_frame, const size_t* offsets, const size_t* sizes, hipStream_t s);
 
 }  // namespace sng

@@ -139,3 +139,54 @@ def test_snapshot_round_trip_and_training_resume(data, tmp_path):
         for tb in (a, b, c):
             if tb is not None:
                 tb.close()
+
+
+def test_malformed_optimizer_block_keeps_the_inference_model(data, tmp_path):
+    """A snapshot whose optimizer block has missing keys or wrong sizes (another tcnn version's layout) still
+    loads for rendering: sng_load_snapshot validates the block before touching the training state, keeps the
+    inference model and reports optimizer_state_loaded = 0."""
+    from synerfgine_amd import synthetic
+    imgs, xf, focal, pp = data
+    cfg, params = synthetic.random_init(7)
+    a, ea = _testbed(data, cfg, params)
+    tbs = [a]
+    try:
+        a.set_training_dataset(imgs, xf, focal, pp)
+        a.train_reset(7)
+        a.train(4)
+        p_opt, p_plain = tmp_path / "opt.ingp", tmp_path / "plain.ingp"
+        a.save_snapshot(p_opt, include_optimizer_state=True)
+        a.save_snapshot(p_plain)
+        bad = []
+        r1 = _decode(p_opt)
+        r1["snapshot"]["optimizer"]["nested"]["nested"]["first_moments_binary"] = b"\0" * 12   # wrong size
+        bad.append(r1)
+        r2 = _decode(p_opt)
+        del r2["snapshot"]["optimizer"]["weights_ema_binary"]                                  # missing key
+        bad.append(r2)
+        r3 = _decode(p_opt)
+        r3["snapshot"]["optimizer"] = {"nested": {"otype": "Adam"}}                           # another layout
+        bad.append(r3)
+        frames = []
+        for k, r in enumerate([None] + bad):
+            path = p_plain if r is None else tmp_path / f"bad{k}.ingp"
+            if r is not None:
+                with open(path, "wb") as f:
+                    f.write(zlib.compress(msgpack.packb(r, use_bin_type=True), 6))
+            b, eb = _testbed(data)
+            tbs.append(b)
+            b.load_snapshot(path)
+            assert eb.get_param("optimizer_state_loaded") == (-1.0 if r is None else 0.0)
+            eb.set_param("show_virtual_obj", 0)
+            eb.init(96, 54)
+            frames.append(eb.frame().download("nerf_rgba"))
+        for f in frames[1:]:
+            assert np.array_equal(frames[0], f)
+        # and the well-formed block is restored
+        b, eb = _testbed(data)
+        tbs.append(b)
+        b.load_snapshot(p_opt)
+        assert eb.get_param("optimizer_state_loaded") == 1.0
+    finally:
+        for tb in tbs:
+            tb.close()
