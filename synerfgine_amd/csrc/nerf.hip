@@ -521,55 +521,61 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             uint32_t trips = 0;
             const uint64_t c0 = a.dbg ? (uint64_t)clock64() : 0ull;
             float* tb = a.tbuf + i;
-            for (uint32_t it = 0; it < K; ++it) {
-                uint32_t cnt = 0;
-                float first = qnan, tl = 0.0f;
-                if constexpr (LIN) {
-                    const f3 hs = half_sign(d);
+            // ONE flattened loop over all K iterations: each trip is one DDA step or one sample, and an
+            // iteration's end (8 samples, or the march leaving the volume) is handled inside the trip, so a
+            // wave runs max(total trips of its lanes) trips, not the sum over iterations of each one's max
+            uint32_t cnt = 0, it = 0;
+            float first = qnan, tl = 0.0f;
+            const f3 hs = half_sign(d);
+            bool going = true;
 #pragma unroll 1
-                    while (cnt < MAX_STEPS_BETWEEN_COMPACTION) {   // generate_kernel's flattened loop
-                        const f3 pos = o + d * t;
-                        ++trips;
-                        if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) break;
+            while (going) {
+                ++trips;
+                bool sample = false, stop = false;   // stop: this iteration's march ends with cnt < 8
+                if constexpr (LIN) {
+                    const f3 pos = o + d * t;
+                    if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) {
+                        stop = true;
+                    } else {
                         bool occ;
                         if constexpr (BRICK) occ = occupied_brick_c(pos, occ_lds, oc);
                         else occ = occupied_linear_c(pos, vol.occ_linear, oc);
-                        if (occ) {
-                            tb[(size_t)(tot + cnt) * n_alive] = t;
-                            if (cnt == 0) first = t;
-                            tl = t;
-                            t += calc_dt(t, 0.0f);
-                            ++cnt;
-                        } else {
-                            t = dda_step_linear(t, pos, idir, hs);
-                        }
+                        if (occ) sample = true;
+                        else t = dda_step_linear(t, pos, idir, hs);
                     }
                 } else {
-#pragma unroll 1
-                    while (cnt < MAX_STEPS_BETWEEN_COMPACTION) {
-                        ++trips;
-                        if (occ_step(t, cone, o, d, idir, 0, vol.max_mip, vol)) {
-                            if (t >= MAX_DEPTH) break;
-                            tb[(size_t)(tot + cnt) * n_alive] = t;
-                            if (cnt == 0) first = t;
-                            tl = t;
-                            t += calc_dt(t, cone);
-                            ++cnt;
-                        }
+                    if (occ_step(t, cone, o, d, idir, 0, vol.max_mip, vol)) {
+                        if (t >= MAX_DEPTH) stop = true;
+                        else sample = true;
                     }
                 }
-                const uint32_t ru = (!a.mode.ngp && cnt > 0 && first == prev) ? 1u : 0u;
-                rbits |= ru << it;
-                tot += cnt;
-                nnet += cnt - ru;
-                ++n_it;
-                cnt_last = cnt;
-                if (cnt < MAX_STEPS_BETWEEN_COMPACTION) break;   // the ray ends in this iteration
-                prev = tl;
-                if (!a.mode.ngp) {   // the compositor's t reset (574) on the iteration's last sample
-                    const f3 wp = ((o + d * tl) - vol.train_aabb.lo) / wdiag;
-                    const f3 pos = vol.train_aabb.lo + wp * wdiag;
-                    t = dot(a.cam.c2, pos - a.cam.c3) / dfw;
+                if (sample) {
+                    tb[(size_t)(tot + cnt) * n_alive] = t;
+                    if (cnt == 0) first = t;
+                    tl = t;
+                    t += LIN ? calc_dt(t, 0.0f) : calc_dt(t, cone);
+                    ++cnt;
+                }
+                if (stop || cnt == MAX_STEPS_BETWEEN_COMPACTION) {   // the iteration's samples are complete
+                    const uint32_t ru = (!a.mode.ngp && cnt > 0 && first == prev) ? 1u : 0u;
+                    rbits |= ru << it;
+                    tot += cnt;
+                    nnet += cnt - ru;
+                    ++n_it;
+                    cnt_last = cnt;
+                    if (cnt < MAX_STEPS_BETWEEN_COMPACTION || it + 1 == K) {
+                        going = false;   // the ray ends in this iteration, or the round's look-ahead does
+                    } else {
+                        prev = tl;
+                        if (!a.mode.ngp) {   // the compositor's t reset (574) on the iteration's last sample
+                            const f3 wp = ((o + d * tl) - vol.train_aabb.lo) / wdiag;
+                            const f3 pos = vol.train_aabb.lo + wp * wdiag;
+                            t = dot(a.cam.c2, pos - a.cam.c3) / dfw;
+                        }
+                        ++it;
+                        cnt = 0;
+                        first = qnan;
+                    }
                 }
             }
             // trace keeps generate's t (836): the survivors' next start
