@@ -362,11 +362,12 @@ const std::map<std::string, double>& default_params() {
         {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
         {"nerf_fused_after", 1},                // ... after this many whole-GPU wavefront iterations (1: the one big
                                                 //   uncontended network launch, then the ray-local tail; measured best)
-        {"nerf_spec_rounds", 4},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
+        {"nerf_spec_rounds", 2},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
         {"nerf_spec_budget", 1048576},          // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax))
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
         {"nerf_spec_rt_gate", 1},
         {"nerf_spec_debug", 0},
+        {"nerf_spec_prepare", 1},               // sample-parallel activations before the spec compositor (exact; 0: in the chain)
         {"occ_lds_kb", 64},
         {"load_optimizer_state", 1},            // sng_load_snapshot restores a snapshot's optimizer state (0: inference model only)
         {"optimizer_state_loaded", -1},         // set by sng_load_snapshot: 1 restored, 0 skipped / malformed, -1 none in the file                     // LDS budget for the occupancy bricks in the linear marchers (0: global loads)                 // 1: spec_generate records per-ray march trips / cycles (sng_frame_buffer "spec_dbg")               // 1: the raytracer starts after the speculative rounds (they get the whole GPU)
@@ -458,6 +459,7 @@ struct sng_ctx {
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
     DevBuf spec_dbg;                       // nerf_spec_debug: per round and ray {trips, samples, cycles, K}
+    DevBuf spec_pre, spec_pre_depth;       // spec_prepare: per network sample {rgb, alpha} and depth
     DevBuf band_rgba8;                     // sng_gather_rgba8: this rank's band as RGBA8
     uint32_t spec_rounds = 0;              // rounds enqueued by the last trace
     DevBuf rt_counts;                      // rt_count frames: path / shadow kernel {queries, box tests, triangle tests}
@@ -641,7 +643,7 @@ Volume make_volume(const sng_ctx* c) {
     v.occ_linear = c->d_occ_linear.as<uint32_t>();
     v.linear = (c->max_cascade == 0 && c->cone <= 1e-5f && c->p("linear_marcher") != 0.0) ? 1 : 0;
     // the bricks in LDS when they fit the budget (lego: 521 bricks, 41 KiB)
-    const uint32_t words = (OCC_BRICK_TABLE_WORDS + 16u * c->occ_brick_n + 3u) & ~3u;
+    const uint32_t words = (OCC_BRICK_TABLE_WORDS + 16u * std::max(1u, c->occ_brick_n) + 3u) & ~3u;   // >= 1 brick: branch-free readers
     if (v.linear && c->d_occ_brick.p && !c->occ_brick_dirty && c->p("occ_lds_kb") * 1024.0 >= 4.0 * words) {
         v.occ_brick = c->d_occ_brick.as<uint32_t>();
         v.occ_brick_words = words;
@@ -1210,6 +1212,13 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), c->s_nerf);
             if (rounds) {
                 c->spec_t.ensure(c->sample_cap * 4);
+                // sample-parallel activations ahead of the compositing chain (not for the instant-NGP render modes
+                // whose colour is not the network's: Positions, Depth, AO)
+                const bool pre = c->p("nerf_spec_prepare") != 0.0 && !(mode.ngp && mode.render_mode != 1 && mode.render_mode != 6);
+                if (pre) {
+                    c->spec_pre.ensure(c->sample_cap * 16);
+                    c->spec_pre_depth.ensure(c->sample_cap * 4);
+                }
                 SpecArgs sa{};
                 sa.vol = vol; sa.cam = cam; sa.mode = mode; sa.ctrl = ctrl;
                 sa.budget = (uint32_t)std::min<double>((double)c->sample_cap, std::max(1.0, c->p("nerf_spec_budget")));
@@ -1217,6 +1226,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 sa.coords = c->coords.as<float>(); sa.samp = c->samp.as<uint2>(); sa.tbuf = c->spec_t.as<float>();
                 sa.net_out = c->net_out.as<uint2>();
                 sa.frame_rgba = c->nerf_rgba.as<float4>(); sa.frame_depth = c->nerf_depth.as<float>(); sa.positions = c->nerf_pos.as<float>();
+                sa.pre = pre ? c->spec_pre.as<float4>() : nullptr;
+                sa.pre_depth = pre ? c->spec_pre_depth.as<float>() : nullptr;
                 // rays alive after the head: at most the band's pixels (grid-stride over the device count)
                 const uint32_t sblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 4));
                 const bool dbg = c->p("nerf_spec_debug") != 0.0;
@@ -1236,6 +1247,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                                    P.collect_kernel_times ? c->net_events[2 * net_launches] : nullptr,
                                    P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr);
                     ++net_launches;
+                    if (pre) launch_spec_prepare(sa, (uint32_t)c->n_cus * 4, c->s_nerf);
                     launch_spec_composite(sa, sblocks, c->s_nerf);
                     p ^= 1;
                 }
@@ -1898,7 +1910,7 @@ void ctx_destroy(sng_ctx* c) {
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
-                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->band_rgba8, &c->display_rgb})
+                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1}) (void)hipEventDestroy(e);

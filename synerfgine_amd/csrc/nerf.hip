@@ -503,6 +503,7 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
     if constexpr (BRICK) stage_occ_brick(occ_lds, vol.occ_brick, vol.occ_brick_words);
     const int lane = threadIdx.x & 63;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
+    const f3 rwdiag = mk(recip_rn(wdiag.x), recip_rn(wdiag.y), recip_rn(wdiag.z));
     const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
     const float qnan = __int_as_float(0x7fc00000);
     for (uint32_t blk = blockIdx.x * THREADS; blk < n_alive; blk += gridDim.x * THREADS) {
@@ -515,12 +516,14 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             d = mk(di.x, di.y, di.z);
             const f3 idir = inv(d);
             const float dfw = dot(a.cam.c2, d);
+            const float rdfw = recip_rn(dfw);   // x / dfw as div_by(x, dfw, rdfw): the IEEE quotient (Markstein), fewer ops
             float t = ot.w;
             float prev = a.mode.ngp ? qnan : a.in.lt[i].x;   // the previous iteration's last sample
             OccCache oc;
             uint32_t trips = 0;
             const uint64_t c0 = a.dbg ? (uint64_t)clock64() : 0ull;
             float* tb = a.tbuf + i;
+            const size_t tstride = n_alive;
             // ONE flattened loop over all K iterations: each trip is one DDA step or one sample, and an
             // iteration's end (8 samples, or the march leaving the volume) is handled inside the trip, so a
             // wave runs max(total trips of its lanes) trips, not the sum over iterations of each one's max
@@ -532,15 +535,21 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             while (going) {
                 ++trips;
                 bool sample = false, stop = false;   // stop: this iteration's march ends with cnt < 8
-                if constexpr (LIN) {
+                if constexpr (LIN && BRICK) {
+                    // branch-free trip: both successors formed, the occupancy bit selects (lanes of a wave
+                    // diverge between DDA steps and samples on nearly every trip)
+                    const f3 pos = o + d * t;   // render_aabb_to_local is the identity (launch_spec_generate)
+                    const bool inside = (t < MAX_DEPTH) & aabb_contains_nb(vol.render_aabb, pos);
+                    stop = !inside;
+                    sample = inside & occupied_brick_nb(pos, occ_lds);
+                    const float t_dda = dda_step_linear(t, pos, idir, hs);
+                    if (!stop && !sample) t = t_dda;
+                } else if constexpr (LIN) {
                     const f3 pos = o + d * t;
                     if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) {
                         stop = true;
                     } else {
-                        bool occ;
-                        if constexpr (BRICK) occ = occupied_brick_c(pos, occ_lds, oc);
-                        else occ = occupied_linear_c(pos, vol.occ_linear, oc);
-                        if (occ) sample = true;
+                        if (occupied_linear_c(pos, vol.occ_linear, oc)) sample = true;
                         else t = dda_step_linear(t, pos, idir, hs);
                     }
                 } else {
@@ -550,7 +559,8 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
                     }
                 }
                 if (sample) {
-                    tb[(size_t)(tot + cnt) * n_alive] = t;
+                    *tb = t;
+                    tb += tstride;
                     if (cnt == 0) first = t;
                     tl = t;
                     t += LIN ? calc_dt(t, 0.0f) : calc_dt(t, cone);
@@ -568,9 +578,10 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
                     } else {
                         prev = tl;
                         if (!a.mode.ngp) {   // the compositor's t reset (574) on the iteration's last sample
-                            const f3 wp = ((o + d * tl) - vol.train_aabb.lo) / wdiag;
+                            const f3 q = (o + d * tl) - vol.train_aabb.lo;
+                            const f3 wp = mk(div_by(q.x, wdiag.x, rwdiag.x), div_by(q.y, wdiag.y, rwdiag.y), div_by(q.z, wdiag.z, rwdiag.z));
                             const f3 pos = vol.train_aabb.lo + wp * wdiag;
-                            t = dot(a.cam.c2, pos - a.cam.c3) / dfw;
+                            t = div_by(dot(a.cam.c2, pos - a.cam.c3), dfw, rdfw);
                         }
                         ++it;
                         cnt = 0;
@@ -585,7 +596,8 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
 #else
             const uint32_t loads = 0u;
 #endif
-            if (a.dbg && i < a.dbg_stride) a.dbg[i] = make_uint4(trips, tot | (loads << 16), (uint32_t)((uint64_t)clock64() - c0), K);
+            const uint32_t pix = __float_as_uint(di.w);   // by pixel: rays can be followed across rounds
+            if (a.dbg && pix < a.dbg_stride) a.dbg[pix] = make_uint4(trips, tot | (loads << 16), (uint32_t)((uint64_t)clock64() - c0), __float_as_uint(a.in.rgba[i].w));
         }
         const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], nnet, nullptr, false, nullptr, false, sh_app, lane);
         if (i < n_alive) {
@@ -611,6 +623,35 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
                 }
             }
         }
+    }
+}
+
+// composite_kernel's per-sample activations (nerf_device.cuh:204-264, testbed_nerf.cu:545-556) of one network
+// sample, from its NerfCoordinate (warped position, warped dt) and raw fp16 output: {logistic rgb, alpha}
+// and its depth dot(fwd, pos - cam).  The float expressions of spec_composite_sample, so the same bits.
+__device__ __forceinline__ float4 spec_activate(const Volume& vol, const CamDev& cam, f3 wp, float wdt, uint2 raw, float& depth) {
+    const f3 diag = vol.train_aabb.hi - vol.train_aabb.lo;
+    const f3 pos = vol.train_aabb.lo + wp * diag;
+    const float dt = unwarp_dt(wdt);
+    const float r = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x & 0xffffu));
+    const float g = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x >> 16));
+    const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y & 0xffffu));
+    const float sg = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
+    depth = dot(cam.c2, pos - cam.c3);
+    return make_float4(logistic(r), logistic(g), logistic(b), 1.f - sng_expf(-sng_expf(sg) * dt));
+}
+
+// Sample-parallel half of the compositor: one thread per network sample of the round forms its activations,
+// so the per-ray compositing chain (spec_composite) is only the front-to-back accumulation.
+__global__ __launch_bounds__(256) void spec_prepare_kernel(SpecArgs a) {
+    const int p = a.p;
+    if (a.ctrl->spec_K[p] == 0) return;
+    const uint32_t n = a.ctrl->n_samples[p];
+    for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
+        const float* c = a.coords + (size_t)s * 7;
+        float depth;
+        a.pre[s] = spec_activate(a.vol, a.cam, mk(c[0], c[1], c[2]), c[3], a.net_out[s], depth);
+        a.pre_depth[s] = depth;
     }
 }
 
@@ -676,6 +717,61 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                 my_samples += cnt;
                 my_reused += ru;
                 my_iter = max(my_iter, k0 + it + 1);
+                if (a.pre) {
+                    // activations precomputed per sample (spec_prepare): the iteration's {rgb, alpha} are loaded
+                    // together, the chain accumulates; the cached boundary sample is activated here
+                    float4 pv[MAX_STEPS_BETWEEN_COMPACTION];
+                    float d0 = 0.0f;
+                    const uint32_t ob0 = ob;
+#pragma unroll
+                    for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q)
+                        if (q < cnt && !(ru && q == 0)) pv[q] = a.pre[ob + q - ru];
+                    if (ru) {
+                        const f3 wp = ((o + d * lt) - vol.train_aabb.lo) / diag;   // generate_kernel's coordinate of t = lt
+                        pv[0] = spec_activate(vol, cam, wp, warp_dt(calc_dt(lt, vol.ss)), lraw, d0);
+                    }
+                    ob += cnt - ru;
+                    uint32_t j = 0, jd = 0;   // jd: the sample whose depth the payload keeps
+                    bool any_depth = false;
+#pragma unroll
+                    for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
+                        if (q >= cnt) break;
+                        j = q + 1;
+                        const float4 v = pv[q];
+                        const float T = 1.f - rgba.w;
+                        const float weight = v.w * T;
+                        rgba.x += v.x * weight;
+                        rgba.y += v.y * weight;
+                        rgba.z += v.z * weight;
+                        rgba.w += weight;
+                        if (mode.ngp) {
+                            if (weight > mw) { mw = weight; jd = q; any_depth = true; }
+                        } else {
+                            jd = q;
+                            any_depth = true;
+                        }
+                        if (rgba.w > (1.0f - vol.min_transmittance)) {
+                            const float aa = rgba.w;
+                            rgba.x /= aa; rgba.y /= aa; rgba.z /= aa; rgba.w /= aa;
+                            j = q;
+                            break;
+                        }
+                    }
+                    if (any_depth) depth = (ru && jd == 0) ? d0 : a.pre_depth[ob0 + jd - ru];
+                    if (!mode.ngp) ot.w = depth / dot(cam.c2, d);   // payload.t reset (574)
+                    if (j < MAX_STEPS_BETWEEN_COMPACTION) {
+                        hit = !last && rgba.w > 0.001f;
+                        death_step = j + istep;
+                        ended = true;
+                    } else if (last) {
+                        ended = true;
+                    } else {
+                        lt = a.tbuf[(size_t)(s + MAX_STEPS_BETWEEN_COMPACTION - 1) * n_alive + i];   // the next iteration's boundary cache
+                        lraw = a.net_out[ob - 1];   // the iteration's last sample is evaluated (8 samples, at most 1 reused)
+                        s += cnt;
+                    }
+                    continue;
+                }
                 // the iteration's t's and outputs are loaded together, ahead of the compositing chain
                 float tv[MAX_STEPS_BETWEEN_COMPACTION];
                 uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
@@ -957,13 +1053,16 @@ void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode,
     else hipLaunchKernelGGL(composite_kernel<256>, dim3(blocks), dim3(256), 0, s, v, cam, mode, sched, in, out, ctrl, p, target, iter, coords, samp, net_out, fb, depth, pos);
 }
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
-    if (a.vol.linear && a.vol.occ_brick_words)
+    if (a.vol.linear && a.vol.occ_brick_words && a.vol.to_local_identity)
         hipLaunchKernelGGL(HIP_KERNEL_NAME(spec_generate_kernel<true, true>), dim3(blocks), dim3(256), a.vol.occ_brick_words * 4, s, a);
     else if (a.vol.linear) hipLaunchKernelGGL(HIP_KERNEL_NAME(spec_generate_kernel<true, false>), dim3(blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(spec_generate_kernel<false, false>), dim3(blocks), dim3(256), 0, s, a);
 }
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_composite_kernel<256>, dim3(blocks), dim3(256), 0, s, a);
+}
+void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
+    hipLaunchKernelGGL(spec_prepare_kernel, dim3(blocks), dim3(256), 0, s, a);
 }
 void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, hipStream_t s) { hipLaunchKernelGGL(tail_prepare_kernel, dim3(1), dim3(64), 0, s, ctrl, work); }
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {

@@ -286,12 +286,15 @@ struct SpecArgs {
     float4* frame_rgba;
     float* frame_depth;
     float* positions;
+    float4* pre;                  // per network sample: {logistic r, g, b, alpha} (spec_prepare; nullptr: the compositor
+    float* pre_depth;             //   activates the raw outputs itself) and dot(fwd, pos - cam)
     uint4* dbg;                   // nerf_spec_debug: per round and ray {march trips, samples, shader cycles, K} (nullptr: off)
     uint32_t dbg_stride;          // rays per round in dbg
 };
 constexpr uint32_t SPEC_KMAX = 16;
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s);
+void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, hipStream_t s);
 
 // nerf.hip

@@ -447,6 +447,28 @@ __device__ __forceinline__ bool occupied_brick_c(f3 pos, const uint32_t* lds, Oc
     }
     return (c.bits >> ((((uint32_t)iy & 3u) << 3) | ((uint32_t)ix & 7u))) & 1u;
 }
+// the same bit without branches: both LDS reads every call (the second from a clamped slot), the cell's
+// in-grid test and the brick's occupancy folded into the result -- for marcher loops whose lanes diverge
+__device__ __forceinline__ bool occupied_brick_nb(f3 pos, const uint32_t* lds) {
+    f3 q = ((pos - splat(0.5f)) + splat(0.5f)) * (float)GRID_SIZE;   // cascaded_grid_idx_at, mip 0
+    const int ix = (int)q.x, iy = (int)q.y, iz = (int)q.z;
+    const bool in = (uint32_t)ix < GRID_SIZE && (uint32_t)iy < GRID_SIZE && (uint32_t)iz < GRID_SIZE;
+    const uint32_t ux = (uint32_t)ix & (GRID_SIZE - 1), uy = (uint32_t)iy & (GRID_SIZE - 1), uz = (uint32_t)iz & (GRID_SIZE - 1);
+    const uint32_t b = (uz >> 3) * 256u + (uy >> 3) * 16u + (ux >> 3);
+    const uint32_t sub = (uz & 7u) * 2u + ((uy & 7u) >> 2);
+    const uint32_t slot = reinterpret_cast<const uint16_t*>(lds)[b];
+    const uint32_t empty = (uint32_t)(slot == 0xffffu);
+    const uint32_t w = lds[OCC_BRICK_TABLE_WORDS + (slot & (empty - 1u)) * 16u + sub];   // empty brick: slot 0's word, masked
+    const uint32_t bit = (w >> (((uy & 3u) << 3) | (ux & 7u))) & 1u;
+    return (bit & (uint32_t)in & (empty ^ 1u)) != 0u;   // bit operations: no short-circuit branches
+}
+// aabb_contains without short-circuit branches: p >= lo <=> fl(p - lo) >= 0 and p <= hi <=> fl(hi - p) >= 0 (IEEE
+// subtraction keeps the sign and is 0 only for equal operands); p is finite in the marchers
+__device__ __forceinline__ bool aabb_contains_nb(const aabb& b, f3 p) {
+    const float m0 = fminf(fminf(p.x - b.lo.x, p.y - b.lo.y), p.z - b.lo.z);
+    const float m1 = fminf(fminf(b.hi.x - p.x, b.hi.y - p.y), b.hi.z - p.z);
+    return fminf(m0, m1) >= 0.0f;
+}
 // copy the OccBrick blob into LDS (every thread of the block; words padded to a multiple of 4)
 __device__ __forceinline__ void stage_occ_brick(uint32_t* lds, const uint32_t* g, uint32_t words) {
     for (uint32_t k = threadIdx.x * 4u; k < words; k += blockDim.x * 4u) *reinterpret_cast<uint4*>(lds + k) = *reinterpret_cast<const uint4*>(g + k);

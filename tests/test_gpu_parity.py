@@ -546,6 +546,8 @@ def test_fused_nerf_kernel_equals_wavefront(config, ngp_mode):
     ("c3", None, {"nerf_spec_rounds": 2, "nerf_spec_budget": 1 << 22}),      # K = 16: look-ahead past most rays' end
     ("c3", 1, {"nerf_spec_rounds": 4}), ("c3", 6, {"nerf_spec_rounds": 4}), ("c3", 4, {"nerf_spec_rounds": 2, "nerf_spec_kmax": 3}),
     ("c4", None, {"nerf_spec_rounds": 4}), ("c4", None, {"nerf_spec_rounds": 2, "nerf_spec_budget": 1 << 22}),
+    ("c3", None, {"nerf_spec_rounds": 4, "nerf_spec_prepare": 0}), ("c3", 1, {"nerf_spec_rounds": 3, "nerf_spec_prepare": 0}),
+    ("c3", None, {"nerf_spec_rounds": 4, "occ_lds_kb": 0}),               # global occupancy words instead of the LDS bricks
 ])
 def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
     """nerf.hip's speculative tail rounds (each alive ray marched K iterations ahead, one whole-GPU network

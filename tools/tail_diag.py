@@ -39,18 +39,29 @@ for ov in sets:
 if any(ov.get("nerf_spec_debug") for ov in sets):
     import numpy as np
     W, H = eng.resolution()["nerf"]
-    dbg = eng.frame_buffer("spec_dbg", np.uint32).reshape(-1, W * H, 4)
+    dbg = eng.frame_buffer("spec_dbg", np.uint32).reshape(-1, W * H, 4)   # [round][pixel] {trips, samples|loads<<16, cycles, A bits}
+    alive = dbg[:, :, 0] > 0
     for r, d in enumerate(dbg):
-        d = d[d[:, 3] > 0]
-        if len(d) == 0:
+        m = alive[r]
+        if not m.any():
             continue
+        d = d[m]
         cyc = d[:, 2].astype(np.float64)
         tr = d[:, 0].astype(np.float64)
-        ld = (d[:, 1] >> 16).astype(np.float64)
         am = int(np.argmax(tr))
-        print(json.dumps({"round": r, "rays": int(len(d)), "K": int(d[0, 3]), "trips_max": int(tr.max()), "trips_mean": round(tr.mean(), 1),
-                          "loads_of_max": int(ld[am]), "loads_mean": round(ld.mean(), 1),
+        print(json.dumps({"round": r, "rays": int(m.sum()), "trips_max": int(tr.max()), "trips_mean": round(tr.mean(), 1),
                           "trips_p99": float(np.percentile(tr, 99)), "samples_max": int((d[:, 1] & 0xffff).max()), "cycles_max": int(cyc.max()),
-                          "cycles_per_trip_median": round(float(np.median(cyc / np.maximum(tr, 1))), 1),
-                          "cycles_per_trip_of_max": round(float(cyc[np.argmax(tr)] / tr.max()), 1)}))
+                          "cycles_per_trip_of_max": round(float(cyc[am] / tr.max()), 1)}))
+    # rounds of one iteration each (nerf_spec_kmax=1): remaining iterations of the rays alive after the head vs their opacity
+    if alive.shape[0] > 1:
+        a0 = dbg[0, :, 3].view(np.float32)
+        rem = alive.sum(axis=0)
+        m = alive[0]
+        for lo, hi in ((0, 0.05), (0.05, 0.2), (0.2, 0.5), (0.5, 0.8), (0.8, 0.95), (0.95, 1.01)):
+            sel = m & (a0 >= lo) & (a0 < hi)
+            if sel.any():
+                q = rem[sel]
+                print(json.dumps({"A_after_head": [lo, hi], "rays": int(sel.sum()), "iters_mean": round(float(q.mean()), 2),
+                                  "iters_p50": float(np.percentile(q, 50)), "iters_p90": float(np.percentile(q, 90)), "iters_max": int(q.max()),
+                                  "frac_1": round(float((q == 1).mean()), 3)}))
 tb.close()
