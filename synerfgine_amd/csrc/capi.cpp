@@ -390,7 +390,7 @@ struct sng_ctx {
     int device = 0;
     int n_cus = 256;
     hipStream_t s_nerf = nullptr, s_rt = nullptr;
-    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr, ev_fused0 = nullptr, ev_fused1 = nullptr, ev_os0 = nullptr, ev_os1 = nullptr;
+    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr, ev_fused0 = nullptr, ev_fused1 = nullptr, ev_os0 = nullptr, ev_os1 = nullptr, ev_alive = nullptr;
     std::vector<hipEvent_t> net_events;
 
     // model
@@ -643,7 +643,7 @@ Volume make_volume(const sng_ctx* c) {
     v.occ_linear = c->d_occ_linear.as<uint32_t>();
     v.linear = (c->max_cascade == 0 && c->cone <= 1e-5f && c->p("linear_marcher") != 0.0) ? 1 : 0;
     // the bricks in LDS when they fit the budget (lego: 521 bricks, 41 KiB)
-    const uint32_t words = (OCC_BRICK_TABLE_WORDS + 16u * std::max(1u, c->occ_brick_n) + 3u) & ~3u;   // >= 1 brick: branch-free readers
+    const uint32_t words = (OCC_BRICK_HDR_WORDS + 16u * std::max(1u, c->occ_brick_n) + 3u) & ~3u;   // >= 1 brick: branch-free readers
     if (v.linear && c->d_occ_brick.p && !c->occ_brick_dirty && c->p("occ_lds_kb") * 1024.0 >= 4.0 * words) {
         v.occ_brick = c->d_occ_brick.as<uint32_t>();
         v.occ_brick_words = words;
@@ -1104,7 +1104,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     for (int b = 0; b < 2; ++b)
         rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>(),
                  c->ray_lt[b].as<float2>(), c->ray_lo[b].as<uint2>()};
-    launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
+    launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(),
+                     (uint32_t)c->n_cus, c->s_nerf);
     reduce_sched(0);
     const uint32_t n_band = (uint32_t)(tr1 - tr0) * (uint32_t)NW;
     c->fused_last = false;
@@ -1119,11 +1120,19 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     const bool probe = mode.ngp && (mode.render_mode == 2 || mode.render_mode == 10);
     // the glow visualisation is a wavefront-compositor term as well (the fused tail does not carry it)
     const bool wavefront_only = probe || (mode.ngp && mode.glow_mode != 0);
+    // the decision needs the alive count after init_rays; when the tail starts after >= 1 whole-GPU
+    // iteration the host reads it only once that first iteration is queued (no idle GPU while it waits)
+    bool fuse_pending = false;
     if (c->p("nerf_fused") != 0.0 && !wavefront_only) {
         HIPCHK(hipMemcpyAsync(c->h_alive, sched_src, 4, hipMemcpyDeviceToHost, c->s_nerf));
-        HIPCHK(hipStreamSynchronize(c->s_nerf));
-        fuse = (uint64_t)c->h_alive[0] * MAX_STEPS_BETWEEN_COMPACTION <= target;
         fuse_after = (uint32_t)std::max(0.0, c->p("nerf_fused_after"));
+        if (fuse_after == 0) {
+            HIPCHK(hipStreamSynchronize(c->s_nerf));
+            fuse = (uint64_t)c->h_alive[0] * MAX_STEPS_BETWEEN_COMPACTION <= target;
+        } else {
+            HIPCHK(hipEventRecord(c->ev_alive, c->s_nerf));
+            fuse_pending = true;
+        }
     }
     const uint32_t blocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
     const uint32_t max_tiles = (uint32_t)((c->sample_cap + 15) / 16);
@@ -1270,7 +1279,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             const bool beside_rt = iter <= (uint32_t)std::max(0.0, c->p("nerf_fused_after"));
             if (fb < 0) fb = (beside_rt && c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0) ? 2.0 * std::max(1.0, c->p("rt_reserved_cus")) : 0.0;
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused0, c->s_nerf));
-            launch_nerf_fused(fa, c->net, iter == 0 && !rounds ? std::min(c->h_alive[0], n_band) : n_band, (uint32_t)fb, c->s_nerf);
+            launch_nerf_fused(fa, c->net, iter == 0 && !rounds ? std::min(c->h_alive[0], n_band) : n_band, (uint32_t)fb, c->s_nerf, rounds == 0);
             HIPCHK(hipGetLastError());
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused1, c->s_nerf));
             HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
@@ -1279,7 +1288,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         }
         for (int k = 0; k < CHUNK && !(fuse && iter >= fuse_after); ++k, ++iter) {
             launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), gen_blocks, mode.ngp, a.sched.global, c->s_nerf,
-                            !fuse && c->p("nerf_gen_wide") != 0.0);
+                            !fuse && !fuse_pending && c->p("nerf_gen_wide") != 0.0);
             if (P.collect_kernel_times) {
                 while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
             }
@@ -1293,9 +1302,14 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));   // render_frame starts the raytracer after the head's network
             ++net_launches;
             launch_composite(vol, cam, mode, a.sched, rb[p], rb[p ^ 1], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), c->net_out.as<uint2>(),
-                             c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf, !fuse);
+                             c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), blocks, c->s_nerf, !fuse && !fuse_pending);
             reduce_sched(p ^ 1);
             p ^= 1;
+            if (fuse_pending) {   // the first iteration is queued: now wait for init_rays' alive count
+                HIPCHK(hipEventSynchronize(c->ev_alive));
+                fuse = (uint64_t)c->h_alive[0] * MAX_STEPS_BETWEEN_COMPACTION <= target;
+                fuse_pending = false;
+            }
         }
         // readback of the alive count after this chunk; check the previous chunk's (already landed)
         HIPCHK(hipMemcpyAsync(&c->h_alive[2 * (chunk & 1)], sched_src, 8, hipMemcpyDeviceToHost, c->s_nerf));
@@ -1887,7 +1901,7 @@ void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_nerf, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_rt, hipStreamNonBlocking, prio_lo));
-    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go, &c->ev_fused0, &c->ev_fused1, &c->ev_os0, &c->ev_os1}) HIPCHK(hipEventCreate(e));
+    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go, &c->ev_fused0, &c->ev_fused1, &c->ev_os0, &c->ev_os1, &c->ev_alive}) HIPCHK(hipEventCreate(e));
     HIPCHK(hipHostMalloc((void**)&c->h_ctrl, sizeof(MarchCtrl), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&c->h_alive, 8 * sizeof(uint32_t), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&c->h_os, sizeof(OnestepState), hipHostMallocDefault));
@@ -1913,7 +1927,7 @@ void ctx_destroy(sng_ctx* c) {
                       &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); }
-    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1}) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1, c->ev_alive}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);

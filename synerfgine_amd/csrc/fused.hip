@@ -739,8 +739,8 @@ __global__ void fused_prepare_kernel(MarchCtrl* ctrl, uint32_t* work) {
     if (threadIdx.x == 0) *work = 0;
 }
 
-void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s) {
-    hipLaunchKernelGGL(fused_prepare_kernel, dim3(1), dim3(64), 0, s, a.ctrl, a.work);
+void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s, bool prepare) {
+    if (prepare) hipLaunchKernelGGL(fused_prepare_kernel, dim3(1), dim3(64), 0, s, a.ctrl, a.work);   // else launch_tail_prepare did it
     const uint32_t waves_needed = (n_rays_hint + a.lanes - 1) / a.lanes;
     const uint32_t cap = max_blocks ? max_blocks : (uint32_t)net.n_cus * 2;
     const uint32_t blocks = std::max(1u, std::min((waves_needed + FUSED_WAVES - 1) / FUSED_WAVES, cap));

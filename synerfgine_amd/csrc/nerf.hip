@@ -19,6 +19,8 @@
 // n_steps = clamp(2^21 / n_alive, 1, 8) and the payload.t reset to the last
 // sample (composite_kernel_nerf_alt:574) are reproduced exactly, so per-pixel
 // results follow the reference's schedule.
+#include <algorithm>
+
 #include "sng_internal.h"
 #include "sng_math.h"
 
@@ -64,67 +66,92 @@ __device__ __forceinline__ uint32_t block_append(uint32_t* counter, uint32_t v, 
 // ---------------------------------------------------------------------------
 // init_rays_with_payload_kernel_nerf + advance_pos_nerf + first compaction
 // ---------------------------------------------------------------------------
+// BRICK: the march to the first occupied voxel reads the occupancy bricks staged in LDS (one copy per
+// workgroup of a persistent grid striding over the pixels) with branch-free trips; otherwise one thread per
+// pixel with the linear / cascaded marcher.
+template <bool BRICK>
 __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf out, MarchCtrl* ctrl, float4* __restrict__ frame_rgba,
                                                         float* __restrict__ frame_depth, float* __restrict__ positions,
-                                                        float* __restrict__ normals) {
+                                                        float* __restrict__ normals, uint32_t n_threads) {
+    extern __shared__ uint32_t occ_lds[];
+    __shared__ uint32_t sh_app[16];
+    if constexpr (BRICK) stage_occ_brick(occ_lds, a.vol.occ_brick, a.vol.occ_brick_words);
     const int lane = threadIdx.x & 63;
     const uint32_t n_band = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    bool alive = false;
-    f3 origin = a.cam.c3, dir = splat(0.0f);
-    float tt = 0.0f;
-    uint32_t idx = 0;
-    int x, y;
-    bool in_band;
-    if (a.ray_tile > 0) {   // thread -> pixel in T x T tiles, tiles row-major over the band
-        const uint32_t T = (uint32_t)a.ray_tile, tiles_x = ((uint32_t)a.W + T - 1) / T, tile = t / (T * T), w = t % (T * T);
-        x = (int)((tile % tiles_x) * T + w % T);
-        y = a.row0 + (int)((tile / tiles_x) * T + w / T);
-        in_band = x < a.W && y < a.row1;
-    } else {
-        x = (int)(t % (uint32_t)a.W);
-        y = a.row0 + (int)(t / (uint32_t)a.W);
-        in_band = t < n_band;
-    }
-    if (in_band) {
-        idx = (uint32_t)x + (uint32_t)a.W * (uint32_t)y;
-        f2 off = ld_random_pixel_offset(a.snap ? 0u : a.spp);
-        f2 uv = {((float)x + off.x) / (float)a.W, ((float)y + off.y) / (float)a.H};
-        // get_xform_given_rolling_shutter (testbed_nerf.cu:1895, common_device.cuh:361-368)
-        const float* rs = a.rolling_shutter;
-        const float pixel_t = rs[0] + rs[1] * uv.x + rs[2] * uv.y + rs[3] * ld_random_val0(a.spp, idx * 72239731u);
-        origin = a.cam.c3 + (a.pos1 - a.cam.c3) * pixel_t;
-        // uv_to_ray (common_device.cuh:403-470): pinhole, no lens/foveation/parallax/aperture
-        f3 d = mk((uv.x - a.screen_center.x) * (float)a.W / a.focal.x, (uv.y - a.screen_center.y) * (float)a.H / a.focal.y, 1.0f);
-        d = mul(shutter_rotation(a.q0, a.q1, pixel_t), d);
-        float4 fb = frame_rgba[idx];
-        fb.x = 0.0f; fb.y = 0.0f; fb.z = 0.0f;
-        if (a.reset) fb.w = 0.0f;
-        frame_rgba[idx] = fb;
-        frame_depth[idx] = MAX_DEPTH;
-        positions[3 * idx + 0] = 0.0f; positions[3 * idx + 1] = 0.0f; positions[3 * idx + 2] = 0.0f;
-        normals[3 * idx + 0] = 0.0f; normals[3 * idx + 1] = 0.0f; normals[3 * idx + 2] = 0.0f;
-        dir = normalize(d);
-        const Volume& v = a.vol;
-        float t0 = fmaxf(aabb_entry(v.render_aabb, to_local(v, origin), to_local(v, dir)), 0.0f) + 1e-6f;
-        if (aabb_contains(v.render_aabb, to_local(v, origin + dir * t0))) {
-            // advance_pos_nerf (testbed_nerf.cu:334-363)
-            f3 idir = inv(dir);
-            float t1 = advance_n_steps(t0, v.cone, ld_random_val0(a.spp, idx * 786433u));
-            t1 = advance_to_occupied(t1, v.cone, origin, dir, idir, 0, v.max_mip, v);
-            if (t1 < MAX_DEPTH) { alive = true; tt = t1; }
+    for (uint32_t base = blockIdx.x * 256u; base < n_threads; base += gridDim.x * 256u) {   // block-uniform trips
+        const uint32_t t = base + threadIdx.x;
+        bool alive = false;
+        f3 origin = a.cam.c3, dir = splat(0.0f);
+        float tt = 0.0f;
+        uint32_t idx = 0;
+        int x, y;
+        bool in_band;
+        if (a.ray_tile > 0) {   // thread -> pixel in T x T tiles, tiles row-major over the band
+            const uint32_t T = (uint32_t)a.ray_tile, tiles_x = ((uint32_t)a.W + T - 1) / T, tile = t / (T * T), w = t % (T * T);
+            x = (int)((tile % tiles_x) * T + w % T);
+            y = a.row0 + (int)((tile / tiles_x) * T + w / T);
+            in_band = t < n_threads && x < a.W && y < a.row1;
+        } else {
+            x = (int)(t % (uint32_t)a.W);
+            y = a.row0 + (int)(t / (uint32_t)a.W);
+            in_band = t < n_band;
         }
-    }
-    __shared__ uint32_t sh_app[16];
-    const uint32_t slot = block_append(&ctrl->n_alive[0], alive ? 1u : 0u, a.sched.global ? &ctrl->n_owned[0] : nullptr,
-                                       alive && idx >= a.sched.own_lo && idx < a.sched.own_hi, nullptr, false, sh_app, lane);
-    if (alive) {
-        out.o_t[slot] = make_float4(origin.x, origin.y, origin.z, tt);
-        out.d_idx[slot] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(idx));
-        out.rgba[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // memset(m_rays[0].rgba) 2102
-        out.depth[slot] = 0.0f;                                // memset(m_rays[0].depth) 2103
-        if (a.mode.ngp) out.mw[slot] = 0.0f;                   // payload.max_weight = 0 (1964)
-        else out.lt[slot] = make_float2(__int_as_float(0x7fc00000), 0.0f);   // no cached boundary sample yet
+        if (in_band) {
+            idx = (uint32_t)x + (uint32_t)a.W * (uint32_t)y;
+            f2 off = ld_random_pixel_offset(a.snap ? 0u : a.spp);
+            f2 uv = {((float)x + off.x) / (float)a.W, ((float)y + off.y) / (float)a.H};
+            // get_xform_given_rolling_shutter (testbed_nerf.cu:1895, common_device.cuh:361-368)
+            const float* rs = a.rolling_shutter;
+            const float pixel_t = rs[0] + rs[1] * uv.x + rs[2] * uv.y + rs[3] * ld_random_val0(a.spp, idx * 72239731u);
+            origin = a.cam.c3 + (a.pos1 - a.cam.c3) * pixel_t;
+            // uv_to_ray (common_device.cuh:403-470): pinhole, no lens/foveation/parallax/aperture
+            f3 d = mk((uv.x - a.screen_center.x) * (float)a.W / a.focal.x, (uv.y - a.screen_center.y) * (float)a.H / a.focal.y, 1.0f);
+            d = mul(shutter_rotation(a.q0, a.q1, pixel_t), d);
+            float4 fb = frame_rgba[idx];
+            fb.x = 0.0f; fb.y = 0.0f; fb.z = 0.0f;
+            if (a.reset) fb.w = 0.0f;
+            frame_rgba[idx] = fb;
+            frame_depth[idx] = MAX_DEPTH;
+            positions[3 * idx + 0] = 0.0f; positions[3 * idx + 1] = 0.0f; positions[3 * idx + 2] = 0.0f;
+            normals[3 * idx + 0] = 0.0f; normals[3 * idx + 1] = 0.0f; normals[3 * idx + 2] = 0.0f;
+            dir = normalize(d);
+            const Volume& v = a.vol;
+            float t0 = fmaxf(aabb_entry(v.render_aabb, to_local(v, origin), to_local(v, dir)), 0.0f) + 1e-6f;
+            if (aabb_contains(v.render_aabb, to_local(v, origin + dir * t0))) {
+                // advance_pos_nerf (testbed_nerf.cu:334-363)
+                f3 idir = inv(dir);
+                float t1 = advance_n_steps(t0, v.cone, ld_random_val0(a.spp, idx * 786433u));
+                if constexpr (BRICK) {
+                    // advance_to_occupied_linear through the LDS bricks, one DDA step per trip, no branch but the exits
+                    const f3 hs = half_sign(dir);
+                    // past t_last the line meets no occupied cell (path_last_occupied_t): the walk's end is known
+                    const float t_last = path_last_occupied_t(origin, dir, idir, t1, occ_lds);
+#pragma unroll 1
+                    while (true) {
+                        const f3 pos = origin + dir * t1;
+                        const bool inside = (t1 < MAX_DEPTH) & (t1 <= t_last) & aabb_contains_nb(v.render_aabb, pos);
+                        const bool occ = inside & occupied_brick_nb(pos, occ_lds);
+                        const float tn = dda_step_linear(t1, pos, idir, hs);
+                        if (!inside) { t1 = MAX_DEPTH; break; }
+                        if (occ) break;
+                        t1 = tn;
+                    }
+                } else {
+                    t1 = advance_to_occupied(t1, v.cone, origin, dir, idir, 0, v.max_mip, v);
+                }
+                if (t1 < MAX_DEPTH) { alive = true; tt = t1; }
+            }
+        }
+        const uint32_t slot = block_append(&ctrl->n_alive[0], alive ? 1u : 0u, a.sched.global ? &ctrl->n_owned[0] : nullptr,
+                                           alive && idx >= a.sched.own_lo && idx < a.sched.own_hi, nullptr, false, sh_app, lane);
+        if (alive) {
+            out.o_t[slot] = make_float4(origin.x, origin.y, origin.z, tt);
+            out.d_idx[slot] = make_float4(dir.x, dir.y, dir.z, __uint_as_float(idx));
+            out.rgba[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // memset(m_rays[0].rgba) 2102
+            out.depth[slot] = 0.0f;                                // memset(m_rays[0].depth) 2103
+            if (a.mode.ngp) out.mw[slot] = 0.0f;                   // payload.max_weight = 0 (1964)
+            else out.lt[slot] = make_float2(__int_as_float(0x7fc00000), 0.0f);   // no cached boundary sample yet
+        }
     }
 }
 
@@ -138,10 +165,11 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
 // distances of a ray go to LDS instead of 8 live registers, which keeps the kernel small
 // and at high occupancy (the DDA walk is latency bound: many waves in flight hide the
 // bitfield gathers).  The general path (cascades / cone stepping) keeps the unrolled form.
-template <bool LIN, int THREADS = 256>
+template <bool LIN, int THREADS = 256, bool BRICK = false>
 __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter,
                                                        float* __restrict__ coords, uint2* __restrict__ samp, int store_t, int global_sched) {
     __shared__ float ts_lds[MAX_STEPS_BETWEEN_COMPACTION * THREADS];
+    extern __shared__ uint32_t occ_lds[];
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t n_sched = global_sched ? ctrl->sched_alive[p] : n_alive;   // Sched
     const uint32_t i_step = ctrl->i_step[p];
@@ -158,6 +186,10 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
         }
     }
     if (!active) return;
+    if constexpr (BRICK) {
+        if (blockIdx.x * blockDim.x >= n_alive) return;
+        stage_occ_brick(occ_lds, vol.occ_brick, vol.occ_brick_words);
+    }
     const int lane = threadIdx.x & 63;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
     const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
@@ -178,7 +210,29 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
             // sample lands on the same t, its NerfCoordinate is bit-identical and so is the network output
             const float lt0 = store_t ? __int_as_float(0x7fc00000) : rays.lt[i].x;
             float tl = 0.0f;
-            if constexpr (LIN) {
+            if constexpr (LIN && BRICK) {
+                // the same loop through the LDS occupancy bricks, branch-free but for the exits; past t_last no
+                // occupied cell is left on the ray (path_last_occupied_t), so the march ends there
+                const f3 hs = half_sign(d);
+                const float t_last = path_last_occupied_t(o, d, idir, t, occ_lds);
+#pragma unroll 1
+                while (cnt < n_steps) {
+                    const f3 pos = o + d * t;
+                    const bool inside = (t < MAX_DEPTH) & (t <= t_last) & aabb_contains_nb(vol.render_aabb, pos);
+                    const bool occ = inside & occupied_brick_nb(pos, occ_lds);
+                    const float tn = dda_step_linear(t, pos, idir, hs);
+                    if (!inside) break;
+                    if (occ) {
+                        if (cnt == 0 && t == lt0) reuse = true;
+                        ts_lds[cnt * THREADS + threadIdx.x] = t;
+                        tl = t;
+                        t += calc_dt(t, 0.0f);
+                        ++cnt;
+                    } else {
+                        t = tn;
+                    }
+                }
+            } else if constexpr (LIN) {
                 // advance_to_occupied_linear + sample, flattened into ONE loop: each trip either
                 // records a sample (occupied voxel) or takes one DDA step, so a lane's cost is its
                 // own total step count instead of the wave's worst walk summed over all 8 samples.
@@ -531,6 +585,9 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             float first = qnan, tl = 0.0f;
             const f3 hs = half_sign(d);
             bool going = true;
+            // the t reset only moves t back to the last sample, so one bound serves the whole round
+            float t_last = 3.0e38f;
+            if constexpr (LIN && BRICK) t_last = path_last_occupied_t(o, d, idir, fminf(t, prev == prev ? prev : t), occ_lds);
 #pragma unroll 1
             while (going) {
                 ++trips;
@@ -539,7 +596,7 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
                     // branch-free trip: both successors formed, the occupancy bit selects (lanes of a wave
                     // diverge between DDA steps and samples on nearly every trip)
                     const f3 pos = o + d * t;   // render_aabb_to_local is the identity (launch_spec_generate)
-                    const bool inside = (t < MAX_DEPTH) & aabb_contains_nb(vol.render_aabb, pos);
+                    const bool inside = (t < MAX_DEPTH) & (t <= t_last) & aabb_contains_nb(vol.render_aabb, pos);
                     stop = !inside;
                     sample = inside & occupied_brick_nb(pos, occ_lds);
                     const float t_dda = dda_step_linear(t, pos, idir, hs);
@@ -705,34 +762,46 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
             const uint32_t n_it = sc.y & 31u, cnt_last = (sc.y >> 5) & 15u, rbits = sc.y >> 9;
             uint32_t ob = sc.x, s = 0;
             bool ended = false;
-            for (uint32_t it = 0; it < n_it && !ended; ++it) {
-                const uint32_t cnt = it + 1 == n_it ? cnt_last : MAX_STEPS_BETWEEN_COMPACTION;
-                const uint32_t ru = (rbits >> it) & 1u;
-                const uint32_t istep = istep0 + MAX_STEPS_BETWEEN_COMPACTION * it;
-                const bool last = istep + MAX_STEPS_BETWEEN_COMPACTION >= MARCH_ITER;
-                if (k0 + it < 64) {
-                    atomicAdd(&hist_alive[k0 + it], 1u);
-                    if (cnt) atomicAdd(&hist_samples[k0 + it], cnt);
+            if (a.pre) {
+                // activations precomputed per sample (spec_prepare).  The chain only accumulates; the next
+                // iteration's {rgb, alpha} are loaded while this one composites.  A reused boundary sample is the
+                // previous iteration's last one (same t, coordinate and output), so it reuses that activation;
+                // the round's first is activated from the ray's cache.  The payload's depth sample is resolved
+                // once at the ray's end of round (its t reset and extraction need nothing earlier).
+                float4 pv[MAX_STEPS_BETWEEN_COMPACTION], pn[MAX_STEPS_BETWEEN_COMPACTION];
+                float4 carry = make_float4(0, 0, 0, 0);
+                float d_carry = 0.0f;
+                if (rbits & 1u) {   // round start: the ray's cached boundary sample (lt, lraw)
+                    const f3 wp = ((o + d * lt) - vol.train_aabb.lo) / diag;   // generate_kernel's coordinate of t = lt
+                    carry = spec_activate(vol, cam, wp, warp_dt(calc_dt(lt, vol.ss)), lraw, d_carry);
                 }
-                my_samples += cnt;
-                my_reused += ru;
-                my_iter = max(my_iter, k0 + it + 1);
-                if (a.pre) {
-                    // activations precomputed per sample (spec_prepare): the iteration's {rgb, alpha} are loaded
-                    // together, the chain accumulates; the cached boundary sample is activated here
-                    float4 pv[MAX_STEPS_BETWEEN_COMPACTION];
-                    float d0 = 0.0f;
-                    const uint32_t ob0 = ob;
+                auto load_it = [&](uint32_t it_, uint32_t ob_, float4* dst) {
+                    const uint32_t cnt_ = it_ + 1 == n_it ? cnt_last : MAX_STEPS_BETWEEN_COMPACTION;
+                    const uint32_t ru_ = (rbits >> it_) & 1u;
 #pragma unroll
                     for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q)
-                        if (q < cnt && !(ru && q == 0)) pv[q] = a.pre[ob + q - ru];
-                    if (ru) {
-                        const f3 wp = ((o + d * lt) - vol.train_aabb.lo) / diag;   // generate_kernel's coordinate of t = lt
-                        pv[0] = spec_activate(vol, cam, wp, warp_dt(calc_dt(lt, vol.ss)), lraw, d0);
+                        if (q < cnt_ && !(ru_ && q == 0)) dst[q] = a.pre[ob_ + q - ru_];
+                };
+                if (n_it) load_it(0, ob, pv);
+                int64_t dsel = -2;   // the depth sample: -2 none, -1 the round's cached boundary sample, else its network index
+                uint32_t last_net = 0;
+                for (uint32_t it = 0; it < n_it && !ended; ++it) {
+                    const uint32_t cnt = it + 1 == n_it ? cnt_last : MAX_STEPS_BETWEEN_COMPACTION;
+                    const uint32_t ru = (rbits >> it) & 1u;
+                    const uint32_t istep = istep0 + MAX_STEPS_BETWEEN_COMPACTION * it;
+                    const bool last = istep + MAX_STEPS_BETWEEN_COMPACTION >= MARCH_ITER;
+                    if (k0 + it < 64) {
+                        atomicAdd(&hist_alive[k0 + it], 1u);
+                        if (cnt) atomicAdd(&hist_samples[k0 + it], cnt);
                     }
+                    my_samples += cnt;
+                    my_reused += ru;
+                    my_iter = max(my_iter, k0 + it + 1);
+                    const uint32_t ob0 = ob;
                     ob += cnt - ru;
-                    uint32_t j = 0, jd = 0;   // jd: the sample whose depth the payload keeps
-                    bool any_depth = false;
+                    if (it + 1 < n_it) load_it(it + 1, ob, pn);   // in flight while this iteration composites
+                    if (ru) pv[0] = carry;
+                    uint32_t j = 0;
 #pragma unroll
                     for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
                         if (q >= cnt) break;
@@ -744,11 +813,11 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                         rgba.y += v.y * weight;
                         rgba.z += v.z * weight;
                         rgba.w += weight;
+                        const int64_t sel = (ru && q == 0) ? (it == 0 ? -1 : (int64_t)last_net) : (int64_t)(ob0 + q - ru);
                         if (mode.ngp) {
-                            if (weight > mw) { mw = weight; jd = q; any_depth = true; }
+                            if (weight > mw) { mw = weight; dsel = sel; }
                         } else {
-                            jd = q;
-                            any_depth = true;
+                            dsel = sel;
                         }
                         if (rgba.w > (1.0f - vol.min_transmittance)) {
                             const float aa = rgba.w;
@@ -757,8 +826,6 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                             break;
                         }
                     }
-                    if (any_depth) depth = (ru && jd == 0) ? d0 : a.pre_depth[ob0 + jd - ru];
-                    if (!mode.ngp) ot.w = depth / dot(cam.c2, d);   // payload.t reset (574)
                     if (j < MAX_STEPS_BETWEEN_COMPACTION) {
                         hit = !last && rgba.w > 0.001f;
                         death_step = j + istep;
@@ -766,12 +833,33 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                     } else if (last) {
                         ended = true;
                     } else {
-                        lt = a.tbuf[(size_t)(s + MAX_STEPS_BETWEEN_COMPACTION - 1) * n_alive + i];   // the next iteration's boundary cache
-                        lraw = a.net_out[ob - 1];   // the iteration's last sample is evaluated (8 samples, at most 1 reused)
+                        carry = pv[MAX_STEPS_BETWEEN_COMPACTION - 1];   // the next iteration's boundary sample
+                        last_net = ob - 1;                              // its network index (8 samples, at most 1 reused)
                         s += cnt;
+#pragma unroll
+                        for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) pv[q] = pn[q];
                     }
-                    continue;
                 }
+                if (!ended && n_it) {   // survivor: the boundary cache of the next round (the last sample, evaluated)
+                    lt = a.tbuf[(size_t)(s - 1) * n_alive + i];
+                    lraw = a.net_out[last_net];
+                }
+                if (dsel >= 0) depth = a.pre_depth[dsel];
+                else if (dsel == -1) depth = d_carry;
+                if (!mode.ngp && n_it) ot.w = depth / dot(cam.c2, d);   // payload.t reset (574)
+            }
+            for (uint32_t it = 0; it < n_it && !ended && !a.pre; ++it) {
+                const uint32_t cnt = it + 1 == n_it ? cnt_last : MAX_STEPS_BETWEEN_COMPACTION;
+                const uint32_t ru = (rbits >> it) & 1u;
+                const uint32_t istep = istep0 + MAX_STEPS_BETWEEN_COMPACTION * it;
+                const bool last = istep + MAX_STEPS_BETWEEN_COMPACTION >= MARCH_ITER;
+                if (k0 + it < 64) {
+                    atomicAdd(&hist_alive[k0 + it], 1u);
+                    if (cnt) atomicAdd(&hist_samples[k0 + it], cnt);
+                }
+                my_samples += cnt;
+                my_reused += ru;
+                my_iter = max(my_iter, k0 + it + 1);
                 // the iteration's t's and outputs are loaded together, ahead of the compositing chain
                 float tv[MAX_STEPS_BETWEEN_COMPACTION];
                 uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
@@ -985,7 +1073,7 @@ __global__ __launch_bounds__(1024) void occ_brick_scan_kernel(const uint32_t* __
         __syncthreads();
     }
     uint32_t slot = ps[t] - sum;
-    uint16_t* tab = reinterpret_cast<uint16_t*>(blob);
+    uint16_t* tab = reinterpret_cast<uint16_t*>(blob + OCC_BRICK_TAB);
     const uint32_t fl[4] = {f0, f1, f2, f3v};
     for (int k = 0; k < 4; ++k) {
         tab[4 * t + k] = fl[k] ? (uint16_t)slot : (uint16_t)0xffffu;
@@ -997,13 +1085,13 @@ __global__ void occ_brick_fill_kernel(const uint32_t* __restrict__ occ, uint32_t
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= 4096 * 16) return;
     const uint32_t b = g >> 4, k = g & 15u;
-    const uint32_t slot = reinterpret_cast<const uint16_t*>(blob)[b];
+    const uint32_t slot = reinterpret_cast<const uint16_t*>(blob + OCC_BRICK_TAB)[b];
     if (slot == 0xffffu) return;
     const uint32_t bz = b >> 8, by = (b >> 4) & 15u, bx = b & 15u;
     const uint32_t z = bz * 8 + (k >> 1), y0 = by * 8 + (k & 1u) * 4;
     uint32_t w = 0;
     for (uint32_t yy = 0; yy < 4; ++yy) w |= ((occ[(z * GRID_SIZE + y0 + yy) * (GRID_SIZE / 32) + (bx >> 2)] >> ((bx & 3u) * 8u)) & 0xffu) << (yy * 8u);
-    blob[OCC_BRICK_TABLE_WORDS + slot * 16u + k] = w;
+    blob[OCC_BRICK_HDR_WORDS + slot * 16u + k] = w;
 }
 
 __global__ void ctrl_init_kernel(MarchCtrl* c) {
@@ -1029,18 +1117,26 @@ __global__ void ctrl_init_kernel(MarchCtrl* c) {
 void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s) { hipLaunchKernelGGL(ctrl_init_kernel, dim3(1), dim3(64), 0, s, ctrl); }
 // ---------------------------------------------------------------------------
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm,
-                      hipStream_t s) {
+                      uint32_t n_cus, hipStream_t s) {
     uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
     if (a.ray_tile > 0) {
         const uint32_t T = (uint32_t)a.ray_tile;
         n = (((uint32_t)a.W + T - 1) / T) * (((uint32_t)(a.row1 - a.row0) + T - 1) / T) * T * T;
     }
-    hipLaunchKernelGGL(init_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, out, ctrl, fb, depth, pos, nrm);
+    const uint32_t blocks = (n + 255) / 256;
+    if (a.vol.linear && a.vol.occ_brick_words && a.vol.to_local_identity && a.vol.bitfield)   // persistent: 3 LDS copies per CU
+        hipLaunchKernelGGL(init_rays_kernel<true>, dim3(std::min(blocks, n_cus * 3u)), dim3(256), a.vol.occ_brick_words * 4, s, a, out, ctrl, fb, depth,
+                           pos, nrm, n);
+    else
+        hipLaunchKernelGGL(init_rays_kernel<false>, dim3(blocks), dim3(256), 0, s, a, out, ctrl, fb, depth, pos, nrm, n);
 }
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
                      uint32_t blocks, int store_t, int global_sched, hipStream_t s, bool wide) {
-    if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
+    if (v.linear && v.occ_brick_words && v.to_local_identity)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(generate_kernel<true, 256, true>), dim3(blocks), dim3(256), v.occ_brick_words * 4, s, v, rays, ctrl, p, target, iter, coords,
+                           samp, store_t, global_sched);
+    else if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
     else if (wide) hipLaunchKernelGGL(HIP_KERNEL_NAME(generate_kernel<false, 1024>), dim3(std::max(1u, blocks / 4u)), dim3(1024), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
     else hipLaunchKernelGGL(generate_kernel<false>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
 }
@@ -1084,7 +1180,24 @@ void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid
                            bf + (size_t)N / 8 * level);
     hipLaunchKernelGGL(bitfield_linear_kernel, dim3(N / 32 / 256), dim3(256), 0, s, bf, occ_linear);
 }
+// dilated brick mask: bit b set when an occupied cell lies in brick b grown by one cell per side.  One
+// thread per (brick, z row of the grown brick); the rows' flags OR into the mask word with an atomic.
+__global__ void occ_brick_dilate_kernel(const uint32_t* __restrict__ occ, uint32_t* __restrict__ blob) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= 4096 * 10) return;
+    const uint32_t b = g / 10, zr = g % 10;
+    const int bz = (int)(b >> 8), by = (int)((b >> 4) & 15u), bx = (int)(b & 15u);
+    const int z = bz * 8 - 1 + (int)zr;
+    if (z < 0 || z > 127) return;
+    const int x0 = max(0, bx * 8 - 1), x1 = min(127, bx * 8 + 8);
+    bool any = false;
+    for (int y = max(0, by * 8 - 1); y <= min(127, by * 8 + 8) && !any; ++y)
+        for (int x = x0; x <= x1 && !any; ++x) any = (occ[((uint32_t)z * GRID_SIZE + (uint32_t)y) * (GRID_SIZE / 32) + ((uint32_t)x >> 5)] >> (x & 31)) & 1u;
+    if (any) atomicOr(&blob[b >> 5], 1u << (b & 31u));
+}
 void launch_occ_brick(const uint32_t* occ_linear, uint32_t* flags, uint32_t* blob, uint32_t* n_bricks, hipStream_t s) {
+    (void)hipMemsetAsync(blob, 0, 128 * 4, s);
+    hipLaunchKernelGGL(occ_brick_dilate_kernel, dim3(4096 * 10 / 256), dim3(256), 0, s, occ_linear, blob);
     hipLaunchKernelGGL(occ_brick_flag_kernel, dim3(16), dim3(256), 0, s, occ_linear, flags);
     hipLaunchKernelGGL(occ_brick_scan_kernel, dim3(1), dim3(1024), 0, s, flags, blob, n_bricks);
     hipLaunchKernelGGL(occ_brick_fill_kernel, dim3(4096 * 16 / 256), dim3(256), 0, s, occ_linear, blob);

@@ -136,7 +136,7 @@ struct FusedArgs {
     int p;                        // ping-pong buffer holding the alive rays (MarchCtrl::n_alive[p], i_step[p])
     uint32_t lanes;               // rays per wave (64; fewer shorten a wave's per-iteration field chain for thin bands)
 };
-void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s);
+void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s, bool prepare = true);
 
 // fused.hip: trace_alt's one-step regime (n_alive > target / 2, so every iteration takes ONE step).
 // A speculative ray-local pass simulates each ray on its own under n_steps = 1 and histograms the
@@ -298,7 +298,8 @@ void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, hipStream_t s);
 
 // nerf.hip
-void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, hipStream_t s);
+void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, uint32_t n_cus,
+                      hipStream_t s);
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
                      uint32_t blocks, int store_t, int global_sched, hipStream_t s, bool wide = false);
 void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const Sched& sched, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p,

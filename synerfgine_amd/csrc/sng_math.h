@@ -392,10 +392,13 @@ struct Volume {
     const uint32_t* occ_brick;
     uint32_t occ_brick_words;
 };
-// OccBrick layout (u32 words): [0, 2048) = u16 slot per brick b = (iz/8)*256 + (iy/8)*16 + ix/8 (0xffff:
-// no occupied cell), then 16 words per occupied brick: word (iz%8)*2 + (iy%8)/4, bit (iy%4)*8 + ix%8.
-constexpr uint32_t OCC_BRICK_TABLE_WORDS = 2048;
-constexpr uint32_t OCC_BRICK_CAP_WORDS = OCC_BRICK_TABLE_WORDS + 4096 * 16;
+// OccBrick layout (u32 words): [0, 128) = 4096-bit "dilated" brick mask (bit b: an occupied cell lies within one
+// cell of brick b -- the conservative test of path_last_occupied_t), [128, 2176) = u16 slot per brick
+// b = (iz/8)*256 + (iy/8)*16 + ix/8 (0xffff: no occupied cell), then 16 words per occupied brick: word
+// (iz%8)*2 + (iy%8)/4, bit (iy%4)*8 + ix%8.
+constexpr uint32_t OCC_BRICK_TAB = 128;
+constexpr uint32_t OCC_BRICK_HDR_WORDS = OCC_BRICK_TAB + 2048;
+constexpr uint32_t OCC_BRICK_CAP_WORDS = OCC_BRICK_HDR_WORDS + 4096 * 16;
 SNG_HD f3 to_local(const Volume& v, f3 p) { return v.to_local_identity ? p : mul(v.to_local, p); }
 
 // Exact specialisation of if_unoccupied_advance_to_next_occupied_voxel<false> for unit-cube
@@ -442,8 +445,8 @@ __device__ __forceinline__ bool occupied_brick_c(f3 pos, const uint32_t* lds, Oc
     const uint32_t key = (b << 4) | sub;
     if (key != c.w) {
         c.w = key;
-        const uint32_t slot = reinterpret_cast<const uint16_t*>(lds)[b];
-        c.bits = slot == 0xffffu ? 0u : lds[OCC_BRICK_TABLE_WORDS + slot * 16u + sub];
+        const uint32_t slot = reinterpret_cast<const uint16_t*>(lds + OCC_BRICK_TAB)[b];
+        c.bits = slot == 0xffffu ? 0u : lds[OCC_BRICK_HDR_WORDS + slot * 16u + sub];
     }
     return (c.bits >> ((((uint32_t)iy & 3u) << 3) | ((uint32_t)ix & 7u))) & 1u;
 }
@@ -456,9 +459,9 @@ __device__ __forceinline__ bool occupied_brick_nb(f3 pos, const uint32_t* lds) {
     const uint32_t ux = (uint32_t)ix & (GRID_SIZE - 1), uy = (uint32_t)iy & (GRID_SIZE - 1), uz = (uint32_t)iz & (GRID_SIZE - 1);
     const uint32_t b = (uz >> 3) * 256u + (uy >> 3) * 16u + (ux >> 3);
     const uint32_t sub = (uz & 7u) * 2u + ((uy & 7u) >> 2);
-    const uint32_t slot = reinterpret_cast<const uint16_t*>(lds)[b];
+    const uint32_t slot = reinterpret_cast<const uint16_t*>(lds + OCC_BRICK_TAB)[b];
     const uint32_t empty = (uint32_t)(slot == 0xffffu);
-    const uint32_t w = lds[OCC_BRICK_TABLE_WORDS + (slot & (empty - 1u)) * 16u + sub];   // empty brick: slot 0's word, masked
+    const uint32_t w = lds[OCC_BRICK_HDR_WORDS + (slot & (empty - 1u)) * 16u + sub];   // empty brick: slot 0's word, masked
     const uint32_t bit = (w >> (((uy & 3u) << 3) | (ux & 7u))) & 1u;
     return (bit & (uint32_t)in & (empty ^ 1u)) != 0u;   // bit operations: no short-circuit branches
 }
@@ -468,6 +471,55 @@ __device__ __forceinline__ bool aabb_contains_nb(const aabb& b, f3 p) {
     const float m0 = fminf(fminf(p.x - b.lo.x, p.y - b.lo.y), p.z - b.lo.z);
     const float m1 = fminf(fminf(b.hi.x - p.x, b.hi.y - p.y), b.hi.z - p.z);
     return fminf(m0, m1) >= 0.0f;
+}
+// The largest t at which the ray o + t d (t >= t0) can still be in an occupied mip-0 cell, or -1 when it
+// cannot at all: a walk over the 16^3 bricks of the unit cube that keeps the exit t of the last brick whose
+// dilated mask bit is set.  Conservative for the exact marchers: their float positions stay within ~1e-6 of
+// the line and a brick's mask bit covers every occupied cell within one cell (1/128) of it, so a marcher
+// past the returned t only ever meets unoccupied cells until it leaves the volume -- stopping there drops
+// no sample.  (Unit-cube occupancy, identity render_aabb_to_local: the linear marchers.)
+__device__ __forceinline__ float path_last_occupied_t(f3 o, f3 d, f3 idir, float t0, const uint32_t* lds) {
+    // the line's span inside [0,1]^3, from t0
+    float ta = t0, tb = 3.0e38f;
+    const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, ii[3] = {idir.x, idir.y, idir.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (dd[k] == 0.0f) {
+            if (oo[k] < 0.0f || oo[k] > 1.0f) return -1.0f;
+        } else {
+            const float u = (0.0f - oo[k]) * ii[k], v = (1.0f - oo[k]) * ii[k];
+            ta = fmaxf(ta, fminf(u, v));
+            tb = fminf(tb, fmaxf(u, v));
+        }
+    }
+    if (!(ta <= tb)) return -1.0f;
+    const float tm = 0.5f * (ta + tb);   // a point safely inside for the start brick, then walk from ta
+    int b[3], st[3];
+    float tmax[3], tdel[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float pk = oo[k] + dd[k] * ta;
+        int c = (int)floorf(pk * 16.0f);
+        c = c < 0 ? 0 : (c > 15 ? 15 : c);
+        b[k] = c;
+        if (dd[k] > 0.0f) { st[k] = 1; tmax[k] = ((float)(c + 1) * 0.0625f - oo[k]) * ii[k]; tdel[k] = 0.0625f * ii[k]; }
+        else if (dd[k] < 0.0f) { st[k] = -1; tmax[k] = ((float)c * 0.0625f - oo[k]) * ii[k]; tdel[k] = -0.0625f * ii[k]; }
+        else { st[k] = 0; tmax[k] = 3.0e38f; tdel[k] = 3.0e38f; }
+    }
+    (void)tm;
+    float last = -1.0f;
+#pragma unroll 1
+    for (int n = 0; n < 48; ++n) {
+        const uint32_t bi = (uint32_t)b[2] * 256u + (uint32_t)b[1] * 16u + (uint32_t)b[0];
+        const float tx = fminf(fminf(tmax[0], tmax[1]), tmax[2]);
+        if ((lds[bi >> 5] >> (bi & 31u)) & 1u) last = fminf(tx, tb);
+        if (tx >= tb) break;
+        const int k = tmax[0] == tx ? 0 : (tmax[1] == tx ? 1 : 2);
+        b[k] += st[k];
+        if (b[k] < 0 || b[k] > 15) break;
+        tmax[k] += tdel[k];
+    }
+    return last < 0.0f ? -1.0f : last * 1.00001f + 1e-5f;
 }
 // copy the OccBrick blob into LDS (every thread of the block; words padded to a multiple of 4)
 __device__ __forceinline__ void stage_occ_brick(uint32_t* lds, const uint32_t* g, uint32_t words) {
