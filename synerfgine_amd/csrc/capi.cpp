@@ -362,10 +362,11 @@ const std::map<std::string, double>& default_params() {
         {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
         {"nerf_fused_after", 1},                // ... after this many whole-GPU wavefront iterations (1: the one big
                                                 //   uncontended network launch, then the ray-local tail; measured best)
-        {"nerf_spec_rounds", 2},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
-        {"nerf_spec_budget", 1048576},          // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax))
+        {"nerf_spec_rounds", 3},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
+        {"nerf_spec_budget", 2097152},          // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax))
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
-        {"nerf_spec_rt_gate", 1},
+        {"nerf_spec_rt_gate", 0},               // 1: the raytracer starts after the speculative rounds (C3: 216 vs 240 frames/s with 0)
+        {"nerf_spec_k_policy", 1},              // per-ray look-ahead from the ray's opacity in all rounds but the last (exact)
         {"nerf_spec_debug", 0},
         {"nerf_spec_prepare", 1},               // sample-parallel activations before the spec compositor (exact; 0: in the chain)
         {"occ_lds_kb", 64},
@@ -448,7 +449,7 @@ struct sng_ctx {
 
     // buffers
     DevBuf nerf_rgba, nerf_depth, nerf_pos, nerf_nrm;
-    DevBuf ray_ot[2], ray_di[2], ray_rgba[2], ray_depth[2], ray_mw[2], ray_lt[2], ray_lo[2];
+    DevBuf ray_ot[2], ray_di[2], ray_rgba[2], ray_depth[2], ray_mw[2], ray_lt[2], ray_lo[2], ray_kk[2];
     DevBuf samp, coords, net_out, ctrl;
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
@@ -995,6 +996,7 @@ void resize(sng_ctx* c) {
         c->ray_mw[b].ensure(nn * 4);
         c->ray_lt[b].ensure(nn * 8);
         c->ray_lo[b].ensure(nn * 8);
+        c->ray_kk[b].ensure(nn * 4);
     }
     c->samp.ensure(nn * 8);
     c->ray_cap = nn;
@@ -1103,7 +1105,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     RayBuf rb[2];
     for (int b = 0; b < 2; ++b)
         rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>(),
-                 c->ray_lt[b].as<float2>(), c->ray_lo[b].as<uint2>()};
+                 c->ray_lt[b].as<float2>(), c->ray_lo[b].as<uint2>(), c->ray_kk[b].as<uint32_t>()};
     launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(),
                      (uint32_t)c->n_cus, c->s_nerf);
     reduce_sched(0);
@@ -1218,7 +1220,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // kernel below then finishes whatever is still alive
             const uint32_t rounds = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds"));
             c->spec_rounds = rounds;
-            launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), c->s_nerf);
+            launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), p, c->s_nerf);
             if (rounds) {
                 c->spec_t.ensure(c->sample_cap * 4);
                 // sample-parallel activations ahead of the compositing chain (not for the instant-NGP render modes
@@ -1246,6 +1248,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 }
                 for (uint32_t r = 0; r < rounds; ++r) {
                     sa.in = rb[p]; sa.out = rb[p ^ 1]; sa.p = p;
+                    // per-ray look-ahead in all but the last round (which then finishes nearly every ray)
+                    sa.k_policy = (c->p("nerf_spec_k_policy") != 0.0 && r + 1 < rounds) ? 1 : 0;
                     sa.dbg = dbg ? c->spec_dbg.as<uint4>() + (size_t)r * n_band : nullptr;
                     sa.dbg_stride = n_band;
                     launch_spec_generate(sa, sblocks, c->s_nerf);
@@ -1926,7 +1930,7 @@ void ctx_destroy(sng_ctx* c) {
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
                       &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
         b->release();
-    for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); }
+    for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); c->ray_kk[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1, c->ev_alive}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);

@@ -64,6 +64,9 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     if (n_rays == 0) return;
     const uint32_t i_step0 = a.ctrl->i_step[a.p];
     const uint32_t k0 = a.ctrl->n_iter;
+    // after speculative rounds each ray carries its own next iteration (RayBuf::kk)
+    const bool kk_in = a.ctrl->spec_kk_valid[a.p] != 0u;
+    const uint32_t base_k = a.ctrl->spec_base_k, base_istep = a.ctrl->spec_base_istep;
     const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
     const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
     const h8* wfrag = reinterpret_cast<const h8*>(a.wfrag);
@@ -104,8 +107,8 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
                         depth = a.rays.depth[r];
                         mw = a.mode.ngp ? a.rays.mw[r] : 0.0f;
                         if (!a.mode.ngp) { lt = a.rays.lt[r].x; lo = a.rays.lo[r]; }
-                        k = k0;
-                        istep = i_step0;
+                        k = kk_in ? a.rays.kk[r] : k0;
+                        istep = kk_in ? base_istep + MAX_STEPS_BETWEEN_COMPACTION * (k - base_k) : i_step0;
                         has = true;
                     }
                 }

@@ -528,6 +528,14 @@ __device__ __forceinline__ bool spec_composite_sample(const Volume& vol, const C
     return false;
 }
 
+// Per-ray look-ahead (SpecArgs::k_policy): iterations a ray is marched ahead in a round, from the opacity it has
+// reached -- about the 90th percentile of the iterations rays of that opacity still live (lego, C2 / C3 after
+// the head: A < 0.05 -> 5, ..., A >= 0.95 -> 1; tools/tail_diag.py), so fewer samples past a ray's end are
+// evaluated.  Any choice is exact: a ray that outlives its look-ahead continues in the next round.
+__device__ __forceinline__ uint32_t spec_k_of(float A) {
+    return A < 0.05f ? 5u : A < 0.2f ? 4u : A < 0.5f ? 3u : A < 0.8f ? 3u : A < 0.95f ? 2u : 1u;
+}
+
 // BRICK: the occupancy bricks are staged in LDS (dynamic shared memory) and the march loop makes no global
 // load, so its per-sample t stores to tbuf are fire-and-forget (no load waits behind them).  Without the
 // bricks (too many for the LDS budget) the loop reads the linear occupancy through a register word cache.
@@ -539,18 +547,19 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
     const int p = a.p;
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t istep0 = ctrl->i_step[p];
-    uint32_t K = 0;
+    const uint32_t base_k = ctrl->spec_base_k, base_istep = ctrl->spec_base_istep;
+    const bool kk_in = ctrl->spec_kk_valid[p] != 0u;   // per-ray iteration indices (after a round), else all at base_k
+    uint32_t K = 0;   // the round's look-ahead bound; a ray's own may be smaller (k_policy, MARCH_ITER)
     if (n_alive > 0 && istep0 < MARCH_ITER) {
         K = a.budget / (MAX_STEPS_BETWEEN_COMPACTION * n_alive);
         K = K < 1u ? 1u : (K > a.kmax ? a.kmax : K);
-        const uint32_t left = (MARCH_ITER - istep0 + MAX_STEPS_BETWEEN_COMPACTION - 1) / MAX_STEPS_BETWEEN_COMPACTION;   // incl. the last
-        K = K < left ? K : left;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctrl->spec_K[p] = K;
         ctrl->spec_k0[p] = ctrl->n_iter;
         ctrl->n_alive[p ^ 1] = 0;
         ctrl->i_step[p ^ 1] = istep0 + MAX_STEPS_BETWEEN_COMPACTION * K;
+        ctrl->spec_kk_valid[p ^ 1] = 1u;   // the compositor writes each survivor's next iteration index
     }
     if (K == 0 || blockIdx.x * THREADS >= n_alive) return;
     const Volume& vol = a.vol;
@@ -568,6 +577,12 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             const float4 ot = a.in.o_t[i], di = a.in.d_idx[i];
             o = mk(ot.x, ot.y, ot.z);
             d = mk(di.x, di.y, di.z);
+            // this ray's iteration, trace_alt step counter and look-ahead
+            const uint32_t k_i = kk_in ? a.in.kk[i] : base_k;
+            const uint32_t istep_i = base_istep + MAX_STEPS_BETWEEN_COMPACTION * (k_i - base_k);
+            const uint32_t left = istep_i < MARCH_ITER ? (MARCH_ITER - istep_i + MAX_STEPS_BETWEEN_COMPACTION - 1) / MAX_STEPS_BETWEEN_COMPACTION : 1u;
+            uint32_t K_i = K < left ? K : left;
+            if (a.k_policy) K_i = min(K_i, spec_k_of(a.in.rgba[i].w));
             const f3 idir = inv(d);
             const float dfw = dot(a.cam.c2, d);
             const float rdfw = recip_rn(dfw);   // x / dfw as div_by(x, dfw, rdfw): the IEEE quotient (Markstein), fewer ops
@@ -630,7 +645,7 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
                     nnet += cnt - ru;
                     ++n_it;
                     cnt_last = cnt;
-                    if (cnt < MAX_STEPS_BETWEEN_COMPACTION || it + 1 == K) {
+                    if (cnt < MAX_STEPS_BETWEEN_COMPACTION || it + 1 == K_i) {
                         going = false;   // the ray ends in this iteration, or the round's look-ahead does
                     } else {
                         prev = tl;
@@ -647,7 +662,7 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
                 }
             }
             // trace keeps generate's t (836): the survivors' next start
-            if (a.mode.ngp && n_it == K && cnt_last == MAX_STEPS_BETWEEN_COMPACTION) reinterpret_cast<float*>(a.in.o_t + i)[3] = t;
+            if (a.mode.ngp && n_it == K_i && cnt_last == MAX_STEPS_BETWEEN_COMPACTION) reinterpret_cast<float*>(a.in.o_t + i)[3] = t;
 #ifdef SNG_OCC_COUNT
             const uint32_t loads = oc.loads;
 #else
@@ -722,8 +737,8 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
     const int p = a.p;
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t K = ctrl->spec_K[p];
-    const uint32_t k0 = ctrl->spec_k0[p];
-    const uint32_t istep0 = ctrl->i_step[p];
+    const uint32_t base_k = ctrl->spec_base_k, base_istep = ctrl->spec_base_istep;
+    const bool kk_in = ctrl->spec_kk_valid[p] != 0u;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (K) {
             ctrl->net_samples += ctrl->n_samples[p];
@@ -749,7 +764,7 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
         float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
         float depth = 0.0f, mw = 0.0f, lt = 0.0f;
         uint2 lraw = make_uint2(0u, 0u);
-        uint32_t death_step = 0;
+        uint32_t death_step = 0, kk_next = 0;
         if (i < n_alive) {
             rgba = a.in.rgba[i];
             depth = a.in.depth[i];
@@ -760,6 +775,9 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
             const f3 o = mk(ot.x, ot.y, ot.z), d = mk(di.x, di.y, di.z);
             const uint2 sc = a.samp[i];
             const uint32_t n_it = sc.y & 31u, cnt_last = (sc.y >> 5) & 15u, rbits = sc.y >> 9;
+            const uint32_t k0 = kk_in ? a.in.kk[i] : base_k;   // this ray's iteration and step counter at the round's start
+            const uint32_t istep0 = base_istep + MAX_STEPS_BETWEEN_COMPACTION * (k0 - base_k);
+            kk_next = k0 + n_it;
             uint32_t ob = sc.x, s = 0;
             bool ended = false;
             if (a.pre) {
@@ -903,6 +921,7 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
             a.out.depth[slot] = depth;
             if (mode.ngp) a.out.mw[slot] = mw;
             else { a.out.lt[slot] = make_float2(lt, 0.0f); a.out.lo[slot] = lraw; }
+            a.out.kk[slot] = kk_next;
         }
         if (hit) {
             ++my_hits;
@@ -950,9 +969,15 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
 }
 
 // the tail's per-iteration statistics: iterations from n_iter on take 8 steps each
-__global__ void tail_prepare_kernel(MarchCtrl* ctrl, uint32_t* work) {
+__global__ void tail_prepare_kernel(MarchCtrl* ctrl, uint32_t* work, int p) {
     if (threadIdx.x < 64 && threadIdx.x >= ctrl->n_iter) ctrl->steps_hist[threadIdx.x] = MAX_STEPS_BETWEEN_COMPACTION;
-    if (threadIdx.x == 0 && work) *work = 0;
+    if (threadIdx.x == 0) {
+        if (work) *work = 0;
+        ctrl->spec_base_k = ctrl->n_iter;        // the tail's first iteration ...
+        ctrl->spec_base_istep = ctrl->i_step[p]; // ... and its step counter
+        ctrl->spec_kk_valid[0] = 0u;
+        ctrl->spec_kk_valid[1] = 0u;
+    }
 }
 
 // write_normals_to_buffer (1523-1576) for rows [row0,row1)
@@ -1109,6 +1134,7 @@ __global__ void ctrl_init_kernel(MarchCtrl* c) {
         c->total_samples = 0; c->net_samples = 0; c->ref_slots = 0; c->reused_samples = 0;
         c->spec_K[0] = 0; c->spec_K[1] = 0; c->spec_k0[0] = 0; c->spec_k0[1] = 0;
         c->spec_evals = 0; c->spec_exec = 0;
+        c->spec_base_k = 0; c->spec_base_istep = 1; c->spec_kk_valid[0] = 0; c->spec_kk_valid[1] = 0;
     }
 }
 
@@ -1160,7 +1186,7 @@ void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
 void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_prepare_kernel, dim3(blocks), dim3(256), 0, s, a);
 }
-void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, hipStream_t s) { hipLaunchKernelGGL(tail_prepare_kernel, dim3(1), dim3(64), 0, s, ctrl, work); }
+void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, int p, hipStream_t s) { hipLaunchKernelGGL(tail_prepare_kernel, dim3(1), dim3(64), 0, s, ctrl, work, p); }
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
     if (!n) return;

@@ -54,6 +54,9 @@ struct MarchCtrl {
     uint32_t spec_k0[2];      // iteration index of the round's first iteration
     unsigned long long spec_evals;   // samples the rounds' network launches evaluated (incl. those past a ray's end)
     unsigned long long spec_exec;    // ... of which composited
+    uint32_t spec_base_k;            // iteration index and trace_alt step counter i at the tail's start: a ray at
+    uint32_t spec_base_istep;        //   iteration k has i = base_istep + 8 (k - base_k)
+    uint32_t spec_kk_valid[2];       // RayBuf::kk of buffer p holds per-ray iteration indices
 };
 
 // Alive-ray SoA buffer (NerfPayload + rgba + depth, nerf_device.cuh:145-153; nerf.h:22-42)
@@ -67,6 +70,8 @@ struct RayBuf {
     // iteration's first sample the previous iteration's last one, bit for bit in the common case.
     float2* lt;        // x: t of the previous iteration's last sample (NaN: none); y: this iteration's (generate)
     uint2* lo;         // raw fp16 (r, g, b, density) network output of that sample
+    uint32_t* kk;      // speculative tail: the ray's next iteration index (rays of one buffer may differ once the
+                       // rounds look ahead per ray; MarchCtrl::spec_kk_valid says whether this buffer's are set)
 };
 
 // n_steps_between_compaction = clamp(target / n_alive, 1, 8) (testbed_nerf.cu:2189-2190)
@@ -279,6 +284,7 @@ struct SpecArgs {
     int p;
     uint32_t budget;              // samples one round may generate: K = clamp(budget / (8 n_alive), 1, kmax)
     uint32_t kmax;                // <= SPEC_KMAX
+    int k_policy;                 // 1: a ray looks ahead fewer iterations the more opaque it already is (spec_k_of)
     float* coords;                // NerfCoordinate AoS of the network samples
     uint2* samp;                  // per ray: {first network sample, n_it | cnt_last << 5 | reuse bits << 9}
     float* tbuf;                  // [sample j of the ray][ray] march t of every sample (incl. reused boundary samples)
@@ -295,7 +301,7 @@ constexpr uint32_t SPEC_KMAX = 16;
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s);
-void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, hipStream_t s);
+void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, int p, hipStream_t s);
 
 // nerf.hip
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, uint32_t n_cus,

@@ -548,6 +548,9 @@ def test_fused_nerf_kernel_equals_wavefront(config, ngp_mode):
     ("c4", None, {"nerf_spec_rounds": 4}), ("c4", None, {"nerf_spec_rounds": 2, "nerf_spec_budget": 1 << 22}),
     ("c3", None, {"nerf_spec_rounds": 4, "nerf_spec_prepare": 0}), ("c3", 1, {"nerf_spec_rounds": 3, "nerf_spec_prepare": 0}),
     ("c3", None, {"nerf_spec_rounds": 4, "occ_lds_kb": 0}),               # global occupancy words instead of the LDS bricks
+    ("c3", None, {"nerf_spec_rounds": 3, "nerf_spec_k_policy": 0}),       # one look-ahead for every ray of a round
+    ("c3", 6, {"nerf_spec_rounds": 5, "nerf_spec_k_policy": 1}),          # per-ray look-ahead, Cost mode's death steps
+    ("c4", None, {"nerf_spec_rounds": 3, "nerf_spec_k_policy": 1}),
 ])
 def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
     """nerf.hip's speculative tail rounds (each alive ray marched K iterations ahead, one whole-GPU network
