@@ -362,7 +362,7 @@ const std::map<std::string, double>& default_params() {
         {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
         {"nerf_fused_after", 1},                // ... after this many whole-GPU wavefront iterations (1: the one big
                                                 //   uncontended network launch, then the ray-local tail; measured best)
-        {"nerf_spec_rounds", 3},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
+        {"nerf_spec_rounds", 2},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
         {"nerf_spec_budget", 2097152},          // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax))
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
         {"nerf_spec_rt_gate", 0},               // 1: the raytracer starts after the speculative rounds (C3: 216 vs 240 frames/s with 0)
