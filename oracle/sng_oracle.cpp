@@ -394,6 +394,27 @@ inline V2 bb_ray_intersect(const BBox& b, V3 pos, V3 dir) {
     if (tzmax < tmax) tmax = tzmax;
     return {tmin, tmax};
 }
+/* The BVH's box test: bounding_box.cuh:163-211 as the reference compiles it (--use_fast_math,
+ * CMakeLists.txt:82, makes each (b - pos) / dir a multiply by rcp(dir)); restated as (b - pos) * y
+ * with y = RN(1 / dir) per ray, the same expressions as the GPU's bvh_box_entry (sng_math.h). */
+inline float bvh_box_entry(const BBox& b, V3 pos, V3 y) {
+    float tmin = (b.min.x - pos.x) * y.x;
+    float tmax = (b.max.x - pos.x) * y.x;
+    if (tmin > tmax) std::swap(tmin, tmax);
+    float tymin = (b.min.y - pos.y) * y.y;
+    float tymax = (b.max.y - pos.y) * y.y;
+    if (tymin > tymax) std::swap(tymin, tymax);
+    const float FMAX = std::numeric_limits<float>::max();
+    if (tmin > tymax || tymin > tmax) return FMAX;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = (b.min.z - pos.z) * y.z;
+    float tzmax = (b.max.z - pos.z) * y.z;
+    if (tzmin > tzmax) std::swap(tzmin, tzmax);
+    if (tmin > tzmax || tzmin > tmax) return FMAX;
+    if (tzmin > tmin) tmin = tzmin;
+    return tmin;
+}
 inline bool bb_contains(const BBox& b, V3 p) {
     return p.x >= b.min.x && p.x <= b.max.x && p.y >= b.min.y && p.y <= b.max.y && p.z >= b.min.z && p.z <= b.max.z;
 }
@@ -762,6 +783,7 @@ std::pair<int, float> ray_intersect_nodes(V3 ro, V3 rd, const float* nodes, cons
     stack[count++] = 0;
     float mint = MAX_DEPTH;
     int shortest = -1;
+    const V3 y = v3(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
     while (count > 0) {
         int idx = stack[--count];
         Node node = load_node(nodes, idx);
@@ -773,7 +795,7 @@ std::pair<int, float> ray_intersect_nodes(V3 ro, V3 rd, const float* nodes, cons
             }
         } else {
             struct DI { float dist; int idx; } ch[2];
-            for (int i = 0; i < 2; ++i) ch[i] = {bb_ray_intersect(load_node(nodes, node.left + i).bb, ro, rd).x, node.left + i};
+            for (int i = 0; i < 2; ++i) ch[i] = {bvh_box_entry(load_node(nodes, node.left + i).bb, ro, y), node.left + i};
             if (ch[0].dist < ch[1].dist) std::swap(ch[0], ch[1]); /* sorting_network<2>: descending */
             for (int i = 0; i < 2; ++i)
                 if (ch[i].dist < mint) {

@@ -67,17 +67,17 @@ struct TraceCtx {
 };
 
 // One BvhWide record: four 16-B loads (ds_read_b128 from the LDS scene blob).  d0, d1: the entry
-// distances of its two child boxes, exactly as aabb_entry(_fast) gives them.
+// distances of its two child boxes, exactly as bvh_box_entry / aabb_entry_fast give them.
 template <bool FAST>
 __device__ __forceinline__ void wide_visit(const BvhWide* __restrict__ rec, f3 ro, f3 rd, f3 y, float& d0, float& d1, int& ref0, int& ref1) {
     const float4* r = reinterpret_cast<const float4*>(rec);
     const float4 a = r[0], b = r[1], c = r[2], e = r[3];
     if constexpr (FAST) {
-        d0 = slab_entry_fast(pf2{a.x, a.y}, pf2{a.z, a.w}, pf2{b.x, b.y}, ro, rd, y);
-        d1 = slab_entry_fast(pf2{b.z, b.w}, pf2{c.x, c.y}, pf2{c.z, c.w}, ro, rd, y);
+        d0 = slab_entry_fast(pf2{a.x, a.y}, pf2{a.z, a.w}, pf2{b.x, b.y}, ro, y);
+        d1 = slab_entry_fast(pf2{b.z, b.w}, pf2{c.x, c.y}, pf2{c.z, c.w}, ro, y);
     } else {
-        d0 = aabb_entry(aabb{mk(a.x, a.z, b.x), mk(a.y, a.w, b.y)}, ro, rd);
-        d1 = aabb_entry(aabb{mk(b.z, c.x, c.z), mk(b.w, c.y, c.w)}, ro, rd);
+        d0 = bvh_box_entry(aabb{mk(a.x, a.z, b.x), mk(a.y, a.w, b.y)}, ro, y);
+        d1 = bvh_box_entry(aabb{mk(b.z, c.x, c.z), mk(b.w, c.y, c.w)}, ro, y);
     }
     ref0 = __float_as_int(e.x);
     ref1 = __float_as_int(e.y);
@@ -143,8 +143,8 @@ __device__ __forceinline__ bool tri_hit(const TriT* tp, f3 ro, f3 rd, float mint
 }
 
 // ray_intersect_nodes_f<2> (triangle_bvh.cu:263-307); returns t, writes triangle index.
-// The box tests use the exact reciprocal-multiply form (aabb_entry_fast) when the ray and the
-// object allow it, which removes 12 IEEE divisions per interior node without changing a bit.
+// Box tests: bvh_box_entry (sng_math.h), in its branch-free form (aabb_entry_fast) when the ray and
+// the object keep every quotient finite; y = inv(rd) once per ray.
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __restrict__ nodes, const TriT* __restrict__ tris, int* stack_lds,
                                           int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
@@ -168,8 +168,8 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
             const aabb b0 = {mk(n0.lo[0], n0.lo[1], n0.lo[2]), mk(n0.hi[0], n0.hi[1], n0.hi[2])};
             const aabb b1 = {mk(n1.lo[0], n1.lo[1], n1.lo[2]), mk(n1.hi[0], n1.hi[1], n1.hi[2])};
             if (cnt) cnt[1] += 2u;
-            float d0 = FAST ? aabb_entry_fast(b0, ro, rd, y) : aabb_entry(b0, ro, rd);
-            float d1 = FAST ? aabb_entry_fast(b1, ro, rd, y) : aabb_entry(b1, ro, rd);
+            float d0 = FAST ? aabb_entry_fast(b0, ro, y) : bvh_box_entry(b0, ro, y);
+            float d1 = FAST ? aabb_entry_fast(b1, ro, y) : bvh_box_entry(b1, ro, y);
             // sorting_network<2>: descending, so the nearer child is pushed last
             int i0 = c0, i1 = c1;
             if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = c1; i1 = c0; }
@@ -268,16 +268,17 @@ __device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu&
     const f3 oro = mul(o.world_to_obj, ro - o.pos);
     const f3 ord = mul(o.world_to_obj, rd);
     const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
+    const f3 y = inv(ord);
     if (o.wide && cx.flat) {
-        if (fast) return bvh_walk_near<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
-        return bvh_walk_near<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
+        if (fast) return bvh_walk_near<true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
+        return bvh_walk_near<false>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
     }
     if (o.wide) {
-        if (fast) return bvh_walk_wide<true>(oro, ord, inv(ord), cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
-        return bvh_walk_wide<false>(oro, ord, ord, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+        if (fast) return bvh_walk_wide<true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+        return bvh_walk_wide<false>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
     }
-    if (fast) return bvh_walk<true>(oro, ord, inv(ord), cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
-    return bvh_walk<false>(oro, ord, ord, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+    if (fast) return bvh_walk<true>(oro, ord, y, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+    return bvh_walk<false>(oro, ord, y, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
 }
 
 // sng::depth_test_world (common.cu:36-48)
@@ -514,15 +515,23 @@ __global__ void mesh_rays_kernel(int W, int H, int row0, int row1, CamDev cam, f
 // ---------------------------------------------------------------------------
 // sng::raytrace (raytracer.cu:101-218), Final buffer
 // ---------------------------------------------------------------------------
+// The reference builds with --use_fast_math (CMakeLists.txt:82), so its sinf/cosf here are the
+// hardware approximations; __sincosf is the same class (v_sin/v_cos on the angle in revolutions).
 __device__ __forceinline__ f3 cone_random_up(f3 orig, f3 up, float longi, float latid) {   // common.cuh:37-48
     const f3 N = normalize(orig);
     const f3 B = normalize(cross(N, up));
     const f3 T = cross(B, N);
-    const f3 off = mk(sinf(longi) * cosf(latid), sinf(longi) * sinf(latid), cosf(longi));
+    float sl, cl, sp, cp;
+    __sincosf(longi, &sl, &cl);
+    __sincosf(latid, &sp, &cp);
+    const f3 off = mk(sl * cp, sl * sp, cl);
     return orig + mul(m3{T, B, N}, off);
 }
 __device__ __forceinline__ f3 cone_random_frame(f3 orig, const m3& frame, float longi, float latid) {   // common.cuh:33-36
-    const f3 off = mk(cosf(longi) * sinf(latid), sinf(longi) * sinf(latid), cosf(longi));
+    float sl, cl, sp, cp;
+    __sincosf(longi, &sl, &cl);
+    __sincosf(latid, &sp, &cp);
+    const f3 off = mk(cl * sp, sl * sp, cl);
     return orig + mul(frame, off);
 }
 //

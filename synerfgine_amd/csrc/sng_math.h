@@ -209,33 +209,49 @@ SNG_HD float aabb_entry(const aabb& b, f3 pos, f3 dir) {
     if (tzmin > tmin) tmin = tzmin;
     return tmin;
 }
-// aabb_entry with each division x / dir_i evaluated as div_by(x, dir_i, 1/dir_i) -- bit-identical
-// to aabb_entry (Markstein correction, see div_by) provided no intermediate over/underflows, which
-// slab_fast_ok() guarantees for the ray and the host guarantees for the boxes (|coord| < 2^40).
-// Branch-free: with no NaN or infinity in play (slab_fast_ok), aabb_entry's swaps are min/max and
-// its two early-outs together test every pair (a_min > b_max, a != b), i.e. max(mins) > min(maxes);
-// the value returned otherwise is max(mins).  Only the sign of a zero result can differ, which no
-// caller observes (the result is only compared).
-// The (lo, hi) pair of each axis is one packed-f32 operand (v_pk_add/mul/fma: two lanes per op).
-typedef float pf2 __attribute__((ext_vector_type(2)));
-SNG_HD pf2 div_by2(pf2 x, float d, float y) {
-    const pf2 dd = {d, d}, yy = {y, y};
-    const pf2 q0 = x * yy;
-    const pf2 r = __builtin_elementwise_fma(-q0, dd, x);
-    return __builtin_elementwise_fma(r, yy, q0);
-}
-// sx, sy, sz: the box's (lo, hi) slab of each axis
-SNG_HD float slab_entry_fast(pf2 sx, pf2 sy, pf2 sz, f3 pos, f3 dir, f3 y) {
+// BVH box entry (bounding_box.cuh:163-211 as the reference compiles it: CMakeLists.txt:82 builds
+// with --use_fast_math, which turns each slab quotient (b - pos) / dir into (b - pos) * rcp(dir)).
+// Restated as (b - pos) * y with y = RN(1 / dir) formed once per ray (inv()): subtract, then multiply
+// by the reciprocal -- the reference's operation order, with a correctly rounded reciprocal instead
+// of the hardware approximation.  The CPU oracle (sng_oracle.cpp bvh_box_entry) evaluates the same
+// expressions, so GPU and oracle traversals agree bit for bit.  The NeRF volume's box tests keep
+// aabb_entry (IEEE division) above.
+SNG_HD float bvh_box_entry(const aabb& b, f3 pos, f3 y) {
     const float FMAX = 3.402823466e+38f;
-    const pf2 tx = div_by2(sx - pos.x, dir.x, y.x);
-    const pf2 ty = div_by2(sy - pos.y, dir.y, y.y);
-    const pf2 tz = div_by2(sz - pos.z, dir.z, y.z);
+    float tmin = (b.lo.x - pos.x) * y.x;
+    float tmax = (b.hi.x - pos.x) * y.x;
+    if (tmin > tmax) fswap(tmin, tmax);
+    float tymin = (b.lo.y - pos.y) * y.y;
+    float tymax = (b.hi.y - pos.y) * y.y;
+    if (tymin > tymax) fswap(tymin, tymax);
+    if (tmin > tymax || tymin > tmax) return FMAX;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    float tzmin = (b.lo.z - pos.z) * y.z;
+    float tzmax = (b.hi.z - pos.z) * y.z;
+    if (tzmin > tzmax) fswap(tzmin, tzmax);
+    if (tmin > tzmax || tzmin > tmax) return FMAX;
+    if (tzmin > tmin) tmin = tzmin;
+    return tmin;
+}
+// bvh_box_entry, branch-free: with no NaN or infinity in play (slab_fast_ok() for the ray, |coord| <
+// 2^40 for the boxes, checked on the host), its swaps are min/max and its two early-outs together
+// test every pair (a_min > b_max), i.e. max(mins) > min(maxes); the value returned otherwise is
+// max(mins).  Only the sign of a zero result can differ, which no caller observes (the result is
+// only compared).  The (lo, hi) pair of each axis is one packed-f32 operand (v_pk_add / v_pk_mul).
+typedef float pf2 __attribute__((ext_vector_type(2)));
+// sx, sy, sz: the box's (lo, hi) slab of each axis
+SNG_HD float slab_entry_fast(pf2 sx, pf2 sy, pf2 sz, f3 pos, f3 y) {
+    const float FMAX = 3.402823466e+38f;
+    const pf2 tx = (sx - pos.x) * y.x;
+    const pf2 ty = (sy - pos.y) * y.y;
+    const pf2 tz = (sz - pos.z) * y.z;
     const float tmin = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y));
     const float tmax = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
     return tmin > tmax ? FMAX : tmin;
 }
-SNG_HD float aabb_entry_fast(const aabb& b, f3 pos, f3 dir, f3 y) {
-    return slab_entry_fast(pf2{b.lo.x, b.hi.x}, pf2{b.lo.y, b.hi.y}, pf2{b.lo.z, b.hi.z}, pos, dir, y);
+SNG_HD float aabb_entry_fast(const aabb& b, f3 pos, f3 y) {
+    return slab_entry_fast(pf2{b.lo.x, b.hi.x}, pf2{b.lo.y, b.hi.y}, pf2{b.lo.z, b.hi.z}, pos, y);
 }
 constexpr float SLAB_FAST_MAX_COORD = 1099511627776.0f;   // 2^40
 SNG_HD bool slab_fast_ok(f3 pos, f3 dir) {

@@ -84,8 +84,8 @@ int main() {
         if (it % 7 == 0) d = d * 37.5f;
         if (!slab_fast_ok(o, d)) continue;
         ++n_slab;
-        // equal up to the sign of a zero result (aabb_entry_fast's min/max form; callers only compare it)
-        const float fa = aabb_entry_fast(box, o, d, inv(d)), fb = aabb_entry(box, o, d);
+        // bvh_box_entry's branch-free form equals the branchy one up to the sign of a zero result (callers only compare it)
+        const float fa = aabb_entry_fast(box, o, inv(d)), fb = bvh_box_entry(box, o, inv(d));
         if (!(same(fa, fb) || (fa == 0.0f && fb == 0.0f))) ++bad_slab;
     }
     // degenerate slabs and origins on a slab plane: the equal-value cases of the swaps and early-outs
@@ -101,7 +101,7 @@ int main() {
         f3 d = mk(q[g() % 5] + 0.125f * (float)(g() % 3), q[g() % 5] - 0.0625f, q[g() % 5] + 0.375f);
         if (d.x == 0.0f || d.y == 0.0f || d.z == 0.0f || !slab_fast_ok(o, d)) continue;
         ++n_slab;
-        const float fa = aabb_entry_fast(box, o, d, inv(d)), fb = aabb_entry(box, o, d);
+        const float fa = aabb_entry_fast(box, o, inv(d)), fb = bvh_box_entry(box, o, inv(d));
         if (!(same(fa, fb) || (fa == 0.0f && fb == 0.0f))) ++bad_slab;
     }
     // sng_logf's f / (2 + f) as div_by(f, d, RN(1/d)): every f it can form (m in [0.5, 1), doubled below
