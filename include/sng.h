@@ -180,7 +180,11 @@ int sng_get_camera_matrix(sng_ctx* ctx, float m[12]);
 /* View::camera1 and View::rolling_shutter (testbed.h:1032,1042; Engine::nerf_render_buffer_view,
  * engine.cuh:50-52): NeRF rays use get_xform_given_rolling_shutter({camera0, camera1}, rolling_shutter,
  * uv, motionblur_time) per pixel (testbed_nerf.cu:1895). camera1 NULL: camera1 = camera0 (the engine's
- * default); rolling_shutter NULL: (0, 0, 0, 1), the View default. */
+ * default); rolling_shutter NULL: (0, 0, 0, 1), the View default.  camera1 is dropped (camera1 =
+ * camera0 again) by the next change of camera0 -- sng_set_camera_matrix / _view, set_fov keeps it,
+ * camera-path playback -- as the reference re-derives camera1 from camera0 every frame
+ * (testbed.cu:2850): set the blur after the pose.  Only the NeRF layer is blurred; the virtual
+ * objects are path-traced from camera0 (the reference's raytracer takes one camera too). */
 int sng_set_motion_blur(sng_ctx* ctx, const float camera1[12], const float rolling_shutter[4]);
 int sng_set_fov(sng_ctx* ctx, float degrees);                 /* fov_axis = 1 */
 int sng_get_focal_length(sng_ctx* ctx, int which /*0 nerf,1 mesh*/, float out[2]);

@@ -879,6 +879,23 @@ float depth_test_nerf_sd(uint32_t n_steps, float cone, V3 src, V3 dst, const Vol
 }
 
 /* sRGB: common_device.cuh:35-70 */
+/* x^n as the GPU's pow_small_int (mesh.hip) forms it: binary exponentiation for integer n in
+ * [0, 4096] (the Phong exponents and shadow intensities of every reference scene), std::pow
+ * otherwise.  The reference builds with --use_fast_math, so its powf is __powf (exp2(n log2 x),
+ * coarser than either); both GPU and oracle use this form, so they agree bit for bit. */
+inline float pow_small_int(float x, float n) {
+    if (std::floor(n) == n && n >= 0.0f && n <= 4096.0f) {
+        uint32_t e = (uint32_t)n;
+        float r = 1.0f, b = x;
+        while (e) {
+            if (e & 1u) r *= b;
+            b *= b;
+            e >>= 1;
+        }
+        return r;
+    }
+    return std::pow(x, n);
+}
 inline float srgb_to_linear(float s) { return s <= 0.04045f ? s / 12.92f : std::pow((s + 0.055f) / 1.055f, 2.4f); }
 inline float linear_to_srgb(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * std::pow(l, 0.41666f) - 0.055f; }
 
@@ -1374,7 +1391,7 @@ void orc_shade_nerf_shadows(const orc_volume* vdesc, const int32_t res[2], float
                         int hit = -1;
                         float syn_depth = depth_test_world(pos, l, objs, hit);
                         float syn_mask = syn_depth / full_d;
-                        overall = std::min(overall, std::pow(syn_mask, nerf_shadow_intensity));
+                        overall = std::min(overall, pow_small_int(syn_mask, nerf_shadow_intensity));
                         V3 fract_offset = full_d * thr * lpos;
                         float nerf_depth = std::min(full_d, depth_test_nerf_sd(n_steps, vol.cone, pos + fract_offset, lpos, vol, 0, vol.max_mip));
                         /* (full_d * (1.0 - thr)) is a double expression (1664) */
@@ -1391,7 +1408,7 @@ void orc_shade_nerf_shadows(const orc_volume* vdesc, const int32_t res[2], float
                 ++blend;
             }
         sum /= (float)blend;
-        sum = std::pow(sum, nerf_shadow_intensity);
+        sum = pow_small_int(sum, nerf_shadow_intensity);
         float* rgba = &frame_rgba[4 * idx];
         rgba[0] = srgb_to_linear(rgba[0]) * sum;
         rgba[1] = srgb_to_linear(rgba[1]) * sum;
@@ -1525,7 +1542,7 @@ struct SampledRay { V3 pos = v3s(0.0f), dir = v3s(0.0f); float pdf = 0.0f, atten
 inline V3 local_color(const orc_material& m, V3 L, V3 N, V3 R, V3 V, const orc_light& light) {
     float a = std::max(0.0f, dot(L, N));
     V3 kd = v3(m.kd[0], m.kd[1], m.kd[2]), ks = v3(m.ks[0], m.ks[1], m.ks[2]);
-    return a * kd * light.intensity + std::pow(std::max(0.0f, dot(R, V)), m.n) * ks;
+    return a * kd * light.intensity + pow_small_int(std::max(0.0f, dot(R, V)), m.n) * ks;
 }
 /* sng::shade_object: synerfgine/raytracer.cu:6-57 */
 V4 shade_object(V3 wi, SampledRay& ray, uint32_t shadow_count, HitRecord& hit, const orc_light* lights, uint32_t n_lights,
@@ -1552,7 +1569,7 @@ V4 shade_object(V3 wi, SampledRay& ray, uint32_t shadow_count, HitRecord& hit, c
                 out_nerf_shadow = std::min(nerf_shadow / full_dist, out_nerf_shadow);
                 float shadow = std::min(std::min(nerf_shadow, syn_shadow), full_dist);
                 float mask = smoothstep(shadow / full_dist);
-                mask = std::pow(mask, syn_shadow_factor);
+                mask = pow_small_int(mask, syn_shadow_factor);
                 V3 R = reflect(L, hit.normal);
                 V3 V = normalize(-wi);
                 color = color + local_color(mat, L, hit.normal, R, V, light) * mask;

@@ -420,6 +420,10 @@ struct sng_ctx {
     float cam1[12] = {};
     float rolling_shutter[4] = {0.0f, 0.0f, 0.0f, 1.0f};
     float m_scale = 1.5f;
+    // NerfDataset::scale / offset as the loaded snapshot held them (json_binding.h:108-132), written
+    // back by save_snapshot; nerf_synthetic's values until a snapshot supplies its own
+    double ds_scale = 0.33;
+    f3 ds_offset = {0.5f, 0.5f, 0.5f};
     // animation state (Engine::m_camera_path, m_anim_speed / m_enable_animations, per light / object)
     CamPathState campath;
     std::vector<LightAnim> light_anim;
@@ -654,7 +658,12 @@ Volume make_volume(const sng_ctx* c) {
 
 // ---- camera (testbed.cu:405-425) -------------------------------------------------
 f3 cam_col(const sng_ctx* c, int i) { return mk(c->cam[3 * i], c->cam[3 * i + 1], c->cam[3 * i + 2]); }
-void set_cam_col(sng_ctx* c, int i, f3 v) { c->cam[3 * i] = v.x; c->cam[3 * i + 1] = v.y; c->cam[3 * i + 2] = v.z; }
+// Every write of camera0 drops an explicit camera1 (sng_set_motion_blur): the reference re-derives
+// camera1 from camera0 each frame (testbed.cu:2850), so a blur set for one pose never applies to another.
+void set_cam_col(sng_ctx* c, int i, f3 v) {
+    c->cam[3 * i] = v.x; c->cam[3 * i + 1] = v.y; c->cam[3 * i + 2] = v.z;
+    c->has_cam1 = false;
+}
 f3 look_at(const sng_ctx* c) { return cam_col(c, 3) + cam_col(c, 2) * c->m_scale; }
 void set_look_at(sng_ctx* c, f3 pos) { set_cam_col(c, 3, cam_col(c, 3) + (pos - look_at(c))); }
 void set_scale(sng_ctx* c, float scale) {
@@ -1507,18 +1516,18 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             RtQueue q{};
             q.nls = (uint32_t)c->lights.size() * ra.shadow_iters;
             q.nps = n_point * ra.shadow_iters;
-            q.rec_stride = 2 + (3 * q.nls + 3) / 4;
+            q.rec_stride = 2 + q.nls;
             // deferred shading inputs after the light colours (not in staged mode, which shades per stage)
             if (c->p("rt_defer_shade") != 0.0 && c->p("rt_staged") == 0.0) {
                 q.shade_in = q.rec_stride;
-                q.rec_stride += 5;
+                q.rec_stride += 4;
             }
-            const uint64_t bytes = cap * (16ull * q.rec_stride + 32ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
+            const uint64_t bytes = cap * (16ull * q.rec_stride + 16ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
             const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
                                    bytes <= (uint64_t)(c->p("rt_queue_gb") * 1073741824.0);
             if (wavefront) {
                 c->rt_rec.ensure(cap * 16ull * q.rec_stride);
-                c->rt_srec.ensure(cap * 32ull * q.nps);
+                c->rt_srec.ensure(cap * 16ull * q.nps);
                 c->rt_mask.ensure(cap * 4ull * q.nps);
                 c->rt_head.ensure((uint64_t)MW * MH * 4);
                 c->rt_count.ensure(16);
@@ -2113,6 +2122,11 @@ void load_snapshot(sng_ctx* c, const std::string& path) {
     const JValue& snap = ps.root["snapshot"];
     set_model(c, &ps.cfg, ps.params.data(), ps.params.size());
     if (!ps.grid.empty()) set_density_grid(c, ps.grid.data(), ps.grid.size());
+    if (snap.contains("nerf") && snap["nerf"].contains("dataset")) {
+        const JValue& ds = snap["nerf"]["dataset"];
+        if (ds.contains("scale")) c->ds_scale = ds["scale"].as_num();
+        if (ds.contains("offset")) c->ds_offset = mk(ds["offset"][0].as_float(), ds["offset"][1].as_float(), ds["offset"][2].as_float());
+    }
     if (snap.contains("up_dir")) c->up = mk(snap["up_dir"][0].as_float(), snap["up_dir"][1].as_float(), snap["up_dir"][2].as_float());
     if (snap.contains("camera")) {
         const JValue& cam = snap["camera"];
@@ -2261,9 +2275,9 @@ void save_snapshot(sng_ctx* c, const std::string& path, bool include_opt, bool c
         w.key("render_aabb"); put_aabb(w, c->box);
         w.key("render_aabb_to_local"); w.arr(3); for (int i = 0; i < 3; ++i) w.nums(ident + 3 * i, 3);
         w.key("up"); put_vec3(w, c->up);
-        w.key("offset"); put_vec3(w, mk(0.5f, 0.5f, 0.5f));
+        w.key("offset"); put_vec3(w, c->ds_offset);
         w.key("envmap_resolution"); w.arr(2); w.uint(0); w.uint(0);
-        w.key("scale"); w.num(0.33);
+        w.key("scale"); w.num(c->ds_scale);
         w.key("aabb_scale"); w.uint(c->cfg.aabb_scale);
         w.key("from_mitsuba"); w.boolean(false);
         w.key("is_hdr"); w.boolean(false);
@@ -2533,7 +2547,9 @@ int sng_set_camera_view(sng_ctx* c, const float v[3], const float at[3], float s
         c->mesh_reset = true;
     });
 }
-int sng_set_camera_matrix(sng_ctx* c, const float m[12]) { return guarded([&] { std::memcpy(c->cam, m, 48); c->mesh_reset = true; }); }
+int sng_set_camera_matrix(sng_ctx* c, const float m[12]) {
+    return guarded([&] { std::memcpy(c->cam, m, 48); c->has_cam1 = false; c->mesh_reset = true; });
+}
 int sng_set_motion_blur(sng_ctx* c, const float camera1[12], const float rolling_shutter[4]) {
     return guarded([&] {
         c->has_cam1 = camera1 != nullptr;

@@ -553,6 +553,41 @@ __device__ __forceinline__ TraceCtx<LDS, CNT> trace_ctx_setup(const RaytraceArgs
     return TraceCtx<LDS, CNT>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt, a.count_waves};
 }
 
+// shade_object's light loop of one hit (raytracer.cu:16-50) in deferred form: per (light, shadow
+// iteration) jl the light colour -> record slot 2 + jl {lc, 0}; per point-light sample jp the shadow
+// ray {L, full_dist} -> q.shadow_ray(k, jp) (its origin, the hit position, is in the record header).
+// One 16-B store each: a wave's lanes write to 64 records at once, so every store instruction costs
+// one cache line per lane -- the float4 slots cut those instructions from 5 to 2 per light sample.
+__device__ __forceinline__ void write_light_samples(const RaytraceArgs& a, const RtQueue& q, uint32_t k, f3 pos, f3 normal, f3 rd,
+                                                    const MaterialGpu& m, Xorwow& r) {
+    float4* lc_out = q.rec + (size_t)k * q.rec_stride + 2;
+    const f3 V = normalize(-rd);
+    uint32_t jl = 0, jp = 0;
+    for (int l = 0; l < a.n_lights; ++l) {
+        const LightGpu L = a.lights[l];
+        for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
+            const f3 lpos = light_sample(L, r);
+#ifdef RT_TIMING_NO_SHADE   // timing-only builds (not exact): the cost of shade_object's per-sample lighting
+            const float full_dist = 1.0f;
+            const f3 Lv = lpos, lc = lpos;
+#else
+            f3 Lv = lpos - pos;
+            const float full_dist = length(Lv);
+            Lv = normalize(Lv);
+            const f3 R = reflect(Lv, normal);
+            const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
+#endif
+            lc_out[jl] = make_float4(lc.x, lc.y, lc.z, 0.0f);
+            if (L.type == 0) *q.shadow_ray(k, jp++) = make_float4(Lv.x, Lv.y, Lv.z, full_dist);
+        }
+    }
+}
+// record header: {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y}
+__device__ __forceinline__ void write_record_header(float4* rk, int next, uint32_t spp, int mat, f3 pos, float pdf, float att) {
+    rk[0] = make_float4(__int_as_float(next), __uint_as_float(spp), __int_as_float(mat), pos.z);
+    rk[1] = make_float4(pdf, att, pos.x, pos.y);
+}
+
 // shade_object + Material::scatter of one hit, deferred form (raytracer.cu:6-57, material.cuh:112-123):
 // the hit record (linked after prev_rec, or as the pixel's head), its light colours and point-light
 // shadow rays go to q; rp / rd / pdf / att become the scattered ray's.
@@ -563,49 +598,22 @@ __device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& 
     if (q.plist) q.plist[(size_t)t * q.max_hits + n_hits] = (int)k;
     ++n_hits;
     float4* rk = q.rec + (size_t)k * q.rec_stride;
-    rk[0] = make_float4(__int_as_float(-1), __uint_as_float(spp), __int_as_float(h.mat), 0.0f);
-    rk[1] = make_float4(pdf, att, 0.0f, 0.0f);
-    float* lc_out = reinterpret_cast<float*>(rk + 2);
+    write_record_header(rk, -1, spp, h.mat, h.pos, pdf, att);
     if (prev_rec < 0) q.head[i] = (int)k;
     else reinterpret_cast<int*>(q.rec + (size_t)prev_rec * q.rec_stride)[0] = (int)k;
     prev_rec = (int)k;
-    uint32_t jl = 0, jp = 0;
     if (q.shade_in) {
         // shading off the chain: keep what rt_shade_records_kernel needs and skip the light
         // samples' draws (3 per light and shadow iteration) -- same RNG position afterwards
         float4* si = q.rec + (size_t)k * q.rec_stride + q.shade_in;
-        si[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, 0.0f);
-        si[1] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.0f);
-        si[2] = make_float4(rd.x, rd.y, rd.z, 0.0f);
-        si[3] = make_float4(__uint_as_float(r.v0), __uint_as_float(r.v1), __uint_as_float(r.v2), __uint_as_float(r.v3));
-        si[4] = make_float4(__uint_as_float(r.v4), __uint_as_float(r.d), 0.0f, 0.0f);
+        si[0] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.0f);
+        si[1] = make_float4(rd.x, rd.y, rd.z, 0.0f);
+        si[2] = make_float4(__uint_as_float(r.v0), __uint_as_float(r.v1), __uint_as_float(r.v2), __uint_as_float(r.v3));
+        si[3] = make_float4(__uint_as_float(r.v4), __uint_as_float(r.d), 0.0f, 0.0f);
         const uint32_t n_draws = 3u * (uint32_t)a.n_lights * a.shadow_iters;
         for (uint32_t j = 0; j < n_draws; ++j) (void)xorwow_next(r);
     } else {
-        for (int l = 0; l < a.n_lights; ++l) {
-            const LightGpu L = a.lights[l];
-            for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
-                const f3 lpos = light_sample(L, r);
-#ifdef RT_TIMING_NO_SHADE   // timing-only builds (not exact): the cost of shade_object's per-sample lighting
-                const float full_dist = 1.0f;
-                const f3 Lv = lpos, lc = lpos;
-#else
-                f3 Lv = lpos - h.pos;
-                const float full_dist = length(Lv);
-                Lv = normalize(Lv);
-                const f3 R = reflect(Lv, h.normal);
-                const f3 V = normalize(-rd);
-                const f3 lc = fmaxf(0.0f, dot(Lv, h.normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
-#endif
-                lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
-                if (L.type == 0) {
-                    float4* sr = q.shadow_ray(k, jp);
-                    sr[0] = make_float4(h.pos.x, h.pos.y, h.pos.z, full_dist);
-                    sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
-                    ++jp;
-                }
-            }
-        }
+        write_light_samples(a, q, k, h.pos, h.normal, rd, m, r);
     }
     const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
     const float lo = curand_uniform(r) * spec;
@@ -890,33 +898,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SPEC_WAVES_
                 if ((uint32_t)b >= nh) break;
                 const uint32_t kr = wbase + wexcl + (uint32_t)b;
                 const bool last = wexcl + (uint32_t)b + 1u == px_first + px_total;
-                float4* rk = q.rec + (size_t)kr * q.rec_stride;
                 const SpecBounce& hb = bh[b];
-                rk[0] = make_float4(__int_as_float(last ? -1 : (int)kr + 1), __uint_as_float((uint32_t)s), __int_as_float(hb.mat), 0.0f);
-                rk[1] = make_float4(hb.pdf, hb.att, 0.0f, 0.0f);
-                float* lc_out = reinterpret_cast<float*>(rk + 2);
-                const MaterialGpu m = a.mats[hb.mat];
+                write_record_header(q.rec + (size_t)kr * q.rec_stride, last ? -1 : (int)kr + 1, (uint32_t)s, hb.mat, hb.pos, hb.pdf, hb.att);
                 Xorwow r = hb.r;
-                uint32_t jl = 0, jp = 0;
-                for (int l = 0; l < a.n_lights; ++l) {
-                    const LightGpu L = a.lights[l];
-                    for (uint32_t si = 0; si < a.shadow_iters; ++si, ++jl) {
-                        const f3 lpos = light_sample(L, r);
-                        f3 Lv = lpos - hb.pos;
-                        const float full_dist = length(Lv);
-                        Lv = normalize(Lv);
-                        const f3 R = reflect(Lv, hb.normal);
-                        const f3 V = normalize(-hb.rd);
-                        const f3 lc = fmaxf(0.0f, dot(Lv, hb.normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
-                        lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
-                        if (L.type == 0) {
-                            float4* sr = q.shadow_ray(kr, jp);
-                            sr[0] = make_float4(hb.pos.x, hb.pos.y, hb.pos.z, full_dist);
-                            sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
-                            ++jp;
-                        }
-                    }
-                }
+                write_light_samples(a, q, kr, hb.pos, hb.normal, hb.rd, a.mats[hb.mat], r);
             }
         }
         // ---- depth from the first-bounce positions summed in sample order; final XORWOW state
@@ -1049,34 +1034,12 @@ __global__ __launch_bounds__(256) void rt_shade_kernel(RaytraceArgs a, RtQueue q
             const MaterialGpu m = a.mats[o.mat_id];
             Xorwow r = load_rng(rng, n_rng, pix);
             // hit record, appended to the pixel's list (stages run in the pixel's path order)
-            float4* rk = q.rec + (size_t)k * q.rec_stride;
-            rk[0] = make_float4(__int_as_float(-1), __uint_as_float(spp), __int_as_float(o.mat_id), 0.0f);
-            rk[1] = make_float4(pdf, att, 0.0f, 0.0f);
-            float* lc_out = reinterpret_cast<float*>(rk + 2);
+            write_record_header(q.rec + (size_t)k * q.rec_stride, -1, spp, o.mat_id, hpos, pdf, att);
             const int prev = st.tail[pix];
             if (prev < 0) q.head[pix] = (int)k;
             else reinterpret_cast<int*>(q.rec + (size_t)prev * q.rec_stride)[0] = (int)k;
             st.tail[pix] = (int)k;
-            uint32_t jl = 0, jp = 0;
-            for (int l = 0; l < a.n_lights; ++l) {
-                const LightGpu L = a.lights[l];
-                for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
-                    const f3 lpos = light_sample(L, r);
-                    f3 Lv = lpos - hpos;
-                    const float full_dist = length(Lv);
-                    Lv = normalize(Lv);
-                    const f3 R = reflect(Lv, normal);
-                    const f3 V = normalize(-rd);
-                    const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
-                    lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
-                    if (L.type == 0) {
-                        float4* sr = q.shadow_ray(k, jp);
-                        sr[0] = make_float4(hpos.x, hpos.y, hpos.z, full_dist);
-                        sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
-                        ++jp;
-                    }
-                }
-            }
+            write_light_samples(a, q, k, hpos, normal, rd, m, r);
             // Material::scatter (material.cuh:112-123)
             const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
             const float lo = curand_uniform(r) * spec;
@@ -1137,33 +1100,12 @@ __global__ __launch_bounds__(512) void rt_bounce_kernel(RaytraceArgs a, RtStage 
 __global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, RtQueue q) {
     const uint32_t n = *q.count;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        float4* rk = q.rec + (size_t)k * q.rec_stride;
+        const float4* rk = q.rec + (size_t)k * q.rec_stride;
         const float4* si = rk + q.shade_in;
-        const float4 s0 = si[0], s1 = si[1], s2 = si[2], s3 = si[3], s4 = si[4];
-        const f3 pos = mk(s0.x, s0.y, s0.z), normal = mk(s1.x, s1.y, s1.z), rd = mk(s2.x, s2.y, s2.z);
-        Xorwow r{__float_as_uint(s3.x), __float_as_uint(s3.y), __float_as_uint(s3.z), __float_as_uint(s3.w), __float_as_uint(s4.x), __float_as_uint(s4.y)};
-        const MaterialGpu m = a.mats[__float_as_int(rk[0].z)];
-        float* lc_out = reinterpret_cast<float*>(rk + 2);
-        uint32_t jl = 0, jp = 0;
-        for (int l = 0; l < a.n_lights; ++l) {
-            const LightGpu L = a.lights[l];
-            for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
-                const f3 lpos = light_sample(L, r);
-                f3 Lv = lpos - pos;
-                const float full_dist = length(Lv);
-                Lv = normalize(Lv);
-                const f3 R = reflect(Lv, normal);
-                const f3 V = normalize(-rd);
-                const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
-                lc_out[3 * jl + 0] = lc.x; lc_out[3 * jl + 1] = lc.y; lc_out[3 * jl + 2] = lc.z;
-                if (L.type == 0) {
-                    float4* sr = q.shadow_ray(k, jp);
-                    sr[0] = make_float4(pos.x, pos.y, pos.z, full_dist);
-                    sr[1] = make_float4(Lv.x, Lv.y, Lv.z, 0.0f);
-                    ++jp;
-                }
-            }
-        }
+        const float4 h0 = rk[0], h1 = rk[1], s0 = si[0], s1 = si[1], s2 = si[2], s3 = si[3];
+        const f3 pos = mk(h1.z, h1.w, h0.w), normal = mk(s0.x, s0.y, s0.z), rd = mk(s1.x, s1.y, s1.z);
+        Xorwow r{__float_as_uint(s2.x), __float_as_uint(s2.y), __float_as_uint(s2.z), __float_as_uint(s2.w), __float_as_uint(s3.x), __float_as_uint(s3.y)};
+        write_light_samples(a, q, k, pos, normal, rd, a.mats[__float_as_int(h0.z)], r);
     }
 }
 
@@ -1197,10 +1139,11 @@ __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQue
         const uint32_t j = c * 64u + (uint32_t)lane;
         if (j >= total) continue;
         const uint32_t kr = j / q.nps, jp = j - kr * q.nps;   // record, shadow sample (RtQueue::shadow_ray)
-        const float4* sr = q.shadow_ray(kr, jp);
-        const float4 s0 = sr[0], s1 = sr[1];
-        const f3 pos = mk(s0.x, s0.y, s0.z), Lv = mk(s1.x, s1.y, s1.z);
-        const float full_dist = s0.w;
+        const float4 s1 = *q.shadow_ray(kr, jp);
+        const float4* rk = q.rec + (size_t)kr * q.rec_stride;   // the origin: the record's hit position (header)
+        const float4 h0 = rk[0], h1 = rk[1];
+        const f3 pos = mk(h1.z, h1.w, h0.w), Lv = mk(s1.x, s1.y, s1.z);
+        const float full_dist = s1.w;
         int oh = -1;
 #ifdef SHADOW_TIMING_NO_BVH   // timing-only builds (not exact): which half of a shadow ray costs what
         const float syn = MAX_DEPTH;
@@ -1240,14 +1183,14 @@ __global__ __launch_bounds__(256) void rt_record_colour_kernel(RaytraceArgs a, R
         if (lane < nk) {
             const float4* rk = recs + lane * rs;
             const float4 h0 = rk[0], h1 = rk[1];
-            const float* lc = reinterpret_cast<const float*>(rk + 2);
+            const float4* lc = rk + 2;
             const float* mk_ = masks + lane * q.nps;
             f3 color = splat(0.0f);
             uint32_t jl = 0, jp = 0;
             for (int l = 0; l < a.n_lights; ++l) {
                 const bool point = a.lights[l].type == 0;
                 for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
-                    const f3 c = mk(lc[3 * jl], lc[3 * jl + 1], lc[3 * jl + 2]);
+                    const f3 c = mk(lc[jl].x, lc[jl].y, lc[jl].z);
                     if (point) color = color + c * mk_[jp++];
                     else color = color + c;
                 }
@@ -1304,13 +1247,13 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
             const float4* rk = q.rec + (size_t)k * q.rec_stride;
             const float4 h0 = rk[0], h1 = rk[1];
             if (__float_as_uint(h0.y) != spp) break;
-            const float* lc = reinterpret_cast<const float*>(rk + 2);
+            const float4* lc = rk + 2;
             f3 color = splat(0.0f);
             uint32_t jl = 0, jp = 0;
             for (int l = 0; l < a.n_lights; ++l) {
                 const bool point = a.lights[l].type == 0;
                 for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
-                    const f3 c = mk(lc[3 * jl], lc[3 * jl + 1], lc[3 * jl + 2]);
+                    const f3 c = mk(lc[jl].x, lc[jl].y, lc[jl].z);
                     if (point) color = color + c * q.mask[q.mask_at((uint32_t)k, jp++)];
                     else color = color + c;
                 }

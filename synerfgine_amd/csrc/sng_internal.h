@@ -241,20 +241,20 @@ struct RaytraceArgs {
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
-// sample, bounce) that hit an object: header {next, spp, mat, -} {pdf, att, -, -} + the light
-// colour lc of every (light, shadow iteration) in loop order.  One "shadow ray" per point-light
-// sample: {pos, full_dist} {L, -}; its mask is written by the shadow kernel.
+// sample, bounce) that hit an object: header {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y} + the
+// light colour {lc, 0} of every (light, shadow iteration) in loop order.  One "shadow ray" per
+// point-light sample: {L, full_dist} (origin: its record's pos); its mask is written by the shadow kernel.
 struct RtQueue {
-    float4* rec;          // cap x rec_stride float4
-    float4* srec;         // cap x nps x 2 float4
+    float4* rec;          // cap x rec_stride float4: {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y} {lc_jl, 0} x nls
+    float4* srec;         // cap x nps float4: {L, full_dist} (origin: the record's pos)
     float* mask;          // cap x nps
     int* head;            // per mesh pixel: first hit record or -1
     uint32_t* count;      // hit records allocated (device counter)
-    uint32_t rec_stride;  // float4 per hit record = 2 + ceil(3 * nls / 4)
+    uint32_t rec_stride;  // float4 per hit record = 2 + nls
     uint32_t nls;         // n_lights * shadow_iters
     uint32_t nps;         // n_point_lights * shadow_iters
     uint32_t cap;
-    uint32_t shade_in;    // > 0: float4 offset of the deferred-shading inputs {pos} {normal} {rd} {rng v0-v3} {rng v4, d}
+    uint32_t shade_in;    // > 0: float4 offset of the deferred-shading inputs {normal} {rd} {rng v0-v3} {rng v4, d}
                           // in each record; raytrace_kernel skips the light samples' draws and
                           // rt_shade_records_kernel computes lc + shadow rays off the path chain
     // per-pixel record lists (tile path kernel): plist[t * max_hits + h] = the pixel's h-th hit record, pcount[t]
@@ -267,7 +267,7 @@ struct RtQueue {
     // shadow ray jp of hit record k, record-major ([k][jp]): a wave traces the nps shadow samples of 64 / nps
     // consecutive records.  (Sample-major, [jp][k] -- 64 records towards one light sample per wave --
     // measured 40 % slower: the rays of one hit point share their walk until they part towards the lights.)
-    __host__ __device__ float4* shadow_ray(uint32_t k, uint32_t jp) const { return srec + 2 * ((size_t)k * nps + jp); }
+    __host__ __device__ float4* shadow_ray(uint32_t k, uint32_t jp) const { return srec + (size_t)k * nps + jp; }
     __host__ __device__ size_t mask_at(uint32_t k, uint32_t jp) const { return (size_t)k * nps + jp; }
 };
 

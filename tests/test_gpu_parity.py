@@ -686,3 +686,42 @@ def test_nerf_gbuffer_matches_oracle():
         assert (np.abs(nrm - rn).max(axis=-1)[m] <= 1e-4).mean() >= 0.995
     finally:
         tb.close()
+
+
+@pytest.mark.parametrize("n_exp", [255.0, 500.0, 37.5])
+def test_high_phong_exponent_frame_matches_oracle(tmp_path, n_exp):
+    """Phong exponents in the hundreds (pow_small_int's binary exponentiation: relative error grows ~ n * 2^-24,
+    mirrored by the oracle; the reference's --use_fast_math __powf is coarser still) and a non-integer one (powf).
+    Tolerance as for every whole frame: PSNR >= 40 dB, >= 99.5 % of pixels within 2/255."""
+    import json
+
+    import oracle as O
+    from synerfgine_amd import Engine, Testbed
+    from synerfgine_amd import scene as S
+    src = os.path.join(S.SCENES, "armadillo.json")
+    sc = json.load(open(src))
+    sc["materials"] = [{"id": 0, "type": "glossy", "n": n_exp, "rg": 0.5, "kd": [0.6, 0.2, 0.3], "ks": [1.0, 1.0, 1.0], "spec_angle": 0.2}]
+    for o in sc["objfile"]:
+        o["file"] = os.path.join(os.path.dirname(src), o["file"])
+    p = tmp_path / "phong.json"
+    p.write_text(json.dumps(sc))
+    cfg, params, grid = S.model_for("c3", 1337, "synthetic")
+    tb = Testbed(0)
+    try:
+        tb.set_nerf_model(cfg, params)
+        tb.set_density_grid(grid)
+        eng = Engine(tb)
+        eng.set_virtual_world(str(p))
+        eng.set_param("camera_path_playing", 0)
+        eng.set_param("res_factor", 8)
+        eng.init(128, 72)
+        nrng, mrng = eng.rng_states(0).copy(), eng.rng_states(1).copy()
+        fin = eng.frame(spp=0, reset=True).download("final_rgba")
+        ref = O.render_frame(O.Model(cfg, params), O.volume_for(cfg, grid), tb, eng, nrng, mrng)
+    finally:
+        tb.close()
+    exp = ref["final"]
+    assert np.isfinite(fin).all()
+    p_db = _psnr(fin[..., :3], exp[..., :3])
+    close = (np.abs(np.clip(fin, 0, 1) - np.clip(exp, 0, 1))[..., :3].max(axis=-1) <= 2 / 255).mean()
+    assert p_db >= 40.0 and close >= 0.995, f"PSNR {p_db:.2f} dB, {close:.4f} of pixels within 2/255"

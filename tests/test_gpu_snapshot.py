@@ -190,3 +190,28 @@ def test_malformed_optimizer_block_keeps_the_inference_model(data, tmp_path):
     finally:
         for tb in tbs:
             tb.close()
+
+
+def test_dataset_scale_and_offset_survive_load_and_save(tmp_path):
+    """nerf.dataset.scale / offset of a loaded snapshot are written back by save_snapshot (the reference writes
+    m_nerf.training.dataset as loaded, and adopts it when a snapshot is loaded without data)."""
+    import gzip
+
+    from synerfgine_amd import Testbed
+    with open(os.path.join(REPO, "data", "lego.ingp"), "rb") as f:   # zlib or gzip wrapped (wbits 47: either)
+        snap = msgpack.unpackb(zlib.decompress(f.read(), 47), raw=False, strict_map_key=False)
+    ds = snap["snapshot"]["nerf"].setdefault("dataset", {})
+    ds["scale"] = 0.5
+    ds["offset"] = [0.25, 0.5, 0.75]
+    src = tmp_path / "src.ingp"
+    src.write_bytes(gzip.compress(msgpack.packb(snap, use_bin_type=True)))
+    tb = Testbed(0)
+    try:
+        tb.load_snapshot(str(src))
+        tb.save_snapshot(str(tmp_path / "out.ingp"))
+    finally:
+        tb.close()
+    out = _decode(tmp_path / "out.ingp")
+    ds = (out["snapshot"] if "snapshot" in out else out)["nerf"]["dataset"]
+    assert ds["scale"] == 0.5
+    assert [float(v) for v in ds["offset"]] == [0.25, 0.5, 0.75]

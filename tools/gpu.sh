@@ -8,6 +8,7 @@
 #   driver                 bench.py with no flags (the driver's own line, incl. CPU baseline and extra legs)
 #   prof[:CFG[:ARGS]]      rocprofv3 --kernel-trace --stats of a short bench.py run (ARGS as for bench)
 #   pmc[:CFG[:ARGS]]       FETCH_SIZE / WRITE_SIZE / MFMA PMC passes (one rocprofv3 run each) + tools/pmc_summary.py
+#   sq[:CFG[:ARGS]]        SQ_INSTS_* + SQ_WAVE_CYCLES pass with kernel trace + tools/sq_summary.py (VALU roofline)
 #   py:SCRIPT[:ARGS]       python3 tools/SCRIPT ARGS
 # Output goes to gpurun_out/$TAG/ (TAG defaults to "run"), one log per step.
 set -o pipefail
@@ -57,6 +58,13 @@ for step in "$@"; do
         rc=$?; echo "MFMA rc=$rc"
       fi
       [ $rc -eq 0 ] && python3 tools/pmc_summary.py $d $OUT/pmc_traffic_${cfg:-c3}.json ${cfg:-c3} > $log 2>&1; rc=$? ;;
+    sq)
+      # SQ instruction counts + kernel durations in one counter pass (serialised kernels) -> VALU roofline
+      d=$OUT/sq$n
+      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+        -d $d -o run --output-format csv -- python3 bench.py --config ${cfg:-c3} --steps 3 --warmup 1 --no-cpu-baseline --no-sweep $args > $log 2>&1
+      rc=$?
+      [ $rc -eq 0 ] && python3 tools/sq_summary.py $d $OUT/sq_${cfg:-c3}.json ${cfg:-c3} 2>&1 | tee -a $log; rc=${PIPESTATUS[0]} ;;
     py)
       timeout -k 10 600 python3 -u tools/$cfg $args > $log 2>&1
       rc=$?; tail -c 3000 $log; echo ;;
