@@ -457,7 +457,7 @@ struct sng_ctx {
     DevBuf samp, coords, net_out, ctrl;
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
-    DevBuf rt_rec, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
+    DevBuf rt_rec, rt_lc, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf rt_hint;                        // sample-parallel path kernel: per-pixel hit-depth sums of the previous frame (u8)
@@ -1516,22 +1516,23 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             RtQueue q{};
             q.nls = (uint32_t)c->lights.size() * ra.shadow_iters;
             q.nps = n_point * ra.shadow_iters;
-            q.rec_stride = 2 + q.nls;
+            q.rec_stride = 2;
             // deferred shading inputs after the light colours (not in staged mode, which shades per stage)
             if (c->p("rt_defer_shade") != 0.0 && c->p("rt_staged") == 0.0) {
                 q.shade_in = q.rec_stride;
                 q.rec_stride += 4;
             }
-            const uint64_t bytes = cap * (16ull * q.rec_stride + 16ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
+            const uint64_t bytes = cap * (16ull * q.rec_stride + 16ull * q.nls + 16ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
             const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
                                    bytes <= (uint64_t)(c->p("rt_queue_gb") * 1073741824.0);
             if (wavefront) {
                 c->rt_rec.ensure(cap * 16ull * q.rec_stride);
                 c->rt_srec.ensure(cap * 16ull * q.nps);
+                c->rt_lc.ensure(cap * 16ull * std::max<uint32_t>(1u, q.nls));
                 c->rt_mask.ensure(cap * 4ull * q.nps);
                 c->rt_head.ensure((uint64_t)MW * MH * 4);
                 c->rt_count.ensure(16);
-                q.rec = c->rt_rec.as<float4>(); q.srec = c->rt_srec.as<float4>(); q.mask = c->rt_mask.as<float>();
+                q.rec = c->rt_rec.as<float4>(); q.lc = c->rt_lc.as<float4>(); q.srec = c->rt_srec.as<float4>(); q.mask = c->rt_mask.as<float>();
                 q.head = c->rt_head.as<int>(); q.count = c->rt_count.as<uint32_t>(); q.cap = (uint32_t)cap;
                 if (c->p("rt_staged") != 0.0) {
                     c->rt_hits.ensure(n_px * 48);
@@ -1936,7 +1937,7 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_trit.release(); o.d_wide.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_lc, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
                       &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); c->ray_kk[b].release(); }

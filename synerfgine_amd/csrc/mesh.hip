@@ -554,13 +554,12 @@ __device__ __forceinline__ TraceCtx<LDS, CNT> trace_ctx_setup(const RaytraceArgs
 }
 
 // shade_object's light loop of one hit (raytracer.cu:16-50) in deferred form: per (light, shadow
-// iteration) jl the light colour -> record slot 2 + jl {lc, 0}; per point-light sample jp the shadow
-// ray {L, full_dist} -> q.shadow_ray(k, jp) (its origin, the hit position, is in the record header).
-// One 16-B store each: a wave's lanes write to 64 records at once, so every store instruction costs
-// one cache line per lane -- the float4 slots cut those instructions from 5 to 2 per light sample.
+// iteration) jl the light colour {lc, 0} -> q.lc_at(k, jl); per point-light sample jp the shadow ray
+// {L, full_dist} -> q.shadow_ray(k, jp) (its origin, the hit position, is in the record header).
+// One 16-B store each, sample-major (RtQueue): the lanes' consecutive records make each store one
+// contiguous run.
 __device__ __forceinline__ void write_light_samples(const RaytraceArgs& a, const RtQueue& q, uint32_t k, f3 pos, f3 normal, f3 rd,
                                                     const MaterialGpu& m, Xorwow& r) {
-    float4* lc_out = q.rec + (size_t)k * q.rec_stride + 2;
     const f3 V = normalize(-rd);
     uint32_t jl = 0, jp = 0;
     for (int l = 0; l < a.n_lights; ++l) {
@@ -577,7 +576,7 @@ __device__ __forceinline__ void write_light_samples(const RaytraceArgs& a, const
             const f3 R = reflect(Lv, normal);
             const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
 #endif
-            lc_out[jl] = make_float4(lc.x, lc.y, lc.z, 0.0f);
+            *q.lc_at(k, jl) = make_float4(lc.x, lc.y, lc.z, 0.0f);
             if (L.type == 0) *q.shadow_ray(k, jp++) = make_float4(Lv.x, Lv.y, Lv.z, full_dist);
         }
     }
@@ -1183,14 +1182,14 @@ __global__ __launch_bounds__(256) void rt_record_colour_kernel(RaytraceArgs a, R
         if (lane < nk) {
             const float4* rk = recs + lane * rs;
             const float4 h0 = rk[0], h1 = rk[1];
-            const float4* lc = rk + 2;
             const float* mk_ = masks + lane * q.nps;
             f3 color = splat(0.0f);
             uint32_t jl = 0, jp = 0;
             for (int l = 0; l < a.n_lights; ++l) {
                 const bool point = a.lights[l].type == 0;
                 for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
-                    const f3 c = mk(lc[jl].x, lc[jl].y, lc[jl].z);
+                    const float4 l4 = *q.lc_at(k0 + lane, jl);
+                    const f3 c = mk(l4.x, l4.y, l4.z);
                     if (point) color = color + c * mk_[jp++];
                     else color = color + c;
                 }
@@ -1247,13 +1246,13 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
             const float4* rk = q.rec + (size_t)k * q.rec_stride;
             const float4 h0 = rk[0], h1 = rk[1];
             if (__float_as_uint(h0.y) != spp) break;
-            const float4* lc = rk + 2;
             f3 color = splat(0.0f);
             uint32_t jl = 0, jp = 0;
             for (int l = 0; l < a.n_lights; ++l) {
                 const bool point = a.lights[l].type == 0;
                 for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
-                    const f3 c = mk(lc[jl].x, lc[jl].y, lc[jl].z);
+                    const float4 l4 = *q.lc_at((uint32_t)k, jl);
+                    const f3 c = mk(l4.x, l4.y, l4.z);
                     if (point) color = color + c * q.mask[q.mask_at((uint32_t)k, jp++)];
                     else color = color + c;
                 }

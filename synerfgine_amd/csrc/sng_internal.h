@@ -241,16 +241,20 @@ struct RaytraceArgs {
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
-// sample, bounce) that hit an object: header {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y} + the
-// light colour {lc, 0} of every (light, shadow iteration) in loop order.  One "shadow ray" per
-// point-light sample: {L, full_dist} (origin: its record's pos); its mask is written by the shadow kernel.
+// sample, bounce) that hit an object: header {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y}, and the
+// light colour {lc, 0} of every (light, shadow iteration) jl in loop order.  One "shadow ray" per
+// point-light sample jp: {L, full_dist} (origin: its record's pos); its mask is written by the shadow
+// kernel.  Light colours and shadow rays are stored sample-major ([jl][k], [jp][k]): the lanes of a
+// wave shade consecutive records (wave_alloc), so each of their stores is one contiguous 1-KiB run
+// instead of 64 scattered 16-B pieces (record-major scatter ran at ~1.7 TB/s, C3 rt_shade_records).
 struct RtQueue {
-    float4* rec;          // cap x rec_stride float4: {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y} {lc_jl, 0} x nls
-    float4* srec;         // cap x nps float4: {L, full_dist} (origin: the record's pos)
+    float4* rec;          // cap x rec_stride float4: {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y} [+ shade inputs]
+    float4* lc;           // nls x cap float4: {lc, 0} of record k, light sample jl at [jl * cap + k]
+    float4* srec;         // nps x cap float4: {L, full_dist} of record k, shadow sample jp at [jp * cap + k]
     float* mask;          // cap x nps
     int* head;            // per mesh pixel: first hit record or -1
     uint32_t* count;      // hit records allocated (device counter)
-    uint32_t rec_stride;  // float4 per hit record = 2 + nls
+    uint32_t rec_stride;  // float4 per hit record = 2 (+ 4 shade inputs)
     uint32_t nls;         // n_lights * shadow_iters
     uint32_t nps;         // n_point_lights * shadow_iters
     uint32_t cap;
@@ -264,10 +268,12 @@ struct RtQueue {
     uint8_t* pcount;
     float4* rval;         // {colour * pdf * att, spp bits}
     uint32_t max_hits;    // samples * bounces (<= 255)
-    // shadow ray jp of hit record k, record-major ([k][jp]): a wave traces the nps shadow samples of 64 / nps
-    // consecutive records.  (Sample-major, [jp][k] -- 64 records towards one light sample per wave --
-    // measured 40 % slower: the rays of one hit point share their walk until they part towards the lights.)
-    __host__ __device__ float4* shadow_ray(uint32_t k, uint32_t jp) const { return srec + (size_t)k * nps + jp; }
+    // The shadow kernel traces in record-major order (a wave: the nps shadow samples of 64 / nps consecutive
+    // records; sample-major tracing -- 64 records towards one light sample per wave -- measured 40 % slower:
+    // the rays of one hit point share their walk until they part towards the lights); the storage is
+    // sample-major (writes coalesce, the shadow kernel's reads are nps runs of 64 / nps records).
+    __host__ __device__ float4* shadow_ray(uint32_t k, uint32_t jp) const { return srec + (size_t)jp * cap + k; }
+    __host__ __device__ float4* lc_at(uint32_t k, uint32_t jl) const { return lc + (size_t)jl * cap + k; }
     __host__ __device__ size_t mask_at(uint32_t k, uint32_t jp) const { return (size_t)k * nps + jp; }
 };
 
