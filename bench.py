@@ -30,7 +30,7 @@ BYTES_PER_SAMPLE = 28 + 8 * 8 * 4 * 2 + 8   # NerfCoordinate read + 8 levels x 8
 FLOPS_PER_SAMPLE = 20480                     # 2*(32*64+64*16) + 2*(32*64+64*64+64*16)
 HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F16_PEAK_TFLOPS = 2500.0                # dense fp16/bf16 MFMA
-ROUND = "r02"
+ROUND = "r03"
 
 WORKLOADS = {
     "c2": "lego NeRF only (show_virtual_obj=0, shadows off)",
@@ -56,7 +56,7 @@ def parse():
                                                             "dmrf-compare-abm --sshadows/--nshadows sweep)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed oracle runs per CPU-baseline leg (median reported)")
     ap.add_argument("--serial-streams", action="store_true", help="run raytracer and NeRF back to back (profiling)")
-    ap.add_argument("--cpu-baseline-scale", type=float, default=1.5, help="the C3-sample leg renders the frame at 1/scale linear resolution")
+    ap.add_argument("--cpu-baseline-scale", type=float, default=1.0, help="the C3-sample leg renders the frame at 1/scale linear resolution")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help="gloo: CPU-side gather (rehearsal on one GPU)")
     ap.add_argument("--dry-run", action="store_true", help="form the ranks and exchange the world size only (no GPU; CPU tests)")
     ap.add_argument("--even-bands", action="store_true", help="equal-height bands instead of cost-balanced ones")
@@ -98,7 +98,14 @@ def cpu_info():
                 break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model}
+    quota = None
+    try:   # cgroup v2 CPU quota (the GPU box grants a share of the host's CPUs; nproc shows them all)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_model": model}
 
 
 def cpu_baseline_c1(model_name, runs):
@@ -171,18 +178,47 @@ def cpu_sample_c3(eng_cfg, config, scale, model_name, overrides):
     return sample, psnr
 
 
+def latest_profile(prefix, config):
+    """profiles/<prefix>_<round>_<config>.json of the newest round that has one (this round's first)."""
+    for rnd in (ROUND, "r02", "r01"):
+        path = os.path.join(REPO, "profiles", f"{prefix}_{rnd}_{config}.json")
+        if os.path.exists(path):
+            return path
+    return None
+
+
 def traffic_profile(config):
-    """HBM bytes per launch of the roofline kernels from this round's PMC passes for this config
-    (tools/gpu_pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 FETCH correction), labelled
+    """HBM bytes per launch of the roofline kernels from the newest PMC passes for this config
+    (tools/gpu.sh pmc: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 FETCH correction), labelled
     with the file they came from; None when no profile of this config exists."""
-    path = os.path.join(REPO, "profiles", f"pmc_traffic_{ROUND}_{config}.json")
-    if not os.path.exists(path):
+    path = latest_profile("pmc_traffic", config)
+    if not path:
         return None
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
     return {"file": os.path.relpath(path, REPO), "config": d.get("config"), "kernels": d.get("roofline_kernels", {})}
+
+
+def valu_profile(config):
+    """VALU roofline of the traversal kernels (tools/gpu.sh sq: SQ_INSTS_VALU per launch over the launch's duration
+    in the same serialised counter pass; peak 1.229e12 wave64 VALU instructions/s), labelled with its file."""
+    path = latest_profile("sq", config)
+    if not path:
+        return None
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    ks = d.get("kernels", {})
+    out = {"source": os.path.relpath(path, REPO), "peak_wave_instr_per_s": 1.2288e12, "bound": "valu"}
+    for k in ("raytrace_kernel", "shadow_rays_kernel"):
+        if k in ks:
+            v = ks[k]
+            out[k] = {"valu_instr_per_launch": v.get("sq_insts_valu_per_launch"), "ms": round(v.get("avg_launch_ms", 0.0), 4),
+                      "frac": round(v.get("valu_frac", 0.0), 4)}
+    return out
 
 
 def frame_cells(eng, cells, frames, warmup, px):
@@ -202,10 +238,14 @@ def frame_cells(eng, cells, frames, warmup, px):
         net_ms = sum(r.ms_network for r in st)
         net_samples = sum(r.n_samples_network for r in st)
         gbs = net_samples * BYTES_PER_SAMPLE / (net_ms * 1e-3) / 1e9 if net_ms > 0 else 0.0
+        ev = sum(r.n_samples - r.n_samples_reused for r in st)
+        f_ms = sum(r.ms_network + r.ms_fused_tail + r.ms_onestep for r in st)
+        fsw = ev * BYTES_PER_SAMPLE / (f_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if f_ms > 0 else 0.0
         r = st[-1]
         out.append({**cell, "frames_per_s": round(frames / el, 2), "ms_frame_device": round(r.ms_frame, 3),
                     "samples_per_px": round(r.n_samples / px, 3), "reference_slots_per_px": round(r.n_reference_slots / px, 3),
-                    "network_roofline_frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "hit_frac": round(r.n_hit / px, 4),
+                    "network_roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "field_sample_weighted_frac": round(fsw, 4),
                     "stages_ms": {"raytrace": round(r.ms_raytrace, 3), "nerf": round(r.ms_nerf, 3), "shadow": round(r.ms_shadow, 3)}})
     return out
 
@@ -224,6 +264,83 @@ def abm_sweep(model, frames, warmup):
                 "cells": frame_cells(eng, cells, frames, warmup, NW * NH)}
     finally:
         tb.close()
+
+
+def _srgb(rgba):
+    import numpy as np
+    lin = np.clip(rgba[..., :3], 0, None)
+    return np.clip(np.where(lin < 0.0031308, 12.92 * lin, 1.055 * np.power(lin, 0.41666) - 0.055), 0, 1)
+
+
+def nerf_views(model, frames, warmup, cpu_check=True):
+    """NeRF-dominated legs (no virtual objects): (a) BASELINE config C2 -- 800x800 at the lego dataset's camera 0
+    (transforms.json frame 0, nerf_matrix_to_ngp, its focal scaled from 400 to 800 px; a view train_lego.py held
+    out), with the model's PSNR against that dataset image (ngp render, 400x400) and the frame's PSNR against the
+    CPU oracle (200x200); (b) a 1920x1080 view filled by the object (the closest of a few zooms whose hit
+    fraction is >= 0.8)."""
+    import math
+
+    import numpy as np
+    from synerfgine_amd import nerf_data
+    from synerfgine_amd import scene as S
+    d = os.path.join(REPO, "data", "nerf", "lego400")
+    meta = json.load(open(os.path.join(d, "transforms.json")))
+    fr0 = meta["frames"][0]
+    cam = nerf_data.nerf_matrix_to_ngp(fr0["transform_matrix"])          # [3 rows, 4 cols]
+    w0 = int(meta.get("w", 400))
+    fl = float(meta.get("fl_x", 0.5 * w0 / math.tan(0.5 * meta["camera_angle_x"])))
+    fov = math.degrees(2.0 * math.atan(0.5 * w0 / fl))                    # resolution-independent
+    out = {"model": model}
+    tb, eng, (ncfg, params, grid) = S.make_engine("c2", width=800, height=800, model=model)
+    try:
+        tb.camera_matrix = np.asarray(cam, np.float32).T.reshape(-1)
+        tb.set_fov(fov)
+        NW, NH = eng.resolution()["nerf"]
+        leg = frame_cells(eng, [{}], frames, warmup, NW * NH)[0]
+        leg.update({"res": [NW, NH], "camera": "data/nerf/lego400/transforms.json frames[0] (" + fr0["file_path"] + "), fov %.3f deg" % fov})
+        # model quality at the dataset's resolution: ngp render path (render_mode Shade) vs the image, premultiplied on black
+        eng.init(w0, w0)
+        tb.camera_matrix = np.asarray(cam, np.float32).T.reshape(-1)
+        tb.set_fov(fov)
+        rgba = eng.render_nerf(render_mode=1).download("nerf_rgba")
+        gt = nerf_data.read_png(os.path.join(d, fr0["file_path"].lstrip("./") + ("" if fr0["file_path"].endswith(".png") else ".png"))).astype(np.float32) / 255.0
+        mse = float(np.mean((_srgb(rgba) - gt[..., :3] * gt[..., 3:4]) ** 2))
+        leg["psnr_vs_dataset_image_db"] = round(10 * np.log10(1.0 / max(mse, 1e-12)), 2)
+        if cpu_check:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle as O
+            eng.init(200, 200)
+            tb.camera_matrix = np.asarray(cam, np.float32).T.reshape(-1)
+            tb.set_fov(fov)
+            nrng, mrng = eng.rng_states(0).copy(), eng.rng_states(1).copy()
+            got = eng.frame(spp=0, reset=True).download("final_rgba")
+            ref = O.render_frame(O.Model(ncfg, params), O.volume_for(ncfg, grid), tb, eng, nrng, mrng)["final"]
+            err = np.abs(np.clip(got[..., :3], 0, 1) - np.clip(ref[..., :3], 0, 1))
+            leg["psnr_vs_oracle_db"] = round(10 * np.log10(1.0 / max(float(np.mean(err ** 2)), 1e-12)), 2)
+            leg["psnr_vs_oracle_res"] = [200, 200]
+        out["c2_dataset_view"] = leg
+    finally:
+        tb.close()
+    tb, eng, _ = S.make_engine("c2", width=1920, height=1080, model=model)
+    try:
+        NW, NH = eng.resolution()["nerf"]
+        pick = None
+        for scale in (1.0, 0.85, 0.7, 0.6, 0.5):
+            tb.set_camera_view((0.62, 0.46, -0.64), (0.5, 0.5, 0.5), scale)
+            r = eng.frame(spp=0, reset=True)
+            hf = r.n_hit / float(NW * NH)
+            if pick is None or hf > pick[1]:
+                pick = (scale, hf)
+            if hf >= 0.8:
+                pick = (scale, hf)
+                break
+        tb.set_camera_view((0.62, 0.46, -0.64), (0.5, 0.5, 0.5), pick[0])
+        leg = frame_cells(eng, [{}], frames, warmup, NW * NH)[0]
+        leg.update({"res": [NW, NH], "camera": "view dir (0.62, 0.46, -0.64) at (0.5, 0.5, 0.5), zoom scale %.2f" % pick[0]})
+        out["frame_filling_1080p"] = leg
+    finally:
+        tb.close()
+    return out
 
 
 def dry_run(args, rank, world):
@@ -459,7 +576,8 @@ def main():
                 q = cnt["path"]["queries"] + cnt["shadow"]["queries"]
                 boxes = cnt["path"]["box_tests"] + cnt["shadow"]["box_tests"]
                 tris = cnt["path"]["tri_tests"] + cnt["shadow"]["tri_tests"]
-                result["bvh"] = {"per_frame": cnt, "rays_per_s": round(q / rt_s, 1) if rt_s > 0 else None,
+                result["bvh"] = {"per_frame": cnt, "valu_roofline": valu_profile(args.config),
+                                 "rays_per_s": round(q / rt_s, 1) if rt_s > 0 else None,
                                  "box_tests_per_s": round(boxes / rt_s, 1) if rt_s > 0 else None,
                                  "tri_tests_per_s": round(tris / rt_s, 1) if rt_s > 0 else None,
                                  "raytrace_stage_ms": round(s0.ms_raytrace, 3),
@@ -472,6 +590,11 @@ def main():
             result["abm_sweep"] = abm_sweep(args.model if args.config != "c4" else "lego", 3, 1)
         except Exception as e:
             result["abm_sweep"] = {"error": repr(e)}
+        try:
+            if os.path.exists(S.LEGO_INGP):
+                result["nerf_views"] = nerf_views("lego", 10, 2, cpu_check=not args.no_cpu_baseline)
+        except Exception as e:
+            result["nerf_views"] = {"error": repr(e)}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
             legs, threads = cpu_baseline_c1(args.model if args.config != "c4" else "lego", args.cpu_runs)

@@ -58,13 +58,16 @@ for step in "$@"; do
         rc=$?; echo "MFMA rc=$rc"
       fi
       [ $rc -eq 0 ] && python3 tools/pmc_summary.py $d $OUT/pmc_traffic_${cfg:-c3}.json ${cfg:-c3} > $log 2>&1; rc=$? ;;
-    sq)
-      # SQ instruction counts + kernel durations in one counter pass (serialised kernels) -> VALU roofline
+    sq|sqlds)
+      # SQ instruction counts + kernel durations in one counter pass (serialised kernels) -> VALU roofline;
+      # sqlds: LDS-array cycles / bank conflicts / waits instead
       d=$OUT/sq$n
-      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+      ctr="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
+      [ $kind = sqlds ] && ctr="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $ctr \
         -d $d -o run --output-format csv -- python3 bench.py --config ${cfg:-c3} --steps 3 --warmup 1 --no-cpu-baseline --no-sweep $args > $log 2>&1
       rc=$?
-      [ $rc -eq 0 ] && python3 tools/sq_summary.py $d $OUT/sq_${cfg:-c3}.json ${cfg:-c3} 2>&1 | tee -a $log; rc=${PIPESTATUS[0]} ;;
+      [ $rc -eq 0 ] && python3 tools/sq_summary.py $d $OUT/${kind}_${cfg:-c3}.json ${cfg:-c3} 2>&1 | tee -a $log; rc=${PIPESTATUS[0]} ;;
     py)
       timeout -k 10 600 python3 -u tools/$cfg $args > $log 2>&1
       rc=$?; tail -c 3000 $log; echo ;;
