@@ -274,10 +274,10 @@ def _srgb(rgba):
 
 def nerf_views(model, frames, warmup, cpu_check=True):
     """NeRF-dominated legs (no virtual objects): (a) BASELINE config C2 -- 800x800 at the lego dataset's camera 0
-    (transforms.json frame 0, nerf_matrix_to_ngp, its focal scaled from 400 to 800 px; a view train_lego.py held
+    (transforms.json frame 0, nerf_matrix_to_ngp, its camera_angle_x field of view; a view train_lego.py held
     out), with the model's PSNR against that dataset image (ngp render, 400x400) and the frame's PSNR against the
-    CPU oracle (200x200); (b) a 1920x1080 view filled by the object (the closest of a few zooms whose hit
-    fraction is >= 0.8)."""
+    CPU oracle (200x200); (b) a 1920x1080 close-up: of three zooms with the camera outside the unit cube, the one
+    whose rays hit the object most."""
     import math
 
     import numpy as np
@@ -288,8 +288,9 @@ def nerf_views(model, frames, warmup, cpu_check=True):
     fr0 = meta["frames"][0]
     cam = nerf_data.nerf_matrix_to_ngp(fr0["transform_matrix"])          # [3 rows, 4 cols]
     w0 = int(meta.get("w", 400))
-    fl = float(meta.get("fl_x", 0.5 * w0 / math.tan(0.5 * meta["camera_angle_x"])))
-    fov = math.degrees(2.0 * math.atan(0.5 * w0 / fl))                    # resolution-independent
+    # the focal data/lego.ingp was trained with (tools/train_lego.py FOCAL_FROM_ANGLE=1): the Blender
+    # camera_angle_x, not the fl_x the file also carries
+    fov = math.degrees(meta["camera_angle_x"])
     out = {"model": model}
     tb, eng, (ncfg, params, grid) = S.make_engine("c2", width=800, height=800, model=model)
     try:
@@ -325,15 +326,12 @@ def nerf_views(model, frames, warmup, cpu_check=True):
     try:
         NW, NH = eng.resolution()["nerf"]
         pick = None
-        for scale in (1.0, 0.85, 0.7, 0.6, 0.5):
+        for scale in (1.2, 1.0, 0.9):   # camera distance from the centre >= 0.9 > the cube's half diagonal
             tb.set_camera_view((0.62, 0.46, -0.64), (0.5, 0.5, 0.5), scale)
             r = eng.frame(spp=0, reset=True)
             hf = r.n_hit / float(NW * NH)
             if pick is None or hf > pick[1]:
                 pick = (scale, hf)
-            if hf >= 0.8:
-                pick = (scale, hf)
-                break
         tb.set_camera_view((0.62, 0.46, -0.64), (0.5, 0.5, 0.5), pick[0])
         leg = frame_cells(eng, [{}], frames, warmup, NW * NH)[0]
         leg.update({"res": [NW, NH], "camera": "view dir (0.62, 0.46, -0.64) at (0.5, 0.5, 0.5), zoom scale %.2f" % pick[0]})
