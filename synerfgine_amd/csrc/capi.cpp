@@ -345,6 +345,7 @@ const std::map<std::string, double>& default_params() {
         {"rt_tile", 8},                         // path-kernel tile edge: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
+        {"nerf_gbuffer", 0},                    // 1: NeRF normals every frame (otherwise only when shadow_on_nerf needs them)
         {"rt_plist", 1},                        // per-pixel hit-record lists for the colour replay (rt_accumulate_kernel)
         {"glow_mode", 0},                       // Testbed::Nerf::glow_mode (testbed.h:871): bits 1 green grid, 2 cut line, 4 mask to alpha,
                                                 // 8 radial, 16 grid mode -- instant-NGP path only (testbed_nerf.cu:638-734)
@@ -360,8 +361,9 @@ const std::map<std::string, double>& default_params() {
         {"train_random_bg", 1},                 // m_nerf.training.random_bg_color (testbed.h:790)
         {"train_debug", 0},                     // parity hook: generate writes per-ray step counts (sng_train_debug)
         {"nerf_fused", 1},                      // ray-local fused NeRF kernel for the tail iterations (fused.hip)
-        {"nerf_fused_after", 1},                // ... after this many whole-GPU wavefront iterations (1: the one big
-                                                //   uncontended network launch, then the ray-local tail; measured best)
+        {"nerf_fused_after", 0},                // ... after this many whole-GPU wavefront iterations (0: the speculative tail
+                                                //   from the first iteration, queued ahead of its device check; C2 1311 -> 1483
+                                                //   frames/s against 1, C3 unchanged)
         {"nerf_spec_rounds", 2},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
         {"nerf_spec_budget", 2097152},          // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax))
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
@@ -1134,13 +1136,21 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     // the decision needs the alive count after init_rays; when the tail starts after >= 1 whole-GPU
     // iteration the host reads it only once that first iteration is queued (no idle GPU while it waits)
     bool fuse_pending = false;
+    // nerf_fused_after = 0 with speculative rounds: the tail is queued at once, ahead of its own check
+    // (tail_prepare_kernel sets MarchCtrl::spec_ok; every tail kernel leaves all state untouched when it is 0),
+    // and the host reads the check while the GPU runs the rounds -- no idle GPU waiting for init_rays' count
+    bool tentative = false;
     if (c->p("nerf_fused") != 0.0 && !wavefront_only) {
-        HIPCHK(hipMemcpyAsync(c->h_alive, sched_src, 4, hipMemcpyDeviceToHost, c->s_nerf));
         fuse_after = (uint32_t)std::max(0.0, c->p("nerf_fused_after"));
-        if (fuse_after == 0) {
+        if (fuse_after == 0 && c->p("nerf_spec_rounds") > 0) {
+            fuse = true;
+            tentative = true;
+        } else if (fuse_after == 0) {
+            HIPCHK(hipMemcpyAsync(c->h_alive, sched_src, 4, hipMemcpyDeviceToHost, c->s_nerf));
             HIPCHK(hipStreamSynchronize(c->s_nerf));
             fuse = (uint64_t)c->h_alive[0] * MAX_STEPS_BETWEEN_COMPACTION <= target;
         } else {
+            HIPCHK(hipMemcpyAsync(c->h_alive, sched_src, 4, hipMemcpyDeviceToHost, c->s_nerf));
             HIPCHK(hipEventRecord(c->ev_alive, c->s_nerf));
             fuse_pending = true;
         }
@@ -1224,12 +1234,19 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             c->fused_work.ensure(16);
             c->fused_last = true;
             c->fused_k0 = iter;
+            const int p_tail = p;
+            const bool tentative_now = tentative;
+            tentative = false;
             // speculative tail rounds (nerf.hip): each marches every alive ray K iterations ahead, one
             // whole-GPU network launch evaluates them, the compositor replays them exactly; the fused
             // kernel below then finishes whatever is still alive
             const uint32_t rounds = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds"));
             c->spec_rounds = rounds;
-            launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), p, c->s_nerf);
+            launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), p, target, a.sched.global, c->s_nerf);
+            if (tentative_now) {
+                HIPCHK(hipMemcpyAsync(&c->h_alive[6], &ctrl->spec_ok, 4, hipMemcpyDeviceToHost, c->s_nerf));
+                HIPCHK(hipEventRecord(c->ev_alive, c->s_nerf));
+            }
             if (rounds) {
                 c->spec_t.ensure(c->sample_cap * 4);
                 // sample-parallel activations ahead of the compositing chain (not for the instant-NGP render modes
@@ -1295,6 +1312,16 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             launch_nerf_fused(fa, c->net, iter == 0 && !rounds ? std::min(c->h_alive[0], n_band) : n_band, (uint32_t)fb, c->s_nerf, rounds == 0);
             HIPCHK(hipGetLastError());
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused1, c->s_nerf));
+            if (tentative_now) {
+                HIPCHK(hipEventSynchronize(c->ev_alive));
+                if (c->h_alive[6] == 0u) {   // not a tail: the queued kernels did nothing; march on as a wavefront
+                    p = p_tail;
+                    fuse = false;
+                    c->fused_last = false;
+                    c->spec_rounds = 0;
+                    continue;
+                }
+            }
             HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
             on_chunk(chunk + 1);
             break;
@@ -1595,7 +1622,9 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             // gated on the last network launch of the head (ev_rt_go, trace_nerf), not the chunk's end
             if (!rt_enqueued && (chunk == rt_start_chunk || (chunk < 0 && rt_start_chunk > 0))) enqueue_raytracer(c->ev_rt_go, 2);
         });
-        launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
+        // write_normals_to_buffer (testbed_nerf.cu:1523-1612): the G-buffer only the NeRF shadow pass reads; without
+        // shadow_on_nerf no output depends on it (nerf_gbuffer = 1 keeps it for sng_frame_buffer("nerf_normals"))
+        if (shadows || c->p("nerf_gbuffer") != 0.0) launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
     }
     if (!rt_enqueued) {
         HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));

@@ -60,8 +60,9 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     // continue where the per-iteration wavefront stopped: its alive buffer, step counter i and
     // iteration count (all 0-based iteration statistics continue at k0)
     const uint32_t n_rays = a.ctrl->n_alive[a.p];
-    // nothing left (the speculative rounds finished every ray): leave before the weight fragments are loaded
-    if (n_rays == 0) return;
+    // nothing left (the speculative rounds finished every ray), or not a tail after all (tail_prepare's check):
+    // leave before the weight fragments are loaded
+    if (n_rays == 0 || !a.ctrl->spec_ok) return;
     const uint32_t i_step0 = a.ctrl->i_step[a.p];
     const uint32_t k0 = a.ctrl->n_iter;
     // after speculative rounds each ray carries its own next iteration (RayBuf::kk)

@@ -544,6 +544,7 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
     extern __shared__ uint32_t occ_lds[];
     __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
     MarchCtrl* ctrl = a.ctrl;
+    if (!ctrl->spec_ok) return;   // not a tail (tail_prepare): touch nothing
     const int p = a.p;
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t istep0 = ctrl->i_step[p];
@@ -717,7 +718,7 @@ __device__ __forceinline__ float4 spec_activate(const Volume& vol, const CamDev&
 // so the per-ray compositing chain (spec_composite) is only the front-to-back accumulation.
 __global__ __launch_bounds__(256) void spec_prepare_kernel(SpecArgs a) {
     const int p = a.p;
-    if (a.ctrl->spec_K[p] == 0) return;
+    if (!a.ctrl->spec_ok || a.ctrl->spec_K[p] == 0) return;
     const uint32_t n = a.ctrl->n_samples[p];
     for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n; s += gridDim.x * 256) {
         const float* c = a.coords + (size_t)s * 7;
@@ -734,6 +735,7 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
     __shared__ unsigned long long blk_samples, blk_reused;
     __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
     MarchCtrl* ctrl = a.ctrl;
+    if (!ctrl->spec_ok) return;
     const int p = a.p;
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t K = ctrl->spec_K[p];
@@ -969,7 +971,16 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
 }
 
 // the tail's per-iteration statistics: iterations from n_iter on take 8 steps each
-__global__ void tail_prepare_kernel(MarchCtrl* ctrl, uint32_t* work, int p) {
+__global__ void tail_prepare_kernel(MarchCtrl* ctrl, uint32_t* work, int p, uint32_t target, int global_sched) {
+    // the tail is exact only if every remaining iteration takes 8 steps: n_alive * 8 <= target now (it only shrinks)
+    const uint32_t n_sched = global_sched ? ctrl->sched_alive[p] : ctrl->n_alive[p];
+    const bool ok = (uint64_t)n_sched * MAX_STEPS_BETWEEN_COMPACTION <= target;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ctrl->spec_ok = ok ? 1u : 0u;
+        if (!ok) { ctrl->n_samples[0] = 0u; ctrl->n_samples[1] = 0u; }   // the queued network launches find nothing
+    }
+    if (!ok) return;
     if (threadIdx.x < 64 && threadIdx.x >= ctrl->n_iter) ctrl->steps_hist[threadIdx.x] = MAX_STEPS_BETWEEN_COMPACTION;
     if (threadIdx.x == 0) {
         if (work) *work = 0;
@@ -1134,7 +1145,7 @@ __global__ void ctrl_init_kernel(MarchCtrl* c) {
         c->total_samples = 0; c->net_samples = 0; c->ref_slots = 0; c->reused_samples = 0;
         c->spec_K[0] = 0; c->spec_K[1] = 0; c->spec_k0[0] = 0; c->spec_k0[1] = 0;
         c->spec_evals = 0; c->spec_exec = 0;
-        c->spec_base_k = 0; c->spec_base_istep = 1; c->spec_kk_valid[0] = 0; c->spec_kk_valid[1] = 0;
+        c->spec_base_k = 0; c->spec_base_istep = 1; c->spec_kk_valid[0] = 0; c->spec_kk_valid[1] = 0; c->spec_ok = 1;
     }
 }
 
@@ -1186,7 +1197,9 @@ void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
 void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_prepare_kernel, dim3(blocks), dim3(256), 0, s, a);
 }
-void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, int p, hipStream_t s) { hipLaunchKernelGGL(tail_prepare_kernel, dim3(1), dim3(64), 0, s, ctrl, work, p); }
+void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, int p, uint32_t target, int global_sched, hipStream_t s) {
+    hipLaunchKernelGGL(tail_prepare_kernel, dim3(1), dim3(64), 0, s, ctrl, work, p, target, global_sched);
+}
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
     if (!n) return;

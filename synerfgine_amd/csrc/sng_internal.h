@@ -57,6 +57,8 @@ struct MarchCtrl {
     uint32_t spec_base_k;            // iteration index and trace_alt step counter i at the tail's start: a ray at
     uint32_t spec_base_istep;        //   iteration k has i = base_istep + 8 (k - base_k)
     uint32_t spec_kk_valid[2];       // RayBuf::kk of buffer p holds per-ray iteration indices
+    uint32_t spec_ok;                // tail_prepare: every later iteration takes 8 steps (else the tail kernels queued
+                                     // ahead of that check leave every buffer untouched and the wavefront continues)
 };
 
 // Alive-ray SoA buffer (NerfPayload + rgba + depth, nerf_device.cuh:145-153; nerf.h:22-42)
@@ -307,7 +309,7 @@ constexpr uint32_t SPEC_KMAX = 16;
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s);
-void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, int p, hipStream_t s);
+void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, int p, uint32_t target, int global_sched, hipStream_t s);
 
 // nerf.hip
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, uint32_t n_cus,

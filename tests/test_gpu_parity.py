@@ -551,6 +551,8 @@ def test_fused_nerf_kernel_equals_wavefront(config, ngp_mode):
     ("c3", None, {"nerf_spec_rounds": 3, "nerf_spec_k_policy": 0}),       # one look-ahead for every ray of a round
     ("c3", 6, {"nerf_spec_rounds": 5, "nerf_spec_k_policy": 1}),          # per-ray look-ahead, Cost mode's death steps
     ("c4", None, {"nerf_spec_rounds": 3, "nerf_spec_k_policy": 1}),
+    ("c3", None, {"nerf_spec_rounds": 2, "nerf_fused_after": 1}),         # one whole-GPU head iteration before the rounds
+    ("c4", None, {"nerf_spec_rounds": 2, "nerf_fused_after": 2}),
 ])
 def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
     """nerf.hip's speculative tail rounds (each alive ray marched K iterations ahead, one whole-GPU network

@@ -50,7 +50,8 @@ for step in "$@"; do
       a="--config ${cfg:-c3} --steps 3 --warmup 1 --no-cpu-baseline --no-sweep $args"
       rc=0
       for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 300 rocprofv3 --pmc $c -d $d/$c -o run --output-format csv -- python3 bench.py $a > $d.$c.log 2>&1
+        kt=""; [ $c = FETCH_SIZE ] && kt="--kernel-trace"
+        timeout -s KILL 300 rocprofv3 $kt --pmc $c -d $d/$c -o run --output-format csv -- python3 bench.py $a > $d.$c.log 2>&1
         rc=$?; echo "$c rc=$rc"; [ $rc -ne 0 ] && break
       done
       if [ $rc -eq 0 ]; then

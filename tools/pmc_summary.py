@@ -55,8 +55,25 @@ def main():
         fetch = sum(2.0 * kernels[k]["fetch_kib_raw_avg"] * 1024 * kernels[k]["launches"] for k in ks) / n
         wr = sum(kernels[k]["write_kib_avg"] * 1024 * kernels[k]["launches"] for k in ks) / n
         roof[key] = {"launches": n, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": wr, "hbm_bytes_per_launch": fetch + wr}
+    # launch durations from the FETCH pass's kernel trace (kernels serialised by the counter pass) -> byte rates.
+    # FETCH_SIZE counts what the L2 (TCC) fetched from below it: the 256 MB Infinity Cache (MALL) serves part of
+    # it, so a rate above the 8 TB/s HBM peak means MALL hits, not HBM traffic.
+    dur = defaultdict(list)
+    for f in glob.glob(f"{d}/FETCH_SIZE/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            dur[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    for key, v in roof.items():
+        ks = [k for k in dur if key in k]
+        n = sum(len(dur[k]) for k in ks)
+        if n:
+            t = sum(sum(dur[k]) for k in ks) / n
+            v["avg_launch_ms"] = t * 1e3
+            v["below_l2_bytes_per_s"] = v["hbm_bytes_per_launch"] / t
+            v["label"] = ("exceeds the HBM peak: part of FETCH_SIZE was served by the Infinity Cache (MALL)" if v["hbm_bytes_per_launch"] / t > 8e12
+                          else "L2 fetch + write bytes (HBM or MALL)")
     net = [k for k in kernels if "nerf_network_kernel" in k]
-    res = {"note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes; averages over all launches of bench.py --steps 3 --warmup 1 --serial-streams",
+    res = {"note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes; averages over all launches of bench.py --steps 3 --warmup 1; "
+                   "FETCH_SIZE = bytes the L2 fetched from the Infinity Cache or HBM, so these are upper bounds on HBM traffic",
            "kernel": net[0] if net else None,
            "hbm_bytes_per_launch": kernels[net[0]]["hbm_bytes_per_launch"] if net else None,
            "calibration_half_to_float": dict(kernels.get("half_to_float_kernel", {}), expected_read_bytes=2 * 128 ** 3,
