@@ -365,7 +365,9 @@ const std::map<std::string, double>& default_params() {
                                                 //   from the first iteration, queued ahead of its device check; C2 1311 -> 1483
                                                 //   frames/s against 1, C3 unchanged)
         {"nerf_spec_rounds", 2},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
-        {"nerf_spec_budget", 2097152},          // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax))
+        {"nerf_spec_budget", 16777216},         // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax)); the
+                                                //   sample buffers are sized for it (16.8 M x 60 B ~ 1 GB of the 288 GB)
+        {"nerf_spec_hint", 1},                  // a ray looks ahead as far as its pixel's ray lived last frame (exact; 0: opacity policy)
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
         {"nerf_spec_rt_gate", 0},               // 1: the raytracer starts after the speculative rounds (C3: 216 vs 240 frames/s with 0)
         {"nerf_spec_k_policy", 1},              // per-ray look-ahead from the ray's opacity in all rounds but the last (exact)
@@ -465,6 +467,8 @@ struct sng_ctx {
     DevBuf rt_hint;                        // sample-parallel path kernel: per-pixel hit-depth sums of the previous frame (u8)
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
+    DevBuf spec_hint;                      // per NeRF pixel: 1 + the iteration its ray ended at last frame (u8, 0 unknown)
+    uint64_t spec_hint_px = 0;
     DevBuf spec_dbg;                       // nerf_spec_debug: per round and ray {trips, samples, cycles, K}
     DevBuf spec_pre, spec_pre_depth;       // spec_prepare: per network sample {rgb, alpha} and depth
     DevBuf band_rgba8;                     // sng_gather_rgba8: this rank's band as RGBA8
@@ -1033,7 +1037,9 @@ void resize(sng_ctx* c) {
 }
 
 void ensure_samples(sng_ctx* c, uint32_t target) {
-    size_t cap = std::max<size_t>(target, c->ray_cap) + 64;
+    // the speculative rounds' sample budget shares these buffers (nerf_spec_budget)
+    const size_t spec = c->p("nerf_spec_rounds") > 0 ? (size_t)std::max(1.0, c->p("nerf_spec_budget")) : 0;
+    size_t cap = std::max(std::max<size_t>(target, c->ray_cap), spec) + 64;
     if (cap > c->sample_cap) {
         c->coords.ensure(cap * 7 * 4);
         c->net_out.ensure(cap * 8);
@@ -1065,6 +1071,7 @@ uint64_t ref_slots_of(const sng_ctx* c) {
 // Returns the number of network launches.
 // own0/own1: the NeRF rows this band owns (the bands of all ranks partition the frame's rows);
 // only used when a schedule communicator is attached (Sched).
+uint8_t* spec_hint_buf(sng_ctx* c);
 uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, const CamDev& cam, f2 sc, int tr0, int tr1, int own0, int own1,
                     TraceMode mode, uint32_t target, const std::function<void(int)>& on_chunk) {
     const int NW = c->nerf_res[0], NH = c->nerf_res[1];
@@ -1265,6 +1272,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 sa.frame_rgba = c->nerf_rgba.as<float4>(); sa.frame_depth = c->nerf_depth.as<float>(); sa.positions = c->nerf_pos.as<float>();
                 sa.pre = pre ? c->spec_pre.as<float4>() : nullptr;
                 sa.pre_depth = pre ? c->spec_pre_depth.as<float>() : nullptr;
+                sa.hint = spec_hint_buf(c);
                 // rays alive after the head: at most the band's pixels (grid-stride over the device count)
                 const uint32_t sblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 4));
                 const bool dbg = c->p("nerf_spec_debug") != 0.0;
@@ -1302,6 +1310,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             fa.frame_rgba = c->nerf_rgba.as<float4>(); fa.frame_depth = c->nerf_depth.as<float>(); fa.positions = c->nerf_pos.as<float>();
             fa.work = c->fused_work.as<uint32_t>();
             fa.lanes = (uint32_t)std::min(64.0, std::max(1.0, c->p("nerf_fused_lanes")));
+            fa.hint = rounds ? spec_hint_buf(c) : nullptr;
             // concurrent frames: the tail runs beside the raytracer on the CUs its grids leave free.  A
             // mid-frame switch (a long march, e.g. C4) happens long after the raytracer has finished: the
             // tail then gets the whole-GPU grid
@@ -1374,6 +1383,19 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         if (!(fuse && iter >= fuse_after && c->p("nerf_spec_rounds") > 0 && c->p("nerf_spec_rt_gate") != 0.0)) on_chunk(chunk);
     }
     return net_launches;
+}
+
+// the per-pixel look-ahead hints of the speculative rounds (nerf_spec_hint), zeroed whenever the NeRF
+// resolution changes; nullptr when off
+uint8_t* spec_hint_buf(sng_ctx* c) {
+    if (c->p("nerf_spec_hint") == 0.0) return nullptr;
+    const uint64_t px = (uint64_t)c->nerf_res[0] * (uint64_t)c->nerf_res[1];
+    if (px != c->spec_hint_px) {
+        c->spec_hint.ensure(px);
+        HIPCHK(hipMemsetAsync(c->spec_hint.p, 0, px, c->s_nerf));
+        c->spec_hint_px = px;
+    }
+    return c->spec_hint.as<uint8_t>();
 }
 
 // march statistics of the last trace (MarchCtrl read back at the end of the frame)
@@ -1524,9 +1546,10 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60);
                 if (phase != 2) {
                     c->rt_tile_cost.ensure((size_t)n_tiles * 4);
-                    c->rt_tile_order.ensure((size_t)n_tiles * 4);
+                    c->rt_tile_order.ensure((size_t)(n_tiles + 64) * 4);   // + launch_tile_sort's 64 aux words
                     rt_sorted = key == c->rt_tile_key;
-                    if (rt_sorted) launch_tile_sort(c->rt_tile_cost.as<uint32_t>(), n_tiles, c->rt_tile_order.as<uint32_t>(), c->s_rt);
+                    if (rt_sorted) launch_tile_sort(c->rt_tile_cost.as<uint32_t>(), n_tiles, c->rt_tile_order.as<uint32_t>(),
+                                                    c->rt_tile_order.as<uint32_t>() + n_tiles, c->s_rt);
                     c->rt_tile_key = key;
                 }
                 if (rt_sorted) ra.tile_order = c->rt_tile_order.as<uint32_t>();

@@ -243,6 +243,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
             } else if (last) {
                 has = false;
             }
+            if (!has && a.hint) a.hint[idx] = (uint8_t)min(k + 1u, 255u);   // the next frame's look-ahead (SpecArgs::hint)
             if (hit) {
                 if (a.mode.ngp) {
                     float4 tmp = rgba;

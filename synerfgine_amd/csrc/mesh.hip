@@ -1339,21 +1339,40 @@ void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 fo
     hipLaunchKernelGGL(mesh_rays_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, H, row0, row1, cam, focal, sc, o, d, acc, accd);
 }
 // Order tiles by descending previous-frame cost: 32 log2 buckets, one workgroup (n_tiles <= 2^20).
-__global__ __launch_bounds__(1024) void tile_sort_kernel(const uint32_t* __restrict__ cost, uint32_t n, uint32_t* __restrict__ order) {
-    __shared__ uint32_t hist[32], base[32];
-    if (threadIdx.x < 32) hist[threadIdx.x] = 0;
+// Tile order for the next path-kernel launch: tiles binned by log2(cost), descending (any order is exact --
+// it only schedules).  Two wide passes instead of one workgroup: per-block LDS histograms summed into 32
+// global bins, then each block takes its bins' ranges with one atomic per bin and scatters.
+// aux: [0, 32) bin counts, [32, 64) bin cursors (zeroed by the launcher).
+__device__ __forceinline__ uint32_t tile_bin(uint32_t cost) { return 31u - min(31u, 31u - (uint32_t)__clz(cost | 1u)); }
+__global__ __launch_bounds__(256) void tile_hist_kernel(const uint32_t* __restrict__ cost, uint32_t n, uint32_t* __restrict__ aux) {
+    __shared__ uint32_t h[32];
+    if (threadIdx.x < 32) h[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[31 - min(31, 31 - __clz(cost[i] | 1u))], 1u);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) atomicAdd(&h[tile_bin(cost[i])], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int b = 0; b < 32; ++b) { base[b] = acc; acc += hist[b]; }
+    if (threadIdx.x < 32 && h[threadIdx.x]) atomicAdd(&aux[threadIdx.x], h[threadIdx.x]);
+}
+__global__ __launch_bounds__(256) void tile_scatter_kernel(const uint32_t* __restrict__ cost, uint32_t n, uint32_t* __restrict__ aux,
+                                                           uint32_t* __restrict__ order) {
+    __shared__ uint32_t h[32], base[32];
+    const uint32_t per = (n + gridDim.x - 1) / gridDim.x, i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+    if (threadIdx.x < 32) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += 256) atomicAdd(&h[tile_bin(cost[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        uint32_t pre = 0;
+        for (uint32_t b = 0; b < threadIdx.x; ++b) pre += aux[b];
+        base[threadIdx.x] = h[threadIdx.x] ? pre + atomicAdd(&aux[32 + threadIdx.x], h[threadIdx.x]) : 0u;
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&base[31 - min(31, 31 - __clz(cost[i] | 1u))], 1u)] = i;
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += 256) order[atomicAdd(&base[tile_bin(cost[i])], 1u)] = i;
 }
-void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, hipStream_t s) {
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(1), dim3(1024), 0, s, cost, n, order);
+void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, uint32_t* aux, hipStream_t s) {
+    (void)hipMemsetAsync(aux, 0, 64 * sizeof(uint32_t), s);
+    const uint32_t blocks = std::max(1u, std::min(256u, (n + 1023) / 1024));
+    hipLaunchKernelGGL(tile_hist_kernel, dim3(blocks), dim3(256), 0, s, cost, n, aux);
+    hipLaunchKernelGGL(tile_scatter_kernel, dim3(blocks), dim3(256), 0, s, cost, n, aux, order);
 }
 
 static size_t trace_lds_bytes(const RaytraceArgs& a, bool lds, uint32_t tpb) {

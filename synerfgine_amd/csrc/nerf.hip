@@ -583,7 +583,11 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             const uint32_t istep_i = base_istep + MAX_STEPS_BETWEEN_COMPACTION * (k_i - base_k);
             const uint32_t left = istep_i < MARCH_ITER ? (MARCH_ITER - istep_i + MAX_STEPS_BETWEEN_COMPACTION - 1) / MAX_STEPS_BETWEEN_COMPACTION : 1u;
             uint32_t K_i = K < left ? K : left;
-            if (a.k_policy) K_i = min(K_i, spec_k_of(a.in.rgba[i].w));
+            // the ray's own end in the last frame, when it is still ahead: look exactly that far; otherwise the
+            // opacity policy.  Any K is exact (the round's replay stops where the wavefront would).
+            const uint32_t h = a.hint ? (uint32_t)a.hint[__float_as_uint(di.w)] : 0u;
+            if (h != 0u && h - 1u >= k_i) K_i = min(K_i, h - k_i);
+            else if (a.k_policy) K_i = min(K_i, spec_k_of(a.in.rgba[i].w));
             const f3 idir = inv(d);
             const float dfw = dot(a.cam.c2, d);
             const float rdfw = recip_rn(dfw);   // x / dfw as div_by(x, dfw, rdfw): the IEEE quotient (Markstein), fewer ops
@@ -766,7 +770,7 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
         float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
         float depth = 0.0f, mw = 0.0f, lt = 0.0f;
         uint2 lraw = make_uint2(0u, 0u);
-        uint32_t death_step = 0, kk_next = 0;
+        uint32_t death_step = 0, kk_next = 0, k_end = 0;
         if (i < n_alive) {
             rgba = a.in.rgba[i];
             depth = a.in.depth[i];
@@ -850,8 +854,10 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                         hit = !last && rgba.w > 0.001f;
                         death_step = j + istep;
                         ended = true;
+                        k_end = k0 + it;
                     } else if (last) {
                         ended = true;
+                        k_end = k0 + it;
                     } else {
                         carry = pv[MAX_STEPS_BETWEEN_COMPACTION - 1];   // the next iteration's boundary sample
                         last_net = ob - 1;                              // its network index (8 samples, at most 1 reused)
@@ -905,8 +911,10 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                     hit = !last && rgba.w > 0.001f;
                     death_step = j + istep;
                     ended = true;
+                    k_end = k0 + it;
                 } else if (last) {
                     ended = true;
+                    k_end = k0 + it;
                 } else {
                     lt = tv[MAX_STEPS_BETWEEN_COMPACTION - 1];   // the boundary-sample cache of the next iteration
                     lraw = last_raw;
@@ -914,6 +922,7 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                 }
             }
             survive = !ended;
+            if (ended && a.hint) a.hint[__float_as_uint(di.w)] = (uint8_t)min(k_end + 1u, 255u);
         }
         const uint32_t slot = block_append<THREADS / 64>(&ctrl->n_alive[p ^ 1], survive ? 1u : 0u, nullptr, false, nullptr, false, sh_app, lane);
         if (survive) {

@@ -142,6 +142,7 @@ struct FusedArgs {
     uint32_t* work;               // ray-queue cursor (zeroed by the launcher)
     int p;                        // ping-pong buffer holding the alive rays (MarchCtrl::n_alive[p], i_step[p])
     uint32_t lanes;               // rays per wave (64; fewer shorten a wave's per-iteration field chain for thin bands)
+    uint8_t* hint;                // SpecArgs::hint, written when a ray ends here (nullptr: off)
 };
 void launch_nerf_fused(const FusedArgs& a, const NetworkDev& net, uint32_t n_rays_hint, uint32_t max_blocks, hipStream_t s, bool prepare = true);
 
@@ -304,6 +305,8 @@ struct SpecArgs {
     float* pre_depth;             //   activates the raw outputs itself) and dot(fwd, pos - cam)
     uint4* dbg;                   // nerf_spec_debug: per round and ray {march trips, samples, shader cycles, K} (nullptr: off)
     uint32_t dbg_stride;          // rays per round in dbg
+    uint8_t* hint;                // per NeRF pixel: 1 + the iteration its ray ended at in the last frame (0: unknown);
+                                  // a ray looks ahead just that far (exact whatever the hint: it only sizes the round)
 };
 constexpr uint32_t SPEC_KMAX = 16;
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s);
@@ -345,7 +348,7 @@ struct RtStage {
 };
 void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st, uint32_t* counters, const float4* o, const float4* d, uint32_t* rng,
                             uint32_t n_rng, float4* acc, float* accd, hipStream_t s);
-void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, hipStream_t s);
+void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, uint32_t* aux, hipStream_t s);
 
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
                      hipStream_t s);

@@ -553,6 +553,8 @@ def test_fused_nerf_kernel_equals_wavefront(config, ngp_mode):
     ("c4", None, {"nerf_spec_rounds": 3, "nerf_spec_k_policy": 1}),
     ("c3", None, {"nerf_spec_rounds": 2, "nerf_fused_after": 1}),         # one whole-GPU head iteration before the rounds
     ("c4", None, {"nerf_spec_rounds": 2, "nerf_fused_after": 2}),
+    ("c3", None, {"nerf_spec_rounds": 2, "nerf_spec_hint": 0}),           # opacity policy only
+    ("c3", None, {"nerf_spec_rounds": 2, "nerf_spec_budget": 1 << 21}),   # round 2 needed by most rays
 ])
 def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
     """nerf.hip's speculative tail rounds (each alive ray marched K iterations ahead, one whole-GPU network
@@ -562,19 +564,21 @@ def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
     tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, config)
     try:
         out = {}
-        for fused in (0, 1):
-            eng.set_param("nerf_fused", fused)
+        # fused = 2: the same frame again, its rounds sized by the first frame's per-pixel hints (nerf_spec_hint)
+        for fused in (0, 1, 2):
+            eng.set_param("nerf_fused", min(fused, 1))
             for k, v in spec.items():
                 eng.set_param(k, v)
-            r = eng.frame() if ngp_mode is None else eng.render_nerf(render_mode=ngp_mode)
+            r = eng.frame(spp=0, reset=True) if ngp_mode is None else eng.render_nerf(render_mode=ngp_mode)
             if fused and spec.get("nerf_spec_rounds", 0):
                 assert r.spec_rounds == spec["nerf_spec_rounds"] and r.spec_exec > 0 and r.spec_evals >= r.spec_exec
             bufs = ["nerf_rgba", "nerf_depth"] + (["nerf_positions"] if ngp_mode is None else [])
             out[fused] = ([r.download(b) for b in bufs], (r.n_samples, r.n_samples_reused, r.n_hit, r.n_iterations, r.n_reference_slots),
                           list(r.alive_per_iter), list(r.steps_per_iter), list(r.samples_per_iter))
-        for a, b in zip(out[0][0], out[1][0]):
-            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
-        assert out[0][1:] == out[1][1:]
+        for f in (1, 2):
+            for a, b in zip(out[0][0], out[f][0]):
+                assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f
+            assert out[0][1:] == out[f][1:], f
     finally:
         tb.close()
 
@@ -727,3 +731,33 @@ def test_high_phong_exponent_frame_matches_oracle(tmp_path, n_exp):
     p_db = _psnr(fin[..., :3], exp[..., :3])
     close = (np.abs(np.clip(fin, 0, 1) - np.clip(exp, 0, 1))[..., :3].max(axis=-1) <= 2 / 255).mean()
     assert p_db >= 40.0 and close >= 0.995, f"PSNR {p_db:.2f} dB, {close:.4f} of pixels within 2/255"
+
+
+def test_spec_hints_from_another_view_are_exact():
+    """The speculative rounds size each ray's look-ahead by its pixel's ray life in the last frame
+    (nerf_spec_hint).  Hints from a different camera only change the work, never the frame: after a frame
+    at one view, the next view equals the per-iteration wavefront's bit for bit."""
+    from synerfgine_amd import scene as S  # noqa: F401
+    tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, "c3")
+    try:
+        views = [((0.62, 0.46, -0.64), 1.0), ((-0.6, 0.5, 0.6), 1.3), ((0.0, -1.0, 0.0), 0.9)]
+        mats = []
+        for v, sc in views:   # set_scale moves the camera relative to its last position: fix the matrices once
+            tb.set_camera_view(v, (0.5, 0.5, 0.5), sc)
+            mats.append(np.array(tb.camera_matrix))
+        ref = {}
+        for fused in (0, 1):
+            eng.set_param("nerf_fused", fused)
+            for vi, m in enumerate(mats):
+                tb.camera_matrix = m
+                r = eng.frame(spp=0, reset=True)
+                got = [r.download(b) for b in ("nerf_rgba", "nerf_depth", "nerf_positions")] + [np.array(list(r.alive_per_iter))]
+                if fused == 0:
+                    ref[vi] = got
+                else:
+                    assert r.spec_rounds > 0
+                    for a, b in zip(ref[vi], got):
+                        assert np.array_equal(np.asarray(a).view(np.uint32) if np.asarray(a).dtype == np.float32 else a,
+                                              np.asarray(b).view(np.uint32) if np.asarray(b).dtype == np.float32 else b), vi
+    finally:
+        tb.close()
