@@ -337,9 +337,6 @@ const std::map<std::string, double>& default_params() {
         {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
-        {"rt_staged", 0},                       // ... plus primary / shade / bounce stages over compacted queues
-        {"rt_defer_shade", 0},                  // ... and the light loop of every hit in its own kernel, off the path chain (exact;
-                                                //   3 % shorter thin-band chains, 6 % slower full frames: off)
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
         {"bvh_flat", 1},                        // BvhWide walk keeping the nearer child in a register (exact)
         {"rt_tile", 8},                         // path-kernel tile edge: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
@@ -354,8 +351,6 @@ const std::map<std::string, double>& default_params() {
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
         {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)
-        {"rt_spec", 0},                         // sample-parallel path kernel (exact; mesh.hip raytrace_spec_kernel): 1 on, 0 off,
-                                                //   -1 for bands of < 25 % of the rows
         {"rt_queue_gb", 48},                    // device-memory budget for the deferred-shadow queues
         {"train_batch", 262144},                // m_training_batch_size (testbed.h:1103)
         {"train_random_bg", 1},                 // m_nerf.training.random_bg_color (testbed.h:790)
@@ -369,18 +364,14 @@ const std::map<std::string, double>& default_params() {
                                                 //   sample buffers are sized for it (16.8 M x 60 B ~ 1 GB of the 288 GB)
         {"nerf_spec_hint", 1},                  // a ray looks ahead as far as its pixel's ray lived last frame (exact; 0: opacity policy)
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
-        {"nerf_spec_rt_gate", 0},               // 1: the raytracer starts after the speculative rounds (C3: 216 vs 240 frames/s with 0)
         {"nerf_spec_k_policy", 1},              // per-ray look-ahead from the ray's opacity in all rounds but the last (exact)
-        {"nerf_spec_debug", 0},
         {"nerf_spec_prepare", 1},               // sample-parallel activations before the spec compositor (exact; 0: in the chain)
-        {"occ_lds_kb", 64},
+        {"occ_lds_kb", 64},                     // LDS budget for the occupancy bricks in the linear marchers (0: global loads)
         {"load_optimizer_state", 1},            // sng_load_snapshot restores a snapshot's optimizer state (0: inference model only)
-        {"optimizer_state_loaded", -1},         // set by sng_load_snapshot: 1 restored, 0 skipped / malformed, -1 none in the file                     // LDS budget for the occupancy bricks in the linear marchers (0: global loads)                 // 1: spec_generate records per-ray march trips / cycles (sng_frame_buffer "spec_dbg")               // 1: the raytracer starts after the speculative rounds (they get the whole GPU)
+        {"optimizer_state_loaded", -1},         // set by sng_load_snapshot: 1 restored, 0 skipped / malformed, -1 none in the file
         {"nerf_fused_lanes", 64},               // rays per wave in the fused kernel
         {"nerf_fused_blocks", -1},              // workgroup cap of the fused kernel (0: 2 per CU; -1: 2 per reserved CU when concurrent)
-        {"nerf_gen_wide", 0},                   // cascaded generate with 1024-thread workgroups while no fused tail runs
         {"nerf_gen_blocks", -1},                 // generate grid (256-thread units): 0 = min(rays, 8 per CU); -1 = all rays in one trip
-        {"nerf_ray_tile", 0},                   // > 0: NeRF rays enter the wavefront in tiles of this many pixels squared
         {"rt_shadow_all_cus", 1},               // shadow-ray kernel on every CU: the NeRF tail has mostly finished by then (C3 +2 %; 0: the path kernel grid)
         {"rt_count", 0},                        // count BVH queries / box / triangle tests of the deferred raytracer (sng_rt_counters); 2: wave iterations
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
@@ -464,17 +455,14 @@ struct sng_ctx {
     DevBuf rt_rec, rt_lc, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
-    DevBuf rt_hint;                        // sample-parallel path kernel: per-pixel hit-depth sums of the previous frame (u8)
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
     DevBuf spec_hint;                      // per NeRF pixel: 1 + the iteration its ray ended at last frame (u8, 0 unknown)
     uint64_t spec_hint_px = 0;
-    DevBuf spec_dbg;                       // nerf_spec_debug: per round and ray {trips, samples, cycles, K}
     DevBuf spec_pre, spec_pre_depth;       // spec_prepare: per network sample {rgb, alpha} and depth
     DevBuf band_rgba8;                     // sng_gather_rgba8: this rank's band as RGBA8
     uint32_t spec_rounds = 0;              // rounds enqueued by the last trace
     DevBuf rt_counts;                      // rt_count frames: path / shadow kernel {queries, box tests, triangle tests}
-    DevBuf rt_hits, rt_rays, rt_next_pos, rt_tail, rt_counters;   // staged path tracer
     bool fused_last = false;               // the last trace finished in the fused kernel
     uint32_t fused_k0 = 0;                 // ... from this iteration on
     DevBuf os_hist, os_state;              // one-step regime: death / no-sample histograms, OnestepState
@@ -1100,7 +1088,6 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     a.spp = P.spp;
     a.snap = 0;
     a.reset = P.reset_accumulation ? 1 : 0;
-    a.ray_tile = (int)std::max(0.0, c->p("nerf_ray_tile"));
     a.target_n_queries = target;
     a.mode = mode;
     const bool gsched = c->sched_comm.active();
@@ -1275,17 +1262,10 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 sa.hint = spec_hint_buf(c);
                 // rays alive after the head: at most the band's pixels (grid-stride over the device count)
                 const uint32_t sblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 4));
-                const bool dbg = c->p("nerf_spec_debug") != 0.0;
-                if (dbg) {
-                    c->spec_dbg.ensure((size_t)rounds * n_band * 16);
-                    HIPCHK(hipMemsetAsync(c->spec_dbg.p, 0, (size_t)rounds * n_band * 16, c->s_nerf));
-                }
                 for (uint32_t r = 0; r < rounds; ++r) {
                     sa.in = rb[p]; sa.out = rb[p ^ 1]; sa.p = p;
                     // per-ray look-ahead in all but the last round (which then finishes nearly every ray)
                     sa.k_policy = (c->p("nerf_spec_k_policy") != 0.0 && r + 1 < rounds) ? 1 : 0;
-                    sa.dbg = dbg ? c->spec_dbg.as<uint4>() + (size_t)r * n_band : nullptr;
-                    sa.dbg_stride = n_band;
                     launch_spec_generate(sa, sblocks, c->s_nerf);
                     if (P.collect_kernel_times) {
                         while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
@@ -1299,10 +1279,6 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                     p ^= 1;
                 }
                 HIPCHK(hipGetLastError());
-                if (c->p("nerf_spec_rt_gate") != 0.0) {   // the raytracer waits for the rounds, not for the head
-                    HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));
-                    on_chunk(-1);
-                }
             }
             FusedArgs fa{};
             fa.vol = vol; fa.cam = cam; fa.mode = mode; fa.rays = rb[p]; fa.ctrl = ctrl; fa.p = p;
@@ -1336,8 +1312,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             break;
         }
         for (int k = 0; k < CHUNK && !(fuse && iter >= fuse_after); ++k, ++iter) {
-            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), gen_blocks, mode.ngp, a.sched.global, c->s_nerf,
-                            !fuse && !fuse_pending && c->p("nerf_gen_wide") != 0.0);
+            launch_generate(vol, rb[p], ctrl, p, target, iter, c->coords.as<float>(), c->samp.as<uint2>(), gen_blocks, mode.ngp, a.sched.global, c->s_nerf);
             if (P.collect_kernel_times) {
                 while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
             }
@@ -1379,8 +1354,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         }
         HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
         ++chunk;
-        // with speculative rounds next, the raytracer is started after them (on_chunk(-1) above)
-        if (!(fuse && iter >= fuse_after && c->p("nerf_spec_rounds") > 0 && c->p("nerf_spec_rt_gate") != 0.0)) on_chunk(chunk);
+        on_chunk(chunk);
     }
     return net_launches;
 }
@@ -1535,12 +1509,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 ra.counts = c->rt_counts.as<unsigned long long>();
                 ra.count_waves = c->p("rt_count") == 2.0 ? 1 : 0;
             }
-            // sample-parallel path kernel: 2..64 samples, <= 2 bounces, its own 8x8 tile pieces, not with the
-            // staged or deferred-shading variants
-            const double rs = c->p("rt_spec");
-            const bool spec = (rs > 0 || (rs < 0 && (y1 - y0) * 4 < MH)) && ra.samples >= 2 && ra.samples <= 64 && ra.bounces <= 2 &&
-                              c->p("rt_staged") == 0.0 && c->p("rt_defer_shade") == 0.0;
-            ra.tile = (c->p("rt_tile") == 4.0 && c->p("rt_staged") == 0.0 && !spec) ? 4 : 8;   // the staged and spec kernels walk 8x8 tiles
+            ra.tile = c->p("rt_tile") == 4.0 ? 4 : 8;
             if (c->p("rt_tile_order") != 0.0) {
                 const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile - 1) / ra.tile);
                 const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60);
@@ -1567,11 +1536,6 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             q.nls = (uint32_t)c->lights.size() * ra.shadow_iters;
             q.nps = n_point * ra.shadow_iters;
             q.rec_stride = 2;
-            // deferred shading inputs after the light colours (not in staged mode, which shades per stage)
-            if (c->p("rt_defer_shade") != 0.0 && c->p("rt_staged") == 0.0) {
-                q.shade_in = q.rec_stride;
-                q.rec_stride += 4;
-            }
             const uint64_t bytes = cap * (16ull * q.rec_stride + 16ull * q.nls + 16ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
             const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
                                    bytes <= (uint64_t)(c->p("rt_queue_gb") * 1073741824.0);
@@ -1584,44 +1548,24 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 c->rt_count.ensure(16);
                 q.rec = c->rt_rec.as<float4>(); q.lc = c->rt_lc.as<float4>(); q.srec = c->rt_srec.as<float4>(); q.mask = c->rt_mask.as<float>();
                 q.head = c->rt_head.as<int>(); q.count = c->rt_count.as<uint32_t>(); q.cap = (uint32_t)cap;
-                if (c->p("rt_staged") != 0.0) {
-                    c->rt_hits.ensure(n_px * 48);
-                    c->rt_rays.ensure(n_px * 48);
-                    c->rt_next_pos.ensure((uint64_t)MW * MH * 16);
-                    c->rt_tail.ensure((uint64_t)MW * MH * 4);
-                    c->rt_counters.ensure((4 + (uint64_t)ra.samples * ra.bounces * 4) * 4);
-                    RtStage st{c->rt_hits.as<float4>(), c->rt_rays.as<float4>(), nullptr, c->rt_next_pos.as<float4>(), q.head, c->rt_tail.as<int>()};
-                    launch_raytrace_staged(ra, q, st, c->rt_counters.as<uint32_t>(), c->mesh_o.as<float4>(), c->mesh_d.as<float4>(),
-                                           c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), c->s_rt);
-                } else if (spec) {
-                    if (c->rt_hint.bytes < (uint64_t)MW * MH) {
-                        c->rt_hint.ensure((uint64_t)MW * MH);
-                        HIPCHK(hipMemsetAsync(c->rt_hint.p, 0, c->rt_hint.bytes, c->s_rt));
-                    }
-                    ra.spec_group = 1;
-                    while ((uint32_t)ra.spec_group < ra.samples) ra.spec_group <<= 1;
-                    launch_raytrace_spec(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
-                                         c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), c->rt_hint.as<uint8_t>(), c->s_rt);
-                } else {
-                    // shadow-ray grid: the CUs the path kernel leaves to the NeRF tail too when rt_shadow_all_cus
-                    // (by then the tail has mostly finished)
-                    const uint32_t sb = c->p("rt_shadow_all_cus") != 0.0 ? (uint32_t)c->n_cus * 1024u / ra.lds_tpb : 0u;
-                    const uint64_t max_hits = (uint64_t)ra.samples * ra.bounces;
-                    const uint64_t stage_b = 16ull * (64ull * q.rec_stride + (64ull * q.nps + 3) / 4);   // rt_record_colour_kernel's LDS per wave
-                    if (c->p("rt_plist") != 0.0 && max_hits <= 255 && stage_b <= 64ull * 1024) {
-                        // per-pixel record lists: the colour replay reads each pixel's records directly instead of
-                        // walking their chain (one dependent load per record)
-                        c->rt_plist.ensure(n_px * max_hits * 4);
-                        c->rt_pcount.ensure(n_px);
-                        c->rt_rval.ensure(cap * 16);
-                        q.plist = c->rt_plist.as<int>();
-                        q.pcount = c->rt_pcount.as<uint8_t>();
-                        q.rval = c->rt_rval.as<float4>();
-                        q.max_hits = (uint32_t)max_hits;
-                    }
-                    launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
-                                              c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt);
+                // shadow-ray grid: the CUs the path kernel leaves to the NeRF tail too when rt_shadow_all_cus
+                // (by then the tail has mostly finished)
+                const uint32_t sb = c->p("rt_shadow_all_cus") != 0.0 ? (uint32_t)c->n_cus * 1024u / ra.lds_tpb : 0u;
+                const uint64_t max_hits = (uint64_t)ra.samples * ra.bounces;
+                const uint64_t stage_b = 16ull * (64ull * q.rec_stride + (64ull * q.nps + 3) / 4);   // rt_record_colour_kernel's LDS per wave
+                if (c->p("rt_plist") != 0.0 && max_hits <= 255 && stage_b <= 64ull * 1024) {
+                    // per-pixel record lists: the colour replay reads each pixel's records directly instead of
+                    // walking their chain (one dependent load per record)
+                    c->rt_plist.ensure(n_px * max_hits * 4);
+                    c->rt_pcount.ensure(n_px);
+                    c->rt_rval.ensure(cap * 16);
+                    q.plist = c->rt_plist.as<int>();
+                    q.pcount = c->rt_pcount.as<uint8_t>();
+                    q.rval = c->rt_rval.as<float4>();
+                    q.max_hits = (uint32_t)max_hits;
                 }
+                launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
+                                          c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt);
             } else {
                 launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
                                 c->acc_depth.as<float>(), c->s_rt);
@@ -1643,7 +1587,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         TraceMode mode{0, 1, 1.0f};
         net_launches = trace_nerf(c, P, vol, cam, sc, tr0, tr1, own0, own1, mode, target, [&](int chunk) {
             // gated on the last network launch of the head (ev_rt_go, trace_nerf), not the chunk's end
-            if (!rt_enqueued && (chunk == rt_start_chunk || (chunk < 0 && rt_start_chunk > 0))) enqueue_raytracer(c->ev_rt_go, 2);
+            if (!rt_enqueued && chunk == rt_start_chunk) enqueue_raytracer(c->ev_rt_go, 2);
         });
         // write_normals_to_buffer (testbed_nerf.cu:1523-1612): the G-buffer only the NeRF shadow pass reads; without
         // shadow_on_nerf no output depends on it (nerf_gbuffer = 1 keeps it for sng_frame_buffer("nerf_normals"))
@@ -1989,8 +1933,8 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_trit.release(); o.d_wide.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_lc, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rt_hits, &c->rt_rays, &c->rt_next_pos, &c->rt_tail, &c->rt_counters, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
-                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_hint, &c->rt_counts, &c->spec_t, &c->spec_dbg, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_lc, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
+                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_counts, &c->spec_t, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); c->ray_kk[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1, c->ev_alive}) (void)hipEventDestroy(e);
@@ -2409,7 +2353,7 @@ int sng_frame_buffer(sng_ctx* c, const char* name, void* out, uint64_t cap, uint
     return guarded([&] {
         if (!c || !name) throw SngError(SNG_ERR_INVALID, "null context or name");
         HIPCHK(hipSetDevice(c->device));
-        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}, {"spec_dbg", &c->spec_dbg}};
+        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}};
         auto it = bufs.find(name);
         if (it == bufs.end()) throw SngError(SNG_ERR_INVALID, std::string("unknown frame buffer ") + name);
         HIPCHK(hipDeviceSynchronize());

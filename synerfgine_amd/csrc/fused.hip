@@ -532,9 +532,6 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
             else need = true;
         }
         // ---- field on the wave's unseen samples, 16 per tile (generate_kernel's coordinate expressions)
-#ifdef OS_TIMING_NO_FIELD   // timing-only builds (not exact): the one-step regime without its field evaluations
-        if (need) { out = make_uint2(0x3c003c00u, 0x3c003c00u); need = false; }
-#endif
         const unsigned long long nb = __ballot(need);
         if (nb) {
             const uint32_t total = (uint32_t)__popcll(nb);

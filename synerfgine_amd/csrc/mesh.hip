@@ -428,22 +428,14 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
             const f3 l = normalize(lpos - pos);
             const float full_d = length(lpos - pos);
             int hit = -1;
-#ifdef SHADOW_NO_BVH   // timing-only builds (tools/gpu_shadow_c4.sh)
-            const float syn_depth = full_d + (float)(hit + 1);
-#else
             const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, cx, hit);
-#endif
             overall = fminf(overall, pow_small_int(syn_depth / full_d, a.intensity));
             const f3 fract_offset = full_d * a.threshold * lpos;
             const f3 src = pos + fract_offset;
             const float fd = length(lpos - src);
             const f3 Ld = normalize(lpos - src);
-#ifdef SHADOW_NO_NERF
-            const float nd = fminf(full_d, fd + Ld.x);
-#else
             const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip,
                                                                    full_d <= fd ? full_d : __builtin_huge_valf()));
-#endif
             const double mask = (double)(nd * (1.0f - fminf(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)a.threshold));
             overall = (float)fmin((double)overall, mask);
         } else {
@@ -566,16 +558,11 @@ __device__ __forceinline__ void write_light_samples(const RaytraceArgs& a, const
         const LightGpu L = a.lights[l];
         for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
             const f3 lpos = light_sample(L, r);
-#ifdef RT_TIMING_NO_SHADE   // timing-only builds (not exact): the cost of shade_object's per-sample lighting
-            const float full_dist = 1.0f;
-            const f3 Lv = lpos, lc = lpos;
-#else
             f3 Lv = lpos - pos;
             const float full_dist = length(Lv);
             Lv = normalize(Lv);
             const f3 R = reflect(Lv, normal);
             const f3 lc = fmaxf(0.0f, dot(Lv, normal)) * m.kd * L.intensity + pow_small_int(fmaxf(0.0f, dot(R, V)), m.n) * m.ks;
-#endif
             *q.lc_at(k, jl) = make_float4(lc.x, lc.y, lc.z, 0.0f);
             if (L.type == 0) *q.shadow_ray(k, jp++) = make_float4(Lv.x, Lv.y, Lv.z, full_dist);
         }
@@ -601,19 +588,7 @@ __device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& 
     if (prev_rec < 0) q.head[i] = (int)k;
     else reinterpret_cast<int*>(q.rec + (size_t)prev_rec * q.rec_stride)[0] = (int)k;
     prev_rec = (int)k;
-    if (q.shade_in) {
-        // shading off the chain: keep what rt_shade_records_kernel needs and skip the light
-        // samples' draws (3 per light and shadow iteration) -- same RNG position afterwards
-        float4* si = q.rec + (size_t)k * q.rec_stride + q.shade_in;
-        si[0] = make_float4(h.normal.x, h.normal.y, h.normal.z, 0.0f);
-        si[1] = make_float4(rd.x, rd.y, rd.z, 0.0f);
-        si[2] = make_float4(__uint_as_float(r.v0), __uint_as_float(r.v1), __uint_as_float(r.v2), __uint_as_float(r.v3));
-        si[3] = make_float4(__uint_as_float(r.v4), __uint_as_float(r.d), 0.0f, 0.0f);
-        const uint32_t n_draws = 3u * (uint32_t)a.n_lights * a.shadow_iters;
-        for (uint32_t j = 0; j < n_draws; ++j) (void)xorwow_next(r);
-    } else {
-        write_light_samples(a, q, k, h.pos, h.normal, rd, m, r);
-    }
+    write_light_samples(a, q, k, h.pos, h.normal, rd, m, r);
     const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
     const float lo = curand_uniform(r) * spec;
     const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
@@ -744,370 +719,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
     if constexpr (CNT) flush_counts(a.counts, counts, lane);
 }
 
-// ===========================================================================================
-// Sample-parallel path tracer (rt_spec): raytrace_pixel<DEFER = true>'s records, shadow rays,
-// depth and final XORWOW state, bit for bit, with a pixel's samples on separate lanes instead of
-// one lane's serial chain.
-//
-// Sample s of a pixel starts at XORWOW offset off_s = sum_{j<s} d_j, where d_j = Dl + h_j * H is
-// sample j's draw count (Dl = 1 or 2 lens draws; H = 3 * n_lights * shadow_iters light draws + 2
-// scatter draws per bounce that hits; h_j = bounces hit before the first miss).  Every lane traces
-// its sample from a guessed offset (the pixel's mean hit depth of the previous frame), then the
-// offsets are re-formed by an exclusive scan of the d's and lanes whose offset changed trace again.
-// The fixed point is the serial sequence: after round r the first r offsets are final, so it ends
-// within `samples` + 1 rounds, and in practice in 2-3 (primary hits are nearly deterministic per
-// pixel; only the bounce hits vary).  A pixel's chain becomes (rounds x one sample) instead of
-// (samples x one sample).  Each lane keeps, per hit bounce, what shade_object needs (position,
-// normal, incoming direction, material, pdf, att and the XORWOW state before the light draws); the
-// converged lanes then write their hit records in (sample, bounce) order into one contiguous block
-// per pixel and draw the light samples from the saved states -- off any chain.
-// ===========================================================================================
-constexpr int SPEC_MAXB = 2;   // bounces kept per lane (path_trace_depth <= 2)
-#ifndef SPEC_WAVES_PER_EU
-#define SPEC_WAVES_PER_EU 2         // ~230 VGPRs without spills: one 512-thread workgroup per CU
-#endif
-
-struct SpecBounce {
-    Xorwow r;      // state before this bounce's light draws
-    f3 pos, normal, rd;
-    int mat;
-    float pdf, att;
-};
-
-
-// One sample of raytrace_pixel's loop from XORWOW offset `off`: returns hit depth, fills the hit
-// bounces, the first-bounce position and the state after the sample's last draw.
-template <bool LDS, bool CNT = false>
-__device__ __forceinline__ uint32_t spec_sample(const RaytraceArgs& a, const TraceCtx<LDS, CNT>& cx, const Xorwow& base, uint32_t off, f3 src_p, f3 src_d,
-                                                uint32_t n_light_draws, SpecBounce (&bh)[SPEC_MAXB], f3& p0, Xorwow& r_end) {
-    Xorwow r = base;
-    xorwow_skip(r, off);
-    const float longi = curand_uniform(r) * a.lens;
-    const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
-    f3 rp = src_p, rd = cone_random_up(src_d, a.up, longi, latid);
-    float pdf = 1.0f / (float)a.bounces, att = 1.0f;
-    uint32_t nh = 0;
-#pragma unroll
-    for (int b = 0; b < SPEC_MAXB; ++b) {
-        if ((uint32_t)b >= a.bounces) break;
-        Hit h;
-        const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h);
-        if (b == 0) p0 = h.pos;
-        if (hit_obj < 0) break;
-        bh[b].r = r;
-        bh[b].pos = h.pos; bh[b].normal = h.normal; bh[b].rd = rd;
-        bh[b].mat = h.mat; bh[b].pdf = pdf; bh[b].att = att;
-        xorwow_skip(r, n_light_draws);
-        // Material::scatter (material.cuh:112-123)
-        const MaterialGpu m = a.mats[h.mat];
-        const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
-        const float lo = curand_uniform(r) * spec;
-        const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
-        const f3 ndir = cone_random_frame(h.normal, h.perturb, lo, la);
-        rp = h.pos;
-        rd = ndir;
-        pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
-        att = 1.0f * m.rg;
-        ++nh;
-    }
-    r_end = r;
-    return nh;
-}
-
-// segmented (width SG) inclusive sum over the wave
-__device__ __forceinline__ uint32_t seg_incl_scan(uint32_t v, int s, int SG) {
-    for (int o = 1; o < SG; o <<= 1) {
-        const uint32_t u = __shfl_up(v, (unsigned)o, SG);
-        if (s >= o) v += u;
-    }
-    return v;
-}
-
-// lanes: SG = a.spec_group lanes per pixel (power of two >= samples), 64 / SG pixels per wave; a
-// wave takes one 64/SG-pixel row piece of an 8x8 tile (tiles in the previous frame's cost order).
-template <bool LDS>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SPEC_WAVES_PER_EU))) void raytrace_spec_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work,
-                                                             const float4* __restrict__ origins, const float4* __restrict__ dirs,
-                                                             uint32_t* __restrict__ rng, uint32_t n_rng, float* __restrict__ acc_depth,
-                                                             uint8_t* __restrict__ hint) {
-    const TraceCtx<LDS> cx = trace_ctx_setup<LDS, false>(a);
-    const int lane = threadIdx.x & 63;
-    const int SG = a.spec_group, PPW = 64 / SG;
-    const int s = lane & (SG - 1), pw = lane / SG;
-    const uint32_t rows = (uint32_t)(a.row1 - a.row0);
-    const uint32_t tiles_x = ((uint32_t)a.W + 7u) / 8u, n_tiles = tiles_x * ((rows + 7u) / 8u);
-    const uint32_t units_per_tile = 64u / (uint32_t)PPW, n_units = n_tiles * units_per_tile;
-    const uint32_t n_light_draws = 3u * (uint32_t)a.n_lights * a.shadow_iters;
-    const uint32_t Dl = a.lens != 0.0f ? 1u : 2u, H = n_light_draws + 2u;
-    while (true) {
-        uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(work, 1u);
-        k = __shfl(k, 0, 64);
-        if (k >= n_units) break;
-        const uint32_t tile = a.tile_order ? a.tile_order[k / units_per_tile] : k / units_per_tile;
-        const uint64_t t0 = wall_clock64();
-        const uint32_t j = (k % units_per_tile) * (uint32_t)PPW + (uint32_t)pw;   // pixel within the tile
-        const uint32_t x = (tile % tiles_x) * 8u + j % 8u, y = (tile / tiles_x) * 8u + j / 8u;
-        const bool px_ok = x < (uint32_t)a.W && y < rows;
-        const bool active = px_ok && (uint32_t)s < a.samples;
-        const size_t i = (size_t)a.row0 * a.W + (px_ok ? y * (uint32_t)a.W + x : 0u);
-
-        Xorwow base{0, 0, 0, 0, 0, 0};
-        f3 src_p = splat(0.0f), src_d = splat(0.0f);
-        uint32_t off = 0, d = 0, nh = 0;
-        if (px_ok) {
-            base = load_rng(rng, n_rng, i);
-            const float4 o4 = origins[i], d4 = dirs[i];
-            src_p = mk(o4.x, o4.y, o4.z);
-            src_d = mk(d4.x, d4.y, d4.z);
-            // guess: every sample hits as deep as this pixel's samples did on average last frame
-            const uint32_t g = ((uint32_t)hint[i] * 2u + a.samples) / (2u * a.samples);
-            off = (uint32_t)s * (Dl + min(g, a.bounces) * H);
-        }
-        SpecBounce bh[SPEC_MAXB];
-        f3 p0 = splat(0.0f);
-        Xorwow r_end = base;
-        bool need = active;
-        while (__ballot(need)) {
-            if (need) {
-                nh = spec_sample<LDS>(a, cx, base, off, src_p, src_d, n_light_draws, bh, p0, r_end);
-                d = Dl + nh * H;
-            }
-            const uint32_t incl = seg_incl_scan(active ? d : 0u, s, SG);
-            const uint32_t noff = incl - (active ? d : 0u);
-            need = active && noff != off;
-            off = noff;
-        }
-
-        // ---- hit records: lanes are pixel-major, sample-minor, so one wave-wide scan of the lanes'
-        // record counts lays out each pixel's records contiguously in (sample, bounce) order
-        const uint32_t my = active ? nh : 0u;
-        const uint32_t wincl = seg_incl_scan(my, lane, 64);
-        const uint32_t wexcl = wincl - my;
-        const uint32_t all = __shfl(wincl, 63, 64);
-        const uint32_t px_first = __shfl(wexcl, pw * SG, 64);
-        const uint32_t px_total = __shfl(wincl, pw * SG + SG - 1, 64) - px_first;
-        uint32_t wbase = 0;
-        if (lane == 0 && all) wbase = atomicAdd(q.count, all);
-        wbase = __shfl(wbase, 0, 64);
-        if (px_ok && s == 0) q.head[i] = px_total ? (int)(wbase + px_first) : -1;
-        if (active) {
-#pragma unroll
-            for (int b = 0; b < SPEC_MAXB; ++b) {
-                if ((uint32_t)b >= nh) break;
-                const uint32_t kr = wbase + wexcl + (uint32_t)b;
-                const bool last = wexcl + (uint32_t)b + 1u == px_first + px_total;
-                const SpecBounce& hb = bh[b];
-                write_record_header(q.rec + (size_t)kr * q.rec_stride, last ? -1 : (int)kr + 1, (uint32_t)s, hb.mat, hb.pos, hb.pdf, hb.att);
-                Xorwow r = hb.r;
-                write_light_samples(a, q, kr, hb.pos, hb.normal, hb.rd, a.mats[hb.mat], r);
-            }
-        }
-        // ---- depth from the first-bounce positions summed in sample order; final XORWOW state
-        f3 next_pos = splat(0.0f);
-        for (uint32_t jj = 0; jj < a.samples; ++jj) {
-            const int src = pw * SG + (int)jj;
-            const f3 v = mk(__shfl(p0.x, src, 64), __shfl(p0.y, src, 64), __shfl(p0.z, src, 64));
-            next_pos = next_pos + v;
-        }
-        if (px_ok && s == 0) {
-            next_pos = next_pos / (float)a.samples;
-            acc_depth[i] = dot(src_d, next_pos - src_p);
-            hint[i] = (uint8_t)min(px_total, 255u);
-        }
-        if (active && (uint32_t)s == a.samples - 1u) store_rng(rng, n_rng, i, r_end);
-        if (a.tile_cost && lane == 0) atomicMax(&a.tile_cost[tile], (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull));
-    }
-}
-
-// ===========================================================================================
-// Staged path tracer (rt_mode 2): the same per-pixel path and RNG sequence as raytrace_pixel,
-// split into dense stages per sample -- primary traversal over all pixels, then for every
-// bounce: shade (light samples -> hit records + shadow queue, scatter) over the compacted hits
-// and traversal over the compacted bounce rays.  A pixel's stages run in its original order
-// (spp-major, bounce-minor), so its XORWOW draws, hit records and next_pos sums are identical;
-// every traversal/shading lane does useful work instead of idling beside other lanes' paths.
-// ===========================================================================================
-// hit entry: [pos, pixel] [rd, spp] [pdf, att, obj, tri] ; ray entry: [origin, pixel] [dir, spp] [pdf, att, -, -]
-
-// depth_test_world(+HitRecord) (common.cu:50-67) without the normal/perturb (the shade stage
-// derives them from (obj, tri) with the same expressions)
-template <bool LDS, bool CNT = false>
-__device__ __forceinline__ int nearest_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, float& t_out,
-                                           int& tri_out) {
-    const f3 off = origin + dir * MIN_DEPTH;
-    int out_obj = -1, out_tri = -1;
-    float best = MAX_DEPTH;
-    for (int c = 0; c < n_objs; ++c) {
-        int tri;
-        const float t = object_intersect(off, dir, objs[c], cx, tri);
-        if (t < best && t > MIN_DEPTH) { out_obj = c; best = t; out_tri = tri; }
-    }
-    t_out = best;
-    tri_out = out_tri;
-    return out_obj;
-}
-
-__device__ __forceinline__ uint32_t wave_claim(uint32_t* counter, uint32_t n, int lane) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(counter, n);
-    return __shfl(base, 0, 64);
-}
-
-template <bool LDS>
-__global__ __launch_bounds__(512) void rt_primary_kernel(RaytraceArgs a, RtStage st, uint32_t spp, uint32_t* __restrict__ work,
-                                                          const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
-                                                          uint32_t n_rng) {
-    const TraceCtx<LDS> cx = trace_ctx_setup<LDS, false>(a);
-    const int lane = threadIdx.x & 63;
-    const uint32_t rows = (uint32_t)(a.row1 - a.row0);
-    const uint32_t tiles_x = ((uint32_t)a.W + 7) / 8, n_tiles = tiles_x * ((rows + 7) / 8);
-    // static round-robin over the (cost-ordered) tiles: the expensive tiles spread over all waves
-    // without a contended work counter (one launch per sample makes per-tile atomics add up)
-    const uint32_t wave_id = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t kk = wave_id; kk < n_tiles; kk += n_waves) {
-        const uint32_t tile = a.tile_order ? a.tile_order[kk] : kk;
-        const uint64_t t0 = wall_clock64();
-        const uint32_t x = (tile % tiles_x) * 8 + (lane & 7), y = (tile / tiles_x) * 8 + (lane >> 3);
-        bool hit = false;
-        f3 hpos = splat(0.0f), rd = splat(0.0f);
-        int obj = -1, tri = -1;
-        uint32_t pix = 0;
-        if (x < (uint32_t)a.W && y < rows) {
-            pix = (uint32_t)a.row0 * (uint32_t)a.W + y * (uint32_t)a.W + x;
-            if (spp == 0) { st.head[pix] = -1; st.tail[pix] = -1; }
-            Xorwow r = load_rng(rng, n_rng, pix);
-            const float4 o4 = origins[pix], d4 = dirs[pix];
-            const f3 src_p = mk(o4.x, o4.y, o4.z), src_d = mk(d4.x, d4.y, d4.z);
-            const float longi = curand_uniform(r) * a.lens;
-            const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
-            rd = cone_random_up(src_d, a.up, longi, latid);
-            float t;
-            obj = nearest_hit(src_p, rd, a.objs, a.n_objs, cx, t, tri);
-            hpos = src_p + t * rd;
-            const float4 np = spp ? st.next_pos[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const f3 n3 = mk(np.x, np.y, np.z) + hpos;
-            st.next_pos[pix] = make_float4(n3.x, n3.y, n3.z, 0.0f);
-            store_rng(rng, n_rng, pix, r);
-            hit = obj >= 0;
-        }
-        const uint32_t slot = wave_append(st.hit_count, hit, lane);
-        if (hit) {
-            float4* e = st.hits + 3 * (size_t)slot;
-            e[0] = make_float4(hpos.x, hpos.y, hpos.z, __uint_as_float(pix));
-            e[1] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(spp));
-            e[2] = make_float4(1.0f / (float)a.bounces, 1.0f, __int_as_float(obj), __int_as_float(tri));
-        }
-        if (a.tile_cost && lane == 0) a.tile_cost[tile] = (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull);
-    }
-}
-
-// shade_object (raytracer.cu:6-57) for the compacted hits of one bounce; writes the hit record
-// (light colours), the point-light shadow rays, and the scattered ray of the next bounce.
-__global__ __launch_bounds__(256) void rt_shade_kernel(RaytraceArgs a, RtQueue q, RtStage st, uint32_t bounce, const uint32_t* __restrict__ n_hits_dev,
-                                                       float4* __restrict__ rays_out, uint32_t* __restrict__ ray_count, uint32_t* __restrict__ rng, uint32_t n_rng) {
-    const uint32_t n_hits = *n_hits_dev;
-    const int lane = threadIdx.x & 63;
-    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < n_hits; base += gridDim.x * blockDim.x) {
-        const uint32_t e_i = base + (uint32_t)lane;
-        const bool valid = e_i < n_hits;
-        const uint32_t k = wave_append(q.count, valid, lane);   // hit record of this entry
-        bool next = false;
-        f3 hpos = splat(0.0f), ndir = splat(0.0f);
-        uint32_t pix = 0, spp = 0;
-        float pdf_n = 0.0f, att_n = 0.0f;
-        if (valid) {
-            const float4* e = st.hits + 3 * (size_t)e_i;
-            const float4 e0 = e[0], e1 = e[1], e2 = e[2];
-            hpos = mk(e0.x, e0.y, e0.z);
-            pix = __float_as_uint(e0.w);
-            const f3 rd = mk(e1.x, e1.y, e1.z);
-            spp = __float_as_uint(e1.w);
-            const float pdf = e2.x, att = e2.y;
-            const ObjectGpu& o = a.objs[__float_as_int(e2.z)];
-            const Tri tr = o.tris[__float_as_int(e2.w)];
-            const f3 N = tri_normal(tr);
-            const f3 normal = mul(o.rot, N);
-            const f3 T = normalize((tr.a + tr.b + tr.c) / 3.0f - tr.a);   // Triangle::get_perturb_matrix (triangle.cuh:164-170)
-            const m3 perturb = {T, cross(T, N), N};
-            const MaterialGpu m = a.mats[o.mat_id];
-            Xorwow r = load_rng(rng, n_rng, pix);
-            // hit record, appended to the pixel's list (stages run in the pixel's path order)
-            write_record_header(q.rec + (size_t)k * q.rec_stride, -1, spp, o.mat_id, hpos, pdf, att);
-            const int prev = st.tail[pix];
-            if (prev < 0) q.head[pix] = (int)k;
-            else reinterpret_cast<int*>(q.rec + (size_t)prev * q.rec_stride)[0] = (int)k;
-            st.tail[pix] = (int)k;
-            write_light_samples(a, q, k, hpos, normal, rd, m, r);
-            // Material::scatter (material.cuh:112-123)
-            const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
-            const float lo = curand_uniform(r) * spec;
-            const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
-            ndir = cone_random_frame(normal, perturb, lo, la);
-            pdf_n = 1.0f / fmaxf(1.0f, spec * 2.0f);
-            att_n = 1.0f * m.rg;
-            store_rng(rng, n_rng, pix, r);
-            next = bounce + 1 < a.bounces;
-        }
-        const uint32_t slot = wave_append(ray_count, next, lane);
-        if (next) {
-            float4* e = rays_out + 3 * (size_t)slot;
-            e[0] = make_float4(hpos.x, hpos.y, hpos.z, __uint_as_float(pix));
-            e[1] = make_float4(ndir.x, ndir.y, ndir.z, __uint_as_float(spp));
-            e[2] = make_float4(pdf_n, att_n, 0.0f, 0.0f);
-        }
-    }
-}
-
-// traversal of the compacted bounce rays; hits go to the next shade stage
-template <bool LDS>
-__global__ __launch_bounds__(512) void rt_bounce_kernel(RaytraceArgs a, RtStage st, const float4* __restrict__ rays_in, const uint32_t* __restrict__ n_rays_dev,
-                                                         uint32_t* __restrict__ work) {
-    const TraceCtx<LDS> cx = trace_ctx_setup<LDS, false>(a);
-    const int lane = threadIdx.x & 63;
-    const uint32_t n_rays = *n_rays_dev;
-    while (true) {
-        const uint32_t base = wave_claim(work, 64u, lane);
-        if (base >= n_rays) break;
-        const uint32_t j = base + (uint32_t)lane;
-        bool hit = false;
-        float4 e0, e1, e2;
-        f3 hpos = splat(0.0f);
-        int obj = -1, tri = -1;
-        if (j < n_rays) {
-            const float4* e = rays_in + 3 * (size_t)j;
-            e0 = e[0]; e1 = e[1]; e2 = e[2];
-            const f3 rp = mk(e0.x, e0.y, e0.z), rd = mk(e1.x, e1.y, e1.z);
-            float t;
-            obj = nearest_hit(rp, rd, a.objs, a.n_objs, cx, t, tri);
-            hpos = rp + t * rd;
-            hit = obj >= 0;
-        }
-        const uint32_t slot = wave_append(st.hit_count, hit, lane);
-        if (hit) {
-            float4* e = st.hits + 3 * (size_t)slot;
-            e[0] = make_float4(hpos.x, hpos.y, hpos.z, e0.w);
-            e[1] = e1;
-            e[2] = make_float4(e2.x, e2.y, __int_as_float(obj), __int_as_float(tri));
-        }
-    }
-}
-
-// shade_object's light loop (raytracer.cu:24-50) for every hit record of the frame, off the path
-// chain: the light samples are redrawn from the XORWOW state the path kernel saved, so lc and the
-// shadow rays are bit-identical to computing them inline.
-__global__ __launch_bounds__(256) void rt_shade_records_kernel(RaytraceArgs a, RtQueue q) {
-    const uint32_t n = *q.count;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const float4* rk = q.rec + (size_t)k * q.rec_stride;
-        const float4* si = rk + q.shade_in;
-        const float4 h0 = rk[0], h1 = rk[1], s0 = si[0], s1 = si[1], s2 = si[2], s3 = si[3];
-        const f3 pos = mk(h1.z, h1.w, h0.w), normal = mk(s0.x, s0.y, s0.z), rd = mk(s1.x, s1.y, s1.z);
-        Xorwow r{__float_as_uint(s2.x), __float_as_uint(s2.y), __float_as_uint(s2.z), __float_as_uint(s2.w), __float_as_uint(s3.x), __float_as_uint(s3.y)};
-        write_light_samples(a, q, k, pos, normal, rd, a.mats[__float_as_int(h0.z)], r);
-    }
-}
-
 // Shadow rays of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
@@ -1144,16 +755,8 @@ __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQue
         const f3 pos = mk(h1.z, h1.w, h0.w), Lv = mk(s1.x, s1.y, s1.z);
         const float full_dist = s1.w;
         int oh = -1;
-#ifdef SHADOW_TIMING_NO_BVH   // timing-only builds (not exact): which half of a shadow ray costs what
-        const float syn = MAX_DEPTH;
-#else
         const float syn = depth_test_world(pos, Lv, a.objs, a.n_objs, cx, oh, full_dist);
-#endif
-#ifdef SHADOW_TIMING_NO_NERF
-        const float nerf = MAX_DEPTH;
-#else
         const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip, fminf(syn, full_dist));
-#endif
         const float sh = fminf(fminf(nerf, syn), full_dist);
         q.mask[q.mask_at(kr, jp)] = pow_small_int(smoothstep(sh / full_dist), a.syn_shadow_factor);
     }
@@ -1411,20 +1014,17 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
         allow_lds(raytrace_kernel<true, true, true>, lp);
         allow_lds(shadow_rays_kernel<true, true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
-        if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
-        hipLaunchKernelGGL((shadow_rays_kernel<true, true>), dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+            hipLaunchKernelGGL((shadow_rays_kernel<true, true>), dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     } else if (lds) {
         allow_lds(raytrace_kernel<true, true>, lp);
         allow_lds(shadow_rays_kernel<true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
-        if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
-        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+            hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     } else {
         allow_lds(raytrace_kernel<true, false>, lp);
         allow_lds(shadow_rays_kernel<false>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
-        if (q.shade_in) hipLaunchKernelGGL(rt_shade_records_kernel, dim3(a.persistent_blocks * 4), dim3(256), 0, s, a, q);
-        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+            hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     }
     if (q.plist) {   // capi.cpp enables the lists only when one wave's staging fits 64 KB
         const size_t per_wave = 16u * (64u * q.rec_stride + (64u * q.nps + 3u) / 4u);
@@ -1435,76 +1035,6 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
 }
 
-// sample-parallel mode: raytrace_spec_kernel replaces the path kernel; shadow and accumulate kernels
-// as in launch_raytrace_wavefront.  `hint`: per-pixel hit depth sums of the previous frame (u8).
-void launch_raytrace_spec(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
-                          float* accd, uint8_t* hint, hipStream_t s) {
-    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
-    if (!n) return;
-    (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);
-    (void)hipMemsetAsync(a.work, 0, RT_WORK_WORDS * sizeof(uint32_t), s);
-    const uint32_t tiles_x = ((uint32_t)a.W + 7u) / 8u, n_tiles = tiles_x * (((uint32_t)(a.row1 - a.row0) + 7u) / 8u);
-    if (a.tile_cost) (void)hipMemsetAsync(a.tile_cost, 0, (size_t)n_tiles * 4, s);   // atomicMax over a tile's row pieces
-    const uint32_t n_units = n_tiles * (uint32_t)a.spec_group;   // 64 / (64 / SG) pieces per tile
-    const bool lds = a.scene_in_lds != 0;
-    const uint32_t tp = 512, ts = lds ? a.lds_tpb : 512u;
-    const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
-    // one 512-thread workgroup per CU (2 waves/SIMD at ~230 VGPRs): a larger grid would spill onto the
-    // CUs left to the NeRF stream
-    const uint32_t bp = std::min((n_units + tp / 64 - 1) / (tp / 64), a.persistent_blocks * (SPEC_WAVES_PER_EU / 2u));
-    if (lds) {
-        allow_lds(raytrace_spec_kernel<true>, lp);
-        allow_lds(shadow_rays_kernel<true>, ls);
-        hipLaunchKernelGGL(raytrace_spec_kernel<true>, dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd, hint);
-        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 1024u / ts), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
-    } else {
-        allow_lds(raytrace_spec_kernel<false>, lp);
-        allow_lds(shadow_rays_kernel<false>, ls);
-        hipLaunchKernelGGL(raytrace_spec_kernel<false>, dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd, hint);
-        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
-    }
-    hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
-}
-
-// staged mode: per sample, primary traversal over all pixels then shade / bounce-traversal stages
-// over compacted queues; counters: [0] hit records, then per (spp, bounce) {hits, rays, work}.
-void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st, uint32_t* counters, const float4* o, const float4* d, uint32_t* rng,
-                            uint32_t n_rng, float4* acc, float* accd, hipStream_t s) {
-    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
-    if (!n) return;
-    const uint32_t n_counters = 4 + a.samples * a.bounces * 4;
-    (void)hipMemsetAsync(counters, 0, n_counters * sizeof(uint32_t), s);
-    RtQueue qq = q;
-    qq.count = counters;
-    const bool lds = a.scene_in_lds != 0;
-    const uint32_t tp = 512, ts = lds ? a.lds_tpb : 512u;
-    const size_t lp = trace_lds_bytes(a, lds, tp);
-    const uint32_t bp = std::min((n + tp - 1) / tp, a.persistent_blocks * 2);
-    if (lds) { allow_lds(rt_primary_kernel<true>, lp); allow_lds(rt_bounce_kernel<true>, lp); allow_lds(shadow_rays_kernel<true>, trace_lds_bytes(a, lds, ts)); }
-    else { allow_lds(rt_primary_kernel<false>, lp); allow_lds(rt_bounce_kernel<false>, lp); allow_lds(shadow_rays_kernel<false>, trace_lds_bytes(a, lds, ts)); }
-    const uint32_t shade_blocks = std::max(1u, std::min((n + 255) / 256, a.persistent_blocks * 8));
-    for (uint32_t sp = 0; sp < a.samples; ++sp) {
-        uint32_t* c = counters + 4 + sp * a.bounces * 4;
-        st.hit_count = c;
-        if (lds) hipLaunchKernelGGL(rt_primary_kernel<true>, dim3(bp), dim3(tp), lp, s, a, st, sp, c + 3, o, d, rng, n_rng);
-        else hipLaunchKernelGGL(rt_primary_kernel<false>, dim3(bp), dim3(tp), lp, s, a, st, sp, c + 3, o, d, rng, n_rng);
-        for (uint32_t b = 0; b < a.bounces; ++b) {
-            uint32_t* cb = c + b * 4;   // {hits of bounce b, rays of bounce b+1, -, work}
-            hipLaunchKernelGGL(rt_shade_kernel, dim3(shade_blocks), dim3(256), 0, s, a, qq, st, b, cb, st.rays, cb + 1, rng, n_rng);
-            if (b + 1 < a.bounces) {
-                uint32_t* cn = c + (b + 1) * 4;
-                RtStage sb = st;
-                sb.hit_count = cn;
-                if (lds) hipLaunchKernelGGL(rt_bounce_kernel<true>, dim3(bp), dim3(tp), lp, s, a, sb, st.rays, cb + 1, cn + 3);
-                else hipLaunchKernelGGL(rt_bounce_kernel<false>, dim3(bp), dim3(tp), lp, s, a, sb, st.rays, cb + 1, cn + 3);
-            }
-        }
-    }
-    (void)hipMemsetAsync(a.work + SHADOW_CTR0, 0, (RT_WORK_WORDS - SHADOW_CTR0) * sizeof(uint32_t), s);
-    if (lds) hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(a.persistent_blocks * 1024u / ts), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + SHADOW_CTR0);
-    else hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(a.persistent_blocks * 2), dim3(ts), trace_lds_bytes(a, lds, ts), s, a, qq, a.work + SHADOW_CTR0);
-    hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, qq, acc, st.next_pos, o, d, accd);
-}
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
                     const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;

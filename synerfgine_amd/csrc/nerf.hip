@@ -86,16 +86,9 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
         uint32_t idx = 0;
         int x, y;
         bool in_band;
-        if (a.ray_tile > 0) {   // thread -> pixel in T x T tiles, tiles row-major over the band
-            const uint32_t T = (uint32_t)a.ray_tile, tiles_x = ((uint32_t)a.W + T - 1) / T, tile = t / (T * T), w = t % (T * T);
-            x = (int)((tile % tiles_x) * T + w % T);
-            y = a.row0 + (int)((tile / tiles_x) * T + w / T);
-            in_band = t < n_threads && x < a.W && y < a.row1;
-        } else {
-            x = (int)(t % (uint32_t)a.W);
-            y = a.row0 + (int)(t / (uint32_t)a.W);
-            in_band = t < n_band;
-        }
+        x = (int)(t % (uint32_t)a.W);
+        y = a.row0 + (int)(t / (uint32_t)a.W);
+        in_band = t < n_band;
         if (in_band) {
             idx = (uint32_t)x + (uint32_t)a.W * (uint32_t)y;
             f2 off = ld_random_pixel_offset(a.snap ? 0u : a.spp);
@@ -594,8 +587,6 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             float t = ot.w;
             float prev = a.mode.ngp ? qnan : a.in.lt[i].x;   // the previous iteration's last sample
             OccCache oc;
-            uint32_t trips = 0;
-            const uint64_t c0 = a.dbg ? (uint64_t)clock64() : 0ull;
             float* tb = a.tbuf + i;
             const size_t tstride = n_alive;
             // ONE flattened loop over all K iterations: each trip is one DDA step or one sample, and an
@@ -610,7 +601,6 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             if constexpr (LIN && BRICK) t_last = path_last_occupied_t(o, d, idir, fminf(t, prev == prev ? prev : t), occ_lds);
 #pragma unroll 1
             while (going) {
-                ++trips;
                 bool sample = false, stop = false;   // stop: this iteration's march ends with cnt < 8
                 if constexpr (LIN && BRICK) {
                     // branch-free trip: both successors formed, the occupancy bit selects (lanes of a wave
@@ -668,13 +658,6 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             }
             // trace keeps generate's t (836): the survivors' next start
             if (a.mode.ngp && n_it == K_i && cnt_last == MAX_STEPS_BETWEEN_COMPACTION) reinterpret_cast<float*>(a.in.o_t + i)[3] = t;
-#ifdef SNG_OCC_COUNT
-            const uint32_t loads = oc.loads;
-#else
-            const uint32_t loads = 0u;
-#endif
-            const uint32_t pix = __float_as_uint(di.w);   // by pixel: rays can be followed across rounds
-            if (a.dbg && pix < a.dbg_stride) a.dbg[pix] = make_uint4(trips, tot | (loads << 16), (uint32_t)((uint64_t)clock64() - c0), __float_as_uint(a.in.rgba[i].w));
         }
         const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], nnet, nullptr, false, nullptr, false, sh_app, lane);
         if (i < n_alive) {
@@ -1166,10 +1149,6 @@ void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl
                       uint32_t n_cus, hipStream_t s) {
     uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
-    if (a.ray_tile > 0) {
-        const uint32_t T = (uint32_t)a.ray_tile;
-        n = (((uint32_t)a.W + T - 1) / T) * (((uint32_t)(a.row1 - a.row0) + T - 1) / T) * T * T;
-    }
     const uint32_t blocks = (n + 255) / 256;
     if (a.vol.linear && a.vol.occ_brick_words && a.vol.to_local_identity && a.vol.bitfield)   // persistent: 3 LDS copies per CU
         hipLaunchKernelGGL(init_rays_kernel<true>, dim3(std::min(blocks, n_cus * 3u)), dim3(256), a.vol.occ_brick_words * 4, s, a, out, ctrl, fb, depth,
@@ -1178,12 +1157,11 @@ void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl
         hipLaunchKernelGGL(init_rays_kernel<false>, dim3(blocks), dim3(256), 0, s, a, out, ctrl, fb, depth, pos, nrm, n);
 }
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
-                     uint32_t blocks, int store_t, int global_sched, hipStream_t s, bool wide) {
+                     uint32_t blocks, int store_t, int global_sched, hipStream_t s) {
     if (v.linear && v.occ_brick_words && v.to_local_identity)
         hipLaunchKernelGGL(HIP_KERNEL_NAME(generate_kernel<true, 256, true>), dim3(blocks), dim3(256), v.occ_brick_words * 4, s, v, rays, ctrl, p, target, iter, coords,
                            samp, store_t, global_sched);
     else if (v.linear) hipLaunchKernelGGL(generate_kernel<true>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
-    else if (wide) hipLaunchKernelGGL(HIP_KERNEL_NAME(generate_kernel<false, 1024>), dim3(std::max(1u, blocks / 4u)), dim3(1024), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
     else hipLaunchKernelGGL(generate_kernel<false>, dim3(blocks), dim3(256), 0, s, v, rays, ctrl, p, target, iter, coords, samp, store_t, global_sched);
 }
 void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const Sched& sched, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p,

@@ -17,8 +17,8 @@
 // of two adjacent 16-row blocks give the 8 k-slots of one 32-deep k step, and
 // the host stores each weight matrix's columns in that permuted k order.
 // The 20 weight fragments (20 KiB) are staged once per workgroup in LDS and read per layer with
-// conflict-free ds_read_b128 (72 VGPRs, 7 waves/SIMD); -DNET_W_REGS keeps them resident in 80 VGPRs
-// per wave instead (149 VGPRs, 3 waves/SIMD), measured 1.5-2 % slower per launch.
+// conflict-free ds_read_b128 (72 VGPRs, 7 waves/SIMD); keeping them resident in 80 VGPRs per wave instead
+// (149 VGPRs, 3 waves/SIMD) measured 1.5-2 % slower per launch.
 #include <hip/hip_ext.h>
 
 #include "nerf_field.h"
@@ -39,25 +39,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NET_WAVES_P
     const int lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
-#ifdef NET_W_REGS
-    if (wave >= n_tiles) return;
-#endif
     const int g = lane >> 4, col = lane & 15;
 
-#ifndef NET_W_REGS
     __shared__ h8 sW[20 * 64];
     for (int k = threadIdx.x; k < 20 * 64; k += blockDim.x) sW[k] = wfrag[k];
     __syncthreads();
     const LdsWeights W{sW, lane};
-#else
-    h8 W[20];
-#pragma unroll
-    for (int f = 0; f < 20; ++f) W[f] = wfrag[f * 64 + lane];
-#endif
-#ifndef NET_XCD_INTERLEAVED
     // workgroup slot x = blockIdx % 8 (one XCD under round-robin dispatch: affinity only) walks one
     // contiguous eighth of the tiles, so neighbouring rays' mid-level cells meet in the same L2
-    // (measured 1.5 % shorter launches than the grid-wide interleave)
+    // (measured 1.5 % shorter launches than the grid-wide interleave over all waves)
     uint32_t t_begin = wave, t_end = n_tiles, t_step = n_waves;
     if ((gridDim.x & 7u) == 0) {
         const uint32_t wpb = blockDim.x >> 6, x = blockIdx.x & 7u;
@@ -67,9 +57,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NET_WAVES_P
         t_step = (gridDim.x >> 3) * wpb;
     }
     for (uint32_t tile = t_begin; tile < t_end; tile += t_step) {
-#else
-    for (uint32_t tile = wave; tile < n_tiles; tile += n_waves) {
-#endif
         const uint32_t s = tile * 16 + col;
         const bool valid = s < n;
         const float* c = coords + (size_t)(valid ? s : n - 1) * stride;
@@ -136,21 +123,11 @@ int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, 
                    uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
     uint32_t tiles = n_dev ? max_tiles_hint : (n_static + 15) / 16;
     if (tiles == 0) return 0;
-    // persistent-style grid: one occupancy's worth of waves (3/SIMD with register weights, 7/SIMD with
-    // LDS weights), never more than the tiles
-#ifndef NET_GRID_WAVES_PER_CU
-#ifdef NET_W_REGS
-#define NET_GRID_WAVES_PER_CU 12u
-#else
-#define NET_GRID_WAVES_PER_CU 28u
-#endif
-#endif
-    uint32_t max_waves = (uint32_t)net.n_cus * NET_GRID_WAVES_PER_CU;
+    // persistent-style grid: one occupancy's worth of waves (7/SIMD), never more than the tiles
+    uint32_t max_waves = (uint32_t)net.n_cus * 28u;
     uint32_t waves = tiles < max_waves ? tiles : max_waves;
     uint32_t blocks = (waves + 3) / 4;
-#ifndef NET_XCD_INTERLEAVED
     blocks = (blocks + 7u) & ~7u;   // whole XCD slots
-#endif
     const h8* w = reinterpret_cast<const h8*>(net.wfrag);
     const _Float16* gr = reinterpret_cast<const _Float16*>(net.grid);
     auto go = [&](auto kernel) {

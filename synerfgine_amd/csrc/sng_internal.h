@@ -119,8 +119,6 @@ struct NerfFrameArgs {
     uint32_t spp;
     int snap;
     int reset;           // clear alpha of the frame buffer (camera moved)
-    int ray_tile;        // > 0: rays enter the buffer in ray_tile x ray_tile pixel tiles (2-D locality of the
-                         //      network launches' samples); 0: row-major.  Per-ray results do not depend on it
     uint32_t target_n_queries;
     TraceMode mode;
     Sched sched;
@@ -238,7 +236,6 @@ struct RaytraceArgs {
     uint32_t* tile_cost;        // per-tile cycles of this frame (nullptr: not recorded)
     int bvh_flat;               // BvhWide traversal with the nearer child in a register (bvh_walk_near)
     int tile;                   // path-kernel tile edge in pixels (8: 64 lanes, 4: 16 lanes per wave)
-    int spec_group;             // > 0: sample-parallel path kernel (raytrace_spec_kernel), lanes per pixel
     unsigned long long* counts; // counting frames (rt_count): path kernel {queries, box, tri}, shadow kernel {queries, box, tri}
     int count_waves;            // rt_count = 2: box / tri entries count wave iterations of those loops (SIMD efficiency)
 };
@@ -249,21 +246,18 @@ struct RaytraceArgs {
 // point-light sample jp: {L, full_dist} (origin: its record's pos); its mask is written by the shadow
 // kernel.  Light colours and shadow rays are stored sample-major ([jl][k], [jp][k]): the lanes of a
 // wave shade consecutive records (wave_alloc), so each of their stores is one contiguous 1-KiB run
-// instead of 64 scattered 16-B pieces (record-major scatter ran at ~1.7 TB/s, C3 rt_shade_records).
+// instead of 64 scattered 16-B pieces (record-major scatter ran at ~1.7 TB/s).
 struct RtQueue {
-    float4* rec;          // cap x rec_stride float4: {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y} [+ shade inputs]
+    float4* rec;          // cap x rec_stride float4: {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y}
     float4* lc;           // nls x cap float4: {lc, 0} of record k, light sample jl at [jl * cap + k]
     float4* srec;         // nps x cap float4: {L, full_dist} of record k, shadow sample jp at [jp * cap + k]
     float* mask;          // cap x nps
     int* head;            // per mesh pixel: first hit record or -1
     uint32_t* count;      // hit records allocated (device counter)
-    uint32_t rec_stride;  // float4 per hit record = 2 (+ 4 shade inputs)
+    uint32_t rec_stride;  // float4 per hit record (2)
     uint32_t nls;         // n_lights * shadow_iters
     uint32_t nps;         // n_point_lights * shadow_iters
     uint32_t cap;
-    uint32_t shade_in;    // > 0: float4 offset of the deferred-shading inputs {normal} {rd} {rng v0-v3} {rng v4, d}
-                          // in each record; raytrace_kernel skips the light samples' draws and
-                          // rt_shade_records_kernel computes lc + shadow rays off the path chain
     // per-pixel record lists (tile path kernel): plist[t * max_hits + h] = the pixel's h-th hit record, pcount[t]
     // = its hits; rt_record_colour_kernel writes each record's colour term to rval and rt_accumulate_kernel
     // sums them in list order without walking the record chain.  nullptr: chain walk.
@@ -303,8 +297,6 @@ struct SpecArgs {
     float* positions;
     float4* pre;                  // per network sample: {logistic r, g, b, alpha} (spec_prepare; nullptr: the compositor
     float* pre_depth;             //   activates the raw outputs itself) and dot(fwd, pos - cam)
-    uint4* dbg;                   // nerf_spec_debug: per round and ray {march trips, samples, shader cycles, K} (nullptr: off)
-    uint32_t dbg_stride;          // rays per round in dbg
     uint8_t* hint;                // per NeRF pixel: 1 + the iteration its ray ended at in the last frame (0: unknown);
                                   // a ray looks ahead just that far (exact whatever the hint: it only sizes the round)
 };
@@ -318,7 +310,7 @@ void launch_tail_prepare(MarchCtrl* ctrl, uint32_t* work, int p, uint32_t target
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm, uint32_t n_cus,
                       hipStream_t s);
 void launch_generate(const Volume& v, const RayBuf& rays, MarchCtrl* ctrl, int p, uint32_t target, uint32_t iter, float* coords, uint2* samp,
-                     uint32_t blocks, int store_t, int global_sched, hipStream_t s, bool wide = false);
+                     uint32_t blocks, int store_t, int global_sched, hipStream_t s);
 void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode, const Sched& sched, const RayBuf& in, const RayBuf& out, MarchCtrl* ctrl, int p,
                       uint32_t target, uint32_t iter, const float* coords, const uint2* samp, const uint2* net_out, float4* fb, float* depth, float* pos, uint32_t blocks,
                       hipStream_t s, bool wide = false);
@@ -334,20 +326,6 @@ void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 fo
                       hipStream_t s);
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
                                float* accd, uint32_t shadow_blocks, hipStream_t s);
-void launch_raytrace_spec(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
-                          float* accd, uint8_t* hint, hipStream_t s);
-// staged path tracer buffers (mesh.hip, rt_staged): hit / ray queues of one stage (3 float4 per entry,
-// capacity = band pixels) and per-pixel state carried across stages
-struct RtStage {
-    float4* hits;            // [pos, pixel] [rd, spp] [pdf, att, obj, tri]
-    float4* rays;            // [origin, pixel] [dir, spp] [pdf, att, -, -]
-    uint32_t* hit_count;     // set per launch
-    float4* next_pos;        // per pixel: sum of the primary hits over the samples
-    int* head;               // per pixel: first hit record (RtQueue::head)
-    int* tail;               // per pixel: last hit record
-};
-void launch_raytrace_staged(const RaytraceArgs& a, const RtQueue& q, RtStage st, uint32_t* counters, const float4* o, const float4* d, uint32_t* rng,
-                            uint32_t n_rng, float4* acc, float* accd, hipStream_t s);
 void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, uint32_t* aux, hipStream_t s);
 
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,

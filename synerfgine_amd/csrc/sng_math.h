@@ -432,9 +432,6 @@ SNG_HD bool occupied_linear(f3 pos, const uint32_t* occ) {
 // the march's dependent chain.  Same bits as occupied_linear.
 struct OccCache {
     uint32_t w = 0xffffffffu, bits = 0u;
-#ifdef SNG_OCC_COUNT
-    uint32_t loads = 0u;
-#endif
 };
 SNG_HD bool occupied_linear_c(f3 pos, const uint32_t* occ, OccCache& c) {
     f3 q = ((pos - splat(0.5f)) + splat(0.5f)) * (float)GRID_SIZE;   // cascaded_grid_idx_at, mip 0
@@ -444,9 +441,6 @@ SNG_HD bool occupied_linear_c(f3 pos, const uint32_t* occ, OccCache& c) {
     if (w != c.w) {
         c.w = w;
         c.bits = occ[w];
-#ifdef SNG_OCC_COUNT
-        ++c.loads;
-#endif
     }
     return (c.bits >> (ix & 31)) & 1u;
 }

@@ -362,7 +362,6 @@ __device__ __forceinline__ void grid_backward_level_coop4(const LevelInfo& L, fl
             const int src = 16 * i + qd;
             const float ws = __shfl(w, src, 64);
             const uint32_t as = __shfl(at, src, 64);
-#ifndef TRAIN_GRID_NO_RUNS
             // consecutive samples of a ray that share this corner entry (the coarse levels: a 16^3 cell
             // holds ~37 samples of a ray) form runs over qd; a segmented scan sums each run and only
             // its last lane adds to memory, instead of up to 16 adds to one address in one instruction
@@ -377,9 +376,6 @@ __device__ __forceinline__ void grid_backward_level_coop4(const LevelInfo& L, fl
             }
             const bool tail = qd == 15 || a_next != as;
             if (tail && v != 0.0f) atomicAdd(ggrad + as + f, v);
-#else
-            if (ds[i] != 0.0f) atomicAdd(ggrad + as + f, ws * ds[i]);
-#endif
         }
     }
 }
@@ -503,13 +499,8 @@ __global__ __launch_bounds__(256) void train_field_kernel(TrainStepArgs a, Train
         float df0[4], df1[4];
         for (int k = 0; k < 4; ++k) { df0[k] = valid ? (float)(_Float16)de0[k] : 0.0f; df1[k] = valid ? (float)(_Float16)de1[k] : 0.0f; }
         if constexpr (F == 4) {
-#ifndef TRAIN_GRID_SCATTERED
             grid_backward_level_coop4(levels[g], ggrad, x0, x1, x2, df0, lane);
             grid_backward_level_coop4(levels[4 + g], ggrad, x0, x1, x2, df1, lane);
-#else
-            grid_backward_level<4>(levels[g], ggrad, x0, x1, x2, df0);
-            grid_backward_level<4>(levels[4 + g], ggrad, x0, x1, x2, df1);
-#endif
         } else {
             if (!valid) continue;
             grid_backward_level<2>(levels[2 * g], ggrad, x0, x1, x2, df0);

@@ -38,11 +38,11 @@ def test_profiling_sh_command_line(cli):
 
 def test_aliases_equals_form_and_headless_flags(cli):
     r = run(cli, "--dry-run", "--load_snapshot=a.ingp", "--rt", "s.json", "--width=640", "--height=360", "--frames", "3", "--out", "o",
-            "--gpus", "8", "--balance", "2", "--set", "rt_spec=1", "--set=nerf_spec_rounds=2", "--display")
+            "--gpus", "8", "--balance", "2", "--set", "rt_tile=4", "--set=nerf_spec_rounds=2", "--display")
     o = json.loads(r.stdout)
     assert (o["snapshot"], o["virtual"], o["width"], o["height"]) == ("a.ingp", "s.json", 640, 360)
     assert (o["frames"], o["out"], o["gpus"], o["balance"], o["display"]) == (3, "o", 8, 2, True)
-    assert o["sets"] == {"rt_spec": 1.0, "nerf_spec_rounds": 2.0}
+    assert o["sets"] == {"rt_tile": 4.0, "nerf_spec_rounds": 2.0}
     assert o["sshadows"] == -1   # not given: the engine keeps the scene JSON's values (main.cu:210)
 
 

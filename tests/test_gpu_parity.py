@@ -252,11 +252,10 @@ def test_errors_are_loud(tb):
         tb.inference_mixed_precision(0, 3, 16, 0)
 
 
-@pytest.mark.parametrize("overrides", [{}, {"path_trace_depth": 3, "light_samples": 3}, {"fast_slab": 0}, {"scene_lds": 0}, {"rt_staged": 1},
-                                       {"rt_staged": 1, "path_trace_depth": 3, "light_samples": 3}, {"rt_staged": 1, "scene_lds": 0}, {"rt_defer_shade": 1}])
+@pytest.mark.parametrize("overrides", [{}, {"path_trace_depth": 3, "light_samples": 3}, {"fast_slab": 0}, {"scene_lds": 0},
+                                       {"scene_lds": 0, "light_samples": 16}, {"path_trace_depth": 1}, {"rt_tile": 4}])
 def test_wavefront_raytracer_equals_megakernel(overrides):
-    """Deferred shadow-ray queues (rt_wavefront=1) and the staged tracer (rt_staged=1) reproduce the one-kernel
-    path tracer bit for bit."""
+    """Deferred shadow-ray queues (rt_wavefront=1) reproduce the one-kernel path tracer bit for bit."""
     import ctypes
     tb, eng, _ = _engine(192, 108, overrides)
     try:
@@ -264,12 +263,10 @@ def test_wavefront_raytracer_equals_megakernel(overrides):
         m0 = eng.rng_states(1).copy()
         n0 = eng.rng_states(0).copy()
         out = {}
-        staged = overrides.get("rt_staged", 0)
         for mode in (0, 1):
             tb._lib.sng_set_rng_states(tb.ctx, 0, n0.ctypes.data_as(P), n0.shape[0])
             tb._lib.sng_set_rng_states(tb.ctx, 1, m0.ctypes.data_as(P), m0.shape[0])
             eng.set_param("rt_wavefront", mode)
-            eng.set_param("rt_staged", staged if mode else 0)
             r = eng.frame()
             out[mode] = (r.download("syn_rgba"), r.download("syn_depth"), eng.rng_states(1).copy())
         for a, b in zip(out[0], out[1]):
@@ -279,36 +276,7 @@ def test_wavefront_raytracer_equals_megakernel(overrides):
         tb.close()
 
 
-@pytest.mark.parametrize("config,overrides,rows", [("c3", {}, None), ("c3", {}, (40, 71)), ("c3", {"light_samples": 3}, None),
-                                                    ("c3", {"path_trace_depth": 1}, None), ("c3", {"scene_lds": 0, "light_samples": 16}, None),
-                                                    ("c4", {}, None), ("c4", {}, (20, 52))])
-def test_sample_parallel_raytracer_equals_path_kernel(config, overrides, rows):
-    """The sample-parallel path kernel (rt_spec=1: a pixel's samples on separate lanes from guessed
-    XORWOW offsets, re-traced until the offsets are the serial ones) reproduces the serial path kernel
-    bit for bit -- colours, depths and the XORWOW states it leaves -- over three frames (frames 2-3 start
-    from the previous frame's hit-depth guesses), full frames and bands, 3 / 8 / 16 samples, 1-2 bounces."""
-    tb, eng, _ = _engine(192, 108, overrides, config=config)
-    try:
-        m0, n0 = eng.rng_states(1).copy(), eng.rng_states(0).copy()
-        out = {}
-        for spec in (0, 1):
-            eng.set_rng_states(0, n0)
-            eng.set_rng_states(1, m0)
-            eng.set_param("rt_spec", spec)
-            frames = []
-            for _ in range(3):
-                r = eng.frame(rows=rows)
-                frames.append((r.download("syn_rgba"), r.download("syn_depth"), r.download("final_rgba"), eng.rng_states(1).copy()))
-            out[spec] = frames
-        for fa, fb in zip(out[0], out[1]):
-            for a, b in zip(fa, fb):
-                assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
-        assert (out[1][0][1] < 100).mean() > 0.02    # objects are in view
-    finally:
-        tb.close()
-
-
-@pytest.mark.parametrize("config,overrides,rows", [("c3", {}, None), ("c3", {}, (37, 90)), ("c3", {"rt_defer_shade": 1}, None),
+@pytest.mark.parametrize("config,overrides,rows", [("c3", {}, None), ("c3", {}, (37, 90)), ("c3", {"light_samples": 16}, None),
                                                     ("c3", {"path_trace_depth": 3, "light_samples": 3}, None), ("c4", {}, (20, 52))])
 def test_record_lists_equal_chain_walk(config, overrides, rows):
     """The colour replay over per-pixel record lists + per-record colour terms (rt_plist=1) equals the walk of

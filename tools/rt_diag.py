@@ -7,7 +7,7 @@ import numpy as np
 
 from synerfgine_amd import scene as S
 
-CASES = [{}, {"rt_staged": 1}, {"rt_tile_order": 0}, {"rt_wavefront": 0}, {"scene_lds": 0}, {"shadow_on_virtual_obj": 0}, {"path_trace_depth": 1}, {"light_samples": 1}, {"syn_shadow_samples": 1},
+CASES = [{}, {"rt_tile_order": 0}, {"rt_wavefront": 0}, {"scene_lds": 0}, {"shadow_on_virtual_obj": 0}, {"path_trace_depth": 1}, {"light_samples": 1}, {"syn_shadow_samples": 1},
          {"show_nerf": 0}, {"fast_slab": 0}]
 for ov in CASES:
     tb, eng, _ = S.make_engine("c3", overrides={"concurrent_streams": 0, "show_nerf": 1, **ov})

@@ -36,32 +36,4 @@ for ov in sets:
                       "raytrace": round(r.ms_raytrace, 3), "net_ms": round(r.ms_network, 4), "launches": r.network_launches,
                       "tail_ms": round(r.ms_fused_tail, 4), "spec_evals": r.spec_evals, "spec_exec": r.spec_exec,
                       "iters": r.n_iterations, "samples": r.n_samples}), flush=True)
-if any(ov.get("nerf_spec_debug") for ov in sets):
-    import numpy as np
-    W, H = eng.resolution()["nerf"]
-    dbg = eng.frame_buffer("spec_dbg", np.uint32).reshape(-1, W * H, 4)   # [round][pixel] {trips, samples|loads<<16, cycles, A bits}
-    alive = dbg[:, :, 0] > 0
-    for r, d in enumerate(dbg):
-        m = alive[r]
-        if not m.any():
-            continue
-        d = d[m]
-        cyc = d[:, 2].astype(np.float64)
-        tr = d[:, 0].astype(np.float64)
-        am = int(np.argmax(tr))
-        print(json.dumps({"round": r, "rays": int(m.sum()), "trips_max": int(tr.max()), "trips_mean": round(tr.mean(), 1),
-                          "trips_p99": float(np.percentile(tr, 99)), "samples_max": int((d[:, 1] & 0xffff).max()), "cycles_max": int(cyc.max()),
-                          "cycles_per_trip_of_max": round(float(cyc[am] / tr.max()), 1)}))
-    # rounds of one iteration each (nerf_spec_kmax=1): remaining iterations of the rays alive after the head vs their opacity
-    if alive.shape[0] > 1:
-        a0 = dbg[0, :, 3].view(np.float32)
-        rem = alive.sum(axis=0)
-        m = alive[0]
-        for lo, hi in ((0, 0.05), (0.05, 0.2), (0.2, 0.5), (0.5, 0.8), (0.8, 0.95), (0.95, 1.01)):
-            sel = m & (a0 >= lo) & (a0 < hi)
-            if sel.any():
-                q = rem[sel]
-                print(json.dumps({"A_after_head": [lo, hi], "rays": int(sel.sum()), "iters_mean": round(float(q.mean()), 2),
-                                  "iters_p50": float(np.percentile(q, 50)), "iters_p90": float(np.percentile(q, 90)), "iters_max": int(q.max()),
-                                  "frac_1": round(float((q == 1).mean()), 3)}))
 tb.close()
