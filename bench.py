@@ -499,7 +499,9 @@ def main():
     evaluated = total_samples - reused                      # network evaluations (launches + fused tail)
     spec_evals = sum(s.spec_evals for s in stats)           # speculative tail rounds: samples their network launches evaluated
     spec_exec = sum(s.spec_exec for s in stats)             # ... of which composited (the rest: look-ahead past a ray's end)
-    tail_samples = evaluated - (samples - (spec_evals - spec_exec))
+    msr_evals = sum(s.msr_evals for s in stats)             # multi-step speculative rounds: samples their launches evaluated
+    msr_exec = sum(s.msr_exec for s in stats)               # ... of which the per-iteration wavefront would have evaluated
+    tail_samples = evaluated - (samples - (spec_evals - spec_exec) - (msr_evals - msr_exec))
     ms_tail = sum(s.ms_fused_tail for s in stats)
     os_evals = sum(s.onestep_field_evals for s in stats)   # field evaluations inside the one-step regime's final pass
     ms_os = sum(s.ms_onestep for s in stats)
@@ -576,6 +578,11 @@ def main():
                                                   "(exact replay), per round", "rounds_per_frame": int(s0.spec_rounds),
                                        "samples_evaluated": int(spec_evals), "samples_composited": int(spec_exec),
                                        "lookahead_discarded_frac": round(1.0 - spec_exec / spec_evals, 4) if spec_evals else 0.0},
+                         "msr_rounds": {"kernels": "msr_generate (K iterations of S steps marched ahead per ray) + nerf_network_kernel + "
+                                                   "msr_count (death histogram) + msr_schedule (committed prefix) + msr_commit (exact replay), "
+                                                   "while n_steps is 2..7", "rounds_per_frame": int(s0.msr_rounds),
+                                        "samples_evaluated": int(msr_evals), "samples_committed": int(msr_exec),
+                                        "discarded_frac": round(1.0 - msr_exec / msr_evals, 4) if msr_evals else 0.0},
                          "onestep_regime": {"kernels": "nerf_onestep_kernel x2 + schedule (trace_alt while n_alive > target/2; ray-local, "
                                                        "periodic rays composited in a closed loop)", "field_evals": int(os_evals),
                                             "ms": round(ms_os, 4)},

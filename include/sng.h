@@ -103,7 +103,9 @@ typedef struct {
     uint32_t spec_rounds;       /* speculative tail rounds enqueued (nerf_spec_rounds; 0: none) */
     uint32_t spec_evals;        /* samples their network launches evaluated, incl. those past a ray's end */
     uint32_t spec_exec;         /* ... of which composited (the rest is the rounds' discarded look-ahead) */
-    uint32_t reserved2[3];
+    uint32_t msr_rounds;        /* multi-step speculative rounds that committed iterations (nerf_msr; 0: none) */
+    uint32_t msr_evals;         /* samples their network launches evaluated ... */
+    uint32_t msr_exec;          /* ... of which the per-iteration wavefront would have evaluated */
 } sng_frame_result;
 
 typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;

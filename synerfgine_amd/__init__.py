@@ -168,7 +168,7 @@ class FrameResult:
                      "ms_overlay", "ms_network", "network_launches",
                      "fused_from_iter", "n_samples_network", "ms_fused_tail", "n_samples_reused",
                      "onestep_from_iter", "onestep_iterations", "ms_onestep", "onestep_field_evals", "spec_rounds", "spec_evals",
-                     "spec_exec"):
+                     "spec_exec", "msr_rounds", "msr_evals", "msr_exec"):
             setattr(self, name, getattr(r, name))
         self.alive_per_iter = list(r.alive_per_iter)[: min(64, r.n_iterations)]
         self.steps_per_iter = list(r.steps_per_iter)[: min(64, r.n_iterations)]

@@ -89,7 +89,9 @@ class sng_frame_result(ctypes.Structure):
         ("spec_rounds", ctypes.c_uint32),
         ("spec_evals", ctypes.c_uint32),
         ("spec_exec", ctypes.c_uint32),
-        ("reserved2", ctypes.c_uint32 * 3),
+        ("msr_rounds", ctypes.c_uint32),
+        ("msr_evals", ctypes.c_uint32),
+        ("msr_exec", ctypes.c_uint32),
     ]
 
 

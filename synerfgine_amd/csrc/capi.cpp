@@ -374,6 +374,10 @@ const std::map<std::string, double>& default_params() {
         {"nerf_gen_blocks", -1},                 // generate grid (256-thread units): 0 = min(rays, 8 per CU); -1 = all rays in one trip
         {"rt_shadow_all_cus", 1},               // shadow-ray kernel on every CU: the NeRF tail has mostly finished by then (C3 +2 %; 0: the path kernel grid)
         {"rt_count", 0},                        // count BVH queries / box / triangle tests of the deferred raytracer (sng_rt_counters); 2: wave iterations
+        {"nerf_msr", 1},                        // multi-step speculative rounds while n_steps is 2..7 (nerf.hip msr_*; exact)
+        {"nerf_msr_budget", 16777216},          // samples one such round may generate (K = clamp(budget / (S n_alive), 1, kmax))
+        {"nerf_msr_kmax", 16},                  // iterations one such round marches ahead (<= 16)
+        {"march_log", 0},                       // diagnostics: log {alive, steps, samples} of every iteration (sng_frame_buffer "march_log")
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
         {"nerf_onestep_horizon", 2048},         // iterations one speculative segment of the regime spans
     };
@@ -456,12 +460,17 @@ struct sng_ctx {
     DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
+    DevBuf tail_live;                      // tail iterations' alive counts as a difference array (reference slots)
+    DevBuf sched_hint;                     // steps of every iteration of the last frame (sizes the msr rounds)
+    DevBuf msr_hist;                       // multi-step rounds: [4][MSR_KMAX] per-iteration deaths / samples
+    DevBuf march_log;                      // diagnostics (param march_log): per iteration {alive, steps, samples}
     DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
     DevBuf spec_hint;                      // per NeRF pixel: 1 + the iteration its ray ended at last frame (u8, 0 unknown)
     uint64_t spec_hint_px = 0;
     DevBuf spec_pre, spec_pre_depth;       // spec_prepare: per network sample {rgb, alpha} and depth
     DevBuf band_rgba8;                     // sng_gather_rgba8: this rank's band as RGBA8
     uint32_t spec_rounds = 0;              // rounds enqueued by the last trace
+    uint32_t msr_rounds = 0;               // multi-step speculative rounds of the last trace that committed iterations
     DevBuf rt_counts;                      // rt_count frames: path / shadow kernel {queries, box tests, triangle tests}
     bool fused_last = false;               // the last trace finished in the fused kernel
     uint32_t fused_k0 = 0;                 // ... from this iteration on
@@ -1047,10 +1056,8 @@ f2 render_screen_center(const sng_ctx* c) {
 // slots the reference would evaluate: sum over iterations of n_alive * n_steps padded to 256
 // (testbed_nerf.cu:2210); the fused kernel only records the per-iteration alive counts
 uint64_t ref_slots_of(const sng_ctx* c) {
-    uint64_t s = c->h_ctrl->ref_slots;   // accumulated by generate_kernel for the wavefront iterations
-    if (!c->fused_last) return s;
-    for (uint32_t k = c->fused_k0; k < std::min<uint32_t>(64u, c->h_ctrl->n_iter); ++k) s += ((uint64_t)c->h_ctrl->alive_hist[k] * 8 + 255) / 256 * 256;
-    return s;
+    // generate_kernel / msr_schedule / the one-step schedule add the wavefront's iterations, tail_slots_kernel the tail's
+    return c->h_ctrl->ref_slots;
 }
 
 // NerfTracer::init_rays_from_camera + trace_alt / trace (testbed_nerf.cu:2037-2401) for NeRF rows
@@ -1065,7 +1072,13 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     const int NW = c->nerf_res[0], NH = c->nerf_res[1];
     uint32_t net_launches = 0;
     MarchCtrl* ctrl = c->ctrl.as<MarchCtrl>();
-    launch_ctrl_init(ctrl, c->s_nerf);
+    if (c->p("march_log") != 0.0) c->march_log.ensure(MARCH_LOG_CAP * 12);
+    c->tail_live.ensure(TAIL_LIVE_CAP * 4);
+    if (!c->sched_hint.p) {
+        c->sched_hint.ensure(TAIL_LIVE_CAP);
+        HIPCHK(hipMemsetAsync(c->sched_hint.p, 0, TAIL_LIVE_CAP, c->s_nerf));
+    }
+    launch_ctrl_init(ctrl, c->tail_live.as<int32_t>(), c->sched_hint.as<uint8_t>(), c->s_nerf, c->p("march_log") != 0.0 ? c->march_log.as<uint32_t>() : nullptr);
     NerfFrameArgs a{};
     a.vol = vol;
     a.cam = cam;
@@ -1117,6 +1130,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     const uint32_t n_band = (uint32_t)(tr1 - tr0) * (uint32_t)NW;
     c->fused_last = false;
     c->fused_k0 = 0;
+    c->msr_rounds = 0;
     // Hybrid schedule (fused.hip): the first `nerf_fused_after` iterations run as whole-GPU
     // wavefront launches (nearly every ray alive: throughput bound), the rest -- the latency-bound
     // tail -- in the ray-local fused kernel.  Valid when every iteration takes 8 steps, i.e. the
@@ -1163,6 +1177,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     // trace_alt's one-step regime (fused.hip): tried at the first chunk boundary at which the alive
     // count may still exceed target / 2 (the boundary-sample caches are warm by then)
     bool os_open = !mode.ngp && c->p("nerf_onestep") != 0.0;
+    const bool msr_on = !mode.ngp && c->p("nerf_msr") != 0.0;
     uint32_t& os_k = c->os_k;
     uint32_t& os_J = c->os_J;
     c->os_ran = false;
@@ -1224,6 +1239,65 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             }
         }
         if (c->os_ran && c->h_os->istep0 + c->h_os->J >= MARCH_ITER) break;
+        // multi-step speculative rounds (nerf.hip msr_*) while the step count is 2..7: each round commits the
+        // iterations its guess S held for; a round whose first iteration does not take 2..7 steps is a no-op
+        if (msr_on && chunk >= 1 && !fuse && (uint64_t)known_alive * MAX_STEPS_BETWEEN_COMPACTION > target) {
+            c->msr_hist.ensure(4 * MSR_KMAX * 4);
+            c->spec_t.ensure(c->sample_cap * 4);
+            MsrArgs ma{};
+            ma.vol = vol; ma.cam = cam; ma.sched = a.sched; ma.ctrl = ctrl; ma.target = target;
+            ma.budget = (uint32_t)std::min<double>((double)c->sample_cap, std::max(1.0, c->p("nerf_msr_budget")));
+            ma.kmax = (uint32_t)std::min<double>(MSR_KMAX, std::max(1.0, c->p("nerf_msr_kmax")));
+            ma.coords = c->coords.as<float>(); ma.samp = c->samp.as<uint2>(); ma.tbuf = c->spec_t.as<float>(); ma.net_out = c->net_out.as<uint2>();
+            ma.hist = c->msr_hist.as<uint32_t>();
+            ma.frame_rgba = c->nerf_rgba.as<float4>(); ma.frame_depth = c->nerf_depth.as<float>(); ma.positions = c->nerf_pos.as<float>();
+            const uint32_t mblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
+            while (true) {
+                ma.in = rb[p]; ma.out = rb[p ^ 1]; ma.p = p;
+                launch_msr_generate(ma, gen_blocks, c->s_nerf);
+                if (P.collect_kernel_times) {
+                    while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
+                }
+                launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf,
+                               P.collect_kernel_times ? c->net_events[2 * net_launches] : nullptr,
+                               P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr);
+                launch_msr_count(ma, mblocks, c->s_nerf);
+                if (gsched) {   // the frame-wide schedule: own-row deaths summed over the ranks
+                    uint32_t* ds = ma.hist + MSR_KMAX;
+                    if (c->sched_comm.comm) {
+                        comm_allreduce_u32(c->sched_comm, ds, MSR_KMAX, c->s_nerf);
+                    } else {
+                        uint32_t h[MSR_KMAX];
+                        HIPCHK(hipMemcpyAsync(h, ds, sizeof(h), hipMemcpyDeviceToHost, c->s_nerf));
+                        HIPCHK(hipStreamSynchronize(c->s_nerf));
+                        if (c->sched_comm.host_fn(h, MSR_KMAX, c->sched_comm.host_user) != 0) throw SngError(SNG_ERR_STATE, "schedule reducer failed");
+                        HIPCHK(hipMemcpyAsync(ds, h, sizeof(h), hipMemcpyHostToDevice, c->s_nerf));
+                    }
+                }
+                launch_msr_schedule(ma, c->s_nerf);
+                launch_msr_commit(ma, mblocks, c->s_nerf);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipMemcpyAsync(c->h_ctrl, ctrl, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
+                HIPCHK(hipStreamSynchronize(c->s_nerf));
+                const MarchCtrl& hc = *c->h_ctrl;
+                if (hc.msr_K[p] == 0) break;   // no-op: the rays are still in buffer p
+                ++net_launches;
+                ++c->msr_rounds;
+                reduce_sched(p ^ 1);
+                p ^= 1;
+                iter = hc.n_iter;
+                // the (frame-wide) count the next round starts from
+                HIPCHK(hipMemcpyAsync(c->h_alive, sched_src + p, 4, hipMemcpyDeviceToHost, c->s_nerf));
+                HIPCHK(hipStreamSynchronize(c->s_nerf));
+                known_alive = c->h_alive[0];
+                if (known_alive == 0) { done = true; break; }
+                if ((uint64_t)known_alive * MAX_STEPS_BETWEEN_COMPACTION <= target) {   // the 8-step tail's regime
+                    if (!wavefront_only && c->p("nerf_fused") != 0.0) { fuse = true; fuse_after = iter; }
+                    break;
+                }
+            }
+            if (done) break;
+        }
         if (fuse && iter >= fuse_after) {
             c->fused_work.ensure(16);
             c->fused_last = true;
@@ -1295,6 +1369,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             if (fb < 0) fb = (beside_rt && c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0) ? 2.0 * std::max(1.0, c->p("rt_reserved_cus")) : 0.0;
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused0, c->s_nerf));
             launch_nerf_fused(fa, c->net, iter == 0 && !rounds ? std::min(c->h_alive[0], n_band) : n_band, (uint32_t)fb, c->s_nerf, rounds == 0);
+            launch_tail_slots(ctrl, c->s_nerf);
             HIPCHK(hipGetLastError());
             if (P.collect_kernel_times) HIPCHK(hipEventRecord(c->ev_fused1, c->s_nerf));
             if (tentative_now) {
@@ -1390,6 +1465,9 @@ void march_stats(const sng_ctx* c, const sng_frame_params& P, sng_frame_result* 
     out->spec_rounds = c->fused_last ? c->spec_rounds : 0u;
     out->spec_evals = (uint32_t)c->h_ctrl->spec_evals;
     out->spec_exec = (uint32_t)c->h_ctrl->spec_exec;
+    out->msr_rounds = c->msr_rounds;
+    out->msr_evals = (uint32_t)c->h_ctrl->msr_evals;
+    out->msr_exec = (uint32_t)c->h_ctrl->msr_exec;
     std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
     std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
     std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
@@ -1934,7 +2012,7 @@ void ctx_destroy(sng_ctx* c) {
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
                       &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_lc, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
-                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_counts, &c->spec_t, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
+                      &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_counts, &c->spec_t, &c->tail_live, &c->sched_hint, &c->msr_hist, &c->march_log, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); c->ray_kk[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1, c->ev_alive}) (void)hipEventDestroy(e);
@@ -2353,7 +2431,7 @@ int sng_frame_buffer(sng_ctx* c, const char* name, void* out, uint64_t cap, uint
     return guarded([&] {
         if (!c || !name) throw SngError(SNG_ERR_INVALID, "null context or name");
         HIPCHK(hipSetDevice(c->device));
-        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}};
+        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}, {"march_log", &c->march_log}};
         auto it = bufs.find(name);
         if (it == bufs.end()) throw SngError(SNG_ERR_INVALID, std::string("unknown frame buffer ") + name);
         HIPCHK(hipDeviceSynchronize());

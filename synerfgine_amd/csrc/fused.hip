@@ -82,6 +82,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     float4 rgba = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     uint32_t idx = 0, k = 0, istep = 0;
     uint32_t my_hits = 0, my_iter = 0;
+    bool loaded = false, left = false;   // the lane took a ray from the queue / retired its ray this trip
     unsigned long long my_samples = 0, my_reused = 0;
     // trace_alt boundary-sample cache (RayBuf::lt/lo): the previous iteration's last sample t and output
     float lt = 0.0f;
@@ -109,12 +110,15 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
                         mw = a.mode.ngp ? a.rays.mw[r] : 0.0f;
                         if (!a.mode.ngp) { lt = a.rays.lt[r].x; lo = a.rays.lo[r]; }
                         k = kk_in ? a.rays.kk[r] : k0;
+                        loaded = true;
                         istep = kk_in ? base_istep + MAX_STEPS_BETWEEN_COMPACTION * (k - base_k) : i_step0;
                         has = true;
                     }
                 }
             }
         }
+        wave_add_keyed(a.ctrl->tail_live, k, 1, loaded);   // alive from its first tail iteration on (reference slots)
+        loaded = false;
         if (!__ballot(has)) break;
 
         // ---- generate: up to 8 samples (generate_next_nerf_network_inputs, testbed_nerf.cu:790-837)
@@ -243,7 +247,8 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
             } else if (last) {
                 has = false;
             }
-            if (!has && a.hint) a.hint[idx] = (uint8_t)min(k + 1u, 255u);   // the next frame's look-ahead (SpecArgs::hint)
+            if (!has && a.hint) a.hint[idx] = (uint8_t)min(k - base_k + 1u, 255u);   // the next frame's look-ahead (SpecArgs::hint)
+            left = !has;   // alive up to iteration k
             if (hit) {
                 if (a.mode.ngp) {
                     float4 tmp = rgba;
@@ -270,6 +275,8 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
             istep += n_steps;
             ++k;
         }
+        wave_add_keyed(a.ctrl->tail_live, k, -1, left);   // k: one past the ray's last iteration
+        left = false;
         wave_sync();
     }
 
@@ -701,6 +708,8 @@ __global__ __launch_bounds__(1024) void onestep_schedule_kernel(OnestepArgs a) {
         slots += ((unsigned long long)alive_l + 255ull) / 256ull * 256ull;
         samp += sm;
         if (k + mm < 64) { c->alive_hist[k + mm] = alive_l; c->steps_hist[k + mm] = 1; c->samples_hist[k + mm] = sm; }
+        if (c->log && k + mm < MARCH_LOG_CAP) { c->log[3 * (k + mm)] = alive_l; c->log[3 * (k + mm) + 1] = 1; c->log[3 * (k + mm) + 2] = sm; }
+        if (k + mm < TAIL_LIVE_CAP) c->sched_hint[k + mm] = 1u;
         alive_l -= a.deaths_local[mm];
     }
     if (slots) atomicAdd(&slots_sh, slots);

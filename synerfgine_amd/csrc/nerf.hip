@@ -174,6 +174,8 @@ __global__ __launch_bounds__(THREADS) void generate_kernel(Volume vol, RayBuf ra
         ctrl->i_step[p ^ 1] = i_step + n_steps;
         if (active) {
             if (iter < 64) { ctrl->alive_hist[iter] = n_alive; ctrl->steps_hist[iter] = n_steps; }
+            if (ctrl->log && iter < MARCH_LOG_CAP) { ctrl->log[3 * iter] = n_alive; ctrl->log[3 * iter + 1] = n_steps; }
+            if (iter < TAIL_LIVE_CAP) ctrl->sched_hint[iter] = (uint8_t)n_steps;
             ctrl->n_iter = iter + 1;
             ctrl->ref_slots += ((unsigned long long)n_alive * n_steps + 255ull) / 256ull * 256ull;
         }
@@ -345,6 +347,7 @@ __global__ __launch_bounds__(THREADS) void composite_kernel(Volume vol, CamDev c
             ctrl->net_samples += ctrl->n_samples[p];
             ctrl->reused_samples += ctrl->n_reused[p];
             if (iter < 64) ctrl->samples_hist[iter] = ctrl->n_samples[p] + ctrl->n_reused[p];
+            if (ctrl->log && iter < MARCH_LOG_CAP) ctrl->log[3 * iter + 2] = ctrl->n_samples[p] + ctrl->n_reused[p];
         }
         ctrl->n_samples[p ^ 1] = 0;
         ctrl->n_reused[p ^ 1] = 0;
@@ -578,8 +581,8 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             uint32_t K_i = K < left ? K : left;
             // the ray's own end in the last frame, when it is still ahead: look exactly that far; otherwise the
             // opacity policy.  Any K is exact (the round's replay stops where the wavefront would).
-            const uint32_t h = a.hint ? (uint32_t)a.hint[__float_as_uint(di.w)] : 0u;
-            if (h != 0u && h - 1u >= k_i) K_i = min(K_i, h - k_i);
+            const uint32_t h = a.hint ? (uint32_t)a.hint[__float_as_uint(di.w)] : 0u;   // relative to the tail's first iteration
+            if (h != 0u && h - 1u >= k_i - base_k) K_i = min(K_i, h - (k_i - base_k));
             else if (a.k_policy) K_i = min(K_i, spec_k_of(a.in.rgba[i].w));
             const f3 idir = inv(d);
             const float dfw = dot(a.cam.c2, d);
@@ -753,7 +756,8 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
         float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
         float depth = 0.0f, mw = 0.0f, lt = 0.0f;
         uint2 lraw = make_uint2(0u, 0u);
-        uint32_t death_step = 0, kk_next = 0, k_end = 0;
+        uint32_t death_step = 0, kk_next = 0, k_end = 0, live_in = 0, live_out = 0;
+        bool live = false;
         if (i < n_alive) {
             rgba = a.in.rgba[i];
             depth = a.in.depth[i];
@@ -905,8 +909,15 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
                 }
             }
             survive = !ended;
-            if (ended && a.hint) a.hint[__float_as_uint(di.w)] = (uint8_t)min(k_end + 1u, 255u);
+            if (ended && a.hint) a.hint[__float_as_uint(di.w)] = (uint8_t)min(k_end - base_k + 1u, 255u);
+            if (n_it) {   // alive at iterations k0 .. (ended ? k_end : kk_next - 1): reference slots (tail_slots_kernel)
+                live_in = k0;
+                live_out = ended ? k_end + 1u : kk_next;
+                live = true;
+            }
         }
+        wave_add_keyed(ctrl->tail_live, live_in, 1, live);
+        wave_add_keyed(ctrl->tail_live, live_out, -1, live);
         const uint32_t slot = block_append<THREADS / 64>(&ctrl->n_alive[p ^ 1], survive ? 1u : 0u, nullptr, false, nullptr, false, sh_app, lane);
         if (survive) {
             a.out.o_t[slot] = ot;
@@ -981,6 +992,356 @@ __global__ void tail_prepare_kernel(MarchCtrl* ctrl, uint32_t* work, int p, uint
         ctrl->spec_kk_valid[0] = 0u;
         ctrl->spec_kk_valid[1] = 0u;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Multi-step speculative rounds (MsrArgs, sng_internal.h)
+// ---------------------------------------------------------------------------
+// The round's shape from the frame-wide alive count at its first iteration: S = that iteration's steps
+// (only 2..7: 1 is the one-step regime's, 8 the tail's), K iterations within the sample budget and
+// before MARCH_ITER.  K == 0: the round is a no-op (every msr kernel returns without touching state).
+// The last frame's schedule (MarchCtrl::sched_hint, frame-wide, so every rank of a banded frame forms the same K)
+// predicts where the step count changes: a round whose first iteration took S steps then too looks ahead as far
+// as S lasted; one whose first iteration took another count then is near a change and looks 2 iterations ahead.
+// Any K is exact (the schedule commits only the iterations whose guess held); the hint bounds the discarded work.
+__device__ __forceinline__ void msr_shape(const MarchCtrl* c, uint32_t n_sched, uint32_t istep0, uint32_t target, uint32_t budget, uint32_t kmax,
+                                          uint32_t& S, uint32_t& K) {
+    S = 0;
+    K = 0;
+    if (n_sched == 0 || istep0 >= MARCH_ITER) return;
+    const uint32_t s = steps_for(n_sched, target);
+    if (s < 2 || s >= MAX_STEPS_BETWEEN_COMPACTION) return;
+    uint32_t k = budget / (s * n_sched);
+    k = k < 1u ? 1u : (k > kmax ? kmax : k);
+    const uint32_t left = (MARCH_ITER - istep0 + s - 1) / s;   // iterations whose i is still < MARCH_ITER
+    k = k < left ? k : left;
+    const uint32_t k0 = c->n_iter;
+    const uint32_t h = k0 < TAIL_LIVE_CAP ? c->sched_hint[k0] : 0u;
+    if (h == s) {
+        uint32_t run = 1;
+        while (run < k && k0 + run < TAIL_LIVE_CAP && c->sched_hint[k0 + run] == s) ++run;
+        k = run;
+    } else if (h != 0u) {
+        k = k < 2u ? k : 2u;
+    }
+    S = s;
+    K = k;
+}
+
+// composite_kernel's opacity step on one sample (spec_composite_sample's alpha and accumulation of .w)
+__device__ __forceinline__ float msr_alpha(const Volume& vol, float ts, uint2 raw) {
+    const float dt = unwarp_dt(warp_dt(calc_dt(ts, vol.ss)));
+    const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
+    return 1.f - sng_expf(-sng_expf(s) * dt);
+}
+
+// every alive ray marched K iterations of S samples ahead (spec_generate_kernel's flattened loop and t reset
+// with S in place of 8, one look-ahead for every ray)
+template <bool LIN, int THREADS = 256>
+__global__ __launch_bounds__(THREADS) void msr_generate_kernel(MsrArgs a) {
+    __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
+    MarchCtrl* ctrl = a.ctrl;
+    const int p = a.p;
+    const uint32_t n_alive = ctrl->n_alive[p];
+    const uint32_t n_sched = a.sched.global ? ctrl->sched_alive[p] : n_alive;
+    uint32_t S, K;
+    msr_shape(ctrl, n_sched, ctrl->i_step[p], a.target, a.budget, a.kmax, S, K);
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) { ctrl->msr_S[p] = S; ctrl->msr_K[p] = K; }
+        if (threadIdx.x < 4 * MSR_KMAX) a.hist[threadIdx.x] = 0u;
+    }
+    if (K == 0 || blockIdx.x * THREADS >= n_alive) return;
+    const Volume& vol = a.vol;
+    const int lane = threadIdx.x & 63;
+    const f3 wdiag = vol.train_aabb.hi - vol.train_aabb.lo;
+    const f3 rwdiag = mk(recip_rn(wdiag.x), recip_rn(wdiag.y), recip_rn(wdiag.z));
+    const StepSpace cone = LIN ? step_space(0.0f) : vol.ss;
+    const float qnan = __int_as_float(0x7fc00000);
+    for (uint32_t blk = blockIdx.x * THREADS; blk < n_alive; blk += gridDim.x * THREADS) {
+        const uint32_t i = blk + threadIdx.x;
+        uint32_t tot = 0, nnet = 0, n_it = 0, cnt_last = 0, rbits = 0;
+        f3 o = splat(0.0f), d = splat(1.0f);
+        if (i < n_alive) {
+            const float4 ot = a.in.o_t[i], di = a.in.d_idx[i];
+            o = mk(ot.x, ot.y, ot.z);
+            d = mk(di.x, di.y, di.z);
+            const f3 idir = inv(d);
+            const float dfw = dot(a.cam.c2, d);
+            const float rdfw = recip_rn(dfw);
+            float t = ot.w;
+            float prev = a.in.lt[i].x;   // the previous iteration's last sample (the boundary-sample cache)
+            OccCache oc;
+            float* tb = a.tbuf + i;
+            uint32_t cnt = 0, it = 0;
+            float first = qnan, tl = 0.0f;
+            const f3 hs = half_sign(d);
+            bool going = true;
+#pragma unroll 1
+            while (going) {
+                bool sample = false, stop = false;
+                if constexpr (LIN) {
+                    const f3 pos = o + d * t;
+                    if (t >= MAX_DEPTH || !aabb_contains(vol.render_aabb, to_local(vol, pos))) {
+                        stop = true;
+                    } else {
+                        if (occupied_linear_c(pos, vol.occ_linear, oc)) sample = true;
+                        else t = dda_step_linear(t, pos, idir, hs);
+                    }
+                } else {
+                    if (occ_step(t, cone, o, d, idir, 0, vol.max_mip, vol)) {
+                        if (t >= MAX_DEPTH) stop = true;
+                        else sample = true;
+                    }
+                }
+                if (sample) {
+                    *tb = t;
+                    tb += n_alive;
+                    if (cnt == 0) first = t;
+                    tl = t;
+                    t += LIN ? calc_dt(t, 0.0f) : calc_dt(t, cone);
+                    ++cnt;
+                }
+                if (stop || cnt == S) {   // the iteration's samples are complete
+                    const uint32_t ru = (cnt > 0 && first == prev) ? 1u : 0u;
+                    rbits |= ru << it;
+                    tot += cnt;
+                    nnet += cnt - ru;
+                    ++n_it;
+                    cnt_last = cnt;
+                    if (cnt < S || it + 1 == K) {
+                        going = false;   // the ray ends in this iteration, or the round's look-ahead does
+                    } else {
+                        prev = tl;       // the compositor's t reset (574) on the iteration's last sample
+                        const f3 q = (o + d * tl) - vol.train_aabb.lo;
+                        const f3 wp = mk(div_by(q.x, wdiag.x, rwdiag.x), div_by(q.y, wdiag.y, rwdiag.y), div_by(q.z, wdiag.z, rwdiag.z));
+                        const f3 pos = vol.train_aabb.lo + wp * wdiag;
+                        t = div_by(dot(a.cam.c2, pos - a.cam.c3), dfw, rdfw);
+                        ++it;
+                        cnt = 0;
+                        first = qnan;
+                    }
+                }
+            }
+        }
+        const uint32_t base = block_append<THREADS / 64>(&ctrl->n_samples[p], nnet, nullptr, false, nullptr, false, sh_app, lane);
+        if (i < n_alive) {
+            a.samp[i] = make_uint2(base, n_it | (cnt_last << 5) | (rbits << 9));
+            const f3 wd = (d + 1.0f) * 0.5f;
+            uint32_t q = base, jx = 0, itx = 0;
+#pragma unroll 1
+            for (uint32_t x = 0; x < tot; ++x) {
+                if (!(jx == 0 && ((rbits >> itx) & 1u))) {   // a cached boundary sample needs no evaluation
+                    const float ts = a.tbuf[(size_t)x * n_alive + i];
+                    const f3 wp = ((o + d * ts) - vol.train_aabb.lo) / wdiag;
+                    float* c = a.coords + (size_t)q * 7;
+                    c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(LIN ? calc_dt(ts, 0.0f) : calc_dt(ts, cone)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+                    ++q;
+                }
+                if (++jx == S) { jx = 0; ++itx; }
+            }
+        }
+    }
+}
+
+// the iteration each ray ends in (opacity, the march's end, or MARCH_ITER's drop), from the opacity chain alone
+template <int THREADS = 256>
+__global__ __launch_bounds__(THREADS) void msr_count_kernel(MsrArgs a) {
+    __shared__ uint32_t h[4 * MSR_KMAX];
+    MarchCtrl* ctrl = a.ctrl;
+    const int p = a.p;
+    const uint32_t K = ctrl->msr_K[p];
+    if (K == 0) return;
+    const uint32_t S = ctrl->msr_S[p], istep0 = ctrl->i_step[p], n_alive = ctrl->n_alive[p];
+    if (threadIdx.x < 4 * MSR_KMAX) h[threadIdx.x] = 0u;
+    __syncthreads();
+    const Volume& vol = a.vol;
+    const float opaque = 1.0f - vol.min_transmittance;
+    for (uint32_t i = blockIdx.x * THREADS + threadIdx.x; i < n_alive; i += gridDim.x * THREADS) {
+        float w = a.in.rgba[i].w;
+        uint2 lraw = a.in.lo[i];
+        const uint32_t idx = __float_as_uint(a.in.d_idx[i].w);
+        const bool own = !a.sched.global || (idx >= a.sched.own_lo && idx < a.sched.own_hi);
+        const uint2 sc = a.samp[i];
+        const uint32_t n_it = sc.y & 31u, cnt_last = (sc.y >> 5) & 15u, rbits = sc.y >> 9;
+        uint32_t ob = sc.x, s = 0, e = K;
+        for (uint32_t it = 0; it < n_it; ++it) {
+            const uint32_t cnt = it + 1 == n_it ? cnt_last : S;
+            const uint32_t ru = (rbits >> it) & 1u;
+            atomicAdd(&h[2 * MSR_KMAX + it], cnt);
+            if (ru) atomicAdd(&h[3 * MSR_KMAX + it], 1u);
+            const bool last = istep0 + S * it + S >= MARCH_ITER;
+            // the iteration's t's and outputs loaded together, ahead of the opacity chain
+            float tv[MAX_STEPS_BETWEEN_COMPACTION];
+            uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
+#pragma unroll
+            for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
+                if (q < cnt) {
+                    tv[q] = a.tbuf[(size_t)(s + q) * n_alive + i];
+                    rv[q] = (ru && q == 0) ? lraw : a.net_out[ob + q - ru];
+                }
+            }
+            uint32_t j = cnt;
+#pragma unroll
+            for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
+                if (q >= cnt) break;
+                const float T = 1.f - w;
+                w += msr_alpha(vol, tv[q], rv[q]) * T;
+                if (w > opaque) { j = q; break; }
+            }
+            if (j < S || last) { e = it; break; }
+            lraw = rv[cnt - 1];   // the next iteration's boundary sample (S >= 2: never the reused one)
+            ob += cnt - ru;
+            s += cnt;
+        }
+        if (e < K) {
+            atomicAdd(&h[e], 1u);
+            if (own) atomicAdd(&h[MSR_KMAX + e], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 * MSR_KMAX && h[threadIdx.x]) atomicAdd(&a.hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// J = the first relative iteration whose frame-wide alive count is 0 or does not take S steps (or whose i
+// reaches MARCH_ITER); the per-iteration statistics of the committed ones as generate / composite record them
+__global__ void msr_schedule_kernel(MsrArgs a) {
+    MarchCtrl* c = a.ctrl;
+    const int p = a.p;
+    const uint32_t K = c->msr_K[p];
+    if (K == 0 || threadIdx.x != 0) return;
+    const uint32_t S = c->msr_S[p], istep0 = c->i_step[p], k = c->n_iter;
+    const uint32_t* deaths_l = a.hist;
+    const uint32_t* deaths_s = a.sched.global ? a.hist + MSR_KMAX : a.hist;
+    uint32_t alive_s = a.sched.global ? c->sched_alive[p] : c->n_alive[p], alive_l = c->n_alive[p];
+    uint32_t J = K;
+    unsigned long long slots = 0, samp = 0, reused = 0;
+    for (uint32_t m = 0; m < K; ++m) {
+        if (alive_s == 0 || steps_for(alive_s, a.target) != S || istep0 + S * m >= MARCH_ITER) { J = m; break; }
+        const uint32_t sm = a.hist[2 * MSR_KMAX + m], rm = a.hist[3 * MSR_KMAX + m];
+        slots += ((unsigned long long)alive_l * S + 255ull) / 256ull * 256ull;
+        samp += sm;
+        reused += rm;
+        if (k + m < 64) { c->alive_hist[k + m] = alive_l; c->steps_hist[k + m] = S; c->samples_hist[k + m] = sm; }
+        if (c->log && k + m < MARCH_LOG_CAP) { c->log[3 * (k + m)] = alive_l; c->log[3 * (k + m) + 1] = S; c->log[3 * (k + m) + 2] = sm; }
+        if (k + m < TAIL_LIVE_CAP) c->sched_hint[k + m] = (uint8_t)S;
+        alive_s -= deaths_s[m];
+        alive_l -= deaths_l[m];
+    }
+    if (J < K && k + J < TAIL_LIVE_CAP && alive_s > 0) c->sched_hint[k + J] = (uint8_t)steps_for(alive_s, a.target);
+    c->msr_J = J;
+    c->ref_slots += slots;
+    c->total_samples += samp;
+    c->reused_samples += reused;
+    c->net_samples += c->n_samples[p];
+    c->msr_evals += c->n_samples[p];
+    c->msr_exec += samp - reused;
+    c->n_iter = k + J;
+    c->i_step[p ^ 1] = istep0 + S * J;
+    c->n_alive[p ^ 1] = 0;
+    c->n_owned[p ^ 1] = 0;
+    c->n_samples[p ^ 1] = 0;
+    c->n_reused[p ^ 1] = 0;
+}
+
+// the first J iterations replayed with composite_kernel's arithmetic: rays ending before k + J are extracted
+// (extract_from_payload), the others appended to buffer p ^ 1 with their state and boundary-sample cache at k + J
+template <int THREADS = 256>
+__global__ __launch_bounds__(THREADS) void msr_commit_kernel(MsrArgs a) {
+    __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
+    MarchCtrl* ctrl = a.ctrl;
+    const int p = a.p;
+    const uint32_t K = ctrl->msr_K[p];
+    if (K == 0) return;
+    const uint32_t S = ctrl->msr_S[p], J = ctrl->msr_J, istep0 = ctrl->i_step[p], n_alive = ctrl->n_alive[p];
+    const Volume& vol = a.vol;
+    const CamDev& cam = a.cam;
+    const TraceMode mode{0, 1, 1.0f, 0, 0.0f};   // trace_alt
+    const int lane = threadIdx.x & 63;
+    const f3 diag = vol.train_aabb.hi - vol.train_aabb.lo;
+    uint32_t my_hits = 0;
+    for (uint32_t blk = blockIdx.x * THREADS; blk < n_alive; blk += gridDim.x * THREADS) {
+        const uint32_t i = blk + threadIdx.x;
+        bool survive = false, hit = false;
+        float4 rgba = make_float4(0, 0, 0, 0), ot = rgba, di = rgba;
+        float depth = 0.0f, mw = 0.0f, lt = 0.0f;
+        uint2 lraw = make_uint2(0u, 0u);
+        if (i < n_alive) {
+            rgba = a.in.rgba[i];
+            depth = a.in.depth[i];
+            ot = a.in.o_t[i];
+            di = a.in.d_idx[i];
+            lt = a.in.lt[i].x;
+            lraw = a.in.lo[i];
+            const f3 o = mk(ot.x, ot.y, ot.z), d = mk(di.x, di.y, di.z);
+            const uint2 sc = a.samp[i];
+            const uint32_t n_it = sc.y & 31u, cnt_last = (sc.y >> 5) & 15u, rbits = sc.y >> 9;
+            uint32_t ob = sc.x, s = 0;
+            bool ended = false;
+            const uint32_t n_run = n_it < J ? n_it : J;
+            for (uint32_t it = 0; it < n_run && !ended; ++it) {
+                const uint32_t cnt = it + 1 == n_it ? cnt_last : S;
+                const uint32_t ru = (rbits >> it) & 1u;
+                const bool last = istep0 + S * it + S >= MARCH_ITER;
+                float tv[MAX_STEPS_BETWEEN_COMPACTION];
+                uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
+#pragma unroll
+                for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
+                    if (q < cnt) {
+                        tv[q] = a.tbuf[(size_t)(s + q) * n_alive + i];
+                        rv[q] = (ru && q == 0) ? lraw : a.net_out[ob + q - ru];
+                    }
+                }
+                uint32_t j = cnt;
+                float tq = 0.0f;
+                uint2 rq = lraw;
+#pragma unroll
+                for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
+                    if (q >= cnt) break;
+                    tq = tv[q];
+                    rq = rv[q];
+                    if (spec_composite_sample(vol, cam, mode, o, d, diag, tq, rq, rgba, depth, mw)) { j = q; break; }
+                }
+                ot.w = depth / dot(cam.c2, d);   // payload.t reset (574)
+                if (j < S) {
+                    hit = !last && rgba.w > 0.001f;
+                    ended = true;
+                } else if (last) {
+                    ended = true;
+                } else {
+                    lt = tq;     // the boundary-sample cache of the next iteration: this one's last sample
+                    lraw = rq;
+                    ob += cnt - ru;
+                    s += cnt;
+                }
+            }
+            survive = !ended;
+        }
+        const uint32_t own_idx = __float_as_uint(di.w);
+        const uint32_t slot = block_append<THREADS / 64>(&ctrl->n_alive[p ^ 1], survive ? 1u : 0u, a.sched.global ? &ctrl->n_owned[p ^ 1] : nullptr,
+                                                         survive && own_idx >= a.sched.own_lo && own_idx < a.sched.own_hi, nullptr, false, sh_app, lane);
+        if (survive) {
+            a.out.o_t[slot] = ot;
+            a.out.d_idx[slot] = di;
+            a.out.rgba[slot] = rgba;
+            a.out.depth[slot] = depth;
+            a.out.lt[slot] = make_float2(lt, 0.0f);
+            a.out.lo[slot] = lraw;
+        }
+        if (hit) {   // extract_from_payload (1578-1612)
+            ++my_hits;
+            const uint32_t idx = own_idx;
+            const f3 dir = mk(di.x, di.y, di.z);
+            const f3 orig = cam.c3 + dir * ot.w;
+            float4 fb = a.frame_rgba[idx];
+            const float ta = rgba.w;
+            const float r = srgb_to_linear(rgba.x), g = srgb_to_linear(rgba.y), b = srgb_to_linear(rgba.z);
+            fb = make_float4(r + fb.x * (1.0f - ta), g + fb.y * (1.0f - ta), b + fb.z * (1.0f - ta), ta + fb.w * (1.0f - ta));
+            a.frame_rgba[idx] = fb;
+            a.positions[3 * idx + 0] = orig.x; a.positions[3 * idx + 1] = orig.y; a.positions[3 * idx + 2] = orig.z;
+            if (ta > 0.2f) a.frame_depth[idx] = depth;
+        }
+    }
+    if (my_hits) atomicAdd(&ctrl->n_hit, my_hits);
 }
 
 // write_normals_to_buffer (1523-1576) for rows [row0,row1)
@@ -1122,7 +1483,7 @@ __global__ void occ_brick_fill_kernel(const uint32_t* __restrict__ occ, uint32_t
     blob[OCC_BRICK_HDR_WORDS + slot * 16u + k] = w;
 }
 
-__global__ void ctrl_init_kernel(MarchCtrl* c) {
+__global__ void ctrl_init_kernel(MarchCtrl* c, int32_t* tail_live, uint8_t* sched_hint, uint32_t* log) {
     if (threadIdx.x < 64) {   // the fused tail kernel accumulates into the histograms
         c->alive_hist[threadIdx.x] = 0; c->steps_hist[threadIdx.x] = 0; c->samples_hist[threadIdx.x] = 0;
     }
@@ -1138,12 +1499,50 @@ __global__ void ctrl_init_kernel(MarchCtrl* c) {
         c->spec_K[0] = 0; c->spec_K[1] = 0; c->spec_k0[0] = 0; c->spec_k0[1] = 0;
         c->spec_evals = 0; c->spec_exec = 0;
         c->spec_base_k = 0; c->spec_base_istep = 1; c->spec_kk_valid[0] = 0; c->spec_kk_valid[1] = 0; c->spec_ok = 1;
+        c->msr_S[0] = 0; c->msr_S[1] = 0; c->msr_K[0] = 0; c->msr_K[1] = 0; c->msr_J = 0; c->msr_evals = 0; c->msr_exec = 0;
+        c->log = log;
+        c->tail_live = tail_live;
+        c->sched_hint = sched_hint;
     }
 }
 
 // ---------------------------------------------------------------------------
 // host-side launchers
-void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s) { hipLaunchKernelGGL(ctrl_init_kernel, dim3(1), dim3(64), 0, s, ctrl); }
+void launch_ctrl_init(MarchCtrl* ctrl, int32_t* tail_live, uint8_t* sched_hint, hipStream_t s, uint32_t* log) {
+    if (log) (void)hipMemsetAsync(log, 0, MARCH_LOG_CAP * 12, s);
+    (void)hipMemsetAsync(tail_live, 0, TAIL_LIVE_CAP * 4, s);
+    hipLaunchKernelGGL(ctrl_init_kernel, dim3(1), dim3(64), 0, s, ctrl, tail_live, sched_hint, log);
+}
+// alive(k) = prefix sum of tail_live; the reference's slots of a tail iteration: n_alive(k) * 8 padded to 256
+__global__ __launch_bounds__(1024) void tail_slots_kernel(MarchCtrl* ctrl) {
+    constexpr uint32_t CH = TAIL_LIVE_CAP / 1024;
+    __shared__ int32_t ps[1024];
+    __shared__ unsigned long long total;
+    if (!ctrl->spec_ok) return;   // the tail did not run (tail_prepare)
+    const uint32_t tid = threadIdx.x;
+    const int32_t* live = ctrl->tail_live;
+    int32_t sum = 0;
+    for (uint32_t x = 0; x < CH; ++x) sum += live[tid * CH + x];
+    ps[tid] = sum;
+    if (tid == 0) total = 0;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const int32_t v = tid >= off ? ps[tid - off] : 0;
+        __syncthreads();
+        ps[tid] += v;
+        __syncthreads();
+    }
+    int32_t alive = ps[tid] - sum;
+    unsigned long long slots = 0;
+    for (uint32_t x = 0; x < CH; ++x) {
+        alive += live[tid * CH + x];
+        slots += ((unsigned long long)(uint32_t)alive * MAX_STEPS_BETWEEN_COMPACTION + 255ull) / 256ull * 256ull;
+    }
+    if (slots) atomicAdd(&total, slots);
+    __syncthreads();
+    if (tid == 0) ctrl->ref_slots += total;
+}
+void launch_tail_slots(MarchCtrl* ctrl, hipStream_t s) { hipLaunchKernelGGL(tail_slots_kernel, dim3(1), dim3(1024), 0, s, ctrl); }
 // ---------------------------------------------------------------------------
 void launch_init_rays(const NerfFrameArgs& a, const RayBuf& out, MarchCtrl* ctrl, float4* fb, float* depth, float* pos, float* nrm,
                       uint32_t n_cus, hipStream_t s) {
@@ -1181,6 +1580,13 @@ void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_composite_kernel<256>, dim3(blocks), dim3(256), 0, s, a);
 }
+void launch_msr_generate(const MsrArgs& a, uint32_t blocks, hipStream_t s) {
+    if (a.vol.linear) hipLaunchKernelGGL(HIP_KERNEL_NAME(msr_generate_kernel<true>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(HIP_KERNEL_NAME(msr_generate_kernel<false>), dim3(blocks), dim3(256), 0, s, a);
+}
+void launch_msr_count(const MsrArgs& a, uint32_t blocks, hipStream_t s) { hipLaunchKernelGGL(msr_count_kernel<256>, dim3(blocks), dim3(256), 0, s, a); }
+void launch_msr_schedule(const MsrArgs& a, hipStream_t s) { hipLaunchKernelGGL(msr_schedule_kernel, dim3(1), dim3(64), 0, s, a); }
+void launch_msr_commit(const MsrArgs& a, uint32_t blocks, hipStream_t s) { hipLaunchKernelGGL(msr_commit_kernel<256>, dim3(blocks), dim3(256), 0, s, a); }
 void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_prepare_kernel, dim3(blocks), dim3(256), 0, s, a);
 }

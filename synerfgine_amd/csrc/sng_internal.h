@@ -59,7 +59,20 @@ struct MarchCtrl {
     uint32_t spec_kk_valid[2];       // RayBuf::kk of buffer p holds per-ray iteration indices
     uint32_t spec_ok;                // tail_prepare: every later iteration takes 8 steps (else the tail kernels queued
                                      // ahead of that check leave every buffer untouched and the wavefront continues)
+    // multi-step speculative rounds (nerf.hip msr_*), per ping-pong buffer of the round's rays
+    uint32_t msr_S[2];               // steps every iteration of the round takes (0: the round is a no-op)
+    uint32_t msr_K[2];               // iterations the round marched ahead
+    uint32_t msr_J;                  // iterations the last round commits (msr_schedule)
+    unsigned long long msr_evals;    // samples the rounds' network launches evaluated
+    unsigned long long msr_exec;     // ... of which the wavefront would have evaluated (the committed iterations')
+    int32_t* tail_live;              // [TAIL_LIVE_CAP] the tail's alive rays per iteration as a difference array (+1 where a
+                                     //   ray enters the tail's bookkeeping, -1 after its last iteration): reference slots
+    uint8_t* sched_hint;             // [TAIL_LIVE_CAP] steps of every iteration of the last frame (0: unknown), written by the
+                                     //   wavefront, one-step and msr schedules; sizes the msr rounds (exact for any value)
+    uint32_t* log;                   // diagnostics (param march_log): [MARCH_LOG_CAP][3] {alive, steps, samples} per iteration
 };
+constexpr uint32_t MARCH_LOG_CAP = 2048;
+constexpr uint32_t TAIL_LIVE_CAP = 10240;   // > MARCH_ITER: iterations a frame can have
 
 // Alive-ray SoA buffer (NerfPayload + rgba + depth, nerf_device.cuh:145-153; nerf.h:22-42)
 struct RayBuf {
@@ -75,6 +88,20 @@ struct RayBuf {
     uint32_t* kk;      // speculative tail: the ray's next iteration index (rays of one buffer may differ once the
                        // rounds look ahead per ray; MarchCtrl::spec_kk_valid says whether this buffer's are set)
 };
+
+// atomicAdd(&arr[key], v) from every lane with on == true, as one atomic per distinct key of the wave (same-address
+// atomics from many lanes serialise).  v is the same on every lane; call with the whole wave converged.
+__device__ __forceinline__ void wave_add_keyed(int32_t* arr, uint32_t key, int32_t v, bool on) {
+    const int lane = (int)(threadIdx.x & 63u);
+    unsigned long long pend = __ballot(on);
+    while (pend) {
+        const int leader = __ffsll((long long)pend) - 1;
+        const uint32_t lk = __shfl(key, leader, 64);
+        const unsigned long long m = pend & __ballot(key == lk);
+        if (lane == leader) atomicAdd(&arr[lk], (int32_t)__popcll(m) * v);
+        pend &= ~m;
+    }
+}
 
 // n_steps_between_compaction = clamp(target / n_alive, 1, 8) (testbed_nerf.cu:2189-2190)
 SNG_HD uint32_t steps_for(uint32_t n_alive, uint32_t target) {
@@ -297,10 +324,44 @@ struct SpecArgs {
     float* positions;
     float4* pre;                  // per network sample: {logistic r, g, b, alpha} (spec_prepare; nullptr: the compositor
     float* pre_depth;             //   activates the raw outputs itself) and dot(fwd, pos - cam)
-    uint8_t* hint;                // per NeRF pixel: 1 + the iteration its ray ended at in the last frame (0: unknown);
+    uint8_t* hint;                // per NeRF pixel: 1 + the iteration its ray ended at in the last frame, counted from the
+                                  // tail's first iteration (0: unknown);
                                   // a ray looks ahead just that far (exact whatever the hint: it only sizes the round)
 };
 constexpr uint32_t SPEC_KMAX = 16;
+
+// nerf.hip: multi-step speculative rounds.  While n_steps = clamp(target / n_alive, 1, 8) is in [2, 7]
+// (between the one-step regime and the 8-step tail) every alive ray of a round is at the same iteration
+// k.  A round guesses that iterations k .. k + K - 1 all take S = steps_for(n_alive(k)) steps and
+// marches every ray that far ahead (the positions depend on the march and the t reset only); ONE
+// network launch evaluates the samples; msr_count replays the opacity of every ray and histograms the
+// iteration it ends in; msr_schedule forms the frame-wide alive count of each iteration from it and
+// commits J = the first iteration whose step count is not S (J >= 1); msr_commit replays the first J
+// iterations exactly as composite_kernel does.
+constexpr uint32_t MSR_KMAX = 16;
+struct MsrArgs {
+    Volume vol;
+    CamDev cam;
+    Sched sched;
+    RayBuf in, out;               // alive rays at k (buffer p) -> alive at k + J (buffer p ^ 1)
+    MarchCtrl* ctrl;
+    int p;
+    uint32_t target;
+    uint32_t budget;              // samples one round may generate: K = clamp(budget / (S n_sched), 1, kmax)
+    uint32_t kmax;                // <= MSR_KMAX
+    float* coords;                // NerfCoordinate AoS of the network samples
+    uint2* samp;                  // per ray: {first network sample, n_it | cnt_last << 5 | reuse bits << 9}
+    float* tbuf;                  // [sample j of the ray][ray] march t of every sample
+    const uint2* net_out;         // [n][4] fp16
+    uint32_t* hist;               // [4][MSR_KMAX]: deaths (band), deaths (own rows; summed over ranks), samples, reused
+    float4* frame_rgba;
+    float* frame_depth;
+    float* positions;
+};
+void launch_msr_generate(const MsrArgs& a, uint32_t blocks, hipStream_t s);
+void launch_msr_count(const MsrArgs& a, uint32_t blocks, hipStream_t s);
+void launch_msr_schedule(const MsrArgs& a, hipStream_t s);
+void launch_msr_commit(const MsrArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s);
@@ -317,7 +378,9 @@ void launch_composite(const Volume& v, const CamDev& cam, const TraceMode& mode,
 void launch_normals(int W, int H, int row0, int row1, const float* pos, float* nrm, hipStream_t s);
 void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid_f32, double* partial, float* mean, uint8_t* bf, uint32_t* occ_linear,
                      hipStream_t s);
-void launch_ctrl_init(MarchCtrl* ctrl, hipStream_t s);
+void launch_ctrl_init(MarchCtrl* ctrl, int32_t* tail_live, uint8_t* sched_hint, hipStream_t s, uint32_t* log = nullptr);
+// reference slots of the tail's iterations (sum over k of n_alive(k) * 8 padded to 256) from MarchCtrl::tail_live
+void launch_tail_slots(MarchCtrl* ctrl, hipStream_t s);
 // OccBrick blob (sng_math.h) of the linear occupancy; flags: 4096 u32 scratch, blob: OCC_BRICK_CAP_WORDS, n_bricks: 1 u32
 void launch_occ_brick(const uint32_t* occ_linear, uint32_t* flags, uint32_t* blob, uint32_t* n_bricks, hipStream_t s);
 // mesh.hip

@@ -614,6 +614,51 @@ def test_onestep_regime_equals_wavefront(config, w, h, target, shade, horizon):
         tb.close()
 
 
+@pytest.mark.parametrize("config,w,h,target,shade,extra", [
+    ("c4", 1920, 1080, 0, False, {}),                                   # the real regime: 78 iterations of 2..8 steps after the one-step one
+    ("c4", 1920, 1080, 0, False, {"nerf_msr_kmax": 3}),                 # short rounds
+    ("c4", 160, 90, 1 << 15, True, {}),                                 # 2..7 steps from the first chunk, shadows + mesh
+    ("c4", 160, 90, 1 << 15, False, {"nerf_msr_budget": 4096}),         # K = 1 from the budget
+    ("c4", 96, 54, 1 << 13, False, {"nerf_fused": 0}),                  # rounds down to the last ray (no tail)
+    ("c3", 160, 90, 1 << 12, False, {}),                                # the linear lego-like marcher
+    ("c3", 160, 90, 1 << 12, False, {"nerf_msr_kmax": 16, "nerf_onestep": 0}),
+])
+def test_msr_rounds_equal_wavefront(config, w, h, target, shade, extra):
+    """nerf.hip's multi-step speculative rounds (while n_steps is 2..7: every ray marched K iterations of S steps
+    ahead, one network launch, the opacity replay's death histogram, the committed prefix of iterations whose
+    step count was S, the exact replay of that prefix) reproduce the per-iteration wavefront bit for bit: frame
+    buffers, hit / sample / reused counts, reference slots and the per-iteration histograms."""
+    ov = {} if shade else {"show_virtual_obj": 0, "shadow_on_nerf": 0}
+    tb, eng, _ = _engine(w, h, ov, config)
+    try:
+        n0, m0 = eng.rng_states(0).copy(), eng.rng_states(1).copy()
+        out = {}
+        # on = 2: the same frame again, its rounds sized by the first one's schedule (MarchCtrl::sched_hint);
+        # on = 3: after a frame at another query target, whose schedule is the wrong hint
+        for on in (0, 1, 2, 3):
+            if on == 3:
+                eng.frame(target_n_queries=(target or (1 << 21)) // 2 * 3)
+            eng.set_rng_states(0, n0)
+            eng.set_rng_states(1, m0)
+            eng.set_param("nerf_msr", min(on, 1))
+            for k, v in extra.items():
+                eng.set_param(k, v)
+            r = eng.frame(target_n_queries=target)
+            if on:
+                assert r.msr_rounds >= 1 and r.msr_evals >= r.msr_exec > 0, (r.msr_rounds, r.msr_evals, r.msr_exec)
+            else:
+                assert r.msr_rounds == 0
+            out[on] = ([r.download(b) for b in ("final_rgba", "nerf_rgba", "nerf_depth", "nerf_positions")],
+                       (r.n_samples, r.n_samples_reused, r.n_hit, r.n_iterations, r.n_reference_slots), list(r.alive_per_iter),
+                       list(r.steps_per_iter), list(r.samples_per_iter))
+        for on in (1, 2, 3):
+            for a, b in zip(out[0][0], out[on][0]):
+                assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), on
+            assert out[0][1:] == out[on][1:], on
+    finally:
+        tb.close()
+
+
 def test_rt_counting_frame_is_exact():
     """rt_count = 1 renders with the counting instantiations of the path and shadow-ray kernels: the frame is
     bit-identical to the timed kernels' and the traversal counters are filled (sng_rt_counters)."""
