@@ -324,14 +324,34 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
 //          ray buffer with their boundary-sample cache.
 constexpr int OS_P = 4;   // longest orbit closed (start t's remembered)
 
+// A wave's LDS: the closed-loop section's orbit entries and the field section's staging are used one
+// after the other in each trip (a wave's LDS operations execute in order), so they share the bytes.
+union OnestepWaveLds {
+    struct {
+        float4 cyc[OS_P][64];    // orbit entry: logistic rgb, alpha
+        float4 cycd[OS_P][64];   // orbit entry: depth, sample t, raw output (2 x u32)
+    } orbit;
+    struct {
+        float4 ray[64][2];
+        float s[64];
+        uint8_t own[64];
+        uint2 out[64];
+    } field;
+};
+
+// The regime evaluates the field for few samples (the march and the closed loops are the work), so
+// the weight fragments live in LDS, not in 80 VGPRs: 3 waves per SIMD instead of 2 (LDS: 3 workgroups
+// x (20 KiB weights + 4 x 8 KiB) per CU).
 template <int F, bool FINAL>
-__global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
-    __shared__ float4 ray_lds[FUSED_WAVES][64][2];
-    __shared__ float s_lds[FUSED_WAVES][64];
-    __shared__ uint8_t own_lds[FUSED_WAVES][64];
-    __shared__ uint2 out_lds[FUSED_WAVES][64];
-    __shared__ float4 cyc_lds[FUSED_WAVES][OS_P][64];   // orbit entry: logistic rgb, alpha
-    __shared__ float4 cycd_lds[FUSED_WAVES][OS_P][64];  // orbit entry: depth, sample t, raw output (2 x u32)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void nerf_onestep_kernel(OnestepArgs a) {
+    __shared__ OnestepWaveLds wl[FUSED_WAVES];
+    __shared__ h8 sW[20 * 64];
+#define ray_lds(w, l, k) wl[w].field.ray[l][k]
+#define s_lds(w, l) wl[w].field.s[l]
+#define own_lds(w, l) wl[w].field.own[l]
+#define out_lds(w, l) wl[w].field.out[l]
+#define cyc_lds(w, q, l) wl[w].orbit.cyc[q][l]
+#define cycd_lds(w, q, l) wl[w].orbit.cycd[q][l]
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int g = lane >> 4, col = lane & 15;
@@ -346,9 +366,9 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
     const float opaque = 1.0f - vol.min_transmittance;
     const h8* wfrag = reinterpret_cast<const h8*>(a.wfrag);
     const _Float16* grid = reinterpret_cast<const _Float16*>(a.grid_params);
-    h8 W[20];
-#pragma unroll
-    for (int f = 0; f < 20; ++f) W[f] = wfrag[f * 64 + lane];
+    for (int k = threadIdx.x; k < 20 * 64; k += blockDim.x) sW[k] = wfrag[k];
+    __syncthreads();
+    const LdsWeights W{sW, lane};
     const float qnan = __int_as_float(0x7fc00000);
 
     bool has = false, own = true;
@@ -437,8 +457,8 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
                             const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
                             const float alpha = 1.f - sng_expf(-sng_expf(s) * dt);
                             all_zero = all_zero && alpha == 0.0f;
-                            cyc_lds[wv][q][lane] = make_float4(logistic(r), logistic(gg), logistic(b), alpha);
-                            cycd_lds[wv][q][lane] = make_float4(dot(cam.c2, pos - cam.c3), sq, __uint_as_float(raw.x), __uint_as_float(raw.y));
+                            cyc_lds(wv, q, lane) = make_float4(logistic(r), logistic(gg), logistic(b), alpha);
+                            cycd_lds(wv, q, lane) = make_float4(dot(cam.c2, pos - cam.c3), sq, __uint_as_float(raw.x), __uint_as_float(raw.y));
                         }
                     }
                     const float dfw = dot(cam.c2, d);
@@ -447,7 +467,7 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
                         // weights are exactly 0: rgba never changes, depth is the last composited sample's
                         if (FINAL) {
                             q = (limit - 1u - m) % (uint32_t)P;
-                            depth = cycd_lds[wv][q][lane].x;
+                            depth = cycd_lds(wv, q, lane).x;
                             t = depth / dfw;
                             survivor = istep0 + limit < MARCH_ITER;   // else dropped in MARCH_ITER's last iteration
                         }
@@ -459,7 +479,7 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
                                 survivor = FINAL;
                                 break;
                             }
-                            const float4 cq = cyc_lds[wv][q][lane];
+                            const float4 cq = cyc_lds(wv, q, lane);
                             const bool last = istep0 + x + 1u >= MARCH_ITER;
                             const float T = 1.f - rgba.w;
                             const float weight = cq.w * T;
@@ -473,7 +493,7 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
                                 if (FINAL) {
                                     const float aa = rgba.w;
                                     rgba.x /= aa; rgba.y /= aa; rgba.z /= aa; rgba.w /= aa;
-                                    depth = cycd_lds[wv][q][lane].x;
+                                    depth = cycd_lds(wv, q, lane).x;
                                     t = depth / dfw;
                                     if (!last) extract();
                                 } else {
@@ -496,13 +516,13 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
                         if (FINAL && survivor) {
                             // alive at k + J: the last composited sample is the orbit entry before q
                             const uint32_t ql = q == 0 ? (uint32_t)P - 1u : q - 1u;
-                            depth = cycd_lds[wv][ql][lane].x;
+                            depth = cycd_lds(wv, ql, lane).x;
                             t = depth / dfw;
                         }
                     }
                     if (FINAL && survivor) {
                         const uint32_t ql = (limit - 1u - m) % (uint32_t)P;
-                        const float4 e = cycd_lds[wv][ql][lane];
+                        const float4 e = cycd_lds(wv, ql, lane);
                         sc0 = e.y;
                         oc0 = make_uint2(__float_as_uint(e.z), __float_as_uint(e.w));
                     }
@@ -544,18 +564,18 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
             const uint32_t total = (uint32_t)__popcll(nb);
             const uint32_t slot = (uint32_t)__popcll(nb & ((1ull << lane) - 1ull));
             if (need) {
-                own_lds[wv][slot] = (uint8_t)lane;
-                s_lds[wv][lane] = s;
-                ray_lds[wv][lane][0] = make_float4(o.x, o.y, o.z, 0.0f);
-                ray_lds[wv][lane][1] = make_float4(d.x, d.y, d.z, 0.0f);
+                own_lds(wv, slot) = (uint8_t)lane;
+                s_lds(wv, lane) = s;
+                ray_lds(wv, lane, 0) = make_float4(o.x, o.y, o.z, 0.0f);
+                ray_lds(wv, lane, 1) = make_float4(d.x, d.y, d.z, 0.0f);
             }
             wave_sync();
             for (uint32_t tile = 0; tile * 16 < total; ++tile) {
                 const uint32_t q = tile * 16 + (uint32_t)col;
                 const bool valid = q < total;
-                const uint32_t ol = own_lds[wv][valid ? q : 0];
-                const float4 ro = ray_lds[wv][ol][0], rd = ray_lds[wv][ol][1];
-                const float ts = s_lds[wv][ol];
+                const uint32_t ol = own_lds(wv, valid ? q : 0);
+                const float4 ro = ray_lds(wv, ol, 0), rd = ray_lds(wv, ol, 1);
+                const float ts = s_lds(wv, ol);
                 const f3 so = mk(ro.x, ro.y, ro.z), sd = mk(rd.x, rd.y, rd.z);
                 const f3 wp = ((so + sd * ts) - vol.train_aabb.lo) / wdiag;
                 const f3 wd = (sd + 1.0f) * 0.5f;
@@ -563,12 +583,12 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
                 field_tile<F>(W, a.levels, grid, g, wp.x, wp.y, wp.z, wd.x, wd.y, wd.z, fo, dens);
                 if (valid && g == 0) {
                     const _Float16 r = (_Float16)fo[0], gg = (_Float16)fo[1], b = (_Float16)fo[2], sg = (_Float16)dens[0];
-                    out_lds[wv][q] = make_uint2((uint32_t)__builtin_bit_cast(uint16_t, r) | ((uint32_t)__builtin_bit_cast(uint16_t, gg) << 16),
+                    out_lds(wv, q) = make_uint2((uint32_t)__builtin_bit_cast(uint16_t, r) | ((uint32_t)__builtin_bit_cast(uint16_t, gg) << 16),
                                                 (uint32_t)__builtin_bit_cast(uint16_t, b) | ((uint32_t)__builtin_bit_cast(uint16_t, sg) << 16));
                 }
             }
             wave_sync();
-            if (need) { out = out_lds[wv][slot]; ++my_evals; }
+            if (need) { out = out_lds(wv, slot); ++my_evals; }
             wave_sync();
         }
         // ---- composite the stepped sample (composite_kernel_nerf_alt 535-574 with n_steps = 1)
@@ -644,6 +664,13 @@ __global__ __launch_bounds__(256) void nerf_onestep_kernel(OnestepArgs a) {
         if (my_evals) atomicAdd(&a.ctrl->reused_samples, (unsigned long long)(-(long long)my_evals));
     }
 }
+
+#undef ray_lds
+#undef s_lds
+#undef own_lds
+#undef out_lds
+#undef cyc_lds
+#undef cycd_lds
 
 __global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k, uint32_t horizon, int first) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ONESTEP_HIST; i += gridDim.x * blockDim.x) {
