@@ -342,6 +342,18 @@ union OnestepWaveLds {
 // The regime evaluates the field for few samples (the march and the closed loops are the work), so
 // the weight fragments live in LDS, not in 80 VGPRs: 3 waves per SIMD instead of 2 (LDS: 3 workgroups
 // x (20 KiB weights + 4 x 8 KiB) per CU).
+// True when a ray compositing (in float) samples of alpha <= amax from opacity w0 provably stays at or below
+// `opaque` for n more iterations.  One iteration is w' = fl(w + fl(a fl(1 - w))); with t = 1 - w and u = 2^-24,
+// t' >= t (1 - a (1 + u)^2) - (w + weight) u >= r t - 1.0001 u, so t_n >= r^n t_0 - 1.0001 n u; w passes
+// `opaque` only when t falls below 1 - opaque.  Evaluated in double with relative margins far above its error.
+__device__ __forceinline__ bool os_no_death(float w0, float amax, uint32_t n, float opaque) {
+    const double u = 5.9604644775390625e-08;
+    const double ar = (double)amax * (1.0 + 2.0 * u + u * u) * (1.0 + 1e-12);
+    if (!(ar < 0.5)) return false;
+    const double tn = (1.0 - (double)w0) * exp((double)n * log1p(-ar) * (1.0 + 1e-12)) * (1.0 - 1e-12) - 1.0001 * (double)n * u;
+    return tn > (1.0 - (double)opaque) * (1.0 + 1e-9) + 1e-15;
+}
+
 template <int F, bool FINAL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void nerf_onestep_kernel(OnestepArgs a) {
     __shared__ OnestepWaveLds wl[FUSED_WAVES];
@@ -442,6 +454,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
                 if (P) {
                     // orbit entry q (0..P-1) = the sample of iteration m - P + q, used at m + q, m + q + P, ...
                     bool all_zero = true;
+                    float amax = 0.0f;   // the orbit's largest alpha
 #pragma unroll
                     for (int q = 0; q < OS_P; ++q) {
                         if (q < P) {
@@ -457,6 +470,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
                             const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y >> 16));
                             const float alpha = 1.f - sng_expf(-sng_expf(s) * dt);
                             all_zero = all_zero && alpha == 0.0f;
+                            amax = fmaxf(amax, alpha);
                             cyc_lds(wv, q, lane) = make_float4(logistic(r), logistic(gg), logistic(b), alpha);
                             cycd_lds(wv, q, lane) = make_float4(dot(cam.c2, pos - cam.c3), sq, __uint_as_float(raw.x), __uint_as_float(raw.y));
                         }
@@ -473,8 +487,62 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
                         }
                         // pass 0: never opaque; dropped at MARCH_ITER's last iteration, past every schedule decision
                     } else {
+                        uint32_t x0 = m;
+                        bool stuck = false;
+                        // iterations x < xnl are not the march's last (istep0 + x + 1 < MARCH_ITER) and inside the span
+                        const uint32_t xnl = min(limit, istep0 + 1u < MARCH_ITER ? MARCH_ITER - 1u - istep0 : 0u);
+                        if (!FINAL && xnl > m && os_no_death(rgba.w, amax, xnl - m, opaque)) {
+                            // pass 0 needs only the iteration the ray leaves at, and it provably passes no opacity
+                            // threshold before xnl: it is dropped at the march's last iteration, or alive at the span's end
+                            if (xnl < limit) record(xnl, false);
+                            stuck = true;
+                        } else if (P == 1) {
+                            // the orbit's one entry in registers: the iterations that neither pass the opacity
+                            // threshold nor are the march's last run here without LDS reads or bookkeeping; the
+                            // loop below takes over from the same state at the first one that does (the same float
+                            // operations in the same order, so the same values)
+                            const float4 c = cyc_lds(wv, 0, lane);
+                            float w = rgba.w, cr = rgba.x, cg = rgba.y, cb = rgba.z;
+                            // four iterations per check: the opacity never decreases (weights are >= 0), so the
+                            // fourth's <= threshold clears all four; a fixed point (w unchanged) persists, so the
+                            // fourth equal to the third catches one reached inside the block (pass 0 stops there)
+                            while (x0 + 4u <= xnl) {
+                                const float w1 = w + c.w * (1.f - w);
+                                const float w2 = w1 + c.w * (1.f - w1);
+                                const float w3 = w2 + c.w * (1.f - w2);
+                                const float k3 = c.w * (1.f - w3);
+                                const float w4 = w3 + k3;
+                                if (w4 > opaque) break;
+                                if (FINAL) {
+                                    const float k0 = c.w * (1.f - w), k1 = c.w * (1.f - w1), k2 = c.w * (1.f - w2);
+                                    cr += c.x * k0; cg += c.y * k0; cb += c.z * k0;
+                                    cr += c.x * k1; cg += c.y * k1; cb += c.z * k1;
+                                    cr += c.x * k2; cg += c.y * k2; cb += c.z * k2;
+                                    cr += c.x * k3; cg += c.y * k3; cb += c.z * k3;
+                                }
+                                x0 += 4u;
+                                const bool fixed = w4 == w3;
+                                w = w4;
+                                if (!FINAL && fixed) { stuck = true; break; }
+                            }
+                            for (; !stuck && x0 < xnl; ++x0) {
+                                const float weight = c.w * (1.f - w);
+                                const float wn = w + weight;
+                                if (wn > opaque) break;
+                                if (FINAL) {
+                                    cr += c.x * weight;
+                                    cg += c.y * weight;
+                                    cb += c.z * weight;
+                                } else if (wn == w) {   // opacity unchanged over the orbit: it never changes again
+                                    stuck = true;
+                                    break;
+                                }
+                                w = wn;
+                            }
+                            rgba = make_float4(cr, cg, cb, w);
+                        }
                         float wprev = rgba.w;
-                        for (uint32_t x = m;; ++x) {
+                        for (uint32_t x = x0; !stuck; ++x) {
                             if (x >= limit) {   // FINAL: alive at k + J
                                 survivor = FINAL;
                                 break;
@@ -763,6 +831,7 @@ void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(onestep_schedule_kernel, dim3(1), dim3(1024), 0, s, a);
 }
 void launch_onestep_pass(const OnestepArgs& a, const NetworkDev& net, int final_pass, uint32_t n_rays_hint, hipStream_t s) {
+
     const uint32_t waves = (n_rays_hint + 63) / 64;
     const uint32_t blocks = std::max(1u, std::min((waves + FUSED_WAVES - 1) / FUSED_WAVES, (uint32_t)net.n_cus * 8));
     if (net.F == 4) {
