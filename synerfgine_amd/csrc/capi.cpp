@@ -460,6 +460,7 @@ struct sng_ctx {
     DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
+    DevBuf shadow_scratch;                 // NeRF shadow pass: light samples + terms per neighbour slot (launch_shadows)
     DevBuf tail_live;                      // tail iterations' alive counts as a difference array (reference slots)
     DevBuf sched_hint;                     // steps of every iteration of the last frame (sizes the msr rounds)
     DevBuf msr_hist;                       // multi-step rounds: [4][MSR_KMAX] per-iteration deaths / samples
@@ -764,6 +765,13 @@ void upload_scene(sng_ctx* c) {
         mg.push_back({mk(m.ka[0], m.ka[1], m.ka[2]), mk(m.kd[0], m.kd[1], m.kd[2]), mk(m.ks[0], m.ks[1], m.ks[2]), m.n, m.rg, m.spec_angle, m.type});
     upload(c->d_mats, mg.data(), mg.size() * sizeof(MaterialGpu));
     c->scene_dirty = false;
+}
+
+// lights whose shadow term draws a light sample (Light::sample, type 0)
+int n_point_lights(const sng_ctx* c) {
+    int n = 0;
+    for (const auto& l : c->lights) n += l.type == 0 ? 1 : 0;
+    return n;
 }
 
 void load_scene(sng_ctx* c, const std::string& path) {
@@ -1685,8 +1693,10 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         sa.threshold = (float)c->p("nerf_on_nerf_shadow_threshold");
         sa.objs = c->d_objs.as<ObjectGpu>(); sa.n_objs = (int)c->objs.size();
         sa.lights = c->d_lights.as<LightGpu>(); sa.n_lights = (int)c->lights.size();
+        sa.n_point = n_point_lights(c);
+        c->shadow_scratch.ensure(shadow_scratch_bytes(sa));
         launch_shadows(sa, c->nerf_rgba.as<float4>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->rng_nerf.as<uint32_t>(), c->n_rng_nerf,
-                       c->s_nerf);
+                       c->shadow_scratch.p, c->s_nerf);
     } else if (shadows) {
         ShadowArgs sa{};
         sa.vol = vol;
@@ -1696,8 +1706,10 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         sa.threshold = (float)c->p("nerf_on_nerf_shadow_threshold");
         sa.objs = c->d_objs.as<ObjectGpu>(); sa.n_objs = 0;
         sa.lights = c->d_lights.as<LightGpu>(); sa.n_lights = (int)c->lights.size();
+        sa.n_point = n_point_lights(c);
+        c->shadow_scratch.ensure(shadow_scratch_bytes(sa));
         launch_shadows(sa, c->nerf_rgba.as<float4>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->rng_nerf.as<uint32_t>(), c->n_rng_nerf,
-                       c->s_nerf);
+                       c->shadow_scratch.p, c->s_nerf);
     }
     HIPCHK(hipEventRecord(c->ev_nerf1, c->s_nerf));
     // ---- overlay (RayTracer::overlay, raytracer.cu:372-392) after both streams

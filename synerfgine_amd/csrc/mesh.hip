@@ -416,15 +416,19 @@ __device__ __forceinline__ void xorwow_skip(Xorwow& r, uint32_t n) {
 // ---------------------------------------------------------------------------
 // shade_with_shadow (testbed_nerf.cu:1702-1786) / shadow_for_px (1614-1700)
 // ---------------------------------------------------------------------------
-// One neighbour's term of shade_with_shadow: shadow_for_px at (pos, nrm) with the pixel's XORWOW
-// state r (3 draws per point light).
+// One neighbour's term of shade_with_shadow: shadow_for_px at (pos, nrm); the k-th point light's sample
+// (Light::sample, 3 draws from the pixel's XORWOW state) is lp[k * lp_stride], drawn beforehand in the
+// reference's order by shadow_draw_kernel.
 template <bool LDS>
-__device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx<LDS>& cx, f3 pos, f3 nrm, Xorwow& r) {
+__device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx<LDS>& cx, f3 pos, f3 nrm, const float4* __restrict__ lp,
+                                             size_t lp_stride) {
     float overall = 1.0f;
+    int k = 0;
     for (int li = 0; li < a.n_lights; ++li) {
         const LightGpu L = a.lights[li];
         if (L.type == 0) {
-            const f3 lpos = light_sample(L, r);
+            const float4 l4 = lp[(size_t)k++ * lp_stride];
+            const f3 lpos = mk(l4.x, l4.y, l4.z);
             const f3 l = normalize(lpos - pos);
             const float full_d = length(lpos - pos);
             int hit = -1;
@@ -435,7 +439,7 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
             const float fd = length(lpos - src);
             const f3 Ld = normalize(lpos - src);
             const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip,
-                                                                   full_d <= fd ? full_d : __builtin_huge_valf()));
+                                                           full_d <= fd ? full_d : __builtin_huge_valf()));
             const double mask = (double)(nd * (1.0f - fminf(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)a.threshold));
             overall = (float)fmin((double)overall, mask);
         } else {
@@ -446,42 +450,75 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
     }
     return overall;
 }
-__device__ __forceinline__ void shadow_apply(const ShadowArgs& a, float4* __restrict__ rgba, size_t idx, float sum) {
+__device__ __forceinline__ f3 load_f3(const float* __restrict__ p, size_t i) { return mk(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
+
+// shade_with_shadow (testbed_nerf.cu:1702-1786) in three passes, so that the (2r+1)^2 neighbour terms of a
+// pixel -- independent once their light samples are drawn -- run on separate lanes (a thin band of rows
+// then still fills the GPU):
+//   shadow_draw_kernel    one lane per pixel: the pixel's XORWOW stream drawn in the reference's order
+//                         (neighbour slots row-major, lights in order, 3 draws per point light), the light
+//                         samples stored per (slot, point light), the state stored back;
+//   shadow_term_kernel    one lane per (slot, pixel): the slot's term (the mesh and NeRF depth tests);
+//   shadow_finish_kernel  one lane per pixel: the terms summed in slot order, / blend, ^ intensity, applied.
+// The same float operations in the same order as one lane looping over the neighbours, so the same bits.
+__device__ __forceinline__ bool shadow_slot(const ShadowArgs& a, uint32_t p, uint32_t slot, int& fx, int& fy) {
+    const int w = 2 * a.radius + 1;
+    const int x = (int)(p % (uint32_t)a.W), y = a.row0 + (int)(p / (uint32_t)a.W);
+    fx = x + (int)slot / w - a.radius;
+    fy = y + (int)slot % w - a.radius;
+    return fx >= 0 && fy >= 0 && fx < a.W && fy < a.H;
+}
+__global__ __launch_bounds__(256) void shadow_draw_kernel(ShadowArgs a, uint32_t n, uint32_t* __restrict__ rng, uint32_t n_rng, float4* __restrict__ lp) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const size_t idx = (size_t)(p % (uint32_t)a.W) + (size_t)a.W * (a.row0 + (int)(p / (uint32_t)a.W));
+    Xorwow r = load_rng(rng, n_rng, idx);
+    const uint32_t slots = (uint32_t)((2 * a.radius + 1) * (2 * a.radius + 1));
+    for (uint32_t sl = 0; sl < slots; ++sl) {
+        int fx, fy;
+        if (!shadow_slot(a, p, sl, fx, fy)) continue;
+        int k = 0;
+        for (int li = 0; li < a.n_lights; ++li) {
+            const LightGpu L = a.lights[li];
+            if (L.type != 0) continue;
+            const f3 q = light_sample(L, r);
+            lp[((size_t)sl * a.n_point + k++) * n + p] = make_float4(q.x, q.y, q.z, 0.0f);
+        }
+    }
+    store_rng(rng, n_rng, idx, r);
+}
+__global__ __launch_bounds__(TPB) void shadow_term_kernel(ShadowArgs a, uint32_t n, const float* __restrict__ positions, const float* __restrict__ normals,
+                                                          const float4* __restrict__ lp, float* __restrict__ terms) {
+    __shared__ int stack_lds[BVH_STACK * TPB];
+    const TraceCtx<false> cx{stack_lds + threadIdx.x, TPB, nullptr, 1};
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t sl = (uint32_t)(t / n), p = (uint32_t)(t % n);
+    if (sl >= (uint32_t)((2 * a.radius + 1) * (2 * a.radius + 1))) return;
+    int fx, fy;
+    if (!shadow_slot(a, p, sl, fx, fy)) return;
+    const size_t tid = (size_t)fy * a.W + fx;
+    terms[(size_t)sl * n + p] = shadow_term(a, cx, load_f3(positions, tid), load_f3(normals, tid), lp + (size_t)sl * a.n_point * n + p, n);
+}
+__global__ __launch_bounds__(256) void shadow_finish_kernel(ShadowArgs a, uint32_t n, const float* __restrict__ terms, float4* __restrict__ rgba) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t slots = (uint32_t)((2 * a.radius + 1) * (2 * a.radius + 1));
+    float sum = 0.0f;
+    int blend = 0;
+    for (uint32_t sl = 0; sl < slots; ++sl) {
+        int fx, fy;
+        if (!shadow_slot(a, p, sl, fx, fy)) continue;
+        sum += terms[(size_t)sl * n + p];
+        ++blend;
+    }
+    sum /= (float)blend;
     sum = pow_small_int(sum, a.intensity);
+    const size_t idx = (size_t)(p % (uint32_t)a.W) + (size_t)a.W * (a.row0 + (int)(p / (uint32_t)a.W));
     float4 c = rgba[idx];
     c.x = srgb_to_linear(c.x) * sum;
     c.y = srgb_to_linear(c.y) * sum;
     c.z = srgb_to_linear(c.z) * sum;
     rgba[idx] = c;
-}
-__device__ __forceinline__ f3 load_f3(const float* __restrict__ p, size_t i) { return mk(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
-
-// One lane per pixel, the neighbours in loop order.  (A form with a pixel's (2r+1)^2 neighbour terms on
-// separate lanes -- each lane skipping the pixel's XORWOW stream to its neighbour's draws -- was exact but
-// 16 % slower at C4's r = 2: the pass is VALU-bound, not latency-bound.)
-__global__ __launch_bounds__(TPB) void shade_shadow_kernel(ShadowArgs a, float4* __restrict__ rgba, const float* __restrict__ positions,
-                                                            const float* __restrict__ normals, uint32_t* __restrict__ rng, uint32_t n_rng) {
-    __shared__ int stack_lds[BVH_STACK * TPB];
-    const TraceCtx<false> cx{stack_lds + threadIdx.x, TPB, nullptr, 1};
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
-    if (t >= n) return;
-    const int x = (int)(t % (uint32_t)a.W), y = a.row0 + (int)(t / (uint32_t)a.W);
-    const size_t idx = (size_t)x + (size_t)a.W * y;
-    Xorwow r = load_rng(rng, n_rng, idx);
-    float sum = 0.0f;
-    int blend = 0;
-    for (int i = -a.radius; i <= a.radius; ++i)
-        for (int j = -a.radius; j <= a.radius; ++j) {
-            const int fx = x + i, fy = y + j;
-            if (fx < 0 || fy < 0 || fx >= a.W || fy >= a.H) continue;
-            const size_t tid = (size_t)fy * a.W + fx;
-            sum += shadow_term(a, cx, load_f3(positions, tid), load_f3(normals, tid), r);
-            ++blend;
-        }
-    sum /= (float)blend;
-    shadow_apply(a, rgba, idx, sum);
-    store_rng(rng, n_rng, idx, r);
 }
 
 // ---------------------------------------------------------------------------
@@ -930,10 +967,20 @@ __global__ void xorwow_init_kernel(uint32_t n, uint32_t seed_lo, uint32_t seed_h
 }
 
 // ---------------------------------------------------------------------------
-void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, hipStream_t s) {
+size_t shadow_scratch_bytes(const ShadowArgs& a) {
+    const size_t n = (size_t)(a.row1 - a.row0) * (size_t)a.W, slots = (size_t)(2 * a.radius + 1) * (size_t)(2 * a.radius + 1);
+    return slots * n * ((size_t)a.n_point * sizeof(float4) + sizeof(float));
+}
+void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, void* scratch, hipStream_t s) {
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
-    hipLaunchKernelGGL(shade_shadow_kernel, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, a, rgba, pos, nrm, rng, n_rng);
+    const size_t slots = (size_t)(2 * a.radius + 1) * (size_t)(2 * a.radius + 1);
+    float4* lp = static_cast<float4*>(scratch);
+    float* terms = reinterpret_cast<float*>(lp + slots * (size_t)a.n_point * n);
+    hipLaunchKernelGGL(shadow_draw_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, n, rng, n_rng, lp);
+    const size_t items = slots * n;
+    hipLaunchKernelGGL(shadow_term_kernel, dim3((uint32_t)((items + TPB - 1) / TPB)), dim3(TPB), 0, s, a, n, pos, nrm, lp, terms);
+    hipLaunchKernelGGL(shadow_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, n, terms, rgba);
 }
 void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
                       hipStream_t s) {

@@ -229,6 +229,7 @@ struct ShadowArgs {
     float threshold;            // nerf_on_nerf_shadow_threshold
     const ObjectGpu* objs; int n_objs;
     const LightGpu* lights; int n_lights;
+    int n_point;                // lights of type 0 (Light::sample draws)
 };
 
 // raytracer work counters (RaytraceArgs::work): [0] path-kernel tiles, [SHADOW_CTR0 + x * SHADOW_CTR_STRIDE]
@@ -384,7 +385,9 @@ void launch_tail_slots(MarchCtrl* ctrl, hipStream_t s);
 // OccBrick blob (sng_math.h) of the linear occupancy; flags: 4096 u32 scratch, blob: OCC_BRICK_CAP_WORDS, n_bricks: 1 u32
 void launch_occ_brick(const uint32_t* occ_linear, uint32_t* flags, uint32_t* blob, uint32_t* n_bricks, hipStream_t s);
 // mesh.hip
-void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, hipStream_t s);
+// scratch: shadow_scratch_bytes(a) of device memory (light samples and terms per neighbour slot)
+size_t shadow_scratch_bytes(const ShadowArgs& a);
+void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, void* scratch, hipStream_t s);
 void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
                       hipStream_t s);
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,

@@ -58,9 +58,11 @@ for ov in CASES:
     res = []
     for r in range(N):
         ms, fr = t_frame((b[r], b[r + 1]))
-        res.append((ms, fr.ms_raytrace, fr.ms_nerf, fr.n_iterations))
+        res.append((ms, fr.ms_raytrace, fr.ms_nerf, fr.n_iterations, fr.ms_frame, fr.ms_shadow, fr.network_launches))
     worst = max(res)
     print(json.dumps({"overrides": ov, "max_band_ms": round(worst[0], 3), "pred_fps": round(1000.0 / worst[0], 1),
                       "pred_eff": round(full / (N * worst[0]), 3), "worst_band_rt_nerf_ms_iters": [round(worst[1], 3), round(worst[2], 3), worst[3]],
-                      "band_ms": [round(x[0], 3) for x in res]}), flush=True)
+                      "band_ms": [round(x[0], 3) for x in res],
+                      "band_device_frame_nerf_shadow_rt_ms": [[round(x[4], 3), round(x[2], 3), round(x[5], 3), round(x[1], 3)] for x in res],
+                      "band_network_launches": [x[6] for x in res]}), flush=True)
 tb.close()
