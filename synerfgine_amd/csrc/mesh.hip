@@ -438,9 +438,19 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
             const f3 src = pos + fract_offset;
             const float fd = length(lpos - src);
             const f3 Ld = normalize(lpos - src);
-            const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip,
-                                                           full_d <= fd ? full_d : __builtin_huge_valf()));
-            const double mask = (double)(nd * (1.0f - fminf(L.intensity, 0.0f))) / ((double)full_d * (1.0 - (double)a.threshold));
+            const float k1 = 1.0f - fminf(L.intensity, 0.0f);
+            const double k2 = (double)full_d * (1.0 - (double)a.threshold);
+            // the march matters only while its mask stays below `overall`: the mask is non-decreasing in the march
+            // distance, so the walk may stop at the smallest c with mask(c) >= overall (depth_test_nerf's cap; the
+            // march distance never decreases, so a walk past c ends at a result >= c and leaves `overall` as it is)
+            float cap = full_d <= fd ? full_d : __builtin_huge_valf();
+            if (k1 > 0.0f && k2 > 0.0 && overall >= 0.0f) {
+                float c = (float)((double)overall * k2 / (double)k1);
+                for (int it = 0; it < 4 && c < cap && (double)(c * k1) / k2 < (double)overall; ++it) c = nextafterf(c, __builtin_huge_valf());
+                if ((double)(c * k1) / k2 >= (double)overall) cap = fminf(cap, c);
+            }
+            const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip, cap));
+            const double mask = (double)(nd * k1) / k2;
             overall = (float)fmin((double)overall, mask);
         } else {
             const f3 l = normalize(L.pos - pos);
