@@ -432,7 +432,9 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
             const f3 l = normalize(lpos - pos);
             const float full_d = length(lpos - pos);
             int hit = -1;
-            const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, cx, hit);
+            // with a non-negative intensity a depth >= full_d gives pow(>= 1) >= 1 = no change to `overall`, so the
+            // query is culled at full_d (the closest hit nearer than that is found as before; none: full_d)
+            const float syn_depth = depth_test_world(pos, l, a.objs, a.n_objs, cx, hit, a.intensity >= 0.0f ? full_d : MAX_DEPTH);
             overall = fminf(overall, pow_small_int(syn_depth / full_d, a.intensity));
             const f3 fract_offset = full_d * a.threshold * lpos;
             const f3 src = pos + fract_offset;
