@@ -464,6 +464,7 @@ struct sng_ctx {
     DevBuf tail_live;                      // tail iterations' alive counts as a difference array (reference slots)
     DevBuf sched_hint;                     // steps of every iteration of the last frame (sizes the msr rounds)
     DevBuf msr_hist;                       // multi-step rounds: [4][MSR_KMAX] per-iteration deaths / samples
+    DevBuf msr_alpha;                      // multi-step rounds: per-sample alpha, msr_count -> msr_commit
     DevBuf march_log;                      // diagnostics (param march_log): per iteration {alive, steps, samples}
     DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
     DevBuf spec_hint;                      // per NeRF pixel: 1 + the iteration its ray ended at last frame (u8, 0 unknown)
@@ -772,6 +773,22 @@ int n_point_lights(const sng_ctx* c) {
     int n = 0;
     for (const auto& l : c->lights) n += l.type == 0 ? 1 : 0;
     return n;
+}
+
+// the NeRF shadow pass's mesh queries: the raytracer's scene blob, in LDS when it fits (2 x 512 or 1 x 1024 threads
+// per CU with their stacks, 16 waves per CU), else traversed from global memory
+void shadow_scene(sng_ctx* c, ShadowArgs& sa) {
+    sa.scene_blob = c->d_scene_blob.as<float4>();
+    sa.scene_f4 = c->scene_f4;
+    sa.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
+    sa.bvh_flat = c->p("bvh_flat") != 0.0 ? 1 : 0;
+    const uint64_t blob_b = (uint64_t)c->scene_f4 * 16;
+    const bool lds_ok = c->p("scene_lds") != 0.0 && sa.scene_blob != nullptr;
+    sa.tpb = 512;
+    sa.scene_in_lds = 0;
+    if (lds_ok && blob_b + (uint64_t)sa.stack_depth * 512 * 4 <= 80u * 1024u) sa.scene_in_lds = 1;
+    else if (lds_ok && blob_b + (uint64_t)sa.stack_depth * 1024 * 4 <= 160u * 1024u) { sa.scene_in_lds = 1; sa.tpb = 1024; }
+    sa.blocks = (uint32_t)c->n_cus * (1024u / sa.tpb);
 }
 
 void load_scene(sng_ctx* c, const std::string& path) {
@@ -1256,7 +1273,9 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             ma.vol = vol; ma.cam = cam; ma.sched = a.sched; ma.ctrl = ctrl; ma.target = target;
             ma.budget = (uint32_t)std::min<double>((double)c->sample_cap, std::max(1.0, c->p("nerf_msr_budget")));
             ma.kmax = (uint32_t)std::min<double>(MSR_KMAX, std::max(1.0, c->p("nerf_msr_kmax")));
+            c->msr_alpha.ensure(c->sample_cap * 4);
             ma.coords = c->coords.as<float>(); ma.samp = c->samp.as<uint2>(); ma.tbuf = c->spec_t.as<float>(); ma.net_out = c->net_out.as<uint2>();
+            ma.abuf = c->msr_alpha.as<float>();
             ma.hist = c->msr_hist.as<uint32_t>();
             ma.frame_rgba = c->nerf_rgba.as<float4>(); ma.frame_depth = c->nerf_depth.as<float>(); ma.positions = c->nerf_pos.as<float>();
             const uint32_t mblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
@@ -1694,6 +1713,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         sa.objs = c->d_objs.as<ObjectGpu>(); sa.n_objs = (int)c->objs.size();
         sa.lights = c->d_lights.as<LightGpu>(); sa.n_lights = (int)c->lights.size();
         sa.n_point = n_point_lights(c);
+        shadow_scene(c, sa);
         c->shadow_scratch.ensure(shadow_scratch_bytes(sa));
         launch_shadows(sa, c->nerf_rgba.as<float4>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->rng_nerf.as<uint32_t>(), c->n_rng_nerf,
                        c->shadow_scratch.p, c->s_nerf);
@@ -1707,6 +1727,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         sa.objs = c->d_objs.as<ObjectGpu>(); sa.n_objs = 0;
         sa.lights = c->d_lights.as<LightGpu>(); sa.n_lights = (int)c->lights.size();
         sa.n_point = n_point_lights(c);
+        shadow_scene(c, sa);
         c->shadow_scratch.ensure(shadow_scratch_bytes(sa));
         launch_shadows(sa, c->nerf_rgba.as<float4>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->rng_nerf.as<uint32_t>(), c->n_rng_nerf,
                        c->shadow_scratch.p, c->s_nerf);

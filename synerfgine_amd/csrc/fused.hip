@@ -763,9 +763,12 @@ __global__ void onestep_begin_kernel(OnestepArgs a, uint32_t k, uint32_t horizon
 
 // alive(k + m) = n_k - sum_{x < m} deaths[x]; J = first m in [0, H) whose alive count is 0 or allows
 // more than one step (H: MARCH_ITER).  Statistics as generate/composite record them per iteration.
-__global__ __launch_bounds__(1024) void onestep_schedule_kernel(OnestepArgs a) {
-    constexpr uint32_t CH = ONESTEP_HIST / 1024;
-    __shared__ uint32_t ps[1024], pl[1024];
+// one 256-thread workgroup (a 1024-thread one waited ~0.5 ms for a free CU beside the raytracer's persistent grids)
+constexpr uint32_t OS_SCHED_THREADS = 256;
+__global__ __launch_bounds__(OS_SCHED_THREADS) void onestep_schedule_kernel(OnestepArgs a) {
+    constexpr uint32_t CH = ONESTEP_HIST / OS_SCHED_THREADS;
+    static_assert(ONESTEP_HIST % OS_SCHED_THREADS == 0, "histogram split");
+    __shared__ uint32_t ps[OS_SCHED_THREADS], pl[OS_SCHED_THREADS];
     __shared__ uint32_t J_sh;
     __shared__ unsigned long long slots_sh, samp_sh;
     OnestepState* os = a.os;
@@ -779,7 +782,7 @@ __global__ __launch_bounds__(1024) void onestep_schedule_kernel(OnestepArgs a) {
     ps[tid] = ss; pl[tid] = sl;
     if (tid == 0) { J_sh = H; slots_sh = 0; samp_sh = 0; }
     __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {   // inclusive Hillis-Steele scans
+    for (uint32_t off = 1; off < OS_SCHED_THREADS; off <<= 1) {   // inclusive Hillis-Steele scans
         const uint32_t vs = tid >= off ? ps[tid - off] : 0u, vl = tid >= off ? pl[tid - off] : 0u;
         __syncthreads();
         ps[tid] += vs; pl[tid] += vl;
@@ -828,7 +831,7 @@ void launch_onestep_begin(const OnestepArgs& a, uint32_t k, uint32_t horizon, in
     hipLaunchKernelGGL(onestep_begin_kernel, dim3((ONESTEP_HIST + 255) / 256), dim3(256), 0, s, a, k, horizon, first);
 }
 void launch_onestep_schedule(const OnestepArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(onestep_schedule_kernel, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(onestep_schedule_kernel, dim3(1), dim3(OS_SCHED_THREADS), 0, s, a);
 }
 void launch_onestep_pass(const OnestepArgs& a, const NetworkDev& net, int final_pass, uint32_t n_rays_hint, hipStream_t s) {
 

@@ -499,17 +499,39 @@ __global__ __launch_bounds__(256) void shadow_draw_kernel(ShadowArgs a, uint32_t
     }
     store_rng(rng, n_rng, idx, r);
 }
-__global__ __launch_bounds__(TPB) void shadow_term_kernel(ShadowArgs a, uint32_t n, const float* __restrict__ positions, const float* __restrict__ normals,
-                                                          const float4* __restrict__ lp, float* __restrict__ terms) {
-    __shared__ int stack_lds[BVH_STACK * TPB];
-    const TraceCtx<false> cx{stack_lds + threadIdx.x, TPB, nullptr, 1};
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t sl = (uint32_t)(t / n), p = (uint32_t)(t % n);
-    if (sl >= (uint32_t)((2 * a.radius + 1) * (2 * a.radius + 1))) return;
-    int fx, fy;
-    if (!shadow_slot(a, p, sl, fx, fy)) return;
-    const size_t tid = (size_t)fy * a.W + fx;
-    terms[(size_t)sl * n + p] = shadow_term(a, cx, load_f3(positions, tid), load_f3(normals, tid), lp + (size_t)sl * a.n_point * n + p, n);
+// persistent grid; with LDS the objects' BVH records and triangles are staged in LDS per workgroup (as the
+// raytracer's traversal kernels do), the stacks follow them.  64-item chunks (one slot, 64 consecutive pixels)
+// are handed out by SHADOW_NCTR counters in separate memory channels (see shadow_rays_kernel).
+template <bool LDS>
+__global__ __launch_bounds__(1024) void shadow_term_kernel(ShadowArgs a, uint32_t n, const float* __restrict__ positions, const float* __restrict__ normals,
+                                                           const float4* __restrict__ lp, float* __restrict__ terms, uint32_t* __restrict__ work) {
+    extern __shared__ float4 smem4[];
+    if constexpr (LDS) {
+        for (uint32_t k = threadIdx.x; k < a.scene_f4; k += blockDim.x) smem4[k] = a.scene_blob[k];
+        __syncthreads();
+    }
+    int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
+    const TraceCtx<LDS> cx{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat};
+    const int lane = threadIdx.x & 63;
+    const uint32_t slots = (uint32_t)((2 * a.radius + 1) * (2 * a.radius + 1));
+    const uint32_t cps = (n + 63u) / 64u, n_chunks = slots * cps;
+    uint32_t x = blockIdx.x % SHADOW_NCTR, tried = 0;
+    while (tried < SHADOW_NCTR) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(work + x * SHADOW_CTR_STRIDE, 1u);
+        k = __shfl(k, 0, 64);
+        const uint32_t c = k * SHADOW_NCTR + x;
+        if (c >= n_chunks) {
+            x = (x + 1u) % SHADOW_NCTR;
+            ++tried;
+            continue;
+        }
+        const uint32_t sl = c / cps, p = (c - sl * cps) * 64u + (uint32_t)lane;
+        int fx, fy;
+        if (p >= n || !shadow_slot(a, p, sl, fx, fy)) continue;
+        const size_t tid = (size_t)fy * a.W + fx;
+        terms[(size_t)sl * n + p] = shadow_term(a, cx, load_f3(positions, tid), load_f3(normals, tid), lp + (size_t)sl * a.n_point * n + p, n);
+    }
 }
 __global__ __launch_bounds__(256) void shadow_finish_kernel(ShadowArgs a, uint32_t n, const float* __restrict__ terms, float4* __restrict__ rgba) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -979,21 +1001,6 @@ __global__ void xorwow_init_kernel(uint32_t n, uint32_t seed_lo, uint32_t seed_h
 }
 
 // ---------------------------------------------------------------------------
-size_t shadow_scratch_bytes(const ShadowArgs& a) {
-    const size_t n = (size_t)(a.row1 - a.row0) * (size_t)a.W, slots = (size_t)(2 * a.radius + 1) * (size_t)(2 * a.radius + 1);
-    return slots * n * ((size_t)a.n_point * sizeof(float4) + sizeof(float));
-}
-void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, void* scratch, hipStream_t s) {
-    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
-    if (!n) return;
-    const size_t slots = (size_t)(2 * a.radius + 1) * (size_t)(2 * a.radius + 1);
-    float4* lp = static_cast<float4*>(scratch);
-    float* terms = reinterpret_cast<float*>(lp + slots * (size_t)a.n_point * n);
-    hipLaunchKernelGGL(shadow_draw_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, n, rng, n_rng, lp);
-    const size_t items = slots * n;
-    hipLaunchKernelGGL(shadow_term_kernel, dim3((uint32_t)((items + TPB - 1) / TPB)), dim3(TPB), 0, s, a, n, pos, nrm, lp, terms);
-    hipLaunchKernelGGL(shadow_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, n, terms, rgba);
-}
 void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
                       hipStream_t s) {
     const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
@@ -1104,6 +1111,31 @@ void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf
 void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(xorwow_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, (uint32_t)seed, (uint32_t)(seed >> 32), seq_pow, st);
+}
+
+constexpr size_t SHADOW_WORK_BYTES = SHADOW_NCTR * SHADOW_CTR_STRIDE * sizeof(uint32_t);
+size_t shadow_scratch_bytes(const ShadowArgs& a) {
+    const size_t n = (size_t)(a.row1 - a.row0) * (size_t)a.W, slots = (size_t)(2 * a.radius + 1) * (size_t)(2 * a.radius + 1);
+    return SHADOW_WORK_BYTES + slots * n * ((size_t)a.n_point * sizeof(float4) + sizeof(float));
+}
+void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, void* scratch, hipStream_t s) {
+    const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
+    if (!n) return;
+    const size_t slots = (size_t)(2 * a.radius + 1) * (size_t)(2 * a.radius + 1);
+    uint32_t* work = static_cast<uint32_t*>(scratch);
+    float4* lp = reinterpret_cast<float4*>(static_cast<char*>(scratch) + SHADOW_WORK_BYTES);
+    float* terms = reinterpret_cast<float*>(lp + slots * (size_t)a.n_point * n);
+    (void)hipMemsetAsync(work, 0, SHADOW_WORK_BYTES, s);   // errors surface through hipGetLastError in the caller
+    hipLaunchKernelGGL(shadow_draw_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, n, rng, n_rng, lp);
+    const size_t lds = (a.scene_in_lds ? (size_t)a.scene_f4 * 16 : 0) + (size_t)a.stack_depth * a.tpb * 4;
+    if (a.scene_in_lds) {
+        allow_lds(shadow_term_kernel<true>, lds);
+        hipLaunchKernelGGL(shadow_term_kernel<true>, dim3(a.blocks), dim3(a.tpb), lds, s, a, n, pos, nrm, lp, terms, work);
+    } else {
+        allow_lds(shadow_term_kernel<false>, lds);
+        hipLaunchKernelGGL(shadow_term_kernel<false>, dim3(a.blocks), dim3(a.tpb), lds, s, a, n, pos, nrm, lp, terms, work);
+    }
+    hipLaunchKernelGGL(shadow_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, n, terms, rgba);
 }
 
 }  // namespace sng

@@ -1143,6 +1143,29 @@ __global__ __launch_bounds__(THREADS) void msr_generate_kernel(MsrArgs a) {
     }
 }
 
+// spec_composite_sample for trace_alt with the sample's alpha given (msr_count formed it with the same expressions)
+__device__ __forceinline__ bool msr_composite_sample(const Volume& vol, const CamDev& cam, f3 o, f3 d, f3 diag, float ts, uint2 raw, float alpha,
+                                                     float4& rgba, float& depth) {
+    const f3 wp = ((o + d * ts) - vol.train_aabb.lo) / diag;   // generate_kernel's coordinate
+    const f3 pos = vol.train_aabb.lo + wp * diag;
+    const float T = 1.f - rgba.w;
+    const float r = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x & 0xffffu));
+    const float g = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.x >> 16));
+    const float b = (float)__builtin_bit_cast(_Float16, (uint16_t)(raw.y & 0xffffu));
+    const float weight = alpha * T;
+    rgba.x += logistic(r) * weight;
+    rgba.y += logistic(g) * weight;
+    rgba.z += logistic(b) * weight;
+    rgba.w += weight;
+    depth = dot(cam.c2, pos - cam.c3);
+    if (rgba.w > (1.0f - vol.min_transmittance)) {
+        const float aa = rgba.w;
+        rgba.x /= aa; rgba.y /= aa; rgba.z /= aa; rgba.w /= aa;
+        return true;
+    }
+    return false;
+}
+
 // the iteration each ray ends in (opacity, the march's end, or MARCH_ITER's drop), from the opacity chain alone
 template <int THREADS = 256>
 __global__ __launch_bounds__(THREADS) void msr_count_kernel(MsrArgs a) {
@@ -1173,11 +1196,13 @@ __global__ __launch_bounds__(THREADS) void msr_count_kernel(MsrArgs a) {
             // the iteration's t's and outputs loaded together, ahead of the opacity chain
             float tv[MAX_STEPS_BETWEEN_COMPACTION];
             uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
+            uint2 rlast = lraw;   // rv[cnt - 1], selected with static indices (a dynamic one puts the arrays in scratch)
 #pragma unroll
             for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
                 if (q < cnt) {
                     tv[q] = a.tbuf[(size_t)(s + q) * n_alive + i];
                     rv[q] = (ru && q == 0) ? lraw : a.net_out[ob + q - ru];
+                    if (q + 1 == cnt) rlast = rv[q];
                 }
             }
             uint32_t j = cnt;
@@ -1185,11 +1210,13 @@ __global__ __launch_bounds__(THREADS) void msr_count_kernel(MsrArgs a) {
             for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
                 if (q >= cnt) break;
                 const float T = 1.f - w;
-                w += msr_alpha(vol, tv[q], rv[q]) * T;
+                const float al = msr_alpha(vol, tv[q], rv[q]);
+                a.abuf[(size_t)(s + q) * n_alive + i] = al;   // msr_commit composites every sample this loop reaches
+                w += al * T;
                 if (w > opaque) { j = q; break; }
             }
             if (j < S || last) { e = it; break; }
-            lraw = rv[cnt - 1];   // the next iteration's boundary sample (S >= 2: never the reused one)
+            lraw = rlast;   // the next iteration's boundary sample (S >= 2: never the reused one)
             ob += cnt - ru;
             s += cnt;
         }
@@ -1282,12 +1309,13 @@ __global__ __launch_bounds__(THREADS) void msr_commit_kernel(MsrArgs a) {
                 const uint32_t cnt = it + 1 == n_it ? cnt_last : S;
                 const uint32_t ru = (rbits >> it) & 1u;
                 const bool last = istep0 + S * it + S >= MARCH_ITER;
-                float tv[MAX_STEPS_BETWEEN_COMPACTION];
+                float tv[MAX_STEPS_BETWEEN_COMPACTION], av[MAX_STEPS_BETWEEN_COMPACTION];
                 uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
 #pragma unroll
                 for (uint32_t q = 0; q < MAX_STEPS_BETWEEN_COMPACTION; ++q) {
                     if (q < cnt) {
                         tv[q] = a.tbuf[(size_t)(s + q) * n_alive + i];
+                        av[q] = a.abuf[(size_t)(s + q) * n_alive + i];
                         rv[q] = (ru && q == 0) ? lraw : a.net_out[ob + q - ru];
                     }
                 }
@@ -1299,7 +1327,7 @@ __global__ __launch_bounds__(THREADS) void msr_commit_kernel(MsrArgs a) {
                     if (q >= cnt) break;
                     tq = tv[q];
                     rq = rv[q];
-                    if (spec_composite_sample(vol, cam, mode, o, d, diag, tq, rq, rgba, depth, mw)) { j = q; break; }
+                    if (msr_composite_sample(vol, cam, o, d, diag, tq, rq, av[q], rgba, depth)) { j = q; break; }
                 }
                 ot.w = depth / dot(cam.c2, d);   // payload.t reset (574)
                 if (j < S) {

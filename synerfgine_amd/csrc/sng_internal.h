@@ -230,6 +230,12 @@ struct ShadowArgs {
     const ObjectGpu* objs; int n_objs;
     const LightGpu* lights; int n_lights;
     int n_point;                // lights of type 0 (Light::sample draws)
+    // the mesh query's scene (as RaytraceArgs): BVH records + triangles staged in LDS when scene_in_lds
+    const float4* scene_blob; uint32_t scene_f4;
+    uint32_t stack_depth;       // traversal stack entries per thread
+    int bvh_flat;
+    int scene_in_lds;
+    uint32_t tpb, blocks;       // persistent grid of the term kernel
 };
 
 // raytracer work counters (RaytraceArgs::work): [0] path-kernel tiles, [SHADOW_CTR0 + x * SHADOW_CTR_STRIDE]
@@ -353,6 +359,7 @@ struct MsrArgs {
     float* coords;                // NerfCoordinate AoS of the network samples
     uint2* samp;                  // per ray: {first network sample, n_it | cnt_last << 5 | reuse bits << 9}
     float* tbuf;                  // [sample j of the ray][ray] march t of every sample
+    float* abuf;                  // [sample j of the ray][ray] its alpha (msr_count -> msr_commit), tbuf's layout
     const uint2* net_out;         // [n][4] fp16
     uint32_t* hist;               // [4][MSR_KMAX]: deaths (band), deaths (own rows; summed over ranks), samples, reused
     float4* frame_rgba;
