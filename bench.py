@@ -591,8 +591,23 @@ def main():
                                                    "frac": round(evaluated * BYTES_PER_SAMPLE / ((field_ms + ms_os) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if field_ms + ms_os > 0 else 0.0}},
         }
     if rank == 0 and world == 1 and not args.no_sweep:
-        # extra legs, after the timed region: C3 with NeRF shadows r = 2 (SURVEY §8d reports r = 0 and r = 2), and
-        # the reference's own sweep (BASELINE.md's scene)
+        # extra legs, after the timed region: the same workload with the two streams serialized (the roofline kernel's
+        # launches then run alone), C3 with NeRF shadows r = 2 (SURVEY §8d reports r = 0 and r = 2), and the
+        # reference's own sweep (BASELINE.md's scene)
+        if not args.serial_streams:
+            try:
+                NW, NH = res["nerf"]
+                u = frame_cells(eng, [{"concurrent_streams": 0}], 10, 2, NW * NH)[0]
+                eng.set_param("concurrent_streams", 1)
+                result["roofline"]["uncontended"] = {
+                    "frac": u["network_roofline_frac"], "field_sample_weighted_frac": u["field_sample_weighted_frac"],
+                    "frames_per_s": u["frames_per_s"],
+                    "note": "the same frames with the raytracer and the NeRF serialized (concurrent_streams=0, 10 frames after "
+                            "the timed region): the network launches run alone. The timed line runs the streams concurrently, "
+                            "where the raytracer's persistent grids leave the NeRF stream rt_reserved_cus CUs, so `frac` above "
+                            "is the launches' duration on that share of the GPU; concurrency is the faster frame"}
+            except Exception as e:
+                result["roofline"]["uncontended"] = {"error": repr(e)}
         try:
             if args.config == "c3":
                 NW, NH = res["nerf"]
