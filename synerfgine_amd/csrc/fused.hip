@@ -540,6 +540,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void n
                                 w = wn;
                             }
                             rgba = make_float4(cr, cg, cb, w);
+                        } else {
+                            // P = 2..4: one whole orbit per check, its entries in registers (a lane whose orbit is
+                            // longer would otherwise hold its wave in the LDS loop below for ~1,100 iterations); the
+                            // orbit that passes the threshold is replayed by that loop from the state before it
+                            float4 e0 = cyc_lds(wv, 0, lane), e1 = cyc_lds(wv, 1, lane), e2 = e1, e3 = e1;
+                            if (P > 2) e2 = cyc_lds(wv, 2, lane);
+                            if (P > 3) e3 = cyc_lds(wv, 3, lane);
+                            float w = rgba.w, cr = rgba.x, cg = rgba.y, cb = rgba.z;
+                            while (x0 + (uint32_t)P <= xnl) {
+                                float wn = w, nr = cr, ng = cg, nb = cb;
+                                auto step = [&](const float4& c) {
+                                    const float weight = c.w * (1.f - wn);
+                                    if (FINAL) { nr += c.x * weight; ng += c.y * weight; nb += c.z * weight; }
+                                    wn += weight;
+                                };
+                                step(e0);
+                                step(e1);
+                                if (P > 2) step(e2);
+                                if (P > 3) step(e3);
+                                if (wn > opaque) break;   // opacity never decreases: the orbit's last value decides
+                                x0 += (uint32_t)P;
+                                const bool fixed = wn == w;   // unchanged over a whole orbit: never changes again
+                                w = wn; cr = nr; cg = ng; cb = nb;
+                                if (!FINAL && fixed) { stuck = true; break; }
+                            }
+                            rgba = make_float4(cr, cg, cb, w);
                         }
                         float wprev = rgba.w;
                         for (uint32_t x = x0; !stuck; ++x) {
