@@ -453,8 +453,10 @@ def main():
     root_gather = world > 1 and on_dev and not args.local_schedule   # the communicator sng_set_comm attached
     if root_gather:
         frame = torch.empty((MH, MW), dtype=torch.int32, device=dev) if rank == 0 else None
-    else:
-        frame = torch.empty((world * band, MW), dtype=torch.int32, device=dev if on_dev else "cpu") if world > 1 else None
+    elif on_dev:
+        frame = torch.empty((world * band, MW), dtype=torch.int32, device=dev) if world > 1 else None
+    else:   # gloo: the bands reassembled into rank 0's frame by their bounds (tiling.gather_to_root)
+        frame = torch.empty((MH, MW), dtype=torch.int32) if world > 1 and rank == 0 else None
 
     def step(collect):
         r = eng.frame(spp=0, reset=True, rows=rows if world > 1 else None, collect_kernel_times=collect)
@@ -467,7 +469,7 @@ def main():
                 T.gather_bands(tile_dev, frame)
             else:
                 tile.copy_(tile_dev)
-                T.gather_bands(tile, frame)
+                T.gather_to_root(tile, bounds, frame)
         return r
 
     for _ in range(args.warmup):
@@ -544,7 +546,7 @@ def main():
                        "width": MW, "height": MH, "nerf_res": list(res["nerf"]),
                        "tiles": f"{world} horizontal bands (rows {bounds}) + " +
                                 (("RCCL gather of the RGBA8 bands to rank 0 (sng_gather_rgba8)" if root_gather else
-                                  ("RCCL" if on_dev else "gloo") + " all_gather of RGBA8 tiles")
+                                  "RCCL all_gather of RGBA8 tiles" if on_dev else "gloo gather of the RGBA8 bands to rank 0 (tiling.gather_to_root)")
                                  if world > 1 else "no gather"),
                        "step_schedule": "band-local" if (world > 1 and args.local_schedule) else ("frame-wide (per-iteration alive-count all-reduce)" if world > 1 else "frame-wide"),
                        "samples_per_frame": int(s0.n_samples), "samples_reused_per_frame": int(s0.n_samples_reused),

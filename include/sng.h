@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 2
+#define SNG_ABI_VERSION 3
 
 enum {
     SNG_OK = 0,
@@ -106,6 +106,8 @@ typedef struct {
     uint32_t msr_rounds;        /* multi-step speculative rounds that committed iterations (nerf_msr; 0: none) */
     uint32_t msr_evals;         /* samples their network launches evaluated ... */
     uint32_t msr_exec;          /* ... of which the per-iteration wavefront would have evaluated */
+    uint32_t sched_reductions;  /* frame-wide schedule reductions (all-reduces per rank) the frame made; 0 without a
+                                   communicator, reducer or replay */
 } sng_frame_result;
 
 typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;
@@ -282,6 +284,13 @@ int sng_set_comm(sng_ctx* ctx, const uint8_t* unique_id, int rank, int world);
  * success; called once per wavefront iteration after a stream sync.  fn NULL detaches. */
 typedef int (*sng_sched_reduce_fn)(uint32_t* values, uint32_t n, void* user);
 int sng_set_sched_reducer(sng_ctx* ctx, sng_sched_reduce_fn fn, void* user);
+/* Schedule replay (profiling: one GPU times a band exactly as its rank renders it under sng_set_comm).
+ * records: the reduced arrays of one frame in call order, each as {n, v[0..n)} -- what a host reducer
+ * returns, e.g. recorded at world size 1 over the full frame.  Every reduction point of the following frames
+ * copies its record to the device asynchronously on the context's stream (no host sync, no communicator);
+ * the cursor restarts at each frame, and a frame whose reductions differ from the records fails with
+ * SNG_ERR_STATE.  records NULL detaches.  Excludes a communicator or host reducer. */
+int sng_set_sched_replay(sng_ctx* ctx, const uint32_t* records, uint64_t n_words);
 /* Final composition of a banded frame ("a final RCCL gather to GPU 0 of RGBA8"): rank r's
  * final rows [bounds[r], bounds[r+1]) as RGBA8 (the sng_final_rgba8 encoding) go to rank 0 over the
  * attached communicator -- grouped ncclSend / ncclRecv, each band received straight into its rows of

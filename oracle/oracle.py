@@ -105,6 +105,7 @@ def lib():
             "orc_grid_level_table": (u32, [vp, vp, vp]), "orc_n_params": (u32, [vp]),
             "orc_hashgrid_encode": (None, [vp, vp, u32, u32, vp]), "orc_sh_encode": (None, [vp, u32, u32, u32, vp]),
             "orc_nerf_inference": (None, [vp, vp, u32, u32, vp]),
+            "orc_wavefront_schedule": (None, [vp, u32, u32, vp, vp]),
             "orc_density_grid_to_bitfield": (None, [vp, u32, vp, vp]),
             "orc_render_nerf": (None, [vp, vp, vp, vp, vp, vp, vp, vp]),
             "orc_render_nerf_ngp": (None, [vp, vp, vp, i32, f32, vp, vp, vp]),

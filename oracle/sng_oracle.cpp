@@ -159,6 +159,18 @@ constexpr float MIN_DEPTH = 0.00001f;
 constexpr uint32_t MARCH_ITER = 10000;                 /* testbed_nerf.cu:47 */
 constexpr uint32_t MIN_STEPS_INBETWEEN_COMPACTION = 1; /* testbed_nerf.cu:49 */
 constexpr uint32_t MAX_STEPS_INBETWEEN_COMPACTION = 8; /* testbed_nerf.cu:50 */
+constexpr uint32_t BATCH_SIZE_GRANULARITY = 256;        /* tcnn (common.h) */
+
+/* trace_alt's per-iteration sizes: n_steps_between_compaction = clamp(target_n_queries / n_alive, 1, 8)
+ * (testbed_nerf.cu:2188-2190) and the batch the network evaluates, n_elements =
+ * next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY) (:2210).  Pinned against the reference's own
+ * executions (its nvprof traces, tests/test_ref_schedule.py). */
+static uint32_t wavefront_steps(uint32_t n_alive, uint32_t target) {
+    return std::min(std::max(target / n_alive, MIN_STEPS_INBETWEEN_COMPACTION), MAX_STEPS_INBETWEEN_COMPACTION);
+}
+static uint64_t wavefront_elements(uint32_t n_alive, uint32_t n_steps) {
+    return ((uint64_t)n_alive * n_steps + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY;
+}
 constexpr float PI_F = 3.14159265358979323846f;        /* tcnn::PI / random_val.cuh:27 */
 
 /* ------------------------------------------------------------------------- */
@@ -1201,7 +1213,7 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
         }
         n_alive = (uint32_t)current.size();
         if (n_alive == 0) break;
-        uint32_t n_steps = std::min(std::max(target / n_alive, MIN_STEPS_INBETWEEN_COMPACTION), MAX_STEPS_INBETWEEN_COMPACTION);
+        uint32_t n_steps = wavefront_steps(n_alive, target);
         if (stats && iter < 64) { stats->alive_per_iter[iter] = n_alive; stats->steps_per_iter[iter] = n_steps; }
         ++iter;
         /* generate_next_nerf_network_inputs 790-837; slot i + j*n_alive */
@@ -1227,7 +1239,7 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
             if (!exhausted) { p.t = t; p.n_steps = (uint16_t)n_steps; }
             real += exhausted ? j : n_steps;
         }
-        if (stats) { stats->n_samples += real; stats->n_slots += ((uint64_t)n_alive * n_steps + 255) / 256 * 256; }
+        if (stats) { stats->n_samples += real; stats->n_slots += wavefront_elements(n_alive, n_steps); }
         /* inference_mixed_precision on the real slots (stale slots do not affect results) */
         outs.assign((size_t)n_alive * n_steps * 4, 0);
 #pragma omp parallel for schedule(dynamic, 256)
@@ -2051,4 +2063,12 @@ extern "C" void orc_display(const float* rgba, int32_t W, int32_t H, int32_t OW,
                 o[k] = (uint8_t)(int)(f * 255.0f + 0.5f);
             }
         }
+}
+
+extern "C" void orc_wavefront_schedule(const uint32_t* n_alive, uint32_t n, uint32_t target, uint32_t* n_steps, uint64_t* n_elements) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t a = n_alive[i];
+        n_steps[i] = a ? wavefront_steps(a, target ? target : 2u * 1024u * 1024u) : 0u;
+        n_elements[i] = a ? wavefront_elements(a, n_steps[i]) : 0u;
+    }
 }

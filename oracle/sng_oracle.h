@@ -114,6 +114,9 @@ void     orc_xorwow_jump_matrix(uint32_t state[6], uint32_t log2_steps);  /* M^(
 /* ---- network (A6-A8) ----------------------------------------------------- */
 uint32_t orc_grid_level_table(const orc_model* m, uint32_t* offsets /* L+1 */, uint32_t* resolutions /* L */);
 uint32_t orc_n_params(const orc_model* m);
+/* trace_alt's per-iteration n_steps (testbed_nerf.cu:2188-2190) and padded batch n_elements (:2210) for each
+ * n_alive; target 0 = 2^21 */
+void orc_wavefront_schedule(const uint32_t* n_alive, uint32_t n, uint32_t target, uint32_t* n_steps, uint64_t* n_elements);
 void orc_hashgrid_encode(const orc_model* m, const float* coords, uint32_t stride_floats, uint32_t n, uint16_t* out /* n x L*F */);
 void orc_sh_encode(const float* coords, uint32_t stride_floats, uint32_t dir_offset, uint32_t n, uint16_t* out /* n x 16 */);
 void orc_nerf_inference(const orc_model* m, const float* coords, uint32_t stride_floats, uint32_t n, uint16_t* out /* n x 16 (tcnn rgbsigma row block) */);

@@ -168,7 +168,7 @@ class FrameResult:
                      "ms_overlay", "ms_network", "network_launches",
                      "fused_from_iter", "n_samples_network", "ms_fused_tail", "n_samples_reused",
                      "onestep_from_iter", "onestep_iterations", "ms_onestep", "onestep_field_evals", "spec_rounds", "spec_evals",
-                     "spec_exec", "msr_rounds", "msr_evals", "msr_exec"):
+                     "spec_exec", "msr_rounds", "msr_evals", "msr_exec", "sched_reductions"):
             setattr(self, name, getattr(r, name))
         self.alive_per_iter = list(r.alive_per_iter)[: min(64, r.n_iterations)]
         self.steps_per_iter = list(r.steps_per_iter)[: min(64, r.n_iterations)]
@@ -297,9 +297,30 @@ class Engine:
         b = (ctypes.c_int32 * len(bounds))(*[int(x) for x in bounds])
         check(self._lib.sng_gather_rgba8(self.ctx, b, ctypes.c_void_p(int(d_frame) or None), ctypes.c_void_p(int(stream) or None)))
 
+    def record_schedule(self):
+        """A world-size-1 host reducer that records every reduced array of the following frames (sng_set_sched_replay's
+        record format); returns the list the records are appended to, as [[n, v0, .., vn-1], ...]."""
+        log = []
+
+        def rec(vals):
+            log.append([len(vals)] + [int(v) for v in vals])
+            return vals
+        self.attach_host_reducer(rec)
+        return log
+
+    def set_sched_replay(self, records):
+        """Replay the reduced arrays `records` ([[n, v...], ...], one frame's reductions in call order) at every
+        reduction point of the following frames (sng_set_sched_replay); None detaches."""
+        if records is None:
+            check(self._lib.sng_set_sched_replay(self.ctx, None, 0))
+            return
+        flat = np.ascontiguousarray([w for r in records for w in r], np.uint32)
+        check(self._lib.sng_set_sched_replay(self.ctx, flat.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), flat.size))
+
     def detach_comm(self):
         check(self._lib.sng_set_comm(self.ctx, None, 0, 0))
         check(self._lib.sng_set_sched_reducer(self.ctx, None, None))
+        check(self._lib.sng_set_sched_replay(self.ctx, None, 0))
         self._reduce_cb = None
 
     # ---- headless display stage (Display::present / save_image, display.cu:265-322) ----------

@@ -92,6 +92,7 @@ class sng_frame_result(ctypes.Structure):
         ("msr_rounds", ctypes.c_uint32),
         ("msr_evals", ctypes.c_uint32),
         ("msr_exec", ctypes.c_uint32),
+        ("sched_reductions", ctypes.c_uint32),
     ]
 
 
@@ -203,6 +204,7 @@ SIGNATURES = {
     "sng_comm_unique_id": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint8)]),
     "sng_set_comm": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint8), ctypes.c_int, ctypes.c_int]),
     "sng_set_sched_reducer": (ctypes.c_int, [P, P, P]),
+    "sng_set_sched_replay": (ctypes.c_int, [P, U32P, U64]),
     "sng_synchronize": (ctypes.c_int, [P]),
     "sng_copy_to_host": (ctypes.c_int, [P, P, P, U64]),
     "sng_copy_device": (ctypes.c_int, [P, P, P, U64, P]),
@@ -215,7 +217,7 @@ SIGNATURES = {
 _lib = None
 
 
-ABI_VERSION = 2   # SNG_ABI_VERSION of include/sng.h
+ABI_VERSION = 3   # SNG_ABI_VERSION of include/sng.h
 
 
 def load():

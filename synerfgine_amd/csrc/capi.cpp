@@ -463,6 +463,7 @@ struct sng_ctx {
     DevBuf shadow_scratch;                 // NeRF shadow pass: light samples + terms per neighbour slot (launch_shadows)
     DevBuf tail_live;                      // tail iterations' alive counts as a difference array (reference slots)
     DevBuf sched_hint;                     // steps of every iteration of the last frame (sizes the msr rounds)
+    uint64_t sched_hint_key = 0;           // the schedule the hints were written under (0: none; see trace_nerf)
     DevBuf msr_hist;                       // multi-step rounds: [4][MSR_KMAX] per-iteration deaths / samples
     DevBuf msr_alpha;                      // multi-step rounds: per-sample alpha, msr_count -> msr_commit
     DevBuf march_log;                      // diagnostics (param march_log): per iteration {alive, steps, samples}
@@ -1092,6 +1093,31 @@ uint64_t ref_slots_of(const sng_ctx* c) {
 // own0/own1: the NeRF rows this band owns (the bands of all ranks partition the frame's rows);
 // only used when a schedule communicator is attached (Sched).
 uint8_t* spec_hint_buf(sng_ctx* c);
+
+// One reduction of the frame-wide schedule (sum over ranks of dev[0..n), in place on the NeRF stream):
+// RCCL all-reduce, the host reducer (a stream sync + callback), or the next replay record (an async copy from
+// pinned memory: a band timed on one GPU as its rank runs it, without a communicator).
+void sched_reduce(sng_ctx* c, uint32_t* dev, uint32_t n) {
+    SchedComm& sc = c->sched_comm;
+    ++sc.replay_calls;
+    if (sc.comm) {
+        comm_allreduce_u32(sc, dev, n, c->s_nerf);
+    } else if (sc.replay) {
+        const size_t at = sc.replay_cursor;
+        if (at >= sc.replay_words || sc.replay[at] != n || at + 1 + n > sc.replay_words)
+            throw SngError(SNG_ERR_STATE, "schedule replay diverged at reduction " + std::to_string(sc.replay_calls) + " (" + std::to_string(n) + " values)");
+        HIPCHK(hipMemcpyAsync(dev, sc.replay + at + 1, (size_t)n * 4, hipMemcpyHostToDevice, c->s_nerf));
+        sc.replay_cursor = at + 1 + n;
+    } else {
+        std::vector<uint32_t> h(n);
+        HIPCHK(hipMemcpyAsync(h.data(), dev, (size_t)n * 4, hipMemcpyDeviceToHost, c->s_nerf));
+        HIPCHK(hipStreamSynchronize(c->s_nerf));
+        if (sc.host_fn(h.data(), n, sc.host_user) != 0) throw SngError(SNG_ERR_STATE, "schedule reducer failed");
+        HIPCHK(hipMemcpyAsync(dev, h.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->s_nerf));
+        HIPCHK(hipStreamSynchronize(c->s_nerf));   // h is a stack buffer
+    }
+}
+
 uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, const CamDev& cam, f2 sc, int tr0, int tr1, int own0, int own1,
                     TraceMode mode, uint32_t target, const std::function<void(int)>& on_chunk) {
     const int NW = c->nerf_res[0], NH = c->nerf_res[1];
@@ -1099,10 +1125,18 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     MarchCtrl* ctrl = c->ctrl.as<MarchCtrl>();
     if (c->p("march_log") != 0.0) c->march_log.ensure(MARCH_LOG_CAP * 12);
     c->tail_live.ensure(TAIL_LIVE_CAP * 4);
-    if (!c->sched_hint.p) {
+    const bool gsched = c->sched_comm.active();
+    // The msr rounds size K from the last frame's per-iteration steps (msr_shape).  Under the frame-wide schedule
+    // every rank must see the same hints, so hints written under another schedule (a band's local one, another
+    // target, before a communicator / reducer / replay was attached or detached) are dropped.
+    const uint64_t hint_key = 1ull | (gsched ? 2ull : 0ull) | ((uint64_t)target << 2);
+    if (!c->sched_hint.p || c->sched_hint_key != hint_key) {
         c->sched_hint.ensure(TAIL_LIVE_CAP);
         HIPCHK(hipMemsetAsync(c->sched_hint.p, 0, TAIL_LIVE_CAP, c->s_nerf));
+        c->sched_hint_key = hint_key;
     }
+    c->sched_comm.replay_cursor = 0;
+    c->sched_comm.replay_calls = 0;
     launch_ctrl_init(ctrl, c->tail_live.as<int32_t>(), c->sched_hint.as<uint8_t>(), c->s_nerf, c->p("march_log") != 0.0 ? c->march_log.as<uint32_t>() : nullptr);
     NerfFrameArgs a{};
     a.vol = vol;
@@ -1128,21 +1162,12 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     a.reset = P.reset_accumulation ? 1 : 0;
     a.target_n_queries = target;
     a.mode = mode;
-    const bool gsched = c->sched_comm.active();
     a.sched = {gsched ? 1 : 0, (uint32_t)own0 * (uint32_t)NW, (uint32_t)own1 * (uint32_t)NW};
     // sched_alive[q] <- sum over ranks of n_owned[q] (the frame-wide alive count of the next iteration)
     auto reduce_sched = [&](int q) {
         if (!gsched) return;
-        if (c->sched_comm.comm) {
-            HIPCHK(hipMemcpyAsync(&ctrl->sched_alive[q], &ctrl->n_owned[q], 4, hipMemcpyDeviceToDevice, c->s_nerf));
-            comm_allreduce_u32(c->sched_comm, &ctrl->sched_alive[q], 1, c->s_nerf);
-        } else {
-            uint32_t* h = &c->h_alive[4];
-            HIPCHK(hipMemcpyAsync(h, &ctrl->n_owned[q], 4, hipMemcpyDeviceToHost, c->s_nerf));
-            HIPCHK(hipStreamSynchronize(c->s_nerf));
-            if (c->sched_comm.host_fn(h, 1, c->sched_comm.host_user) != 0) throw SngError(SNG_ERR_STATE, "schedule reducer failed");
-            HIPCHK(hipMemcpyAsync(&ctrl->sched_alive[q], h, 4, hipMemcpyHostToDevice, c->s_nerf));
-        }
+        HIPCHK(hipMemcpyAsync(&ctrl->sched_alive[q], &ctrl->n_owned[q], 4, hipMemcpyDeviceToDevice, c->s_nerf));
+        sched_reduce(c, &ctrl->sched_alive[q], 1);
     };
     uint32_t* const sched_src = gsched ? &ctrl->sched_alive[0] : &ctrl->n_alive[0];   // counts the host loop reads
     RayBuf rb[2];
@@ -1235,17 +1260,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 launch_onestep_begin(oa, iter, horizon, c->os_ran ? 0 : 1, c->s_nerf);
                 launch_onestep_pass(oa, c->net, 0, hc.n_alive[p], c->s_nerf);
                 HIPCHK(hipGetLastError());
-                if (gsched) {   // the frame-wide schedule: own-row deaths summed over the ranks
-                    if (c->sched_comm.comm) {
-                        comm_allreduce_u32(c->sched_comm, oa.deaths_sched, ONESTEP_HIST, c->s_nerf);
-                    } else {
-                        std::vector<uint32_t> h(ONESTEP_HIST);
-                        HIPCHK(hipMemcpyAsync(h.data(), oa.deaths_sched, ONESTEP_HIST * 4, hipMemcpyDeviceToHost, c->s_nerf));
-                        HIPCHK(hipStreamSynchronize(c->s_nerf));
-                        if (c->sched_comm.host_fn(h.data(), ONESTEP_HIST, c->sched_comm.host_user) != 0) throw SngError(SNG_ERR_STATE, "schedule reducer failed");
-                        HIPCHK(hipMemcpyAsync(oa.deaths_sched, h.data(), ONESTEP_HIST * 4, hipMemcpyHostToDevice, c->s_nerf));
-                    }
-                }
+                if (gsched) sched_reduce(c, oa.deaths_sched, ONESTEP_HIST);   // own-row deaths summed over the ranks
                 launch_onestep_schedule(oa, c->s_nerf);
                 HIPCHK(hipMemcpyAsync(c->h_os, oa.os, sizeof(OnestepState), hipMemcpyDeviceToHost, c->s_nerf));
                 HIPCHK(hipStreamSynchronize(c->s_nerf));
@@ -1289,18 +1304,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                                P.collect_kernel_times ? c->net_events[2 * net_launches] : nullptr,
                                P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr);
                 launch_msr_count(ma, mblocks, c->s_nerf);
-                if (gsched) {   // the frame-wide schedule: own-row deaths summed over the ranks
-                    uint32_t* ds = ma.hist + MSR_KMAX;
-                    if (c->sched_comm.comm) {
-                        comm_allreduce_u32(c->sched_comm, ds, MSR_KMAX, c->s_nerf);
-                    } else {
-                        uint32_t h[MSR_KMAX];
-                        HIPCHK(hipMemcpyAsync(h, ds, sizeof(h), hipMemcpyDeviceToHost, c->s_nerf));
-                        HIPCHK(hipStreamSynchronize(c->s_nerf));
-                        if (c->sched_comm.host_fn(h, MSR_KMAX, c->sched_comm.host_user) != 0) throw SngError(SNG_ERR_STATE, "schedule reducer failed");
-                        HIPCHK(hipMemcpyAsync(ds, h, sizeof(h), hipMemcpyHostToDevice, c->s_nerf));
-                    }
-                }
+                if (gsched) sched_reduce(c, ma.hist + MSR_KMAX, MSR_KMAX);   // own-row deaths summed over the ranks
                 launch_msr_schedule(ma, c->s_nerf);
                 launch_msr_commit(ma, mblocks, c->s_nerf);
                 HIPCHK(hipGetLastError());
@@ -1458,6 +1462,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         ++chunk;
         on_chunk(chunk);
     }
+    if (c->sched_comm.replay && c->sched_comm.replay_cursor != c->sched_comm.replay_words)
+        throw SngError(SNG_ERR_STATE, "schedule replay diverged: the frame made " + std::to_string(c->sched_comm.replay_calls) + " reductions, the records hold more");
     return net_launches;
 }
 
@@ -1495,6 +1501,7 @@ void march_stats(const sng_ctx* c, const sng_frame_params& P, sng_frame_result* 
     out->msr_rounds = c->msr_rounds;
     out->msr_evals = (uint32_t)c->h_ctrl->msr_evals;
     out->msr_exec = (uint32_t)c->h_ctrl->msr_exec;
+    out->sched_reductions = (uint32_t)c->sched_comm.replay_calls;
     std::memcpy(out->alive_per_iter, c->h_ctrl->alive_hist, sizeof(out->alive_per_iter));
     std::memcpy(out->steps_per_iter, c->h_ctrl->steps_hist, sizeof(out->steps_per_iter));
     std::memcpy(out->samples_per_iter, c->h_ctrl->samples_hist, sizeof(out->samples_per_iter));
@@ -2053,6 +2060,7 @@ void ctx_destroy(sng_ctx* c) {
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);
     (void)hipHostFree(c->h_os);
+    if (c->sched_comm.replay) (void)hipHostFree(c->sched_comm.replay);
     (void)hipStreamDestroy(c->s_nerf);
     (void)hipStreamDestroy(c->s_rt);
     delete c;
@@ -2944,18 +2952,40 @@ int sng_set_comm(sng_ctx* c, const uint8_t* id, int rank, int world) {
         if (!c) throw SngError(SNG_ERR_INVALID, "null context");
         HIPCHK(hipSetDevice(c->device));
         HIPCHK(hipStreamSynchronize(c->s_nerf));
+        c->sched_hint_key = 0;   // hints of another schedule (trace_nerf)
         if (!id) { comm_destroy(c->sched_comm); return; }
         if (world < 1 || rank < 0 || rank >= world) throw SngError(SNG_ERR_INVALID, "bad rank/world");
-        if (c->sched_comm.host_fn) throw SngError(SNG_ERR_STATE, "a host schedule reducer is attached");
+        if (c->sched_comm.host_fn || c->sched_comm.replay) throw SngError(SNG_ERR_STATE, "a host schedule reducer or replay is attached");
         comm_init(c->sched_comm, id, rank, world);
     });
 }
 int sng_set_sched_reducer(sng_ctx* c, sng_sched_reduce_fn fn, void* user) {
     return guarded([&] {
         if (!c) throw SngError(SNG_ERR_INVALID, "null context");
-        if (fn && c->sched_comm.comm) throw SngError(SNG_ERR_STATE, "an RCCL communicator is attached");
+        if (fn && (c->sched_comm.comm || c->sched_comm.replay)) throw SngError(SNG_ERR_STATE, "an RCCL communicator or replay is attached");
+        c->sched_hint_key = 0;
         c->sched_comm.host_fn = fn;
         c->sched_comm.host_user = fn ? user : nullptr;
+    });
+}
+int sng_set_sched_replay(sng_ctx* c, const uint32_t* records, uint64_t n_words) {
+    return guarded([&] {
+        if (!c) throw SngError(SNG_ERR_INVALID, "null context");
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipStreamSynchronize(c->s_nerf));   // no copy from the old records is still queued
+        SchedComm& sc = c->sched_comm;
+        // attaching or detaching drops the step hints (another schedule wrote them); replacing the records of an
+        // attached replay keeps them, as a rank keeps its frame-wide hints from one frame to the next
+        if (!records || !sc.replay) c->sched_hint_key = 0;
+        if (sc.replay) { (void)hipHostFree(sc.replay); sc.replay = nullptr; sc.replay_words = 0; }
+        if (!records) return;
+        if (sc.comm || sc.host_fn) throw SngError(SNG_ERR_STATE, "an RCCL communicator or host reducer is attached");
+        for (uint64_t at = 0; at < n_words; at += 1 + (uint64_t)records[at])
+            if (records[at] == 0 || at + 1 + records[at] > n_words) throw SngError(SNG_ERR_INVALID, "malformed replay records");
+        HIPCHK(hipHostMalloc((void**)&sc.replay, std::max<uint64_t>(1, n_words) * 4, hipHostMallocDefault));
+        if (n_words) std::memcpy(sc.replay, records, n_words * 4);
+        sc.replay_words = (size_t)n_words;
+        sc.replay_cursor = 0;
     });
 }
 int sng_synchronize(sng_ctx* c) { return guarded([&] { HIPCHK(hipStreamSynchronize(c->s_nerf)); HIPCHK(hipStreamSynchronize(c->s_rt)); }); }

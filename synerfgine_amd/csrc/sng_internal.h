@@ -423,7 +423,11 @@ struct SchedComm {
     int rank = 0, world = 0;
     sng_sched_reduce_fn host_fn = nullptr;
     void* host_user = nullptr;
-    bool active() const { return comm != nullptr || host_fn != nullptr; }
+    // schedule replay (sng_set_sched_replay): records {n, v[0..n)} of one frame's reductions in pinned memory,
+    // copied to the device at each reduction point in call order; the cursor restarts every frame
+    uint32_t* replay = nullptr;
+    size_t replay_words = 0, replay_cursor = 0, replay_calls = 0;
+    bool active() const { return comm != nullptr || host_fn != nullptr || replay != nullptr; }
 };
 void comm_unique_id(uint8_t out[SNG_COMM_ID_BYTES]);
 void comm_init(SchedComm& c, const uint8_t* id, int rank, int world);

@@ -2,9 +2,9 @@
 
 SURVEY.md §8e: rays are independent, so the frame shards into contiguous row bands with no
 data-path collective; halo rows needed by normals (+-2) and NeRF shadows (+-r) are recomputed
-inside sng_render_frame (capi.cpp render_frame), not exchanged.  The only exchange is the final
-gather of the RGBA bands to every rank (all_gather_into_tensor over RCCL/xGMI; one ~1-8 MB tile
-per peer at 1080p).
+inside sng_render_frame (capi.cpp render_frame), not exchanged.  The exchanges are the frame-wide
+step schedule (comm.cpp) and the final gather of the RGBA8 bands to rank 0 (sng_gather_rgba8: grouped
+ncclSend / ncclRecv over xGMI, ~1 MB per peer at 1080p); gather_to_root is its gloo rehearsal.
 """
 import math
 
@@ -33,6 +33,26 @@ def gather_bands(tile, frame, group=None):
         return frame
     dist.all_gather_into_tensor(frame, tile, group=group)
     return frame
+
+
+def assemble_bands(parts, bounds, frame):
+    """Frame rows from the ranks' band tiles: part r holds its rows [bounds[r], bounds[r+1]) at the top of a tile
+    padded to the tallest band (what sng_final_rgba8 of a band leaves in the tile)."""
+    for r, part in enumerate(parts):
+        frame[bounds[r]:bounds[r + 1]] = part[: bounds[r + 1] - bounds[r]]
+    return frame
+
+
+def gather_to_root(tile, bounds, frame=None, group=None):
+    """The gloo (CPU) rehearsal of sng_gather_rgba8: every rank's band rows, the top rows of its padded `tile`, go
+    to rank 0 only and land in rows [bounds[r], bounds[r+1]) of `frame` (rank 0: [height, ...]; other ranks may
+    pass None).  Returns the frame on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    parts = [torch.empty_like(tile) for _ in range(world)] if rank == 0 else None
+    dist.gather(tile, parts, dst=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    return assemble_bands(parts, bounds, frame) if rank == 0 else None
 
 
 def even_bounds(height, world):

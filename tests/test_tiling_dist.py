@@ -82,3 +82,44 @@ def test_balance_bounds_equalises_cost():
     # equal cost stays (nearly) equal-height
     b2 = balance_bounds(H, even_bounds(H, N), [1.0] * N)
     assert max(abs(x - y) for x, y in zip(b2, even_bounds(H, N))) <= 1
+
+
+def _root_worker(rank, world, port, bounds, q):
+    import torch
+    import torch.distributed as dist
+    from synerfgine_amd.tiling import gather_to_root
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # the oracle-rendered 64x64 frame as RGBA8 words (the sng_final_rgba8 / sng_gather_rgba8 payload)
+        full = np.load(os.path.join(HERE, "golden", "frame_nerf_64.npz"))["rgba"]
+        words = np.ascontiguousarray((np.clip(full, 0, 1) * 255 + 0.5).astype(np.uint8)).view(np.int32)[..., 0]
+        H, W = words.shape
+        band = max(bounds[k + 1] - bounds[k] for k in range(world))
+        r0, r1 = bounds[rank], bounds[rank + 1]
+        tile = torch.full((band, W), -1, dtype=torch.int32)           # padding rows must not reach the frame
+        tile[: r1 - r0] = torch.from_numpy(words[r0:r1])
+        frame = torch.zeros((H, W), dtype=torch.int32) if rank == 0 else None
+        out = gather_to_root(tile, bounds, frame)
+        q.put((rank, out is None if rank else bool(np.array_equal(out.numpy(), words))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bounds", [[0, 9, 64], [0, 40, 41, 64], [0, 0, 64]], ids=["uneven2", "uneven3", "empty_band"])
+def test_gloo_gather_to_root_reassembles_uneven_bands(bounds):
+    """bench.py --gpus N --dist-backend gloo: the cost-balanced (uneven) bands reach rank 0's frame rows by their
+    bounds, as sng_gather_rgba8 does over RCCL (comm.cpp); other ranks receive nothing."""
+    import torch.multiprocessing as mp
+    world = len(bounds) - 1
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_root_worker, args=(r, world, port, bounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok in res), res
