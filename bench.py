@@ -30,7 +30,7 @@ BYTES_PER_SAMPLE = 28 + 8 * 8 * 4 * 2 + 8   # NerfCoordinate read + 8 levels x 8
 FLOPS_PER_SAMPLE = 20480                     # 2*(32*64+64*16) + 2*(32*64+64*64+64*16)
 HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F16_PEAK_TFLOPS = 2500.0                # dense fp16/bf16 MFMA
-ROUND = "r03"
+ROUND = "r04"
 
 WORKLOADS = {
     "c2": "lego NeRF only (show_virtual_obj=0, shadows off)",
@@ -180,17 +180,19 @@ def cpu_sample_c3(eng_cfg, config, scale, model_name, overrides):
 
 def latest_profile(prefix, config):
     """profiles/<prefix>_<round>_<config>.json of the newest round that has one (this round's first)."""
-    for rnd in (ROUND, "r02", "r01"):
+    for rnd in (ROUND, "r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", f"{prefix}_{rnd}_{config}.json")
         if os.path.exists(path):
             return path
     return None
 
 
-def traffic_profile(config):
+def traffic_profile(config, samples_per_launch):
     """HBM bytes per launch of the roofline kernels from the newest PMC passes for this config
     (tools/gpu.sh pmc: separate FETCH_SIZE / WRITE_SIZE passes, gfx950 x2 FETCH correction), labelled
-    with the file they came from; None when no profile of this config exists."""
+    with the file they came from.  The counted run must have launched the network on the same work as this
+    line: a file whose samples per launch differ by more than 5 % (or that does not record them) is refused,
+    and the reason is returned instead of the bytes.  None when no profile of this config exists."""
     path = latest_profile("pmc_traffic", config)
     if not path:
         return None
@@ -198,7 +200,13 @@ def traffic_profile(config):
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
-    return {"file": os.path.relpath(path, REPO), "config": d.get("config"), "kernels": d.get("roofline_kernels", {})}
+    rel = os.path.relpath(path, REPO)
+    spl = (d.get("roofline_kernels", {}).get("nerf_network_kernel") or {}).get("samples_per_launch")
+    if not spl:
+        return {"file": rel, "refused": "the file does not record the counted run's samples per network launch"}
+    if abs(spl - samples_per_launch) > 0.05 * max(1.0, samples_per_launch):
+        return {"file": rel, "refused": f"counted run: {spl:.0f} samples per launch, this line: {samples_per_launch:.0f} (> 5 % apart)"}
+    return {"file": rel, "config": d.get("config"), "kernels": d.get("roofline_kernels", {}), "samples_per_launch": spl}
 
 
 def valu_profile(config):
@@ -272,6 +280,45 @@ def _srgb(rgba):
     return np.clip(np.where(lin < 0.0031308, 12.92 * lin, 1.055 * np.power(lin, 0.41666) - 0.055), 0, 1)
 
 
+def orbit_leg(config, w, h, model, warmup, n=60):
+    """The camera orbits the lego 1 degree per frame: nerf_spec_hint on vs off (alternating passes, mean of two each).
+    The hints are read only when a frame repeats the previous frame's view (spec_view_key, capi.cpp), so on the
+    orbit both settings march with the opacity policy; the leg shows that hints cost nothing under motion."""
+    import math
+
+    import numpy as np
+    import torch
+    from synerfgine_amd import scene as S
+    tb, eng, _ = S.make_engine(config, width=w, height=h, model=model)
+    try:
+        mats = []
+        for k in range(n):
+            ang = math.radians(1.0 * k)
+            v = (0.62 * math.cos(ang) + 0.64 * math.sin(ang), 0.46, -0.64 * math.cos(ang) + 0.62 * math.sin(ang))
+            tb.set_camera_view(v, (0.5, 0.5, 0.5), 1.0)
+            mats.append(np.array(tb.camera_matrix))
+        runs = {1: [], 0: []}
+        for hint in (1, 0, 1, 0):
+            eng.set_param("nerf_spec_hint", hint)
+            for m in mats[:warmup]:
+                tb.camera_matrix = m
+                eng.frame(spp=0, reset=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for m in mats[warmup:]:
+                tb.camera_matrix = m
+                eng.frame(spp=0, reset=True)
+            torch.cuda.synchronize()
+            runs[hint].append((len(mats) - warmup) / (time.perf_counter() - t0))
+        eng.set_param("nerf_spec_hint", 1)
+        return {"frames_per_s": {"hints": round(sum(runs[1]) / 2, 1), "no_hints": round(sum(runs[0]) / 2, 1)},
+                "passes": {"hints": [round(x, 1) for x in runs[1]], "no_hints": [round(x, 1) for x in runs[0]]},
+                "res": [w, h], "config": config,
+                "note": "camera orbiting the lego 1 degree per frame; hints are read only for a repeated view (spec_view_key)"}
+    finally:
+        tb.close()
+
+
 def nerf_views(model, frames, warmup, cpu_check=True):
     """NeRF-dominated legs (no virtual objects): (a) BASELINE config C2 -- 800x800 at the lego dataset's camera 0
     (transforms.json frame 0, nerf_matrix_to_ngp, its camera_angle_x field of view; a view train_lego.py held
@@ -322,34 +369,9 @@ def nerf_views(model, frames, warmup, cpu_check=True):
         out["c2_dataset_view"] = leg
     finally:
         tb.close()
-    # (c) C2 with a moving camera: an orbit of 1 degree per frame, so every frame's per-pixel look-ahead hints
-    # (nerf_spec_hint: the ray lives of the previous frame) come from a different view; hints on vs off
-    tb, eng, _ = S.make_engine("c2", width=800, height=800, model=model)
-    try:
-        import torch
-        mats = []
-        for k in range(60):
-            ang = math.radians(1.0 * k)
-            v = (0.62 * math.cos(ang) + 0.64 * math.sin(ang), 0.46, -0.64 * math.cos(ang) + 0.62 * math.sin(ang))
-            tb.set_camera_view(v, (0.5, 0.5, 0.5), 1.0)
-            mats.append(np.array(tb.camera_matrix))
-        orbit = {}
-        for hint in (1, 0):
-            eng.set_param("nerf_spec_hint", hint)
-            for m in mats[:warmup]:
-                tb.camera_matrix = m
-                eng.frame(spp=0, reset=True)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for m in mats[warmup:]:
-                tb.camera_matrix = m
-                eng.frame(spp=0, reset=True)
-            torch.cuda.synchronize()
-            orbit["hints" if hint else "no_hints"] = round((len(mats) - warmup) / (time.perf_counter() - t0), 1)
-        out["c2_orbit_1deg_per_frame"] = {"frames_per_s": orbit, "res": [800, 800],
-                                          "note": "camera orbiting the lego 1 degree per frame: the look-ahead hints come from the previous view"}
-    finally:
-        tb.close()
+    # (c) a moving camera: an orbit of 1 degree per frame at C2 (800x800) and at the benchmarked C3 (1080p + mesh)
+    out["c2_orbit_1deg_per_frame"] = orbit_leg("c2", 800, 800, model, warmup)
+    out["c3_orbit_1deg_per_frame"] = orbit_leg("c3", 1920, 1080, model, warmup)
     tb, eng, _ = S.make_engine("c2", width=1920, height=1080, model=model)
     try:
         NW, NH = eng.resolution()["nerf"]
@@ -515,9 +537,9 @@ def main():
     tail_gbs = tail_samples * BYTES_PER_SAMPLE / (ms_tail * 1e-3) / 1e9 if ms_tail > 0 else 0.0
     field_ms = ms_net + ms_tail
     field_gbs = evaluated * BYTES_PER_SAMPLE / (field_ms * 1e-3) / 1e9 if field_ms > 0 else 0.0
-    prof = traffic_profile(args.config)
+    prof = traffic_profile(args.config, samples / max(1, launches))
     traffic = None
-    if prof:
+    if prof and "refused" not in prof:
         net_prof = prof["kernels"].get("nerf_network_kernel")
         traffic = net_prof.get("hbm_bytes_per_launch") if net_prof else None
 
@@ -561,11 +583,14 @@ def main():
             "stages_ms_last_frame": {"frame": round(s0.ms_frame, 3), "raytrace": round(s0.ms_raytrace, 3), "nerf": round(s0.ms_nerf, 3),
                                      "shadow": round(s0.ms_shadow, 3), "overlay": round(s0.ms_overlay, 3)},
             "temporal_hints": "the speculative NeRF tail sizes each ray's look-ahead by its pixel's ray life in the previous "
-                              "frame (nerf_spec_hint; exact whatever the hint); the timed frames repeat one camera, so after the "
-                              "first frame the hints are exact; nerf_views.c2_orbit_1deg_per_frame measures a moving camera",
+                              "frame (nerf_spec_hint; exact whatever the hint), read only when the frame repeats that frame's view "
+                              "(spec_view_key); the timed frames repeat one camera, so after the first frame the hints are read; "
+                              "nerf_views.c2_orbit_1deg_per_frame / c3_orbit_1deg_per_frame measure a moving camera",
             "roofline": {"kernel": "nerf_network_kernel<4,1> (fused hash grid + SH + density/rgb MLP)", "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": prof["file"] if prof else None,
+                         "traffic_refused": prof.get("refused") if prof else None,
+                         "traffic_over_algorithmic": round(traffic / bytes_per_launch, 4) if traffic and bytes_per_launch else None,
                          "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
                          "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches, "samples_in_launches": int(samples),
                          "timing": "HIP events recorded by each launch's own dispatch (hipExtLaunchKernelGGL start/stop events) on the NeRF stream over the timed region" +

@@ -81,7 +81,8 @@ class orc_frame_params(ctypes.Structure):
                 ("nerf_on_nerf_shadow_threshold", ctypes.c_float), ("nerf_kernel_size", ctypes.c_int32),
                 ("light_samples", ctypes.c_uint32), ("path_trace_depth", ctypes.c_uint32), ("shadow_iters", ctypes.c_uint32),
                 ("shadow_steps", ctypes.c_uint32), ("lens_angle_constant", ctypes.c_float), ("syn_shadow_factor", ctypes.c_float),
-                ("rt_depth_offset", ctypes.c_float), ("exposure", ctypes.c_float), ("srgb_output", ctypes.c_int32)]
+                ("rt_depth_offset", ctypes.c_float), ("exposure", ctypes.c_float), ("srgb_output", ctypes.c_int32),
+                ("tonemap_curve", ctypes.c_int32)]
 
 
 _lib = None
@@ -118,7 +119,7 @@ def lib():
             "orc_render_frame": (None, [vp, vp, vp, vp, vp, vp, u32, vp, u32, vp, u32, vp, vp, vp, vp, vp, vp, vp]),
             "orc_num_threads": (i32, []), "orc_set_num_threads": (None, [i32]), "orc_set_mlp_accum": (None, [i32, i32]),
             "orc_set_visualization": (None, [i32, i32]),
-            "orc_set_motion_blur": (None, [vp, vp]), "orc_set_glow": (None, [i32, f32]), "orc_set_shadow_rng_mode": (None, [i32]),
+            "orc_set_motion_blur": (None, [vp, vp]), "orc_set_glow": (None, [i32, f32]), "orc_set_shadow_rng_mode": (None, [i32]), "orc_set_literal": (None, [i32]),
             "orc_set_gbuffer_out": (None, [vp, vp]),
             "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
             "orc_display": (None, [vp, i32, i32, i32, i32, vp, vp]),
@@ -131,6 +132,22 @@ def lib():
             fn.restype = res
             fn.argtypes = args
     return _lib
+
+
+class literal:
+    """Context manager: the oracle evaluates the reference's text as written (on = 1, the default) or the product's
+    restatements of its --use_fast_math build (on = 0: reciprocal-multiply box tests, integer powers by binary
+    exponentiation, the clamped overlay index; orc_set_literal, sng_oracle.h)."""
+    def __init__(self, on):
+        self.on = on
+
+    def __enter__(self):
+        lib().orc_set_literal(1 if self.on else 0)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_literal(1)
+        return False
 
 
 class mlp_accum:
@@ -324,7 +341,7 @@ def frame_params_from_engine(eng):
     p.nerf_kernel_size = int(g("nerf_shadow_samples")); p.light_samples = int(g("light_samples"))
     p.path_trace_depth = int(g("path_trace_depth")); p.shadow_iters = int(g("syn_shadow_samples")); p.shadow_steps = int(g("n_steps"))
     p.lens_angle_constant = g("lens_size"); p.syn_shadow_factor = g("syn_shadow_intensity"); p.rt_depth_offset = g("depth_offset")
-    p.exposure = g("exposure"); p.srgb_output = int(g("srgb"))
+    p.exposure = g("exposure"); p.srgb_output = int(g("srgb")); p.tonemap_curve = int(g("tonemap_curve"))
     return p
 
 

@@ -406,6 +406,8 @@ inline V2 bb_ray_intersect(const BBox& b, V3 pos, V3 dir) {
     if (tzmax < tmax) tmax = tzmax;
     return {tmin, tmax};
 }
+/* orc_set_literal (sng_oracle.h): 1 = the reference's text as written, 0 = the product's fast-math restatements */
+static int g_literal = 1;
 /* The BVH's box test: bounding_box.cuh:163-211 as the reference compiles it (--use_fast_math,
  * CMakeLists.txt:82, makes each (b - pos) / dir a multiply by rcp(dir)); restated as (b - pos) * y
  * with y = RN(1 / dir) per ray, the same expressions as the GPU's bvh_box_entry (sng_math.h). */
@@ -807,7 +809,12 @@ std::pair<int, float> ray_intersect_nodes(V3 ro, V3 rd, const float* nodes, cons
             }
         } else {
             struct DI { float dist; int idx; } ch[2];
-            for (int i = 0; i < 2; ++i) ch[i] = {bvh_box_entry(load_node(nodes, node.left + i).bb, ro, y), node.left + i};
+            /* BoundingBox::ray_intersect(...).x (triangle_bvh.cu:296-298): IEEE division as written, or the product's
+             * multiply by the per-ray reciprocal */
+            for (int i = 0; i < 2; ++i) {
+                const BBox& bb = load_node(nodes, node.left + i).bb;
+                ch[i] = {g_literal ? bb_ray_intersect(bb, ro, rd).x : bvh_box_entry(bb, ro, y), node.left + i};
+            }
             if (ch[0].dist < ch[1].dist) std::swap(ch[0], ch[1]); /* sorting_network<2>: descending */
             for (int i = 0; i < 2; ++i)
                 if (ch[i].dist < mint) {
@@ -908,6 +915,9 @@ inline float pow_small_int(float x, float n) {
     }
     return std::pow(x, n);
 }
+/* pow(x, n) of the render path's Phong term and shadow masks: powf as the text writes it (literal mode), or the
+ * product's pow_small_int */
+inline float pow_src(float x, float n) { return g_literal ? std::pow(x, n) : pow_small_int(x, n); }
 inline float srgb_to_linear(float s) { return s <= 0.04045f ? s / 12.92f : std::pow((s + 0.055f) / 1.055f, 2.4f); }
 inline float linear_to_srgb(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * std::pow(l, 0.41666f) - 0.055f; }
 
@@ -1403,7 +1413,7 @@ void orc_shade_nerf_shadows(const orc_volume* vdesc, const int32_t res[2], float
                         int hit = -1;
                         float syn_depth = depth_test_world(pos, l, objs, hit);
                         float syn_mask = syn_depth / full_d;
-                        overall = std::min(overall, pow_small_int(syn_mask, nerf_shadow_intensity));
+                        overall = std::min(overall, pow_src(syn_mask, nerf_shadow_intensity));
                         V3 fract_offset = full_d * thr * lpos;
                         float nerf_depth = std::min(full_d, depth_test_nerf_sd(n_steps, vol.cone, pos + fract_offset, lpos, vol, 0, vol.max_mip));
                         /* (full_d * (1.0 - thr)) is a double expression (1664) */
@@ -1420,7 +1430,7 @@ void orc_shade_nerf_shadows(const orc_volume* vdesc, const int32_t res[2], float
                 ++blend;
             }
         sum /= (float)blend;
-        sum = pow_small_int(sum, nerf_shadow_intensity);
+        sum = pow_src(sum, nerf_shadow_intensity);
         float* rgba = &frame_rgba[4 * idx];
         rgba[0] = srgb_to_linear(rgba[0]) * sum;
         rgba[1] = srgb_to_linear(rgba[1]) * sum;
@@ -1554,7 +1564,7 @@ struct SampledRay { V3 pos = v3s(0.0f), dir = v3s(0.0f); float pdf = 0.0f, atten
 inline V3 local_color(const orc_material& m, V3 L, V3 N, V3 R, V3 V, const orc_light& light) {
     float a = std::max(0.0f, dot(L, N));
     V3 kd = v3(m.kd[0], m.kd[1], m.kd[2]), ks = v3(m.ks[0], m.ks[1], m.ks[2]);
-    return a * kd * light.intensity + pow_small_int(std::max(0.0f, dot(R, V)), m.n) * ks;
+    return a * kd * light.intensity + pow_src(std::max(0.0f, dot(R, V)), m.n) * ks;
 }
 /* sng::shade_object: synerfgine/raytracer.cu:6-57 */
 V4 shade_object(V3 wi, SampledRay& ray, uint32_t shadow_count, HitRecord& hit, const orc_light* lights, uint32_t n_lights,
@@ -1581,7 +1591,7 @@ V4 shade_object(V3 wi, SampledRay& ray, uint32_t shadow_count, HitRecord& hit, c
                 out_nerf_shadow = std::min(nerf_shadow / full_dist, out_nerf_shadow);
                 float shadow = std::min(std::min(nerf_shadow, syn_shadow), full_dist);
                 float mask = smoothstep(shadow / full_dist);
-                mask = pow_small_int(mask, syn_shadow_factor);
+                mask = pow_src(mask, syn_shadow_factor);
                 V3 R = reflect(L, hit.normal);
                 V3 V = normalize(-wi);
                 color = color + local_color(mat, L, hit.normal, R, V, light) * mask;
@@ -1667,25 +1677,71 @@ void orc_raytrace(const orc_volume* vdesc, const float* camera, const orc_frame_
     }
 }
 
-/* sng::overlay_nerf: synerfgine/raytracer.cu:220-258 (Identity tonemap) */
+/* sng_tonemap: synerfgine/common.cu:186-243 (ETonemapCurve, common.h:113: 0 Identity, 1 ACES, 2 Hable, 3 Reinhard) */
+V3 sng_tonemap(V3 x, int curve) {
+    if (curve == 0) return x;
+    x = v3(std::max(x.x, 0.0f), std::max(x.y, 0.0f), std::max(x.z, 0.0f));
+    float k0, k1, k2, k3, k4, k5;
+    if (curve == 1) {   /* ACES approximation, pre-exposure cancelled into the constants */
+        k0 = 0.6f * 0.6f * 2.51f;
+        k1 = 0.6f * 0.03f;
+        k2 = 0.0f;
+        k3 = 0.6f * 0.6f * 2.43f;
+        k4 = 0.6f * 0.59f;
+        k5 = 0.14f;
+    } else if (curve == 2) {   /* Hable, white point 11.2, white scale and exposure bias folded in */
+        const float A = 0.15f, B = 0.50f, C = 0.10f, D = 0.20f, E = 0.02f, F = 0.30f;
+        k0 = A * F - A * E;
+        k1 = C * B * F - B * E;
+        k2 = 0.0f;
+        k3 = A * F;
+        k4 = B * F;
+        k5 = D * F * F;
+        const float W = 11.2f;
+        const float nom = k0 * (W * W) + k1 * W + k2;
+        const float denom = k3 * (W * W) + k4 * W + k5;
+        const float white_scale = denom / nom;
+        k0 = 4.0f * k0 * white_scale;
+        k1 = 2.0f * k1 * white_scale;
+        k2 = k2 * white_scale;
+        k3 = 4.0f * k3;
+        k4 = 2.0f * k4;
+    } else {   /* Reinhard on luminance */
+        const float Y = 0.2126f * x.x + 0.7152f * x.y + 0.0722f * x.z;
+        return x * (1.f / (Y + 1.0f));
+    }
+    const V3 sq = x * x;
+    const V3 nom = sq * k0 + x * k1 + k2;
+    const V3 denom = sq * k3 + x * k4 + k5;
+    return v3(nom.x / denom.x, nom.y / denom.y, nom.z / denom.z);
+}
+
+/* sng::overlay_nerf: synerfgine/raytracer.cu:220-258 */
 void orc_overlay(const orc_frame_params* P, const float* syn_rgba, const float* syn_depth, const float* nerf_rgba, const float* nerf_depth,
                  float* final_rgba, float* final_depth) {
     const int W = P->mesh_res[0], H = P->mesh_res[1], s = P->syn_px_scale;
     const int nW = W / s;
+    const int n_nerf = P->nerf_res[0] * P->nerf_res[1];
     float e = std::pow(2.0f, P->exposure);
+    const float qnan = std::numeric_limits<float>::quiet_NaN();
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
             int sid = x + y * W;
-            int nid = std::min((x / s) + (y / s) * nW, P->nerf_res[0] * P->nerf_res[1] - 1);  /* clamp as the product does */
+            int nid = (x / s) + (y / s) * nW;
+            float* f = &final_rgba[4 * (size_t)sid];
+            final_depth[sid] = syn_depth[sid];
+            if (nid >= n_nerf) {
+                if (g_literal) { f[0] = f[1] = f[2] = f[3] = qnan; continue; }   /* the reference reads past the buffer */
+                nid = n_nerf - 1;                                               /* the product clamps */
+            }
             const float* sr = &syn_rgba[4 * (size_t)sid];
             const float* nr = &nerf_rgba[4 * (size_t)nid];
             float sdepth = syn_depth[sid], ndepth = nerf_depth[nid];
             const float* use = (!P->show_nerf || sdepth - P->rt_depth_offset < ndepth) ? sr : nr;
-            float rgb[3] = {use[0] * e, use[1] * e, use[2] * e};
-            float* f = &final_rgba[4 * (size_t)sid];
-            for (int k = 0; k < 3; ++k) f[k] = P->srgb_output ? linear_to_srgb(rgb[k]) : rgb[k];
+            V3 rgb = sng_tonemap(v3(use[0] * e, use[1] * e, use[2] * e), P->tonemap_curve);
+            f[0] = rgb.x; f[1] = rgb.y; f[2] = rgb.z;
+            if (P->srgb_output) for (int k = 0; k < 3; ++k) f[k] = linear_to_srgb(f[k]);
             f[3] = use[3];
-            final_depth[sid] = sdepth;
         }
 }
 
@@ -2072,3 +2128,5 @@ extern "C" void orc_wavefront_schedule(const uint32_t* n_alive, uint32_t n, uint
         n_elements[i] = a ? wavefront_elements(a, n_steps[i]) : 0u;
     }
 }
+
+extern "C" void orc_set_literal(int32_t on) { g_literal = on ? 1 : 0; }

@@ -92,6 +92,7 @@ typedef struct {
     float rt_depth_offset;          /* RayTracer::m_depth_offset (overlay z-test) */
     float exposure;
     int32_t srgb_output;            /* EColorSpace::SRGB (engine.cu:406) */
+    int32_t tonemap_curve;          /* Testbed::m_tonemap_curve (engine.cu:406): ETonemapCurve 0 Identity, 1 ACES, 2 Hable, 3 Reinhard */
 } orc_frame_params;
 
 /* ---- primitives (KAT-level) --------------------------------------------- */
@@ -142,6 +143,13 @@ void orc_set_glow(int32_t mode, float y_cutoff);
 /* shade_nerf_shadows' light-sample RNG for nerf_shadow_samples > 0: 0 = the centre pixel's stream (this
  * library's kernels), 1 = the neighbour's stream as the reference's racy rand_state[idx] (serialised) */
 void orc_set_shadow_rng_mode(int32_t neighbour);
+/* 1 (default): the reference's text as written -- IEEE division in the BVH box test (bounding_box.cuh:163-211),
+ * powf for the Phong term and the shadow masks (material.cuh:96-98, raytracer.cu:6-57, testbed_nerf.cu:1614-1786),
+ * overlay_nerf's NeRF pixel index unclamped (raytracer.cu:242-246; an index past the buffer, which the reference
+ * reads out of bounds, gives NaN).  0: the product's restatements of the reference's --use_fast_math build
+ * (CMakeLists.txt:82): (b - o) * RN(1/d) box tests, integer powers by binary exponentiation, the clamped index --
+ * the forms libsng_hip.so evaluates, so GPU and oracle agree bit for bit. */
+void orc_set_literal(int32_t on);
 void orc_render_nerf_ngp(const orc_model* m, const orc_volume* v, const orc_camera* c, int32_t render_mode, float depth_scale,
                          float* frame_rgba /* W*H*4 */, float* frame_depth /* W*H */, orc_nerf_stats* stats);
 void orc_shade_nerf_shadows(const orc_volume* v, const int32_t res[2],

@@ -310,6 +310,7 @@ const std::map<std::string, double>& default_params() {
         {"res_factor", 64},                     // Testbed::m_fixed_res_factor (testbed.h:656)
         {"vo_scale", 4},                        // Engine::m_relative_vo_scale (engine.cuh:113)
         {"exposure", 0.0},                      // Testbed::m_exposure
+        {"tonemap_curve", 0},                   // Testbed::m_tonemap_curve (engine.cu:406): 0 Identity, 1 ACES, 2 Hable, 3 Reinhard
         {"path_trace_depth", 2},                // RayTracer::m_ray_iters (raytracer.cuh:160)
         {"light_samples", 2},                   // RayTracer::m_samples
         {"syn_shadow_samples", 4},              // RayTracer::m_shadow_iters
@@ -363,6 +364,7 @@ const std::map<std::string, double>& default_params() {
         {"nerf_spec_budget", 16777216},         // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax)); the
                                                 //   sample buffers are sized for it (16.8 M x 60 B ~ 1 GB of the 288 GB)
         {"nerf_spec_hint", 1},                  // a ray looks ahead as far as its pixel's ray lived last frame (exact; 0: opacity policy)
+        {"nerf_spec_hint_any_view", 0},         // 1: read the hints whatever view wrote them (tests: exact for any hint)
         {"nerf_spec_kmax", 16},                 // iterations one round marches ahead (<= 16)
         {"nerf_spec_k_policy", 1},              // per-ray look-ahead from the ray's opacity in all rounds but the last (exact)
         {"nerf_spec_prepare", 1},               // sample-parallel activations before the spec compositor (exact; 0: in the chain)
@@ -470,6 +472,8 @@ struct sng_ctx {
     DevBuf spec_t;                         // speculative tail rounds: march t of every sample ([sample][ray])
     DevBuf spec_hint;                      // per NeRF pixel: 1 + the iteration its ray ended at last frame (u8, 0 unknown)
     uint64_t spec_hint_px = 0;
+    uint64_t spec_hint_key = 0;            // the view the hints were written for (spec_view_key); another view reads none
+    uint64_t model_epoch = 0;              // bumped when the model or its occupancy changes (part of that key)
     DevBuf spec_pre, spec_pre_depth;       // spec_prepare: per network sample {rgb, alpha} and depth
     DevBuf band_rgba8;                     // sng_gather_rgba8: this rank's band as RGBA8
     uint32_t spec_rounds = 0;              // rounds enqueued by the last trace
@@ -610,6 +614,7 @@ void set_model(sng_ctx* c, const sng_nerf_config* cfg, const uint16_t* params, u
     c->cone = cfg->aabb_scale <= 1 ? 0.0f : 1.0f / 256.0f;
     c->has_model = true;
     c->has_bitfield = false;
+    ++c->model_epoch;
 }
 
 void build_occ_brick(sng_ctx* c, hipStream_t s);
@@ -638,6 +643,7 @@ void build_occ_brick(sng_ctx* c, hipStream_t s) {
     launch_occ_brick(c->d_occ_linear.as<uint32_t>(), c->d_occ_brick_aux.as<uint32_t>(), c->d_occ_brick.as<uint32_t>(),
                      c->d_occ_brick_aux.as<uint32_t>() + 4096, s);
     c->occ_brick_dirty = true;
+    ++c->model_epoch;
 }
 
 Volume make_volume(const sng_ctx* c) {
@@ -1094,6 +1100,28 @@ uint64_t ref_slots_of(const sng_ctx* c) {
 // only used when a schedule communicator is attached (Sched).
 uint8_t* spec_hint_buf(sng_ctx* c);
 
+// The view a frame's NeRF rays come from: camera0 / camera1 / rolling shutter, focal length, screen centre, NeRF
+// resolution and the model (FNV-1a over the bytes).  The speculative rounds read the per-pixel look-ahead hints only
+// when the hints were written for the same view: on a moving camera a pixel's last ray ended elsewhere, and the
+// opacity policy (spec_k_of) sizes the look-ahead better (round 3: 1 deg/frame orbit 571 frames/s with hints read,
+// 623 without).  The pixel jitter (spp) is not part of it: sub-pixel moves keep the hints close.
+uint64_t spec_view_key(const sng_ctx* c, f2 focal, f2 sc) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        const uint8_t* b = static_cast<const uint8_t*>(p);
+        for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
+    };
+    mix(c->cam, sizeof(c->cam));
+    mix(&c->has_cam1, sizeof(c->has_cam1));
+    if (c->has_cam1) mix(c->cam1, sizeof(c->cam1));
+    mix(c->rolling_shutter, sizeof(c->rolling_shutter));
+    mix(&focal, sizeof(focal));
+    mix(&sc, sizeof(sc));
+    mix(c->nerf_res, sizeof(c->nerf_res));
+    mix(&c->model_epoch, sizeof(c->model_epoch));
+    return h | 1ull;   // never 0 (no hints)
+}
+
 // One reduction of the frame-wide schedule (sum over ranks of dev[0..n), in place on the NeRF stream):
 // RCCL all-reduce, the host reducer (a stream sync + callback), or the next replay record (an async copy from
 // pinned memory: a band timed on one GPU as its rank runs it, without a communicator).
@@ -1365,6 +1393,11 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 sa.pre = pre ? c->spec_pre.as<float4>() : nullptr;
                 sa.pre_depth = pre ? c->spec_pre_depth.as<float>() : nullptr;
                 sa.hint = spec_hint_buf(c);
+                {   // hints of this view?  (this frame's rays rewrite them either way)
+                    const uint64_t key = spec_view_key(c, a.focal, sc);
+                    sa.hint_read = (key == c->spec_hint_key || c->p("nerf_spec_hint_any_view") != 0.0) ? 1 : 0;
+                    c->spec_hint_key = sa.hint ? key : 0;
+                }
                 // rays alive after the head: at most the band's pixels (grid-stride over the device count)
                 const uint32_t sblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 4));
                 for (uint32_t r = 0; r < rounds; ++r) {
@@ -1743,6 +1776,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     // ---- overlay (RayTracer::overlay, raytracer.cu:372-392) after both streams
     HIPCHK(hipStreamWaitEvent(c->s_nerf, c->ev_rt1, 0));
     launch_overlay(MW, y0, y1, S, MW / S, NW * NH, show_nerf ? 1 : 0, (float)c->p("depth_offset"), std::pow(2.0f, (float)c->p("exposure")), (int)c->p("srgb"),
+                   (int)c->p("tonemap_curve"),
                    c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->final_rgba.as<float4>(),
                    c->final_depth.as<float>(), c->s_nerf);
     HIPCHK(hipGetLastError());
@@ -2598,6 +2632,8 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
             return;
         }
         if (!default_params().count(k)) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
+        if (k == "tonemap_curve" && !(v == 0.0 || v == 1.0 || v == 2.0 || v == 3.0))
+            throw SngError(SNG_ERR_INVALID, "tonemap_curve is an ETonemapCurve: 0 Identity, 1 ACES, 2 Hable, 3 Reinhard");
         c->params[k] = v;
         c->mesh_reset = true;
         if ((k == "fast_slab" || k == "scene_lds" || k == "bvh_wide") && !c->objs.empty()) upload_scene(c);

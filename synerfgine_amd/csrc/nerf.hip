@@ -581,7 +581,7 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
             uint32_t K_i = K < left ? K : left;
             // the ray's own end in the last frame, when it is still ahead: look exactly that far; otherwise the
             // opacity policy.  Any K is exact (the round's replay stops where the wavefront would).
-            const uint32_t h = a.hint ? (uint32_t)a.hint[__float_as_uint(di.w)] : 0u;   // relative to the tail's first iteration
+            const uint32_t h = (a.hint && a.hint_read) ? (uint32_t)a.hint[__float_as_uint(di.w)] : 0u;   // relative to the tail's first iteration
             if (h != 0u && h - 1u >= k_i - base_k) K_i = min(K_i, h - (k_i - base_k));
             else if (a.k_policy) K_i = min(K_i, spec_k_of(a.in.rgba[i].w));
             const f3 idir = inv(d);

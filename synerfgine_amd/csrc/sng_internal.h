@@ -334,6 +334,7 @@ struct SpecArgs {
     uint8_t* hint;                // per NeRF pixel: 1 + the iteration its ray ended at in the last frame, counted from the
                                   // tail's first iteration (0: unknown);
                                   // a ray looks ahead just that far (exact whatever the hint: it only sizes the round)
+    int hint_read;                // 0: the hints are another view's (the camera moved): written, not read
 };
 constexpr uint32_t SPEC_KMAX = 16;
 
@@ -407,7 +408,7 @@ void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, ui
 void launch_display(const float4* img, int W, int H, int OW, int OH, f3 clear, uint8_t* out, hipStream_t s);
 void launch_rgba8_band(const float4* img, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
-                    const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s);
+                    int tonemap, const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s);
 void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s);
 
 // error carrying an sng_status code (capi.cpp turns it into the return value + sng_last_error)

@@ -749,9 +749,11 @@ def test_high_phong_exponent_frame_matches_oracle(tmp_path, n_exp):
 def test_spec_hints_from_another_view_are_exact():
     """The speculative rounds size each ray's look-ahead by its pixel's ray life in the last frame
     (nerf_spec_hint).  Hints from a different camera only change the work, never the frame: after a frame
-    at one view, the next view equals the per-iteration wavefront's bit for bit."""
+    at one view, the next view equals the per-iteration wavefront's bit for bit.  (By default another view's
+    hints are not read at all -- spec_view_key; nerf_spec_hint_any_view = 1 reads them here.)"""
     from synerfgine_amd import scene as S  # noqa: F401
     tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, "c3")
+    eng.set_param("nerf_spec_hint_any_view", 1)
     try:
         views = [((0.62, 0.46, -0.64), 1.0), ((-0.6, 0.5, 0.6), 1.3), ((0.0, -1.0, 0.0), 0.9)]
         mats = []
@@ -772,5 +774,35 @@ def test_spec_hints_from_another_view_are_exact():
                     for a, b in zip(ref[vi], got):
                         assert np.array_equal(np.asarray(a).view(np.uint32) if np.asarray(a).dtype == np.float32 else a,
                                               np.asarray(b).view(np.uint32) if np.asarray(b).dtype == np.float32 else b), vi
+    finally:
+        tb.close()
+
+
+def test_spec_hints_are_read_for_the_same_view_only():
+    """spec_view_key: a repeated view reads the hints its last frame wrote (less look-ahead: fewer evaluated samples),
+    a moved camera does not; both frames equal the hint-free frame bit for bit."""
+    tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, "c3")
+    try:
+        eng.set_param("nerf_spec_hint", 0)
+        base = eng.frame(spp=0, reset=True)
+        ref, evals_none = base.download("nerf_rgba"), base.spec_evals
+        eng.set_param("nerf_spec_hint", 1)
+        eng.frame(spp=0, reset=True)                  # writes the hints of this view
+        same = eng.frame(spp=0, reset=True)           # reads them
+        assert np.array_equal(same.download("nerf_rgba").view(np.uint32), ref.view(np.uint32))
+        assert same.spec_evals < evals_none, (same.spec_evals, evals_none)
+        m = np.array(tb.camera_matrix)
+        m2 = m.copy()
+        m2.reshape(-1)[-1] += 1e-3                    # the camera moved: hints of the old view are not read
+        tb.camera_matrix = m2
+        eng.set_param("nerf_spec_hint", 0)
+        moved_none = eng.frame(spp=0, reset=True)
+        tb.camera_matrix = m
+        eng.set_param("nerf_spec_hint", 1)
+        eng.frame(spp=0, reset=True)
+        tb.camera_matrix = m2
+        moved = eng.frame(spp=0, reset=True)
+        assert moved.spec_evals == moved_none.spec_evals, (moved.spec_evals, moved_none.spec_evals)
+        assert np.array_equal(moved.download("nerf_rgba").view(np.uint32), moved_none.download("nerf_rgba").view(np.uint32))
     finally:
         tb.close()

@@ -58,7 +58,7 @@ for step in "$@"; do
         timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE -d $d/MFMA -o run --output-format csv -- python3 bench.py $a > $d.MFMA.log 2>&1
         rc=$?; echo "MFMA rc=$rc"
       fi
-      [ $rc -eq 0 ] && python3 tools/pmc_summary.py $d $OUT/pmc_traffic_${cfg:-c3}.json ${cfg:-c3} > $log 2>&1; rc=$? ;;
+      [ $rc -eq 0 ] && python3 tools/pmc_summary.py $d $OUT/pmc_traffic_${cfg:-c3}.json ${cfg:-c3} $d.FETCH_SIZE.log > $log 2>&1; rc=$? ;;
     sq|sqlds)
       # SQ instruction counts + kernel durations in one counter pass (serialised kernels) -> VALU roofline;
       # sqlds: LDS-array cycles / bank conflicts / waits instead

@@ -4,7 +4,10 @@ FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB.  MI355X_MICROARCH
 on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads -> x2; WRITE_SIZE is exact for
 16-B-per-lane stores.  half_to_float_kernel (reads 2 B, writes 4 B per density-grid cell, 128^3
 cells, runs once per model load) is reported beside as a calibration point.
-usage: python tools/pmc_summary.py <pmc dir> <out.json>
+usage: python tools/pmc_summary.py <pmc dir> <out.json> [config] [bench log of the FETCH pass]
+
+With the bench log, the file also records the counted run's own network samples per launch and launches per
+frame (its bench.py line), which bench.py compares with the timed line before it quotes the traffic.
 """
 import csv
 import glob
@@ -91,6 +94,21 @@ def main():
                        "note": "GRBM_GUI_ACTIVE is the sum over the 8 XCDs (137 K cycles = the 57 us launch at 2.4 GHz); "
                                "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES (16 per v_mfma_f32_16x16x32_f16, summed over SIMDs) / "
                                "(kernel cycles x 1024 SIMDs); flop = MOPS_F16 x 512 (= samples x 20,480, SURVEY 8d)"}
+    if len(sys.argv) > 4:   # the counted run's own bench line: samples per network launch, launches per frame
+        line = None
+        for l in open(sys.argv[4]):
+            if l.startswith('{"metric"'):
+                line = json.loads(l)
+        if line:
+            rf = line["roofline"]
+            res["bench_line"] = {"samples_per_launch": rf["samples_in_launches"] / max(1, rf["launches"]),
+                                 "launches_per_frame": rf["launches"] / max(1, line["steps"]), "steps": line["steps"],
+                                 "warmup": line["warmup"], "workload": line["config"]["workload"]}
+            if "nerf_network_kernel" in roof:
+                v = roof["nerf_network_kernel"]
+                v["samples_per_launch"] = res["bench_line"]["samples_per_launch"]
+                v["algorithmic_bytes_per_launch"] = v["samples_per_launch"] * (28 + 8 * 8 * 4 * 2 + 8)
+                v["traffic_over_algorithmic"] = v["hbm_bytes_per_launch"] / v["algorithmic_bytes_per_launch"]
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * max(1, kv[1]["launches"]))[:12]:
