@@ -274,6 +274,52 @@ def abm_sweep(model, frames, warmup):
         tb.close()
 
 
+def train_leg(steps=200, warmup=50, seed=1337):
+    """BASELINE config C5: online training on the reference's lego set (data/nerf/lego400, 95
+    views, every 20th held out as tools/train_lego.py does) from a fresh init, batch 2^18 samples per step
+    (m_training_batch_size, testbed.h:1103): `warmup` untimed steps, then `steps` timed ones (host wall clock
+    around sng_train, which syncs once per step for the batch counters as NerfCounters::update_after_training
+    does, testbed_nerf.cu:3272-3296).  fp16 parameters / activations / gradient GEMM operands with f32 master
+    weights and accumulation, tcnn's types (BASELINE.json C5 names bf16)."""
+    import numpy as np
+    from synerfgine_amd import Testbed, nerf_data, synthetic
+    d = os.path.join(REPO, "data", "nerf", "lego400")
+    imgs, xf, focal, pp = nerf_data.load_nerf_synthetic(d)
+    angle = json.load(open(os.path.join(d, "transforms.json")))["camera_angle_x"]
+    import math
+    focal[:] = 0.5 * imgs.shape[2] / math.tan(0.5 * angle)   # the Blender focal (DESIGN.md §7)
+    train = [i for i in range(len(imgs)) if i % 20]
+    tb = Testbed(0)
+    try:
+        cfg, params = synthetic.random_init(seed)
+        tb.set_nerf_model(cfg, params)
+        tb.set_training_dataset(imgs[train], xf[train], focal[train], pp[train])
+        tb.train_reset(seed)
+        tb.train(warmup)
+        import torch
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = tb.train(steps)
+        el = time.perf_counter() - t0
+        samples = int(st["measured_batch"])
+        # algorithmic work of one step at the measured (compacted) batch: the five weight gradients dW = delta act^T
+        # (K = samples; 64x32 + 16x64 + 64x32 + 64x64 + 16x64 = 10,240 weights), forward + backward of the fused MLPs,
+        # and the hash-grid gradient scatter (8 levels x 8 corners x F = 4 f32 adds per sample)
+        dw_flop = 2 * samples * 10240
+        return {"steps_per_s": round(steps / el, 1), "ms_per_step": round(1e3 * el / steps, 3),
+                "ms_per_step_device": round(st["ms"] / steps, 3), "steps": steps, "warmup": warmup,
+                "batch_target": 1 << 18, "measured_batch": samples, "rays_per_batch": int(st["rays_per_batch"]),
+                "loss_after": round(float(st["loss"]), 6), "step_after": int(st["step"]),
+                "algorithmic_per_step": {"dw_gemm_flop": dw_flop, "mlp_fwd_bwd_flop": 3 * 20480 * samples,
+                                         "grid_scatter_atomic_bytes": samples * 8 * 8 * 4 * 4},
+                "dtype": "fp16 params / activations / GEMM operands, f32 master weights, gradients and accumulation "
+                         "(tcnn's network_precision_t; BASELINE.json C5 says bf16)",
+                "data": "data/nerf/lego400 (the reference's lego set at 400x400), 90 training views, fresh init (seed 1337)",
+                "kernel_profile": "profiles/r04_train_kernel_table.txt (rocprofv3 of tools/train_bench.py)"}
+    finally:
+        tb.close()
+
+
 def _srgb(rgba):
     import numpy as np
     lin = np.clip(rgba[..., :3], 0, None)
@@ -673,6 +719,10 @@ def main():
                 result["nerf_views"] = nerf_views("lego", 10, 2, cpu_check=not args.no_cpu_baseline)
         except Exception as e:
             result["nerf_views"] = {"error": repr(e)}
+        try:
+            result["train"] = train_leg()
+        except Exception as e:
+            result["train"] = {"error": repr(e)}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
             legs, threads = cpu_baseline_c1(args.model if args.config != "c4" else "lego", args.cpu_runs)

@@ -392,7 +392,7 @@ struct sng_ctx {
     int device = 0;
     int n_cus = 256;
     hipStream_t s_nerf = nullptr, s_rt = nullptr;
-    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr, ev_fused0 = nullptr, ev_fused1 = nullptr, ev_os0 = nullptr, ev_os1 = nullptr, ev_alive = nullptr;
+    hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr, ev_fused0 = nullptr, ev_fused1 = nullptr, ev_os0 = nullptr, ev_os1 = nullptr, ev_alive = nullptr, ev_brick = nullptr;
     std::vector<hipEvent_t> net_events;
 
     // model
@@ -491,7 +491,7 @@ struct sng_ctx {
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
     DevBuf d_seq;
     MarchCtrl* h_ctrl = nullptr;
-    uint32_t* h_alive = nullptr;  // pinned readback [chunk][2], [4..5] host-reducer exchange
+    uint32_t* h_alive = nullptr;  // pinned readback [chunk][2], [6] spec_ok, [7] occupancy brick count
     SchedComm sched_comm;         // frame-wide step schedule across ranks (comm.cpp)
     DevBuf d_params;              // the model's fp16 parameter blob (tcnn order), training source
 
@@ -642,6 +642,9 @@ void build_occ_brick(sng_ctx* c, hipStream_t s) {
     c->d_occ_brick_aux.ensure((4096 + 4) * 4);
     launch_occ_brick(c->d_occ_linear.as<uint32_t>(), c->d_occ_brick_aux.as<uint32_t>(), c->d_occ_brick.as<uint32_t>(),
                      c->d_occ_brick_aux.as<uint32_t>() + 4096, s);
+    // the brick count travels to pinned memory behind the rebuild; render_frame waits for this event only
+    HIPCHK(hipMemcpyAsync(&c->h_alive[7], c->d_occ_brick_aux.as<uint32_t>() + 4096, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(c->ev_brick, s));
     c->occ_brick_dirty = true;
     ++c->model_epoch;
 }
@@ -1066,8 +1069,11 @@ void resize(sng_ctx* c) {
 }
 
 void ensure_samples(sng_ctx* c, uint32_t target) {
-    // the speculative rounds' sample budget shares these buffers (nerf_spec_budget)
-    const size_t spec = c->p("nerf_spec_rounds") > 0 ? (size_t)std::max(1.0, c->p("nerf_spec_budget")) : 0;
+    // the speculative rounds' sample budget shares these buffers (nerf_spec_budget): a round marches at most kmax
+    // iterations of 8 samples per ray, so a small frame (or a training-only context, ray_cap 0) needs no more
+    const size_t kmax = (size_t)std::min<double>(SPEC_KMAX, std::max(1.0, c->p("nerf_spec_kmax")));
+    const size_t spec = c->p("nerf_spec_rounds") > 0 ? std::min((size_t)std::max(1.0, c->p("nerf_spec_budget")),
+                                                                MAX_STEPS_BETWEEN_COMPACTION * kmax * c->ray_cap) : 0;
     size_t cap = std::max(std::max<size_t>(target, c->ray_cap), spec) + 64;
     if (cap > c->sample_cap) {
         c->coords.ensure(cap * 7 * 4);
@@ -1583,8 +1589,8 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     // (engine.cu:386-397 passes m_nerf.density_grid_bitfield unconditionally)
     Volume vol{};
     if (c->occ_brick_dirty && c->d_occ_brick_aux.p) {   // the brick count of the last occupancy rebuild
-        HIPCHK(hipDeviceSynchronize());
-        HIPCHK(hipMemcpy(&c->occ_brick_n, c->d_occ_brick_aux.as<uint32_t>() + 4096, 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipEventSynchronize(c->ev_brick));
+        c->occ_brick_n = c->h_alive[7];
         c->occ_brick_dirty = false;
     }
     if (c->has_model && c->has_bitfield) vol = make_volume(c);
@@ -2063,7 +2069,7 @@ void ctx_create(const sng_ctx_desc* desc, sng_ctx** out) {
     HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_nerf, hipStreamNonBlocking, prio_hi));
     HIPCHK(hipStreamCreateWithPriority(&c->s_rt, hipStreamNonBlocking, prio_lo));
-    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go, &c->ev_fused0, &c->ev_fused1, &c->ev_os0, &c->ev_os1, &c->ev_alive}) HIPCHK(hipEventCreate(e));
+    for (hipEvent_t* e : {&c->ev_start, &c->ev_rt0, &c->ev_rt1, &c->ev_nerf0, &c->ev_nerf1, &c->ev_shadow1, &c->ev_end, &c->ev_rt_go, &c->ev_fused0, &c->ev_fused1, &c->ev_os0, &c->ev_os1, &c->ev_alive, &c->ev_brick}) HIPCHK(hipEventCreate(e));
     HIPCHK(hipHostMalloc((void**)&c->h_ctrl, sizeof(MarchCtrl), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&c->h_alive, 8 * sizeof(uint32_t), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&c->h_os, sizeof(OnestepState), hipHostMallocDefault));
@@ -2089,7 +2095,7 @@ void ctx_destroy(sng_ctx* c) {
                       &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_counts, &c->spec_t, &c->tail_live, &c->sched_hint, &c->msr_hist, &c->march_log, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); c->ray_kk[b].release(); }
-    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1, c->ev_alive}) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1, c->ev_alive, c->ev_brick}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);

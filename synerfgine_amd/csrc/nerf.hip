@@ -547,7 +547,10 @@ __global__ __launch_bounds__(THREADS) void spec_generate_kernel(SpecArgs a) {
     const uint32_t base_k = ctrl->spec_base_k, base_istep = ctrl->spec_base_istep;
     const bool kk_in = ctrl->spec_kk_valid[p] != 0u;   // per-ray iteration indices (after a round), else all at base_k
     uint32_t K = 0;   // the round's look-ahead bound; a ray's own may be smaller (k_policy, MARCH_ITER)
-    if (n_alive > 0 && istep0 < MARCH_ITER) {
+    // i_step[p] after a round is its largest look-ahead's (istep0 + 8 K); rays that looked ahead less are behind it.
+    // Every survivor of a round is below MARCH_ITER (its last iteration was not the `last` one), so with per-ray
+    // indices the round runs whatever i_step[p] says, and each ray's own `left` bounds its look-ahead.
+    if (n_alive > 0 && (kk_in || istep0 < MARCH_ITER)) {
         K = a.budget / (MAX_STEPS_BETWEEN_COMPACTION * n_alive);
         K = K < 1u ? 1u : (K > a.kmax ? a.kmax : K);
     }

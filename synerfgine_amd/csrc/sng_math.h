@@ -660,7 +660,20 @@ struct Tri { f3 a, b, c; };                                 // Triangle (36 B)
 // (its triangle range travels in the stack entry).  Each box is stored slab by slab
 // (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z) so that an axis is one packed-f32 register pair.
 // ref >= 0: inner record index; ref < 0: leaf, ~ref = first_triangle | triangle_count << 24.
-struct alignas(16) BvhWide { float s0[6], s1[6]; int ref0, ref1, pad0, pad1; };
+// Records are 80 B apart (one 16-B pad slot): ds_read_b128 serves 16 lanes per LDS cycle from the 16 slots of a
+// 256-B bank row, and the q-th load of record i sits in slot (5 i + q) mod 16 -- distinct for 16 consecutive
+// records -- where a 64-B stride put every record's q-th load in one of only 4 slots (up to 4-way conflicts
+// between lanes walking different records).
+#ifndef SNG_WIDE_PAD
+#define SNG_WIDE_PAD 1
+#endif
+struct alignas(16) BvhWide {
+    float s0[6], s1[6];
+    int ref0, ref1, pad0, pad1;
+#if SNG_WIDE_PAD
+    int pad2[4];
+#endif
+};
 constexpr uint32_t WIDE_MAX_BEGIN = 1u << 24, WIDE_MAX_COUNT = 127u;
 constexpr int WIDE_DONE = (int)0x80000000;   // traversal sentinel; wide_bvh never encodes a leaf as ~0x7FFFFFFF
 // Traversal copy of a triangle (capi.cpp upload_scene): a, e1 = b - a, e2 = c - a and n = cross(e1, e2),

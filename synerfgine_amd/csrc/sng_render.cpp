@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
+#include <signal.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -297,17 +298,32 @@ int main(int argc, char** argv) {
         const pid_t pid = fork();
         if (pid < 0) { std::perror("fork"); return 1; }
         if (pid == 0) {
+            // keep only this rank's pipe ends: a sibling that dies then closes the last write end of a pipe, so a
+            // reader sees EOF instead of blocking forever
+            for (int k = 1; k < o.gpus; ++k) {
+                if (r != k) close(rd[k - 1]);
+                if (r != 0) close(wr[k - 1]);
+            }
             const int rc = run_rank(o, r, o.gpus, r > 0 ? rd[r - 1] : -1, r == 0 ? wr : std::vector<int>{});
             std::fflush(stdout);
             _exit(rc);
         }
         kids.push_back(pid);
     }
+    for (int k = 1; k < o.gpus; ++k) { close(rd[k - 1]); close(wr[k - 1]); }
+    // the first rank that fails ends the run: the others would wait for it in RCCL or in the id pipe
     int worst = 0;
-    for (pid_t pid : kids) {
+    std::vector<bool> reaped(kids.size(), false);
+    for (size_t left = kids.size(); left > 0;) {
         int st = 0;
-        waitpid(pid, &st, 0);
+        const pid_t pid = waitpid(-1, &st, 0);
+        if (pid < 0) break;
+        for (size_t k = 0; k < kids.size(); ++k)
+            if (kids[k] == pid && !reaped[k]) { reaped[k] = true; --left; }
         const int rc = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+        if (rc != 0 && worst == 0)
+            for (size_t k = 0; k < kids.size(); ++k)
+                if (!reaped[k]) kill(kids[k], SIGTERM);
         worst = std::max(worst, rc);
     }
     return worst;

@@ -10,6 +10,8 @@
 #   pmc[:CFG[:ARGS]]       FETCH_SIZE / WRITE_SIZE / MFMA PMC passes (one rocprofv3 run each) + tools/pmc_summary.py
 #   sq[:CFG[:ARGS]]        SQ_INSTS_* + SQ_WAVE_CYCLES pass with kernel trace + tools/sq_summary.py (VALU roofline)
 #   py:SCRIPT[:ARGS]       python3 tools/SCRIPT ARGS
+#   profpy:SCRIPT[:ARGS]   rocprofv3 --kernel-trace --stats of python3 tools/SCRIPT ARGS (+ kernel table)
+#   pmcpy:SCRIPT[:ARGS]    FETCH_SIZE / WRITE_SIZE / MFMA passes over python3 tools/SCRIPT ARGS + tools/pmc_summary.py
 # Output goes to gpurun_out/$TAG/ (TAG defaults to "run"), one log per step.
 set -o pipefail
 export TMPDIR=/tmp
@@ -72,6 +74,24 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python3 -u tools/$cfg $args > $log 2>&1
       rc=$?; tail -c 3000 $log; echo ;;
+    profpy)
+      d=$OUT/prof$n
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- python3 tools/$cfg $args > $log 2>&1
+      rc=$?
+      [ $rc -eq 0 ] && python3 tools/kernel_table.py $(find $d -name "*kernel_trace.csv" | head -1) > $d/kernel_table.txt 2>&1 && head -30 $d/kernel_table.txt ;;
+    pmcpy)
+      d=$OUT/pmc$n
+      rc=0
+      for c in FETCH_SIZE WRITE_SIZE; do
+        kt=""; [ $c = FETCH_SIZE ] && kt="--kernel-trace"
+        timeout -s KILL 300 rocprofv3 $kt --pmc $c -d $d/$c -o run --output-format csv -- python3 tools/$cfg $args > $d.$c.log 2>&1
+        rc=$?; echo "$c rc=$rc"; [ $rc -ne 0 ] && break
+      done
+      if [ $rc -eq 0 ]; then
+        timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE -d $d/MFMA -o run --output-format csv -- python3 tools/$cfg $args > $d.MFMA.log 2>&1
+        rc=$?; echo "MFMA rc=$rc"
+      fi
+      [ $rc -eq 0 ] && python3 tools/pmc_summary.py $d $OUT/pmc_${cfg%.py}.json ${cfg%.py} > $log 2>&1; rc=$? ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -50,7 +50,9 @@ def main():
     # per-launch HBM bytes of the kernels bench.py reports, keyed by plain name (launch-weighted over variants)
     roof = {}
     for key in ("nerf_network_kernel", "nerf_fused_kernel", "nerf_onestep_kernel", "generate_kernel", "composite_kernel", "raytrace_kernel",
-                "shadow_rays_kernel", "rt_accumulate_kernel", "shade_shadow_kernel", "init_rays_kernel"):
+                "shadow_rays_kernel", "rt_accumulate_kernel", "shade_shadow_kernel", "init_rays_kernel", "shadow_term_kernel",
+                "msr_generate_kernel", "msr_commit_kernel", "train_field_kernel", "train_dw_kernel", "train_generate_kernel",
+                "train_adam_kernel", "train_loss_kernel"):
         ks = [k for k in kernels if key in k]
         n = sum(kernels[k]["launches"] for k in ks)
         if not n:
@@ -94,6 +96,18 @@ def main():
                        "note": "GRBM_GUI_ACTIVE is the sum over the 8 XCDs (137 K cycles = the 57 us launch at 2.4 GHz); "
                                "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES (16 per v_mfma_f32_16x16x32_f16, summed over SIMDs) / "
                                "(kernel cycles x 1024 SIMDs); flop = MOPS_F16 x 512 (= samples x 20,480, SURVEY 8d)"}
+    # MFMA pass, every kernel: busy fraction and flop per launch (the training GEMMs as well as the network)
+    if glob.glob(f"{d}/MFMA/**/*counter_collection.csv", recursive=True):
+        busy, mops, gui = (load(d, c, "MFMA") for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F16", "GRBM_GUI_ACTIVE"))
+        per = {}
+        for k in busy:
+            b, m, g = busy[k], mops.get(k, []), gui.get(k, [])
+            if not b or not g or not sum(m):
+                continue
+            ba, ma, ga = sum(b) / len(b), sum(m) / len(m), sum(g) / len(g)
+            per[k] = {"launches": len(b), "flop_per_launch": ma * 512, "mfma_busy_frac": ba / (ga / N_XCD * N_SIMD) if ga else None,
+                      "mfma_tflops": ma * 512 / (ga / N_XCD / 2.4e9) / 1e12 if ga else None}
+        res["mfma_per_kernel"] = per
     if len(sys.argv) > 4:   # the counted run's own bench line: samples per network launch, launches per frame
         line = None
         for l in open(sys.argv[4]):
