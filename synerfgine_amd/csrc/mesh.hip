@@ -308,25 +308,31 @@ template <bool LDS, bool CNT = false>
 __device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, Hit& h) {
     const f3 off = origin + dir * MIN_DEPTH;
     if constexpr (CNT) cx.cnt[0] += 1u;
-    int out_obj = -1;
-    h.t = MAX_DEPTH;
+    // only the winner's (object, triangle, t) stay live across the objects' traversals; its record is formed once
+    // after them, from the same values as the reference forms it at each improvement (common.cu:58-64)
+    int out_obj = -1, out_tri = 0;
+    float best = MAX_DEPTH;
+    for (int c = 0; c < n_objs; ++c) {
+        int tri;
+        const float t = object_intersect(off, dir, objs[c], cx, tri);
+        if (t < best && t > MIN_DEPTH) {
+            out_obj = c;
+            out_tri = tri;
+            best = t;
+        }
+    }
+    h.t = best;
     h.normal = splat(0.0f);
     h.mat = -1;
     h.perturb = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)};
-    for (int c = 0; c < n_objs; ++c) {
-        int tri;
-        const ObjectGpu& o = objs[c];
-        const float t = object_intersect(off, dir, o, cx, tri);
-        if (t < h.t && t > MIN_DEPTH) {
-            out_obj = c;
-            h.t = t;
-            h.mat = o.mat_id;
-            const Tri tr = o.tris[tri];
-            const f3 N = tri_normal(tr);
-            h.normal = mul(o.rot, N);
-            const f3 T = normalize((tr.a + tr.b + tr.c) / 3.0f - tr.a);   // Triangle::get_perturb_matrix (triangle.cuh:164-170)
-            h.perturb = {T, cross(T, N), N};
-        }
+    if (out_obj >= 0) {
+        const ObjectGpu& o = objs[out_obj];
+        h.mat = o.mat_id;
+        const Tri tr = o.tris[out_tri];
+        const f3 N = tri_normal(tr);
+        h.normal = mul(o.rot, N);
+        const f3 T = normalize((tr.a + tr.b + tr.c) / 3.0f - tr.a);   // Triangle::get_perturb_matrix (triangle.cuh:164-170)
+        h.perturb = {T, cross(T, N), N};
     }
     h.pos = origin + h.t * dir;
     return out_obj;
