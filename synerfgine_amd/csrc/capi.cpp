@@ -1342,19 +1342,19 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 launch_msr_schedule(ma, c->s_nerf);
                 launch_msr_commit(ma, mblocks, c->s_nerf);
                 HIPCHK(hipGetLastError());
+                // the next round's frame-wide count is reduced before the one readback of the round (a no-op round's
+                // reduction is unused; every rank makes it, as every rank sees the same no-op)
+                reduce_sched(p ^ 1);
                 HIPCHK(hipMemcpyAsync(c->h_ctrl, ctrl, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
                 HIPCHK(hipStreamSynchronize(c->s_nerf));
                 const MarchCtrl& hc = *c->h_ctrl;
                 if (hc.msr_K[p] == 0) break;   // no-op: the rays are still in buffer p
                 ++net_launches;
                 ++c->msr_rounds;
-                reduce_sched(p ^ 1);
                 p ^= 1;
                 iter = hc.n_iter;
                 // the (frame-wide) count the next round starts from
-                HIPCHK(hipMemcpyAsync(c->h_alive, sched_src + p, 4, hipMemcpyDeviceToHost, c->s_nerf));
-                HIPCHK(hipStreamSynchronize(c->s_nerf));
-                known_alive = c->h_alive[0];
+                known_alive = gsched ? hc.sched_alive[p] : hc.n_alive[p];
                 if (known_alive == 0) { done = true; break; }
                 if ((uint64_t)known_alive * MAX_STEPS_BETWEEN_COMPACTION <= target) {   // the 8-step tail's regime
                     if (!wavefront_only && c->p("nerf_fused") != 0.0) { fuse = true; fuse_after = iter; }
