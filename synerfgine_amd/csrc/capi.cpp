@@ -379,7 +379,6 @@ const std::map<std::string, double>& default_params() {
         {"nerf_msr", 1},                        // multi-step speculative rounds while n_steps is 2..7 (nerf.hip msr_*; exact)
         {"nerf_msr_budget", 16777216},          // samples one such round may generate (K = clamp(budget / (S n_alive), 1, kmax))
         {"nerf_msr_kmax", 16},                  // iterations one such round marches ahead (<= 16)
-        {"nerf_msr_threads", 0},                // their generate / commit workgroups: 64 or 256 threads; 0 = 64 below 2^20 band pixels
         {"march_log", 0},                       // diagnostics: log {alive, steps, samples} of every iteration (sng_frame_buffer "march_log")
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
         {"nerf_onestep_horizon", 2048},         // iterations one speculative segment of the regime spans
@@ -1329,13 +1328,9 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             ma.hist = c->msr_hist.as<uint32_t>();
             ma.frame_rgba = c->nerf_rgba.as<float4>(); ma.frame_depth = c->nerf_depth.as<float>(); ma.positions = c->nerf_pos.as<float>();
             const uint32_t mblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 8));
-            const double mt = c->p("nerf_msr_threads");
-            const int mthr = mt == 64.0 || (mt == 0.0 && n_band < (1u << 20)) ? 64 : 256;
-            const uint32_t gblocks64 = gb > 0 ? (uint32_t)gb * 4 : gb < 0 ? std::max(1u, (n_band + 63) / 64) : blocks * 4;
-            const uint32_t mblocks64 = std::max(1u, std::min((n_band + 63) / 64, (uint32_t)c->n_cus * 32));
             while (true) {
                 ma.in = rb[p]; ma.out = rb[p ^ 1]; ma.p = p;
-                launch_msr_generate(ma, mthr == 64 ? gblocks64 : gen_blocks, mthr, c->s_nerf);
+                launch_msr_generate(ma, gen_blocks, c->s_nerf);
                 if (P.collect_kernel_times) {
                     while (c->net_events.size() < 2 * (net_launches + 1)) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->net_events.push_back(e); }
                 }
@@ -1345,7 +1340,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 launch_msr_count(ma, mblocks, c->s_nerf);
                 if (gsched) sched_reduce(c, ma.hist + MSR_KMAX, MSR_KMAX);   // own-row deaths summed over the ranks
                 launch_msr_schedule(ma, c->s_nerf);
-                launch_msr_commit(ma, mthr == 64 ? mblocks64 : mblocks, mthr, c->s_nerf);
+                launch_msr_commit(ma, mblocks, c->s_nerf);
                 HIPCHK(hipGetLastError());
                 // the next round's frame-wide count is reduced before the one readback of the round (a no-op round's
                 // reduction is unused; every rank makes it, as every rank sees the same no-op)

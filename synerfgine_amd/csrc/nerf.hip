@@ -1611,23 +1611,13 @@ void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_composite_kernel<256>, dim3(blocks), dim3(256), 0, s, a);
 }
-// threads 64: one wave per workgroup, for a band's few rays (the rounds are latency-bound per ray; 64-lane groups
-// spread the waves evenly over the CUs where 256-lane groups leave some CUs twice the waves of others)
-void launch_msr_generate(const MsrArgs& a, uint32_t blocks, int threads, hipStream_t s) {
-    if (threads == 64) {
-        if (a.vol.linear) hipLaunchKernelGGL(HIP_KERNEL_NAME(msr_generate_kernel<true, 64>), dim3(blocks), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(msr_generate_kernel<false, 64>), dim3(blocks), dim3(64), 0, s, a);
-        return;
-    }
+void launch_msr_generate(const MsrArgs& a, uint32_t blocks, hipStream_t s) {
     if (a.vol.linear) hipLaunchKernelGGL(HIP_KERNEL_NAME(msr_generate_kernel<true>), dim3(blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(HIP_KERNEL_NAME(msr_generate_kernel<false>), dim3(blocks), dim3(256), 0, s, a);
 }
 void launch_msr_count(const MsrArgs& a, uint32_t blocks, hipStream_t s) { hipLaunchKernelGGL(msr_count_kernel<256>, dim3(blocks), dim3(256), 0, s, a); }
 void launch_msr_schedule(const MsrArgs& a, hipStream_t s) { hipLaunchKernelGGL(msr_schedule_kernel, dim3(1), dim3(64), 0, s, a); }
-void launch_msr_commit(const MsrArgs& a, uint32_t blocks, int threads, hipStream_t s) {
-    if (threads == 64) hipLaunchKernelGGL(msr_commit_kernel<64>, dim3(blocks), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(msr_commit_kernel<256>, dim3(blocks), dim3(256), 0, s, a);
-}
+void launch_msr_commit(const MsrArgs& a, uint32_t blocks, hipStream_t s) { hipLaunchKernelGGL(msr_commit_kernel<256>, dim3(blocks), dim3(256), 0, s, a); }
 void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s) {
     hipLaunchKernelGGL(spec_prepare_kernel, dim3(blocks), dim3(256), 0, s, a);
 }

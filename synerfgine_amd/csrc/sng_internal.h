@@ -367,10 +367,10 @@ struct MsrArgs {
     float* frame_depth;
     float* positions;
 };
-void launch_msr_generate(const MsrArgs& a, uint32_t blocks, int threads, hipStream_t s);
+void launch_msr_generate(const MsrArgs& a, uint32_t blocks, hipStream_t s);
 void launch_msr_count(const MsrArgs& a, uint32_t blocks, hipStream_t s);
 void launch_msr_schedule(const MsrArgs& a, hipStream_t s);
-void launch_msr_commit(const MsrArgs& a, uint32_t blocks, int threads, hipStream_t s);
+void launch_msr_commit(const MsrArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_generate(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_composite(const SpecArgs& a, uint32_t blocks, hipStream_t s);
 void launch_spec_prepare(const SpecArgs& a, uint32_t blocks, hipStream_t s);
