@@ -126,26 +126,9 @@ __device__ __forceinline__ float rcp_exact(float x) {
     if (ax >= 0x1p-126f && ax < 0x1p126f) return recip_rn(x);
     return 1.0f / x;
 }
-// LDS = true: tp points into the LDS scene blob.  The record is read as three ds_read_b128 (volatile address-space-3
-// loads: the compiler otherwise splits the 48 B by use into b128 + b96 + b64 + b32 + read2_b32, five LDS instructions
-// whose b96 / read2 forms bank on 32 dwords and cost 8 + 4 cycles where the three b128 cost 4 each).
-template <bool LDS>
 __device__ __forceinline__ bool tri_hit(const TriT* tp, f3 ro, f3 rd, float mint, float& t_out) {
-    float4 w0, w1, w2;
-    if constexpr (LDS) {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        typedef __attribute__((address_space(3))) volatile v4f lds_v4f;
-        const lds_v4f* q = (const lds_v4f*)(const __attribute__((address_space(3))) void*)tp;
-        const v4f a = q[0], b = q[1], c = q[2];
-        w0 = make_float4(a.x, a.y, a.z, a.w);
-        w1 = make_float4(b.x, b.y, b.z, b.w);
-        w2 = make_float4(c.x, c.y, c.z, c.w);
-    } else {
-        const float4* p4 = reinterpret_cast<const float4*>(tp);
-        w0 = p4[0];
-        w1 = p4[1];
-        w2 = p4[2];
-    }
+    const float4* p4 = reinterpret_cast<const float4*>(tp);
+    const float4 w0 = p4[0], w1 = p4[1], w2 = p4[2];
     const f3 v1v0 = mk(w0.w, w1.x, w1.y), v2v0 = mk(w1.z, w1.w, w2.x), n = mk(w2.y, w2.z, w2.w);
     const f3 rov0 = ro - mk(w0.x, w0.y, w0.z);
     const float d = rcp_exact(dot(rd, n));
@@ -162,7 +145,7 @@ __device__ __forceinline__ bool tri_hit(const TriT* tp, f3 ro, f3 rd, float mint
 // ray_intersect_nodes_f<2> (triangle_bvh.cu:263-307); returns t, writes triangle index.
 // Box tests: bvh_box_entry (sng_math.h), in its branch-free form (aabb_entry_fast) when the ray and
 // the object keep every quotient finite; y = inv(rd) once per ray.
-template <bool FAST, bool LDS>
+template <bool FAST>
 __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __restrict__ nodes, const TriT* __restrict__ tris, int* stack_lds,
                                           int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
     Stack st{stack_lds, stride, 0};
@@ -177,7 +160,7 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
             if (cnt) cnt[2] += (uint32_t)(end + node.left + 1);
             for (int i = -node.left - 1; i < end; ++i) {
                 float t;
-                if (tri_hit<LDS>(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
+                if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
             }
         } else {
             const int c0 = node.left, c1 = node.left + 1;
@@ -199,7 +182,7 @@ __device__ __forceinline__ float bvh_walk(f3 ro, f3 rd, f3 y, const BvhNode* __r
 }
 // The same traversal over the BvhWide layout: identical box tests, push order, overflow rule and
 // triangle order, so identical results; one record load per inner node, none per leaf.
-template <bool FAST, bool LDS>
+template <bool FAST>
 __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const TriT* __restrict__ tris, int root_ref,
                                                int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr) {
     Stack st{stack_lds, stride, 0};
@@ -214,7 +197,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
             if (cnt) cnt[2] += (uint32_t)(end - b);
             for (int i = b; i < end; ++i) {
                 float t;
-                if (tri_hit<LDS>(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
+                if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
             }
         } else {
             if (cnt) cnt[1] += 2u;
@@ -235,7 +218,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
 // The visiting sequence, `d < mint` culling at push time and triangle order are the reference's, so
 // the result is identical.  (The reference's FixedStack<32> overflow rule cannot fire: the stack
 // never holds more than max BVH depth + 2 <= 32 entries, capi.cpp upload_scene.)
-template <bool FAST, bool LDS>
+template <bool FAST>
 __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const TriT* __restrict__ tris, int root_ref,
                                                int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr, bool cw = false) {
     PStack st{(lds_int*)stack_lds, (lds_int*)stack_lds, stride};
@@ -269,7 +252,7 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
         for (int i = b; i < end; ++i) {
             if (cnt && cw) cnt[2] += (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id());
             float t;
-            if (tri_hit<LDS>(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
+            if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
         }
         if (st.empty()) break;
         cur = st.pop();
@@ -287,15 +270,15 @@ __device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu&
     const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
     const f3 y = inv(ord);
     if (o.wide && cx.flat) {
-        if (fast) return bvh_walk_near<true, LDS>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
-        return bvh_walk_near<false, LDS>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
+        if (fast) return bvh_walk_near<true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
+        return bvh_walk_near<false>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
     }
     if (o.wide) {
-        if (fast) return bvh_walk_wide<true, LDS>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
-        return bvh_walk_wide<false, LDS>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+        if (fast) return bvh_walk_wide<true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+        return bvh_walk_wide<false>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
     }
-    if (fast) return bvh_walk<true, LDS>(oro, ord, y, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
-    return bvh_walk<false, LDS>(oro, ord, y, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+    if (fast) return bvh_walk<true>(oro, ord, y, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
+    return bvh_walk<false>(oro, ord, y, cx.nodes(o), cx.tris(o), cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr);
 }
 
 // sng::depth_test_world (common.cu:36-48)

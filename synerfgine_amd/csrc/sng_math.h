@@ -664,15 +664,10 @@ struct Tri { f3 a, b, c; };                                 // Triangle (36 B)
 // 256-B bank row, and the q-th load of record i sits in slot (5 i + q) mod 16 -- distinct for 16 consecutive
 // records -- where a 64-B stride put every record's q-th load in one of only 4 slots (up to 4-way conflicts
 // between lanes walking different records).
-#ifndef SNG_WIDE_PAD
-#define SNG_WIDE_PAD 1
-#endif
 struct alignas(16) BvhWide {
     float s0[6], s1[6];
     int ref0, ref1, pad0, pad1;
-#if SNG_WIDE_PAD
     int pad2[4];
-#endif
 };
 constexpr uint32_t WIDE_MAX_BEGIN = 1u << 24, WIDE_MAX_COUNT = 127u;
 constexpr int WIDE_DONE = (int)0x80000000;   // traversal sentinel; wide_bvh never encodes a leaf as ~0x7FFFFFFF
