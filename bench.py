@@ -672,9 +672,14 @@ def main():
                 NW, NH = res["nerf"]
                 u = frame_cells(eng, [{"concurrent_streams": 0}], 10, 2, NW * NH)[0]
                 eng.set_param("concurrent_streams", 1)
+                chk = os.path.join(REPO, "profiles", f"{ROUND}_roofline_check.json")
                 result["roofline"]["uncontended"] = {
                     "frac": u["network_roofline_frac"], "field_sample_weighted_frac": u["field_sample_weighted_frac"],
                     "frames_per_s": u["frames_per_s"],
+                    "rocprof_same_process": json.load(open(chk)).get("uncontended") if os.path.exists(chk) else None,
+                    "rocprof_note": "tools/gpu.sh profdriver: rocprofv3 kernel trace of a bench.py process like this one; its own durations "
+                                    "of the same launches (profiles/<round>_roofline_check.json). Each frame's second speculative round is a "
+                                    "~6 us launch whose HIP-event duration is ~2x its rocprof one, which lowers this leg's frac by ~6 %",
                     "note": "the same frames with the raytracer and the NeRF serialized (concurrent_streams=0, 10 frames after "
                             "the timed region): the network launches run alone. The timed line runs the streams concurrently, "
                             "where the raytracer's persistent grids leave the NeRF stream rt_reserved_cus CUs, so `frac` above "

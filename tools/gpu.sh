@@ -7,6 +7,7 @@
 #   bench[:CFG[:ARGS]]     bench.py --config CFG --no-cpu-baseline --no-sweep ARGS   (ARGS: ',' for spaces)
 #   driver                 bench.py with no flags (the driver's own line, incl. CPU baseline and extra legs)
 #   prof[:CFG[:ARGS]]      rocprofv3 --kernel-trace --stats of a short bench.py run (ARGS as for bench)
+#   profdriver             rocprofv3 over bench.py --no-cpu-baseline + tools/roofline_check.py (same-process roofline check)
 #   pmc[:CFG[:ARGS]]       FETCH_SIZE / WRITE_SIZE / MFMA PMC passes (one rocprofv3 run each) + tools/pmc_summary.py
 #   sq[:CFG[:ARGS]]        SQ_INSTS_* + SQ_WAVE_CYCLES pass with kernel trace + tools/sq_summary.py (VALU roofline)
 #   py:SCRIPT[:ARGS]       python3 tools/SCRIPT ARGS
@@ -47,6 +48,16 @@ for step in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- python3 bench.py --config ${cfg:-c3} --steps 10 --warmup 2 --no-cpu-baseline --no-sweep $args > $log 2>&1
       rc=$?
       [ $rc -eq 0 ] && python3 tools/kernel_table.py $(find $d -name "*kernel_trace.csv" | head -1) > $d/kernel_table.txt 2>&1 && head -30 $d/kernel_table.txt ;;
+    profdriver)
+      # rocprofv3 over the driver-format line without the CPU legs (the serialized leg and the extras run); the
+      # roofline fields of that line recomputed from the same process's kernel trace (tools/roofline_check.py)
+      d=$OUT/prof$n
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- python3 bench.py --no-cpu-baseline $args > $log 2>&1
+      rc=$?
+      if [ $rc -eq 0 ]; then
+        tr=$(find $d -name "*kernel_trace.csv" | head -1)
+        python3 tools/kernel_table.py $tr > $d/kernel_table.txt 2>&1 && python3 tools/roofline_check.py $tr $log $OUT/roofline_check.json; rc=$?
+      fi ;;
     pmc)
       d=$OUT/pmc$n
       a="--config ${cfg:-c3} --steps 3 --warmup 1 --no-cpu-baseline --no-sweep $args"
