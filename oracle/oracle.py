@@ -82,7 +82,7 @@ class orc_frame_params(ctypes.Structure):
                 ("light_samples", ctypes.c_uint32), ("path_trace_depth", ctypes.c_uint32), ("shadow_iters", ctypes.c_uint32),
                 ("shadow_steps", ctypes.c_uint32), ("lens_angle_constant", ctypes.c_float), ("syn_shadow_factor", ctypes.c_float),
                 ("rt_depth_offset", ctypes.c_float), ("exposure", ctypes.c_float), ("srgb_output", ctypes.c_int32),
-                ("tonemap_curve", ctypes.c_int32)]
+                ("tonemap_curve", ctypes.c_int32), ("rt_buffer_type", ctypes.c_int32)]
 
 
 _lib = None
@@ -342,6 +342,7 @@ def frame_params_from_engine(eng):
     p.path_trace_depth = int(g("path_trace_depth")); p.shadow_iters = int(g("syn_shadow_samples")); p.shadow_steps = int(g("n_steps"))
     p.lens_angle_constant = g("lens_size"); p.syn_shadow_factor = g("syn_shadow_intensity"); p.rt_depth_offset = g("depth_offset")
     p.exposure = g("exposure"); p.srgb_output = int(g("srgb")); p.tonemap_curve = int(g("tonemap_curve"))
+    p.rt_buffer_type = int(g("rt_buffer_type"))
     return p
 
 

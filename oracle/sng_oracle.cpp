@@ -1621,7 +1621,7 @@ V4 shade_object(V3 wi, SampledRay& ray, uint32_t shadow_count, HitRecord& hit, c
 
 extern "C" {
 
-/* sng::raytrace: synerfgine/raytracer.cu:101-218 (Final buffer) */
+/* sng::raytrace: synerfgine/raytracer.cu:101-218, every ImgBufferType (raytracer.cuh:20-30) */
 void orc_raytrace(const orc_volume* vdesc, const float* camera, const orc_frame_params* P,
                   const orc_object* objd, uint32_t n_objs, const orc_light* lights, uint32_t n_lights,
                   const orc_material* mats, uint32_t n_mats, const float* origins, const float* dirs, uint32_t n,
@@ -1672,8 +1672,23 @@ void orc_raytrace(const orc_volume* vdesc, const float* camera, const orc_frame_
         float depth = dot(src_d, next_pos - src_p);
         acc_depth[i] = depth;
         V3 curr = v3(acc_rgba[4 * i], acc_rgba[4 * i + 1], acc_rgba[4 * i + 2]);
-        if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
-        acc_rgba[4 * i] = shade.x; acc_rgba[4 * i + 1] = shade.y; acc_rgba[4 * i + 2] = shade.z;
+        /* vec3_to_col (common.cu:300-302) */
+        auto to_col = [](V3 v) { return v * 0.5f + v3s(0.5f); };
+        V3 out;
+        switch (P->rt_buffer_type) {   /* raytracer.cu:189-216 */
+        case 1: out = length(next_pos - view_pos) + MIN_DEPTH > MAX_DEPTH ? v3s(0.0f) : to_col(normalize(next_pos)); break;   /* NextOrigin */
+        case 2: out = to_col(normalize(view_pos)); break;   /* SrcOrigin */
+        case 3: out = to_col(next_dir); break;              /* NextDirection */
+        case 4: out = to_col(view_dir); break;              /* SrcDirection */
+        case 5: out = to_col(normal); break;                /* Normal */
+        case 6: out = v3s(depth); break;                    /* Depth */
+        case 7: out = v3s(nerf_shadow); break;              /* NerfShadow */
+        default:                                            /* Final */
+            if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
+            out = shade;
+            break;
+        }
+        acc_rgba[4 * i] = out.x; acc_rgba[4 * i + 1] = out.y; acc_rgba[4 * i + 2] = out.z;
     }
 }
 

@@ -93,6 +93,7 @@ typedef struct {
     float exposure;
     int32_t srgb_output;            /* EColorSpace::SRGB (engine.cu:406) */
     int32_t tonemap_curve;          /* Testbed::m_tonemap_curve (engine.cu:406): ETonemapCurve 0 Identity, 1 ACES, 2 Hable, 3 Reinhard */
+    int32_t rt_buffer_type;         /* RayTracer::m_buffer_to_show (raytracer.cuh:20,179): ImgBufferType 0 Final .. 7 NerfShadow */
 } orc_frame_params;
 
 /* ---- primitives (KAT-level) --------------------------------------------- */

@@ -310,7 +310,9 @@ const std::map<std::string, double>& default_params() {
         {"res_factor", 64},                     // Testbed::m_fixed_res_factor (testbed.h:656)
         {"vo_scale", 4},                        // Engine::m_relative_vo_scale (engine.cuh:113)
         {"exposure", 0.0},                      // Testbed::m_exposure
-        {"tonemap_curve", 0},                   // Testbed::m_tonemap_curve (engine.cu:406): 0 Identity, 1 ACES, 2 Hable, 3 Reinhard
+        {"tonemap_curve", 0},
+        {"rt_buffer_type", 0},                  // RayTracer::m_buffer_to_show (raytracer.cuh:20,179): 0 Final, 1 NextOrigin, 2 SrcOrigin,
+                                                //   3 NextDirection, 4 SrcDirection, 5 Normal, 6 Depth, 7 NerfShadow                   // Testbed::m_tonemap_curve (engine.cu:406): 0 Identity, 1 ACES, 2 Hable, 3 Reinhard
         {"path_trace_depth", 2},                // RayTracer::m_ray_iters (raytracer.cuh:160)
         {"light_samples", 2},                   // RayTracer::m_samples
         {"syn_shadow_samples", 4},              // RayTracer::m_shadow_iters
@@ -473,6 +475,7 @@ struct sng_ctx {
     DevBuf spec_hint;                      // per NeRF pixel: 1 + the iteration its ray ended at last frame (u8, 0 unknown)
     uint64_t spec_hint_px = 0;
     uint64_t spec_hint_key = 0;            // the view the hints were written for (spec_view_key); another view reads none
+    uint64_t spec_prev_view = 0;           // the last traced frame's view (spec_view_key); a repeat writes hints
     uint64_t model_epoch = 0;              // bumped when the model or its occupancy changes (part of that key)
     DevBuf spec_pre, spec_pre_depth;       // spec_prepare: per network sample {rgb, alpha} and depth
     DevBuf band_rgba8;                     // sng_gather_rgba8: this rank's band as RGBA8
@@ -1110,7 +1113,8 @@ uint8_t* spec_hint_buf(sng_ctx* c);
 // resolution and the model (FNV-1a over the bytes).  The speculative rounds read the per-pixel look-ahead hints only
 // when the hints were written for the same view: on a moving camera a pixel's last ray ended elsewhere, and the
 // opacity policy (spec_k_of) sizes the look-ahead better (round 3: 1 deg/frame orbit 571 frames/s with hints read,
-// 623 without).  The pixel jitter (spp) is not part of it: sub-pixel moves keep the hints close.
+// 623 without).  They are written only by a frame that repeats the previous frame's view, so a moving camera
+// makes none of their scattered byte stores.  The pixel jitter (spp) is not part of it: sub-pixel moves keep the hints close.
 uint64_t spec_view_key(const sng_ctx* c, f2 focal, f2 sc) {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](const void* p, size_t n) {
@@ -1374,6 +1378,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // whole-GPU network launch evaluates them, the compositor replays them exactly; the fused
             // kernel below then finishes whatever is still alive
             const uint32_t rounds = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds"));
+            uint8_t* hint_w = nullptr;   // the hints this frame writes (SpecArgs::hint), nullptr when it writes none
             c->spec_rounds = rounds;
             launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), p, target, a.sched.global, c->s_nerf);
             if (tentative_now) {
@@ -1398,14 +1403,20 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 sa.frame_rgba = c->nerf_rgba.as<float4>(); sa.frame_depth = c->nerf_depth.as<float>(); sa.positions = c->nerf_pos.as<float>();
                 sa.pre = pre ? c->spec_pre.as<float4>() : nullptr;
                 sa.pre_depth = pre ? c->spec_pre_depth.as<float>() : nullptr;
-                sa.hint = spec_hint_buf(c);
-                {   // hints of this view?  (this frame's rays rewrite them either way)
+                {   // hints are read when they were written for this view, and written only when the view repeats the
+                    // last frame's (a moving camera neither reads nor writes them: no scattered byte stores for nothing)
+                    uint8_t* hint = spec_hint_buf(c);
                     const uint64_t key = spec_view_key(c, a.focal, sc);
-                    sa.hint_read = (key == c->spec_hint_key || c->p("nerf_spec_hint_any_view") != 0.0) ? 1 : 0;
-                    c->spec_hint_key = sa.hint ? key : 0;
+                    const bool any = c->p("nerf_spec_hint_any_view") != 0.0;
+                    const bool read = hint && (key == c->spec_hint_key || any);
+                    const bool write = hint && (read || any || key == c->spec_prev_view);
+                    sa.hint = write ? hint : nullptr;
+                    sa.hint_read = read ? 1 : 0;
+                    if (write) c->spec_hint_key = key;
                 }
                 // rays alive after the head: at most the band's pixels (grid-stride over the device count)
                 const uint32_t sblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 4));
+                hint_w = sa.hint;
                 for (uint32_t r = 0; r < rounds; ++r) {
                     sa.in = rb[p]; sa.out = rb[p ^ 1]; sa.p = p;
                     // per-ray look-ahead in all but the last round (which then finishes nearly every ray)
@@ -1430,7 +1441,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             fa.frame_rgba = c->nerf_rgba.as<float4>(); fa.frame_depth = c->nerf_depth.as<float>(); fa.positions = c->nerf_pos.as<float>();
             fa.work = c->fused_work.as<uint32_t>();
             fa.lanes = (uint32_t)std::min(64.0, std::max(1.0, c->p("nerf_fused_lanes")));
-            fa.hint = rounds ? spec_hint_buf(c) : nullptr;
+            fa.hint = rounds ? hint_w : nullptr;
             // concurrent frames: the tail runs beside the raytracer on the CUs its grids leave free.  A
             // mid-frame switch (a long march, e.g. C4) happens long after the raytracer has finished: the
             // tail then gets the whole-GPU grid
@@ -1503,6 +1514,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     }
     if (c->sched_comm.replay && c->sched_comm.replay_cursor != c->sched_comm.replay_words)
         throw SngError(SNG_ERR_STATE, "schedule replay diverged: the frame made " + std::to_string(c->sched_comm.replay_calls) + " reductions, the records hold more");
+    c->spec_prev_view = spec_view_key(c, a.focal, sc);
     return net_launches;
 }
 
@@ -1661,6 +1673,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 ra.count_waves = c->p("rt_count") == 2.0 ? 1 : 0;
             }
             ra.tile = c->p("rt_tile") == 4.0 ? 4 : 8;
+            ra.buffer_type = (int)c->p("rt_buffer_type");
             if (c->p("rt_tile_order") != 0.0) {
                 const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile - 1) / ra.tile);
                 const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60);
@@ -1688,7 +1701,8 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             q.nps = n_point * ra.shadow_iters;
             q.rec_stride = 2;
             const uint64_t bytes = cap * (16ull * q.rec_stride + 16ull * q.nls + 16ull * q.nps + 4ull * q.nps) + (uint64_t)MW * MH * 4;
-            const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
+            // (the ImgBufferType debug views come from the one-kernel path, which carries their sums)
+            const bool wavefront = c->p("rt_wavefront") != 0.0 && ra.buffer_type == 0 && ra.show_nerf_shadow && q.nps > 0 && cap > 0 && cap < (1ull << 31) &&
                                    bytes <= (uint64_t)(c->p("rt_queue_gb") * 1073741824.0);
             if (wavefront) {
                 c->rt_rec.ensure(cap * 16ull * q.rec_stride);
@@ -2638,6 +2652,8 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
             return;
         }
         if (!default_params().count(k)) throw SngError(SNG_ERR_INVALID, "unknown parameter '" + k + "'");
+        if (k == "rt_buffer_type" && !(v >= 0.0 && v <= 7.0 && v == std::floor(v)))
+            throw SngError(SNG_ERR_INVALID, "rt_buffer_type is an ImgBufferType: 0 Final, 1 NextOrigin, 2 SrcOrigin, 3 NextDirection, 4 SrcDirection, 5 Normal, 6 Depth, 7 NerfShadow");
         if (k == "tonemap_curve" && !(v == 0.0 || v == 1.0 || v == 2.0 || v == 3.0))
             throw SngError(SNG_ERR_INVALID, "tonemap_curve is an ETonemapCurve: 0 Identity, 1 ACES, 2 Hable, 3 Reinhard");
         c->params[k] = v;

@@ -686,6 +686,10 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
     const float4 o4 = origins[i], d4 = dirs[i];
     const f3 src_p = mk(o4.x, o4.y, o4.z), src_d = mk(d4.x, d4.y, d4.z);
     f3 shade = splat(0.0f), next_pos = splat(0.0f);
+    // the ImgBufferType views' sums (raytracer.cu:134-143; one-kernel path only, DEFER requires Final)
+    const int buf = DEFER ? 0 : a.buffer_type;
+    f3 normal = splat(0.0f), view_pos = splat(0.0f), view_dir = splat(0.0f), next_dir = splat(0.0f);
+    float nerf_shadow = 1.0f;
     int prev_rec = -1;
     uint32_t n_hits = 0;
     if (DEFER) q.head[i] = -1;
@@ -698,7 +702,10 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
         for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
             Hit h;
             const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h);
-            if (!bounce) next_pos = next_pos + h.pos;
+            if (!bounce) {
+                next_pos = next_pos + h.pos;
+                if (buf != 0) { normal = normal + h.normal; view_pos = view_pos + rp; view_dir = view_dir + rd; }
+            }
             if (hit_obj < 0) break;
             if (DEFER) {
                 defer_hit(a, q, lane, i, t, spp, h, prev_rec, n_hits, r, rp, rd, pdf, att);
@@ -721,10 +728,12 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
                         const f3 invL = inv(Lv);
                         int oh = -1;
                         const float syn = a.show_nerf_shadow ? depth_test_world(h.pos, Lv, a.objs, a.n_objs, cx, oh) : 1.0f;
+                        // the NerfShadow view needs the march's own value, not only min(it, syn, full_dist): no cap then
                         const float nerf = a.show_nerf_shadow
                                                ? depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, h.pos, Lv, invL, 0, a.vol.max_mip,
-                                                                 fminf(syn, full_dist))
+                                                                 buf == 7 ? 3.0e38f : fminf(syn, full_dist))
                                                : 1.0f;
+                        nerf_shadow = fminf(nerf / full_dist, nerf_shadow);   // out_nerf_shadow (raytracer.cu:32)
                         const float sh = fminf(fminf(nerf, syn), full_dist);
                         const float mask = pow_small_int(smoothstep(sh / full_dist), a.syn_shadow_factor);
                         color = color + lc * mask;
@@ -741,6 +750,7 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
             const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
             const f3 ndir = cone_random_frame(h.normal, h.perturb, lo, la);
             shade_s = shade_s + color * pdf * att;
+            if (!bounce) next_dir = next_dir + ndir;
             rp = h.pos;
             rd = ndir;
             pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
@@ -750,12 +760,27 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
     }
     const float weight = (float)a.samples;
     next_pos = next_pos / weight;
-    acc_depth[i] = dot(src_d, next_pos - src_p);
+    const float depth = dot(src_d, next_pos - src_p);
+    acc_depth[i] = depth;
     if (!DEFER) {
         shade = shade / weight;
         float4 cur = acc_rgba[i];
         const f3 curr = mk(cur.x, cur.y, cur.z);
-        if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
+        if (buf == 0) {
+            if (dot(curr, curr) > 0.001f) shade = shade * 0.5f + curr * 0.5f;
+        } else {   // raytracer.cu:189-209, vec3_to_col (common.cu:300-302) = v * 0.5 + 0.5
+            view_pos = view_pos / weight; view_dir = view_dir / weight; next_dir = next_dir / weight; normal = normal / weight;
+            auto col = [](f3 v) { return v * 0.5f + splat(0.5f); };
+            switch (buf) {
+            case 1: shade = length(next_pos - view_pos) + MIN_DEPTH > MAX_DEPTH ? splat(0.0f) : col(normalize(next_pos)); break;   // NextOrigin
+            case 2: shade = col(normalize(view_pos)); break;   // SrcOrigin
+            case 3: shade = col(next_dir); break;              // NextDirection
+            case 4: shade = col(view_dir); break;              // SrcDirection
+            case 5: shade = col(normal); break;                // Normal
+            case 6: shade = splat(depth); break;               // Depth
+            default: shade = splat(nerf_shadow); break;        // NerfShadow
+            }
+        }
         acc_rgba[i] = make_float4(shade.x, shade.y, shade.z, cur.w);
     }
     if (DEFER && q.pcount) q.pcount[t] = (uint8_t)n_hits;

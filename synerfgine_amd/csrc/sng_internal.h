@@ -272,6 +272,7 @@ struct RaytraceArgs {
     int tile;                   // path-kernel tile edge in pixels (8: 64 lanes, 4: 16 lanes per wave)
     unsigned long long* counts; // counting frames (rt_count): path kernel {queries, box, tri}, shadow kernel {queries, box, tri}
     int count_waves;            // rt_count = 2: box / tri entries count wave iterations of those loops (SIMD efficiency)
+    int buffer_type;            // ImgBufferType (raytracer.cuh:20): 0 Final, 1 NextOrigin .. 7 NerfShadow (one-kernel path)
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,

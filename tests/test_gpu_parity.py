@@ -806,3 +806,32 @@ def test_spec_hints_are_read_for_the_same_view_only():
         assert np.array_equal(moved.download("nerf_rgba").view(np.uint32), moved_none.download("nerf_rgba").view(np.uint32))
     finally:
         tb.close()
+
+
+def test_spec_hints_are_written_only_when_the_view_repeats():
+    """A frame writes hints only when it repeats the previous frame's view: alternating views never read any (the
+    same look-ahead as without hints), and a view read after one repeat.  Every frame equals the hint-free one."""
+    tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, "c3")
+    try:
+        m = np.array(tb.camera_matrix)
+        m2 = m.copy()
+        m2.reshape(-1)[-1] += 1e-3
+        eng.set_param("nerf_spec_hint", 0)
+        none = {}
+        for k, mat in (("a", m), ("b", m2)):
+            tb.camera_matrix = mat
+            r = eng.frame(spp=0, reset=True)
+            none[k] = (r.spec_evals, r.download("nerf_rgba").view(np.uint32).copy())
+        eng.set_param("nerf_spec_hint", 1)
+        for mat, k in ((m, "a"), (m2, "b"), (m, "a"), (m2, "b"), (m, "a")):   # alternating: nothing written
+            tb.camera_matrix = mat
+            r = eng.frame(spp=0, reset=True)
+            assert r.spec_evals == none[k][0], (k, r.spec_evals, none[k][0])
+            assert np.array_equal(r.download("nerf_rgba").view(np.uint32), none[k][1])
+        r = eng.frame(spp=0, reset=True)     # view a repeated: writes, reads nothing yet
+        assert r.spec_evals == none["a"][0]
+        r = eng.frame(spp=0, reset=True)     # reads the hints the repeat wrote
+        assert r.spec_evals < none["a"][0], (r.spec_evals, none["a"][0])
+        assert np.array_equal(r.download("nerf_rgba").view(np.uint32), none["a"][1])
+    finally:
+        tb.close()
