@@ -2526,7 +2526,8 @@ int sng_frame_buffer(sng_ctx* c, const char* name, void* out, uint64_t cap, uint
     return guarded([&] {
         if (!c || !name) throw SngError(SNG_ERR_INVALID, "null context or name");
         HIPCHK(hipSetDevice(c->device));
-        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}, {"march_log", &c->march_log}};
+        const std::map<std::string, DevBuf*> bufs = {{"coords", &c->coords}, {"net_out", &c->net_out}, {"samp", &c->samp}, {"march_log", &c->march_log},
+                                                       {"rt_tile_cost", &c->rt_tile_cost}, {"rt_tile_order", &c->rt_tile_order}};
         auto it = bufs.find(name);
         if (it == bufs.end()) throw SngError(SNG_ERR_INVALID, std::string("unknown frame buffer ") + name);
         HIPCHK(hipDeviceSynchronize());
