@@ -345,6 +345,7 @@ const std::map<std::string, double>& default_params() {
         {"rt_tile", 8},                         // path-kernel tile edge: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
+        {"rt_prio_frac", 0.1},                    // the costliest fraction of the path tiles (last frame's order) at wave priority 3
         {"nerf_gbuffer", 0},                    // 1: NeRF normals every frame (otherwise only when shadow_on_nerf needs them)
         {"rt_plist", 1},                        // per-pixel hit-record lists for the colour replay (rt_accumulate_kernel)
         {"glow_mode", 0},                       // Testbed::Nerf::glow_mode (testbed.h:871): bits 1 green grid, 2 cut line, 4 mask to alpha,
@@ -1685,7 +1686,10 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                                                     c->rt_tile_order.as<uint32_t>() + n_tiles, c->s_rt);
                     c->rt_tile_key = key;
                 }
-                if (rt_sorted) ra.tile_order = c->rt_tile_order.as<uint32_t>();
+                if (rt_sorted) {
+                    ra.tile_order = c->rt_tile_order.as<uint32_t>();
+                    ra.prio_tiles = (uint32_t)(std::max(0.0, c->p("rt_prio_frac")) * n_tiles);
+                }
                 ra.tile_cost = c->rt_tile_cost.as<uint32_t>();
             }
             if (phase == 1) return;

@@ -677,7 +677,7 @@ __device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& 
 }
 
 template <bool DEFER, bool LDS, bool CNT = false>
-__device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t t,
+__device__ __forceinline__ uint32_t raytrace_pixel(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t t,
                                                const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
                                                uint32_t n_rng, float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
     const size_t i = (size_t)a.row0 * a.W + t;
@@ -785,6 +785,7 @@ __device__ __forceinline__ void raytrace_pixel(const RaytraceArgs& a, const RtQu
     }
     if (DEFER && q.pcount) q.pcount[t] = (uint8_t)n_hits;
     store_rng(rng, n_rng, i, r);
+    return n_hits;
 }
 
 // Persistent workgroups; each wave takes T x T pixel tiles (T = 8, or 4 for thin bands: a tile is a
@@ -813,6 +814,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
         // tiles in descending cost of the previous frame (tile_sort_kernel), so the few expensive
         // object tiles start first instead of being the latency tail of the launch
         const uint32_t tile = a.tile_order ? a.tile_order[k] : k;
+        // the costliest tiles of the last frame (the first prio_tiles of the order) issue ahead of the other waves
+        // of their SIMD: the launch lasts as long as its slowest tile's chain, and the others have slack
+        if (a.prio_tiles) {
+            if (__builtin_amdgcn_readfirstlane(k) < a.prio_tiles) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const uint64_t t0 = wall_clock64();
         const uint32_t x = (tile % tiles_x) * T + (uint32_t)lane % T, y = (tile / tiles_x) * T + (uint32_t)lane / T;
         if ((uint32_t)lane < T * T && x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth);
@@ -821,10 +828,27 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
     if constexpr (CNT) flush_counts(a.counts, counts, lane);
 }
 
-// Shadow rays of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
+// One shadow ray of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
 // depend on its cap syn + 1 >= full_dist), so the result is bit-identical.
+template <bool LDS, bool CNT = false>
+__device__ __forceinline__ void trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t kr, uint32_t jp) {
+    const float4 s1 = *q.shadow_ray(kr, jp);
+    const float4* rk = q.rec + (size_t)kr * q.rec_stride;   // the origin: the record's hit position (header)
+    const float4 h0 = rk[0], h1 = rk[1];
+    const f3 pos = mk(h1.z, h1.w, h0.w), Lv = mk(s1.x, s1.y, s1.z);
+    const float full_dist = s1.w;
+    int oh = -1;
+    const float syn = depth_test_world(pos, Lv, a.objs, a.n_objs, cx, oh, full_dist);
+    const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip, fminf(syn, full_dist));
+    const float sh = fminf(fminf(nerf, syn), full_dist);
+    q.mask[q.mask_at(kr, jp)] = pow_small_int(smoothstep(sh / full_dist), a.syn_shadow_factor);
+}
+
+// The shadow-ray pass after the path kernel.  (Tracing each tile's shadow rays in the wave that traced its paths
+// measured 30 % slower: the shadow work, ~5,000 wave-ms per C3 frame, about equals the path work, and it lands on
+// the costliest tiles, which bound the launch.)
 template <bool LDS, bool CNT = false>
 __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work) {
     uint32_t counts[3] = {0u, 0u, 0u};
@@ -851,16 +875,7 @@ __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQue
         const uint32_t j = c * 64u + (uint32_t)lane;
         if (j >= total) continue;
         const uint32_t kr = j / q.nps, jp = j - kr * q.nps;   // record, shadow sample (RtQueue::shadow_ray)
-        const float4 s1 = *q.shadow_ray(kr, jp);
-        const float4* rk = q.rec + (size_t)kr * q.rec_stride;   // the origin: the record's hit position (header)
-        const float4 h0 = rk[0], h1 = rk[1];
-        const f3 pos = mk(h1.z, h1.w, h0.w), Lv = mk(s1.x, s1.y, s1.z);
-        const float full_dist = s1.w;
-        int oh = -1;
-        const float syn = depth_test_world(pos, Lv, a.objs, a.n_objs, cx, oh, full_dist);
-        const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip, fminf(syn, full_dist));
-        const float sh = fminf(fminf(nerf, syn), full_dist);
-        q.mask[q.mask_at(kr, jp)] = pow_small_int(smoothstep(sh / full_dist), a.syn_shadow_factor);
+        trace_shadow_ray(a, q, cx, kr, jp);
     }
     if constexpr (CNT) flush_counts(a.counts + 3, counts, lane);
 }
@@ -1153,12 +1168,12 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
         allow_lds(raytrace_kernel<true, true>, lp);
         allow_lds(shadow_rays_kernel<true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
-            hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+        hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     } else {
         allow_lds(raytrace_kernel<true, false>, lp);
         allow_lds(shadow_rays_kernel<false>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
-            hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+        hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
     }
     if (q.plist) {   // capi.cpp enables the lists only when one wave's staging fits 64 KB
         const size_t per_wave = 16u * (64u * q.rec_stride + (64u * q.nps + 3u) / 4u);

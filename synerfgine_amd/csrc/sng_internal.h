@@ -273,6 +273,7 @@ struct RaytraceArgs {
     unsigned long long* counts; // counting frames (rt_count): path kernel {queries, box, tri}, shadow kernel {queries, box, tri}
     int count_waves;            // rt_count = 2: box / tri entries count wave iterations of those loops (SIMD efficiency)
     int buffer_type;            // ImgBufferType (raytracer.cuh:20): 0 Final, 1 NextOrigin .. 7 NerfShadow (one-kernel path)
+    uint32_t prio_tiles;        // the first prio_tiles tiles of tile_order run at wave priority 3 (0: off)
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
