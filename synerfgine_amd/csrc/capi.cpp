@@ -1078,7 +1078,11 @@ void ensure_samples(sng_ctx* c, uint32_t target) {
     const size_t kmax = (size_t)std::min<double>(SPEC_KMAX, std::max(1.0, c->p("nerf_spec_kmax")));
     const size_t spec = c->p("nerf_spec_rounds") > 0 ? std::min((size_t)std::max(1.0, c->p("nerf_spec_budget")),
                                                                 MAX_STEPS_BETWEEN_COMPACTION * kmax * c->ray_cap) : 0;
-    size_t cap = std::max(std::max<size_t>(target, c->ray_cap), spec) + 64;
+    // the multi-step rounds' budget (nerf_msr_budget): at most kmax iterations of < 8 samples per ray
+    const size_t mkmax = (size_t)std::min<double>(MSR_KMAX, std::max(1.0, c->p("nerf_msr_kmax")));
+    const size_t msr = c->p("nerf_msr") != 0.0 ? std::min((size_t)std::max(1.0, c->p("nerf_msr_budget")),
+                                                          (MAX_STEPS_BETWEEN_COMPACTION - 1) * mkmax * c->ray_cap) : 0;
+    size_t cap = std::max(std::max(std::max<size_t>(target, c->ray_cap), spec), msr) + 64;
     if (cap > c->sample_cap) {
         c->coords.ensure(cap * 7 * 4);
         c->net_out.ensure(cap * 8);
@@ -1136,11 +1140,12 @@ uint64_t spec_view_key(const sng_ctx* c, f2 focal, f2 sc) {
 // One reduction of the frame-wide schedule (sum over ranks of dev[0..n), in place on the NeRF stream):
 // RCCL all-reduce, the host reducer (a stream sync + callback), or the next replay record (an async copy from
 // pinned memory: a band timed on one GPU as its rank runs it, without a communicator).
-void sched_reduce(sng_ctx* c, uint32_t* dev, uint32_t n) {
+// src: the values to sum when they are not already in dev (out of place: no copy into dev first).
+void sched_reduce(sng_ctx* c, uint32_t* dev, uint32_t n, const uint32_t* src = nullptr) {
     SchedComm& sc = c->sched_comm;
     ++sc.replay_calls;
     if (sc.comm) {
-        comm_allreduce_u32(sc, dev, n, c->s_nerf);
+        comm_allreduce_u32(sc, src ? src : dev, dev, n, c->s_nerf);
     } else if (sc.replay) {
         const size_t at = sc.replay_cursor;
         if (at >= sc.replay_words || sc.replay[at] != n || at + 1 + n > sc.replay_words)
@@ -1149,7 +1154,7 @@ void sched_reduce(sng_ctx* c, uint32_t* dev, uint32_t n) {
         sc.replay_cursor = at + 1 + n;
     } else {
         std::vector<uint32_t> h(n);
-        HIPCHK(hipMemcpyAsync(h.data(), dev, (size_t)n * 4, hipMemcpyDeviceToHost, c->s_nerf));
+        HIPCHK(hipMemcpyAsync(h.data(), src ? src : dev, (size_t)n * 4, hipMemcpyDeviceToHost, c->s_nerf));
         HIPCHK(hipStreamSynchronize(c->s_nerf));
         if (sc.host_fn(h.data(), n, sc.host_user) != 0) throw SngError(SNG_ERR_STATE, "schedule reducer failed");
         HIPCHK(hipMemcpyAsync(dev, h.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->s_nerf));
@@ -1205,8 +1210,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     // sched_alive[q] <- sum over ranks of n_owned[q] (the frame-wide alive count of the next iteration)
     auto reduce_sched = [&](int q) {
         if (!gsched) return;
-        HIPCHK(hipMemcpyAsync(&ctrl->sched_alive[q], &ctrl->n_owned[q], 4, hipMemcpyDeviceToDevice, c->s_nerf));
-        sched_reduce(c, &ctrl->sched_alive[q], 1);
+        sched_reduce(c, &ctrl->sched_alive[q], 1, &ctrl->n_owned[q]);
     };
     uint32_t* const sched_src = gsched ? &ctrl->sched_alive[0] : &ctrl->n_alive[0];   // counts the host loop reads
     RayBuf rb[2];
@@ -3088,7 +3092,7 @@ int sng_comm_allreduce_u32(sng_ctx* c, uint32_t* d, uint64_t n, void* stream) {
         if (!c || !d) throw SngError(SNG_ERR_INVALID, "null context or buffer");
         HIPCHK(hipSetDevice(c->device));
         if (!c->sched_comm.comm) throw SngError(SNG_ERR_STATE, "no communicator attached (sng_set_comm)");
-        comm_allreduce_u32(c->sched_comm, d, (size_t)n, stream ? (hipStream_t)stream : c->s_nerf);
+        comm_allreduce_u32(c->sched_comm, d, d, (size_t)n, stream ? (hipStream_t)stream : c->s_nerf);
     });
 }
 int sng_final_rgba8(sng_ctx* c, int32_t row_begin, int32_t row_end, uint32_t* d_out, void* stream) {

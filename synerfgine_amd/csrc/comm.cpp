@@ -86,8 +86,8 @@ void comm_destroy(SchedComm& c) {
     c.world = 0;
 }
 
-void comm_allreduce_u32(SchedComm& c, uint32_t* dev, size_t n, hipStream_t s) {
-    check(rccl().all_reduce(dev, dev, n, ncclUint32, ncclSum, static_cast<ncclComm_t>(c.comm), s), "ncclAllReduce");
+void comm_allreduce_u32(SchedComm& c, const uint32_t* src, uint32_t* dst, size_t n, hipStream_t s) {
+    check(rccl().all_reduce(src, dst, n, ncclUint32, ncclSum, static_cast<ncclComm_t>(c.comm), s), "ncclAllReduce");
 }
 
 // The final composition: every rank's band of RGBA8 rows goes to the root rank only -- one

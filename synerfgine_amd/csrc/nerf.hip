@@ -1000,35 +1000,42 @@ __global__ void tail_prepare_kernel(MarchCtrl* ctrl, uint32_t* work, int p, uint
 // ---------------------------------------------------------------------------
 // Multi-step speculative rounds (MsrArgs, sng_internal.h)
 // ---------------------------------------------------------------------------
-// The round's shape from the frame-wide alive count at its first iteration: S = that iteration's steps
-// (only 2..7: 1 is the one-step regime's, 8 the tail's), K iterations within the sample budget and
-// before MARCH_ITER.  K == 0: the round is a no-op (every msr kernel returns without touching state).
-// The last frame's schedule (MarchCtrl::sched_hint, frame-wide, so every rank of a banded frame forms the same K)
-// predicts where the step count changes: a round whose first iteration took S steps then too looks ahead as far
-// as S lasted; one whose first iteration took another count then is near a change and looks 2 iterations ahead.
-// Any K is exact (the schedule commits only the iterations whose guess held); the hint bounds the discarded work.
-__device__ __forceinline__ void msr_shape(const MarchCtrl* c, uint32_t n_sched, uint32_t istep0, uint32_t target, uint32_t budget, uint32_t kmax,
-                                          uint32_t& S, uint32_t& K) {
-    S = 0;
-    K = 0;
-    if (n_sched == 0 || istep0 >= MARCH_ITER) return;
+// The round's shape from the frame-wide alive count at its first iteration: S_0 = that iteration's steps
+// (only 2..7: 1 is the one-step regime's, 8 the tail's) and K iterations before MARCH_ITER, each with its own
+// step count Sv[m].  K == 0: the round is a no-op (every msr kernel returns without touching state).
+// The last frame's schedule (MarchCtrl::sched_hint, frame-wide, so every rank of a banded frame forms the same
+// round) predicts the steps of the iterations ahead: when it agrees with S_0 the round follows it, across step
+// changes, for as long as it stays in 2..7 (up to kmax iterations and budget / n_sched samples per ray);
+// otherwise the round assumes S_0 throughout (no hint: as far as the budget allows; a hint that disagrees: the
+// schedule is near a change, 2 iterations).  Any guess is exact: msr_schedule commits the iterations whose
+// frame-wide count takes the guessed steps, and the rest are marched again.
+__device__ __forceinline__ uint32_t msr_shape(const MarchCtrl* c, uint32_t n_sched, uint32_t istep0, uint32_t target, uint32_t budget,
+                                              uint32_t kmax, uint8_t* Sv) {
+    if (n_sched == 0 || istep0 >= MARCH_ITER) return 0u;
     const uint32_t s = steps_for(n_sched, target);
-    if (s < 2 || s >= MAX_STEPS_BETWEEN_COMPACTION) return;
-    uint32_t k = budget / (s * n_sched);
+    if (s < 2 || s >= MAX_STEPS_BETWEEN_COMPACTION) return 0u;
+    const uint32_t per_ray = budget / n_sched;   // samples per ray the round may generate
+    const uint32_t k0 = c->n_iter;
+    const uint32_t h = k0 < TAIL_LIVE_CAP ? c->sched_hint[k0] : 0u;
+    uint32_t K = 0;
+    if (h == s) {
+        uint32_t istep = istep0, tot = 0;
+        while (K < kmax && istep < MARCH_ITER) {
+            const uint32_t sm = K == 0 ? s : (k0 + K < TAIL_LIVE_CAP ? (uint32_t)c->sched_hint[k0 + K] : 0u);
+            if (sm < 2 || sm >= MAX_STEPS_BETWEEN_COMPACTION || (K > 0 && tot + sm > per_ray)) break;
+            Sv[K++] = (uint8_t)sm;
+            tot += sm;
+            istep += sm;
+        }
+        return K;
+    }
+    uint32_t k = per_ray / s;
     k = k < 1u ? 1u : (k > kmax ? kmax : k);
     const uint32_t left = (MARCH_ITER - istep0 + s - 1) / s;   // iterations whose i is still < MARCH_ITER
     k = k < left ? k : left;
-    const uint32_t k0 = c->n_iter;
-    const uint32_t h = k0 < TAIL_LIVE_CAP ? c->sched_hint[k0] : 0u;
-    if (h == s) {
-        uint32_t run = 1;
-        while (run < k && k0 + run < TAIL_LIVE_CAP && c->sched_hint[k0 + run] == s) ++run;
-        k = run;
-    } else if (h != 0u) {
-        k = k < 2u ? k : 2u;
-    }
-    S = s;
-    K = k;
+    if (h != 0u) k = k < 2u ? k : 2u;
+    for (uint32_t m = 0; m < k; ++m) Sv[m] = (uint8_t)s;
+    return k;
 }
 
 // composite_kernel's opacity step on one sample (spec_composite_sample's alpha and accumulation of .w)
@@ -1043,16 +1050,26 @@ __device__ __forceinline__ float msr_alpha(const Volume& vol, float ts, uint2 ra
 template <bool LIN, int THREADS = 256>
 __global__ __launch_bounds__(THREADS) void msr_generate_kernel(MsrArgs a) {
     __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
+    __shared__ uint8_t sh_S[MSR_KMAX];
     MarchCtrl* ctrl = a.ctrl;
     const int p = a.p;
     const uint32_t n_alive = ctrl->n_alive[p];
     const uint32_t n_sched = a.sched.global ? ctrl->sched_alive[p] : n_alive;
-    uint32_t S, K;
-    msr_shape(ctrl, n_sched, ctrl->i_step[p], a.target, a.budget, a.kmax, S, K);
-    if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) { ctrl->msr_S[p] = S; ctrl->msr_K[p] = K; }
-        if (threadIdx.x < 4 * MSR_KMAX) a.hist[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) {
+        uint8_t Sv[MSR_KMAX];
+        const uint32_t K = msr_shape(ctrl, n_sched, ctrl->i_step[p], a.target, a.budget, a.kmax, Sv);
+        sh_app[3 * (THREADS / 64)] = K;
+        for (uint32_t m = 0; m < MSR_KMAX; ++m) sh_S[m] = m < K ? Sv[m] : (uint8_t)0;
+        if (blockIdx.x == 0) {
+            ctrl->msr_S[p] = K ? Sv[0] : 0u;
+            ctrl->msr_K[p] = K;
+            for (uint32_t m = 0; m < MSR_KMAX; ++m) ctrl->msr_Sv[p][m] = sh_S[m];
+        }
     }
+    if (blockIdx.x == 0 && threadIdx.x < 4 * MSR_KMAX) a.hist[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t K = sh_app[3 * (THREADS / 64)];
+    __syncthreads();   // sh_app is block_append's scratch below
     if (K == 0 || blockIdx.x * THREADS >= n_alive) return;
     const Volume& vol = a.vol;
     const int lane = threadIdx.x & 63;
@@ -1075,7 +1092,7 @@ __global__ __launch_bounds__(THREADS) void msr_generate_kernel(MsrArgs a) {
             float prev = a.in.lt[i].x;   // the previous iteration's last sample (the boundary-sample cache)
             OccCache oc;
             float* tb = a.tbuf + i;
-            uint32_t cnt = 0, it = 0;
+            uint32_t cnt = 0, it = 0, S = sh_S[0];   // S: the current iteration's steps
             float first = qnan, tl = 0.0f;
             const f3 hs = half_sign(d);
             bool going = true;
@@ -1120,6 +1137,7 @@ __global__ __launch_bounds__(THREADS) void msr_generate_kernel(MsrArgs a) {
                         const f3 pos = vol.train_aabb.lo + wp * wdiag;
                         t = div_by(dot(a.cam.c2, pos - a.cam.c3), dfw, rdfw);
                         ++it;
+                        S = sh_S[it];
                         cnt = 0;
                         first = qnan;
                     }
@@ -1130,7 +1148,7 @@ __global__ __launch_bounds__(THREADS) void msr_generate_kernel(MsrArgs a) {
         if (i < n_alive) {
             a.samp[i] = make_uint2(base, n_it | (cnt_last << 5) | (rbits << 9));
             const f3 wd = (d + 1.0f) * 0.5f;
-            uint32_t q = base, jx = 0, itx = 0;
+            uint32_t q = base, jx = 0, itx = 0, S = sh_S[0];
 #pragma unroll 1
             for (uint32_t x = 0; x < tot; ++x) {
                 if (!(jx == 0 && ((rbits >> itx) & 1u))) {   // a cached boundary sample needs no evaluation
@@ -1140,7 +1158,7 @@ __global__ __launch_bounds__(THREADS) void msr_generate_kernel(MsrArgs a) {
                     c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(LIN ? calc_dt(ts, 0.0f) : calc_dt(ts, cone)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
                     ++q;
                 }
-                if (++jx == S) { jx = 0; ++itx; }
+                if (++jx == S) { jx = 0; ++itx; S = sh_S[itx < MSR_KMAX ? itx : 0]; }
             }
         }
     }
@@ -1175,10 +1193,12 @@ __global__ __launch_bounds__(THREADS) void msr_count_kernel(MsrArgs a) {
     __shared__ uint32_t h[4 * MSR_KMAX];
     MarchCtrl* ctrl = a.ctrl;
     const int p = a.p;
+    __shared__ uint8_t sh_S[MSR_KMAX];
     const uint32_t K = ctrl->msr_K[p];
     if (K == 0) return;
-    const uint32_t S = ctrl->msr_S[p], istep0 = ctrl->i_step[p], n_alive = ctrl->n_alive[p];
+    const uint32_t istep0 = ctrl->i_step[p], n_alive = ctrl->n_alive[p];
     if (threadIdx.x < 4 * MSR_KMAX) h[threadIdx.x] = 0u;
+    if (threadIdx.x < MSR_KMAX) sh_S[threadIdx.x] = ctrl->msr_Sv[p][threadIdx.x];
     __syncthreads();
     const Volume& vol = a.vol;
     const float opaque = 1.0f - vol.min_transmittance;
@@ -1189,13 +1209,15 @@ __global__ __launch_bounds__(THREADS) void msr_count_kernel(MsrArgs a) {
         const bool own = !a.sched.global || (idx >= a.sched.own_lo && idx < a.sched.own_hi);
         const uint2 sc = a.samp[i];
         const uint32_t n_it = sc.y & 31u, cnt_last = (sc.y >> 5) & 15u, rbits = sc.y >> 9;
-        uint32_t ob = sc.x, s = 0, e = K;
+        uint32_t ob = sc.x, s = 0, e = K, istep = istep0;
         for (uint32_t it = 0; it < n_it; ++it) {
+            const uint32_t S = sh_S[it];
             const uint32_t cnt = it + 1 == n_it ? cnt_last : S;
             const uint32_t ru = (rbits >> it) & 1u;
             atomicAdd(&h[2 * MSR_KMAX + it], cnt);
             if (ru) atomicAdd(&h[3 * MSR_KMAX + it], 1u);
-            const bool last = istep0 + S * it + S >= MARCH_ITER;
+            istep += S;
+            const bool last = istep >= MARCH_ITER;
             // the iteration's t's and outputs loaded together, ahead of the opacity chain
             float tv[MAX_STEPS_BETWEEN_COMPACTION];
             uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
@@ -1239,14 +1261,17 @@ __global__ void msr_schedule_kernel(MsrArgs a) {
     const int p = a.p;
     const uint32_t K = c->msr_K[p];
     if (K == 0 || threadIdx.x != 0) return;
-    const uint32_t S = c->msr_S[p], istep0 = c->i_step[p], k = c->n_iter;
+    const uint32_t istep0 = c->i_step[p], k = c->n_iter;
+    uint32_t istep = istep0;
     const uint32_t* deaths_l = a.hist;
     const uint32_t* deaths_s = a.sched.global ? a.hist + MSR_KMAX : a.hist;
     uint32_t alive_s = a.sched.global ? c->sched_alive[p] : c->n_alive[p], alive_l = c->n_alive[p];
     uint32_t J = K;
     unsigned long long slots = 0, samp = 0, reused = 0;
     for (uint32_t m = 0; m < K; ++m) {
-        if (alive_s == 0 || steps_for(alive_s, a.target) != S || istep0 + S * m >= MARCH_ITER) { J = m; break; }
+        const uint32_t S = c->msr_Sv[p][m];
+        if (alive_s == 0 || steps_for(alive_s, a.target) != S || istep >= MARCH_ITER) { J = m; break; }
+        istep += S;
         const uint32_t sm = a.hist[2 * MSR_KMAX + m], rm = a.hist[3 * MSR_KMAX + m];
         slots += ((unsigned long long)alive_l * S + 255ull) / 256ull * 256ull;
         samp += sm;
@@ -1266,7 +1291,7 @@ __global__ void msr_schedule_kernel(MsrArgs a) {
     c->msr_evals += c->n_samples[p];
     c->msr_exec += samp - reused;
     c->n_iter = k + J;
-    c->i_step[p ^ 1] = istep0 + S * J;
+    c->i_step[p ^ 1] = istep;   // istep0 + the committed iterations' steps
     c->n_alive[p ^ 1] = 0;
     c->n_owned[p ^ 1] = 0;
     c->n_samples[p ^ 1] = 0;
@@ -1280,9 +1305,12 @@ __global__ __launch_bounds__(THREADS) void msr_commit_kernel(MsrArgs a) {
     __shared__ uint32_t sh_app[3 * (THREADS / 64) + 1];
     MarchCtrl* ctrl = a.ctrl;
     const int p = a.p;
+    __shared__ uint8_t sh_S[MSR_KMAX];
     const uint32_t K = ctrl->msr_K[p];
     if (K == 0) return;
-    const uint32_t S = ctrl->msr_S[p], J = ctrl->msr_J, istep0 = ctrl->i_step[p], n_alive = ctrl->n_alive[p];
+    const uint32_t J = ctrl->msr_J, istep0 = ctrl->i_step[p], n_alive = ctrl->n_alive[p];
+    if (threadIdx.x < MSR_KMAX) sh_S[threadIdx.x] = ctrl->msr_Sv[p][threadIdx.x];
+    __syncthreads();
     const Volume& vol = a.vol;
     const CamDev& cam = a.cam;
     const TraceMode mode{0, 1, 1.0f, 0, 0.0f};   // trace_alt
@@ -1305,13 +1333,15 @@ __global__ __launch_bounds__(THREADS) void msr_commit_kernel(MsrArgs a) {
             const f3 o = mk(ot.x, ot.y, ot.z), d = mk(di.x, di.y, di.z);
             const uint2 sc = a.samp[i];
             const uint32_t n_it = sc.y & 31u, cnt_last = (sc.y >> 5) & 15u, rbits = sc.y >> 9;
-            uint32_t ob = sc.x, s = 0;
+            uint32_t ob = sc.x, s = 0, istep = istep0;
             bool ended = false;
             const uint32_t n_run = n_it < J ? n_it : J;
             for (uint32_t it = 0; it < n_run && !ended; ++it) {
+                const uint32_t S = sh_S[it];
                 const uint32_t cnt = it + 1 == n_it ? cnt_last : S;
                 const uint32_t ru = (rbits >> it) & 1u;
-                const bool last = istep0 + S * it + S >= MARCH_ITER;
+                istep += S;
+                const bool last = istep >= MARCH_ITER;
                 float tv[MAX_STEPS_BETWEEN_COMPACTION], av[MAX_STEPS_BETWEEN_COMPACTION];
                 uint2 rv[MAX_STEPS_BETWEEN_COMPACTION];
 #pragma unroll

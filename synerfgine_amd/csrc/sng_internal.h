@@ -60,9 +60,10 @@ struct MarchCtrl {
     uint32_t spec_ok;                // tail_prepare: every later iteration takes 8 steps (else the tail kernels queued
                                      // ahead of that check leave every buffer untouched and the wavefront continues)
     // multi-step speculative rounds (nerf.hip msr_*), per ping-pong buffer of the round's rays
-    uint32_t msr_S[2];               // steps every iteration of the round takes (0: the round is a no-op)
+    uint32_t msr_S[2];               // steps the round's first iteration takes (0: the round is a no-op)
     uint32_t msr_K[2];               // iterations the round marched ahead
     uint32_t msr_J;                  // iterations the last round commits (msr_schedule)
+    uint8_t msr_Sv[2][16];           // steps of each of the round's K iterations (MSR_KMAX; from the last frame's schedule)
     unsigned long long msr_evals;    // samples the rounds' network launches evaluated
     unsigned long long msr_exec;     // ... of which the wavefront would have evaluated (the committed iterations')
     int32_t* tail_live;              // [TAIL_LIVE_CAP] the tail's alive rays per iteration as a difference array (+1 where a
@@ -435,7 +436,7 @@ struct SchedComm {
 void comm_unique_id(uint8_t out[SNG_COMM_ID_BYTES]);
 void comm_init(SchedComm& c, const uint8_t* id, int rank, int world);
 void comm_destroy(SchedComm& c);
-void comm_allreduce_u32(SchedComm& c, uint32_t* dev, size_t n, hipStream_t s);
+void comm_allreduce_u32(SchedComm& c, const uint32_t* src, uint32_t* dst, size_t n, hipStream_t s);   // src == dst: in place
 void comm_gather_to_root(SchedComm& c, const void* d_band, void* d_frame, const size_t* offsets, const size_t* sizes, hipStream_t s);
 
 }  // namespace sng

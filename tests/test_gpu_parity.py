@@ -633,10 +633,18 @@ def test_msr_rounds_equal_wavefront(config, w, h, target, shade, extra):
     try:
         n0, m0 = eng.rng_states(0).copy(), eng.rng_states(1).copy()
         out = {}
-        # on = 2: the same frame again, its rounds sized by the first one's schedule (MarchCtrl::sched_hint);
-        # on = 3: after a frame at another query target, whose schedule is the wrong hint
-        for on in (0, 1, 2, 3):
+        # on = 2: the same frame again, its rounds sized by the first one's schedule (MarchCtrl::sched_hint), which
+        # the rounds follow across step changes; on = 3: after a frame from a moved camera, whose schedule is a wrong
+        # hint; on = 4: after a frame at another query target (the hints are dropped: no hint)
+        cam = np.array(tb.camera_matrix)
+        for on in (0, 1, 2, 3, 4):
             if on == 3:
+                moved = cam.copy()
+                moved[9:12] += np.array([0.05, -0.03, 0.04], np.float32)   # camera position (column 3)
+                tb.camera_matrix = moved
+                eng.frame(target_n_queries=target)
+                tb.camera_matrix = cam
+            if on == 4:
                 eng.frame(target_n_queries=(target or (1 << 21)) // 2 * 3)
             eng.set_rng_states(0, n0)
             eng.set_rng_states(1, m0)
@@ -651,7 +659,7 @@ def test_msr_rounds_equal_wavefront(config, w, h, target, shade, extra):
             out[on] = ([r.download(b) for b in ("final_rgba", "nerf_rgba", "nerf_depth", "nerf_positions")],
                        (r.n_samples, r.n_samples_reused, r.n_hit, r.n_iterations, r.n_reference_slots), list(r.alive_per_iter),
                        list(r.steps_per_iter), list(r.samples_per_iter))
-        for on in (1, 2, 3):
+        for on in (1, 2, 3, 4):
             for a, b in zip(out[0][0], out[on][0]):
                 assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), on
             assert out[0][1:] == out[on][1:], on
