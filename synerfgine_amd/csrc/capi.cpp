@@ -342,7 +342,8 @@ const std::map<std::string, double>& default_params() {
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
         {"bvh_flat", 1},                        // BvhWide walk keeping the nearer child in a register (exact)
-        {"rt_tile", 8},                         // path-kernel tile edge: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
+        {"rt_tile", 8},                         // path-kernel tile width: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
+        {"rt_tile_h", 0},                       // path-kernel tile height: 0 = rt_tile; 4 with rt_tile 8: 8x4 (32 lanes per wave)
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"rt_prio_frac", 0.1},                    // the costliest fraction of the path tiles (last frame's order) at wave priority 3
@@ -1678,10 +1679,11 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 ra.count_waves = c->p("rt_count") == 2.0 ? 1 : 0;
             }
             ra.tile = c->p("rt_tile") == 4.0 ? 4 : 8;
+            ra.tile_h = c->p("rt_tile_h") == 4.0 ? 4 : (c->p("rt_tile_h") == 8.0 && ra.tile == 8 ? 8 : ra.tile);
             ra.buffer_type = (int)c->p("rt_buffer_type");
             if (c->p("rt_tile_order") != 0.0) {
-                const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile - 1) / ra.tile);
-                const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60);
+                const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile_h - 1) / ra.tile_h);
+                const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60) ^ ((uint64_t)ra.tile_h << 56);
                 if (phase != 2) {
                     c->rt_tile_cost.ensure((size_t)n_tiles * 4);
                     c->rt_tile_order.ensure((size_t)(n_tiles + 64) * 4);   // + launch_tile_sort's 64 aux words

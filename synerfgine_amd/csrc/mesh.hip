@@ -805,7 +805,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
     const TraceCtx<LDS, CNT> cx = trace_ctx_setup<LDS, CNT>(a, counts);
     const int lane = threadIdx.x & 63;
     const uint32_t rows = (uint32_t)(a.row1 - a.row0);
-    const uint32_t T = (uint32_t)a.tile, tiles_x = ((uint32_t)a.W + T - 1) / T, n_tiles = tiles_x * ((rows + T - 1) / T);
+    const uint32_t T = (uint32_t)a.tile, TH = (uint32_t)a.tile_h, tiles_x = ((uint32_t)a.W + T - 1) / T, n_tiles = tiles_x * ((rows + TH - 1) / TH);
     while (true) {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(work, 1u);
@@ -821,8 +821,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
             else __builtin_amdgcn_s_setprio(0);
         }
         const uint64_t t0 = wall_clock64();
-        const uint32_t x = (tile % tiles_x) * T + (uint32_t)lane % T, y = (tile / tiles_x) * T + (uint32_t)lane / T;
-        if ((uint32_t)lane < T * T && x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth);
+        const uint32_t x = (tile % tiles_x) * T + (uint32_t)lane % T, y = (tile / tiles_x) * TH + (uint32_t)lane / T;
+        if ((uint32_t)lane < T * TH && x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth);
         if (a.tile_cost && lane == 0) a.tile_cost[tile] = (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull);
     }
     if constexpr (CNT) flush_counts(a.counts, counts, lane);
@@ -833,7 +833,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
 // depend on its cap syn + 1 >= full_dist), so the result is bit-identical.
 template <bool LDS, bool CNT = false>
-__device__ __forceinline__ void trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t kr, uint32_t jp) {
+__device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t kr, uint32_t jp) {
     const float4 s1 = *q.shadow_ray(kr, jp);
     const float4* rk = q.rec + (size_t)kr * q.rec_stride;   // the origin: the record's hit position (header)
     const float4 h0 = rk[0], h1 = rk[1];
@@ -843,7 +843,7 @@ __device__ __forceinline__ void trace_shadow_ray(const RaytraceArgs& a, const Rt
     const float syn = depth_test_world(pos, Lv, a.objs, a.n_objs, cx, oh, full_dist);
     const float nerf = depth_test_nerf((float)((double)syn + 1.0), a.shadow_steps, a.vol, pos, Lv, inv(Lv), 0, a.vol.max_mip, fminf(syn, full_dist));
     const float sh = fminf(fminf(nerf, syn), full_dist);
-    q.mask[q.mask_at(kr, jp)] = pow_small_int(smoothstep(sh / full_dist), a.syn_shadow_factor);
+    return pow_small_int(smoothstep(sh / full_dist), a.syn_shadow_factor);
 }
 
 // The shadow-ray pass after the path kernel.  (Tracing each tile's shadow rays in the wave that traced its paths
@@ -875,7 +875,7 @@ __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQue
         const uint32_t j = c * 64u + (uint32_t)lane;
         if (j >= total) continue;
         const uint32_t kr = j / q.nps, jp = j - kr * q.nps;   // record, shadow sample (RtQueue::shadow_ray)
-        trace_shadow_ray(a, q, cx, kr, jp);
+        q.mask[q.mask_at(kr, jp)] = trace_shadow_ray(a, q, cx, kr, jp);
     }
     if constexpr (CNT) flush_counts(a.counts + 3, counts, lane);
 }
@@ -1156,7 +1156,7 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     const bool lds = a.scene_in_lds != 0;
     const uint32_t tp = lds ? a.lds_tpb : 512u, ts = tp, per_cu = 1024u / tp;   // 16 waves per CU either way
     const size_t lp = trace_lds_bytes(a, lds, tp), ls = trace_lds_bytes(a, lds, ts);
-    const uint32_t n_tiles = (((uint32_t)a.W + a.tile - 1) / a.tile) * (((uint32_t)(a.row1 - a.row0) + a.tile - 1) / a.tile);
+    const uint32_t n_tiles = (((uint32_t)a.W + a.tile - 1) / a.tile) * (((uint32_t)(a.row1 - a.row0) + a.tile_h - 1) / a.tile_h);
     const uint32_t bp = std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * per_cu);
     const uint32_t sb = shadow_blocks ? shadow_blocks : a.persistent_blocks * per_cu;
     if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in

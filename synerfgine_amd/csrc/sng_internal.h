@@ -270,7 +270,8 @@ struct RaytraceArgs {
     const uint32_t* tile_order; // 8x8 tile visiting order (nullptr: row-major)
     uint32_t* tile_cost;        // per-tile cycles of this frame (nullptr: not recorded)
     int bvh_flat;               // BvhWide traversal with the nearer child in a register (bvh_walk_near)
-    int tile;                   // path-kernel tile edge in pixels (8: 64 lanes, 4: 16 lanes per wave)
+    int tile;                   // path-kernel tile width in pixels (8 or 4)
+    int tile_h;                 // ... and height (tile * tile_h <= 64 lanes per wave: 8x8, 8x4, 4x4)
     unsigned long long* counts; // counting frames (rt_count): path kernel {queries, box, tri}, shadow kernel {queries, box, tri}
     int count_waves;            // rt_count = 2: box / tri entries count wave iterations of those loops (SIMD efficiency)
     int buffer_type;            // ImgBufferType (raytracer.cuh:20): 0 Final, 1 NextOrigin .. 7 NerfShadow (one-kernel path)

@@ -253,7 +253,8 @@ def test_errors_are_loud(tb):
 
 
 @pytest.mark.parametrize("overrides", [{}, {"path_trace_depth": 3, "light_samples": 3}, {"fast_slab": 0}, {"scene_lds": 0},
-                                       {"scene_lds": 0, "light_samples": 16}, {"path_trace_depth": 1}, {"rt_tile": 4}])
+                                       {"scene_lds": 0, "light_samples": 16}, {"path_trace_depth": 1}, {"rt_tile": 4}, {"rt_tile_h": 4},
+                                       {"rt_prio_frac": 0}])
 def test_wavefront_raytracer_equals_megakernel(overrides):
     """Deferred shadow-ray queues (rt_wavefront=1) reproduce the one-kernel path tracer bit for bit."""
     import ctypes

@@ -21,9 +21,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3")
 ap.add_argument("--bounds", action="append", default=[])
 ap.add_argument("--frames", type=int, default=5)
+ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE")
 args = ap.parse_args()
 model = "lego" if args.config != "c4" else "synthetic"
-tb, eng, _ = S.make_engine(args.config, model=model)
+ov = {kv.split("=")[0]: float(kv.split("=")[1]) for kv in args.set}
+tb, eng, _ = S.make_engine(args.config, model=model, overrides=ov)
 W, H = eng.resolution()["mesh"]
 cases = [None] + [tuple(int(x) for x in b.replace("-", ",").split(",")) for b in args.bounds]
 for rows in cases:
@@ -35,7 +37,8 @@ for rows in cases:
         ms.append(r.ms_raytrace)
     torch.cuda.synchronize()
     y0, y1 = rows if rows else (0, H)
-    n_tiles = ((W + 7) // 8) * ((y1 - y0 + 7) // 8)
+    tw, th = int(eng.get_param("rt_tile")), int(eng.get_param("rt_tile_h")) or int(eng.get_param("rt_tile"))
+    n_tiles = ((W + tw - 1) // tw) * ((y1 - y0 + th - 1) // th)
     cost = eng.frame_buffer("rt_tile_cost", np.uint32)[:n_tiles].astype(np.float64) / CLOCK_HZ * 1e3
     q = np.quantile(cost, [0.5, 0.9, 0.99, 0.999, 1.0])
     print(json.dumps({"config": args.config, "rows": [y0, y1], "tiles": n_tiles, "raytrace_ms_median": round(float(np.median(ms)), 3),
