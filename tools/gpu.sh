@@ -60,7 +60,7 @@ for step in "$@"; do
       fi ;;
     pmc)
       d=$OUT/pmc$n
-      a="--config ${cfg:-c3} --steps 3 --warmup 1 --no-cpu-baseline --no-sweep $args"
+      a="--config ${cfg:-c3} --steps 3 --warmup 2 --no-cpu-baseline --no-sweep $args"
       rc=0
       for c in FETCH_SIZE WRITE_SIZE; do
         kt=""; [ $c = FETCH_SIZE ] && kt="--kernel-trace"
@@ -79,7 +79,7 @@ for step in "$@"; do
       ctr="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
       [ $kind = sqlds ] && ctr="SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
       timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $ctr \
-        -d $d -o run --output-format csv -- python3 bench.py --config ${cfg:-c3} --steps 3 --warmup 1 --no-cpu-baseline --no-sweep $args > $log 2>&1
+        -d $d -o run --output-format csv -- python3 bench.py --config ${cfg:-c3} --steps 3 --warmup 2 --no-cpu-baseline --no-sweep $args > $log 2>&1
       rc=$?
       [ $rc -eq 0 ] && python3 tools/sq_summary.py $d $OUT/${kind}_${cfg:-c3}.json ${cfg:-c3} 2>&1 | tee -a $log; rc=${PIPESTATUS[0]} ;;
     py)

@@ -30,7 +30,7 @@ def load(d, counter, sub=None):
     if not f:
         raise SystemExit(f"no counter_collection.csv for {counter}")
     per = defaultdict(list)
-    for r in csv.DictReader(open(f[0])):
+    for r in sorted(csv.DictReader(open(f[0])), key=lambda r: int(r.get("Dispatch_Id", 0) or 0)):
         if r.get("Counter_Name", counter) != counter:
             continue
         per[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
@@ -77,7 +77,7 @@ def main():
             v["label"] = ("exceeds the HBM peak: part of FETCH_SIZE was served by the Infinity Cache (MALL)" if v["hbm_bytes_per_launch"] / t > 8e12
                           else "L2 fetch + write bytes (HBM or MALL)")
     net = [k for k in kernels if "nerf_network_kernel" in k]
-    res = {"note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes; averages over all launches of bench.py --steps 3 --warmup 1; "
+    res = {"note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->bytes; averages over all launches of bench.py --steps 3 --warmup 2 (the network kernel's roofline entry and hbm_bytes_per_launch: the timed frames' launches only); "
                    "FETCH_SIZE = bytes the L2 fetched from the Infinity Cache or HBM, so these are upper bounds on HBM traffic",
            "kernel": net[0] if net else None,
            "hbm_bytes_per_launch": kernels[net[0]]["hbm_bytes_per_launch"] if net else None,
@@ -118,8 +118,19 @@ def main():
             res["bench_line"] = {"samples_per_launch": rf["samples_in_launches"] / max(1, rf["launches"]),
                                  "launches_per_frame": rf["launches"] / max(1, line["steps"]), "steps": line["steps"],
                                  "warmup": line["warmup"], "workload": line["config"]["workload"]}
-            if "nerf_network_kernel" in roof:
+            if "nerf_network_kernel" in roof and net:
                 v = roof["nerf_network_kernel"]
+                # the timed frames' launches only (the last steps x launches-per-frame in dispatch order): the warm-up
+                # frames march without the look-ahead hints, so their launches are larger than the line's
+                n_t = int(round(rf["launches"]))
+                f_all, w_all = load(d, "FETCH_SIZE").get(net[0], []), load(d, "WRITE_SIZE").get(net[0], [])
+                if 0 < n_t <= min(len(f_all), len(w_all)):
+                    f_t, w_t = f_all[-n_t:], w_all[-n_t:]
+                    v["fetch_bytes_per_launch"] = 2.0 * sum(f_t) / n_t * 1024
+                    v["write_bytes_per_launch"] = sum(w_t) / n_t * 1024
+                    v["hbm_bytes_per_launch"] = v["fetch_bytes_per_launch"] + v["write_bytes_per_launch"]
+                    v["launches_timed"] = n_t
+                    res["hbm_bytes_per_launch"] = v["hbm_bytes_per_launch"]
                 v["samples_per_launch"] = res["bench_line"]["samples_per_launch"]
                 v["algorithmic_bytes_per_launch"] = v["samples_per_launch"] * (28 + 8 * 8 * 4 * 2 + 8)
                 v["traffic_over_algorithmic"] = v["hbm_bytes_per_launch"] / v["algorithmic_bytes_per_launch"]
