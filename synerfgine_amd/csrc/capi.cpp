@@ -383,6 +383,7 @@ const std::map<std::string, double>& default_params() {
         {"nerf_msr", 1},                        // multi-step speculative rounds while n_steps is 2..7 (nerf.hip msr_*; exact)
         {"nerf_msr_budget", 16777216},          // samples one such round may generate (K = clamp(budget / (S n_alive), 1, kmax))
         {"nerf_msr_kmax", 16},                  // iterations one such round marches ahead (<= 16)
+        {"nerf_msr_span", -1},                  // rounds follow the last frame's schedule across step changes (1), not (0), -1: on banded frames
         {"march_log", 0},                       // diagnostics: log {alive, steps, samples} of every iteration (sng_frame_buffer "march_log")
         {"nerf_onestep", 1},                    // trace_alt's one-step regime (n_alive > target / 2) ray-local and speculative (fused.hip)
         {"nerf_onestep_horizon", 2048},         // iterations one speculative segment of the regime spans
@@ -1332,6 +1333,10 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             ma.vol = vol; ma.cam = cam; ma.sched = a.sched; ma.ctrl = ctrl; ma.target = target;
             ma.budget = (uint32_t)std::min<double>((double)c->sample_cap, std::max(1.0, c->p("nerf_msr_budget")));
             ma.kmax = (uint32_t)std::min<double>(MSR_KMAX, std::max(1.0, c->p("nerf_msr_kmax")));
+            // rounds across step changes: fewer rounds (their fixed cost matters most on a thin band) for more
+            // samples past the rays' ends; by default under the frame-wide schedule of a banded frame only
+            const double span = c->p("nerf_msr_span");
+            ma.span = span < 0 ? (gsched ? 1 : 0) : (span != 0.0 ? 1 : 0);
             c->msr_alpha.ensure(c->sample_cap * 4);
             ma.coords = c->coords.as<float>(); ma.samp = c->samp.as<uint2>(); ma.tbuf = c->spec_t.as<float>(); ma.net_out = c->net_out.as<uint2>();
             ma.abuf = c->msr_alpha.as<float>();

@@ -1004,13 +1004,14 @@ __global__ void tail_prepare_kernel(MarchCtrl* ctrl, uint32_t* work, int p, uint
 // (only 2..7: 1 is the one-step regime's, 8 the tail's) and K iterations before MARCH_ITER, each with its own
 // step count Sv[m].  K == 0: the round is a no-op (every msr kernel returns without touching state).
 // The last frame's schedule (MarchCtrl::sched_hint, frame-wide, so every rank of a banded frame forms the same
-// round) predicts the steps of the iterations ahead: when it agrees with S_0 the round follows it, across step
-// changes, for as long as it stays in 2..7 (up to kmax iterations and budget / n_sched samples per ray);
+// round) predicts the steps of the iterations ahead: when it agrees with S_0 the round follows it -- across step
+// changes when `span` (MsrArgs), else while it stays S_0 -- in 2..7, up to kmax iterations and budget / n_sched
+// samples per ray;
 // otherwise the round assumes S_0 throughout (no hint: as far as the budget allows; a hint that disagrees: the
 // schedule is near a change, 2 iterations).  Any guess is exact: msr_schedule commits the iterations whose
 // frame-wide count takes the guessed steps, and the rest are marched again.
 __device__ __forceinline__ uint32_t msr_shape(const MarchCtrl* c, uint32_t n_sched, uint32_t istep0, uint32_t target, uint32_t budget,
-                                              uint32_t kmax, uint8_t* Sv) {
+                                              uint32_t kmax, int span, uint8_t* Sv) {
     if (n_sched == 0 || istep0 >= MARCH_ITER) return 0u;
     const uint32_t s = steps_for(n_sched, target);
     if (s < 2 || s >= MAX_STEPS_BETWEEN_COMPACTION) return 0u;
@@ -1022,7 +1023,7 @@ __device__ __forceinline__ uint32_t msr_shape(const MarchCtrl* c, uint32_t n_sch
         uint32_t istep = istep0, tot = 0;
         while (K < kmax && istep < MARCH_ITER) {
             const uint32_t sm = K == 0 ? s : (k0 + K < TAIL_LIVE_CAP ? (uint32_t)c->sched_hint[k0 + K] : 0u);
-            if (sm < 2 || sm >= MAX_STEPS_BETWEEN_COMPACTION || (K > 0 && tot + sm > per_ray)) break;
+            if (sm < 2 || sm >= MAX_STEPS_BETWEEN_COMPACTION || (K > 0 && tot + sm > per_ray) || (!span && sm != s)) break;
             Sv[K++] = (uint8_t)sm;
             tot += sm;
             istep += sm;
@@ -1057,7 +1058,7 @@ __global__ __launch_bounds__(THREADS) void msr_generate_kernel(MsrArgs a) {
     const uint32_t n_sched = a.sched.global ? ctrl->sched_alive[p] : n_alive;
     if (threadIdx.x == 0) {
         uint8_t Sv[MSR_KMAX];
-        const uint32_t K = msr_shape(ctrl, n_sched, ctrl->i_step[p], a.target, a.budget, a.kmax, Sv);
+        const uint32_t K = msr_shape(ctrl, n_sched, ctrl->i_step[p], a.target, a.budget, a.kmax, a.span, Sv);
         sh_app[3 * (THREADS / 64)] = K;
         for (uint32_t m = 0; m < MSR_KMAX; ++m) sh_S[m] = m < K ? Sv[m] : (uint8_t)0;
         if (blockIdx.x == 0) {

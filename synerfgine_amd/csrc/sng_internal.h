@@ -361,6 +361,7 @@ struct MsrArgs {
     uint32_t target;
     uint32_t budget;              // samples one round may generate: K = clamp(budget / (S n_sched), 1, kmax)
     uint32_t kmax;                // <= MSR_KMAX
+    int span;                     // a round may follow the hint across step changes (else: one step count per round)
     float* coords;                // NerfCoordinate AoS of the network samples
     uint2* samp;                  // per ray: {first network sample, n_it | cnt_last << 5 | reuse bits << 9}
     float* tbuf;                  // [sample j of the ray][ray] march t of every sample

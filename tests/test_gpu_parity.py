@@ -618,6 +618,7 @@ def test_onestep_regime_equals_wavefront(config, w, h, target, shade, horizon):
 @pytest.mark.parametrize("config,w,h,target,shade,extra", [
     ("c4", 1920, 1080, 0, False, {}),                                   # the real regime: 78 iterations of 2..8 steps after the one-step one
     ("c4", 1920, 1080, 0, False, {"nerf_msr_kmax": 3}),                 # short rounds
+    ("c4", 1920, 1080, 0, False, {"nerf_msr_span": 1}),                 # rounds across step changes (banded frames' default)
     ("c4", 160, 90, 1 << 15, True, {}),                                 # 2..7 steps from the first chunk, shadows + mesh
     ("c4", 160, 90, 1 << 15, False, {"nerf_msr_budget": 4096}),         # K = 1 from the budget
     ("c4", 96, 54, 1 << 13, False, {"nerf_fused": 0}),                  # rounds down to the last ray (no tail)
