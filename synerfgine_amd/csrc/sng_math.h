@@ -300,7 +300,7 @@ SNG_HD float advance_n_steps(float t, float cone, float n) { return from_steppin
 // frame by step_space() -- identical float expressions, so identical bits; the marchers' inner loops
 // then spend one log or exp per conversion instead of seven.
 struct StepSpace {
-    float cone, log1p_c, a, b, at, bt;
+    float cone, log1p_c, a, b, at, bt, rlog1p_c;   // rlog1p_c = RN(1 / log1p_c)
 };
 SNG_HD StepSpace step_space(float cone) {
     StepSpace k{};
@@ -311,6 +311,7 @@ SNG_HD StepSpace step_space(float cone) {
     k.b = (sng_logf(MAX_STEP) - sng_logf(k.log1p_c)) / k.log1p_c;
     k.at = sng_expf(k.a * k.log1p_c);
     k.bt = sng_expf(k.b * k.log1p_c);
+    k.rlog1p_c = recip_rn(k.log1p_c);
     return k;
 }
 // The two constant divisions as exact reciprocal forms: x / MIN_STEP is div_by (see above), and since
@@ -319,7 +320,7 @@ SNG_HD StepSpace step_space(float cone) {
 SNG_HD float to_stepping_space(float t, const StepSpace& k) {
     if (k.cone <= 1e-5f) return div_by(t, MIN_STEP, INV_MIN_STEP);
     if (t <= k.at) return div_by(t - k.at, MIN_STEP, INV_MIN_STEP) + k.a;
-    else if (t <= k.bt) return sng_logf(t) / k.log1p_c;
+    else if (t <= k.bt) return div_by(sng_logf(t), k.log1p_c, k.rlog1p_c);   // the IEEE quotient (Markstein, as div_by above)
     else return div_by(t - k.bt, MIN_STEP, INV_MIN_STEP) * (1.0f / 1024.0f) + k.b;
 }
 static_assert(MAX_STEP == MIN_STEP * 1024.0f, "MAX_STEP / MIN_STEP must be 2^10");

@@ -116,7 +116,25 @@ int main() {
         ++n_log;
         if (!same(div_by(f, den, recip_rn(den)), f / den)) ++bad_log;
     }
-    std::printf("{\"div\": [%ld, %ld], \"march\": [%ld, %ld, %ld], \"slab\": [%ld, %ld], \"logdiv\": [%ld, %ld]}\n", n_div, bad_div, n_march,
-                n_samples, bad_march, n_slab, bad_slab, n_log, bad_log);
-    return (bad_div || bad_march || bad_slab || bad_log) ? 1 : 0;
+    // to_stepping_space's log branch: sng_logf(t) / log1p_c as div_by with RN(1 / log1p_c), for every t in
+    // (at, bt] (strided by 7 ulps) at five cone angles.  Its quotients are IEEE whenever |sng_logf(t)| >= 2^-105
+    // (below that the FMA remainder underflows); t != 1 gives |log t| >= 2^-25 and t == 1 gives 0 exactly.
+    long bad_step = 0, n_step = 0;
+    const float cones[5] = {1.0f / 1024.0f, 1.0f / 256.0f, 1.0f / 128.0f, 0.01f, 0.05f};
+    for (float cone : cones) {
+        const StepSpace k = step_space(cone);
+        uint32_t u0, u1;
+        std::memcpy(&u0, &k.at, 4);
+        std::memcpy(&u1, &k.bt, 4);
+        for (uint32_t u = u0 + 1; u <= u1; u += 7) {
+            float t;
+            std::memcpy(&t, &u, 4);
+            ++n_step;
+            const float x = sng_logf(t);
+            if (!same(div_by(x, k.log1p_c, k.rlog1p_c), x / k.log1p_c) || !same(to_stepping_space(t, k), x / k.log1p_c)) ++bad_step;
+        }
+    }
+    std::printf("{\"div\": [%ld, %ld], \"march\": [%ld, %ld, %ld], \"slab\": [%ld, %ld], \"logdiv\": [%ld, %ld], \"stepdiv\": [%ld, %ld]}\n", n_div,
+                bad_div, n_march, n_samples, bad_march, n_slab, bad_slab, n_log, bad_log, n_step, bad_step);
+    return (bad_div || bad_march || bad_slab || bad_log || bad_step) ? 1 : 0;
 }

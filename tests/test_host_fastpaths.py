@@ -23,6 +23,7 @@ def test_fast_division_linear_marcher_and_slab_are_exact():
         assert r["div"][0] > 7_000_000 and r["div"][1] == 0
         assert r["march"][1] > 100_000 and r["march"][2] == 0
         assert r["slab"][0] > 1_000_000 and r["slab"][1] == 0
+        assert r["stepdiv"][0] > 1_000_000 and r["stepdiv"][1] == 0
         assert out.returncode == 0
     finally:
         shutil.rmtree(d, ignore_errors=True)
