@@ -451,11 +451,13 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
             // the march matters only while its mask stays below `overall`: the mask is non-decreasing in the march
             // distance, so the walk may stop at the smallest c with mask(c) >= overall (depth_test_nerf's cap; the
             // march distance never decreases, so a walk past c ends at a result >= c and leaves `overall` as it is)
+            // Any cap c with mask(c) >= overall is exact; c = overall k2 / k1 (1 + 2^-20) is one: mask(c) rounds c k1 to
+            // float and divides by k2, relative errors below 2^-23 in all, so mask(c) >= overall (1 + 2^-20)(1 - 2^-23).
+            // No division is needed (k1 >= 1: a multiply by 1 / k1 in double is within 2^-52 of the quotient).
             float cap = full_d <= fd ? full_d : __builtin_huge_valf();
             if (k1 > 0.0f && k2 > 0.0 && overall >= 0.0f) {
-                float c = (float)((double)overall * k2 / (double)k1);
-                for (int it = 0; it < 4 && c < cap && (double)(c * k1) / k2 < (double)overall; ++it) c = nextafterf(c, __builtin_huge_valf());
-                if ((double)(c * k1) / k2 >= (double)overall) cap = fminf(cap, c);
+                const float c = (float)((double)overall * k2 * (1.0 / (double)k1) * (1.0 + 0x1p-20));
+                cap = fminf(cap, c);
             }
             const float nd = fminf(full_d, depth_test_nerf(fd, MAX_STEPS_BETWEEN_COMPACTION, a.vol, src, Ld, inv(Ld), 0, a.vol.max_mip, cap));
             const double mask = (double)(nd * k1) / k2;
