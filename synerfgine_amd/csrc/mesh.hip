@@ -819,7 +819,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
         // the costliest tiles of the last frame (the first prio_tiles of the order) issue ahead of the other waves
         // of their SIMD: the launch lasts as long as its slowest tile's chain, and the others have slack
         if (a.prio_tiles) {
-            if (__builtin_amdgcn_readfirstlane(k) < a.prio_tiles) __builtin_amdgcn_s_setprio(3);
+            const uint32_t ks = __builtin_amdgcn_readfirstlane(k);
+            if (ks < a.prio_tiles) __builtin_amdgcn_s_setprio(3);
+            else if (ks < a.prio2_tiles) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
         }
         const uint64_t t0 = wall_clock64();

@@ -276,6 +276,7 @@ struct RaytraceArgs {
     int count_waves;            // rt_count = 2: box / tri entries count wave iterations of those loops (SIMD efficiency)
     int buffer_type;            // ImgBufferType (raytracer.cuh:20): 0 Final, 1 NextOrigin .. 7 NerfShadow (one-kernel path)
     uint32_t prio_tiles;        // the first prio_tiles tiles of tile_order run at wave priority 3 (0: off)
+    uint32_t prio2_tiles;       // ... and the tiles before prio2_tiles at priority 2
 };
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
