@@ -346,8 +346,8 @@ const std::map<std::string, double>& default_params() {
         {"rt_tile_h", 0},                       // path-kernel tile height: 0 = rt_tile; 4 with rt_tile 8: 8x4 (32 lanes per wave)
         {"scene_lds", 1},                       // BVH nodes + triangles staged in LDS per workgroup when they fit
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
-        {"rt_prio_frac", 0.1},
-        {"rt_prio2_frac", 0.25},                // ... the tiles up to this fraction of the order at priority 2                    // the costliest fraction of the path tiles (last frame's order) at wave priority 3
+        {"rt_prio_frac", 0.1},                  // the costliest fraction of the path tiles (last frame's order) at wave priority 3
+        {"rt_prio2_frac", 0.25},                // ... the tiles up to this fraction of the order at priority 2
         {"nerf_gbuffer", 0},                    // 1: NeRF normals every frame (otherwise only when shadow_on_nerf needs them)
         {"rt_plist", 1},                        // per-pixel hit-record lists for the colour replay (rt_accumulate_kernel)
         {"glow_mode", 0},                       // Testbed::Nerf::glow_mode (testbed.h:871): bits 1 green grid, 2 cut line, 4 mask to alpha,
