@@ -30,7 +30,7 @@ BYTES_PER_SAMPLE = 28 + 8 * 8 * 4 * 2 + 8   # NerfCoordinate read + 8 levels x 8
 FLOPS_PER_SAMPLE = 20480                     # 2*(32*64+64*16) + 2*(32*64+64*64+64*16)
 HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F16_PEAK_TFLOPS = 2500.0                # dense fp16/bf16 MFMA
-ROUND = "r04"
+ROUND = "r05"
 
 WORKLOADS = {
     "c2": "lego NeRF only (show_virtual_obj=0, shadows off)",
@@ -180,7 +180,7 @@ def cpu_sample_c3(eng_cfg, config, scale, model_name, overrides):
 
 def latest_profile(prefix, config):
     """profiles/<prefix>_<round>_<config>.json of the newest round that has one (this round's first)."""
-    for rnd in (ROUND, "r03", "r02", "r01"):
+    for rnd in (ROUND, "r04", "r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", f"{prefix}_{rnd}_{config}.json")
         if os.path.exists(path):
             return path
@@ -229,6 +229,20 @@ def valu_profile(config):
     return out
 
 
+def per_launch_table(stats):
+    """Per launch index of a frame (the head round's network launch, the second round's, ...): the samples the
+    launch evaluated (read by the kernel itself) and its duration (its own dispatch's HIP events), averaged over
+    the frames; the line's `frac` is their sample-weighted figure (sum of bytes over sum of durations)."""
+    out = []
+    for k in range(max((len(s.network_launch) for s in stats), default=0)):
+        rows = [s.network_launch[k] for s in stats if len(s.network_launch) > k]
+        smp = sum(r[0] for r in rows) / len(rows)
+        ms = sum(r[1] for r in rows) / len(rows)
+        out.append({"index": k, "frames": len(rows), "samples": round(smp, 1), "ms": round(ms, 5),
+                    "frac": round(smp * BYTES_PER_SAMPLE / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if ms > 0 else None})
+    return out
+
+
 def frame_cells(eng, cells, frames, warmup, px):
     """Render `frames` timed frames (after `warmup`) per parameter cell; frames/s (host wall clock around the
     synchronous sng_render_frame calls), samples per NeRF pixel and the network launches' roofline fraction."""
@@ -254,6 +268,7 @@ def frame_cells(eng, cells, frames, warmup, px):
                     "samples_per_px": round(r.n_samples / px, 3), "reference_slots_per_px": round(r.n_reference_slots / px, 3),
                     "hit_frac": round(r.n_hit / px, 4),
                     "network_roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "field_sample_weighted_frac": round(fsw, 4),
+                    "network_per_launch": per_launch_table(st),
                     "stages_ms": {"raytrace": round(r.ms_raytrace, 3), "nerf": round(r.ms_nerf, 3), "shadow": round(r.ms_shadow, 3)}})
     return out
 
@@ -577,6 +592,7 @@ def main():
     ms_os = sum(s.ms_onestep for s in stats)
     tail_samples -= os_evals
     avg_launch_ms = ms_net / max(1, launches)
+    per_launch = per_launch_table(stats)
     bytes_per_launch = samples * BYTES_PER_SAMPLE / max(1, launches)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     tflops = samples * FLOPS_PER_SAMPLE / (ms_net * 1e-3) / 1e12 if ms_net > 0 else 0.0
@@ -639,6 +655,7 @@ def main():
                          "traffic_over_algorithmic": round(traffic / bytes_per_launch, 4) if traffic and bytes_per_launch else None,
                          "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
                          "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches, "samples_in_launches": int(samples),
+                         "per_launch": per_launch,
                          "timing": "HIP events recorded by each launch's own dispatch (hipExtLaunchKernelGGL start/stop events) on the NeRF stream over the timed region" +
                                    ("" if args.serial_streams else "; the kernel shares the GPU with the raytracer stream, so this is the "
                                     "contended duration (uncontended: --serial-streams)"),
@@ -673,13 +690,18 @@ def main():
                 u = frame_cells(eng, [{"concurrent_streams": 0}], 10, 2, NW * NH)[0]
                 eng.set_param("concurrent_streams", 1)
                 chk = os.path.join(REPO, "profiles", f"{ROUND}_roofline_check.json")
+                same = json.load(open(chk)).get("uncontended") if os.path.exists(chk) else None
+                # one source per figure: the uncontended frac is the rocprofv3 trace's (the same bench.py command under
+                # tools/gpu.sh profdriver, durations from the kernel trace); this process's HIP events are the labelled
+                # alternate (a ~6 us launch's HIP-event duration is ~2x its trace duration)
                 result["roofline"]["uncontended"] = {
-                    "frac": u["network_roofline_frac"], "field_sample_weighted_frac": u["field_sample_weighted_frac"],
+                    "frac": round(same["rocprof_frac"], 4) if same and "rocprof_frac" in same else u["network_roofline_frac"],
+                    "source": (f"rocprofv3 kernel trace of the driver-format command ({os.path.relpath(chk, REPO)}, tools/gpu.sh profdriver)"
+                               if same and "rocprof_frac" in same else "HIP events of this process (no rocprof check of this round)"),
+                    "per_launch": same.get("per_launch") if same else None,
+                    "alternates": {"hip_events_this_process": {"frac": u["network_roofline_frac"], "per_launch": u["network_per_launch"]}},
+                    "field_sample_weighted_frac": u["field_sample_weighted_frac"],
                     "frames_per_s": u["frames_per_s"],
-                    "rocprof_same_process": json.load(open(chk)).get("uncontended") if os.path.exists(chk) else None,
-                    "rocprof_note": "tools/gpu.sh profdriver: rocprofv3 kernel trace of a bench.py process like this one; its own durations "
-                                    "of the same launches (profiles/<round>_roofline_check.json). Each frame's second speculative round is a "
-                                    "~6 us launch whose HIP-event duration is ~2x its rocprof one, which lowers this leg's frac by ~6 %",
                     "note": "the same frames with the raytracer and the NeRF serialized (concurrent_streams=0, 10 frames after "
                             "the timed region): the network launches run alone. The timed line runs the streams concurrently, "
                             "where the raytracer's persistent grids leave the NeRF stream rt_reserved_cus CUs, so `frac` above "

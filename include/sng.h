@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 3
+#define SNG_ABI_VERSION 4
 
 enum {
     SNG_OK = 0,
@@ -108,6 +108,9 @@ typedef struct {
     uint32_t msr_exec;          /* ... of which the per-iteration wavefront would have evaluated */
     uint32_t sched_reductions;  /* frame-wide schedule reductions (all-reduces per rank) the frame made; 0 without a
                                    communicator, reducer or replay */
+    uint32_t n_launch_rec;      /* network launches recorded below (collect_kernel_times; min(network_launches, 16)) */
+    float ms_network_launch[16];        /* each launch's duration (its own dispatch's start/stop events) ... */
+    uint32_t samples_network_launch[16];/* ... and the sample count it evaluated (read by the kernel itself) */
 } sng_frame_result;
 
 typedef struct { float pos[3]; float intensity; float size; int32_t type; /* 0 point, 1 directional */ } sng_light;
@@ -289,7 +292,8 @@ int sng_set_sched_reducer(sng_ctx* ctx, sng_sched_reduce_fn fn, void* user);
  * returns, e.g. recorded at world size 1 over the full frame.  Every reduction point of the following frames
  * copies its record to the device asynchronously on the context's stream (no host sync, no communicator);
  * the cursor restarts at each frame, and a frame whose reductions differ from the records fails with
- * SNG_ERR_STATE.  records NULL detaches.  Excludes a communicator or host reducer. */
+ * SNG_ERR_STATE.  records NULL detaches; n_words 0 with records non-NULL is SNG_ERR_INVALID.  Excludes a
+ * communicator or host reducer. */
 int sng_set_sched_replay(sng_ctx* ctx, const uint32_t* records, uint64_t n_words);
 /* Final composition of a banded frame ("a final RCCL gather to GPU 0 of RGBA8"): rank r's
  * final rows [bounds[r], bounds[r+1]) as RGBA8 (the sng_final_rgba8 encoding) go to rank 0 over the

@@ -173,6 +173,8 @@ class FrameResult:
         self.alive_per_iter = list(r.alive_per_iter)[: min(64, r.n_iterations)]
         self.steps_per_iter = list(r.steps_per_iter)[: min(64, r.n_iterations)]
         self.samples_per_iter = list(r.samples_per_iter)[: min(64, r.n_iterations)]
+        # per network launch (collect_kernel_times): (samples the launch evaluated, its duration in ms)
+        self.network_launch = [(int(r.samples_network_launch[k]), float(r.ms_network_launch[k])) for k in range(r.n_launch_rec)]
 
     def download(self, name):
         """Copy a device output buffer to host as float32 [H, W, C]."""

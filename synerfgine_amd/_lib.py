@@ -93,6 +93,9 @@ class sng_frame_result(ctypes.Structure):
         ("msr_evals", ctypes.c_uint32),
         ("msr_exec", ctypes.c_uint32),
         ("sched_reductions", ctypes.c_uint32),
+        ("n_launch_rec", ctypes.c_uint32),
+        ("ms_network_launch", ctypes.c_float * 16),
+        ("samples_network_launch", ctypes.c_uint32 * 16),
     ]
 
 
@@ -217,7 +220,7 @@ SIGNATURES = {
 _lib = None
 
 
-ABI_VERSION = 3   # SNG_ABI_VERSION of include/sng.h
+ABI_VERSION = 4   # SNG_ABI_VERSION of include/sng.h
 
 
 def load():

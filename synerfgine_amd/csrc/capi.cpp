@@ -310,9 +310,9 @@ const std::map<std::string, double>& default_params() {
         {"res_factor", 64},                     // Testbed::m_fixed_res_factor (testbed.h:656)
         {"vo_scale", 4},                        // Engine::m_relative_vo_scale (engine.cuh:113)
         {"exposure", 0.0},                      // Testbed::m_exposure
-        {"tonemap_curve", 0},
+        {"tonemap_curve", 0},                   // Testbed::m_tonemap_curve (engine.cu:406): 0 Identity, 1 ACES, 2 Hable, 3 Reinhard
         {"rt_buffer_type", 0},                  // RayTracer::m_buffer_to_show (raytracer.cuh:20,179): 0 Final, 1 NextOrigin, 2 SrcOrigin,
-                                                //   3 NextDirection, 4 SrcDirection, 5 Normal, 6 Depth, 7 NerfShadow                   // Testbed::m_tonemap_curve (engine.cu:406): 0 Identity, 1 ACES, 2 Hable, 3 Reinhard
+                                                //   3 NextDirection, 4 SrcDirection, 5 Normal, 6 Depth, 7 NerfShadow
         {"path_trace_depth", 2},                // RayTracer::m_ray_iters (raytracer.cuh:160)
         {"light_samples", 2},                   // RayTracer::m_samples
         {"syn_shadow_samples", 4},              // RayTracer::m_shadow_iters
@@ -334,8 +334,11 @@ const std::map<std::string, double>& default_params() {
         {"smooth_threshold", 1.0},              // sng_position_kernel_threshold (unused by the path)
         {"max_shadow_variance", 0.0},           // sng_shadow_depth_variance (unused by the path)
         {"concurrent_streams", 1},              // 1: raytracer and NeRF streams overlap (engine.cu:386-405 run them back to back)
-        {"rt_start_chunk", -1},                 // concurrent mode: raytracer starts after this many 4-iteration NeRF chunks (-1: 1 for
-                                                //   bands of >= 60 % of the rows, else 0 -- thin bands are latency bound)
+        {"rt_start_chunk", 0},                  // concurrent mode: 0 the raytracer starts at frame start beside init_rays; k > 0 its path
+                                                //   kernel waits for the head's network launch (the first speculative round's, or the
+                                                //   wavefront's of chunk k); -1: 1 for bands of >= 60 % of the rows, else 0.  C3 A/B
+                                                //   (round 5, 4 alternating pairs): 0 -> 295-298 frames/s, 1 -> 271-272 (the path kernel,
+                                                //   the frame's critical path, idles ~0.3 ms behind init_rays + generate + network)
         {"rt_reserved_cus", 32},                // concurrent mode: CUs (4 per XCD) the persistent raytracer grids leave to the NeRF stream
         {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
@@ -1216,6 +1219,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         sched_reduce(c, &ctrl->sched_alive[q], 1, &ctrl->n_owned[q]);
     };
     uint32_t* const sched_src = gsched ? &ctrl->sched_alive[0] : &ctrl->n_alive[0];   // counts the host loop reads
+    // where network launch k records the sample count it read (timed frames; the per-launch roofline)
+    auto net_rec = [&](uint32_t k) -> uint32_t* { return P.collect_kernel_times && k < 16 ? &ctrl->net_launch_samples[k] : nullptr; };
     RayBuf rb[2];
     for (int b = 0; b < 2; ++b)
         rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>(),
@@ -1332,8 +1337,12 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             c->spec_t.ensure(c->sample_cap * 4);
             MsrArgs ma{};
             ma.vol = vol; ma.cam = cam; ma.sched = a.sched; ma.ctrl = ctrl; ma.target = target;
-            ma.budget = (uint32_t)std::min<double>((double)c->sample_cap, std::max(1.0, c->p("nerf_msr_budget")));
             ma.kmax = (uint32_t)std::min<double>(MSR_KMAX, std::max(1.0, c->p("nerf_msr_kmax")));
+            // from the parameters and the frame size alone (ensure_samples' bound, so <= sample_cap), never from
+            // sample_cap itself, which depends on the context's resize history: under the frame-wide schedule
+            // every rank must choose the same round length K (msr_shape), or the ranks make different reductions
+            ma.budget = (uint32_t)std::min<double>(std::max(1.0, c->p("nerf_msr_budget")),
+                                                   (double)(MAX_STEPS_BETWEEN_COMPACTION - 1) * ma.kmax * (double)c->ray_cap);
             // rounds across step changes: fewer rounds (their fixed cost matters most on a thin band) for more
             // samples past the rays' ends; by default under the frame-wide schedule of a banded frame only
             const double span = c->p("nerf_msr_span");
@@ -1352,7 +1361,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 }
                 launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf,
                                P.collect_kernel_times ? c->net_events[2 * net_launches] : nullptr,
-                               P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr);
+                               P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr, net_rec(net_launches));
                 launch_msr_count(ma, mblocks, c->s_nerf);
                 if (gsched) sched_reduce(c, ma.hist + MSR_KMAX, MSR_KMAX);   // own-row deaths summed over the ranks
                 launch_msr_schedule(ma, c->s_nerf);
@@ -1408,8 +1417,9 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 }
                 SpecArgs sa{};
                 sa.vol = vol; sa.cam = cam; sa.mode = mode; sa.ctrl = ctrl;
-                sa.budget = (uint32_t)std::min<double>((double)c->sample_cap, std::max(1.0, c->p("nerf_spec_budget")));
                 sa.kmax = (uint32_t)std::min<double>(SPEC_KMAX, std::max(1.0, c->p("nerf_spec_kmax")));
+                sa.budget = (uint32_t)std::min<double>(std::max(1.0, c->p("nerf_spec_budget")),
+                                                       (double)MAX_STEPS_BETWEEN_COMPACTION * sa.kmax * (double)c->ray_cap);   // as ma.budget
                 sa.coords = c->coords.as<float>(); sa.samp = c->samp.as<uint2>(); sa.tbuf = c->spec_t.as<float>();
                 sa.net_out = c->net_out.as<uint2>();
                 sa.frame_rgba = c->nerf_rgba.as<float4>(); sa.frame_depth = c->nerf_depth.as<float>(); sa.positions = c->nerf_pos.as<float>();
@@ -1439,8 +1449,10 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                     }
                     launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf,
                                    P.collect_kernel_times ? c->net_events[2 * net_launches] : nullptr,
-                                   P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr);
+                                   P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr, net_rec(net_launches));
                     ++net_launches;
+                    // render_frame gates the raytracer's path kernel on the head's network launch (the first round's)
+                    if (r == 0) HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));
                     if (pre) launch_spec_prepare(sa, (uint32_t)c->n_cus * 4, c->s_nerf);
                     launch_spec_composite(sa, sblocks, c->s_nerf);
                     p ^= 1;
@@ -1581,6 +1593,11 @@ void network_times(sng_ctx* c, const sng_frame_params& P, uint32_t net_launches,
         tot += ms;
     }
     out->ms_network = tot;
+    out->n_launch_rec = std::min<uint32_t>(net_launches, 16u);
+    for (uint32_t k = 0; k < out->n_launch_rec; ++k) {
+        HIPCHK(hipEventElapsedTime(&out->ms_network_launch[k], c->net_events[2 * k], c->net_events[2 * k + 1]));
+        out->samples_network_launch[k] = c->h_ctrl->net_launch_samples[k];
+    }
     if (c->fused_last) HIPCHK(hipEventElapsedTime(&out->ms_fused_tail, c->ev_fused0, c->ev_fused1));
     if (c->os_ran) HIPCHK(hipEventElapsedTime(&out->ms_onestep, c->ev_os0, c->ev_os1));
 }
@@ -3055,6 +3072,8 @@ int sng_set_sched_replay(sng_ctx* c, const uint32_t* records, uint64_t n_words) 
         if (!records || !sc.replay) c->sched_hint_key = 0;
         if (sc.replay) { (void)hipHostFree(sc.replay); sc.replay = nullptr; sc.replay_words = 0; }
         if (!records) return;
+        // an empty replay would make every later frame fail with "diverged": detach with records = NULL instead
+        if (n_words == 0) throw SngError(SNG_ERR_INVALID, "empty replay records (detach with records = NULL)");
         if (sc.comm || sc.host_fn) throw SngError(SNG_ERR_STATE, "an RCCL communicator or host reducer is attached");
         for (uint64_t at = 0; at < n_words; at += 1 + (uint64_t)records[at])
             if (records[at] == 0 || at + 1 + records[at] > n_words) throw SngError(SNG_ERR_INVALID, "malformed replay records");

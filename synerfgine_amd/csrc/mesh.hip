@@ -817,8 +817,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
         // object tiles start first instead of being the latency tail of the launch
         const uint32_t tile = a.tile_order ? a.tile_order[k] : k;
         // the costliest tiles of the last frame (the first prio_tiles of the order) issue ahead of the other waves
-        // of their SIMD: the launch lasts as long as its slowest tile's chain, and the others have slack
-        if (a.prio_tiles) {
+        // of their SIMD: the launch lasts as long as its slowest tile's chain, and the others have slack.  prio_tiles
+        // and prio2_tiles are both cumulative bounds of the order (level 3 below the first, level 2 below the second)
+        if (a.prio_tiles || a.prio2_tiles) {
             const uint32_t ks = __builtin_amdgcn_readfirstlane(k);
             if (ks < a.prio_tiles) __builtin_amdgcn_s_setprio(3);
             else if (ks < a.prio2_tiles) __builtin_amdgcn_s_setprio(2);

@@ -33,8 +33,9 @@ template <int F, int OUT_LAYOUT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NET_WAVES_PER_EU))) void nerf_network_kernel(const float* __restrict__ coords, uint32_t stride, uint32_t n_static,
                                                            const uint32_t* __restrict__ n_dev, const h8* __restrict__ wfrag,
                                                            const _Float16* __restrict__ grid, const LevelInfo* __restrict__ levels,
-                                                           uint16_t* __restrict__ out, uint32_t out_rows_stride) {
+                                                           uint16_t* __restrict__ out, uint32_t out_rows_stride, uint32_t* __restrict__ n_rec) {
     const uint32_t n = n_dev ? *n_dev : n_static;
+    if (n_rec && blockIdx.x == 0 && threadIdx.x == 0) *n_rec = n;   // the launch's sample count (per-launch roofline)
     const uint32_t n_tiles = (n + 15) >> 4;
     const int lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -120,7 +121,7 @@ void launch_sh_encode(const float* coords, uint32_t stride, uint32_t dir_offset,
 }
 
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
-                   uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
+                   uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1, uint32_t* n_rec) {
     uint32_t tiles = n_dev ? max_tiles_hint : (n_static + 15) / 16;
     if (tiles == 0) return 0;
     // persistent-style grid: one occupancy's worth of waves (7/SIMD), never more than the tiles
@@ -132,9 +133,9 @@ int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, 
     const _Float16* gr = reinterpret_cast<const _Float16*>(net.grid);
     auto go = [&](auto kernel) {
         if (ev0 || ev1)
-            hipExtLaunchKernelGGL(kernel, dim3(blocks), dim3(256), 0, stream, ev0, ev1, 0u, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static);
+            hipExtLaunchKernelGGL(kernel, dim3(blocks), dim3(256), 0, stream, ev0, ev1, 0u, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static, n_rec);
         else
-            hipLaunchKernelGGL(kernel, dim3(blocks), dim3(256), 0, stream, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static);
+            hipLaunchKernelGGL(kernel, dim3(blocks), dim3(256), 0, stream, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static, n_rec);
     };
     if (net.F == 4) {
         if (layout == 1) go(nerf_network_kernel<4, 1>);

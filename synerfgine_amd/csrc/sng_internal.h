@@ -71,6 +71,8 @@ struct MarchCtrl {
     uint8_t* sched_hint;             // [TAIL_LIVE_CAP] steps of every iteration of the last frame (0: unknown), written by the
                                      //   wavefront, one-step and msr schedules; sizes the msr rounds (exact for any value)
     uint32_t* log;                   // diagnostics (param march_log): [MARCH_LOG_CAP][3] {alive, steps, samples} per iteration
+    uint32_t net_launch_samples[16]; // sample count each whole-GPU network launch of the frame read (collect_kernel_times;
+                                     //   indexed like the host's launch events: the per-launch roofline)
 };
 constexpr uint32_t MARCH_LOG_CAP = 2048;
 constexpr uint32_t TAIL_LIVE_CAP = 10240;   // > MARCH_ITER: iterations a frame can have
@@ -216,7 +218,7 @@ void launch_sh_encode(const float* coords, uint32_t stride, uint32_t dir_offset,
 // the measured interval is the kernel's execution, as rocprofv3 reports it
 int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, uint32_t n_static, const uint32_t* n_dev,
                    uint16_t* out, int layout, uint32_t max_tiles_hint, hipStream_t stream, hipEvent_t ev0 = nullptr,
-                   hipEvent_t ev1 = nullptr);
+                   hipEvent_t ev1 = nullptr, uint32_t* n_rec = nullptr);
 // Normals (mode 2) input gradient / EncodingVis (mode 10) activation, rewriting the samples' coordinates in place
 void launch_field_probe(const NetworkDev& net, const uint16_t* mlp_params, float* coords, const uint32_t* n_dev, int mode, int layer, int dim,
                         hipStream_t stream);

@@ -190,6 +190,107 @@ struct aabb { f3 lo, hi; };
 constexpr float INV_MIN_STEP = 1.0f / MIN_STEP;   // RN(1/MIN_STEP), folded at compile time
 
 struct f2 { float x, y; };
+
+// ---- lens models: ELensMode / Lens (common.h:188-205), distortion deltas and the Newton undistortion
+// (common_device.cuh:250-338), uv_to_ray's direction per mode (403-447), pos_to_uv's forward distortion (507-541).
+// tcnn's mat2 inverse (vec.h, unvendored) is restated as 1/det times the adjugate.
+enum : int32_t { LENS_PERSPECTIVE = 0, LENS_OPENCV = 1, LENS_FTHETA = 2, LENS_LATLONG = 3, LENS_OPENCV_FISHEYE = 4, LENS_EQUIRECTANGULAR = 5 };
+struct Lens { int32_t mode; float params[7]; };
+
+// opencv_lens_distortion_delta (common_device.cuh:250-266): params k1 k2 p1 p2
+SNG_HD void opencv_delta(const float* p, float u, float v, float& du, float& dv) {
+    const float k1 = p[0], k2 = p[1], p1 = p[2], p2 = p[3];
+    const float u2 = u * u, uv = u * v, v2 = v * v;
+    const float r2 = u2 + v2;
+    const float radial = k1 * r2 + k2 * r2 * r2;
+    du = u * radial + 2.0f * p1 * uv + p2 * (r2 + 2.0f * u2);
+    dv = v * radial + 2.0f * p2 * uv + p1 * (r2 + 2.0f * v2);
+}
+// opencv_fisheye_lens_distortion_delta (268-292): params k1 k2 k3 k4; the threshold is double's epsilon as a float
+SNG_HD void fisheye_delta(const float* p, float u, float v, float& du, float& dv) {
+    const float r = sqrtf(u * u + v * v);
+    if (r > 2.220446049250313e-16f) {
+        const float theta = atanf(r);
+        const float t2 = theta * theta, t4 = t2 * t2, t6 = t4 * t2, t8 = t4 * t4;
+        const float thetad = theta * (1.0f + p[0] * t2 + p[1] * t4 + p[2] * t6 + p[3] * t8);
+        du = u * thetad / r - u;
+        dv = v * thetad / r - v;
+    } else {
+        du = 0.0f;
+        dv = 0.0f;
+    }
+}
+SNG_HD void lens_delta(int32_t mode, const float* p, float u, float v, float& du, float& dv) {
+    if (mode == LENS_OPENCV_FISHEYE) fisheye_delta(p, u, v, du, dv);
+    else opencv_delta(p, u, v, du, dv);
+}
+// iterative_lens_undistortion (294-330): Newton on x + delta(x) = x0 with central-difference Jacobians, at most 100
+// iterations, stop once |step|^2 < 1e-10
+SNG_HD void lens_undistort(int32_t mode, const float* p, float& u, float& v) {
+    const float x0u = u, x0v = v;
+    float xu = u, xv = v;
+#pragma unroll 1
+    for (uint32_t i = 0; i < 100; ++i) {
+        const float s0 = fmaxf(1.1920929e-07f, fabsf(1e-6f * xu));   // max(FLT_EPSILON, |kRelStepSize x|)
+        const float s1 = fmaxf(1.1920929e-07f, fabsf(1e-6f * xv));
+        float du, dv, u0b, v0b, u0f, v0f, u1b, v1b, u1f, v1f;
+        lens_delta(mode, p, xu, xv, du, dv);
+        lens_delta(mode, p, xu - s0, xv, u0b, v0b);
+        lens_delta(mode, p, xu + s0, xv, u0f, v0f);
+        lens_delta(mode, p, xu, xv - s1, u1b, v1b);
+        lens_delta(mode, p, xu, xv + s1, u1f, v1f);
+        // J column-major: J[0][0] J[0][1] first column, J[1][0] J[1][1] second
+        const float j00 = 1.0f + (u0f - u0b) / (2.0f * s0);
+        const float j10 = (u1f - u1b) / (2.0f * s1);
+        const float j01 = (v0f - v0b) / (2.0f * s0);
+        const float j11 = 1.0f + (v1f - v1b) / (2.0f * s1);
+        const float d = 1.0f / (j00 * j11 - j10 * j01);
+        const float i00 = d * j11, i01 = -d * j01, i10 = -d * j10, i11 = d * j00;   // inverse(J), column-major
+        const float ru = xu + du - x0u, rv = xv + dv - x0v;
+        const float su = i00 * ru + i10 * rv, sv = i01 * ru + i11 * rv;
+        xu -= su;
+        xv -= sv;
+        if (su * su + sv * sv < 1e-10f) break;
+    }
+    u = xu;
+    v = xv;
+}
+// uv_to_ray's camera-space direction (common_device.cuh:425-447) for a non-foveated, unmasked view: false when the
+// ray is invalid (F-Theta outside its domain)
+SNG_HD bool lens_dir(const Lens& L, f2 uv, f2 sc, int W, int H, f2 focal, f3& dir) {
+    if (L.mode == LENS_FTHETA) {   // f_theta_undistortion (370-384), error direction 0
+        const float xpix = (uv.x - sc.x) * L.params[5], ypix = (uv.y - sc.y) * L.params[6];
+        const float norm = sqrtf(xpix * xpix + ypix * ypix);
+        const float alpha = L.params[0] + norm * (L.params[1] + norm * (L.params[2] + norm * (L.params[3] + norm * L.params[4])));
+        float sa, ca;
+        sincosf(alpha, &sa, &ca);
+        if (ca <= 1.17549435e-38f || norm == 0.0f) { dir = splat(0.0f); return false; }
+        sa *= 1.0f / norm;
+        dir = mk(sa * xpix, sa * ypix, ca);
+        return true;
+    }
+    if (L.mode == LENS_LATLONG) {   // latlong_to_dir (386-393)
+        const float theta = (uv.y - 0.5f) * PI_F, phi = (uv.x - 0.5f) * PI_F * 2.0f;
+        float sp, cp, st, ct;
+        sincosf(theta, &st, &ct);
+        sincosf(phi, &sp, &cp);
+        dir = mk(sp * ct, st, cp * ct);
+        return true;
+    }
+    if (L.mode == LENS_EQUIRECTANGULAR) {   // equirectangular_to_dir (395-401)
+        const float ct = (uv.y - 0.5f) * 2.0f;
+        const float st = sqrtf(fmaxf(1.0f - ct * ct, 0.0f));
+        const float phi = (uv.x - 0.5f) * PI_F * 2.0f;
+        float sp, cp;
+        sincosf(phi, &sp, &cp);
+        dir = mk(sp * st, ct, cp * st);
+        return true;
+    }
+    dir = mk((uv.x - sc.x) * (float)W / focal.x, (uv.y - sc.y) * (float)H / focal.y, 1.0f);
+    if (L.mode == LENS_OPENCV || L.mode == LENS_OPENCV_FISHEYE) lens_undistort(L.mode, L.params, dir.x, dir.y);
+    return true;
+}
+
 SNG_HD void fswap(float& a, float& b) { float t = a; a = b; b = t; }
 SNG_HD float aabb_entry(const aabb& b, f3 pos, f3 dir) {
     const float FMAX = 3.402823466e+38f;

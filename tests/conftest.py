@@ -10,6 +10,21 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libsng_hip.so)")
+    config.addinivalue_line("markers", "oracle_mode(mode): the oracle formulas a test compares against: 'literal' (the "
+                                       "reference's text as written) or 'product' (the product's fast-math restatements)")
+
+
+@pytest.fixture(autouse=True)
+def _oracle_mode(request):
+    """Every test starts with the oracle mode it states (pytest.mark.oracle_mode, module- or test-level), 'literal'
+    when it states none, so no test inherits another's mode (orc_set_literal, oracle/sng_oracle.h)."""
+    m = request.node.get_closest_marker("oracle_mode")
+    mode = m.args[0] if m else "literal"
+    assert mode in ("literal", "product"), mode
+    if m is not None or "oracle" in sys.modules:
+        import oracle as O
+        O.lib().orc_set_literal(1 if mode == "literal" else 0)
+    yield
 
 
 @pytest.fixture(scope="session")

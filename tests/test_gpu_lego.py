@@ -17,7 +17,7 @@ import os
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.oracle_mode("literal")]   # the oracle compares the reference's text as written
 
 torch = pytest.importorskip("torch")
 

@@ -10,6 +10,8 @@
 #   profdriver             rocprofv3 over bench.py --no-cpu-baseline + tools/roofline_check.py (same-process roofline check)
 #   pmc[:CFG[:ARGS]]       FETCH_SIZE / WRITE_SIZE / MFMA PMC passes (one rocprofv3 run each) + tools/pmc_summary.py
 #   sq[:CFG[:ARGS]]        SQ_INSTS_* + SQ_WAVE_CYCLES pass with kernel trace + tools/sq_summary.py (VALU roofline)
+#   ab:CFG:PAIRS:A/B       PAIRS alternating bench.py runs of two settings (A, B: KEY=V[,KEY=V...], '-' for the defaults),
+#                          then tools/bsum.py over the logs (replaces round 4's one-off ab_r04*.sh scripts)
 #   py:SCRIPT[:ARGS]       python3 tools/SCRIPT ARGS
 #   profpy:SCRIPT[:ARGS]   rocprofv3 --kernel-trace --stats of python3 tools/SCRIPT ARGS (+ kernel table)
 #   pmcpy:SCRIPT[:ARGS]    FETCH_SIZE / WRITE_SIZE / MFMA passes over python3 tools/SCRIPT ARGS + tools/pmc_summary.py
@@ -82,6 +84,19 @@ for step in "$@"; do
         -d $d -o run --output-format csv -- python3 bench.py --config ${cfg:-c3} --steps 3 --warmup 2 --no-cpu-baseline --no-sweep $args > $log 2>&1
       rc=$?
       [ $rc -eq 0 ] && python3 tools/sq_summary.py $d $OUT/${kind}_${cfg:-c3}.json ${cfg:-c3} 2>&1 | tee -a $log; rc=${PIPESTATUS[0]} ;;
+    ab)
+      IFS=: read -r cfg pairs spec <<< "$rest"
+      rc=0
+      for i in $(seq 1 ${pairs:-4}); do
+        for side in A B; do
+          [ $side = A ] && sets=${spec%%/*} || sets=${spec#*/}
+          sa=()
+          if [ "$sets" != "-" ]; then IFS=, read -ra kv <<< "$sets"; for x in "${kv[@]}"; do sa+=(--set "$x"); done; fi
+          timeout -k 10 600 python3 -u bench.py --config ${cfg:-c3} --no-cpu-baseline --no-sweep "${sa[@]}" > $OUT/ab$n.$side.$i.log 2>&1
+          rc=$?; [ $rc -ne 0 ] && break 2
+        done
+      done
+      [ $rc -eq 0 ] && python3 tools/bsum.py $OUT/ab$n.*.log | tee $log ;;
     py)
       timeout -k 10 600 python3 -u tools/$cfg $args > $log 2>&1
       rc=$?; tail -c 3000 $log; echo ;;
