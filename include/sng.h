@@ -258,6 +258,22 @@ typedef struct {
 int sng_image_load_png(const char* path, uint8_t* out_rgba8, uint64_t capacity, int32_t* width, int32_t* height);
 int sng_train_set_dataset(sng_ctx* ctx, uint32_t n_images, uint32_t width, uint32_t height, const uint8_t* rgba8, const float* xforms_4x3,
                           const float* focal_px, const float* principal_uv);
+/* Lens (common.h:188-205): mode 0 Perspective, 1 OpenCV {k1 k2 p1 p2}, 2 F-Theta {p0..p4, w, h}, 3 LatLong,
+ * 4 OpenCV fisheye {k1 k2 k3 k4}, 5 Equirectangular -- what read_lens (nerf_loader.cu:175-239) takes from a
+ * transforms.json / frame, and TrainingImageMetadata::lens */
+typedef struct { int32_t mode; float params[7]; } sng_lens;
+/* the training images' lenses, one per image of sng_train_set_dataset (NULL / 0: all Perspective, also the state
+ * after sng_train_set_dataset); generate_training_samples_nerf's uv_to_ray(..., lens) (testbed_nerf.cu:890-905) and
+ * mark_untrained_density_grid's pos_to_uv / uv_to_ray round trip (testbed_nerf.cu:112-141) use them */
+int sng_train_set_lens(sng_ctx* ctx, const sng_lens* lenses, uint32_t n);
+/* Testbed::Nerf::render_lens: the NeRF camera rays go through it when param render_with_lens_distortion is set
+ * (render_nerf_with_buffers, testbed_nerf.cu:2504; uv_to_ray 403-447).  sng_load_snapshot sets it to the
+ * dataset's first lens (load_nerf_post, testbed_nerf.cu:3051-3052).  NULL: Perspective. */
+int sng_set_render_lens(sng_ctx* ctx, const sng_lens* lens);
+int sng_get_render_lens(sng_ctx* ctx, sng_lens* out);
+/* Testbed::set_camera_to_training_view (testbed.cu:453-469): camera, relative focal length, screen centre
+ * (1 - principal point) and render lens of training image `view`, render_with_lens_distortion on */
+int sng_set_camera_to_training_view(sng_ctx* ctx, int32_t view);
 /* Testbed::reset_network's training state: fp32 master weights from the current model, zero
  * moments, m_rng = pcg32(seed), density_grid_rng = pcg32(m_rng.next_uint()) (testbed.cu:3654-3667) */
 int sng_train_reset(sng_ctx* ctx, uint64_t seed);

@@ -121,6 +121,8 @@ def lib():
             "orc_set_visualization": (None, [i32, i32]),
             "orc_set_motion_blur": (None, [vp, vp]), "orc_set_glow": (None, [i32, f32]), "orc_set_shadow_rng_mode": (None, [i32]), "orc_set_literal": (None, [i32]),
             "orc_set_gbuffer_out": (None, [vp, vp]),
+            "orc_set_render_lens": (None, [vp]), "orc_set_train_lens": (None, [vp, u32]),
+            "orc_uv_to_ray_dir": (i32, [vp, vp, i32, i32, vp, vp, vp]), "orc_lens_distortion_delta": (None, [vp, f32, f32, vp, vp]),
             "orc_train_generate": (None, [vp, vp, u64, u64, u32, u32, vp, vp, vp]),
             "orc_display": (None, [vp, i32, i32, i32, i32, vp, vp]),
             "orc_camera_set_view": (None, [vp, vp, vp, vp, vp, f32]),
@@ -372,9 +374,52 @@ def render_frame(model, vol, tb, eng, nerf_rng, mesh_rng, spp=0, target=0, gbuff
 
 
 # ---- online training (config 5) ----------------------------------------------------
+class orc_lens(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("params", ctypes.c_float * 7)]
+
+
+def _lens_array(lenses):
+    """[(mode, params...), ...] -> ctypes array of orc_lens (params padded to 7)"""
+    arr = (orc_lens * max(1, len(lenses)))()
+    for i, (mode, params) in enumerate(lenses):
+        arr[i].mode = int(mode)
+        for k, v in enumerate(list(params)[:7]):
+            arr[i].params[k] = float(v)
+    return arr
+
+
+def set_render_lens(mode=0, params=()):
+    """the NeRF camera rays' lens (Testbed::Nerf::render_lens with render_with_lens_distortion); mode 0 = Perspective"""
+    lib().orc_set_render_lens(ctypes.byref(_lens_array([(mode, params)])[0]) if mode else None)
+
+
+def uv_to_ray_dir(lens, uv, res, focal, screen_center):
+    """uv_to_ray's camera-space direction (valid, dir[3]) for lens = (mode, params)"""
+    arr = _lens_array([lens])
+    u = np.asarray(uv, np.float32)
+    f = np.asarray(focal, np.float32)
+    sc = np.asarray(screen_center, np.float32)
+    d = np.zeros(3, np.float32)
+    ok = lib().orc_uv_to_ray_dir(ctypes.byref(arr[0]), u.ctypes.data, int(res[0]), int(res[1]), f.ctypes.data, sc.ctypes.data, d.ctypes.data)
+    return bool(ok), d
+
+
+def lens_distortion_delta(lens, u, v):
+    arr = _lens_array([lens])
+    du, dv = ctypes.c_float(), ctypes.c_float()
+    lib().orc_lens_distortion_delta(ctypes.byref(arr[0]), float(u), float(v), ctypes.byref(du), ctypes.byref(dv))
+    return du.value, dv.value
+
+
+def set_train_lens(lenses):
+    """one (mode, params) per training image for train_generate; [] = all Perspective"""
+    arr = _lens_array(lenses)
+    lib().orc_set_train_lens(arr, len(lenses))
+
+
 def train_generate(vol, images, xforms, focal, pp, rng_state, rng_inc, n_rays, max_per_ray=1024):
     """generate_training_samples_nerf for rays [0, n_rays): (numsteps [n], rays [n][6], coords [n][max_per_ray][7]).
-    images [n, h, w, 4] uint8; xforms [n, 3, 4] NGP camera (columns c0..c3)."""
+    images [n, h, w, 4] uint8; xforms [n, 3, 4] NGP camera (columns c0..c3); the lenses of set_train_lens."""
     im = np.ascontiguousarray(images, np.uint8)
     xf = np.ascontiguousarray(np.asarray(xforms, np.float32).reshape(-1, 3, 4).transpose(0, 2, 1).reshape(-1, 12))
     fo = np.ascontiguousarray(focal, np.float32)

@@ -1004,6 +1004,111 @@ M3 shutter_rotation(Quat a, Quat b, float t) {
 /* View::camera1 / rolling_shutter (testbed.h:1032,1042): orc_set_motion_blur */
 static bool g_has_cam1 = false;
 static float g_cam1[12], g_rs[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+/* Lens (common.h:188-205): the render lens (Testbed::Nerf::render_lens with render_with_lens_distortion,
+ * testbed_nerf.cu:2504; orc_set_render_lens) and the training images' lenses (orc_set_train_lens) */
+struct OrcLens { int32_t mode = 0; float params[7] = {}; };
+static OrcLens g_render_lens;
+static std::vector<OrcLens> g_train_lens;
+
+/* opencv_lens_distortion_delta (common_device.cuh:250-266) */
+static void opencv_lens_distortion_delta(const float* extra_params, float u, float v, float* du, float* dv) {
+    const float k1 = extra_params[0];
+    const float k2 = extra_params[1];
+    const float p1 = extra_params[2];
+    const float p2 = extra_params[3];
+    const float u2 = u * u;
+    const float uv = u * v;
+    const float v2 = v * v;
+    const float r2 = u2 + v2;
+    const float radial = k1 * r2 + k2 * r2 * r2;
+    *du = u * radial + 2.0f * p1 * uv + p2 * (r2 + 2.0f * u2);
+    *dv = v * radial + 2.0f * p2 * uv + p1 * (r2 + 2.0f * v2);
+}
+/* opencv_fisheye_lens_distortion_delta (common_device.cuh:268-292) */
+static void opencv_fisheye_lens_distortion_delta(const float* extra_params, float u, float v, float* du, float* dv) {
+    const float k1 = extra_params[0], k2 = extra_params[1], k3 = extra_params[2], k4 = extra_params[3];
+    const float r = std::sqrt(u * u + v * v);
+    if (r > (float)std::numeric_limits<double>::epsilon()) {
+        const float theta = std::atan(r);
+        const float theta2 = theta * theta;
+        const float theta4 = theta2 * theta2;
+        const float theta6 = theta4 * theta2;
+        const float theta8 = theta4 * theta4;
+        const float thetad = theta * (1.0f + k1 * theta2 + k2 * theta4 + k3 * theta6 + k4 * theta8);
+        *du = u * thetad / r - u;
+        *dv = v * thetad / r - v;
+    } else {
+        *du = 0.0f;
+        *dv = 0.0f;
+    }
+}
+/* iterative_lens_undistortion (common_device.cuh:294-330); mat2 J column-major, tcnn inverse(mat2) as 1/det x adjugate */
+template <typename F>
+static void iterative_lens_undistortion(const float* params, float* u, float* v, F distortion_fun) {
+    const uint32_t kNumIterations = 100;
+    const float kMaxStepNorm = 1e-10f;
+    const float kRelStepSize = 1e-6f;
+    float J[2][2];
+    const V2 x0 = {*u, *v};
+    V2 x = {*u, *v};
+    V2 dx, dx_0b, dx_0f, dx_1b, dx_1f;
+    for (uint32_t i = 0; i < kNumIterations; ++i) {
+        const float step0 = std::max(std::numeric_limits<float>::epsilon(), std::abs(kRelStepSize * x.x));
+        const float step1 = std::max(std::numeric_limits<float>::epsilon(), std::abs(kRelStepSize * x.y));
+        distortion_fun(params, x.x, x.y, &dx.x, &dx.y);
+        distortion_fun(params, x.x - step0, x.y, &dx_0b.x, &dx_0b.y);
+        distortion_fun(params, x.x + step0, x.y, &dx_0f.x, &dx_0f.y);
+        distortion_fun(params, x.x, x.y - step1, &dx_1b.x, &dx_1b.y);
+        distortion_fun(params, x.x, x.y + step1, &dx_1f.x, &dx_1f.y);
+        J[0][0] = 1 + (dx_0f.x - dx_0b.x) / (2 * step0);
+        J[1][0] = (dx_1f.x - dx_1b.x) / (2 * step1);
+        J[0][1] = (dx_0f.y - dx_0b.y) / (2 * step0);
+        J[1][1] = 1 + (dx_1f.y - dx_1b.y) / (2 * step1);
+        const float d = 1.0f / (J[0][0] * J[1][1] - J[1][0] * J[0][1]);
+        const float inv[2][2] = {{d * J[1][1], -d * J[0][1]}, {-d * J[1][0], d * J[0][0]}};
+        const V2 r = {x.x + dx.x - x0.x, x.y + dx.y - x0.y};
+        const V2 step_x = {inv[0][0] * r.x + inv[1][0] * r.y, inv[0][1] * r.x + inv[1][1] * r.y};
+        x.x -= step_x.x;
+        x.y -= step_x.y;
+        if (step_x.x * step_x.x + step_x.y * step_x.y < kMaxStepNorm) break;
+    }
+    *u = x.x;
+    *v = x.y;
+}
+/* uv_to_ray's direction (common_device.cuh:403-447; identity foveation, no mask / distortion map); false = Ray::invalid() */
+static bool uv_to_ray_dir(const OrcLens& lens, V2 uv, int W, int H, V2 focal, V2 screen_center, V3* dir) {
+    const float PI_ = 3.14159265358979323846f;
+    if (lens.mode == 2) {   /* f_theta_undistortion (370-384) */
+        const V2 d = {uv.x - screen_center.x, uv.y - screen_center.y};
+        const float xpix = d.x * lens.params[5];
+        const float ypix = d.y * lens.params[6];
+        const float norm = std::sqrt(xpix * xpix + ypix * ypix);
+        const float alpha = lens.params[0] + norm * (lens.params[1] + norm * (lens.params[2] + norm * (lens.params[3] + norm * lens.params[4])));
+        float sin_alpha = std::sin(alpha), cos_alpha = std::cos(alpha);
+        if (cos_alpha <= std::numeric_limits<float>::min() || norm == 0.f) return false;
+        sin_alpha *= 1.f / norm;
+        *dir = v3(sin_alpha * xpix, sin_alpha * ypix, cos_alpha);
+        return true;
+    } else if (lens.mode == 3) {   /* latlong_to_dir (386-393) */
+        const float theta = (uv.y - 0.5f) * PI_;
+        const float phi = (uv.x - 0.5f) * PI_ * 2.0f;
+        const float st = std::sin(theta), ct = std::cos(theta), sp = std::sin(phi), cp = std::cos(phi);
+        *dir = v3(sp * ct, st, cp * ct);
+        return true;
+    } else if (lens.mode == 5) {   /* equirectangular_to_dir (395-401) */
+        const float ct = (uv.y - 0.5f) * 2.0f;
+        const float st = std::sqrt(std::max(1.0f - ct * ct, 0.0f));
+        const float phi = (uv.x - 0.5f) * PI_ * 2.0f;
+        const float sp = std::sin(phi), cp = std::cos(phi);
+        *dir = v3(sp * st, ct, cp * st);
+        return true;
+    }
+    *dir = v3((uv.x - screen_center.x) * (float)W / focal.x, (uv.y - screen_center.y) * (float)H / focal.y, 1.0f);
+    if (lens.mode == 1) iterative_lens_undistortion(lens.params, &dir->x, &dir->y, opencv_lens_distortion_delta);
+    else if (lens.mode == 4) iterative_lens_undistortion(lens.params, &dir->x, &dir->y, opencv_fisheye_lens_distortion_delta);
+    return true;
+}
+
 /* Testbed::Nerf::glow_mode / glow_y_cutoff (testbed.h:870-871): orc_set_glow */
 static int g_glow_mode = 0;
 static float g_glow_y_cutoff = 0.0f;
@@ -1184,11 +1289,14 @@ static void render_nerf_impl(const orc_model* m, const orc_volume* vdesc, const 
         p.max_weight = 0.0f;
         frame_depth[idx] = MAX_DEPTH;
         V2 uv = {((float)x + pixel_offset.x) / (float)W, ((float)y + pixel_offset.y) / (float)H};
-        /* uv_to_ray (common_device.cuh:403-470) with identity foveation, no lens, no parallax, aperture 0, near 0 */
-        V3 dir = v3((uv.x - sc.x) * (float)W / focal.x, (uv.y - sc.y) * (float)H / focal.y, 1.0f);
+        /* uv_to_ray (common_device.cuh:403-470) with identity foveation, the render lens, no parallax, aperture 0, near 0 */
+        V3 dir;
+        const bool valid = uv_to_ray_dir(g_render_lens, uv, W, H, focal, sc, &dir);
         const float pixel_t = g_rs[0] + g_rs[1] * uv.x + g_rs[2] * uv.y + g_rs[3] * ld_random_val(c->spp, (uint32_t)idx * 72239731u);
         dir = mul(shutter_rotation(q0, q1, pixel_t), dir);
         V3 origin = cam_pos + (pos1 - cam_pos) * pixel_t;
+        p.origin = origin;
+        if (!valid) { p.alive = false; p.dir = normalize(dir); p.idx = (uint32_t)idx; continue; }   /* !ray.is_valid() (1919-1923) */
         frame_rgba[4 * idx + 0] = 0.0f; frame_rgba[4 * idx + 1] = 0.0f; frame_rgba[4 * idx + 2] = 0.0f; /* rgb only */
         dir = normalize(dir);
         float t = std::fmax(bb_ray_intersect(vol.render_aabb, to_local(vol, origin), to_local(vol, dir)).x, 0.0f) + 1e-6f;
@@ -1800,6 +1908,26 @@ void orc_set_motion_blur(const float* camera1, const float* rolling_shutter) {
     std::memcpy(g_rs, rolling_shutter ? rolling_shutter : rs0, sizeof(g_rs));
 }
 void orc_set_shadow_rng_mode(int32_t neighbour) { g_shadow_rng_neighbour = neighbour; }
+void orc_set_render_lens(const orc_lens* lens) {
+    g_render_lens = OrcLens{};
+    if (lens) { g_render_lens.mode = lens->mode; std::memcpy(g_render_lens.params, lens->params, sizeof(g_render_lens.params)); }
+}
+int32_t orc_uv_to_ray_dir(const orc_lens* lens, const float* uv, int32_t W, int32_t H, const float* focal, const float* screen_center, float* dir) {
+    OrcLens l;
+    if (lens) { l.mode = lens->mode; std::memcpy(l.params, lens->params, sizeof(l.params)); }
+    V3 d;
+    const bool ok = uv_to_ray_dir(l, V2{uv[0], uv[1]}, W, H, V2{focal[0], focal[1]}, V2{screen_center[0], screen_center[1]}, &d);
+    dir[0] = d.x; dir[1] = d.y; dir[2] = d.z;
+    return ok ? 1 : 0;
+}
+void orc_lens_distortion_delta(const orc_lens* lens, float u, float v, float* du, float* dv) {
+    if (lens->mode == 4) opencv_fisheye_lens_distortion_delta(lens->params, u, v, du, dv);
+    else opencv_lens_distortion_delta(lens->params, u, v, du, dv);
+}
+void orc_set_train_lens(const orc_lens* lenses, uint32_t n) {
+    g_train_lens.assign(n, OrcLens{});
+    for (uint32_t i = 0; i < n; ++i) { g_train_lens[i].mode = lenses[i].mode; std::memcpy(g_train_lens[i].params, lenses[i].params, sizeof(lenses[i].params)); }
+}
 void orc_set_glow(int32_t mode, float y_cutoff) {
     g_glow_mode = mode;
     g_glow_y_cutoff = y_cutoff;
@@ -1898,14 +2026,17 @@ void orc_train_generate(const orc_volume* vdesc, const orc_train_images* im, uin
         const uint8_t* tex = im->rgba + (((size_t)img * im->h + ty) * im->w + tx) * 4;
         if (tex[0] == 0xFF && tex[1] == 0x00 && tex[2] == 0xFF && tex[3] == 0x00) continue;
         (void)rng.next_float();   /* motionblur_time */
-        /* get_xform_given_rolling_shutter (common_device.cuh:361-368), then uv_to_ray pinhole (403-470) */
+        /* get_xform_given_rolling_shutter (common_device.cuh:361-368), then uv_to_ray with the image's lens (403-470);
+         * an invalid ray is {xform[3], xform[2]} (testbed_nerf.cu:901-903) */
         const float* xf = im->xforms + 12 * (size_t)img;
         const M43 cam = m43_load(xf);
         const M3 rot = rolling_shutter_rotation(m3_of(cam));
         const float* fo = im->focal + 2 * (size_t)img;
         const float* pp = im->pp + 2 * (size_t)img;
-        V3 dir = v3((uv.x - pp[0]) * (float)im->w / fo[0], (uv.y - pp[1]) * (float)im->h / fo[1], 1.0f);
-        dir = mul(rot, dir);
+        const OrcLens lens = img < g_train_lens.size() ? g_train_lens[img] : OrcLens{};
+        V3 dir;
+        if (uv_to_ray_dir(lens, uv, im->w, im->h, V2{fo[0], fo[1]}, V2{pp[0], pp[1]}, &dir)) dir = mul(rot, dir);
+        else dir = rot.c[2];
         const V3 o = cam.c[3];
         const V3 dn = normalize(dir);
         V2 tminmax = bb_ray_intersect(aabb, o, dn);

@@ -139,6 +139,16 @@ void orc_render_nerf(const orc_model* m, const orc_volume* v, const orc_camera* 
 /* View::camera1 / rolling_shutter (testbed.h:1032,1042) for the NeRF camera rays (testbed_nerf.cu:1895);
  * camera1 NULL: camera0, rolling_shutter NULL: (0, 0, 0, 1) */
 void orc_set_motion_blur(const float* camera1, const float* rolling_shutter);
+/* Lens (common.h:188-205): mode 0 Perspective, 1 OpenCV {k1 k2 p1 p2}, 2 F-Theta {p0..p4, w, h}, 3 LatLong,
+ * 4 OpenCV fisheye {k1..k4}, 5 Equirectangular.  orc_set_render_lens: the NeRF camera rays' lens (NULL:
+ * Perspective); orc_set_train_lens: one per training image for orc_train_generate (n = 0: all Perspective) */
+typedef struct { int32_t mode; float params[7]; } orc_lens;
+void orc_set_render_lens(const orc_lens* lens);
+void orc_set_train_lens(const orc_lens* lenses, uint32_t n);
+/* uv_to_ray's camera-space direction for one uv (common_device.cuh:403-447); returns 0 for Ray::invalid() */
+int32_t orc_uv_to_ray_dir(const orc_lens* lens, const float* uv, int32_t W, int32_t H, const float* focal, const float* screen_center, float* dir);
+/* the forward distortion pos_to_uv applies (common_device.cuh:526-534): OpenCV or OpenCV fisheye delta */
+void orc_lens_distortion_delta(const orc_lens* lens, float u, float v, float* du, float* dv);
 /* Testbed::Nerf::glow_mode / glow_y_cutoff (testbed.h:870-871) for orc_render_nerf_ngp (testbed_nerf.cu:638-734) */
 void orc_set_glow(int32_t mode, float y_cutoff);
 /* shade_nerf_shadows' light-sample RNG for nerf_shadow_samples > 0: 0 = the centre pixel's stream (this

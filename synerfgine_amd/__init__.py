@@ -91,6 +91,37 @@ class Testbed:
         pp = np.ascontiguousarray(np.full((n, 2), 0.5, np.float32) if principal is None else np.asarray(principal, np.float32).reshape(n, 2))
         check(self._lib.sng_train_set_dataset(self.ctx, n, w, h, im.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), _fptr(xf), _fptr(fo), _fptr(pp)))
 
+    def set_training_lens(self, lenses):
+        """One (mode, params) per training image (read_lens, nerf_loader.cu:175-239; mode 0 Perspective, 1 OpenCV
+        {k1 k2 p1 p2}, 2 F-Theta, 3 LatLong, 4 OpenCV fisheye {k1..k4}, 5 Equirectangular); None / [] = all Perspective."""
+        if not lenses:
+            check(self._lib.sng_train_set_lens(self.ctx, None, 0))
+            return
+        arr = (_lib.sng_lens * len(lenses))()
+        for i, (mode, params) in enumerate(lenses):
+            arr[i].mode = int(mode)
+            for k, v in enumerate(list(params)[:7]):
+                arr[i].params[k] = float(v)
+        check(self._lib.sng_train_set_lens(self.ctx, arr, len(lenses)))
+
+    def set_render_lens(self, mode=0, params=()):
+        """Testbed::Nerf::render_lens (used while param render_with_lens_distortion is 1); mode 0 = Perspective."""
+        l = _lib.sng_lens()
+        l.mode = int(mode)
+        for k, v in enumerate(list(params)[:7]):
+            l.params[k] = float(v)
+        check(self._lib.sng_set_render_lens(self.ctx, ctypes.byref(l)))
+
+    def render_lens(self):
+        l = _lib.sng_lens()
+        check(self._lib.sng_get_render_lens(self.ctx, ctypes.byref(l)))
+        return int(l.mode), [float(x) for x in l.params]
+
+    def set_camera_to_training_view(self, view):
+        """Testbed::set_camera_to_training_view (testbed.cu:453-469): the training image's camera, focal length,
+        principal point and lens (render_with_lens_distortion on)."""
+        check(self._lib.sng_set_camera_to_training_view(self.ctx, int(view)))
+
     def train_reset(self, seed=1337):
         check(self._lib.sng_train_reset(self.ctx, int(seed)))
 

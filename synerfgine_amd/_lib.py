@@ -99,6 +99,10 @@ class sng_frame_result(ctypes.Structure):
     ]
 
 
+class sng_lens(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("params", ctypes.c_float * 7)]
+
+
 class sng_light(ctypes.Structure):
     _fields_ = [("pos", ctypes.c_float * 3), ("intensity", ctypes.c_float), ("size", ctypes.c_float), ("type", ctypes.c_int32)]
 
@@ -200,6 +204,10 @@ SIGNATURES = {
                                            ctypes.POINTER(U32)]),
     "sng_image_load_png": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint8), U64, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "sng_train_set_dataset": (ctypes.c_int, [P, U32, U32, U32, ctypes.POINTER(ctypes.c_uint8), FP, FP, FP]),
+    "sng_train_set_lens": (ctypes.c_int, [P, ctypes.POINTER(sng_lens), U32]),
+    "sng_set_render_lens": (ctypes.c_int, [P, ctypes.POINTER(sng_lens)]),
+    "sng_get_render_lens": (ctypes.c_int, [P, ctypes.POINTER(sng_lens)]),
+    "sng_set_camera_to_training_view": (ctypes.c_int, [P, ctypes.c_int32]),
     "sng_train_reset": (ctypes.c_int, [P, U64]),
     "sng_train": (ctypes.c_int, [P, U32, ctypes.POINTER(sng_train_stats)]),
     "sng_train_export": (ctypes.c_int, [P, U16P, U64, U16P, U64]),

@@ -359,6 +359,8 @@ const std::map<std::string, double>& default_params() {
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
+        {"render_with_lens_distortion", 0},     // Testbed::Nerf::render_with_lens_distortion (testbed_nerf.cu:2504): NeRF rays through
+                                                //   render_lens (sng_set_render_lens; the snapshot dataset's first lens)
         {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)
         {"rt_queue_gb", 48},                    // device-memory budget for the deferred-shadow queues
         {"train_batch", 262144},                // m_training_batch_size (testbed.h:1103)
@@ -429,6 +431,9 @@ struct sng_ctx {
     bool has_cam1 = false;
     float cam1[12] = {};
     float rolling_shutter[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    // Testbed::Nerf::render_lens (testbed.h; the dataset's metadata[0].lens at load, testbed_nerf.cu:3051-3053),
+    // applied when param render_with_lens_distortion is set (testbed_nerf.cu:2504)
+    Lens render_lens{};
     float m_scale = 1.5f;
     // NerfDataset::scale / offset as the loaded snapshot held them (json_binding.h:108-132), written
     // back by save_snapshot; nerf_synthetic's values until a snapshot supplies its own
@@ -514,6 +519,8 @@ struct sng_ctx {
         Pcg32 rng{}, grid_rng{};
         int w = 0, h = 0, n_images = 0;
         DevBuf pixels, xforms, xforms_ray, focal, pp;
+        DevBuf lens;                                   // [n_images] Lens (sng_train_set_lens); h_lens empty: all Perspective
+        std::vector<Lens> h_lens;
         DevBuf master, grads, m1, m2, steps, ema, p_train, p_infer, wfrag_train, wfrag_t;
         DevBuf grid, grid_tmp, grid_coords, grid_idx, grid_out;
         DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts, partial, rayrec;
@@ -1126,6 +1133,13 @@ uint8_t* spec_hint_buf(sng_ctx* c);
 // opacity policy (spec_k_of) sizes the look-ahead better (round 3: 1 deg/frame orbit 571 frames/s with hints read,
 // 623 without).  They are written only by a frame that repeats the previous frame's view, so a moving camera
 // makes none of their scattered byte stores.  The pixel jitter (spp) is not part of it: sub-pixel moves keep the hints close.
+// the lens the NeRF rays of a frame go through: render_lens when render_with_lens_distortion is set, else Perspective
+// (Testbed::render_nerf_with_buffers, testbed_nerf.cu:2504)
+Lens frame_lens(const sng_ctx* c) {
+    Lens l{};
+    if (c->p("render_with_lens_distortion") != 0.0) l = c->render_lens;
+    return l;
+}
 uint64_t spec_view_key(const sng_ctx* c, f2 focal, f2 sc) {
     uint64_t h = 1469598103934665603ull;
     auto mix = [&](const void* p, size_t n) {
@@ -1136,6 +1150,8 @@ uint64_t spec_view_key(const sng_ctx* c, f2 focal, f2 sc) {
     mix(&c->has_cam1, sizeof(c->has_cam1));
     if (c->has_cam1) mix(c->cam1, sizeof(c->cam1));
     mix(c->rolling_shutter, sizeof(c->rolling_shutter));
+    const Lens lens = frame_lens(c);
+    mix(&lens, sizeof(lens));
     mix(&focal, sizeof(focal));
     mix(&sc, sizeof(sc));
     mix(c->nerf_res, sizeof(c->nerf_res));
@@ -1203,6 +1219,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
         a.pos1 = cam.c3;
     }
     for (int k = 0; k < 4; ++k) a.rolling_shutter[k] = c->rolling_shutter[k];
+    a.lens = frame_lens(c);
     const int nres[2] = {NW, NH};
     a.focal = focal_for(c, nres);
     a.screen_center = sc;
@@ -1869,7 +1886,8 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
 // ================================================================================================
 TrainImages train_images(sng_ctx* c) {
     auto& t = c->tr;
-    return {t.pixels.as<uint32_t>(), t.xforms.as<float>(), t.xforms_ray.as<float>(), t.focal.as<float>(), t.pp.as<float>(), t.w, t.h, t.n_images};
+    return {t.pixels.as<uint32_t>(), t.xforms.as<float>(), t.xforms_ray.as<float>(), t.focal.as<float>(), t.pp.as<float>(),
+            t.h_lens.empty() ? nullptr : t.lens.as<Lens>(), t.w, t.h, t.n_images};
 }
 
 // Testbed::reset_network's training state: fp32 master weights from the current model, zeroed
@@ -2321,6 +2339,30 @@ void restore_training_state(sng_ctx* c, const JValue& snap) {
     c->has_bitfield = true;
 }
 
+// from_json(Lens) (json_binding.h:65-95)
+Lens lens_from_json(const JValue& j) {
+    Lens l{};
+    auto num = [&](const char* k) { return j[k].as_float(); };
+    if (j.contains("k1")) {
+        if (j.contains("is_fisheye") && j["is_fisheye"].as_bool()) {
+            l.mode = LENS_OPENCV_FISHEYE;
+            l.params[0] = num("k1"); l.params[1] = num("k2"); l.params[2] = num("k3"); l.params[3] = num("k4");
+        } else {
+            l.mode = LENS_OPENCV;
+            l.params[0] = num("k1"); l.params[1] = num("k2"); l.params[2] = num("p1"); l.params[3] = num("p2");
+        }
+    } else if (j.contains("ftheta_p0")) {
+        l.mode = LENS_FTHETA;
+        const char* kf[7] = {"ftheta_p0", "ftheta_p1", "ftheta_p2", "ftheta_p3", "ftheta_p4", "w", "h"};
+        for (int i = 0; i < 7; ++i) l.params[i] = num(kf[i]);
+    } else if (j.contains("latlong")) {
+        l.mode = LENS_LATLONG;
+    } else if (j.contains("equirectangular")) {
+        l.mode = LENS_EQUIRECTANGULAR;
+    }
+    return l;
+}
+
 void load_snapshot(sng_ctx* c, const std::string& path) {
     ParsedSnapshot ps = parse_snapshot(path);
     const JValue& snap = ps.root["snapshot"];
@@ -2330,6 +2372,12 @@ void load_snapshot(sng_ctx* c, const std::string& path) {
         const JValue& ds = snap["nerf"]["dataset"];
         if (ds.contains("scale")) c->ds_scale = ds["scale"].as_num();
         if (ds.contains("offset")) c->ds_offset = mk(ds["offset"][0].as_float(), ds["offset"][1].as_float(), ds["offset"][2].as_float());
+        // load_nerf_post: render_lens = metadata[0].lens (testbed_nerf.cu:3051-3052; NerfDataset from_json reads the global
+        // "lens" default, then the image's own, json_binding.h:141-160); render_with_lens_distortion is left as it is
+        c->render_lens = Lens{};
+        if (ds.contains("lens")) c->render_lens = lens_from_json(ds["lens"]);
+        if (ds.contains("metadata") && ds["metadata"].size() > 0 && ds["metadata"][0].contains("lens"))
+            c->render_lens = lens_from_json(ds["metadata"][0]["lens"]);
     }
     if (snap.contains("up_dir")) c->up = mk(snap["up_dir"][0].as_float(), snap["up_dir"][1].as_float(), snap["up_dir"][2].as_float());
     if (snap.contains("camera")) {
@@ -2376,6 +2424,25 @@ void put_mat43(MsgpackWriter& w, const float m[12]) {   // tcnn mat json: an arr
     for (int i = 0; i < 4; ++i) w.nums(m + 3 * i, 3);
 }
 void put_aabb(MsgpackWriter& w, const aabb& b) { w.map(2); w.key("min"); put_vec3(w, b.lo); w.key("max"); put_vec3(w, b.hi); }
+// to_json(Lens) (json_binding.h:37-63)
+void put_lens(MsgpackWriter& w, const Lens& l) {
+    const char* k4[4] = {"k1", "k2", l.mode == LENS_OPENCV_FISHEYE ? "k3" : "p1", l.mode == LENS_OPENCV_FISHEYE ? "k4" : "p2"};
+    if (l.mode == LENS_OPENCV || l.mode == LENS_OPENCV_FISHEYE) {
+        w.map(5);
+        w.key("is_fisheye"); w.boolean(l.mode == LENS_OPENCV_FISHEYE);
+        for (int i = 0; i < 4; ++i) { w.key(k4[i]); w.num(l.params[i]); }
+    } else if (l.mode == LENS_FTHETA) {
+        const char* kf[7] = {"ftheta_p0", "ftheta_p1", "ftheta_p2", "ftheta_p3", "ftheta_p4", "w", "h"};
+        w.map(7);
+        for (int i = 0; i < 7; ++i) { w.key(kf[i]); w.num(l.params[i]); }
+    } else if (l.mode == LENS_LATLONG) {
+        w.map(1); w.key("latlong"); w.boolean(true);
+    } else if (l.mode == LENS_EQUIRECTANGULAR) {
+        w.map(1); w.key("equirectangular"); w.boolean(true);
+    } else {
+        w.map(0);
+    }
+}
 void put_network_config(MsgpackWriter& w, const sng_nerf_config& g) {
     w.key("loss"); w.map(1); w.key("otype"); w.str("Huber");
     w.key("optimizer"); w.map(3); w.key("otype"); w.str("Ema"); w.key("decay"); w.num(0.95);
@@ -2467,7 +2534,7 @@ void save_snapshot(sng_ctx* c, const std::string& path, bool include_opt, bool c
             for (int i = 0; i < ni; ++i) {
                 w.map(5);
                 w.key("focal_length"); w.nums(&fo[2 * i], 2);
-                w.key("lens"); w.map(0);
+                w.key("lens"); put_lens(w, t.h_lens.empty() ? Lens{} : t.h_lens[i]);
                 w.key("principal_point"); w.nums(&pp[2 * i], 2);
                 const float rs[4] = {0, 0, 0, 0};
                 w.key("rolling_shutter"); w.nums(rs, 4);
@@ -2759,6 +2826,35 @@ int sng_set_camera_view(sng_ctx* c, const float v[3], const float at[3], float s
 int sng_set_camera_matrix(sng_ctx* c, const float m[12]) {
     return guarded([&] { std::memcpy(c->cam, m, 48); c->has_cam1 = false; c->mesh_reset = true; });
 }
+// Testbed::set_camera_to_training_view (testbed.cu:453-469): the training image's camera (its xform through
+// get_xform_given_rolling_shutter at uv (0.5, 0.5), t 0: the quat round trip), relative focal length =
+// focal / resolution[fov_axis], m_scale from the old look-at, render_with_lens_distortion on with the image's
+// lens, screen centre 1 - principal point
+int sng_set_camera_to_training_view(sng_ctx* c, int32_t view) {
+    return guarded([&] {
+        if (!c) throw SngError(SNG_ERR_INVALID, "null context");
+        auto& t = c->tr;
+        if (view < 0 || view >= t.n_images) throw SngError(SNG_ERR_INVALID, "no such training view");
+        HIPCHK(hipSetDevice(c->device));
+        const f3 old_look_at = look_at(c);
+        float xf[12], fo[2], pp[2];
+        HIPCHK(hipMemcpy(xf, t.xforms.as<float>() + 12 * (size_t)view, 48, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(fo, t.focal.as<float>() + 2 * (size_t)view, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(pp, t.pp.as<float>() + 2 * (size_t)view, 8, hipMemcpyDeviceToHost));
+        const m3 r = rolling_shutter_rotation({mk(xf[0], xf[1], xf[2]), mk(xf[3], xf[4], xf[5]), mk(xf[6], xf[7], xf[8])});
+        set_cam_col(c, 0, r.c0); set_cam_col(c, 1, r.c1); set_cam_col(c, 2, r.c2); set_cam_col(c, 3, mk(xf[9], xf[10], xf[11]));
+        c->has_cam1 = false;
+        const float res = (float)(c->fov_axis == 0 ? t.w : t.h);
+        c->rel_focal[0] = fo[0] / res;
+        c->rel_focal[1] = fo[1] / res;
+        c->m_scale = std::max(dot(old_look_at - cam_col(c, 3), cam_col(c, 2)), 0.1f);
+        c->params["render_with_lens_distortion"] = 1.0;
+        c->render_lens = t.h_lens.empty() ? Lens{} : t.h_lens[(size_t)view];
+        c->screen_center[0] = 1.0f - pp[0];
+        c->screen_center[1] = 1.0f - pp[1];
+        c->mesh_reset = true;
+    });
+}
 int sng_set_motion_blur(sng_ctx* c, const float camera1[12], const float rolling_shutter[4]) {
     return guarded([&] {
         c->has_cam1 = camera1 != nullptr;
@@ -2984,6 +3080,44 @@ int sng_train_set_dataset(sng_ctx* c, uint32_t n, uint32_t w, uint32_t h, const 
         upload(t.focal, focal, (size_t)n * 2 * 4);
         upload(t.pp, pp, (size_t)n * 2 * 4);
         t.w = (int)w; t.h = (int)h; t.n_images = (int)n;
+        t.h_lens.clear();   // a new dataset is Perspective until sng_train_set_lens
+    });
+}
+static_assert(sizeof(Lens) == sizeof(sng_lens), "Lens mirrors sng_lens");
+int sng_train_set_lens(sng_ctx* c, const sng_lens* lenses, uint32_t n) {
+    return guarded([&] {
+        if (!c) throw SngError(SNG_ERR_INVALID, "null context");
+        HIPCHK(hipSetDevice(c->device));
+        auto& t = c->tr;
+        if (!lenses || n == 0) { t.h_lens.clear(); return; }
+        if ((int)n != t.n_images) throw SngError(SNG_ERR_INVALID, "one lens per training image (sng_train_set_dataset) expected");
+        std::vector<Lens> h(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            if (lenses[i].mode < 0 || lenses[i].mode > 5) throw SngError(SNG_ERR_INVALID, "unknown lens mode");
+            h[i].mode = lenses[i].mode;
+            for (int k = 0; k < 7; ++k) h[i].params[k] = lenses[i].params[k];
+        }
+        upload(t.lens, h.data(), (size_t)n * sizeof(Lens));
+        t.h_lens = h;
+    });
+}
+int sng_set_render_lens(sng_ctx* c, const sng_lens* lens) {
+    return guarded([&] {
+        if (!c) throw SngError(SNG_ERR_INVALID, "null context");
+        Lens l{};
+        if (lens) {
+            if (lens->mode < 0 || lens->mode > 5) throw SngError(SNG_ERR_INVALID, "unknown lens mode");
+            l.mode = lens->mode;
+            for (int k = 0; k < 7; ++k) l.params[k] = lens->params[k];
+        }
+        c->render_lens = l;
+    });
+}
+int sng_get_render_lens(sng_ctx* c, sng_lens* out) {
+    return guarded([&] {
+        if (!c || !out) throw SngError(SNG_ERR_INVALID, "null argument");
+        out->mode = c->render_lens.mode;
+        for (int k = 0; k < 7; ++k) out->params[k] = c->render_lens.params[k];
     });
 }
 int sng_train_reset(sng_ctx* c, uint64_t seed) {

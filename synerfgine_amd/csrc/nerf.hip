@@ -97,11 +97,17 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
             const float* rs = a.rolling_shutter;
             const float pixel_t = rs[0] + rs[1] * uv.x + rs[2] * uv.y + rs[3] * ld_random_val0(a.spp, idx * 72239731u);
             origin = a.cam.c3 + (a.pos1 - a.cam.c3) * pixel_t;
-            // uv_to_ray (common_device.cuh:403-470): pinhole, no lens/foveation/parallax/aperture
-            f3 d = mk((uv.x - a.screen_center.x) * (float)a.W / a.focal.x, (uv.y - a.screen_center.y) * (float)a.H / a.focal.y, 1.0f);
+            // uv_to_ray (common_device.cuh:403-470): the frame's lens (Perspective unless render_with_lens_distortion),
+            // no foveation / parallax / aperture
+            f3 d;
+            bool valid = true;
+            if (a.lens.mode == LENS_PERSPECTIVE)
+                d = mk((uv.x - a.screen_center.x) * (float)a.W / a.focal.x, (uv.y - a.screen_center.y) * (float)a.H / a.focal.y, 1.0f);
+            else
+                valid = lens_dir(a.lens, uv, a.screen_center, a.W, a.H, a.focal, d);
             d = mul(shutter_rotation(a.q0, a.q1, pixel_t), d);
             float4 fb = frame_rgba[idx];
-            fb.x = 0.0f; fb.y = 0.0f; fb.z = 0.0f;
+            if (valid) { fb.x = 0.0f; fb.y = 0.0f; fb.z = 0.0f; }   // an invalid ray returns before the clear (1919-1923)
             if (a.reset) fb.w = 0.0f;
             frame_rgba[idx] = fb;
             frame_depth[idx] = MAX_DEPTH;
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(256) void init_rays_kernel(NerfFrameArgs a, RayBuf 
             dir = normalize(d);
             const Volume& v = a.vol;
             float t0 = fmaxf(aabb_entry(v.render_aabb, to_local(v, origin), to_local(v, dir)), 0.0f) + 1e-6f;
-            if (aabb_contains(v.render_aabb, to_local(v, origin + dir * t0))) {
+            if (valid && aabb_contains(v.render_aabb, to_local(v, origin + dir * t0))) {
                 // advance_pos_nerf (testbed_nerf.cu:334-363)
                 f3 idir = inv(dir);
                 float t1 = advance_n_steps(t0, v.cone, ld_random_val0(a.spp, idx * 786433u));

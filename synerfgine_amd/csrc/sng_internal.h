@@ -142,6 +142,7 @@ struct NerfFrameArgs {
     q4 q0, q1;           // quat_cast of camera0 / camera1 (get_xform_given_rolling_shutter, common_device.cuh:361-368)
     f3 pos1;             // camera1 position (camera0's: cam.c3)
     float rolling_shutter[4];
+    Lens lens;           // uv_to_ray's lens (Perspective unless render_with_lens_distortion)
     f2 focal;
     f2 screen_center;
     int W, H;            // full NeRF resolution (pixel indices are global)

@@ -59,6 +59,7 @@ struct TrainImages {
     const float* xforms_ray;  // the same after get_xform_given_rolling_shutter's quat round trip (ray generation)
     const float* focal;       // [n][2] pixels
     const float* pp;          // [n][2] principal point (uv)
+    const Lens* lens;         // [n] dataset lens per image (read_lens, nerf_loader.cu:175-239); nullptr: every image Perspective
     int w, h, n;
 };
 
@@ -84,11 +85,17 @@ SNG_HD f2 train_image_pos(Pcg32& rng, const TrainImages& im) {
 }
 
 struct TrainRay { f3 o, d; };
-// uv_to_ray (common_device.cuh:403-470), pinhole, no parallax / aperture / near distance
+// uv_to_ray (common_device.cuh:403-470) with the image's lens (testbed_nerf.cu:890-905), no parallax / aperture / near
+// distance / distortion map; an invalid ray (F-Theta outside its domain) becomes {xform[3], xform[2]} (testbed_nerf.cu:901-903)
 SNG_HD TrainRay train_ray(const TrainImages& im, uint32_t img, f2 uv) {
     const float* xf = im.xforms_ray + 12 * img;
     const m3 rot = {mk(xf[0], xf[1], xf[2]), mk(xf[3], xf[4], xf[5]), mk(xf[6], xf[7], xf[8])};
-    const f3 dir = mk((uv.x - im.pp[2 * img]) * (float)im.w / im.focal[2 * img], (uv.y - im.pp[2 * img + 1]) * (float)im.h / im.focal[2 * img + 1], 1.0f);
+    const f2 pp = {im.pp[2 * img], im.pp[2 * img + 1]}, focal = {im.focal[2 * img], im.focal[2 * img + 1]};
+    f3 dir;
+    if (!im.lens || im.lens[img].mode == LENS_PERSPECTIVE)
+        dir = mk((uv.x - pp.x) * (float)im.w / focal.x, (uv.y - pp.y) * (float)im.h / focal.y, 1.0f);
+    else if (!lens_dir(im.lens[img], uv, pp, im.w, im.h, focal, dir))
+        return {mk(xf[9], xf[10], xf[11]), rot.c2};
     return {mk(xf[9], xf[10], xf[11]), mul(rot, dir)};
 }
 

@@ -29,8 +29,8 @@ typedef _Float16 h4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4v mfma16k16(h4v a, h4v b, f4v c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
 
 // ---------------------------------------------------------------------------------------------
-// generate_training_samples_nerf (testbed_nerf.cu:838-998), no error-map CDFs, no distortion,
-// no envmap, max_level_rand_training off, pinhole lens
+// generate_training_samples_nerf (testbed_nerf.cu:838-998), no error-map CDFs, no distortion map,
+// no envmap, max_level_rand_training off; the dataset lens per image (train_ray)
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void train_generate_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -607,15 +607,27 @@ __global__ void train_mark_untrained_kernel(uint32_t n_elements, float* __restri
         const float* xf = im.xforms + 12 * j;
         const f3 c0 = mk(xf[0], xf[1], xf[2]), c1 = mk(xf[3], xf[4], xf[5]), c2 = mk(xf[6], xf[7], xf[8]), c3 = mk(xf[9], xf[10], xf[11]);
         const f2 focal = {im.focal[2 * j], im.focal[2 * j + 1]}, pp = {im.pp[2 * j], im.pp[2 * j + 1]};
+        const int32_t lm = im.lens ? im.lens[j].mode : LENS_PERSPECTIVE;
+        // F-Theta has no forward mapping and LatLong / Equirectangular see everything: counted as seeing the cell (116-121)
+        if (lm == LENS_FTHETA || lm == LENS_LATLONG || lm == LENS_EQUIRECTANGULAR) { ++count; continue; }
         for (uint32_t k = 0; k < 8; ++k) {
             const f3 corner = pos + mk((k & 1) ? voxel_size : 0.0f, (k & 2) ? voxel_size : 0.0f, (k & 4) ? voxel_size : 0.0f);
             const f3 dir = normalize(corner - c3);
             if (dot(dir, c2) < 1e-4f) continue;
-            // pos_to_uv (pinhole): camera-space direction, project, then uv_to_ray round trip
+            // pos_to_uv (common_device.cuh:507-541): camera-space direction, the lens's forward distortion, project; then the
+            // uv_to_ray round trip (through the Newton undistortion for OpenCV lenses)
             const f3 v = corner - c3;
             const f3 lc = mk(dot(v, c0), dot(v, c1), dot(v, c2));
-            const f2 uv = {lc.x / lc.z * focal.x / (float)im.w + pp.x, lc.y / lc.z * focal.y / (float)im.h + pp.y};
-            const f3 dl = mk((uv.x - pp.x) * (float)im.w / focal.x, (uv.y - pp.y) * (float)im.h / focal.y, 1.0f);
+            float px = lc.x / lc.z, py = lc.y / lc.z;
+            if (lm != LENS_PERSPECTIVE) {
+                float du, dv;
+                lens_delta(lm, im.lens[j].params, px, py, du, dv);
+                px += du;
+                py += dv;
+            }
+            const f2 uv = {px * focal.x / (float)im.w + pp.x, py * focal.y / (float)im.h + pp.y};
+            f3 dl = mk((uv.x - pp.x) * (float)im.w / focal.x, (uv.y - pp.y) * (float)im.h / focal.y, 1.0f);
+            if (lm != LENS_PERSPECTIVE) lens_undistort(lm, im.lens[j].params, dl.x, dl.y);
             const f3 rd = normalize(c0 * dl.x + c1 * dl.y + c2 * dl.z);
             if (length(rd - dir) < 1e-3f && uv.x > 0.0f && uv.y > 0.0f && uv.x < 1.0f && uv.y < 1.0f) { ++count; break; }
         }

@@ -1,5 +1,7 @@
 """Training data for the online trainer (BASELINE config 5).
 
+* `load_nerf` reads a transforms.json scene with its lens model (read_lens / read_focal_length,
+  nerf_loader.cu:175-270), e.g. the reference's real fox capture (OpenCV k1 k2 p1 p2, cx cy).
 * `load_nerf_synthetic` reads a NeRF-synthetic scene (transforms.json + 8-bit PNGs, e.g. the lego
   set the reference ships under data/nerf/lego) the way ngp's loader does (nerf_loader.cu:
   focal from fl_x / camera_angle_x, principal point cx/w or 0.5, scale 0.33, offset 0.5, and
@@ -57,6 +59,116 @@ def load_nerf_synthetic(scene_dir, split_json="transforms.json", max_images=None
         focal.append((fx, fy))
         pp.append((meta.get("cx", 0.5 * w) / w, meta.get("cy", 0.5 * h) / h))
     return np.stack(images), np.stack(xforms), np.array(focal, np.float32), np.array(pp, np.float32)
+
+
+LENS_PERSPECTIVE, LENS_OPENCV, LENS_FTHETA, LENS_LATLONG, LENS_OPENCV_FISHEYE, LENS_EQUIRECTANGULAR = range(6)   # ELensMode (common.h:188-195)
+
+
+def read_lens(j, lens, principal_point, rolling_shutter):
+    """read_lens (nerf_loader.cu:175-239) on one JSON object (the transforms file or a frame): updates
+    lens = [mode, params(7)], principal_point = [x, y] (uv) and rolling_shutter = [4] in place."""
+    mode = LENS_PERSPECTIVE
+    opencv_mode = LENS_OPENCV_FISHEYE if j.get("is_fisheye", False) else LENS_OPENCV
+    for name, idx in (("k1", 0), ("k2", 1), ("k3", 2), ("k4", 3), ("p1", 2), ("p2", 3)):
+        if name in j:
+            lens[1][idx] = float(np.float32(j[name]))
+            if lens[1][idx] != 0.0:
+                mode = opencv_mode
+    if "cx" in j:
+        principal_point[0] = float(np.float32(j["cx"]) / np.float32(j["w"]))
+    if "cy" in j:
+        principal_point[1] = float(np.float32(j["cy"]) / np.float32(j["h"]))
+    if "rolling_shutter" in j:
+        rs = j["rolling_shutter"]
+        rolling_shutter[:] = [float(rs[0]), float(rs[1]), float(rs[2]), float(rs[3]) if len(rs) >= 4 else 0.0]
+    if "ftheta_p0" in j:
+        for k in range(5):
+            lens[1][k] = float(j[f"ftheta_p{k}"])
+        lens[1][5], lens[1][6] = float(j["w"]), float(j["h"])
+        mode = LENS_FTHETA
+    if "latlong" in j:
+        mode = LENS_LATLONG
+    if "equirectangular" in j:
+        mode = LENS_EQUIRECTANGULAR
+    if mode != LENS_PERSPECTIVE:   # an outer distortion mode is not overridden by nothing
+        lens[0] = mode
+
+
+def _fov_to_focal(res, deg):
+    return 0.5 * res / math.tan(0.5 * deg * math.pi / 180.0)
+
+
+def read_focal_length(j, focal, res):
+    """read_focal_length (nerf_loader.cu:241-270): per axis x_fov (deg) > fl_x > camera_angle_x (rad); y falls back to x."""
+    def axis(r, a):
+        if f"{a}_fov" in j:
+            return _fov_to_focal(r, float(j[f"{a}_fov"]))
+        if f"fl_{a}" in j:
+            return float(j[f"fl_{a}"])
+        if f"camera_angle_{a}" in j:
+            return _fov_to_focal(r, float(j[f"camera_angle_{a}"]) * 180.0 / math.pi)
+        return 0.0
+    x, y = axis(res[0], "x"), axis(res[1], "y")
+    if x != 0.0:
+        focal[0] = focal[1] = x
+        if y != 0.0:
+            focal[1] = y
+    elif y != 0.0:
+        focal[0] = focal[1] = y
+    else:
+        return False
+    return True
+
+
+def load_nerf(scene_dir, split_json="transforms.json", max_images=None):
+    """load_nerf (nerf_loader.cu:272-700) for one transforms file of 8-bit PNG images: scale 0.33 / offset 0.5 unless
+    the file gives them, aabb_scale, the lens / principal point / rolling shutter of read_lens (the file's, then each
+    frame's), the focal length of read_focal_length (the file's, then each frame's), frames kept only when their image
+    exists (the sharpness branch, threshold 0 by default, nerf_loader.cu:364-386), nerf_matrix_to_ngp.
+    Returns a dict: images [n,h,w,4] u8, xforms [n,3,4], focal [n,2], pp [n,2], lenses [(mode, params)], aabb_scale,
+    scale, offset, paths."""
+    with open(os.path.join(scene_dir, split_json)) as f:
+        meta = json.load(f)
+    frames = meta["frames"]
+    if "n_frames" in meta:
+        frames = frames[: min(len(frames), int(meta["n_frames"]))]
+    if frames and "sharpness" in frames[0]:
+        thr = float(meta.get("sharpness_discard_threshold", 0.0))
+        kept = []
+        for i, fr in enumerate(frames):
+            a, b = max(0, i - 3), min(i + 3, len(frames) - 1)
+            mean = sum(float(frames[k].get("sharpness", 1.0)) for k in range(a, b)) / max(1, b - a)
+            if os.path.exists(os.path.join(scene_dir, fr["file_path"])) and float(fr.get("sharpness", 1.0)) > thr * mean:
+                kept.append(fr)
+        frames = kept
+    frames = frames[:max_images] if max_images else frames
+    scale = float(meta.get("scale", NERF_SCALE))
+    off = meta.get("offset", 0.5)
+    offset = tuple(float(v) for v in off) if isinstance(off, list) else (float(off),) * 3
+    lens0, pp0, rs0 = [LENS_PERSPECTIVE, [0.0] * 7], [0.5, 0.5], [0.0] * 4
+    read_lens(meta, lens0, pp0, rs0)
+    images, xforms, focal, pp, lenses, paths = [], [], [], [], [], []
+    for fr in frames:
+        path = os.path.join(scene_dir, fr["file_path"])
+        if not os.path.splitext(path)[1]:
+            path += ".png"
+        img = read_png(path)
+        h, w = img.shape[:2]
+        fo = [0.0, 0.0]
+        got = read_focal_length(meta, fo, (w, h))
+        got |= read_focal_length(fr, fo, (w, h))
+        if not got:
+            raise ValueError(f"{path}: no focal length")
+        lens, p, rs = [lens0[0], list(lens0[1])], list(pp0), list(rs0)
+        read_lens(fr, lens, p, rs)
+        images.append(img)
+        xforms.append(nerf_matrix_to_ngp(fr.get("transform_matrix_start", fr["transform_matrix"]), scale, offset))
+        focal.append(fo)
+        pp.append(p)
+        lenses.append((lens[0], lens[1]))
+        paths.append(fr["file_path"])
+    return {"images": np.stack(images), "xforms": np.stack(xforms), "focal": np.array(focal, np.float32), "pp": np.array(pp, np.float32),
+            "lenses": lenses, "aabb_scale": int(meta.get("aabb_scale", 1)), "scale": scale, "offset": offset, "paths": paths}
 
 
 def orbit_cameras(n, radius=1.6, center=(0.5, 0.5, 0.5), elevation_deg=(-20.0, 50.0), seed=0):

@@ -15,6 +15,10 @@ CONFIGS = {
                                                                             "shadow_on_virtual_obj": 0}),
     "c3": dict(scene="armadillo.json", width=1920, height=1080, overrides={}),
     "c4": dict(scene="kitchen-rocks.json", width=1920, height=1080, overrides={"light_samples": 4}),
+    # C4's workload (bunny / rock / box, one light, light_samples 4, NeRF shadows r = 2) on a TRAINED cascaded field:
+    # the reference's real fox capture (aabb_scale 4, OpenCV lens) trained by tools/train_fox.py, camera and object
+    # placement of scenes/fox-rocks.json (kitchen-rocks.json's rendering block, materials and meshes)
+    "c4fox": dict(scene="fox-rocks.json", width=1920, height=1080, overrides={"light_samples": 4}),
     # the scene of every reference measurement in BASELINE.md (scripts/render/profiling.sh:12-18): lego +
     # armadillo/bunny/monkey at 1280x720, swept over --sshadows/--nshadows in {1,2,4,8}
     "abm": dict(scene="dmrf-compare-abm.json", width=1280, height=720, overrides={}),
@@ -23,6 +27,8 @@ CONFIGS = {
 # the trained lego snapshot (tools/train_lego.py on data/nerf/lego400, the reference's lego set); configs
 # c2/c3 render it when model="lego" (bench.py's default), the tests default to the synthetic model
 LEGO_INGP = os.path.join(REPO, "data", "lego.ingp")
+# the trained fox snapshot (tools/train_fox.py on data/nerf/fox270, the reference's fox capture); config c4fox
+FOX_INGP = os.path.join(REPO, "data", "fox.ingp")
 
 _MODEL_CACHE = {}
 
@@ -30,7 +36,11 @@ _MODEL_CACHE = {}
 def snapshot_path(config, model):
     """.ingp path a (config, model) pair renders, or None for the synthetic content."""
     if model in (None, "synthetic"):
+        if config == "c4fox":
+            raise ValueError("c4fox renders the trained fox snapshot (data/fox.ingp)")
         return None
+    if model == "fox" or (config == "c4fox" and model in ("lego", "default")):
+        return FOX_INGP
     if model == "lego":
         if config == "c4":
             raise ValueError("c4 renders the kitchen-like synthetic snapshot (no kitchen capture in the reference)")

@@ -226,13 +226,33 @@ def kitchen_like(seed=1337, ramp=0.2, a=2.6, b=2.3):
     return cfg, params, dg.astype(np.float16)
 
 
-def random_init(seed=1337, cfg=None):
+def per_level_scale(aabb_scale, n_levels=L, base_resolution=NMIN, desired_resolution=2048.0):
+    """Testbed::reset_network's automatic per_level_scale (testbed.cu:3737-3741), in float with glibc's expf / logf:
+    exp(log(desired_resolution * aabb_scale / base_resolution) / (n_levels - 1))."""
+    import ctypes
+    import ctypes.util
+    libm = ctypes.CDLL(ctypes.util.find_library("m"))
+    libm.expf.restype = libm.logf.restype = ctypes.c_float
+    libm.expf.argtypes = libm.logf.argtypes = [ctypes.c_float]
+    x = np.float32(np.float32(desired_resolution) * np.float32(aabb_scale) / np.float32(base_resolution))
+    return float(libm.expf(np.float32(np.float32(libm.logf(x)) / np.float32(n_levels - 1))))
+
+
+def random_init(seed=1337, cfg=None, aabb_scale=1):
     """Freshly initialised base.json network (tcnn: hash-grid entries U(-1e-4, 1e-4), Xavier-uniform
-    MLP weights) -- the starting point of online training."""
+    MLP weights) -- the starting point of online training.  `aabb_scale` > 1 (a real capture such as fox):
+    the per_level_scale reset_network derives for it, and the grid sized by the library's level table."""
     rng = np.random.default_rng(seed)
     mlp = np.concatenate([_xavier(rng, 64, 32).ravel(), _xavier(rng, 16, 64).ravel(), _xavier(rng, 64, 32).ravel(), _xavier(rng, 64, 64).ravel(),
                           _xavier(rng, 16, 64).ravel()])
-    offsets, _ = level_table()
-    grid = rng.uniform(-1e-4, 1e-4, size=offsets[-1] * F)
-    cfg = cfg or dict(n_levels=L, n_features_per_level=F, log2_hashmap_size=LOG2T, base_resolution=NMIN, per_level_scale=PER_LEVEL_SCALE, aabb_scale=1)
+    if cfg is None:
+        pls = PER_LEVEL_SCALE if aabb_scale == 1 else per_level_scale(aabb_scale)
+        cfg = dict(n_levels=L, n_features_per_level=F, log2_hashmap_size=LOG2T, base_resolution=NMIN, per_level_scale=pls, aabb_scale=aabb_scale)
+    if cfg.get("aabb_scale", 1) == 1 and cfg.get("per_level_scale") == PER_LEVEL_SCALE:
+        offsets, _ = level_table()
+        n_grid = offsets[-1] * F
+    else:   # the library's GridEncoding level table (sng_nerf_param_count)
+        from . import _lib
+        n_grid = int(_lib.load().sng_nerf_param_count(_lib.sng_nerf_config(**cfg))) - 10240
+    grid = rng.uniform(-1e-4, 1e-4, size=n_grid)
     return cfg, np.concatenate([mlp, grid]).astype(np.float16)

@@ -24,6 +24,8 @@ def _oracle_mode(request):
     if m is not None or "oracle" in sys.modules:
         import oracle as O
         O.lib().orc_set_literal(1 if mode == "literal" else 0)
+        O.lib().orc_set_render_lens(None)   # and no lens left over from another test
+        O.lib().orc_set_train_lens(None, 0)
     yield
 
 
