@@ -301,7 +301,7 @@ def train_leg(steps=200, warmup=50, seed=1337):
     does, testbed_nerf.cu:3272-3296).  fp16 parameters / activations / gradient GEMM operands with f32 master
     weights and accumulation, tcnn's types (BASELINE.json C5 names bf16)."""
     import numpy as np
-    from synerfgine_amd import Testbed, nerf_data, synthetic
+    from synerfgine_amd import Engine, Testbed, nerf_data, synthetic
     d = os.path.join(REPO, "data", "nerf", "lego400")
     imgs, xf, focal, pp = nerf_data.load_nerf_synthetic(d)
     angle = json.load(open(os.path.join(d, "transforms.json")))["camera_angle_x"]
@@ -325,12 +325,44 @@ def train_leg(steps=200, warmup=50, seed=1337):
         # (K = samples; 64x32 + 16x64 + 64x32 + 64x64 + 16x64 = 10,240 weights), forward + backward of the fused MLPs,
         # and the hash-grid gradient scatter (8 levels x 8 corners x F = 4 f32 adds per sample)
         dw_flop = 2 * samples * 10240
+        # per-stage device times of 50 more steps (HIP events per stage, param train_kernel_times; after the timed steps)
+        # -> the roofline of each stage at its own bound
+        eng = Engine(tb)
+        eng.set_param("train_kernel_times", 1)
+        st2 = tb.train(50)
+        eng.set_param("train_kernel_times", 0)
+        sm = st2.get("stage_ms", {})
+        n_before = int(st2["measured_batch_before_compaction"])
+        n_after = int(st2["measured_batch"])
+        n_params = int(synthetic.n_params())
+        rl = {}
+        if sm:
+            def frac(b, ms, peak):
+                return round(b / (ms * 1e-3) / 1e9 / peak, 4) if ms > 0 else None
+            rl = {"stage_ms": sm,
+                  "network": {"bound": "hbm", "bytes": n_before * BYTES_PER_SAMPLE, "frac": frac(n_before * BYTES_PER_SAMPLE, sm["network"], HBM_PEAK_GBS),
+                              "note": "inference forward of every generated sample, 548 B/sample (SURVEY 8d)"},
+                  "field": {"bound": "float atomics", "bytes": n_after * 8 * 8 * 4 * 4, "peak_GBps": 1300.0,
+                            "frac": frac(n_after * 8 * 8 * 4 * 4, sm["field"], 1300.0),
+                            "note": "hash-grid gradient scatter, 8 levels x 8 corners x 4 features x 4 B per compacted sample, against the "
+                                    "chip-wide float-atomic rate (MI355X_MICROARCH.md, Global float atomics); the kernel also runs the MLP "
+                                    "forward + backward on MFMA and folds runs of equal entries before adding"},
+                  "dw": {"bound": "hbm", "bytes": n_after * 960, "frac": frac(n_after * 960, sm["dw"], HBM_PEAK_GBS),
+                         "mfma_tflops": round(dw_flop / (sm["dw"] * 1e-3) / 1e12, 2) if sm["dw"] > 0 else None,
+                         "mfma_frac": round(dw_flop / (sm["dw"] * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS, 4) if sm["dw"] > 0 else None,
+                         "note": "dW = delta act^T over K = samples: reads the 960 B/sample fp16 activation + gradient tiles once"},
+                  "optimizer": {"bound": "hbm", "bytes_min": n_params * 20, "frac_min": frac(n_params * 20, sm["optimizer"], HBM_PEAK_GBS),
+                                "note": "Ema(ExpDecay(Adam)) over every param: >= 20 B/param (gradient, master, EMA read; EMA, fp16 training "
+                                        "and inference copies written) + 28 B per touched param (moments, step count)"},
+                  "generate": {"bound": "latency", "rays": int(st2["rays_per_batch"]),
+                               "note": "one thread per training ray marches the occupancy grid twice (count, then write)"}}
         return {"steps_per_s": round(steps / el, 1), "ms_per_step": round(1e3 * el / steps, 3),
                 "ms_per_step_device": round(st["ms"] / steps, 3), "steps": steps, "warmup": warmup,
                 "batch_target": 1 << 18, "measured_batch": samples, "rays_per_batch": int(st["rays_per_batch"]),
                 "loss_after": round(float(st["loss"]), 6), "step_after": int(st["step"]),
                 "algorithmic_per_step": {"dw_gemm_flop": dw_flop, "mlp_fwd_bwd_flop": 3 * 20480 * samples,
                                          "grid_scatter_atomic_bytes": samples * 8 * 8 * 4 * 4},
+                "roofline": rl,
                 "dtype": "fp16 params / activations / GEMM operands, f32 master weights, gradients and accumulation "
                          "(tcnn's network_precision_t; BASELINE.json C5 says bf16)",
                 "data": "data/nerf/lego400 (the reference's lego set at 400x400), 90 training views, fresh init (seed 1337)",

@@ -252,7 +252,10 @@ typedef struct {
     uint32_t measured_batch;                    /* compacted samples of the last step */
     uint32_t measured_batch_before_compaction;
     float ms;                                   /* device time of the call */
-    uint32_t reserved[10];
+    /* param train_kernel_times = 1: each stage's device time per step (HIP events), averaged over timed_steps */
+    float ms_generate, ms_network, ms_loss, ms_grad_clear, ms_field, ms_dw, ms_optimizer;
+    uint32_t timed_steps;
+    uint32_t reserved[2];
 } sng_train_stats;
 /* 8-bit PNG -> RGBA8 (host): the dataset loader's image decode (nerf_loader.cu, stb_image); out may be NULL to query the size */
 int sng_image_load_png(const char* path, uint8_t* out_rgba8, uint64_t capacity, int32_t* width, int32_t* height);

@@ -128,7 +128,10 @@ class Testbed:
     def train(self, n_steps):
         st = _lib.sng_train_stats()
         check(self._lib.sng_train(self.ctx, int(n_steps), ctypes.byref(st)))
-        return {k: getattr(st, k) for k in ("step", "loss", "rays_per_batch", "measured_batch", "measured_batch_before_compaction", "ms")}
+        out = {k: getattr(st, k) for k in ("step", "loss", "rays_per_batch", "measured_batch", "measured_batch_before_compaction", "ms")}
+        if st.timed_steps:   # param train_kernel_times
+            out["stage_ms"] = {k: round(getattr(st, "ms_" + k), 5) for k in ("generate", "network", "loss", "grad_clear", "field", "dw", "optimizer")}
+        return out
 
     def training_snapshot(self, n_params, n_cells):
         """(params fp16, density grid fp16) of the trained model -- the .ingp snapshot fields"""

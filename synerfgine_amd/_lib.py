@@ -147,7 +147,15 @@ class sng_train_stats(ctypes.Structure):
         ("measured_batch", ctypes.c_uint32),
         ("measured_batch_before_compaction", ctypes.c_uint32),
         ("ms", ctypes.c_float),
-        ("reserved", ctypes.c_uint32 * 10),
+        ("ms_generate", ctypes.c_float),
+        ("ms_network", ctypes.c_float),
+        ("ms_loss", ctypes.c_float),
+        ("ms_grad_clear", ctypes.c_float),
+        ("ms_field", ctypes.c_float),
+        ("ms_dw", ctypes.c_float),
+        ("ms_optimizer", ctypes.c_float),
+        ("timed_steps", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 2),
     ]
 
 

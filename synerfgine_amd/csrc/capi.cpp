@@ -359,6 +359,7 @@ const std::map<std::string, double>& default_params() {
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
+        {"train_kernel_times", 0},              // 1: sng_train times the stages of every step with HIP events (sng_train_stats.ms_*)
         {"render_with_lens_distortion", 0},     // Testbed::Nerf::render_with_lens_distortion (testbed_nerf.cu:2504): NeRF rays through
                                                 //   render_lens (sng_set_render_lens; the snapshot dataset's first lens)
         {"depth_scale", 1.0},                   // 1 / dataset.scale (testbed_nerf.cu:2748)
@@ -405,6 +406,7 @@ struct sng_ctx {
     hipStream_t s_nerf = nullptr, s_rt = nullptr;
     hipEvent_t ev_start = nullptr, ev_rt0 = nullptr, ev_rt1 = nullptr, ev_nerf0 = nullptr, ev_nerf1 = nullptr, ev_shadow1 = nullptr, ev_end = nullptr, ev_rt_go = nullptr, ev_fused0 = nullptr, ev_fused1 = nullptr, ev_os0 = nullptr, ev_os1 = nullptr, ev_alive = nullptr, ev_brick = nullptr;
     std::vector<hipEvent_t> net_events;
+    std::vector<hipEvent_t> train_events;   // train_kernel_times: the stages of a training step
 
     // model
     bool has_model = false;
@@ -1992,14 +1994,19 @@ TrainBatch train_batch(sng_ctx* c) {
 
 // train_nerf_step (3532-3780) up to the gradients; stage > 0 stops early (parity hooks):
 // 1 = samples generated, 2 = network outputs, 3 = loss / compaction, 4 = gradients
-void train_forward_backward(sng_ctx* c, int stage, hipStream_t s) {
+// ev (train_kernel_times): 8 events bracketing generate | network | loss | gradient clear | field | dW (the optimizer's
+// event is recorded by train_steps)
+void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev = nullptr) {
     auto& t = c->tr;
     const TrainStepArgs a = train_args(c);
     const TrainBatch b = train_batch(c);
     const TrainImages im = train_images(c);
     HIPCHK(hipMemsetAsync(t.ctrl.p, 0, sizeof(TrainCtrl), s));
     HIPCHK(hipMemsetAsync(t.loss.p, 0, (size_t)a.n_rays * 4, s));
+    auto mark = [&](int k) { if (ev) HIPCHK(hipEventRecord(ev[k], s)); };
+    mark(0);
     launch_train_generate(a, im, b, t.rng, s);
+    mark(1);
     if (stage == 1) return;
     // inference forward of every sample with the training params
     launch_train_pack(t.p_train.as<uint16_t>(), t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
@@ -2007,13 +2014,18 @@ void train_forward_backward(sng_ctx* c, int stage, hipStream_t s) {
     // count = min(numsteps_counter, max_samples): the generator drops rays beyond max_samples
     launch_train_clamp_count(&b.ctrl->numsteps_counter, a.max_samples, t.ctrl.as<uint32_t>() + 3, s);
     launch_network(net, b.coords, 7, 0, t.ctrl.as<uint32_t>() + 3, b.mlp_out, 1, (a.max_samples + 15) / 16, s);
+    mark(2);
     if (stage == 2) return;
     launch_train_loss(a, im, b, t.rng, c->d_mean.as<float>(), s);
+    mark(3);
     if (stage == 3) return;
     HIPCHK(hipMemsetAsync(t.grads.p, 0, c->n_params * 4, s));
+    mark(4);
     float* g = t.grads.as<float>();
     launch_train_field(a, b, net, t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), static_cast<uint16_t*>(net.grid), g + 3072 + 7168, s);
+    mark(5);
     launch_train_dw(a, b.acts, g, (uint32_t)c->n_cus, s);
+    mark(6);
 }
 
 void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
@@ -2023,24 +2035,40 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
     hipStream_t s = c->s_nerf;
     HIPCHK(hipEventRecord(c->ev_start, s));
     double loss_acc = 0.0;
+    // per-stage device times (param train_kernel_times): generate, network, loss, gradient clear, field, dW, optimizer
+    const bool timed = c->p("train_kernel_times") != 0.0;
+    while (timed && c->train_events.size() < 8) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->train_events.push_back(e); }
+    double stage_ms[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t timed_steps = 0;
     for (uint32_t k = 0; k < n_steps; ++k) {
         // Testbed::train: training_prep_nerf every clamp(step / 16, 1, 16) steps (testbed.cu:4081-4091)
         const uint32_t skip = std::min(16u, std::max(1u, t.step / 16u));
         if (t.step % skip == 0) train_density_update(c, s);
-        train_forward_backward(c, 0, s);
+        train_forward_backward(c, 0, s, timed ? c->train_events.data() : nullptr);
         // optimizer_step: Ema(ExponentialDecay(Adam)) (base.json)
         AdamArgs o{};
         const uint32_t decays = t.step >= 20000 ? (t.step - 20000) / 10000 + 1 : 0;
         o.lr = 1e-2f * std::pow(0.33f, (float)decays);
         o.beta1 = 0.9f; o.beta2 = 0.99f; o.epsilon = 1e-15f; o.l2_reg = 1e-6f; o.loss_scale = 128.0f; o.ema_decay = 0.95f; o.ema_step = t.step;
+        o.deb_old = 1.0f - std::pow(o.ema_decay, (float)o.ema_step);
+        o.deb_new = 1.0f - std::pow(o.ema_decay, (float)(o.ema_step + 1));
         launch_train_adam(o, c->n_params, 3072 + 7168, t.master.as<float>(), t.grads.as<float>(), t.m1.as<float>(), t.m2.as<float>(), t.steps.as<uint32_t>(),
                           t.ema.as<float>(), t.p_train.as<uint16_t>(), t.p_infer.as<uint16_t>(), s);
+        if (timed) HIPCHK(hipEventRecord(c->train_events[7], s));
         t.rng.advance();
         ++t.step;
         // NerfCounters::update_after_training (3272-3296): host readback of the two sample counts
         TrainCtrl h{};
         HIPCHK(hipMemcpyAsync(&h, t.ctrl.p, sizeof(TrainCtrl), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        if (timed) {
+            for (int q = 0; q < 7; ++q) {
+                float ms = 0.0f;
+                HIPCHK(hipEventElapsedTime(&ms, c->train_events[q], c->train_events[q + 1]));
+                stage_ms[q] += ms;
+            }
+            ++timed_steps;
+        }
         if (h.numsteps_counter == 0 || h.numsteps_compacted == 0) {
             t.measured = t.measured_before = 0;
         } else {
@@ -2072,6 +2100,9 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
         out->measured_batch = t.measured;
         out->measured_batch_before_compaction = t.measured_before;
         HIPCHK(hipEventElapsedTime(&out->ms, c->ev_start, c->ev_end));
+        out->timed_steps = timed_steps;
+        float* dst[7] = {&out->ms_generate, &out->ms_network, &out->ms_loss, &out->ms_grad_clear, &out->ms_field, &out->ms_dw, &out->ms_optimizer};
+        for (int q = 0; q < 7; ++q) *dst[q] = timed_steps ? (float)(stage_ms[q] / timed_steps) : 0.0f;
     }
 }
 
@@ -2163,6 +2194,7 @@ void ctx_destroy(sng_ctx* c) {
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); c->ray_kk[b].release(); }
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1, c->ev_alive, c->ev_brick}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->train_events) (void)hipEventDestroy(e);
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);
     (void)hipHostFree(c->h_os);

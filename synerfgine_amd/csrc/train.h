@@ -152,6 +152,7 @@ constexpr int TRAIN_FEATS = 480;
 struct AdamArgs {
     float lr, beta1, beta2, epsilon, l2_reg, loss_scale, ema_decay;
     uint32_t ema_step;
+    float deb_old, deb_new;   // 1 - ema_decay^ema_step, 1 - ema_decay^(ema_step + 1) (host powf, as the oracle)
 };
 
 void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, hipStream_t s);

@@ -561,34 +561,75 @@ __global__ __launch_bounds__(320) void train_dw_kernel(TrainStepArgs a, const ui
 // counts for the bias correction).  Writes the fp32 master, the fp16 training copy and the EMA
 // (debiased) fp16 inference copy.
 // ---------------------------------------------------------------------------------------------
-__global__ void train_adam_kernel(AdamArgs o, uint64_t n, uint32_t n_matrix, float* __restrict__ master, const float* __restrict__ grads,
-                                  float* __restrict__ m1, float* __restrict__ m2, uint32_t* __restrict__ steps, float* __restrict__ ema,
-                                  uint16_t* __restrict__ p_train, uint16_t* __restrict__ p_infer) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    float gradient = grads[i] / o.loss_scale;
-    const bool matrix = i < n_matrix;
-    float w = master[i];
-    if (!(matrix || gradient != 0.0f)) {
-        // untouched grid entry: weights unchanged, EMA still advances (tcnn EmaOptimizer steps every param)
-    } else {
-        const uint32_t step = ++steps[i];
+// One parameter's update; `deb_old` / `deb_new` are the EMA debias terms 1 - decay^t, 1 - decay^(t+1) (uniform over the
+// params: formed once per step on the host with the same powf the oracle uses)
+__device__ __forceinline__ void adam_one(const AdamArgs& o, bool matrix, float gsum, float& w, float& m1, float& m2, uint32_t& step, float& e, bool& touched) {
+    float gradient = gsum / o.loss_scale;
+    touched = matrix || gradient != 0.0f;
+    if (touched) {   // an untouched grid entry keeps its weight; the EMA still advances (tcnn EmaOptimizer steps every param)
+        step += 1;
         if (matrix) gradient += o.l2_reg * w;
         const float gsq = gradient * gradient;
-        const float fm = m1[i] = o.beta1 * m1[i] + (1.0f - o.beta1) * gradient;
-        const float sm = m2[i] = o.beta2 * m2[i] + (1.0f - o.beta2) * gsq;
+        m1 = o.beta1 * m1 + (1.0f - o.beta1) * gradient;
+        m2 = o.beta2 * m2 + (1.0f - o.beta2) * gsq;
         // tcnn adam_step: learning_rate *= sqrtf(1 - beta2^t) / (1 - beta1^t) (the quotient first)
         const float lr = o.lr * (sqrtf(1.0f - powf(o.beta2, (float)step)) / (1.0f - powf(o.beta1, (float)step)));
-        const float eff = lr / (sqrtf(sm) + o.epsilon);
-        w = w - eff * fm;
-        master[i] = w;
+        const float eff = lr / (sqrtf(m2) + o.epsilon);
+        w = w - eff * m1;
     }
-    p_train[i] = f2h(w);
-    // EMA with debiasing (tcnn EmaOptimizer)
-    const float deb_old = 1.0f - powf(o.ema_decay, (float)o.ema_step), deb_new = 1.0f - powf(o.ema_decay, (float)(o.ema_step + 1));
-    const float e = (ema[i] * o.ema_decay * deb_old + w * (1.0f - o.ema_decay)) / deb_new;
-    ema[i] = e;
-    p_infer[i] = f2h(e);
+    e = (e * o.ema_decay * o.deb_old + w * (1.0f - o.ema_decay)) / o.deb_new;   // EMA with debiasing (tcnn EmaOptimizer)
+}
+// Four consecutive params per thread with 16-B loads / stores (8-B for the fp16 copies); the first-moment / second-moment /
+// step arrays are read and written only for the groups that hold a touched param.  A group is all-matrix or all-grid
+// (n_matrix % 4 == 0); n % 4 != 0 leaves a scalar tail.
+__global__ __launch_bounds__(256) void train_adam_kernel(AdamArgs o, uint64_t n, uint32_t n_matrix, float* __restrict__ master,
+                                                         const float* __restrict__ grads, float* __restrict__ m1, float* __restrict__ m2,
+                                                         uint32_t* __restrict__ steps, float* __restrict__ ema, uint16_t* __restrict__ p_train,
+                                                         uint16_t* __restrict__ p_infer) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t i0 = q * 4;
+    if (i0 >= n) return;
+    if (i0 + 4 > n) {   // scalar tail
+        for (uint64_t i = i0; i < n; ++i) {
+            float w = master[i], a = m1[i], b = m2[i], e = ema[i];
+            uint32_t st = steps[i];
+            bool touched;
+            adam_one(o, i < n_matrix, grads[i], w, a, b, st, e, touched);
+            if (touched) { master[i] = w; m1[i] = a; m2[i] = b; steps[i] = st; }
+            ema[i] = e;
+            p_train[i] = f2h(w);
+            p_infer[i] = f2h(e);
+        }
+        return;
+    }
+    const bool matrix = i0 < n_matrix;
+    const float4 g = *reinterpret_cast<const float4*>(grads + i0);
+    float4 w = *reinterpret_cast<const float4*>(master + i0);
+    float4 e = *reinterpret_cast<const float4*>(ema + i0);
+    const bool any = matrix || g.x != 0.0f || g.y != 0.0f || g.z != 0.0f || g.w != 0.0f;
+    float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = a;
+    uint4 st = make_uint4(0u, 0u, 0u, 0u);
+    if (any) {
+        a = *reinterpret_cast<const float4*>(m1 + i0);
+        b = *reinterpret_cast<const float4*>(m2 + i0);
+        st = *reinterpret_cast<const uint4*>(steps + i0);
+    }
+    bool t0, t1, t2, t3;
+    adam_one(o, matrix, g.x, w.x, a.x, b.x, st.x, e.x, t0);
+    adam_one(o, matrix, g.y, w.y, a.y, b.y, st.y, e.y, t1);
+    adam_one(o, matrix, g.z, w.z, a.z, b.z, st.z, e.z, t2);
+    adam_one(o, matrix, g.w, w.w, a.w, b.w, st.w, e.w, t3);
+    if (any) {   // untouched params of the group carry their loaded values back unchanged
+        *reinterpret_cast<float4*>(master + i0) = w;
+        *reinterpret_cast<float4*>(m1 + i0) = a;
+        *reinterpret_cast<float4*>(m2 + i0) = b;
+        *reinterpret_cast<uint4*>(steps + i0) = st;
+    }
+    *reinterpret_cast<float4*>(ema + i0) = e;
+    const uint2 pt = make_uint2((uint32_t)f2h(w.x) | ((uint32_t)f2h(w.y) << 16), (uint32_t)f2h(w.z) | ((uint32_t)f2h(w.w) << 16));
+    const uint2 pi = make_uint2((uint32_t)f2h(e.x) | ((uint32_t)f2h(e.y) << 16), (uint32_t)f2h(e.z) | ((uint32_t)f2h(e.w) << 16));
+    *reinterpret_cast<uint2*>(p_train + i0) = pt;
+    *reinterpret_cast<uint2*>(p_infer + i0) = pi;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -715,7 +756,9 @@ void launch_train_dw(const TrainStepArgs& a, const uint16_t* acts, float* wgrad,
 }
 void launch_train_adam(const AdamArgs& o, uint64_t n, uint32_t n_matrix, float* master, const float* grads, float* m1, float* m2, uint32_t* steps, float* ema,
                        uint16_t* p_train, uint16_t* p_infer, hipStream_t s) {
-    hipLaunchKernelGGL(train_adam_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, o, n, n_matrix, master, grads, m1, m2, steps, ema, p_train, p_infer);
+    const uint64_t groups = (n + 3) / 4;   // every buffer is a hipMalloc allocation (16-B aligned); n_matrix % 4 == 0
+    hipLaunchKernelGGL(train_adam_kernel, dim3((uint32_t)((groups + 255) / 256)), dim3(256), 0, s, o, n, n_matrix, master, grads, m1, m2, steps, ema,
+                       p_train, p_infer);
 }
 void launch_train_mark_untrained(uint32_t n, float* grid, const TrainImages& im, int clear_visible, hipStream_t s) {
     hipLaunchKernelGGL(train_mark_untrained_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, grid, im, clear_visible);
