@@ -265,12 +265,15 @@ struct HostObject {
     std::vector<BvhNode> nodes;
     std::vector<BvhWide> wide;    // traversal layout of `nodes` (wide_bvh), empty if not representable
     int root_ref = 0;
+    std::vector<BvhQuad> quad;    // four-wide layout (quad_bvh), empty if not representable
+    int root_quad = 0;
+    uint32_t quad_stack = 0;      // stack entries its walk can hold at once (push-far-continue-near)
     m3 rot;
     f3 pos;
     float scale = 1.0f;
     int mat = 0;
     ObjAnim anim;
-    DevBuf d_nodes, d_tris, d_trit, d_wide;
+    DevBuf d_nodes, d_tris, d_trit, d_wide, d_quad;
 };
 
 // BvhWide records of the inner nodes of a TriangleBvhNode array (children at left, left + 1).
@@ -302,6 +305,59 @@ bool wide_bvh(const std::vector<BvhNode>& nodes, std::vector<BvhWide>& wide, int
     }
     root_ref = nodes.empty() ? 0 : ref_of(0);
     if (!ok) wide.clear();
+    return ok;
+}
+
+// BvhQuad records (sng_math.h) of a TriangleBvhNode array: one per binary inner node reachable as a quad child (the
+// root, and the inner grandchildren of every record), its children the binary grandchildren where a binary child is
+// inner, else that child itself.  stack_need: the most stack entries the quad walk holds at once -- along a root-to-leaf
+// path every record pushes its other (children - 1) entries before descending.  Returns false when a leaf range does
+// not fit the BvhWide encoding.
+bool quad_bvh(const std::vector<BvhNode>& nodes, std::vector<BvhQuad>& quad, int& root_ref, uint32_t& stack_need) {
+    quad.clear();
+    stack_need = 0;
+    if (nodes.empty()) { root_ref = 0; return true; }
+    bool ok = true;
+    auto leaf_ref = [&](const BvhNode& n) -> int {
+        const int b = -n.left - 1, e = -n.right - 1;
+        if (b < 0 || e < b || (uint32_t)b >= WIDE_MAX_BEGIN || (uint32_t)(e - b) > WIDE_MAX_COUNT) { ok = false; return 0; }
+        if (((uint32_t)b | ((uint32_t)(e - b) << 24)) == 0x7FFFFFFFu) { ok = false; return 0; }
+        return (int)~((uint32_t)b | ((uint32_t)(e - b) << 24));
+    };
+    // build recursively: returns the ref of binary node i and its stack need
+    std::function<int(int, uint32_t&)> build = [&](int i, uint32_t& need) -> int {
+        const BvhNode& n = nodes[i];
+        if (n.left < 0) { need = 0; return leaf_ref(n); }
+        if ((size_t)n.left + 1 >= nodes.size()) { ok = false; need = 0; return 0; }
+        std::vector<int> kids;
+        for (int c = n.left; c <= n.left + 1; ++c) {
+            const BvhNode& cn = nodes[c];
+            if (cn.left >= 0 && (size_t)cn.left + 1 < nodes.size()) { kids.push_back(cn.left); kids.push_back(cn.left + 1); }
+            else kids.push_back(c);
+        }
+        const int id = (int)quad.size();
+        quad.push_back(BvhQuad{});
+        uint32_t sub = 0;
+        int refs[4] = {WIDE_DONE, WIDE_DONE, WIDE_DONE, WIDE_DONE};
+        float box[6][4];
+        for (int k = 0; k < 4; ++k) { box[0][k] = box[2][k] = box[4][k] = 0.0f; box[1][k] = box[3][k] = box[5][k] = 0.0f; }
+        for (size_t k = 0; k < kids.size(); ++k) {
+            const BvhNode& cn = nodes[kids[k]];
+            for (int a = 0; a < 3; ++a) { box[2 * a][k] = cn.lo[a]; box[2 * a + 1][k] = cn.hi[a]; }
+            uint32_t nk = 0;
+            refs[k] = build(kids[k], nk);
+            sub = std::max(sub, nk);
+        }
+        BvhQuad& q = quad[id];   // (quad may have grown)
+        for (int k = 0; k < 4; ++k) {
+            q.lox[k] = box[0][k]; q.hix[k] = box[1][k]; q.loy[k] = box[2][k]; q.hiy[k] = box[3][k]; q.loz[k] = box[4][k]; q.hiz[k] = box[5][k];
+            q.ref[k] = refs[k];
+        }
+        need = (uint32_t)kids.size() - 1u + sub;
+        return id;
+    };
+    root_ref = build(0, stack_need);
+    if (!ok) quad.clear();
     return ok;
 }
 
@@ -344,6 +400,7 @@ const std::map<std::string, double>& default_params() {
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
+        {"bvh_quad", 1},                        // four-wide BvhQuad records and walk (exact: the same closest hit)
         {"bvh_flat", 1},                        // BvhWide walk keeping the nearer child in a register (exact)
         {"rt_tile", 8},                         // path-kernel tile width: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
         {"rt_tile_h", 0},                       // path-kernel tile height: 0 = rt_tile; 4 with rt_tile 8: 8x4 (32 lanes per wave)
@@ -522,6 +579,7 @@ struct sng_ctx {
         int w = 0, h = 0, n_images = 0;
         DevBuf pixels, xforms, xforms_ray, focal, pp;
         DevBuf lens;                                   // [n_images] Lens (sng_train_set_lens); h_lens empty: all Perspective
+        DevBuf tscr;                                   // generate's sample distances [NERF_STEPS][rays_per_batch]
         std::vector<Lens> h_lens;
         DevBuf master, grads, m1, m2, steps, ema, p_train, p_infer, wfrag_train, wfrag_t;
         DevBuf grid, grid_tmp, grid_coords, grid_idx, grid_out;
@@ -538,6 +596,7 @@ struct sng_ctx {
     DevBuf d_objs, d_lights, d_mats;
     DevBuf d_scene_blob;          // every object's nodes + triangles (traversal kernels copy it to LDS)
     uint32_t scene_f4 = 0, bvh_depth = 0;
+    uint32_t bvh_stack = 0;       // stack entries per lane the scene's walks need (depth + 2, or the quad walk's need + 1)
     bool scene_dirty = true;
 
     double p(const char* k) const { return params.at(k); }
@@ -748,6 +807,7 @@ void upload_scene(sng_ctx* c) {
         return (uint32_t)off;
     };
     c->bvh_depth = 0;
+    c->bvh_stack = 0;
     for (auto& o : c->objs) {
         upload(o.d_nodes, o.nodes.data(), o.nodes.size() * sizeof(BvhNode));
         upload(o.d_tris, o.tris.data(), o.tris.size() * sizeof(Tri));
@@ -770,7 +830,19 @@ void upload_scene(sng_ctx* c) {
             for (int k = 0; k < 3; ++k) max_coord = std::max(max_coord, std::max(std::fabs(n.lo[k]), std::fabs(n.hi[k])));
         g.fast_slab = (c->p("fast_slab") != 0.0 && max_coord < SLAB_FAST_MAX_COORD) ? 1 : 0;
         const bool wide = c->p("bvh_wide") != 0.0 && wide_bvh(o.nodes, o.wide, o.root_ref);
-        if (wide) {
+        const bool quad = wide && c->p("bvh_quad") != 0.0 && quad_bvh(o.nodes, o.quad, o.root_quad, o.quad_stack);
+        if (quad) {   // the four-wide walk needs only its own records in the blob
+            upload(o.d_quad, o.quad.data(), std::max<size_t>(1, o.quad.size()) * sizeof(BvhQuad));
+            g.quad = o.d_quad.as<BvhQuad>();
+            g.lds_quad = append(o.quad.data(), o.quad.size() * sizeof(BvhQuad));
+            g.root_quad = o.root_quad;
+            upload(o.d_wide, o.wide.data(), std::max<size_t>(1, o.wide.size()) * sizeof(BvhWide));
+            g.wide = o.d_wide.as<BvhWide>();
+            g.lds_wide = 0;
+            g.root_ref = o.root_ref;
+            g.lds_nodes = 0;
+            c->bvh_stack = std::max(c->bvh_stack, o.quad_stack + 1u);
+        } else if (wide) {
             upload(o.d_wide, o.wide.data(), std::max<size_t>(1, o.wide.size()) * sizeof(BvhWide));
             g.wide = o.d_wide.as<BvhWide>();
             g.lds_wide = append(o.wide.data(), o.wide.size() * sizeof(BvhWide));
@@ -781,6 +853,7 @@ void upload_scene(sng_ctx* c) {
         }
         g.lds_trit = append(trit.data(), trit.size() * sizeof(TriT));
         c->bvh_depth = std::max(c->bvh_depth, bvh_depth(o.nodes));
+        c->bvh_stack = std::max(c->bvh_stack, c->bvh_depth + 2u);
         og.push_back(g);
     }
     upload(c->d_objs, og.data(), og.size() * sizeof(ObjectGpu));
@@ -809,7 +882,7 @@ int n_point_lights(const sng_ctx* c) {
 void shadow_scene(sng_ctx* c, ShadowArgs& sa) {
     sa.scene_blob = c->d_scene_blob.as<float4>();
     sa.scene_f4 = c->scene_f4;
-    sa.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
+    sa.stack_depth = std::min<uint32_t>(32u, c->bvh_stack);
     sa.bvh_flat = c->p("bvh_flat") != 0.0 ? 1 : 0;
     const uint64_t blob_b = (uint64_t)c->scene_f4 * 16;
     const bool lds_ok = c->p("scene_lds") != 0.0 && sa.scene_blob != nullptr;
@@ -1698,7 +1771,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
             ra.scene_blob = c->d_scene_blob.as<float4>();
             ra.scene_f4 = c->scene_f4;
             // max stack use of the reference traversal is depth + 1; FixedStack<32> drops pushes at 31
-            ra.stack_depth = std::min<uint32_t>(32u, c->bvh_depth + 2u);
+            ra.stack_depth = std::min<uint32_t>(32u, c->bvh_stack);
             ra.bvh_flat = c->p("bvh_flat") != 0.0 ? 1 : 0;
             // blob + stacks in LDS: two 512-thread workgroups per CU (80 KB each), else one of 1024 threads
             // (one blob copy per CU, 160 KB); both give 16 waves per CU
@@ -2005,7 +2078,8 @@ void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev
     HIPCHK(hipMemsetAsync(t.loss.p, 0, (size_t)a.n_rays * 4, s));
     auto mark = [&](int k) { if (ev) HIPCHK(hipEventRecord(ev[k], s)); };
     mark(0);
-    launch_train_generate(a, im, b, t.rng, s);
+    t.tscr.ensure((size_t)a.n_rays * NERF_STEPS * 4);
+    launch_train_generate(a, im, b, t.rng, t.tscr.as<float>(), s);
     mark(1);
     if (stage == 1) return;
     // inference forward of every sample with the training params
@@ -2792,7 +2866,7 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
             throw SngError(SNG_ERR_INVALID, "tonemap_curve is an ETonemapCurve: 0 Identity, 1 ACES, 2 Hable, 3 Reinhard");
         c->params[k] = v;
         c->mesh_reset = true;
-        if ((k == "fast_slab" || k == "scene_lds" || k == "bvh_wide") && !c->objs.empty()) upload_scene(c);
+        if ((k == "fast_slab" || k == "scene_lds" || k == "bvh_wide" || k == "bvh_quad") && !c->objs.empty()) upload_scene(c);
     });
 }
 int sng_get_param(sng_ctx* c, const char* key, double* v) {

@@ -60,6 +60,10 @@ struct TraceCtx {
         if constexpr (LDS) return reinterpret_cast<const BvhWide*>(scene + o.lds_wide);
         else return o.wide;
     }
+    __device__ __forceinline__ const BvhQuad* quad(const ObjectGpu& o) const {
+        if constexpr (LDS) return reinterpret_cast<const BvhQuad*>(scene + o.lds_quad);
+        else return o.quad;
+    }
     __device__ __forceinline__ const TriT* tris(const ObjectGpu& o) const {
         if constexpr (LDS) return reinterpret_cast<const TriT*>(scene + o.lds_trit);
         else return o.trit;
@@ -261,6 +265,74 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
     return mint;
 }
 
+// The four-wide walk over BvhQuad records (capi.cpp quad_bvh): one record visit tests up to four boxes -- the binary
+// walk's boxes of two consecutive levels -- with the same slab arithmetic (slab_entry_fast / bvh_box_entry per box),
+// sorts them by entry distance, continues with the nearest whose entry is below mint and pushes the other surviving
+// ones far-first (push far, continue near), so it pops them nearest-first.  Leaves run the same triangle test with
+// the strict `t < mint` update.  The result is the minimum t over the triangles whose boxes the culling keeps, the
+// binary walk's closest hit; only the order of the visits differs (a tie in t between two triangles could then pick
+// the other one: tests/test_gpu_parity.py checks whole frames bit for bit against the TriangleBvhNode walk).
+template <bool FAST>
+__device__ __forceinline__ float bvh_walk_quad(f3 ro, f3 rd, f3 y, const BvhQuad* __restrict__ quad, const TriT* __restrict__ tris, int root_ref,
+                                               int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr, bool cw = false) {
+    const float FMAX = 3.402823466e+38f;
+    PStack st{(lds_int*)stack_lds, (lds_int*)stack_lds, stride};
+    float mint = t_max;
+    int shortest = -1;
+    int cur = root_ref;
+    while (true) {
+        while (cur >= 0) {
+            const float4* r = reinterpret_cast<const float4*>(quad + cur);
+            const float4 lx = r[0], hx = r[1], ly = r[2], hy = r[3], lz = r[4], hz = r[5];
+            const int4 rf = *reinterpret_cast<const int4*>(r + 6);
+            float d[4];
+            int f[4] = {rf.x, rf.y, rf.z, rf.w};
+            const float lxa[4] = {lx.x, lx.y, lx.z, lx.w}, hxa[4] = {hx.x, hx.y, hx.z, hx.w};
+            const float lya[4] = {ly.x, ly.y, ly.z, ly.w}, hya[4] = {hy.x, hy.y, hy.z, hy.w};
+            const float lza[4] = {lz.x, lz.y, lz.z, lz.w}, hza[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float e;
+                if constexpr (FAST) e = slab_entry_fast(pf2{lxa[k], hxa[k]}, pf2{lya[k], hya[k]}, pf2{lza[k], hza[k]}, ro, y);
+                else e = bvh_box_entry(aabb{mk(lxa[k], lya[k], lza[k]), mk(hxa[k], hya[k], hza[k])}, ro, y);
+                d[k] = f[k] == WIDE_DONE ? FMAX : e;
+            }
+            if (cnt) cnt[1] += cw ? (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id())
+                                  : (uint32_t)((f[0] != WIDE_DONE) + (f[1] != WIDE_DONE) + (f[2] != WIDE_DONE) + (f[3] != WIDE_DONE));
+            // sorting network (0,1) (2,3) (0,2) (1,3) (1,2): ascending entry distance
+            auto cas = [&](int i, int j) {
+                const bool sw = d[j] < d[i];
+                const float di = d[i], dj = d[j];
+                const int fi = f[i], fj = f[j];
+                d[i] = sw ? dj : di; d[j] = sw ? di : dj;
+                f[i] = sw ? fj : fi; f[j] = sw ? fi : fj;
+            };
+            cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
+            if (!(d[0] < mint)) {   // nothing in this record survives: next stack entry
+                cur = st.empty() ? WIDE_DONE : st.pop();
+                continue;
+            }
+            if (d[3] < mint) st.push(f[3]);
+            if (d[2] < mint) st.push(f[2]);
+            if (d[1] < mint) st.push(f[1]);
+            cur = f[0];
+        }
+        if (cur == WIDE_DONE) break;
+        const uint32_t e = ~(uint32_t)cur;
+        const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
+        if (cnt && !cw) cnt[2] += (uint32_t)(end - b);
+        for (int i = b; i < end; ++i) {
+            if (cnt && cw) cnt[2] += (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id());
+            float t;
+            if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
+        }
+        if (st.empty()) break;
+        cur = st.pop();
+    }
+    tri_out = shortest;
+    return mint;
+}
+
 // t_max < MAX_DEPTH culls everything at or beyond t_max (the result is then min(closest, t_max));
 // only the shadow kernel uses it, where any value >= full_dist yields the same mask.
 template <bool LDS, bool CNT = false>
@@ -269,6 +341,10 @@ __device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu&
     const f3 ord = mul(o.world_to_obj, rd);
     const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
     const f3 y = inv(ord);
+    if (o.quad) {
+        if (fast) return bvh_walk_quad<true>(oro, ord, y, cx.quad(o), cx.tris(o), o.root_quad, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
+        return bvh_walk_quad<false>(oro, ord, y, cx.quad(o), cx.tris(o), o.root_quad, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
+    }
     if (o.wide && cx.flat) {
         if (fast) return bvh_walk_near<true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
         return bvh_walk_near<false>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);

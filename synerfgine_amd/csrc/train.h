@@ -156,7 +156,8 @@ struct AdamArgs {
 };
 
 void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, hipStream_t s);
-void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, hipStream_t s);
+// tscr: [NERF_STEPS][n_rays] floats of scratch (the first march's sample distances)
+void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, float* tscr, hipStream_t s);
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s);
 void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s);
 void launch_train_field(const TrainStepArgs& a, const TrainBatch& b, const NetworkDev& net, const uint16_t* wfrag, const uint16_t* wfrag_t,

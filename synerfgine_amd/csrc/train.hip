@@ -32,7 +32,16 @@ __device__ __forceinline__ f4v mfma16k16(h4v a, h4v b, f4v c) { return __builtin
 // generate_training_samples_nerf (testbed_nerf.cu:838-998), no error-map CDFs, no distortion map,
 // no envmap, max_level_rand_training off; the dataset lens per image (train_ray)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void train_generate_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng) {
+// One march per ray (the reference marches twice: once to count, once to write).  The sample distances of the first
+// march go to tscr (sample-major [j][ray], so a wave's stores of one step are contiguous); once the ray's range of the
+// batch is reserved, its NerfCoordinates are formed from them with the same expressions (pos = o + t dn, dt =
+// calc_dt(t)), so the samples are the reference's bit for bit.  BRICK (unit-cube scenes): the occupancy lookups read
+// the mip-0 bricks staged in LDS (occupied_brick_nb, the render marchers' exact form) instead of global memory.
+// One 64-lane workgroup per 64 rays: a batch has only ~4K rays, so small workgroups spread them over the CUs.
+template <bool BRICK>
+__global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, float* __restrict__ tscr) {
+    extern __shared__ uint32_t occ_lds[];
+    if constexpr (BRICK) stage_occ_brick(occ_lds, a.vol.occ_brick, a.vol.occ_brick_words);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n_rays) return;
     const uint32_t img = ((i * im.n) / a.n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
@@ -52,13 +61,16 @@ __global__ __launch_bounds__(256) void train_generate_kernel(TrainStepArgs a, Tr
     f3 pos;
     // unit-cube scenes (cone 0, one cascade): the exact linear specialisation of the occupancy test and
     // of advance_to_next_voxel that the render marcher uses (sng_math.h, tests/test_host_fastpaths.py)
-    const bool lin = a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_linear != nullptr;
+    const bool lin = BRICK || (a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_linear != nullptr);
     const f3 hs = half_sign(dn);
+    float* const ts = tscr + i;
     while (aabb_contains(box, pos = ray.o + t * dn) && j < NERF_STEPS) {
         const float dt = calc_dt(t, cone);
-        const uint32_t mip = mip_from_dt(dt, pos, a.vol.max_mip);
-        if (lin ? occupied_linear(pos, a.vol.occ_linear) : occupied_at(pos, a.vol.bitfield, mip)) { ++j; t += dt; }
-        else t = lin ? dda_step_linear(t, pos, idir, hs) : advance_to_next_voxel(t, cone, pos, dn, idir, mip);
+        bool occ;
+        if constexpr (BRICK) occ = occupied_brick_nb(pos, occ_lds);
+        else occ = lin ? occupied_linear(pos, a.vol.occ_linear) : occupied_at(pos, a.vol.bitfield, mip_from_dt(dt, pos, a.vol.max_mip));
+        if (occ) { ts[(size_t)j * a.n_rays] = t; ++j; t += dt; }
+        else t = lin ? dda_step_linear(t, pos, idir, hs) : advance_to_next_voxel(t, cone, pos, dn, idir, mip_from_dt(dt, pos, a.vol.max_mip));
     }
     if (a.debug) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
     if (j == 0) return;
@@ -72,21 +84,13 @@ __global__ __launch_bounds__(256) void train_generate_kernel(TrainStepArgs a, Tr
     b.numsteps[ray_idx] = make_uint2(numsteps, base);
     const f3 wd = (dn + 1.0f) * 0.5f;   // warp_direction
     const f3 diag = box.hi - box.lo;
-    t = startt;
-    j = 0;
     float* co = b.coords + (size_t)base * 7;
-    while (aabb_contains(box, pos = ray.o + t * dn) && j < numsteps) {
-        const float dt = calc_dt(t, cone);
-        const uint32_t mip = mip_from_dt(dt, pos, a.vol.max_mip);
-        if (lin ? occupied_linear(pos, a.vol.occ_linear) : occupied_at(pos, a.vol.bitfield, mip)) {
-            const f3 wp = (pos - box.lo) / diag;   // warp_position = aabb.relative_pos
-            float* c = co + (size_t)j * 7;
-            c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(dt); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
-            ++j;
-            t += dt;
-        } else {
-            t = lin ? dda_step_linear(t, pos, idir, hs) : advance_to_next_voxel(t, cone, pos, dn, idir, mip);
-        }
+    for (uint32_t k = 0; k < numsteps; ++k) {
+        const float tk = ts[(size_t)k * a.n_rays];
+        const f3 p = ray.o + tk * dn;
+        const f3 wp = (p - box.lo) / diag;   // warp_position = aabb.relative_pos
+        float* c = co + (size_t)k * 7;
+        c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(calc_dt(tk, cone)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
     }
 }
 
@@ -725,8 +729,12 @@ __global__ void train_clamp_count_kernel(const uint32_t* __restrict__ in, uint32
 void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, hipStream_t s) {
     hipLaunchKernelGGL(train_clamp_count_kernel, dim3(1), dim3(64), 0, s, in, cap, out);
 }
-void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, hipStream_t s) {
-    hipLaunchKernelGGL(train_generate_kernel, dim3((a.n_rays + 255) / 256), dim3(256), 0, s, a, im, b, rng);
+void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, float* tscr, hipStream_t s) {
+    const dim3 grid((a.n_rays + 63) / 64);
+    if (a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_brick_words && a.vol.occ_brick_words * 4u <= 64u * 1024u)
+        hipLaunchKernelGGL(train_generate_kernel<true>, grid, dim3(64), a.vol.occ_brick_words * 4, s, a, im, b, rng, tscr);
+    else
+        hipLaunchKernelGGL(train_generate_kernel<false>, grid, dim3(64), 0, s, a, im, b, rng, tscr);
 }
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
     (void)hipMemsetAsync(b.rayrec, 0, (size_t)a.n_rays * 48, s);
