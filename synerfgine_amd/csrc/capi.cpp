@@ -400,7 +400,7 @@ const std::map<std::string, double>& default_params() {
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
-        {"bvh_quad", 1},                        // four-wide BvhQuad records and walk (exact: the same closest hit)
+        {"bvh_quad", 1},                        // four-wide BvhQuad records and walk in the shadow kernels (exact: the same closest hit)
         {"bvh_flat", 1},                        // BvhWide walk keeping the nearer child in a register (exact)
         {"rt_tile", 8},                         // path-kernel tile width: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
         {"rt_tile_h", 0},                       // path-kernel tile height: 0 = rt_tile; 4 with rt_tile 8: 8x4 (32 lanes per wave)
@@ -831,18 +831,14 @@ void upload_scene(sng_ctx* c) {
         g.fast_slab = (c->p("fast_slab") != 0.0 && max_coord < SLAB_FAST_MAX_COORD) ? 1 : 0;
         const bool wide = c->p("bvh_wide") != 0.0 && wide_bvh(o.nodes, o.wide, o.root_ref);
         const bool quad = wide && c->p("bvh_quad") != 0.0 && quad_bvh(o.nodes, o.quad, o.root_quad, o.quad_stack);
-        if (quad) {   // the four-wide walk needs only its own records in the blob
+        if (quad) {   // the shadow kernels' four-wide walk; the path kernel walks the BvhWide records (both in the blob)
             upload(o.d_quad, o.quad.data(), std::max<size_t>(1, o.quad.size()) * sizeof(BvhQuad));
             g.quad = o.d_quad.as<BvhQuad>();
             g.lds_quad = append(o.quad.data(), o.quad.size() * sizeof(BvhQuad));
             g.root_quad = o.root_quad;
-            upload(o.d_wide, o.wide.data(), std::max<size_t>(1, o.wide.size()) * sizeof(BvhWide));
-            g.wide = o.d_wide.as<BvhWide>();
-            g.lds_wide = 0;
-            g.root_ref = o.root_ref;
-            g.lds_nodes = 0;
             c->bvh_stack = std::max(c->bvh_stack, o.quad_stack + 1u);
-        } else if (wide) {
+        }
+        if (wide) {
             upload(o.d_wide, o.wide.data(), std::max<size_t>(1, o.wide.size()) * sizeof(BvhWide));
             g.wide = o.d_wide.as<BvhWide>();
             g.lds_wide = append(o.wide.data(), o.wide.size() * sizeof(BvhWide));

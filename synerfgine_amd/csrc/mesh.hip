@@ -44,7 +44,9 @@ struct PStack {
 // FixedStack<32> overflow rule can never trigger differently).
 // CNT = true (bench's counting frames only, sng_rt_counters): cnt -> this thread's {world queries,
 // box tests, triangle tests}; the timed kernels are the CNT = false instantiations (no counting code).
-template <bool LDS, bool CNT = false>
+// QUAD = true (the shadow kernels): objects with BvhQuad records take the four-wide walk; the path kernel keeps the
+// binary near-walk (it has no registers to spare: the four-wide walk made it spill, round 5)
+template <bool LDS, bool CNT = false, bool QUAD = false>
 struct TraceCtx {
     int* stack;            // this thread's first stack slot
     int stride;
@@ -283,19 +285,39 @@ __device__ __forceinline__ float bvh_walk_quad(f3 ro, f3 rd, f3 y, const BvhQuad
     while (true) {
         while (cur >= 0) {
             const float4* r = reinterpret_cast<const float4*>(quad + cur);
-            const float4 lx = r[0], hx = r[1], ly = r[2], hy = r[3], lz = r[4], hz = r[5];
             const int4 rf = *reinterpret_cast<const int4*>(r + 6);
             float d[4];
             int f[4] = {rf.x, rf.y, rf.z, rf.w};
-            const float lxa[4] = {lx.x, lx.y, lx.z, lx.w}, hxa[4] = {hx.x, hx.y, hx.z, hx.w};
-            const float lya[4] = {ly.x, ly.y, ly.z, ly.w}, hya[4] = {hy.x, hy.y, hy.z, hy.w};
-            const float lza[4] = {lz.x, lz.y, lz.z, lz.w}, hza[4] = {hz.x, hz.y, hz.z, hz.w};
+            if constexpr (FAST) {
+                // slab_entry_fast of the four boxes, one axis at a time (the same quotients and min / max, which do not
+                // round, so the order of the axes' combination cannot change a bit): 8 running values instead of the
+                // whole record live at once
+                float tn[4], tx[4];
+                auto axis = [&](const float4 lo4, const float4 hi4, float o, float yy, bool first) {
+                    const float lo[4] = {lo4.x, lo4.y, lo4.z, lo4.w}, hi[4] = {hi4.x, hi4.y, hi4.z, hi4.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float e;
-                if constexpr (FAST) e = slab_entry_fast(pf2{lxa[k], hxa[k]}, pf2{lya[k], hya[k]}, pf2{lza[k], hza[k]}, ro, y);
-                else e = bvh_box_entry(aabb{mk(lxa[k], lya[k], lza[k]), mk(hxa[k], hya[k], hza[k])}, ro, y);
-                d[k] = f[k] == WIDE_DONE ? FMAX : e;
+                    for (int k = 0; k < 4; ++k) {
+                        const pf2 tt = (pf2{lo[k], hi[k]} - o) * yy;
+                        const float mn = fminf(tt.x, tt.y), mx = fmaxf(tt.x, tt.y);
+                        tn[k] = first ? mn : fmaxf(tn[k], mn);
+                        tx[k] = first ? mx : fminf(tx[k], mx);
+                    }
+                };
+                axis(r[0], r[1], ro.x, y.x, true);
+                axis(r[2], r[3], ro.y, y.y, false);
+                axis(r[4], r[5], ro.z, y.z, false);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) d[k] = (f[k] == WIDE_DONE || tn[k] > tx[k]) ? FMAX : tn[k];
+            } else {
+                const float4 lx = r[0], hx = r[1], ly = r[2], hy = r[3], lz = r[4], hz = r[5];
+                const float lxa[4] = {lx.x, lx.y, lx.z, lx.w}, hxa[4] = {hx.x, hx.y, hx.z, hx.w};
+                const float lya[4] = {ly.x, ly.y, ly.z, ly.w}, hya[4] = {hy.x, hy.y, hy.z, hy.w};
+                const float lza[4] = {lz.x, lz.y, lz.z, lz.w}, hza[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float e = bvh_box_entry(aabb{mk(lxa[k], lya[k], lza[k]), mk(hxa[k], hya[k], hza[k])}, ro, y);
+                    d[k] = f[k] == WIDE_DONE ? FMAX : e;
+                }
             }
             if (cnt) cnt[1] += cw ? (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id())
                                   : (uint32_t)((f[0] != WIDE_DONE) + (f[1] != WIDE_DONE) + (f[2] != WIDE_DONE) + (f[3] != WIDE_DONE));
@@ -335,13 +357,13 @@ __device__ __forceinline__ float bvh_walk_quad(f3 ro, f3 rd, f3 y, const BvhQuad
 
 // t_max < MAX_DEPTH culls everything at or beyond t_max (the result is then min(closest, t_max));
 // only the shadow kernel uses it, where any value >= full_dist yields the same mask.
-template <bool LDS, bool CNT = false>
-__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, const TraceCtx<LDS, CNT>& cx, int& tri, float t_max = MAX_DEPTH) {
+template <bool LDS, bool CNT = false, bool QUAD = false>
+__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, const TraceCtx<LDS, CNT, QUAD>& cx, int& tri, float t_max = MAX_DEPTH) {
     const f3 oro = mul(o.world_to_obj, ro - o.pos);
     const f3 ord = mul(o.world_to_obj, rd);
     const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
     const f3 y = inv(ord);
-    if (o.quad) {
+    if (QUAD && o.quad) {
         if (fast) return bvh_walk_quad<true>(oro, ord, y, cx.quad(o), cx.tris(o), o.root_quad, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
         return bvh_walk_quad<false>(oro, ord, y, cx.quad(o), cx.tris(o), o.root_quad, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
     }
@@ -358,8 +380,8 @@ __device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu&
 }
 
 // sng::depth_test_world (common.cu:36-48)
-template <bool LDS, bool CNT = false>
-__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, int& out_obj,
+template <bool LDS, bool CNT = false, bool QUAD = false>
+__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT, QUAD>& cx, int& out_obj,
                                   float t_max = MAX_DEPTH) {
     float depth = MAX_DEPTH;
     const f3 off = origin + dir * MIN_DEPTH;
@@ -380,8 +402,8 @@ struct Hit {
 };
 __device__ __forceinline__ f3 tri_normal(const Tri& t) { return normalize(cross(t.b - t.a, t.c - t.a)); }
 // sng::depth_test_world(+HitRecord) (common.cu:50-67)
-template <bool LDS, bool CNT = false>
-__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, Hit& h) {
+template <bool LDS, bool CNT = false, bool QUAD = false>
+__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT, QUAD>& cx, Hit& h) {
     const f3 off = origin + dir * MIN_DEPTH;
     if constexpr (CNT) cx.cnt[0] += 1u;
     // only the winner's (object, triangle, t) stay live across the objects' traversals; its record is formed once
@@ -501,8 +523,8 @@ __device__ __forceinline__ void xorwow_skip(Xorwow& r, uint32_t n) {
 // One neighbour's term of shade_with_shadow: shadow_for_px at (pos, nrm); the k-th point light's sample
 // (Light::sample, 3 draws from the pixel's XORWOW state) is lp[k * lp_stride], drawn beforehand in the
 // reference's order by shadow_draw_kernel.
-template <bool LDS>
-__device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx<LDS>& cx, f3 pos, f3 nrm, const float4* __restrict__ lp,
+template <bool LDS, bool QUAD = false>
+__device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx<LDS, false, QUAD>& cx, f3 pos, f3 nrm, const float4* __restrict__ lp,
                                              size_t lp_stride) {
     float overall = 1.0f;
     int k = 0;
@@ -595,7 +617,7 @@ __global__ __launch_bounds__(1024) void shadow_term_kernel(ShadowArgs a, uint32_
         __syncthreads();
     }
     int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
-    const TraceCtx<LDS> cx{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat};
+    const TraceCtx<LDS, false, true> cx{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat};
     const int lane = threadIdx.x & 63;
     const uint32_t slots = (uint32_t)((2 * a.radius + 1) * (2 * a.radius + 1));
     const uint32_t cps = (n + 63u) / 64u, n_chunks = slots * cps;
@@ -689,15 +711,15 @@ __device__ __forceinline__ f3 cone_random_frame(f3 orig, const m3& frame, float 
 //                colour sums in the original order.  Bit-identical to DEFER = false.
 // Dynamic LDS of the traversal kernels: [scene blob (LDS = true)][stack: stack_depth x blockDim ints].
 // Workgroups are persistent (grid-stride), so each copies the scene blob once.
-template <bool LDS, bool CNT = false>
-__device__ __forceinline__ TraceCtx<LDS, CNT> trace_ctx_setup(const RaytraceArgs& a, uint32_t* cnt = nullptr) {
+template <bool LDS, bool CNT = false, bool QUAD = false>
+__device__ __forceinline__ TraceCtx<LDS, CNT, QUAD> trace_ctx_setup(const RaytraceArgs& a, uint32_t* cnt = nullptr) {
     extern __shared__ float4 smem4[];
     if constexpr (LDS) {
         for (uint32_t k = threadIdx.x; k < a.scene_f4; k += blockDim.x) smem4[k] = a.scene_blob[k];
         __syncthreads();
     }
     int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
-    return TraceCtx<LDS, CNT>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt, a.count_waves};
+    return TraceCtx<LDS, CNT, QUAD>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt, a.count_waves};
 }
 
 // shade_object's light loop of one hit (raytracer.cu:16-50) in deferred form: per (light, shadow
@@ -913,8 +935,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
 // depend on its cap syn + 1 >= full_dist), so the result is bit-identical.
-template <bool LDS, bool CNT = false>
-__device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t kr, uint32_t jp) {
+template <bool LDS, bool CNT = false, bool QUAD = false>
+__device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT, QUAD>& cx, uint32_t kr, uint32_t jp) {
     const float4 s1 = *q.shadow_ray(kr, jp);
     const float4* rk = q.rec + (size_t)kr * q.rec_stride;   // the origin: the record's hit position (header)
     const float4 h0 = rk[0], h1 = rk[1];
@@ -933,7 +955,7 @@ __device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const R
 template <bool LDS, bool CNT = false>
 __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work) {
     uint32_t counts[3] = {0u, 0u, 0u};
-    const TraceCtx<LDS, CNT> cx = trace_ctx_setup<LDS, CNT>(a, counts);
+    const TraceCtx<LDS, CNT, true> cx = trace_ctx_setup<LDS, CNT, true>(a, counts);
     const uint32_t n_rec = *q.count, total = n_rec * q.nps;
     const int lane = threadIdx.x & 63;
     // 64-ray chunks handed out by SHADOW_NCTR counters in separate memory channels: chunk c belongs to
