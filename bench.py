@@ -314,9 +314,7 @@ def train_leg(steps=200, warmup=50, seed=1337):
         tb.set_nerf_model(cfg, params)
         tb.set_training_dataset(imgs[train], xf[train], focal[train], pp[train])
         tb.train_reset(seed)
-        tb.train(warmup)
-        import torch
-        torch.cuda.synchronize()
+        tb.train(warmup)   # sng_train returns after its stream has finished (one host sync per step)
         t0 = time.perf_counter()
         st = tb.train(steps)
         el = time.perf_counter() - t0

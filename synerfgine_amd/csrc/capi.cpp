@@ -400,7 +400,9 @@ const std::map<std::string, double>& default_params() {
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
-        {"bvh_quad", 1},                        // four-wide BvhQuad records and walk in the shadow kernels (exact: the same closest hit)
+        {"bvh_quad", 0},                        // 1: four-wide BvhQuad records and walk in the shadow kernels (exact: the same closest hit);
+                                                //   measured no faster (round 5: shadow rays 1.247 vs 1.251 ms, C3 A/B 295-298 vs 294-295
+                                                //   frames/s; in the path kernel too it lost 2 % to spills), so off -- DESIGN.md §3
         {"bvh_flat", 1},                        // BvhWide walk keeping the nearer child in a register (exact)
         {"rt_tile", 8},                         // path-kernel tile width: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
         {"rt_tile_h", 0},                       // path-kernel tile height: 0 = rt_tile; 4 with rt_tile 8: 8x4 (32 lanes per wave)
