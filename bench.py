@@ -293,7 +293,7 @@ def abm_sweep(model, frames, warmup):
         tb.close()
 
 
-def train_leg(steps=200, warmup=50, seed=1337):
+def train_leg(steps=200, warmup=50, seed=1337, engine_params=None):
     """BASELINE config C5: online training on the reference's lego set (data/nerf/lego400, 95
     views, every 20th held out as tools/train_lego.py does) from a fresh init, batch 2^18 samples per step
     (m_training_batch_size, testbed.h:1103): `warmup` untimed steps, then `steps` timed ones (host wall clock
@@ -313,6 +313,10 @@ def train_leg(steps=200, warmup=50, seed=1337):
         cfg, params = synthetic.random_init(seed)
         tb.set_nerf_model(cfg, params)
         tb.set_training_dataset(imgs[train], xf[train], focal[train], pp[train])
+        if engine_params:
+            eng0 = Engine(tb)
+            for k, v in engine_params.items():
+                eng0.set_param(k, v)
         tb.train_reset(seed)
         tb.train(warmup)   # sng_train returns after its stream has finished (one host sync per step)
         t0 = time.perf_counter()

@@ -418,6 +418,7 @@ const std::map<std::string, double>& default_params() {
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
+        {"train_gen_bricks", 0},                // training generator's occupancy: 0 the linear words (measured fastest, tools/train_ab.py), 1 the OccBrick blob (LDS when it fits, else global)
         {"train_kernel_times", 0},              // 1: sng_train times the stages of every step with HIP events (sng_train_stats.ms_*)
         {"render_with_lens_distortion", 0},     // Testbed::Nerf::render_with_lens_distortion (testbed_nerf.cu:2504): NeRF rays through
                                                 //   render_lens (sng_set_render_lens; the snapshot dataset's first lens)
@@ -729,6 +730,16 @@ void build_occ_brick(sng_ctx* c, hipStream_t s) {
     ++c->model_epoch;
 }
 
+// the brick count of the last occupancy rebuild (build_occ_brick), read back behind it: the marchers stage the bricks in
+// LDS only when the count is known
+void resolve_occ_brick(sng_ctx* c) {
+    if (c->occ_brick_dirty && c->d_occ_brick_aux.p) {
+        HIPCHK(hipEventSynchronize(c->ev_brick));
+        c->occ_brick_n = c->h_alive[7];
+        c->occ_brick_dirty = false;
+    }
+}
+
 Volume make_volume(const sng_ctx* c) {
     Volume v{};
     v.render_aabb = c->box;
@@ -744,6 +755,7 @@ Volume make_volume(const sng_ctx* c) {
     v.linear = (c->max_cascade == 0 && c->cone <= 1e-5f && c->p("linear_marcher") != 0.0) ? 1 : 0;
     // the bricks in LDS when they fit the budget (lego: 521 bricks, 41 KiB)
     const uint32_t words = (OCC_BRICK_HDR_WORDS + 16u * std::max(1u, c->occ_brick_n) + 3u) & ~3u;   // >= 1 brick: branch-free readers
+    if (v.linear && c->d_occ_brick.p) v.occ_brick_g = c->d_occ_brick.as<uint32_t>();   // rebuilt in stream order with the bitfield
     if (v.linear && c->d_occ_brick.p && !c->occ_brick_dirty && c->p("occ_lds_kb") * 1024.0 >= 4.0 * words) {
         v.occ_brick = c->d_occ_brick.as<uint32_t>();
         v.occ_brick_words = words;
@@ -1719,11 +1731,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     // the raytracer's NeRF shadow test uses the density bitfield whether or not the NeRF is shown
     // (engine.cu:386-397 passes m_nerf.density_grid_bitfield unconditionally)
     Volume vol{};
-    if (c->occ_brick_dirty && c->d_occ_brick_aux.p) {   // the brick count of the last occupancy rebuild
-        HIPCHK(hipEventSynchronize(c->ev_brick));
-        c->occ_brick_n = c->h_alive[7];
-        c->occ_brick_dirty = false;
-    }
+    resolve_occ_brick(c);
     if (c->has_model && c->has_bitfield) vol = make_volume(c);
     else { vol.render_aabb = c->box; vol.train_aabb = c->box; vol.to_local = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)}; vol.to_local_identity = 1; }
     const CamDev cam = cam_dev(c);
@@ -2054,6 +2062,7 @@ TrainStepArgs train_args(sng_ctx* c) {
     a.loss_scale = 128.0f;   // default_loss_scale<__half>
     a.near_distance = 0.1f;
     a.debug = c->p("train_debug") != 0.0 ? 1 : 0;
+    a.gen_bricks = c->p("train_gen_bricks") != 0.0 ? 1 : 0;
     return a;
 }
 

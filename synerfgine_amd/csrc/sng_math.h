@@ -509,6 +509,8 @@ struct Volume {
     // the linear marchers' loops then make no global load.  occ_brick_words == 0: not available.
     const uint32_t* occ_brick;
     uint32_t occ_brick_words;
+    const uint32_t* occ_brick_g;  // the same blob in global memory whenever it is built (its size need not be known on the host):
+                                  // the training generator reads it through L1 / L2 when it cannot stage it (nullptr: not built)
 };
 // OccBrick layout (u32 words): [0, 128) = 4096-bit "dilated" brick mask (bit b: an occupied cell lies within one
 // cell of brick b -- the conservative test of path_last_occupied_t), [128, 2176) = u16 slot per brick

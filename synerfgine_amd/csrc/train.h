@@ -84,6 +84,24 @@ SNG_HD f2 train_image_pos(Pcg32& rng, const TrainImages& im) {
     return {((float)px + 0.5f) / (float)im.w, ((float)py + 0.5f) / (float)im.h};
 }
 
+// n items per lane reserved from one counter with ONE atomic per wave (every lane of the wave must be active): the
+// lane's exclusive prefix within the wave plus the wave's base.  The reference reserves per thread
+// (testbed_nerf.cu:956-963, 1150); the batch order of the atomics is arbitrary in both, and ~20 K single-word atomics per
+// batch serialise at ~90 per us (MI355X_MICROARCH.md, dequeue).
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* counter, uint32_t n, int lane) {
+    uint32_t incl = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    uint32_t base = 0;
+    if (lane == 63 && total) base = atomicAdd(counter, total);
+    base = __shfl(base, 63, 64);
+    return base + incl - n;
+}
+
 struct TrainRay { f3 o, d; };
 // uv_to_ray (common_device.cuh:403-470) with the image's lens (testbed_nerf.cu:890-905), no parallax / aperture / near
 // distance / distortion map; an invalid ray (F-Theta outside its domain) becomes {xform[3], xform[2]} (testbed_nerf.cu:901-903)
@@ -127,6 +145,7 @@ struct TrainStepArgs {
     float loss_scale;        // LOSS_SCALE() = 128 for fp16
     float near_distance;     // 0.1
     int debug;               // generate: per-ray step count / entry distances into loss / coords_c
+    int gen_bricks;          // generate's unit-cube occupancy source: 1 bricks (LDS when staged, else global), 0 linear words
 };
 
 // per-batch buffers

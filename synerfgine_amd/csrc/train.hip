@@ -38,16 +38,22 @@ __device__ __forceinline__ f4v mfma16k16(h4v a, h4v b, f4v c) { return __builtin
 // calc_dt(t)), so the samples are the reference's bit for bit.  BRICK (unit-cube scenes): the occupancy lookups read
 // the mip-0 bricks staged in LDS (occupied_brick_nb, the render marchers' exact form) instead of global memory.
 // One 64-lane workgroup per 64 rays: a batch has only ~4K rays, so small workgroups spread them over the CUs.
-template <bool BRICK>
+// BRICK 0: bitfield / linear occupancy; 1: the bricks staged in LDS; 2: the bricks read from global memory (their count
+// is not known on the host while training rebuilds them every few steps)
+template <int BRICK>
 __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, float* __restrict__ tscr) {
     extern __shared__ uint32_t occ_lds[];
-    if constexpr (BRICK) stage_occ_brick(occ_lds, a.vol.occ_brick, a.vol.occ_brick_words);
+    if constexpr (BRICK == 1) stage_occ_brick(occ_lds, a.vol.occ_brick, a.vol.occ_brick_words);
+    const uint32_t* const bricks = BRICK == 1 ? occ_lds : a.vol.occ_brick_g;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n_rays) return;
-    const uint32_t img = ((i * im.n) / a.n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
-    rng.advance((uint64_t)i * N_MAX_RANDOM_SAMPLES_PER_RAY);
+    const int lane = threadIdx.x & 63;
+    // every lane stays to the wave's reservations below (wave_reserve); a lane without a ray marches nothing
+    const bool in = i < a.n_rays;
+    const uint32_t ii = in ? i : 0u;
+    const uint32_t img = ((ii * im.n) / a.n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
+    rng.advance((uint64_t)ii * N_MAX_RANDOM_SAMPLES_PER_RAY);
     const f2 uv = train_image_pos(rng, im);
-    if (read_rgba(im, img, uv).x < 0.0f) return;              // masked pixel
+    const bool live = in && !(read_rgba(im, img, uv).x < 0.0f);   // masked pixel: no samples
     (void)rng.next_float();                                    // motionblur_time
     const TrainRay ray = train_ray(im, img, uv);
     const f3 dn = normalize(ray.d);
@@ -61,23 +67,26 @@ __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, Tra
     f3 pos;
     // unit-cube scenes (cone 0, one cascade): the exact linear specialisation of the occupancy test and
     // of advance_to_next_voxel that the render marcher uses (sng_math.h, tests/test_host_fastpaths.py)
-    const bool lin = BRICK || (a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_linear != nullptr);
+    const bool lin = BRICK != 0 || (a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_linear != nullptr);
     const f3 hs = half_sign(dn);
-    float* const ts = tscr + i;
-    while (aabb_contains(box, pos = ray.o + t * dn) && j < NERF_STEPS) {
+    float* const ts = tscr + ii;
+    OccCache oc;
+    while (live && aabb_contains(box, pos = ray.o + t * dn) && j < NERF_STEPS) {
         const float dt = calc_dt(t, cone);
         bool occ;
-        if constexpr (BRICK) occ = occupied_brick_nb(pos, occ_lds);
-        else occ = lin ? occupied_linear(pos, a.vol.occ_linear) : occupied_at(pos, a.vol.bitfield, mip_from_dt(dt, pos, a.vol.max_mip));
+        // the cached forms reload a word only when the position leaves the last one (~4.6 samples per cell): each trip
+        // is a dependent load otherwise, and a batch has too few rays to hide that latency
+        if constexpr (BRICK != 0) occ = occupied_brick_c(pos, bricks, oc);
+        else occ = lin ? occupied_linear_c(pos, a.vol.occ_linear, oc) : occupied_at(pos, a.vol.bitfield, mip_from_dt(dt, pos, a.vol.max_mip));
         if (occ) { ts[(size_t)j * a.n_rays] = t; ++j; t += dt; }
         else t = lin ? dda_step_linear(t, pos, idir, hs) : advance_to_next_voxel(t, cone, pos, dn, idir, mip_from_dt(dt, pos, a.vol.max_mip));
     }
-    if (a.debug) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
-    if (j == 0) return;
+    if (a.debug && live) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
     const uint32_t numsteps = j;
-    const uint32_t base = atomicAdd(&b.ctrl->numsteps_counter, numsteps);
-    if (base + numsteps > a.max_samples) return;
-    const uint32_t ray_idx = atomicAdd(&b.ctrl->ray_counter, 1u);
+    const uint32_t base = wave_reserve(&b.ctrl->numsteps_counter, numsteps, lane);
+    const bool keep = numsteps > 0 && base + numsteps <= a.max_samples;
+    const uint32_t ray_idx = wave_reserve(&b.ctrl->ray_counter, keep ? 1u : 0u, lane);
+    if (!keep) return;
     b.ray_indices[ray_idx] = i;
     b.rays[2 * ray_idx] = make_float4(ray.o.x, ray.o.y, ray.o.z, 0.0f);
     b.rays[2 * ray_idx + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
@@ -100,9 +109,11 @@ __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, Tra
 // error map, sharpness, exposure or depth supervision
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, const float* __restrict__ mean_density) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.ctrl->ray_counter) return;
-    const uint2 ns = b.numsteps[i];
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool in = i0 < b.ctrl->ray_counter;   // the lanes past the last ray stay for the wave's reservation (cn = 0)
+    const uint32_t i = in ? i0 : 0u;
+    const uint2 ns = in ? b.numsteps[i] : make_uint2(0u, 0u);
     const uint32_t numsteps = ns.x, base = ns.y;
     const float* __restrict__ cin = b.coords + (size_t)base * 7;
     const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
@@ -165,9 +176,9 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
     }
     if (cn == numsteps) rgb_ray = rgb_ray + T * bg;
 
-    const uint32_t cbase = atomicAdd(&b.ctrl->numsteps_compacted, cn);
+    const uint32_t cbase = wave_reserve(&b.ctrl->numsteps_compacted, in ? cn : 0u, lane);
     const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
-    if (ccount == 0) return;
+    if (!in || ccount == 0) return;
     // Huber loss (alpha = 0.1) / 5, loss_and_gradient (nerf_device.cuh:100-117, 601-616)
     f3 grad;
     float loss_sum = 0.0f;
@@ -731,10 +742,12 @@ void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, h
 }
 void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, float* tscr, hipStream_t s) {
     const dim3 grid((a.n_rays + 63) / 64);
-    if (a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_brick_words && a.vol.occ_brick_words * 4u <= 64u * 1024u)
-        hipLaunchKernelGGL(train_generate_kernel<true>, grid, dim3(64), a.vol.occ_brick_words * 4, s, a, im, b, rng, tscr);
+    if (a.gen_bricks && a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_brick_words && a.vol.occ_brick_words * 4u <= 64u * 1024u)
+        hipLaunchKernelGGL(train_generate_kernel<1>, grid, dim3(64), a.vol.occ_brick_words * 4, s, a, im, b, rng, tscr);
+    else if (a.gen_bricks && a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_brick_g)
+        hipLaunchKernelGGL(train_generate_kernel<2>, grid, dim3(64), 0, s, a, im, b, rng, tscr);
     else
-        hipLaunchKernelGGL(train_generate_kernel<false>, grid, dim3(64), 0, s, a, im, b, rng, tscr);
+        hipLaunchKernelGGL(train_generate_kernel<0>, grid, dim3(64), 0, s, a, im, b, rng, tscr);
 }
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
     (void)hipMemsetAsync(b.rayrec, 0, (size_t)a.n_rays * 48, s);

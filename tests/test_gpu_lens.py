@@ -70,7 +70,15 @@ def test_fox_opencv_train_generate_matches_oracle(fox):
     nr = int(g["ctrl"][0])
     assert nr > 32, "too few training rays hit the occupancy grid"
     assert int(g["ctrl"][1]) == int(ns.sum())
-    assert sorted(g["ray_indices"].tolist()) == np.nonzero(ns)[0].tolist()
+    mb = int(fox["stats"]["measured_batch_before_compaction"])
+    max_samples = 16 * BATCH if mb == 0 else (min(mb, 16 * BATCH) + 255) // 256 * 256   # train_nerf_step max_samples
+    # every ray the oracle finds samples on is on the GPU list, and nothing else -- unless the sample budget overflowed:
+    # the dropped rays then depend on the order of the reservations (atomics in the reference too)
+    got = set(g["ray_indices"].tolist())
+    if int(g["ctrl"][1]) <= max_samples:
+        assert sorted(got) == np.nonzero(ns)[0].tolist()
+    else:
+        assert got <= set(np.nonzero(ns)[0].tolist())
     for k in range(nr):
         i = int(g["ray_indices"][k])
         n, base = g["numsteps"][k]
@@ -98,7 +106,7 @@ def test_fox_fisheye_train_generate_close_to_oracle(fox):
         idx = g["ray_indices"].astype(np.int64)
         gd, od = g["rays"][:, 4:7], rays[idx, 3:6]
         assert np.abs(gd - od).max() <= 2e-6 * np.abs(od).max(), "fisheye ray directions beyond 2e-6 relative"
-        same = (g["numsteps"][:, 0] == ns[idx]).mean()
+        same = (g["numsteps"][:, 0] == ns[idx]).mean()   # (the GPU's rays only: the sample budget may drop some)
         assert same >= 0.99, f"{same:.4f} of the rays have the oracle's sample count"
     finally:
         tb.set_training_lens(fox["d"]["lenses"])

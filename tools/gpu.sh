@@ -12,6 +12,7 @@
 #   sq[:CFG[:ARGS]]        SQ_INSTS_* + SQ_WAVE_CYCLES pass with kernel trace + tools/sq_summary.py (VALU roofline)
 #   ab:CFG:PAIRS:A/B       PAIRS alternating bench.py runs of two settings (A, B: KEY=V[,KEY=V...], '-' for the defaults),
 #                          then tools/bsum.py over the logs (replaces round 4's one-off ab_r04*.sh scripts)
+#   sqpy:SCRIPT[:ARGS]     the sq pass over python3 tools/SCRIPT ARGS
 #   py:SCRIPT[:ARGS]       python3 tools/SCRIPT ARGS
 #   profpy:SCRIPT[:ARGS]   rocprofv3 --kernel-trace --stats of python3 tools/SCRIPT ARGS (+ kernel table)
 #   pmcpy:SCRIPT[:ARGS]    FETCH_SIZE / WRITE_SIZE / MFMA passes over python3 tools/SCRIPT ARGS + tools/pmc_summary.py
@@ -97,6 +98,13 @@ for step in "$@"; do
         done
       done
       [ $rc -eq 0 ] && python3 tools/bsum.py $OUT/ab$n.*.log | tee $log ;;
+    sqpy)
+      # the SQ pass over python3 tools/SCRIPT ARGS (e.g. train_bench.py) + tools/sq_summary.py
+      d=$OUT/sq$n
+      ctr="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
+      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $ctr -d $d -o run --output-format csv -- python3 tools/$cfg $args > $log 2>&1
+      rc=$?
+      [ $rc -eq 0 ] && python3 tools/sq_summary.py $d $OUT/sq_${cfg%.py}.json ${cfg%.py} 2>&1 | tee -a $log; rc=${PIPESTATUS[0]} ;;
     py)
       timeout -k 10 600 python3 -u tools/$cfg $args > $log 2>&1
       rc=$?; tail -c 3000 $log; echo ;;

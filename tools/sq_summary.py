@@ -18,7 +18,8 @@ PEAK_WAVE_INSTR_PER_S = 256 * 4 * 0.5 * 2.4e9
 KEYS = ("raytrace_kernel", "raytrace_pl_kernel", "shadow_rays_kernel", "rt_record_colour_kernel", "rt_accumulate_kernel", "rt_shade_records_kernel",
         "nerf_network_kernel", "spec_generate_kernel", "spec_composite_kernel", "init_rays_kernel", "generate_kernel", "nerf_fused_kernel",
         "shade_shadow_kernel", "shadow_draw_kernel", "shadow_term_kernel", "shadow_finish_kernel", "msr_generate_kernel", "msr_count_kernel",
-        "msr_commit_kernel", "nerf_onestep_kernel", "onestep_schedule_kernel")
+        "msr_commit_kernel", "nerf_onestep_kernel", "onestep_schedule_kernel", "train_generate_kernel", "train_field_kernel",
+        "train_loss_kernel", "train_dloss_kernel", "train_dw_kernel", "train_adam_kernel")
 
 
 def short(n):
