@@ -410,6 +410,13 @@ const std::map<std::string, double>& default_params() {
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"rt_prio_frac", 0.1},                  // the costliest fraction of the path tiles (last frame's order) at wave priority 3
         {"rt_prio2_frac", 0.25},                // ... the tiles up to this fraction of the order at priority 2
+        {"rt_fused_shadow", 1},                 // banded frames: the path kernel's idle waves trace the shadow rays (mesh.hip fq_consume)
+        {"rt_fused_tiles_per_wave", 1},         // ... when the band has at most this many path tiles per wave (a full queue is traced in place)
+        {"rt_chain_split", 0},                  // ... and their pixels' sample chains split: chain walk, then every (tile, sample) apart
+        {"rt_chain_any", 1},                    // ... the chain walk's last bounce as an any-hit query (depth_test_world_any)
+        {"rt_chain_split_used", 0},             // (output) 1 when the last frame split the chains
+        {"rt_fused_shadow_used", 0},            // (output) 1 when the last frame's path kernel traced its shadow rays itself
+        {"rt_spread", 1},                       // the path kernel's first tiles dealt across all CUs (costliest one per CU / SIMD)
         {"nerf_gbuffer", 0},                    // 1: NeRF normals every frame (otherwise only when shadow_on_nerf needs them)
         {"rt_plist", 1},                        // per-pixel hit-record lists for the colour replay (rt_accumulate_kernel)
         {"glow_mode", 0},                       // Testbed::Nerf::glow_mode (testbed.h:871): bits 1 green grid, 2 cut line, 4 mask to alpha,
@@ -536,6 +543,7 @@ struct sng_ctx {
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
     DevBuf rt_rec, rt_lc, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
+    DevBuf rt_chain_state, rt_chain_off, rt_chain_nh;   // split path chain (banded frames)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf shadow_scratch;                 // NeRF shadow pass: light samples + terms per neighbour slot (launch_shadows)
@@ -1761,6 +1769,8 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         }
         if (c->p("show_virtual_obj") != 0.0 && !c->objs.empty()) {
             RaytraceArgs ra{};
+            c->params["rt_fused_shadow_used"] = 0;
+            c->params["rt_chain_split_used"] = 0;
             ra.vol = vol;
             ra.W = MW; ra.row0 = y0; ra.row1 = y1;
             ra.up = cam.c0;
@@ -1799,9 +1809,14 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 ra.counts = c->rt_counts.as<unsigned long long>();
                 ra.count_waves = c->p("rt_count") == 2.0 ? 1 : 0;
             }
-            ra.tile = c->p("rt_tile") == 4.0 ? 4 : 8;
-            ra.tile_h = c->p("rt_tile_h") == 4.0 ? 4 : (c->p("rt_tile_h") == 8.0 && ra.tile == 8 ? 8 : ra.tile);
+            // tile width 1, 2, 4 or 8 pixels (else 8); height 1..8 (0: square), at most 64 pixels per wave
+            {
+                const int tw = (int)c->p("rt_tile"), th = (int)c->p("rt_tile_h");
+                ra.tile = (tw == 1 || tw == 2 || tw == 4) ? tw : 8;
+                ra.tile_h = (th >= 1 && th <= 8) ? th : ra.tile;
+            }
             ra.buffer_type = (int)c->p("rt_buffer_type");
+            ra.spread = c->p("rt_spread") != 0.0 ? 1 : 0;
             if (c->p("rt_tile_order") != 0.0) {
                 const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile_h - 1) / ra.tile_h);
                 const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60) ^ ((uint64_t)ra.tile_h << 56);
@@ -1861,8 +1876,31 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                     q.rval = c->rt_rval.as<float4>();
                     q.max_hits = (uint32_t)max_hits;
                 }
+                // banded frames (at most rt_fused_tiles_per_wave tiles per path-kernel wave): the waves past their tiles
+                // trace the shadow rays as the records appear, and the shadow-ray kernel is not launched
+                {
+                    const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile_h - 1) / ra.tile_h);
+                    const uint32_t tpb = ra.scene_in_lds ? ra.lds_tpb : 512u;
+                    const size_t lds_need = (ra.scene_in_lds ? (size_t)ra.scene_f4 * 16 : 0) + (size_t)ra.stack_depth * tpb * 4 + RT_FQ_WORDS * 4;
+                    ra.fused_shadow = c->p("rt_fused_shadow") != 0.0 && ra.spread && !ra.counts && n_tiles <= (uint32_t)(c->p("rt_fused_tiles_per_wave") * ra.persistent_blocks * 16u) &&
+                                      lds_need <= 160u * 1024u ? 1 : 0;
+                    c->params["rt_fused_shadow_used"] = ra.fused_shadow;
+                }
+                // ... and with the record lists, the pixels' sample chains split (rt_chain_kernel + rt_sample_kernel)
+                RtChain chain{};
+                const bool split = ra.fused_shadow && q.plist && ra.scene_in_lds && ra.samples > 1 && c->p("rt_chain_split") != 0.0;
+                if (split) {
+                    c->rt_chain_state.ensure((size_t)6 * ra.samples * n_px * 4);
+                    c->rt_chain_off.ensure((size_t)ra.samples * n_px);
+                    c->rt_chain_nh.ensure((size_t)ra.samples * n_px);
+                    chain.state = c->rt_chain_state.as<uint32_t>();
+                    chain.off = c->rt_chain_off.as<uint8_t>();
+                    chain.nh = c->rt_chain_nh.as<uint8_t>();
+                }
+                c->params["rt_chain_split_used"] = split ? 1 : 0;
+                ra.chain_any = c->p("rt_chain_any") != 0.0 ? 1 : 0;
                 launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
-                                          c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt);
+                                          c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt, split ? &chain : nullptr);
             } else {
                 launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
                                 c->acc_depth.as<float>(), c->s_rt);

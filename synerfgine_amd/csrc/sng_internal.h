@@ -280,7 +280,14 @@ struct RaytraceArgs {
     int buffer_type;            // ImgBufferType (raytracer.cuh:20): 0 Final, 1 NextOrigin .. 7 NerfShadow (one-kernel path)
     uint32_t prio_tiles;        // the first prio_tiles tiles of tile_order run at wave priority 3 (0: off)
     uint32_t prio2_tiles;       // ... and the tiles before prio2_tiles at priority 2
+    int spread;                 // first tile of every wave dealt statically across the CUs (rt_spread), the rest claimed
+    int fused_shadow;           // the path kernel's idle waves trace the shadow rays (banded frames, mesh.hip fq_consume)
+    int chain_any;              // rt_chain_kernel: the last bounce's query as depth_test_world_any (else the closest-hit walk)
 };
+
+// fused shadow queue of a banded path kernel (mesh.hip fq_publish / fq_consume): entries per workgroup, LDS words
+constexpr uint32_t RT_FQ_CAP = 1024;
+constexpr uint32_t RT_FQ_WORDS = 4 + 2 * RT_FQ_CAP;
 
 // Deferred-shadow raytracer queues (mesh.hip, wavefront mode).  One "hit record" per (pixel,
 // sample, bounce) that hit an object: header {next, spp, mat, pos.z} {pdf, att, pos.x, pos.y}, and the
@@ -407,8 +414,15 @@ size_t shadow_scratch_bytes(const ShadowArgs& a);
 void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, void* scratch, hipStream_t s);
 void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
                       hipStream_t s);
+// Split path chain of a banded frame (mesh.hip rt_chain_kernel / rt_sample_kernel, rt_chain_split): per (sample, pixel)
+// the XORWOW state at the sample's first draw, the pixel's hits before the sample and the sample's own hits.
+struct RtChain {
+    uint32_t* state;      // 6 x samples x n_px words: word w of sample s of pixel t at [(w * samples + s) * n_px + t]
+    uint8_t* off;         // samples x n_px
+    uint8_t* nh;          // samples x n_px
+};
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
-                               float* accd, uint32_t shadow_blocks, hipStream_t s);
+                               float* accd, uint32_t shadow_blocks, hipStream_t s, const RtChain* chain = nullptr);
 void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, uint32_t* aux, hipStream_t s);
 
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,
