@@ -412,9 +412,6 @@ const std::map<std::string, double>& default_params() {
         {"rt_prio2_frac", 0.25},                // ... the tiles up to this fraction of the order at priority 2
         {"rt_fused_shadow", 1},                 // banded frames: the path kernel's idle waves trace the shadow rays (mesh.hip fq_consume)
         {"rt_fused_tiles_per_wave", 1},         // ... when the band has at most this many path tiles per wave (a full queue is traced in place)
-        {"rt_chain_split", 0},                  // ... and their pixels' sample chains split: chain walk, then every (tile, sample) apart
-        {"rt_chain_any", 1},                    // ... the chain walk's last bounce as an any-hit query (depth_test_world_any)
-        {"rt_chain_split_used", 0},             // (output) 1 when the last frame split the chains
         {"rt_fused_shadow_used", 0},            // (output) 1 when the last frame's path kernel traced its shadow rays itself
         {"rt_spread", 1},                       // the path kernel's first tiles dealt across all CUs (costliest one per CU / SIMD)
         {"nerf_gbuffer", 0},                    // 1: NeRF normals every frame (otherwise only when shadow_on_nerf needs them)
@@ -543,7 +540,6 @@ struct sng_ctx {
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
     DevBuf rt_rec, rt_lc, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
-    DevBuf rt_chain_state, rt_chain_off, rt_chain_nh;   // split path chain (banded frames)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf shadow_scratch;                 // NeRF shadow pass: light samples + terms per neighbour slot (launch_shadows)
@@ -1770,7 +1766,6 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         if (c->p("show_virtual_obj") != 0.0 && !c->objs.empty()) {
             RaytraceArgs ra{};
             c->params["rt_fused_shadow_used"] = 0;
-            c->params["rt_chain_split_used"] = 0;
             ra.vol = vol;
             ra.W = MW; ra.row0 = y0; ra.row1 = y1;
             ra.up = cam.c0;
@@ -1886,21 +1881,8 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                                       lds_need <= 160u * 1024u ? 1 : 0;
                     c->params["rt_fused_shadow_used"] = ra.fused_shadow;
                 }
-                // ... and with the record lists, the pixels' sample chains split (rt_chain_kernel + rt_sample_kernel)
-                RtChain chain{};
-                const bool split = ra.fused_shadow && q.plist && ra.scene_in_lds && ra.samples > 1 && c->p("rt_chain_split") != 0.0;
-                if (split) {
-                    c->rt_chain_state.ensure((size_t)6 * ra.samples * n_px * 4);
-                    c->rt_chain_off.ensure((size_t)ra.samples * n_px);
-                    c->rt_chain_nh.ensure((size_t)ra.samples * n_px);
-                    chain.state = c->rt_chain_state.as<uint32_t>();
-                    chain.off = c->rt_chain_off.as<uint8_t>();
-                    chain.nh = c->rt_chain_nh.as<uint8_t>();
-                }
-                c->params["rt_chain_split_used"] = split ? 1 : 0;
-                ra.chain_any = c->p("rt_chain_any") != 0.0 ? 1 : 0;
                 launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
-                                          c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt, split ? &chain : nullptr);
+                                          c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt);
             } else {
                 launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
                                 c->acc_depth.as<float>(), c->s_rt);

@@ -224,8 +224,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
 // The visiting sequence, `d < mint` culling at push time and triangle order are the reference's, so
 // the result is identical.  (The reference's FixedStack<32> overflow rule cannot fire: the stack
 // never holds more than max BVH depth + 2 <= 32 entries, capi.cpp upload_scene.)
-// ANY: return at the first triangle the culling admits (some t < t_max exists; not the closest one)
-template <bool FAST, bool ANY = false>
+template <bool FAST>
 __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const TriT* __restrict__ tris, int root_ref,
                                                int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr, bool cw = false) {
     PStack st{(lds_int*)stack_lds, (lds_int*)stack_lds, stride};
@@ -259,14 +258,7 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
         for (int i = b; i < end; ++i) {
             if (cnt && cw) cnt[2] += (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id());
             float t;
-            if (tri_hit(tris + i, ro, rd, mint, t)) {
-                mint = t;
-                shortest = i;
-                if constexpr (ANY) {
-                    tri_out = shortest;
-                    return mint;
-                }
-            }
+            if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
         }
         if (st.empty()) break;
         cur = st.pop();
@@ -442,40 +434,6 @@ __device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restri
     }
     h.pos = origin + h.t * dir;
     return out_obj;
-}
-
-// Whether depth_test_world_hit(origin, dir) finds an object (its result >= 0), without the closest triangle: an object
-// counts when its closest accepted t (tri_hit: 0 <= t < MAX_DEPTH) exceeds MIN_DEPTH.  So it counts exactly when some
-// accepted t exists and none is <= MIN_DEPTH: a walk that stops at the first admitted triangle (ANY) answers the first
-// question, and when that triangle's t > MIN_DEPTH a walk culled at the next float above MIN_DEPTH (tiny: only the
-// boxes around the start point) the second.  Other layouts: the closest walk.
-template <bool LDS, bool CNT = false, bool QUAD = false>
-__device__ bool depth_test_world_any(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT, QUAD>& cx) {
-    const f3 off = origin + dir * MIN_DEPTH;
-    if constexpr (CNT) cx.cnt[0] += 1u;
-    const float t_near = __uint_as_float(__float_as_uint(MIN_DEPTH) + 1u);   // accepted t < t_near <=> t <= MIN_DEPTH
-    for (int c = 0; c < n_objs; ++c) {
-        const ObjectGpu& o = objs[c];
-        int tri;
-        if (!(o.wide && cx.flat) || (QUAD && o.quad)) {
-            const float t = object_intersect(off, dir, o, cx, tri);
-            if (t < MAX_DEPTH && t > MIN_DEPTH) return true;
-            continue;
-        }
-        const f3 oro = mul(o.world_to_obj, off - o.pos);
-        const f3 ord = mul(o.world_to_obj, dir);
-        const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
-        const f3 y = inv(ord);
-        uint32_t* cn = CNT ? cx.cnt : nullptr;
-        const bool cw = CNT && cx.cnt_waves;
-        const float t = fast ? bvh_walk_near<true, true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, MAX_DEPTH, cn, cw)
-                             : bvh_walk_near<false, true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, MAX_DEPTH, cn, cw);
-        if (!(t < MAX_DEPTH && t > MIN_DEPTH)) continue;   // none, or one at or below MIN_DEPTH (the closest is too)
-        const float tn = fast ? bvh_walk_near<true, true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_near, cn, cw)
-                              : bvh_walk_near<false, true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_near, cn, cw);
-        if (!(tn < t_near)) return true;
-    }
-    return false;
 }
 
 // sng::depth_test_nerf (common.cu:69-83), with two exact early exits.  The march's distance s never
@@ -857,19 +815,16 @@ __device__ __forceinline__ void write_record_header(float4* rk, int next, uint32
 // shadow rays go to q; rp / rd / pdf / att become the scattered ray's.
 template <bool LDS, bool CNT>
 __device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t* fq, int lane, size_t i, uint32_t t,
-                                          uint32_t spp, const Hit& h, int& prev_rec, uint32_t& n_hits, Xorwow& r, f3& rp, f3& rd, float& pdf, float& att,
-                                          bool link = true) {
+                                          uint32_t spp, const Hit& h, int& prev_rec, uint32_t& n_hits, Xorwow& r, f3& rp, f3& rd, float& pdf, float& att) {
     const MaterialGpu m = a.mats[h.mat];
     const uint32_t k = wave_alloc(q.count, lane);
     if (q.plist) q.plist[(size_t)t * q.max_hits + n_hits] = (int)k;
     ++n_hits;
     float4* rk = q.rec + (size_t)k * q.rec_stride;
     write_record_header(rk, -1, spp, h.mat, h.pos, pdf, att);
-    if (link) {   // the record chain (list mode reads plist instead; the split chain writes only the lists)
-        if (prev_rec < 0) q.head[i] = (int)k;
-        else reinterpret_cast<int*>(q.rec + (size_t)prev_rec * q.rec_stride)[0] = (int)k;
-        prev_rec = (int)k;
-    }
+    if (prev_rec < 0) q.head[i] = (int)k;
+    else reinterpret_cast<int*>(q.rec + (size_t)prev_rec * q.rec_stride)[0] = (int)k;
+    prev_rec = (int)k;
     write_light_samples(a, q, k, h.pos, h.normal, rd, m, r);
     if (fq) fq_publish(fq, a, q, cx, k, lane);
     const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
@@ -1056,157 +1011,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
         if (fq) fq_consume(fq, a, q, cx, lane);
     }
     if constexpr (CNT) flush_counts(a.counts, counts, lane);
-}
-
-// ---------------------------------------------------------------------------------------------------------------------
-// Split path chain (banded frames, rt_chain_split).  A pixel's 8 samples x 2 bounces are one chain only through its XORWOW
-// stream: sample s starts at the draw after samples 0..s-1, and a sample draws 1 (lens) + 3 nls + 2 per hit, so its
-// start depends on how many hits the earlier samples made.  rt_chain_kernel walks that chain alone -- per sample the
-// lens draws, the primary query (the first hit's position feeds the depth), the scatter draws and direction, and for
-// the last bounce only whether it hits (depth_test_world_any) -- skipping the light-sample draws, and records each
-// sample's start state and hit offset; it also writes the depth, the hit count and the pixel's final state, as
-// raytrace_pixel does.  rt_sample_kernel then traces every (tile, sample) as a unit of its own from the recorded state
-// (the same draws, queries and records as raytrace_pixel's sample, list-mode records at the recorded offsets), so a
-// costly tile's 8 samples run on 8 waves.  Every value is raytrace_pixel's; rt_accumulate_kernel sums the lists.
-// ---------------------------------------------------------------------------------------------------------------------
-template <bool LDS>
-__device__ __forceinline__ void chain_pixel(const RaytraceArgs& a, const RtQueue& q, const RtChain& ch, const TraceCtx<LDS, false>& cx, uint32_t t,
-                                            const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
-                                            uint32_t n_rng, float* __restrict__ acc_depth) {
-    const size_t i = (size_t)a.row0 * a.W + t;
-    const size_t n = (size_t)(a.row1 - a.row0) * (size_t)a.W;
-    Xorwow r = load_rng(rng, n_rng, i);
-    const float4 o4 = origins[i], d4 = dirs[i];
-    const f3 src_p = mk(o4.x, o4.y, o4.z), src_d = mk(d4.x, d4.y, d4.z);
-    f3 next_pos = splat(0.0f);
-    uint32_t n_hits = 0;
-    q.head[i] = -1;
-    for (uint32_t spp = 0; spp < a.samples; ++spp) {
-        const size_t si = (size_t)spp * n + t, sw = (size_t)a.samples * n;
-        ch.state[si] = r.v0; ch.state[sw + si] = r.v1; ch.state[2 * sw + si] = r.v2;
-        ch.state[3 * sw + si] = r.v3; ch.state[4 * sw + si] = r.v4; ch.state[5 * sw + si] = r.d;
-        ch.off[si] = (uint8_t)n_hits;
-        const float longi = curand_uniform(r) * a.lens;
-        const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
-        f3 rp = src_p, rd = cone_random_up(src_d, a.up, longi, latid);
-        uint32_t hs = 0;
-        for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
-            const bool last = bounce + 1 == a.bounces;
-            Hit h;
-            bool hit;
-            if (!last || bounce == 0 || !a.chain_any) {
-                hit = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h) >= 0;
-                if (!bounce) next_pos = next_pos + h.pos;
-            } else {
-                hit = depth_test_world_any(rp, rd, a.objs, a.n_objs, cx);
-            }
-            if (!hit) break;
-            ++hs;
-            xorwow_skip(r, 3u * q.nls);   // write_light_samples: Light::sample's 3 draws per (light, shadow iteration)
-            if (last) {
-                xorwow_skip(r, 2u);       // Material::scatter's draws (its ray is not traced)
-                break;
-            }
-            const MaterialGpu m = a.mats[h.mat];
-            const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
-            const float lo = curand_uniform(r) * spec;
-            const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
-            rd = cone_random_frame(h.normal, h.perturb, lo, la);
-            rp = h.pos;
-        }
-        ch.nh[si] = (uint8_t)hs;
-        n_hits += hs;
-    }
-    const float weight = (float)a.samples;
-    next_pos = next_pos / weight;
-    acc_depth[i] = dot(src_d, next_pos - src_p);
-    q.pcount[t] = (uint8_t)n_hits;
-    store_rng(rng, n_rng, i, r);
-}
-
-// the tile loop of raytrace_kernel (spread first round, claimed rest, cost order, wave priorities) over n_units units;
-// unit u is tile rank u / per_tile, part u % per_tile
-template <typename F>
-__device__ __forceinline__ void rt_unit_loop(const RaytraceArgs& a, uint32_t* __restrict__ work, uint32_t n_units, uint32_t per_tile, F&& body) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t n_first = a.spread ? gridDim.x * (blockDim.x >> 6) : 0u;
-    bool first = a.spread != 0;
-    while (true) {
-        uint32_t k = 0;
-        if (first) {
-            k = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
-            first = false;
-        } else {
-            if (lane == 0) k = atomicAdd(work, 1u);
-            k = __shfl(k, 0, 64) + n_first;
-        }
-        if (k >= n_units) break;
-        const uint32_t rank = k / per_tile, part = k - rank * per_tile;
-        if (a.prio_tiles || a.prio2_tiles) {
-            const uint32_t ks = __builtin_amdgcn_readfirstlane(rank);
-            if (ks < a.prio_tiles) __builtin_amdgcn_s_setprio(3);
-            else if (ks < a.prio2_tiles) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-        body(a.tile_order ? a.tile_order[rank] : rank, part);
-    }
-}
-
-template <bool LDS>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void rt_chain_kernel(RaytraceArgs a, RtQueue q, RtChain ch, uint32_t* __restrict__ work,
-                                                        const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
-                                                        uint32_t n_rng, float* __restrict__ acc_depth) {
-    const TraceCtx<LDS, false> cx = trace_ctx_setup<LDS, false>(a);
-    const int lane = threadIdx.x & 63;
-    const uint32_t rows = (uint32_t)(a.row1 - a.row0);
-    const uint32_t T = (uint32_t)a.tile, TH = (uint32_t)a.tile_h, tiles_x = ((uint32_t)a.W + T - 1) / T, n_tiles = tiles_x * ((rows + TH - 1) / TH);
-    rt_unit_loop(a, work, n_tiles, 1u, [&](uint32_t tile, uint32_t) {
-        const uint64_t t0 = wall_clock64();
-        const uint32_t x = (tile % tiles_x) * T + (uint32_t)lane % T, y = (tile / tiles_x) * TH + (uint32_t)lane / T;
-        if ((uint32_t)lane < T * TH && x < (uint32_t)a.W && y < rows) chain_pixel<LDS>(a, q, ch, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_depth);
-        if (a.tile_cost && lane == 0) a.tile_cost[tile] = (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull);
-    });
-}
-
-template <bool LDS>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void rt_sample_kernel(RaytraceArgs a, RtQueue q, RtChain ch, uint32_t* __restrict__ work,
-                                                         const float4* __restrict__ origins, const float4* __restrict__ dirs) {
-    uint32_t* fq = nullptr;
-    if (a.fused_shadow) {
-        extern __shared__ float4 smem4[];
-        fq = reinterpret_cast<uint32_t*>(smem4 + (LDS ? a.scene_f4 : 0u)) + (size_t)a.stack_depth * blockDim.x;
-        for (uint32_t w = threadIdx.x; w < RT_FQ_WORDS; w += blockDim.x) fq[w] = 0u;
-        __syncthreads();
-    }
-    const TraceCtx<LDS, false> cx = trace_ctx_setup<LDS, false>(a);
-    const int lane = threadIdx.x & 63;
-    const uint32_t rows = (uint32_t)(a.row1 - a.row0);
-    const uint32_t T = (uint32_t)a.tile, TH = (uint32_t)a.tile_h, tiles_x = ((uint32_t)a.W + T - 1) / T, n_tiles = tiles_x * ((rows + TH - 1) / TH);
-    const size_t n = (size_t)rows * (size_t)a.W;
-    rt_unit_loop(a, work, n_tiles * a.samples, a.samples, [&](uint32_t tile, uint32_t spp) {
-        const uint32_t x = (tile % tiles_x) * T + (uint32_t)lane % T, y = (tile / tiles_x) * TH + (uint32_t)lane / T;
-        if (!((uint32_t)lane < T * TH && x < (uint32_t)a.W && y < rows)) return;
-        const uint32_t t = y * (uint32_t)a.W + x;
-        const size_t si = (size_t)spp * n + t, sw = (size_t)a.samples * n;
-        if (ch.nh[si] == 0) return;   // the primary ray missed: no record, and the chain kernel did its draws
-        Xorwow r{ch.state[si], ch.state[sw + si], ch.state[2 * sw + si], ch.state[3 * sw + si], ch.state[4 * sw + si], ch.state[5 * sw + si]};
-        uint32_t n_hits = ch.off[si];
-        const size_t i = (size_t)a.row0 * a.W + t;
-        const float4 o4 = origins[i], d4 = dirs[i];
-        const f3 src_p = mk(o4.x, o4.y, o4.z), src_d = mk(d4.x, d4.y, d4.z);
-        // raytrace_pixel's sample, DEFER form
-        const float longi = curand_uniform(r) * a.lens;
-        const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
-        f3 rp = src_p, rd = cone_random_up(src_d, a.up, longi, latid);
-        float pdf = 1.0f / (float)a.bounces, att = 1.0f;
-        int prev_rec = -1;
-        for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
-            Hit h;
-            if (depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h) < 0) break;
-            defer_hit(a, q, cx, fq, lane, i, t, spp, h, prev_rec, n_hits, r, rp, rd, pdf, att, false);
-        }
-    });
-    if (fq) fq_consume(fq, a, q, cx, lane);
 }
 
 // One shadow ray of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
@@ -1526,7 +1330,7 @@ void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, ui
     hipLaunchKernelGGL((raytrace_kernel<false, false>), dim3(blocks), dim3(tpb), lds, s, a, RtQueue{}, a.work, o, d, rng, n_rng, acc, accd);
 }
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
-                               float* accd, uint32_t shadow_blocks, hipStream_t s, const RtChain* chain) {
+                               float* accd, uint32_t shadow_blocks, hipStream_t s) {
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
     (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);   // errors surface through hipGetLastError in the caller
@@ -1541,15 +1345,7 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     // rt_spread: every CU gets a workgroup (a thin band's tiles then spread over the whole GPU, one wave each)
     const uint32_t bp = a.spread ? a.persistent_blocks * per_cu : std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * per_cu);
     const uint32_t sb = shadow_blocks ? shadow_blocks : a.persistent_blocks * per_cu;
-    if (chain) {   // split path chain (capi.cpp enables it with the fused shadow queue, the record lists and the LDS blob)
-        const size_t lc = trace_lds_bytes(a, lds, tp);
-        allow_lds(rt_chain_kernel<true>, lc);
-        allow_lds(rt_sample_kernel<true>, lp);
-        hipLaunchKernelGGL(rt_chain_kernel<true>, dim3(bp), dim3(tp), lc, s, a, q, *chain, a.work, o, d, rng, n_rng, accd);
-        (void)hipMemsetAsync(a.work, 0, sizeof(uint32_t), s);
-        hipLaunchKernelGGL(rt_sample_kernel<true>, dim3(bp), dim3(tp), lp, s, a, q, *chain, a.work, o, d);
-        if (!a.fused_shadow) hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
-    } else if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in
+    if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in
         allow_lds(raytrace_kernel<true, true, true>, lp);
         allow_lds(shadow_rays_kernel<true, true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);

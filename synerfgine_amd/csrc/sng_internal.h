@@ -282,7 +282,6 @@ struct RaytraceArgs {
     uint32_t prio2_tiles;       // ... and the tiles before prio2_tiles at priority 2
     int spread;                 // first tile of every wave dealt statically across the CUs (rt_spread), the rest claimed
     int fused_shadow;           // the path kernel's idle waves trace the shadow rays (banded frames, mesh.hip fq_consume)
-    int chain_any;              // rt_chain_kernel: the last bounce's query as depth_test_world_any (else the closest-hit walk)
 };
 
 // fused shadow queue of a banded path kernel (mesh.hip fq_publish / fq_consume): entries per workgroup, LDS words
@@ -414,15 +413,8 @@ size_t shadow_scratch_bytes(const ShadowArgs& a);
 void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, void* scratch, hipStream_t s);
 void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
                       hipStream_t s);
-// Split path chain of a banded frame (mesh.hip rt_chain_kernel / rt_sample_kernel, rt_chain_split): per (sample, pixel)
-// the XORWOW state at the sample's first draw, the pixel's hits before the sample and the sample's own hits.
-struct RtChain {
-    uint32_t* state;      // 6 x samples x n_px words: word w of sample s of pixel t at [(w * samples + s) * n_px + t]
-    uint8_t* off;         // samples x n_px
-    uint8_t* nh;          // samples x n_px
-};
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
-                               float* accd, uint32_t shadow_blocks, hipStream_t s, const RtChain* chain = nullptr);
+                               float* accd, uint32_t shadow_blocks, hipStream_t s);
 void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, uint32_t* aux, hipStream_t s);
 
 void launch_raytrace(const RaytraceArgs& a, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc, float* accd,

@@ -333,25 +333,22 @@ def test_rccl_gather_rgba8_world1_equals_final_rgba8():
 def test_fused_shadow_band_equals_separate_shadow_kernel(rows):
     """rt_fused_shadow: a thin band whose tiles all fit the path kernel's first round has its shadow rays traced by the
     path kernel's idle waves (a workgroup-local LDS queue of record allocations, mesh.hip fq_publish / fq_consume)
-    instead of shadow_rays_kernel; rt_chain_split also splits the pixels' sample chains (rt_chain_kernel walks each
-    pixel's XORWOW chain, rt_sample_kernel traces every (tile, sample) apart).  The band's frame buffers and the mesh
-    XORWOW states the frame leaves are the same bits in all three forms."""
+    instead of shadow_rays_kernel.  The band's frame buffers and the mesh XORWOW states the frame leaves are the same
+    bits either way."""
     from synerfgine_amd import scene as S
     tb, eng, _ = S.make_engine("c3")
     try:
         fresh = _fresh_fn(eng)
         out = {}
-        for fused, split in ((0, 0), (1, 0), (1, 1)):
+        for fused in (0, 1):
             eng.set_param("rt_fused_shadow", fused)
-            eng.set_param("rt_chain_split", split)
             for k in range(2):   # a second frame: tile order and wave priorities from the first one's costs
                 fresh()
                 r = eng.frame(rows=rows, target_n_queries=TARGET)
-            assert eng.get_param("rt_fused_shadow_used") == fused and eng.get_param("rt_chain_split_used") == split
-            out[(fused, split)] = {b: r.download(b)[rows[0]:rows[1]].copy() for b in ("final_rgba", "syn_rgba", "syn_depth")}
-            out[(fused, split)]["rng"] = eng.rng_states(1).copy()
-        for key in ((1, 0), (1, 1)):
-            for b in out[(0, 0)]:
-                assert np.array_equal(out[(0, 0)][b].view(np.uint32), out[key][b].view(np.uint32)), (key, b)
+            assert eng.get_param("rt_fused_shadow_used") == fused
+            out[fused] = {b: r.download(b)[rows[0]:rows[1]].copy() for b in ("final_rgba", "syn_rgba", "syn_depth")}
+            out[fused]["rng"] = eng.rng_states(1).copy()
+        for b in out[0]:
+            assert np.array_equal(out[0][b].view(np.uint32), out[1][b].view(np.uint32)), b
     finally:
         tb.close()
