@@ -40,7 +40,9 @@ __device__ __forceinline__ f4v mfma16k16(h4v a, h4v b, f4v c) { return __builtin
 // One 64-lane workgroup per 64 rays: a batch has only ~4K rays, so small workgroups spread them over the CUs.
 // BRICK 0: bitfield / linear occupancy; 1: the bricks staged in LDS; 2: the bricks read from global memory (their count
 // is not known on the host while training rebuilds them every few steps)
-template <int BRICK>
+// LIN (compile time): the unit-cube linear specialisation (cone 0, one cascade); otherwise the cascaded march with the
+// volume's StepSpace constants (the same float expressions as the cone forms, so the same bits, without their logs)
+template <int BRICK, bool LIN>
 __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, float* __restrict__ tscr) {
     extern __shared__ uint32_t occ_lds[];
     if constexpr (BRICK == 1) stage_occ_brick(occ_lds, a.vol.occ_brick, a.vol.occ_brick_words);
@@ -59,27 +61,35 @@ __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, Tra
     const f3 dn = normalize(ray.d);
     const aabb box = a.vol.train_aabb;
     float tmin = fmaxf(aabb_entry(box, ray.o, dn), 0.0f);      // aabb.ray_intersect(...).x, clamped at 0
-    const float cone = a.vol.cone;
-    const float startt = advance_n_steps(tmin, cone, rng.next_float());
+    const StepSpace& ss = a.vol.ss;
+    const float startt = LIN ? advance_n_steps(tmin, 0.0f, rng.next_float()) : advance_n_steps(tmin, ss, rng.next_float());
     const f3 idir = inv(dn);
     uint32_t j = 0;
     float t = startt;
     f3 pos;
     // unit-cube scenes (cone 0, one cascade): the exact linear specialisation of the occupancy test and
     // of advance_to_next_voxel that the render marcher uses (sng_math.h, tests/test_host_fastpaths.py)
-    const bool lin = BRICK != 0 || (a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_linear != nullptr);
+    static_assert(BRICK == 0 || LIN, "the brick forms are unit-cube only");
     const f3 hs = half_sign(dn);
     float* const ts = tscr + ii;
     OccCache oc;
     while (live && aabb_contains(box, pos = ray.o + t * dn) && j < NERF_STEPS) {
-        const float dt = calc_dt(t, cone);
+        const float dt = LIN ? calc_dt(t, 0.0f) : calc_dt(t, ss);
         bool occ;
         // the cached forms reload a word only when the position leaves the last one (~4.6 samples per cell): each trip
         // is a dependent load otherwise, and a batch has too few rays to hide that latency
         if constexpr (BRICK != 0) occ = occupied_brick_c(pos, bricks, oc);
-        else occ = lin ? occupied_linear_c(pos, a.vol.occ_linear, oc) : occupied_at(pos, a.vol.bitfield, mip_from_dt(dt, pos, a.vol.max_mip));
-        if (occ) { ts[(size_t)j * a.n_rays] = t; ++j; t += dt; }
-        else t = lin ? dda_step_linear(t, pos, idir, hs) : advance_to_next_voxel(t, cone, pos, dn, idir, mip_from_dt(dt, pos, a.vol.max_mip));
+        else if constexpr (LIN) occ = occupied_linear_c(pos, a.vol.occ_linear, oc);
+        else occ = occupied_at(pos, a.vol.bitfield, mip_from_dt(dt, pos, a.vol.max_mip));
+        // one trip is one sample or one DDA step, as a select: with an if / else the compiler nests a loop of DDA steps
+        // inside the sample loop, and a wave then waits at every sample for its lanes' longest run of empty cells
+        // (measured 3.4x slower)
+        float t_skip;
+        if constexpr (LIN) t_skip = dda_step_linear(t, pos, idir, hs);
+        else t_skip = advance_to_next_voxel(t, ss, pos, dn, idir, mip_from_dt(dt, pos, a.vol.max_mip));
+        if (occ) ts[(size_t)j * a.n_rays] = t;
+        j += occ ? 1u : 0u;
+        t = occ ? t + dt : t_skip;
     }
     if (a.debug && live) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
     const uint32_t numsteps = j;
@@ -99,7 +109,7 @@ __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, Tra
         const f3 p = ray.o + tk * dn;
         const f3 wp = (p - box.lo) / diag;   // warp_position = aabb.relative_pos
         float* c = co + (size_t)k * 7;
-        c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(calc_dt(tk, cone)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+        c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(LIN ? calc_dt(tk, 0.0f) : calc_dt(tk, ss)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
     }
 }
 
@@ -742,12 +752,15 @@ void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, h
 }
 void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, float* tscr, hipStream_t s) {
     const dim3 grid((a.n_rays + 63) / 64);
-    if (a.gen_bricks && a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_brick_words && a.vol.occ_brick_words * 4u <= 64u * 1024u)
-        hipLaunchKernelGGL(train_generate_kernel<1>, grid, dim3(64), a.vol.occ_brick_words * 4, s, a, im, b, rng, tscr);
-    else if (a.gen_bricks && a.vol.linear && a.vol.max_mip == 0 && a.vol.occ_brick_g)
-        hipLaunchKernelGGL(train_generate_kernel<2>, grid, dim3(64), 0, s, a, im, b, rng, tscr);
+    const bool lin = a.vol.linear && a.vol.max_mip == 0 && a.vol.cone <= 1e-5f;
+    if (a.gen_bricks && lin && a.vol.occ_brick_words && a.vol.occ_brick_words * 4u <= 64u * 1024u)
+        hipLaunchKernelGGL((train_generate_kernel<1, true>), grid, dim3(64), a.vol.occ_brick_words * 4, s, a, im, b, rng, tscr);
+    else if (a.gen_bricks && lin && a.vol.occ_brick_g)
+        hipLaunchKernelGGL((train_generate_kernel<2, true>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
+    else if (lin && a.vol.occ_linear)
+        hipLaunchKernelGGL((train_generate_kernel<0, true>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
     else
-        hipLaunchKernelGGL(train_generate_kernel<0>, grid, dim3(64), 0, s, a, im, b, rng, tscr);
+        hipLaunchKernelGGL((train_generate_kernel<0, false>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
 }
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
     (void)hipMemsetAsync(b.rayrec, 0, (size_t)a.n_rays * 48, s);
