@@ -118,51 +118,46 @@ __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, Tra
 // SRGB colour space (train_in_linear_colors = false), random background colour, no envmap,
 // error map, sharpness, exposure or depth supervision
 // ---------------------------------------------------------------------------------------------
+// 16 lanes per ray (LOSS_G): the lanes form 16 samples' colours and opacities at once (logistic, exp -- the bulk of the
+// work), and the group then runs the serial transmittance chain over them, one sample per trip, from shuffled values:
+// the chain is the reference's float sequence (weight = alpha T, rgb_ray += weight rgb, T *= 1 - alpha, the EPSILON
+// stop before each sample), and the lane that owns a sample writes its partial.  (One lane per ray left the chain's
+// per-sample math on the critical path of the longest ray: 0.20 ms per batch.)
+constexpr uint32_t LOSS_G = 16;
 __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, const float* __restrict__ mean_density) {
-    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / LOSS_G;
     const int lane = threadIdx.x & 63;
-    const bool in = i0 < b.ctrl->ray_counter;   // the lanes past the last ray stay for the wave's reservation (cn = 0)
-    const uint32_t i = in ? i0 : 0u;
+    const uint32_t gl = (uint32_t)lane % LOSS_G, g0 = (uint32_t)lane - gl;   // lane within the ray's group, the group's first lane
+    const bool in = gi < b.ctrl->ray_counter;   // the groups past the last ray stay for the wave's reservation (cn = 0)
+    const uint32_t i = in ? gi : 0u;
     const uint2 ns = in ? b.numsteps[i] : make_uint2(0u, 0u);
     const uint32_t numsteps = ns.x, base = ns.y;
     const float* __restrict__ cin = b.coords + (size_t)base * 7;
     const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
-    const aabb box = a.vol.train_aabb;
-    const f3 diag = box.hi - box.lo;
-    const float4 ro4 = b.rays[2 * i];
-    const f3 ray_o = mk(ro4.x, ro4.y, ro4.z);
     float T = 1.0f;
     const float EPSILON = 1e-4f;
     f3 rgb_ray = splat(0.0f);
     uint32_t cn = 0;
-    // the per-ray chain is serial in T; the loads of the next LOSS_AHEAD samples are independent of it
-    // and are issued as one batch (few rays per batch leave most of the GPU idle, so the chain's memory
-    // latency is the cost)
-    constexpr uint32_t LOSS_AHEAD = 4;
     bool stop = false;
-    for (; cn < numsteps && !stop;) {
-        float dtw[LOSS_AHEAD];
-        uint2 ow[LOSS_AHEAD];
-#pragma unroll
-        for (uint32_t u = 0; u < LOSS_AHEAD; ++u) {
-            const uint32_t j = min(cn + u, numsteps - 1);
-            dtw[u] = cin[(size_t)j * 7 + 3];
-            ow[u] = *reinterpret_cast<const uint2*>(nout + (size_t)j * 4);
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < LOSS_AHEAD; ++u) {
-            if (cn >= numsteps) break;
+    for (uint32_t c0 = 0; c0 < numsteps && !stop; c0 += LOSS_G) {
+        const uint32_t j = min(c0 + gl, numsteps - 1);
+        const uint2 ow = *reinterpret_cast<const uint2*>(nout + (size_t)j * 4);
+        const float o0 = h2f((uint16_t)(ow.x & 0xffffu)), o1 = h2f((uint16_t)(ow.x >> 16));
+        const float o2 = h2f((uint16_t)(ow.y & 0xffffu)), o3 = h2f((uint16_t)(ow.y >> 16));
+        const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
+        const float dt = unwarp_dt(cin[(size_t)j * 7 + 3]);
+        const float density = sng_expf(o3);
+        const float alpha = 1.0f - sng_expf(-density * dt);
+        for (uint32_t u = 0; u < LOSS_G; ++u) {
+            if (c0 + u >= numsteps) break;
             if (T < EPSILON) { stop = true; break; }
-            const float o0 = h2f((uint16_t)(ow[u].x & 0xffffu)), o1 = h2f((uint16_t)(ow[u].x >> 16));
-            const float o2 = h2f((uint16_t)(ow[u].y & 0xffffu)), o3 = h2f((uint16_t)(ow[u].y >> 16));
-            const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
-            const float dt = unwarp_dt(dtw[u]);
-            const float density = sng_expf(o3);
-            const float alpha = 1.0f - sng_expf(-density * dt);
-            const float weight = alpha * T;
-            rgb_ray = rgb_ray + weight * rgb;
-            b.partial[base + cn] = make_float4(T, rgb_ray.x, rgb_ray.y, rgb_ray.z);   // train_dloss_kernel replays from here
-            T *= (1.0f - alpha);
+            const int src = (int)(g0 + u);
+            const float au = __shfl(alpha, src, 64);
+            const f3 ru = mk(__shfl(rgb.x, src, 64), __shfl(rgb.y, src, 64), __shfl(rgb.z, src, 64));
+            const float weight = au * T;
+            rgb_ray = rgb_ray + weight * ru;
+            if (gl == u) b.partial[base + cn] = make_float4(T, rgb_ray.x, rgb_ray.y, rgb_ray.z);   // train_dloss_kernel replays from here
+            T *= (1.0f - au);
             ++cn;
         }
     }
@@ -186,9 +181,10 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
     }
     if (cn == numsteps) rgb_ray = rgb_ray + T * bg;
 
-    const uint32_t cbase = wave_reserve(&b.ctrl->numsteps_compacted, in ? cn : 0u, lane);
+    uint32_t cbase = wave_reserve(&b.ctrl->numsteps_compacted, in && gl == 0 ? cn : 0u, lane);
+    cbase = __shfl(cbase, (int)g0, 64);
     const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
-    if (!in || ccount == 0) return;
+    if (!in || ccount == 0 || gl != 0) return;
     // Huber loss (alpha = 0.1) / 5, loss_and_gradient (nerf_device.cuh:100-117, 601-616)
     f3 grad;
     float loss_sum = 0.0f;
@@ -764,7 +760,7 @@ void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const 
 }
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
     (void)hipMemsetAsync(b.rayrec, 0, (size_t)a.n_rays * 48, s);
-    hipLaunchKernelGGL(train_loss_kernel, dim3((a.n_rays + 255) / 256), dim3(256), 0, s, a, im, b, rng, mean_density);
+    hipLaunchKernelGGL(train_loss_kernel, dim3((a.n_rays * LOSS_G + 255) / 256), dim3(256), 0, s, a, im, b, rng, mean_density);
     hipLaunchKernelGGL(train_dloss_kernel, dim3((a.n_rays + 3) / 4), dim3(256), 0, s, a, b);
     hipLaunchKernelGGL(train_rollover_kernel, dim3((a.target_batch + 255) / 256), dim3(256), 0, s, a, b);
 }
