@@ -423,6 +423,7 @@ const std::map<std::string, double>& default_params() {
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
         {"train_gen_bricks", 0},                // training generator's occupancy: 0 the linear words (measured fastest, tools/train_ab.py), 1 the OccBrick blob (LDS when it fits, else global)
+        {"train_gen_lanes", 8},                 // lanes per ray of the training generator's speculative march (8 or 16; 1: one lane per ray; tools/train_ab.py)
         {"train_kernel_times", 0},              // 1: sng_train times the stages of every step with HIP events (sng_train_stats.ms_*)
         {"render_with_lens_distortion", 0},     // Testbed::Nerf::render_with_lens_distortion (testbed_nerf.cu:2504): NeRF rays through
                                                 //   render_lens (sng_set_render_lens; the snapshot dataset's first lens)
@@ -590,7 +591,7 @@ struct sng_ctx {
         std::vector<Lens> h_lens;
         DevBuf master, grads, m1, m2, steps, ema, p_train, p_infer, wfrag_train, wfrag_t;
         DevBuf grid, grid_tmp, grid_coords, grid_idx, grid_out;
-        DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts, partial, rayrec;
+        DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts, partial, rayrec, cnt_i, cbase_i;
         uint32_t target = 1u << 18;                    // m_training_batch_size (testbed.h:1103)
         float last_loss = 0.0f;
     } tr;
@@ -2024,6 +2025,7 @@ void train_reset(sng_ctx* c, uint64_t seed) {
     t.coords_c.ensure((size_t)target * 28); t.dloss.ensure((size_t)target * 8); t.loss.ensure(max_rays * 4);
     t.acts.ensure((size_t)((target + 15) / 16) * TRAIN_FEATS * 16 * 2);
     t.partial.ensure((size_t)max_samples * 16); t.rayrec.ensure(max_rays * 48);
+    t.cnt_i.ensure(max_rays * 4); t.cbase_i.ensure(max_rays * 4);
     // the bitfield the training marcher reads (density grid -> bitfield after every update)
     c->d_grid_f32.ensure((size_t)n_cells * 4);
     c->d_partial.ensure(1024 * sizeof(double));
@@ -2083,13 +2085,15 @@ TrainStepArgs train_args(sng_ctx* c) {
     a.near_distance = 0.1f;
     a.debug = c->p("train_debug") != 0.0 ? 1 : 0;
     a.gen_bricks = c->p("train_gen_bricks") != 0.0 ? 1 : 0;
+    a.gen_lanes = (int)c->p("train_gen_lanes");
     return a;
 }
 
 TrainBatch train_batch(sng_ctx* c) {
     auto& t = c->tr;
     return {t.ctrl.as<TrainCtrl>(), t.ray_indices.as<uint32_t>(), t.rays.as<float4>(), t.numsteps.as<uint2>(), t.coords.as<float>(), t.mlp_out.as<uint16_t>(),
-            t.coords_c.as<float>(), t.dloss.as<uint16_t>(), t.loss.as<float>(), t.acts.as<uint16_t>(), t.partial.as<float4>(), t.rayrec.as<float4>()};
+            t.coords_c.as<float>(), t.dloss.as<uint16_t>(), t.loss.as<float>(), t.acts.as<uint16_t>(), t.partial.as<float4>(), t.rayrec.as<float4>(),
+            t.cnt_i.as<uint32_t>(), t.cbase_i.as<uint32_t>()};
 }
 
 // train_nerf_step (3532-3780) up to the gradients; stage > 0 stops early (parity hooks):

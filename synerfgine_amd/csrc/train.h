@@ -146,6 +146,7 @@ struct TrainStepArgs {
     float near_distance;     // 0.1
     int debug;               // generate: per-ray step count / entry distances into loss / coords_c
     int gen_bricks;          // generate's unit-cube occupancy source: 1 bricks (LDS when staged, else global), 0 linear words
+    int gen_lanes;           // lanes per ray of the generator's speculative march (8, 16; else one lane per ray)
 };
 
 // per-batch buffers
@@ -162,6 +163,8 @@ struct TrainBatch {
     uint16_t* acts;          // [target/16][TRAIN_FEATS][16] fp16
     float4* partial;         // [max_samples] {T before the sample, running rgb after it} (train_loss_kernel)
     float4* rayrec;          // [n_rays][3] {cbase, ccount, base, -} {grad, loss_scale} {rgb_ray, l1_reg} (train_dloss_kernel)
+    uint32_t* cnt_i;         // [n_rays] composited samples per ray, by the ray's image index (train_compact_kernel)
+    uint32_t* cbase_i;       // [n_rays] its compaction slot (exclusive prefix of cnt_i)
 };
 
 // feature rows of the tiled activation / gradient buffer

@@ -113,6 +113,101 @@ __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, Tra
     }
 }
 
+// The same march with G lanes per ray (train_gen_lanes): each trip of the group speculates G steps of the current kind
+// and tests their cells together.  In sample mode lane k takes k further samples from t (t += calc_dt(t), the serial
+// chain's own float sequence, k times) and tests the cell at its position; the group keeps the samples before the
+// first lane whose cell is empty (or that left the box / reached NERF_STEPS), and that lane's position takes the DDA
+// step.  In DDA mode lane k takes k further DDA steps and the group continues from the first lane whose cell is
+// occupied.  Every t is the one the serial march reaches, so the samples are the same; only the number of dependent
+// trips drops (one trip per ~G samples in occupied stretches, where the longest rays spend most of their march).
+template <bool LIN, int G>
+__global__ __launch_bounds__(64) void train_generate_spec_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, float* __restrict__ tscr) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t gl = (uint32_t)lane % G, g0 = (uint32_t)lane - gl;
+    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << g0;
+    const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const bool in = i < a.n_rays;
+    const uint32_t ii = in ? i : 0u;
+    const uint32_t img = ((ii * im.n) / a.n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
+    rng.advance((uint64_t)ii * N_MAX_RANDOM_SAMPLES_PER_RAY);
+    const f2 uv = train_image_pos(rng, im);
+    const bool live = in && !(read_rgba(im, img, uv).x < 0.0f);   // masked pixel: no samples
+    (void)rng.next_float();                                    // motionblur_time
+    const TrainRay ray = train_ray(im, img, uv);
+    const f3 dn = normalize(ray.d);
+    const aabb box = a.vol.train_aabb;
+    const float tmin = fmaxf(aabb_entry(box, ray.o, dn), 0.0f);
+    const StepSpace& ss = a.vol.ss;
+    const float startt = LIN ? advance_n_steps(tmin, 0.0f, rng.next_float()) : advance_n_steps(tmin, ss, rng.next_float());
+    const f3 idir = inv(dn);
+    const f3 hs = half_sign(dn);
+    auto step_dt = [&](float t) { return LIN ? calc_dt(t, 0.0f) : calc_dt(t, ss); };
+    auto skip = [&](float t, f3 p) {
+        if constexpr (LIN) return dda_step_linear(t, p, idir, hs);
+        else return advance_to_next_voxel(t, ss, p, dn, idir, mip_from_dt(step_dt(t), p, a.vol.max_mip));
+    };
+    auto occupied = [&](float t, f3 p) {
+        if constexpr (LIN) return occupied_linear(p, a.vol.occ_linear);
+        else return occupied_at(p, a.vol.bitfield, mip_from_dt(step_dt(t), p, a.vol.max_mip));
+    };
+    float* const ts = tscr + ii;
+    uint32_t j = 0;
+    float t = startt;
+    bool dda = false, done = !live;   // uniform over the group
+    while (!done) {
+        float tk = t;
+        if (!dda) {
+            for (uint32_t u = 0; u < gl; ++u) tk = tk + step_dt(tk);
+        } else {
+            for (uint32_t u = 0; u < gl; ++u) tk = skip(tk, ray.o + tk * dn);
+        }
+        const f3 pk = ray.o + tk * dn;
+        const bool ink = aabb_contains(box, pk) && (dda ? j : j + gl) < NERF_STEPS;
+        const bool occk = ink && occupied(tk, pk);
+        const bool stopk = dda ? (!ink || occk) : !occk;
+        const uint64_t sb = __ballot(stopk) & gmask;
+        const uint32_t m = sb ? (uint32_t)(__ffsll((long long)sb) - 1) - g0 : (uint32_t)G;
+        if (!dda) {
+            if (gl < m) ts[(size_t)(j + gl) * a.n_rays] = tk;
+            j += m;
+        }
+        if (m == (uint32_t)G) {   // every lane continued the kind: the next trip starts after lane G - 1
+            const float tl = __shfl(tk, (int)(g0 + G - 1), 64);
+            t = dda ? skip(tl, ray.o + tl * dn) : tl + step_dt(tl);
+            continue;
+        }
+        const float tm = __shfl(tk, (int)(g0 + m), 64);
+        const bool inm = __shfl((int)ink, (int)(g0 + m), 64) != 0;
+        if (!inm) { done = true; continue; }
+        if (!dda) { t = skip(tm, ray.o + tm * dn); dda = true; }   // an empty cell inside: its DDA step
+        else { t = tm; dda = false; }                              // an occupied cell: samples from here
+    }
+    if (a.debug && live && gl == 0) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
+    const uint32_t numsteps = j;
+    uint32_t base = wave_reserve(&b.ctrl->numsteps_counter, gl == 0 ? numsteps : 0u, lane);
+    base = __shfl(base, (int)g0, 64);
+    const bool keep = numsteps > 0 && base + numsteps <= a.max_samples;
+    uint32_t ray_idx = wave_reserve(&b.ctrl->ray_counter, gl == 0 && keep ? 1u : 0u, lane);
+    ray_idx = __shfl(ray_idx, (int)g0, 64);
+    if (!keep) return;
+    if (gl == 0) {
+        b.ray_indices[ray_idx] = i;
+        b.rays[2 * ray_idx] = make_float4(ray.o.x, ray.o.y, ray.o.z, 0.0f);
+        b.rays[2 * ray_idx + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
+        b.numsteps[ray_idx] = make_uint2(numsteps, base);
+    }
+    const f3 wd = (dn + 1.0f) * 0.5f;   // warp_direction
+    const f3 diag = box.hi - box.lo;
+    float* co = b.coords + (size_t)base * 7;
+    for (uint32_t k = gl; k < numsteps; k += G) {
+        const float tk = ts[(size_t)k * a.n_rays];
+        const f3 p = ray.o + tk * dn;
+        const f3 wp = (p - box.lo) / diag;   // warp_position = aabb.relative_pos
+        float* c = co + (size_t)k * 7;
+        c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(step_dt(tk)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // compute_loss_kernel_train_nerf (testbed_nerf.cu:1000-1313): Logistic rgb / Exponential density,
 // SRGB colour space (train_in_linear_colors = false), random background colour, no envmap,
@@ -180,11 +275,9 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
         target = bg;
     }
     if (cn == numsteps) rgb_ray = rgb_ray + T * bg;
-
-    uint32_t cbase = wave_reserve(&b.ctrl->numsteps_compacted, in && gl == 0 ? cn : 0u, lane);
-    cbase = __shfl(cbase, (int)g0, 64);
-    const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
-    if (!in || ccount == 0 || gl != 0) return;
+    if (!in || gl != 0) return;
+    // the compaction slot comes from train_compact_kernel (a prefix of the composited counts in the rays' image order)
+    b.cnt_i[ray_idx] = cn;
     // Huber loss (alpha = 0.1) / 5, loss_and_gradient (nerf_device.cuh:100-117, 601-616)
     f3 grad;
     float loss_sum = 0.0f;
@@ -206,9 +299,46 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
     const float l1_reg_density = *mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
     // the per-sample gradients need only this ray's constants and the forward partials: they are
     // written by train_dloss_kernel with one wave per ray instead of this lane's serial loop
-    b.rayrec[3 * i] = make_float4(__uint_as_float(cbase), __uint_as_float(ccount), __uint_as_float(base), 0.0f);
+    b.rayrec[3 * i] = make_float4(0.0f, 0.0f, __uint_as_float(base), 0.0f);   // slot and count: train_finalize_kernel
     b.rayrec[3 * i + 1] = make_float4(grad.x, grad.y, grad.z, loss_scale);
     b.rayrec[3 * i + 2] = make_float4(rgb_ray.x, rgb_ray.y, rgb_ray.z, l1_reg_density);
+}
+
+// The compaction of the composited samples into the batch (testbed_nerf.cu:1150: an atomicAdd per ray, so the reference
+// fills the batch in the order its threads finish): here an exclusive prefix over the rays in their image order (the
+// random pixel index i of generate_training_samples_nerf), so which rays make the batch does not depend on how fast each
+// ray's march or composite ran.  (A completion order favours the short rays whenever the batch overflows its target: with
+// 4 rays per wave in the loss kernel that bias was strong enough to collapse the density field within 200 steps.)  One
+// workgroup: ~10^4 rays.
+__global__ __launch_bounds__(1024) void train_compact_kernel(uint32_t n, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ cbase, TrainCtrl* ctrl) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (n + 1023u) / 1024u, t0 = threadIdx.x * per, t1 = min(n, t0 + per);
+    uint32_t sum = 0;
+    for (uint32_t k = t0; k < t1; ++k) sum += cnt[k];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {   // Hillis-Steele inclusive scan of the thread sums
+        const uint32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (uint32_t k = t0; k < t1; ++k) { cbase[k] = run; run += cnt[k]; }
+    if (threadIdx.x == 1023) ctrl->numsteps_compacted = part[1023];
+}
+__global__ __launch_bounds__(256) void train_finalize_kernel(TrainStepArgs a, TrainBatch b) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.ctrl->ray_counter) return;
+    const uint32_t ri = b.ray_indices[i], cn = b.cnt_i[ri], cbase = b.cbase_i[ri];
+    const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
+    if (ccount == 0) {   // past the batch target: no loss and no gradient for this ray (testbed_nerf.cu: compacted_numsteps == 0)
+        b.rayrec[3 * i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        b.loss[i] = 0.0f;
+        return;
+    }
+    b.rayrec[3 * i].x = __uint_as_float(cbase);
+    b.rayrec[3 * i].y = __uint_as_float(ccount);
 }
 
 // compute_loss_kernel_train_nerf's gradient loop (testbed_nerf.cu:1209-1275) for the ray's first
@@ -753,14 +883,26 @@ void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const 
         hipLaunchKernelGGL((train_generate_kernel<1, true>), grid, dim3(64), a.vol.occ_brick_words * 4, s, a, im, b, rng, tscr);
     else if (a.gen_bricks && lin && a.vol.occ_brick_g)
         hipLaunchKernelGGL((train_generate_kernel<2, true>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
-    else if (lin && a.vol.occ_linear)
+    else if (a.gen_lanes == 8 || a.gen_lanes == 16) {
+        const dim3 g2((a.n_rays * (uint32_t)a.gen_lanes + 63) / 64);
+        if (lin && a.vol.occ_linear) {
+            if (a.gen_lanes == 8) hipLaunchKernelGGL((train_generate_spec_kernel<true, 8>), g2, dim3(64), 0, s, a, im, b, rng, tscr);
+            else hipLaunchKernelGGL((train_generate_spec_kernel<true, 16>), g2, dim3(64), 0, s, a, im, b, rng, tscr);
+        } else {
+            if (a.gen_lanes == 8) hipLaunchKernelGGL((train_generate_spec_kernel<false, 8>), g2, dim3(64), 0, s, a, im, b, rng, tscr);
+            else hipLaunchKernelGGL((train_generate_spec_kernel<false, 16>), g2, dim3(64), 0, s, a, im, b, rng, tscr);
+        }
+    } else if (lin && a.vol.occ_linear)
         hipLaunchKernelGGL((train_generate_kernel<0, true>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
     else
         hipLaunchKernelGGL((train_generate_kernel<0, false>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
 }
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
     (void)hipMemsetAsync(b.rayrec, 0, (size_t)a.n_rays * 48, s);
+    (void)hipMemsetAsync(b.cnt_i, 0, (size_t)a.n_rays * 4, s);
     hipLaunchKernelGGL(train_loss_kernel, dim3((a.n_rays * LOSS_G + 255) / 256), dim3(256), 0, s, a, im, b, rng, mean_density);
+    hipLaunchKernelGGL(train_compact_kernel, dim3(1), dim3(1024), 0, s, a.n_rays, b.cnt_i, b.cbase_i, b.ctrl);
+    hipLaunchKernelGGL(train_finalize_kernel, dim3((a.n_rays + 255) / 256), dim3(256), 0, s, a, b);
     hipLaunchKernelGGL(train_dloss_kernel, dim3((a.n_rays + 3) / 4), dim3(256), 0, s, a, b);
     hipLaunchKernelGGL(train_rollover_kernel, dim3((a.target_batch + 255) / 256), dim3(256), 0, s, a, b);
 }

@@ -114,8 +114,8 @@ def test_snapshot_round_trip_and_training_resume(data, tmp_path):
         # (measured update differences 2e-8 .. 0.7 between two runs of the same state). The optimizer state
         # carries the run: Adam's second moment after the step is 0.99 v_prev + 0.01 g^2 (first: 0.9 m_prev +
         # 0.1 g), so the resumed moments stay next to the uninterrupted ones whatever the batch, while the
-        # restarted ones (v_prev = m_prev = 0) do not. Measured: v 1e-7 / m 6e-8 (same batch), m 0.41 / v 0.21
-        # (another batch) vs 1.0 restarted.
+        # restarted ones (v_prev = m_prev = 0) do not. Measured: v 1e-7 / m 6e-8 (same batch), m 0.41 (another
+        # batch) vs 1.0 restarted.
         c, _ = _testbed(data)
         c.load_snapshot(p_plain)
         c.set_training_dataset(imgs, xf, focal, pp)
@@ -132,7 +132,7 @@ def test_snapshot_round_trip_and_training_resume(data, tmp_path):
         rel_ab_v, rel_ac_v = rel(va, vb), rel(va, vc)
         print("resume: update rel. difference", rel_ab, "vs without optimizer state", rel_ac,
               "| Adam m1 (MLP)", rel_ab_m, "vs", rel_ac_m, "| Adam v (MLP)", rel_ab_v, "vs", rel_ac_v)
-        assert rel_ac_v > 0.5 and rel_ab_v < 0.5 * rel_ac_v, (rel_ab_v, rel_ac_v)
+        assert rel_ac_v > 0.5 and rel_ab_v < 0.2 * rel_ac_v, (rel_ab_v, rel_ac_v)
         assert rel_ab_m < 0.75 * rel_ac_m, (rel_ab_m, rel_ac_m)
         assert rel_ab < 0.5 * rel_ac, (rel_ab, rel_ac)
     finally:
