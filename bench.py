@@ -357,7 +357,7 @@ def train_leg(steps=200, warmup=50, seed=1337, engine_params=None):
                                 "note": "Ema(ExpDecay(Adam)) over every param: >= 20 B/param (gradient, master, EMA read; EMA, fp16 training "
                                         "and inference copies written) + 28 B per touched param (moments, step count)"},
                   "generate": {"bound": "latency", "rays": int(st2["rays_per_batch"]),
-                               "note": "one thread per training ray marches the occupancy grid twice (count, then write)"}}
+                               "note": "one march per training ray, 8 lanes per ray speculating 8 steps at a time (train_generate_spec_kernel); the samples then written in the batch slot the ray reserved"}}
         return {"steps_per_s": round(steps / el, 1), "ms_per_step": round(1e3 * el / steps, 3),
                 "ms_per_step_device": round(st["ms"] / steps, 3), "steps": steps, "warmup": warmup,
                 "batch_target": 1 << 18, "measured_batch": samples, "rays_per_batch": int(st["rays_per_batch"]),

@@ -195,20 +195,31 @@ class Testbed:
 
 
 class FrameResult:
+    """sng_frame_result of one frame.  The fields are read from the C struct when first used (a frame loop that does not
+    look at them pays no Python time between frames, when the GPU has nothing queued)."""
+    _SCALARS = frozenset(("n_iterations", "n_hit", "n_samples", "n_reference_slots", "ms_frame", "ms_raytrace", "ms_nerf", "ms_shadow",
+                          "ms_overlay", "ms_network", "network_launches",
+                          "fused_from_iter", "n_samples_network", "ms_fused_tail", "n_samples_reused",
+                          "onestep_from_iter", "onestep_iterations", "ms_onestep", "onestep_field_evals", "spec_rounds", "spec_evals",
+                          "spec_exec", "msr_rounds", "msr_evals", "msr_exec", "sched_reductions"))
+
     def __init__(self, engine, r):
         self._engine = engine
         self.raw = r
-        for name in ("n_iterations", "n_hit", "n_samples", "n_reference_slots", "ms_frame", "ms_raytrace", "ms_nerf", "ms_shadow",
-                     "ms_overlay", "ms_network", "network_launches",
-                     "fused_from_iter", "n_samples_network", "ms_fused_tail", "n_samples_reused",
-                     "onestep_from_iter", "onestep_iterations", "ms_onestep", "onestep_field_evals", "spec_rounds", "spec_evals",
-                     "spec_exec", "msr_rounds", "msr_evals", "msr_exec", "sched_reductions"):
-            setattr(self, name, getattr(r, name))
-        self.alive_per_iter = list(r.alive_per_iter)[: min(64, r.n_iterations)]
-        self.steps_per_iter = list(r.steps_per_iter)[: min(64, r.n_iterations)]
-        self.samples_per_iter = list(r.samples_per_iter)[: min(64, r.n_iterations)]
-        # per network launch (collect_kernel_times): (samples the launch evaluated, its duration in ms)
-        self.network_launch = [(int(r.samples_network_launch[k]), float(r.ms_network_launch[k])) for k in range(r.n_launch_rec)]
+
+    def __getattr__(self, name):   # only for names not set on the instance
+        r = self.__dict__["raw"]
+        if name in FrameResult._SCALARS:
+            v = getattr(r, name)
+        elif name in ("alive_per_iter", "steps_per_iter", "samples_per_iter"):
+            v = list(getattr(r, name))[: min(64, r.n_iterations)]
+        elif name == "network_launch":
+            # per network launch (collect_kernel_times): (samples the launch evaluated, its duration in ms)
+            v = [(int(r.samples_network_launch[k]), float(r.ms_network_launch[k])) for k in range(r.n_launch_rec)]
+        else:
+            raise AttributeError(name)
+        self.__dict__[name] = v
+        return v
 
     def download(self, name):
         """Copy a device output buffer to host as float32 [H, W, C]."""

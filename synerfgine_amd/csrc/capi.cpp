@@ -1606,7 +1606,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // timing events recorded by the network kernel's own dispatch (hipExtLaunchKernelGGL)
             launch_network(c->net, c->coords.as<float>(), 7, 0, &ctrl->n_samples[p], c->net_out.as<uint16_t>(), 1, max_tiles, c->s_nerf,
                            P.collect_kernel_times ? c->net_events[2 * net_launches] : nullptr,
-                           P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr);
+                           P.collect_kernel_times ? c->net_events[2 * net_launches + 1] : nullptr, net_rec(net_launches));
             if (probe)   // Normals / EncodingVis: input gradient or activation into the coordinates (testbed_nerf.cu:2363-2366)
                 launch_field_probe(c->net, c->d_params.as<uint16_t>(), c->coords.as<float>(), &ctrl->n_samples[p], mode.render_mode,
                                    (int)c->p("visualized_layer"), (int)c->p("visualized_dimension"), c->s_nerf);
