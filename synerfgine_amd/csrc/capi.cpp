@@ -423,6 +423,8 @@ const std::map<std::string, double>& default_params() {
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
         {"train_gen_bricks", 0},                // training generator's occupancy: 0 the linear words (measured fastest, tools/train_ab.py), 1 the OccBrick blob (LDS when it fits, else global)
+        {"train_dw_pipe", 1},                   // dW kernel: the next tile's operands in flight during the current tile's MFMAs (0: load, then multiply)
+        {"train_dw_blocks_per_cu", 2},          // dW kernel: workgroups per CU (tools/train_ab.py)
         {"train_gen_lanes", 8},                 // lanes per ray of the training generator's speculative march (8 or 16; 1: one lane per ray; tools/train_ab.py)
         {"train_kernel_times", 0},              // 1: sng_train times the stages of every step with HIP events (sng_train_stats.ms_*)
         {"render_with_lens_distortion", 0},     // Testbed::Nerf::render_with_lens_distortion (testbed_nerf.cu:2504): NeRF rays through
@@ -2086,6 +2088,8 @@ TrainStepArgs train_args(sng_ctx* c) {
     a.debug = c->p("train_debug") != 0.0 ? 1 : 0;
     a.gen_bricks = c->p("train_gen_bricks") != 0.0 ? 1 : 0;
     a.gen_lanes = (int)c->p("train_gen_lanes");
+    a.dw_pipe = c->p("train_dw_pipe") != 0.0 ? 1 : 0;
+    a.dw_blocks_per_cu = std::max(1, (int)c->p("train_dw_blocks_per_cu"));
     return a;
 }
 

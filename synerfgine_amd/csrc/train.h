@@ -147,6 +147,8 @@ struct TrainStepArgs {
     int debug;               // generate: per-ray step count / entry distances into loss / coords_c
     int gen_bricks;          // generate's unit-cube occupancy source: 1 bricks (LDS when staged, else global), 0 linear words
     int gen_lanes;           // lanes per ray of the generator's speculative march (8, 16; else one lane per ray)
+    int dw_pipe;             // dW kernel: 1 = the next tile's operands loaded while the current tile's MFMAs run
+    int dw_blocks_per_cu;    // dW kernel: workgroups per CU (each adds its partial sums to the gradient once)
 };
 
 // per-batch buffers

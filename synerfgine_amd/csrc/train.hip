@@ -678,27 +678,65 @@ __device__ __forceinline__ DwJob dw_job(int blk) {
     const int b = blk - 36;
     return {D_DENS, A_H0, 0, b, 64, 64 * 32};
 }
+template <bool PIPE>
 __global__ __launch_bounds__(320) void train_dw_kernel(TrainStepArgs a, const uint16_t* __restrict__ acts, uint32_t tiles_per_block, float* __restrict__ wgrad) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;   // 5 waves x 8 blocks
     const uint32_t n_tiles = (a.target_batch + 15) >> 4;
     const uint32_t t0 = blockIdx.x * tiles_per_block, t1 = min(n_tiles, t0 + tiles_per_block);
     const int r = lane & 15, kq = lane >> 4;
     f4v acc[8];
-    DwJob job[8];
+    uint32_t oa[8], ob[8];   // the job's A / B operand offsets inside a tile
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { acc[j] = f4v{0.0f, 0.0f, 0.0f, 0.0f}; job[j] = dw_job(wv * 8 + j); }
-    for (uint32_t t = t0; t < t1; ++t) {
-        const uint16_t* tb = acts + (size_t)t * TRAIN_FEATS * 16;
+    for (int j = 0; j < 8; ++j) {
+        acc[j] = f4v{0.0f, 0.0f, 0.0f, 0.0f};
+        const DwJob jb = dw_job(wv * 8 + j);
+        oa[j] = (uint32_t)((jb.dfeat + 16 * jb.mb + r) * 16 + 4 * kq);
+        ob[j] = (uint32_t)((jb.afeat + 16 * jb.nb + r) * 16 + 4 * kq);
+    }
+    if constexpr (PIPE) {
+        // two register sets used in turn: the loads of the next tile are issued before the current tile's 8 MFMAs,
+        // and no copy between the sets waits on them (the last trips reload the last tile and multiply nothing twice)
+        if (t0 < t1) {
+            h4v A0[8], B0[8], A1[8], B1[8];
+            auto load = [&](uint32_t t, h4v* A, h4v* B) {
+                const uint16_t* tb = acts + (size_t)min(t, t1 - 1) * TRAIN_FEATS * 16;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const h4v A = *reinterpret_cast<const h4v*>(tb + (job[j].dfeat + 16 * job[j].mb + r) * 16 + 4 * kq);
-            const h4v B = *reinterpret_cast<const h4v*>(tb + (job[j].afeat + 16 * job[j].nb + r) * 16 + 4 * kq);
-            acc[j] = mfma16k16(A, B, acc[j]);
+                for (int j = 0; j < 8; ++j) { A[j] = *reinterpret_cast<const h4v*>(tb + oa[j]); B[j] = *reinterpret_cast<const h4v*>(tb + ob[j]); }
+            };
+            load(t0, A0, B0);
+            // one basic block per trip (a branch between the halves lets the compiler sink the loads to their use);
+            // an odd slab's last half multiplies the reloaded last tile and keeps the old sums (select)
+            for (uint32_t t = t0; t < t1; t += 2) {
+                load(t + 1, A1, B1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[j] = mfma16k16(A0[j], B0[j], acc[j]);
+                __builtin_amdgcn_sched_barrier(0);
+                load(t + 2, A0, B0);
+                __builtin_amdgcn_sched_barrier(0);
+                const bool second = t + 1 < t1;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const f4v r = mfma16k16(A1[j], B1[j], acc[j]);
+                    acc[j] = second ? r : acc[j];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    } else {
+        for (uint32_t t = t0; t < t1; ++t) {
+            const uint16_t* tb = acts + (size_t)t * TRAIN_FEATS * 16;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const h4v A = *reinterpret_cast<const h4v*>(tb + oa[j]);
+                const h4v B = *reinterpret_cast<const h4v*>(tb + ob[j]);
+                acc[j] = mfma16k16(A, B, acc[j]);
+            }
         }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        const DwJob& jb = job[j];
+        const DwJob jb = dw_job(wv * 8 + j);
         for (int k = 0; k < 4; ++k) {
             const int row = 16 * jb.mb + 4 * kq + k, cin = 16 * jb.nb + r;
             atomicAdd(&wgrad[jb.param_off + row * jb.n_in + cin], acc[j][k]);
@@ -922,9 +960,10 @@ void launch_train_field(const TrainStepArgs& a, const TrainBatch& b, const Netwo
 }
 void launch_train_dw(const TrainStepArgs& a, const uint16_t* acts, float* wgrad, uint32_t n_cus, hipStream_t s) {
     const uint32_t tiles = (a.target_batch + 15) / 16;
-    const uint32_t blocks_target = n_cus * 2;
-    const uint32_t per = std::max<uint32_t>(16, (tiles + blocks_target - 1) / blocks_target);
-    hipLaunchKernelGGL(train_dw_kernel, dim3((tiles + per - 1) / per), dim3(320), 0, s, a, acts, per, wgrad);
+    const uint32_t blocks_target = n_cus * (uint32_t)std::max(1, a.dw_blocks_per_cu);
+    const uint32_t per = std::max<uint32_t>(8, (tiles + blocks_target - 1) / blocks_target);
+    if (a.dw_pipe) hipLaunchKernelGGL(train_dw_kernel<true>, dim3((tiles + per - 1) / per), dim3(320), 0, s, a, acts, per, wgrad);
+    else hipLaunchKernelGGL(train_dw_kernel<false>, dim3((tiles + per - 1) / per), dim3(320), 0, s, a, acts, per, wgrad);
 }
 void launch_train_adam(const AdamArgs& o, uint64_t n, uint32_t n_matrix, float* master, const float* grads, float* m1, float* m2, uint32_t* steps, float* ema,
                        uint16_t* p_train, uint16_t* p_infer, hipStream_t s) {

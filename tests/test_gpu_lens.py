@@ -63,7 +63,17 @@ def _generate(T):
     return g, ns, rays, co
 
 
-def test_fox_opencv_train_generate_matches_oracle(fox):
+@pytest.mark.parametrize("lanes", [8, 1, 16], ids=["8_lanes", "one_lane", "16_lanes"])
+def test_fox_opencv_train_generate_matches_oracle(fox, lanes):
+    """The cascaded (aabb_scale 4, cone-stepped) generator in each form (train_gen_lanes) against the oracle, bit-exact."""
+    fox["eng"].set_param("train_gen_lanes", lanes)
+    try:
+        _check_fox_opencv(fox)
+    finally:
+        fox["eng"].set_param("train_gen_lanes", 8)
+
+
+def _check_fox_opencv(fox):
     import oracle as O
     O.set_train_lens(fox["d"]["lenses"])
     g, ns, rays, co = _generate(fox)

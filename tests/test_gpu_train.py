@@ -72,6 +72,23 @@ def _step_state(T, stage):
 
 
 def test_train_generate_matches_oracle(trainer, oracle_lib):
+    _check_generate(trainer, oracle_lib)
+
+
+@pytest.mark.parametrize("lanes,bricks", [(1, 0), (16, 0), (1, 1)], ids=["one_lane", "16_lanes", "lds_bricks"])
+def test_train_generate_variants_match_oracle(trainer, oracle_lib, lanes, bricks):
+    """The generator's other forms (train_gen_lanes 1 / 16, train_gen_bricks 1) against the same oracle, bit-exact."""
+    eng = trainer["eng"]
+    eng.set_param("train_gen_lanes", lanes)
+    eng.set_param("train_gen_bricks", bricks)
+    try:
+        _check_generate(trainer, oracle_lib)
+    finally:
+        eng.set_param("train_gen_lanes", 8)
+        eng.set_param("train_gen_bricks", 0)
+
+
+def _check_generate(trainer, oracle_lib):
     import train_ref as R
     O = oracle_lib
     d = _step_state(trainer, 1)
