@@ -592,6 +592,8 @@ struct sng_ctx {
         DevBuf tscr;                                   // generate's sample distances [NERF_STEPS][rays_per_batch]
         std::vector<Lens> h_lens;
         DevBuf master, grads, m1, m2, steps, ema, p_train, p_infer, wfrag_train, wfrag_t;
+        DevBuf adam_corr;                              // Adam's bias correction per step count (launch_train_adam_corr)
+        uint32_t adam_corr_n = 0;                      // valid entries 1..adam_corr_n
         DevBuf grid, grid_tmp, grid_coords, grid_idx, grid_out;
         DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts, partial, rayrec, cnt_i, cbase_i;
         uint32_t target = 1u << 18;                    // m_training_batch_size (testbed.h:1103)
@@ -2161,6 +2163,18 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
         o.beta1 = 0.9f; o.beta2 = 0.99f; o.epsilon = 1e-15f; o.l2_reg = 1e-6f; o.loss_scale = 128.0f; o.ema_decay = 0.95f; o.ema_step = t.step;
         o.deb_old = 1.0f - std::pow(o.ema_decay, (float)o.ema_step);
         o.deb_new = 1.0f - std::pow(o.ema_decay, (float)(o.ema_step + 1));
+        // per-parameter step counts reach at most t.step + 1 after this update (a larger one forms the factor itself)
+        if (t.adam_corr_n < t.step + 1) {
+            const uint32_t need = t.step + 1;
+            if (t.adam_corr.bytes < (size_t)(need + 1) * 4) {
+                t.adam_corr.ensure(((size_t)need + 4096) / 4096 * 4096 * 4);
+                t.adam_corr_n = 0;
+            }
+            launch_train_adam_corr(t.adam_corr.as<float>(), t.adam_corr_n + 1, need, o.beta1, o.beta2, s);
+            t.adam_corr_n = need;
+        }
+        o.corr = t.adam_corr.as<float>();
+        o.corr_n = t.adam_corr_n;
         launch_train_adam(o, c->n_params, 3072 + 7168, t.master.as<float>(), t.grads.as<float>(), t.m1.as<float>(), t.m2.as<float>(), t.steps.as<uint32_t>(),
                           t.ema.as<float>(), t.p_train.as<uint16_t>(), t.p_infer.as<uint16_t>(), s);
         if (timed) HIPCHK(hipEventRecord(c->train_events[7], s));

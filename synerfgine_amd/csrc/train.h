@@ -177,6 +177,8 @@ struct AdamArgs {
     float lr, beta1, beta2, epsilon, l2_reg, loss_scale, ema_decay;
     uint32_t ema_step;
     float deb_old, deb_new;   // 1 - ema_decay^ema_step, 1 - ema_decay^(ema_step + 1) (host powf, as the oracle)
+    const float* corr;        // [corr_n + 1] Adam's bias correction sqrtf(1 - beta2^s) / (1 - beta1^s) for s = 1..corr_n
+    uint32_t corr_n;
 };
 
 void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, hipStream_t s);
@@ -189,6 +191,8 @@ void launch_train_field(const TrainStepArgs& a, const TrainBatch& b, const Netwo
 void launch_train_dw(const TrainStepArgs& a, const uint16_t* acts, float* wgrad, uint32_t n_cus, hipStream_t s);
 void launch_train_adam(const AdamArgs& o, uint64_t n, uint32_t n_matrix, float* master, const float* grads, float* m1, float* m2, uint32_t* steps, float* ema,
                        uint16_t* p_train, uint16_t* p_infer, hipStream_t s);
+// Adam's bias-correction factor for the per-parameter step counts s = from..to (the expression adam_one would form)
+void launch_train_adam_corr(float* corr, uint32_t from, uint32_t to, float beta1, float beta2, hipStream_t s);
 void launch_train_mark_untrained(uint32_t n, float* grid, const TrainImages& im, int clear_visible, hipStream_t s);
 void launch_train_grid_samples(uint32_t n, Pcg32 rng, uint32_t step, const aabb& box, const float* grid, float* coords, uint32_t* indices, uint32_t n_cascades,
                                float thresh, hipStream_t s);

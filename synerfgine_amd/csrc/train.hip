@@ -750,6 +750,13 @@ __global__ __launch_bounds__(320) void train_dw_kernel(TrainStepArgs a, const ui
 // counts for the bias correction).  Writes the fp32 master, the fp16 training copy and the EMA
 // (debiased) fp16 inference copy.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float adam_corr(float beta1, float beta2, uint32_t step) {
+    return sqrtf(1.0f - powf(beta2, (float)step)) / (1.0f - powf(beta1, (float)step));
+}
+__global__ void train_adam_corr_kernel(float* __restrict__ corr, uint32_t from, uint32_t to, float beta1, float beta2) {
+    const uint32_t s = from + blockIdx.x * blockDim.x + threadIdx.x;
+    if (s <= to) corr[s] = adam_corr(beta1, beta2, s);
+}
 // One parameter's update; `deb_old` / `deb_new` are the EMA debias terms 1 - decay^t, 1 - decay^(t+1) (uniform over the
 // params: formed once per step on the host with the same powf the oracle uses)
 __device__ __forceinline__ void adam_one(const AdamArgs& o, bool matrix, float gsum, float& w, float& m1, float& m2, uint32_t& step, float& e, bool& touched) {
@@ -761,8 +768,9 @@ __device__ __forceinline__ void adam_one(const AdamArgs& o, bool matrix, float g
         const float gsq = gradient * gradient;
         m1 = o.beta1 * m1 + (1.0f - o.beta1) * gradient;
         m2 = o.beta2 * m2 + (1.0f - o.beta2) * gsq;
-        // tcnn adam_step: learning_rate *= sqrtf(1 - beta2^t) / (1 - beta1^t) (the quotient first)
-        const float lr = o.lr * (sqrtf(1.0f - powf(o.beta2, (float)step)) / (1.0f - powf(o.beta1, (float)step)));
+        // tcnn adam_step: learning_rate *= sqrtf(1 - beta2^t) / (1 - beta1^t) (the quotient first); the quotient from the
+        // step-indexed table (train_adam_corr_kernel, the same expression), so no powf per parameter
+        const float lr = o.lr * (step <= o.corr_n ? o.corr[step] : adam_corr(o.beta1, o.beta2, step));
         const float eff = lr / (sqrtf(m2) + o.epsilon);
         w = w - eff * m1;
     }
@@ -970,6 +978,11 @@ void launch_train_adam(const AdamArgs& o, uint64_t n, uint32_t n_matrix, float* 
     const uint64_t groups = (n + 3) / 4;   // every buffer is a hipMalloc allocation (16-B aligned); n_matrix % 4 == 0
     hipLaunchKernelGGL(train_adam_kernel, dim3((uint32_t)((groups + 255) / 256)), dim3(256), 0, s, o, n, n_matrix, master, grads, m1, m2, steps, ema,
                        p_train, p_infer);
+}
+void launch_train_adam_corr(float* corr, uint32_t from, uint32_t to, float beta1, float beta2, hipStream_t s) {
+    if (to < from) return;
+    const uint32_t n = to - from + 1;
+    hipLaunchKernelGGL(train_adam_corr_kernel, dim3((n + 255) / 256), dim3(256), 0, s, corr, from, to, beta1, beta2);
 }
 void launch_train_mark_untrained(uint32_t n, float* grid, const TrainImages& im, int clear_visible, hipStream_t s) {
     hipLaunchKernelGGL(train_mark_untrained_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, grid, im, clear_visible);
