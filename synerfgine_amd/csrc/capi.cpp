@@ -1821,7 +1821,11 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 const uint32_t n_tiles = (uint32_t)((MW + ra.tile - 1) / ra.tile) * (uint32_t)((y1 - y0 + ra.tile_h - 1) / ra.tile_h);
                 const uint64_t key = ((uint64_t)MW << 40) ^ ((uint64_t)y0 << 20) ^ (uint64_t)y1 ^ ((uint64_t)ra.tile << 60) ^ ((uint64_t)ra.tile_h << 56);
                 if (phase != 2) {
+#ifdef RT_CHAIN_PROBE
+                    c->rt_tile_cost.ensure((size_t)n_tiles * 4 * 9);   // + the chain probe's 8 words per tile
+#else
                     c->rt_tile_cost.ensure((size_t)n_tiles * 4);
+#endif
                     c->rt_tile_order.ensure((size_t)(n_tiles + 64) * 4);   // + launch_tile_sort's 64 aux words
                     rt_sorted = key == c->rt_tile_key;
                     if (rt_sorted) launch_tile_sort(c->rt_tile_cost.as<uint32_t>(), n_tiles, c->rt_tile_order.as<uint32_t>(),

@@ -815,9 +815,20 @@ __device__ __forceinline__ void write_record_header(float4* rk, int next, uint32
 // shadow rays go to q; rp / rd / pdf / att become the scattered ray's.
 template <bool LDS, bool CNT>
 __device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t* fq, int lane, size_t i, uint32_t t,
-                                          uint32_t spp, const Hit& h, int& prev_rec, uint32_t& n_hits, Xorwow& r, f3& rp, f3& rd, float& pdf, float& att) {
+                                          uint32_t spp, const Hit& h, int& prev_rec, uint32_t& n_hits, Xorwow& r, f3& rp, f3& rd, float& pdf, float& att
+#ifdef RT_CHAIN_PROBE
+                                          , uint64_t* al_acc = nullptr
+#endif
+                                          ) {
     const MaterialGpu m = a.mats[h.mat];
+#ifdef RT_CHAIN_PROBE
+    const uint64_t pa = (uint64_t)wall_clock64();
     const uint32_t k = wave_alloc(q.count, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the atomic's return (and the stores still in flight)
+    if (al_acc) *al_acc += (uint64_t)wall_clock64() - pa;
+#else
+    const uint32_t k = wave_alloc(q.count, lane);
+#endif
     if (q.plist) q.plist[(size_t)t * q.max_hits + n_hits] = (int)k;
     ++n_hits;
     float4* rk = q.rec + (size_t)k * q.rec_stride;
@@ -837,10 +848,21 @@ __device__ __forceinline__ void defer_hit(const RaytraceArgs& a, const RtQueue& 
     att = 1.0f * m.rg;
 }
 
+#ifdef RT_CHAIN_PROBE
+// timing-only build (make BUILD=_build_probe EXTRA=-DRT_CHAIN_PROBE, tools/chain_probe.py): s_memrealtime ticks of a
+// pixel's phases -- [0] world queries, [1] deferred shading (record allocation included), [2] the allocation's atomic
+// alone, [3] queries made -- written after the frame's per-tile costs (rt_tile_cost[n_tiles + 8 tile + j], lane 0)
+struct ChainProbe { uint64_t q, sh, al; uint32_t nq; };
+#define PROBE_T() ((uint64_t)wall_clock64())
+#endif
 template <bool DEFER, bool LDS, bool CNT = false>
 __device__ __forceinline__ uint32_t raytrace_pixel(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t t,
                                                const float4* __restrict__ origins, const float4* __restrict__ dirs, uint32_t* __restrict__ rng,
-                                               uint32_t n_rng, float4* __restrict__ acc_rgba, float* __restrict__ acc_depth, uint32_t* fq = nullptr) {
+                                               uint32_t n_rng, float4* __restrict__ acc_rgba, float* __restrict__ acc_depth, uint32_t* fq = nullptr
+#ifdef RT_CHAIN_PROBE
+                                               , ChainProbe* pr = nullptr
+#endif
+                                               ) {
     const size_t i = (size_t)a.row0 * a.W + t;
     const int lane = threadIdx.x & 63;
     Xorwow r = load_rng(rng, n_rng, i);
@@ -862,14 +884,30 @@ __device__ __forceinline__ uint32_t raytrace_pixel(const RaytraceArgs& a, const 
         f3 shade_s = splat(0.0f);
         for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
             Hit h;
+#ifdef RT_CHAIN_PROBE
+            const uint64_t pt0 = PROBE_T();
+#endif
             const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h);
+#ifdef RT_CHAIN_PROBE
+            if (pr) { pr->q += PROBE_T() - pt0; pr->nq += 1; }
+#endif
             if (!bounce) {
                 next_pos = next_pos + h.pos;
                 if (buf != 0) { normal = normal + h.normal; view_pos = view_pos + rp; view_dir = view_dir + rd; }
             }
             if (hit_obj < 0) break;
             if (DEFER) {
+#ifdef RT_CHAIN_PROBE
+                const uint64_t pt1 = PROBE_T();
+#endif
+#ifdef RT_CHAIN_PROBE
+                defer_hit(a, q, cx, fq, lane, i, t, spp, h, prev_rec, n_hits, r, rp, rd, pdf, att, pr ? &pr->al : nullptr);
+#else
                 defer_hit(a, q, cx, fq, lane, i, t, spp, h, prev_rec, n_hits, r, rp, rd, pdf, att);
+#endif
+#ifdef RT_CHAIN_PROBE
+                if (pr) pr->sh += PROBE_T() - pt1;
+#endif
                 continue;
             }
             // shade_object (raytracer.cu:6-57)
@@ -1004,7 +1042,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
         }
         const uint64_t t0 = wall_clock64();
         const uint32_t x = (tile % tiles_x) * T + (uint32_t)lane % T, y = (tile / tiles_x) * TH + (uint32_t)lane / T;
+#ifdef RT_CHAIN_PROBE
+        ChainProbe pr{0, 0, 0, 0};
+        const uint32_t c0 = counts[0], c1 = counts[1], c2 = counts[2];   // counting frames (rt_count): this tile's share
+        if ((uint32_t)lane < T * TH && x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth, FQ ? fq : nullptr, &pr);
+        if (a.tile_cost && lane == 0) {
+            uint32_t* pp = a.tile_cost + n_tiles + 8u * tile;
+            pp[0] = (uint32_t)pr.q; pp[1] = (uint32_t)pr.sh; pp[2] = (uint32_t)pr.al; pp[3] = pr.nq;
+            pp[4] = counts[0] - c0; pp[5] = counts[1] - c1; pp[6] = counts[2] - c2;
+        }
+#else
         if ((uint32_t)lane < T * TH && x < (uint32_t)a.W && y < rows) raytrace_pixel<DEFER>(a, q, cx, y * (uint32_t)a.W + x, origins, dirs, rng, n_rng, acc_rgba, acc_depth, FQ ? fq : nullptr);
+#endif
         if (a.tile_cost && lane == 0) a.tile_cost[tile] = (uint32_t)min<uint64_t>(wall_clock64() - t0, 0xFFFFFFFFull);
     }
     if constexpr (DEFER && FQ) {
