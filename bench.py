@@ -334,6 +334,7 @@ def train_leg(steps=200, warmup=50, seed=1337, engine_params=None):
         st2 = tb.train(50)
         eng.set_param("train_kernel_times", 0)
         sm = st2.get("stage_ms", {})
+        gb = 2 if eng.get_param("train_grid_grad_f16") else 4   # bytes per scattered gradient feature
         n_before = int(st2["measured_batch_before_compaction"])
         n_after = int(st2["measured_batch"])
         n_params = int(synthetic.n_params())
@@ -344,11 +345,12 @@ def train_leg(steps=200, warmup=50, seed=1337, engine_params=None):
             rl = {"stage_ms": sm,
                   "network": {"bound": "hbm", "bytes": n_before * BYTES_PER_SAMPLE, "frac": frac(n_before * BYTES_PER_SAMPLE, sm["network"], HBM_PEAK_GBS),
                               "note": "inference forward of every generated sample, 548 B/sample (SURVEY 8d)"},
-                  "field": {"bound": "float atomics", "bytes": n_after * 8 * 8 * 4 * 4, "peak_GBps": 1300.0,
-                            "frac": frac(n_after * 8 * 8 * 4 * 4, sm["field"], 1300.0),
-                            "note": "hash-grid gradient scatter, 8 levels x 8 corners x 4 features x 4 B per compacted sample, against the "
-                                    "chip-wide float-atomic rate (MI355X_MICROARCH.md, Global float atomics); the kernel also runs the MLP "
-                                    "forward + backward on MFMA and folds runs of equal entries before adding"},
+                  "field": {"bound": "float atomics", "bytes": n_after * 8 * 8 * 4 * gb, "peak_GBps": 1300.0,
+                            "frac": frac(n_after * 8 * 8 * 4 * gb, sm["field"], 1300.0),
+                            "note": f"hash-grid gradient scatter, 8 levels x 8 corners x 4 features x {gb} B per compacted sample "
+                                    f"({'fp16 packed atomics, tcnn grad_t' if gb == 2 else 'f32 atomics'}), against the chip-wide float-atomic "
+                                    "rate (MI355X_MICROARCH.md, Global float atomics, measured at the same byte rate for f32 and packed 16-bit "
+                                    "adds); the kernel also runs the MLP forward + backward on MFMA and folds runs of equal entries before adding"},
                   "dw": {"bound": "hbm", "bytes": n_after * 960, "frac": frac(n_after * 960, sm["dw"], HBM_PEAK_GBS),
                          "mfma_tflops": round(dw_flop / (sm["dw"] * 1e-3) / 1e12, 2) if sm["dw"] > 0 else None,
                          "mfma_frac": round(dw_flop / (sm["dw"] * 1e-3) / 1e12 / MFMA_F16_PEAK_TFLOPS, 4) if sm["dw"] > 0 else None,
@@ -363,9 +365,9 @@ def train_leg(steps=200, warmup=50, seed=1337, engine_params=None):
                 "batch_target": 1 << 18, "measured_batch": samples, "rays_per_batch": int(st["rays_per_batch"]),
                 "loss_after": round(float(st["loss"]), 6), "step_after": int(st["step"]),
                 "algorithmic_per_step": {"dw_gemm_flop": dw_flop, "mlp_fwd_bwd_flop": 3 * 20480 * samples,
-                                         "grid_scatter_atomic_bytes": samples * 8 * 8 * 4 * 4},
+                                         "grid_scatter_atomic_bytes": samples * 8 * 8 * 4 * 2},
                 "roofline": rl,
-                "dtype": "fp16 params / activations / GEMM operands, f32 master weights, gradients and accumulation "
+                "dtype": "fp16 params / activations / GEMM operands / hash-grid gradients (tcnn's grad_t), f32 master weights, MLP gradients and accumulation "
                          "(tcnn's network_precision_t; BASELINE.json C5 says bf16)",
                 "data": "data/nerf/lego400 (the reference's lego set at 400x400), 90 training views, fresh init (seed 1337)",
                 "kernel_profile": "profiles/r04_train_kernel_table.txt (rocprofv3 of tools/train_bench.py)"}

@@ -423,6 +423,7 @@ const std::map<std::string, double>& default_params() {
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
         {"train_gen_bricks", 0},                // training generator's occupancy: 0 the linear words (measured fastest, tools/train_ab.py), 1 the OccBrick blob (LDS when it fits, else global)
+        {"train_grid_grad_f16", 1},             // hash-grid gradients in fp16 with packed atomics, tcnn's grad_t (__half2 atomicAdd); 0: f32
         {"train_dw_pipe", 1},                   // dW kernel: the next tile's operands in flight during the current tile's MFMAs (0: load, then multiply)
         {"train_dw_blocks_per_cu", 2},          // dW kernel: workgroups per CU (tools/train_ab.py)
         {"train_gen_lanes", 8},                 // lanes per ray of the training generator's speculative march (8 or 16; 1: one lane per ray; tools/train_ab.py)
@@ -593,6 +594,8 @@ struct sng_ctx {
         std::vector<Lens> h_lens;
         DevBuf master, grads, m1, m2, steps, ema, p_train, p_infer, wfrag_train, wfrag_t;
         DevBuf adam_corr;                              // Adam's bias correction per step count (launch_train_adam_corr)
+        DevBuf grads_h;                                // fp16 hash-grid gradients (train_grid_grad_f16)
+        bool grads_h_used = false;                     // the last step's grid gradients are in grads_h
         uint32_t adam_corr_n = 0;                      // valid entries 1..adam_corr_n
         DevBuf grid, grid_tmp, grid_coords, grid_idx, grid_out;
         DevBuf ctrl, ray_indices, rays, numsteps, coords, mlp_out, coords_c, dloss, loss, acts, partial, rayrec, cnt_i, cbase_i;
@@ -2096,6 +2099,7 @@ TrainStepArgs train_args(sng_ctx* c) {
     a.gen_lanes = (int)c->p("train_gen_lanes");
     a.dw_pipe = c->p("train_dw_pipe") != 0.0 ? 1 : 0;
     a.dw_blocks_per_cu = std::max(1, (int)c->p("train_dw_blocks_per_cu"));
+    a.grid_grad_f16 = c->p("train_grid_grad_f16") != 0.0 && c->net.F == 4 ? 1 : 0;
     return a;
 }
 
@@ -2134,10 +2138,19 @@ void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev
     launch_train_loss(a, im, b, t.rng, c->d_mean.as<float>(), s);
     mark(3);
     if (stage == 3) return;
-    HIPCHK(hipMemsetAsync(t.grads.p, 0, c->n_params * 4, s));
+    const uint64_t n_mlp = 3072 + 7168;
+    t.grads_h_used = a.grid_grad_f16 != 0;
+    if (t.grads_h_used) {   // f32 MLP gradients + fp16 grid gradients (tcnn's grad_t)
+        t.grads_h.ensure((c->n_params - n_mlp) * 2);
+        HIPCHK(hipMemsetAsync(t.grads.p, 0, n_mlp * 4, s));
+        HIPCHK(hipMemsetAsync(t.grads_h.p, 0, (c->n_params - n_mlp) * 2, s));
+    } else {
+        HIPCHK(hipMemsetAsync(t.grads.p, 0, c->n_params * 4, s));
+    }
     mark(4);
     float* g = t.grads.as<float>();
-    launch_train_field(a, b, net, t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), static_cast<uint16_t*>(net.grid), g + 3072 + 7168, s);
+    launch_train_field(a, b, net, t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), static_cast<uint16_t*>(net.grid), g + n_mlp,
+                       t.grads_h_used ? t.grads_h.as<uint16_t>() : nullptr, s);
     mark(5);
     launch_train_dw(a, b.acts, g, (uint32_t)c->n_cus, s);
     mark(6);
@@ -2179,6 +2192,7 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
         }
         o.corr = t.adam_corr.as<float>();
         o.corr_n = t.adam_corr_n;
+        o.grads_h = t.grads_h_used ? t.grads_h.as<uint16_t>() : nullptr;
         launch_train_adam(o, c->n_params, 3072 + 7168, t.master.as<float>(), t.grads.as<float>(), t.m1.as<float>(), t.m2.as<float>(), t.steps.as<uint32_t>(),
                           t.ema.as<float>(), t.p_train.as<uint16_t>(), t.p_infer.as<uint16_t>(), s);
         if (timed) HIPCHK(hipEventRecord(c->train_events[7], s));
@@ -3324,7 +3338,17 @@ int sng_train_debug(sng_ctx* c, int stage, const char* name, void* out, uint64_t
         if (it == bufs.end()) throw SngError(SNG_ERR_INVALID, "unknown training buffer " + k);
         const uint64_t n = it->second->bytes;
         if (size) *size = n;
-        if (out) HIPCHK(hipMemcpy(out, it->second->p, std::min(n, cap), hipMemcpyDeviceToHost));
+        if (out && k == "grads" && t.grads_h_used) {   // f32 view: the fp16 grid gradients as the optimizer reads them
+            const uint64_t n_mlp = 3072 + 7168, n_grid = c->n_params - n_mlp;
+            std::vector<float> f(n / 4, 0.0f);
+            std::vector<uint16_t> hg(n_grid);
+            HIPCHK(hipMemcpy(f.data(), t.grads.p, n_mlp * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(hg.data(), t.grads_h.p, n_grid * 2, hipMemcpyDeviceToHost));
+            for (uint64_t i = 0; i < n_grid && n_mlp + i < f.size(); ++i) f[n_mlp + i] = h2f(hg[i]);
+            std::memcpy(out, f.data(), std::min(n, cap));
+        } else if (out) {
+            HIPCHK(hipMemcpy(out, it->second->p, std::min(n, cap), hipMemcpyDeviceToHost));
+        }
     });
 }
 int sng_comm_unique_id(uint8_t* out) {

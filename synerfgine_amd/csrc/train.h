@@ -149,6 +149,7 @@ struct TrainStepArgs {
     int gen_lanes;           // lanes per ray of the generator's speculative march (8, 16; else one lane per ray)
     int dw_pipe;             // dW kernel: 1 = the next tile's operands loaded while the current tile's MFMAs run
     int dw_blocks_per_cu;    // dW kernel: workgroups per CU (each adds its partial sums to the gradient once)
+    int grid_grad_f16;       // hash-grid gradients accumulated in fp16 with packed atomics (tcnn's grad_t = __half), else f32
 };
 
 // per-batch buffers
@@ -179,6 +180,7 @@ struct AdamArgs {
     float deb_old, deb_new;   // 1 - ema_decay^ema_step, 1 - ema_decay^(ema_step + 1) (host powf, as the oracle)
     const float* corr;        // [corr_n + 1] Adam's bias correction sqrtf(1 - beta2^s) / (1 - beta1^s) for s = 1..corr_n
     uint32_t corr_n;
+    const uint16_t* grads_h;  // fp16 grid gradients (param index - n_matrix), nullptr: every gradient in `grads`
 };
 
 void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, hipStream_t s);
@@ -187,7 +189,7 @@ void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const 
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s);
 void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s);
 void launch_train_field(const TrainStepArgs& a, const TrainBatch& b, const NetworkDev& net, const uint16_t* wfrag, const uint16_t* wfrag_t,
-                        const uint16_t* grid, float* ggrad, hipStream_t s);
+                        const uint16_t* grid, float* ggrad, uint16_t* ggrad_h, hipStream_t s);
 void launch_train_dw(const TrainStepArgs& a, const uint16_t* acts, float* wgrad, uint32_t n_cus, hipStream_t s);
 void launch_train_adam(const AdamArgs& o, uint64_t n, uint32_t n_matrix, float* master, const float* grads, float* m1, float* m2, uint32_t* steps, float* ema,
                        uint16_t* p_train, uint16_t* p_infer, hipStream_t s);

@@ -531,15 +531,67 @@ __device__ __forceinline__ void grid_backward_level_coop4(const LevelInfo& L, fl
     }
 }
 
+// The same scatter into an fp16 gradient with packed atomics (train_grid_grad_f16): tcnn accumulates the hash-grid
+// gradient in the network's precision, __half2 atomicAdd per feature pair (GridEncoding backward, grad_t = T when a
+// thread holds 2 features).  One global_atomic_pk_add_f16 wave-instruction covers 32 corner entries x 2 feature pairs
+// (lane 2q' + h adds features 2h, 2h+1 of source lane 32i + q'), half the bytes of the f32 scatter, which the
+// memory-side atomic unit moves at the same byte rate (MI355X_MICROARCH.md, Global float atomics).  Runs of equal
+// entries are summed in f32 (the segmented scan of the f32 form) and rounded to fp16 once per run.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void grid_backward_level_coop4_h(const LevelInfo& L, uint16_t* __restrict__ ggrad, float x0, float x1, float x2,
+                                                            const float* dfeat, int lane) {
+    const float p0 = fmaf(L.scale, x0, 0.5f), p1 = fmaf(L.scale, x1, 0.5f), p2 = fmaf(L.scale, x2, 0.5f);
+    const float q0 = floorf(p0), q1 = floorf(p1), q2 = floorf(p2);
+    const uint32_t g0 = (uint32_t)(int)q0, g1 = (uint32_t)(int)q1, g2 = (uint32_t)(int)q2;
+    const float f0 = p0 - q0, f1 = p1 - q1, f2 = p2 - q2;
+    const int h = lane & 1, qd = (lane >> 1) & 15, sq = lane >> 1;
+    float dlo[2], dhi[2];   // features 2h, 2h+1 of source lane 32i + sq
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int src = 32 * i + sq;
+        const float v0 = __shfl(dfeat[0], src, 64), v1 = __shfl(dfeat[1], src, 64), v2 = __shfl(dfeat[2], src, 64), v3 = __shfl(dfeat[3], src, 64);
+        dlo[i] = h ? v2 : v0;
+        dhi[i] = h ? v3 : v1;
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float w = 1.0f;
+        w *= (c & 1) ? f0 : 1.0f - f0;
+        w *= (c & 2) ? f1 : 1.0f - f1;
+        w *= (c & 4) ? f2 : 1.0f - f2;
+        const uint32_t at = L.offset * 4u + grid_index(L, g0 + (c & 1), g1 + ((c >> 1) & 1), g2 + ((c >> 2) & 1)) * 4u;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int src = 32 * i + sq;
+            const float ws = __shfl(w, src, 64);
+            const uint32_t as = __shfl(at, src, 64);
+            float va = ws * dlo[i], vb = ws * dhi[i];
+            const uint32_t a_prev = __shfl_up(as, 2u, 64), a_next = __shfl_down(as, 2u, 64);
+            bool head = qd == 0 || a_prev != as;
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) {
+                const float ua = __shfl_up(va, 2u * (unsigned)d, 64), ub = __shfl_up(vb, 2u * (unsigned)d, 64);
+                const bool hu = __shfl_up(head, 2u * (unsigned)d, 64);
+                if (qd >= d && !head) { va += ua; vb += ub; head = hu; }
+            }
+            const bool tail = qd == 15 || a_next != as;
+            if (tail && (va != 0.0f || vb != 0.0f)) {
+                const h2v v = {(_Float16)va, (_Float16)vb};
+                __builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) h2v*)(ggrad + as + 2 * h), v);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // NerfNetwork forward + backward per 16-sample tile (nerf_network.h:144-268).  Activations
 // (post-ReLU, fp16) and pre-activation gradients (fp16) go to acts[tile][TRAIN_FEATS][16] for
 // train_dw_kernel; the encoding gradient is scattered into the f32 grid gradient.
 // ---------------------------------------------------------------------------------------------
-template <int F>
+template <int F, bool H16 = false>
 __global__ __launch_bounds__(256) void train_field_kernel(TrainStepArgs a, TrainBatch b, const h8* __restrict__ wfrag, const h4v* __restrict__ wfrag_t,
                                                           const _Float16* __restrict__ grid, const LevelInfo* __restrict__ levels,
-                                                          float* __restrict__ ggrad) {
+                                                          float* __restrict__ ggrad, uint16_t* __restrict__ ggrad_h) {
     const uint32_t n = a.target_batch;
     const uint32_t n_tiles = (n + 15) >> 4;
     const int lane = threadIdx.x & 63;
@@ -649,7 +701,10 @@ __global__ __launch_bounds__(256) void train_field_kernel(TrainStepArgs a, Train
         // features 4g..4g+3 and 16+4g..16+4g+3 (tail lanes of the last tile contribute nothing)
         float df0[4], df1[4];
         for (int k = 0; k < 4; ++k) { df0[k] = valid ? (float)(_Float16)de0[k] : 0.0f; df1[k] = valid ? (float)(_Float16)de1[k] : 0.0f; }
-        if constexpr (F == 4) {
+        if constexpr (F == 4 && H16) {
+            grid_backward_level_coop4_h(levels[g], ggrad_h, x0, x1, x2, df0, lane);
+            grid_backward_level_coop4_h(levels[4 + g], ggrad_h, x0, x1, x2, df1, lane);
+        } else if constexpr (F == 4) {
             grid_backward_level_coop4(levels[g], ggrad, x0, x1, x2, df0, lane);
             grid_backward_level_coop4(levels[4 + g], ggrad, x0, x1, x2, df1, lane);
         } else {
@@ -791,7 +846,8 @@ __global__ __launch_bounds__(256) void train_adam_kernel(AdamArgs o, uint64_t n,
             float w = master[i], a = m1[i], b = m2[i], e = ema[i];
             uint32_t st = steps[i];
             bool touched;
-            adam_one(o, i < n_matrix, grads[i], w, a, b, st, e, touched);
+            const float gi = (o.grads_h && i >= n_matrix) ? h2f(o.grads_h[i - n_matrix]) : grads[i];
+            adam_one(o, i < n_matrix, gi, w, a, b, st, e, touched);
             if (touched) { master[i] = w; m1[i] = a; m2[i] = b; steps[i] = st; }
             ema[i] = e;
             p_train[i] = f2h(w);
@@ -800,7 +856,13 @@ __global__ __launch_bounds__(256) void train_adam_kernel(AdamArgs o, uint64_t n,
         return;
     }
     const bool matrix = i0 < n_matrix;
-    const float4 g = *reinterpret_cast<const float4*>(grads + i0);
+    float4 g;
+    if (o.grads_h && !matrix) {   // four fp16 grid gradients (n_matrix % 4 == 0: 8-B aligned)
+        const uint2 hg = *reinterpret_cast<const uint2*>(o.grads_h + (i0 - n_matrix));
+        g = make_float4(h2f((uint16_t)(hg.x & 0xffffu)), h2f((uint16_t)(hg.x >> 16)), h2f((uint16_t)(hg.y & 0xffffu)), h2f((uint16_t)(hg.y >> 16)));
+    } else {
+        g = *reinterpret_cast<const float4*>(grads + i0);
+    }
     float4 w = *reinterpret_cast<const float4*>(master + i0);
     float4 e = *reinterpret_cast<const float4*>(ema + i0);
     const bool any = matrix || g.x != 0.0f || g.y != 0.0f || g.z != 0.0f || g.w != 0.0f;
@@ -956,15 +1018,16 @@ void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_
     hipLaunchKernelGGL(train_pack_kernel, dim3(56), dim3(64), 0, s, params, wfrag, wfrag_t);
 }
 void launch_train_field(const TrainStepArgs& a, const TrainBatch& b, const NetworkDev& net, const uint16_t* wfrag, const uint16_t* wfrag_t,
-                        const uint16_t* grid, float* ggrad, hipStream_t s) {
+                        const uint16_t* grid, float* ggrad, uint16_t* ggrad_h, hipStream_t s) {
     const uint32_t tiles = (a.target_batch + 15) / 16;
     const uint32_t waves = std::min<uint32_t>(tiles, (uint32_t)net.n_cus * 8u);
     const uint32_t blocks = (waves + 3) / 4;
     const h8* w = reinterpret_cast<const h8*>(wfrag);
     const h4v* wt = reinterpret_cast<const h4v*>(wfrag_t);
     const _Float16* gr = reinterpret_cast<const _Float16*>(grid);
-    if (net.F == 4) hipLaunchKernelGGL((train_field_kernel<4>), dim3(blocks), dim3(256), 0, s, a, b, w, wt, gr, net.levels, ggrad);
-    else hipLaunchKernelGGL((train_field_kernel<2>), dim3(blocks), dim3(256), 0, s, a, b, w, wt, gr, net.levels, ggrad);
+    if (net.F == 4 && ggrad_h) hipLaunchKernelGGL((train_field_kernel<4, true>), dim3(blocks), dim3(256), 0, s, a, b, w, wt, gr, net.levels, ggrad, ggrad_h);
+    else if (net.F == 4) hipLaunchKernelGGL((train_field_kernel<4>), dim3(blocks), dim3(256), 0, s, a, b, w, wt, gr, net.levels, ggrad, ggrad_h);
+    else hipLaunchKernelGGL((train_field_kernel<2>), dim3(blocks), dim3(256), 0, s, a, b, w, wt, gr, net.levels, ggrad, ggrad_h);
 }
 void launch_train_dw(const TrainStepArgs& a, const uint16_t* acts, float* wgrad, uint32_t n_cus, hipStream_t s) {
     const uint32_t tiles = (a.target_batch + 15) / 16;

@@ -183,9 +183,16 @@ def test_train_loss_and_output_gradients(trainer):
     assert bad == 0, f"{bad} samples with dL/d(output) off (worst {worst:.2f}x tolerance)"
 
 
-def test_train_param_gradients(trainer):
+@pytest.mark.parametrize("grid_f16", [0, 1], ids=["grid_f32", "grid_f16"])
+def test_train_param_gradients(trainer, grid_f16):
+    """train_grid_grad_f16 = 1 accumulates the hash-grid gradients in fp16 with packed atomics, as tcnn does (its grad_t
+    is the network's __half); the same bound against the float64 reference holds for both."""
     import train_ref as R
-    d = _step_state(trainer, 4)
+    trainer["eng"].set_param("train_grid_grad_f16", grid_f16)
+    try:
+        d = _step_state(trainer, 4)
+    finally:
+        trainer["eng"].set_param("train_grid_grad_f16", 0)
     net = R.TorchNetwork(trainer["cfg"], d["params"])
     ref = net.param_grads(d["coords_c"], d["dloss"].astype(np.float64))
     got = d["grads"][: len(ref)].astype(np.float64)
@@ -201,12 +208,17 @@ def test_train_param_gradients(trainer):
         assert rel <= 3e-2 and cos >= 0.999, f"{name}: relative error {rel:.3g}, cosine {cos:.6f}"
 
 
-def test_train_adam_ema_matches_oracle(trainer, oracle_lib):
+@pytest.mark.parametrize("grid_f16", [0, 1], ids=["grid_f32", "grid_f16"])
+def test_train_adam_ema_matches_oracle(trainer, oracle_lib, grid_f16):
     tb = trainer["tb"]
     pre = {k: tb.train_debug(0, k, dt).copy() for k, dt in (("master", np.float32), ("m1", np.float32), ("m2", np.float32),
                                                              ("steps", np.uint32), ("ema", np.float32))}
     step = int(trainer["stats"]["step"])
-    trainer["stats"] = tb.train(1)
+    trainer["eng"].set_param("train_grid_grad_f16", grid_f16)
+    try:
+        trainer["stats"] = tb.train(1)
+    finally:
+        trainer["eng"].set_param("train_grid_grad_f16", 0)
     grads = tb.train_debug(0, "grads", np.float32).copy()
     post = {k: tb.train_debug(0, k, dt) for k, dt in (("master", np.float32), ("m1", np.float32), ("m2", np.float32), ("steps", np.uint32),
                                                       ("ema", np.float32))}

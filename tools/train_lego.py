@@ -5,7 +5,7 @@ data/nerf/lego400 (tools/make_lego400.py) with the reference's defaults (batch 2
 Ema(ExpDecay(Adam)), density-grid EMA every 16 steps), holds out every 20th view, and reports
 training throughput, loss and held-out PSNR.  Writes the trained model as an .ingp snapshot.
 
-usage: python tools/train_lego.py [steps] [out.ingp]
+usage: [SNG_SET=key=value,...] [FOCAL_FROM_ANGLE=1] python tools/train_lego.py [steps] [out.ingp]
 """
 import json
 import math
@@ -38,6 +38,8 @@ tb = Testbed(0)
 cfg, params = synthetic.random_init(1337)
 tb.set_nerf_model(cfg, params)
 eng = Engine(tb)
+for kv in filter(None, os.environ.get("SNG_SET", "").split(",")):   # engine parameters, e.g. SNG_SET=train_grid_grad_f16=1
+    eng.set_param(kv.split("=")[0], float(kv.split("=")[1]))
 tb.set_training_dataset(imgs[train], xf[train], focal[train], pp[train])
 tb.train_reset(1337)
 print(json.dumps({"dataset": "lego400", "train_views": len(train), "test_views": test, "res": [W, H]}), flush=True)
