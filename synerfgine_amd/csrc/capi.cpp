@@ -410,6 +410,8 @@ const std::map<std::string, double>& default_params() {
         {"rt_tile_order", 1},                   // visit raytracer tiles in descending previous-frame cost
         {"rt_prio_frac", 0.1},                  // the costliest fraction of the path tiles (last frame's order) at wave priority 3
         {"rt_prio2_frac", 0.25},                // ... the tiles up to this fraction of the order at priority 2
+        {"rt_first", 1},                        // concurrent frames: init_rays waits (device-side, bounded) for the path kernel's first workgroup
+        {"rt_first_timeout_us", 100},           // ... at most this long
         {"rt_fused_shadow", 1},                 // banded frames: the path kernel's idle waves trace the shadow rays (mesh.hip fq_consume)
         {"rt_fused_tiles_per_wave", 1},         // ... when the band has at most this many path tiles per wave (a full queue is traced in place)
         {"rt_fused_shadow_used", 0},            // (output) 1 when the last frame's path kernel traced its shadow rays itself
@@ -545,6 +547,8 @@ struct sng_ctx {
     DevBuf rt_rec, rt_lc, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
     DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
+    DevBuf rt_started;                    // rt_first: the path kernel's landing flag (frame sequence number)
+    uint32_t frame_seq = 0, rt_wait_seq = 0;
     DevBuf fused_work;                     // ray-queue cursor of the fused NeRF kernel
     DevBuf shadow_scratch;                 // NeRF shadow pass: light samples + terms per neighbour slot (launch_shadows)
     DevBuf tail_live;                      // tail iterations' alive counts as a difference array (reference slots)
@@ -1339,6 +1343,10 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
     for (int b = 0; b < 2; ++b)
         rb[b] = {c->ray_ot[b].as<float4>(), c->ray_di[b].as<float4>(), c->ray_rgba[b].as<float4>(), c->ray_depth[b].as<float>(), c->ray_mw[b].as<float>(),
                  c->ray_lt[b].as<float2>(), c->ray_lo[b].as<uint2>(), c->ray_kk[b].as<uint32_t>()};
+    if (c->rt_wait_seq) {   // rt_first (render_frame)
+        launch_rt_wait_started(c->rt_started.as<uint32_t>(), c->rt_wait_seq, (uint32_t)std::max(1.0, c->p("rt_first_timeout_us")), c->s_nerf);
+        c->rt_wait_seq = 0;
+    }
     launch_init_rays(a, rb[0], ctrl, c->nerf_rgba.as<float4>(), c->nerf_depth.as<float>(), c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(),
                      (uint32_t)c->n_cus, c->s_nerf);
     reduce_sched(0);
@@ -1758,6 +1766,18 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     int rt_start_chunk = (concurrent && show_nerf) ? (int)c->p("rt_start_chunk") : 0;
     if (rt_start_chunk < 0) rt_start_chunk = (y1 - y0) * 10 >= MH * 6 ? 1 : 0;
     bool rt_enqueued = false, rt_sorted = false;
+    // rt_first: the path kernel's workgroups land before init_rays takes the CUs (the faster of the concurrent frame's two
+    // dispatch orders): init_rays waits, on the device and bounded, for the first one
+    const bool rt_first = concurrent && show_nerf && rt_start_chunk <= 0 && c->p("rt_first") != 0.0 && c->p("show_virtual_obj") != 0.0 &&
+                          !c->objs.empty();
+    if (rt_first) {
+        if (!c->rt_started.p) {
+            c->rt_started.ensure(256);
+            HIPCHK(hipMemsetAsync(c->rt_started.p, 0, 256, c->s_rt));
+        }
+        c->rt_wait_seq = ++c->frame_seq;
+        if (c->rt_wait_seq == 0) c->rt_wait_seq = ++c->frame_seq;   // 0 = no wait
+    }
     // phase 0: everything after `after`; 1 (concurrent frames, at frame start): the work that does not
     // wait for the NeRF head -- mesh rays and the tile-order sort -- so it overlaps init_rays; 2: the
     // rest, gated on `after`
@@ -1774,6 +1794,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         if (c->p("show_virtual_obj") != 0.0 && !c->objs.empty()) {
             RaytraceArgs ra{};
             c->params["rt_fused_shadow_used"] = 0;
+            if (rt_first) { ra.started = c->rt_started.as<uint32_t>(); ra.started_seq = c->rt_wait_seq; }
             ra.vol = vol;
             ra.W = MW; ra.row0 = y0; ra.row1 = y1;
             ra.up = cam.c0;
@@ -1922,6 +1943,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
         // shadow_on_nerf no output depends on it (nerf_gbuffer = 1 keeps it for sng_frame_buffer("nerf_normals"))
         if (shadows || c->p("nerf_gbuffer") != 0.0) launch_normals(NW, NH, nr0, nr1, c->nerf_pos.as<float>(), c->nerf_nrm.as<float>(), c->s_nerf);
     }
+    c->rt_wait_seq = 0;
     if (!rt_enqueued) {
         HIPCHK(hipEventRecord(c->ev_rt_go, c->s_nerf));
         enqueue_raytracer(c->ev_rt_go, rt_start_chunk <= 0 ? 0 : 2);

@@ -987,6 +987,15 @@ __device__ __forceinline__ uint32_t raytrace_pixel(const RaytraceArgs& a, const 
     return n_hits;
 }
 
+__global__ void rt_wait_started_kernel(const uint32_t* __restrict__ started, uint32_t seq, uint64_t timeout_ticks) {
+    const uint64_t t0 = wall_clock64();   // s_memrealtime, 100 MHz
+    while (__hip_atomic_load(started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != seq && wall_clock64() - t0 < timeout_ticks)
+        __builtin_amdgcn_s_sleep(8);
+}
+void launch_rt_wait_started(const uint32_t* started, uint32_t seq, uint32_t timeout_us, hipStream_t s) {
+    hipLaunchKernelGGL(rt_wait_started_kernel, dim3(1), dim3(64), 0, s, started, seq, (uint64_t)timeout_us * 100u);
+}
+
 // Persistent workgroups; each wave takes T x T pixel tiles (T = 8, or 4 for thin bands: a tile is a
 // serial chain of 8 samples x 2 bounces whose divergent traversals cost the union of its lanes' paths,
 // so fewer pixels per wave shorten the chain when there are too few tiles to fill the GPU anyway)
@@ -1002,6 +1011,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
                                                         const float4* __restrict__ dirs, uint32_t* __restrict__ rng, uint32_t n_rng,
                                                         float4* __restrict__ acc_rgba, float* __restrict__ acc_depth) {
     uint32_t counts[3] = {0u, 0u, 0u};
+    if (a.started && threadIdx.x == 0) __hip_atomic_store(a.started, a.started_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the fused shadow queue sits after the blob and the stacks in the dynamic LDS
     uint32_t* fq = nullptr;
     if (DEFER && FQ && a.fused_shadow) {

@@ -282,6 +282,8 @@ struct RaytraceArgs {
     uint32_t prio2_tiles;       // ... and the tiles before prio2_tiles at priority 2
     int spread;                 // first tile of every wave dealt statically across the CUs (rt_spread), the rest claimed
     int fused_shadow;           // the path kernel's idle waves trace the shadow rays (banded frames, mesh.hip fq_consume)
+    uint32_t* started;          // rt_first: every path-kernel workgroup writes started_seq here as it lands (nullptr: off)
+    uint32_t started_seq;
 };
 
 // fused shadow queue of a banded path kernel (mesh.hip fq_publish / fq_consume): entries per workgroup, LDS words
@@ -413,6 +415,9 @@ size_t shadow_scratch_bytes(const ShadowArgs& a);
 void launch_shadows(const ShadowArgs& a, float4* rgba, const float* pos, const float* nrm, uint32_t* rng, uint32_t n_rng, void* scratch, hipStream_t s);
 void launch_mesh_rays(int W, int H, int row0, int row1, const CamDev& cam, f2 focal, f2 sc, float4* o, float4* d, float4* acc, float* accd,
                       hipStream_t s);
+// rt_first: one wave on the NeRF stream waits until the path kernel's first workgroup has landed (*started == seq) or
+// `timeout_us` has passed, so init_rays does not take the CUs first (the slower of the frame's two dispatch orders)
+void launch_rt_wait_started(const uint32_t* started, uint32_t seq, uint32_t timeout_us, hipStream_t s);
 void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const float4* o, const float4* d, uint32_t* rng, uint32_t n_rng, float4* acc,
                                float* accd, uint32_t shadow_blocks, hipStream_t s);
 void launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t* order, uint32_t* aux, hipStream_t s);
