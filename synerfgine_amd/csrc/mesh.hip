@@ -16,6 +16,18 @@
 
 namespace sng {
 
+// Read-only scene tables (objects, lights) through the constant address space: written by the host before the launch and
+// never by a kernel, so a wave-uniform index loads with scalar loads into SGPRs (the scalar cache) instead of a vector
+// load and a vmcnt wait on every query -- the compiler cannot prove the global copies unclobbered by the kernels' stores.
+template <class T>
+__device__ __forceinline__ T const_load(const T* p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return ((const __attribute__((address_space(4))) T*)p)[i];
+#else
+    return p[i];   // (the host pass of this device function: never executed)
+#endif
+}
+
 constexpr int BVH_STACK = 32;
 constexpr int TPB = 128;   // threads per block for the traversal kernels
 
@@ -388,7 +400,7 @@ __device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict
     if constexpr (CNT) cx.cnt[0] += 1u;
     for (int c = 0; c < n_objs; ++c) {
         int tri;
-        const float t = object_intersect(off, dir, objs[c], cx, tri, t_max);
+        const float t = object_intersect(off, dir, const_load(objs, c), cx, tri, t_max);
         if (t < depth && t > MIN_DEPTH) { out_obj = c; depth = t; }
     }
     return depth;
@@ -412,7 +424,7 @@ __device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restri
     float best = MAX_DEPTH;
     for (int c = 0; c < n_objs; ++c) {
         int tri;
-        const float t = object_intersect(off, dir, objs[c], cx, tri);
+        const float t = object_intersect(off, dir, const_load(objs, c), cx, tri);
         if (t < best && t > MIN_DEPTH) {
             out_obj = c;
             out_tri = tri;
@@ -424,7 +436,7 @@ __device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restri
     h.mat = -1;
     h.perturb = {mk(1, 0, 0), mk(0, 1, 0), mk(0, 0, 1)};
     if (out_obj >= 0) {
-        const ObjectGpu& o = objs[out_obj];
+        const ObjectGpu o = n_objs == 1 ? const_load(objs, 0) : objs[out_obj];   // (one object: a uniform index)
         h.mat = o.mat_id;
         const Tri tr = o.tris[out_tri];
         const f3 N = tri_normal(tr);
@@ -529,7 +541,7 @@ __device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx
     float overall = 1.0f;
     int k = 0;
     for (int li = 0; li < a.n_lights; ++li) {
-        const LightGpu L = a.lights[li];
+        const LightGpu L = const_load(a.lights, li);
         if (L.type == 0) {
             const float4 l4 = lp[(size_t)k++ * lp_stride];
             const f3 lpos = mk(l4.x, l4.y, l4.z);
@@ -597,7 +609,7 @@ __global__ __launch_bounds__(256) void shadow_draw_kernel(ShadowArgs a, uint32_t
         if (!shadow_slot(a, p, sl, fx, fy)) continue;
         int k = 0;
         for (int li = 0; li < a.n_lights; ++li) {
-            const LightGpu L = a.lights[li];
+            const LightGpu L = const_load(a.lights, li);
             if (L.type != 0) continue;
             const f3 q = light_sample(L, r);
             lp[((size_t)sl * a.n_point + k++) * n + p] = make_float4(q.x, q.y, q.z, 0.0f);
@@ -732,7 +744,7 @@ __device__ __forceinline__ void write_light_samples(const RaytraceArgs& a, const
     const f3 V = normalize(-rd);
     uint32_t jl = 0, jp = 0;
     for (int l = 0; l < a.n_lights; ++l) {
-        const LightGpu L = a.lights[l];
+        const LightGpu L = const_load(a.lights, l);
         for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
             const f3 lpos = light_sample(L, r);
             f3 Lv = lpos - pos;
@@ -914,7 +926,7 @@ __device__ __forceinline__ uint32_t raytrace_pixel(const RaytraceArgs& a, const 
             const MaterialGpu m = a.mats[h.mat];
             f3 color = splat(0.0f);
             for (int l = 0; l < a.n_lights; ++l) {
-                const LightGpu L = a.lights[l];
+                const LightGpu L = const_load(a.lights, l);
                 for (uint32_t s = 0; s < a.shadow_iters; ++s) {
                     const f3 lpos = light_sample(L, r);
                     f3 Lv = lpos - h.pos;
@@ -1150,7 +1162,7 @@ __global__ __launch_bounds__(256) void rt_record_colour_kernel(RaytraceArgs a, R
             f3 color = splat(0.0f);
             uint32_t jl = 0, jp = 0;
             for (int l = 0; l < a.n_lights; ++l) {
-                const bool point = a.lights[l].type == 0;
+                const bool point = const_load(a.lights, l).type == 0;
                 for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
                     const float4 l4 = *q.lc_at(k0 + lane, jl);
                     const f3 c = mk(l4.x, l4.y, l4.z);
@@ -1182,9 +1194,19 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
         constexpr uint32_t PRE = 16;
         const uint32_t cnt = q.pcount[t];
         const int* L = q.plist + (size_t)t * q.max_hits;
+        // unconditional loads within the pixel's list (slots past the count re-read its last record and are discarded by the
+        // select): a conditional load per slot compiled into a branch and a wait per record, i.e. 16 serial round trips
         float4 v[PRE];
+        if (cnt) {   // (a pixel without hits -- most of them -- loads nothing)
+            int idx[PRE];
 #pragma unroll
-        for (uint32_t h = 0; h < PRE; ++h) v[h] = h < cnt ? q.rval[L[h]] : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0xFFFFFFFFu));
+            for (uint32_t h = 0; h < PRE; ++h) idx[h] = L[min(h, cnt - 1u)];
+#pragma unroll
+            for (uint32_t h = 0; h < PRE; ++h) {
+                const float4 x = q.rval[idx[h]];
+                v[h] = h < cnt ? x : make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(0xFFFFFFFFu));
+            }
+        }
         uint32_t h = 0;
         for (uint32_t spp = 0; spp < a.samples; ++spp) {
             f3 shade_s = splat(0.0f);
@@ -1213,7 +1235,7 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
             f3 color = splat(0.0f);
             uint32_t jl = 0, jp = 0;
             for (int l = 0; l < a.n_lights; ++l) {
-                const bool point = a.lights[l].type == 0;
+                const bool point = const_load(a.lights, l).type == 0;
                 for (uint32_t s = 0; s < a.shadow_iters; ++s, ++jl) {
                     const float4 l4 = *q.lc_at((uint32_t)k, jl);
                     const f3 c = mk(l4.x, l4.y, l4.z);
