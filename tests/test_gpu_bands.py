@@ -352,3 +352,27 @@ def test_fused_shadow_band_equals_separate_shadow_kernel(rows):
             assert np.array_equal(out[0][b].view(np.uint32), out[1][b].view(np.uint32)), b
     finally:
         tb.close()
+
+
+@pytest.mark.parametrize("config", ["c3", "c4"])
+def test_rt_first_is_scheduling_only(config):
+    """rt_first: on concurrent frames the NeRF stream waits on the device (bounded) for the path kernel's first workgroup
+    before init_rays.  It changes only when work lands on the CUs: the frame buffers and the RNG states are the same bits
+    with and without it, over two frames."""
+    from synerfgine_amd import scene as S
+    tb, eng, _ = S.make_engine(config, width=480, height=270, model="lego" if config == "c3" else "synthetic")
+    try:
+        fresh = _fresh_fn(eng)
+        out = {}
+        for on in (0, 1):
+            eng.set_param("rt_first", on)
+            fresh()
+            for k in range(2):
+                r = eng.frame(target_n_queries=TARGET if config == "c3" else 0)
+            out[on] = {b: r.download(b).copy() for b in ("final_rgba", "syn_rgba", "syn_depth", "nerf_rgba")}
+            out[on]["rng0"] = eng.rng_states(0).copy()
+            out[on]["rng1"] = eng.rng_states(1).copy()
+        for b in out[0]:
+            assert np.array_equal(out[0][b].view(np.uint32), out[1][b].view(np.uint32)), b
+    finally:
+        tb.close()
