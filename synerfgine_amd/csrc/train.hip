@@ -229,34 +229,8 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
     const uint32_t numsteps = ns.x, base = ns.y;
     const float* __restrict__ cin = b.coords + (size_t)base * 7;
     const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
-    float T = 1.0f;
-    const float EPSILON = 1e-4f;
-    f3 rgb_ray = splat(0.0f);
-    uint32_t cn = 0;
-    bool stop = false;
-    for (uint32_t c0 = 0; c0 < numsteps && !stop; c0 += LOSS_G) {
-        const uint32_t j = min(c0 + gl, numsteps - 1);
-        const uint2 ow = *reinterpret_cast<const uint2*>(nout + (size_t)j * 4);
-        const float o0 = h2f((uint16_t)(ow.x & 0xffffu)), o1 = h2f((uint16_t)(ow.x >> 16));
-        const float o2 = h2f((uint16_t)(ow.y & 0xffffu)), o3 = h2f((uint16_t)(ow.y >> 16));
-        const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
-        const float dt = unwarp_dt(cin[(size_t)j * 7 + 3]);
-        const float density = sng_expf(o3);
-        const float alpha = 1.0f - sng_expf(-density * dt);
-        for (uint32_t u = 0; u < LOSS_G; ++u) {
-            if (c0 + u >= numsteps) break;
-            if (T < EPSILON) { stop = true; break; }
-            const int src = (int)(g0 + u);
-            const float au = __shfl(alpha, src, 64);
-            const f3 ru = mk(__shfl(rgb.x, src, 64), __shfl(rgb.y, src, 64), __shfl(rgb.z, src, 64));
-            const float weight = au * T;
-            rgb_ray = rgb_ray + weight * ru;
-            if (gl == u) b.partial[base + cn] = make_float4(T, rgb_ray.x, rgb_ray.y, rgb_ray.z);   // train_dloss_kernel replays from here
-            T *= (1.0f - au);
-            ++cn;
-        }
-    }
-    // same RNG draws as train_generate_kernel for this ray: uv, (max_level off), motionblur, then bg
+    // the ray's target colour first (independent of the chain below, so its image read overlaps it): the same RNG draws
+    // as train_generate_kernel for this ray -- uv, (max_level off), motionblur, then bg
     const uint32_t ray_idx = b.ray_indices[i];
     rng.advance((uint64_t)ray_idx * N_MAX_RANDOM_SAMPLES_PER_RAY);
     const uint32_t img = ((ray_idx * im.n) / a.n_rays) % im.n;
@@ -273,6 +247,47 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
         target = mk(linear_to_srgb(lin.x), linear_to_srgb(lin.y), linear_to_srgb(lin.z)) * tex.w + (1.0f - tex.w) * bg;
     } else {
         target = bg;
+    }
+    float T = 1.0f;
+    const float EPSILON = 1e-4f;
+    f3 rgb_ray = splat(0.0f);
+    uint32_t cn = 0;
+    bool stop = false;
+    // the next chunk's output and dt are loaded while this chunk's transmittance chain runs (clamped index: the last
+    // sample again past the ray's end, unused)
+    uint2 ow_n = make_uint2(0u, 0u);
+    float wdt_n = 0.0f;
+    if (numsteps) {
+        const uint32_t j0 = min(gl, numsteps - 1);
+        ow_n = *reinterpret_cast<const uint2*>(nout + (size_t)j0 * 4);
+        wdt_n = cin[(size_t)j0 * 7 + 3];
+    }
+    for (uint32_t c0 = 0; c0 < numsteps && !stop; c0 += LOSS_G) {
+        const uint2 ow = ow_n;
+        const float wdt = wdt_n;
+        {
+            const uint32_t jn = min(c0 + LOSS_G + gl, numsteps - 1);
+            ow_n = *reinterpret_cast<const uint2*>(nout + (size_t)jn * 4);
+            wdt_n = cin[(size_t)jn * 7 + 3];
+        }
+        const float o0 = h2f((uint16_t)(ow.x & 0xffffu)), o1 = h2f((uint16_t)(ow.x >> 16));
+        const float o2 = h2f((uint16_t)(ow.y & 0xffffu)), o3 = h2f((uint16_t)(ow.y >> 16));
+        const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
+        const float dt = unwarp_dt(wdt);
+        const float density = sng_expf(o3);
+        const float alpha = 1.0f - sng_expf(-density * dt);
+        for (uint32_t u = 0; u < LOSS_G; ++u) {
+            if (c0 + u >= numsteps) break;
+            if (T < EPSILON) { stop = true; break; }
+            const int src = (int)(g0 + u);
+            const float au = __shfl(alpha, src, 64);
+            const f3 ru = mk(__shfl(rgb.x, src, 64), __shfl(rgb.y, src, 64), __shfl(rgb.z, src, 64));
+            const float weight = au * T;
+            rgb_ray = rgb_ray + weight * ru;
+            if (gl == u) b.partial[base + cn] = make_float4(T, rgb_ray.x, rgb_ray.y, rgb_ray.z);   // train_dloss_kernel replays from here
+            T *= (1.0f - au);
+            ++cn;
+        }
     }
     if (cn == numsteps) rgb_ray = rgb_ray + T * bg;
     if (!in || gl != 0) return;
