@@ -155,7 +155,9 @@ int sng_get_density_mean(sng_ctx* ctx, float* out);
 /* ---- operator boundary: NerfNetwork::inference_mixed_precision (nerf_network.h:105-139)
  * d_coords: NerfCoordinate AoS {pos(3), dt, dir(3)} with stride_floats >= 7;
  * out_layout 0: tcnn GPUMatrix<half,RM> [16][n] (row c at c*n; row 3 = density);
- * out_layout 1: AoS [n][4] = (r,g,b,density) raw network outputs. */
+ * out_layout 1: AoS [n][4] = (r,g,b,density) raw network outputs;
+ * out_layout 2: AoS [n][4] with the density only, rgb = 0 (NerfNetwork::density, nerf_network.h:270: the density MLP
+ *               alone, as the density-grid update evaluates it). */
 int sng_nerf_inference(sng_ctx* ctx, const float* d_coords, uint32_t stride_floats, uint32_t n,
                        uint16_t* d_out, int32_t out_layout, void* hip_stream);
 /* pos encoding only (tcnn GridEncoding forward), out [n][L*F] fp16 -- parity hook */

@@ -426,6 +426,7 @@ const std::map<std::string, double>& default_params() {
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
         {"train_gen_bricks", 0},                // training generator's occupancy: 0 the linear words (measured fastest, tools/train_ab.py), 1 the OccBrick blob (LDS when it fits, else global)
         {"train_grid_grad_f16", 1},             // hash-grid gradients in fp16 with packed atomics, tcnn's grad_t (__half2 atomicAdd); 0: f32
+        {"train_grid_density_only", 1},         // density-grid update: the density MLP alone (NerfNetwork::density), not the full network
         {"train_dw_pipe", 1},                   // dW kernel: the next tile's operands in flight during the current tile's MFMAs (0: load, then multiply)
         {"train_dw_blocks_per_cu", 2},          // dW kernel: workgroups per CU (tools/train_ab.py)
         {"train_gen_lanes", 8},                 // lanes per ray of the training generator's speculative march (8 or 16; 1: one lane per ray; tools/train_ab.py)
@@ -2094,7 +2095,8 @@ void train_density_update(sng_ctx* c, hipStream_t s) {
     t.grid_rng.advance();
     // density of the training parameters (m_nerf_network->density, use_inference_params = false)
     launch_train_pack(t.p_train.as<uint16_t>(), t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
-    launch_network(train_net(c, t.p_train, t.wfrag_train), t.grid_coords.as<float>(), 7, n_tot, nullptr, t.grid_out.as<uint16_t>(), 1, 0, s);
+    launch_network(train_net(c, t.p_train, t.wfrag_train), t.grid_coords.as<float>(), 7, n_tot, nullptr, t.grid_out.as<uint16_t>(),
+                   c->p("train_grid_density_only") != 0.0 ? 2 : 1, 0, s);
     launch_train_grid_splat_ema(n_tot, t.grid_idx.as<uint32_t>(), t.grid_out.as<uint16_t>(), t.grid_tmp.as<float>(), n_cells, 0.95f, t.grid.as<float>(), s);
     ++t.grid_ema_step;
     HIPCHK(hipMemcpyAsync(c->d_grid_f32.p, t.grid.p, (size_t)n_cells * 4, hipMemcpyDeviceToDevice, s));
@@ -2894,7 +2896,7 @@ int sng_nerf_inference(sng_ctx* c, const float* coords, uint32_t stride, uint32_
     return guarded([&] {
         if (!c->has_model) throw SngError(SNG_ERR_STATE, "no model");
         if (stride < 7) throw SngError(SNG_ERR_INVALID, "NerfCoordinate stride must be >= 7 floats");
-        if (layout != 0 && layout != 1) throw SngError(SNG_ERR_INVALID, "out_layout must be 0 or 1");
+        if (layout < 0 || layout > 2) throw SngError(SNG_ERR_INVALID, "out_layout must be 0, 1 or 2");
         if (n == 0) return;
         launch_network(c->net, coords, stride, n, nullptr, out, layout, 0, (hipStream_t)stream);
         HIPCHK(hipGetLastError());

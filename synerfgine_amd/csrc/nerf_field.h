@@ -198,7 +198,8 @@ struct LdsWeights {
     __device__ __forceinline__ h8 operator[](int f) const { return base[f * 64 + lane]; }
 };
 
-template <int F, bool GATHER_ALL = false, typename WT = const h8*>
+// DENS_ONLY: the density MLP alone (NerfNetwork::density, the density-grid update): o = 0, no SH, no rgb MLP
+template <int F, bool GATHER_ALL = false, typename WT = const h8*, bool DENS_ONLY = false>
 __device__ __forceinline__ void field_tile(WT W, const LevelInfo* __restrict__ levels, const _Float16* __restrict__ grid, int g, float x0,
                                            float x1, float x2, float d0, float d1, float d2, f4v& o, f4v& dens) {
     const f4v zero = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -208,6 +209,10 @@ __device__ __forceinline__ void field_tile(WT W, const LevelInfo* __restrict__ l
     f4v a0 = mfma16(W[0], enc, zero), a1 = mfma16(W[1], enc, zero), a2 = mfma16(W[2], enc, zero), a3 = mfma16(W[3], enc, zero);
     dens = mfma16(W[4], pack_relu(a0, a1), zero);
     dens = mfma16(W[5], pack_relu(a2, a3), dens);
+    if constexpr (DENS_ONLY) {
+        o = zero;
+        return;
+    }
     // ---- rgb MLP input: slots 0-3 = density_out rows 4g..4g+3 (fp16), 4-7 = SH 4g..4g+3
     float sh[4];
     sh_lane(g, d0, d1, d2, sh);

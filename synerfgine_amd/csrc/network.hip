@@ -29,7 +29,7 @@ namespace sng {
 #ifndef NET_WAVES_PER_EU
 #define NET_WAVES_PER_EU 3
 #endif
-template <int F, int OUT_LAYOUT>
+template <int F, int OUT_LAYOUT, bool DENS_ONLY = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NET_WAVES_PER_EU))) void nerf_network_kernel(const float* __restrict__ coords, uint32_t stride, uint32_t n_static,
                                                            const uint32_t* __restrict__ n_dev, const h8* __restrict__ wfrag,
                                                            const _Float16* __restrict__ grid, const LevelInfo* __restrict__ levels,
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NET_WAVES_P
         const float d0 = c[4], d1 = c[5], d2 = c[6];
 
         f4v o, dens;
-        field_tile<F>(W, levels, grid, g, x0, x1, x2, d0, d1, d2, o, dens);
+        field_tile<F, false, LdsWeights, DENS_ONLY>(W, levels, grid, g, x0, x1, x2, d0, d1, d2, o, dens);
 
         if (!valid) continue;
         if constexpr (OUT_LAYOUT == 1) {
@@ -137,11 +137,14 @@ int launch_network(const NetworkDev& net, const float* coords, uint32_t stride, 
         else
             hipLaunchKernelGGL(kernel, dim3(blocks), dim3(256), 0, stream, coords, stride, n_static, n_dev, w, gr, net.levels, out, n_static, n_rec);
     };
+    // layout 2: [n][4] with the density only (rgb 0; NerfNetwork::density for the density-grid update)
     if (net.F == 4) {
-        if (layout == 1) go(nerf_network_kernel<4, 1>);
+        if (layout == 2) go(nerf_network_kernel<4, 1, true>);
+        else if (layout == 1) go(nerf_network_kernel<4, 1>);
         else go(nerf_network_kernel<4, 0>);
     } else {
-        if (layout == 1) go(nerf_network_kernel<2, 1>);
+        if (layout == 2) go(nerf_network_kernel<2, 1, true>);
+        else if (layout == 1) go(nerf_network_kernel<2, 1>);
         else go(nerf_network_kernel<2, 0>);
     }
     return 0;

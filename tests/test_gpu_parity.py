@@ -142,6 +142,21 @@ def test_network_stride_and_padding(tb, model, oracle_lib):
     assert (np.abs(got - ref) <= 2 * _fp16_ulp(ref) + 1e-3).all()
 
 
+def test_network_density_only_layout(tb, model):
+    """out_layout 2 (NerfNetwork::density, nerf_network.h:270; the density-grid update): the density column is the full
+    network's bit for bit, the rgb columns are 0."""
+    n = 4099
+    dc = torch.from_numpy(_coords(n, seed=5)).cuda()
+    full = torch.zeros((n, 4), dtype=torch.float16, device="cuda")
+    dens = torch.full((n, 4), 7.0, dtype=torch.float16, device="cuda")
+    tb.inference_mixed_precision(dc.data_ptr(), 7, n, full.data_ptr(), layout=1)
+    tb.inference_mixed_precision(dc.data_ptr(), 7, n, dens.data_ptr(), layout=2)
+    torch.cuda.synchronize()
+    f, d = full.cpu().numpy(), dens.cpu().numpy()
+    assert np.array_equal(f[:, 3].view(np.uint16), d[:, 3].view(np.uint16))
+    assert (d[:, :3] == 0).all()
+
+
 def _engine(w, h, overrides=None, config="c3"):
     from synerfgine_amd import scene as S
     ov = {"res_factor": 8}
