@@ -150,7 +150,7 @@ class Testbed:
 
     # ---- NerfNetwork::inference_mixed_precision (nerf_network.h:105) -------------
     def inference_mixed_precision(self, d_coords, stride_floats, n, d_out, layout=0, stream=0):
-        """Device pointers in, device pointer out (layout 0: tcnn [16][n]; 1: [n][4])."""
+        """Device pointers in, device pointer out (layout 0: tcnn [16][n]; 1: [n][4]; 2: [n][4] density only, NerfNetwork::density)."""
         check(self._lib.sng_nerf_inference(self.ctx, ctypes.c_void_p(d_coords), stride_floats, n, ctypes.c_void_p(d_out), layout,
                                            ctypes.c_void_p(stream)))
 
