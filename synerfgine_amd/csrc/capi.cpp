@@ -424,6 +424,8 @@ const std::map<std::string, double>& default_params() {
         {"render_mode", 1},                     // ERenderMode of the instant-NGP path (sng_render_nerf_ngp): Shade
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
+        {"train_grid_est", 0},                  // > 0: the per-ray training kernels' grid sized for this many rays (tests of their grid-stride loops)
+        {"train_grid_morton", 1},               // density-grid update: the uniform samples in the Morton order of their cells (same samples, same grid)
         {"train_gen_bricks", 0},                // training generator's occupancy: 0 the linear words (measured fastest, tools/train_ab.py), 1 the OccBrick blob (LDS when it fits, else global)
         {"train_grid_grad_f16", 1},             // hash-grid gradients in fp16 with packed atomics, tcnn's grad_t (__half2 atomicAdd); 0: f32
         {"train_grid_density_only", 1},         // density-grid update: the density MLP alone (NerfNetwork::density), not the full network
@@ -591,6 +593,17 @@ struct sng_ctx {
         uint32_t step = 0, grid_ema_step = 0;
         uint32_t rays_per_batch = 1u << 12;            // testbed.h:509
         uint32_t measured = 0, measured_before = 0;
+        // the device copy of those (TrainSched) is the one the steps read and update; the host fields above are pushed
+        // when set on the host (reset, snapshot load) and pulled when train_steps returns
+        DevBuf sched;
+        bool sched_dirty = true;
+        // pinned readbacks of the device's batch sizes every 8 steps into two slots; reusing a slot waits for its
+        // previous copy, so the host queues at most ~16 steps ahead and the grid-size estimate lags by at most that
+        TrainSched* h_sched = nullptr;                 // [2]
+        hipEvent_t sched_ev[2] = {nullptr, nullptr};
+        bool sched_pending[2] = {false, false};
+        uint32_t sched_slot = 0;
+        uint32_t n_rays_est = 1u << 12;                // grid sizes only (n_rays_grid)
         Pcg32 rng{}, grid_rng{};
         int w = 0, h = 0, n_images = 0;
         DevBuf pixels, xforms, xforms_ray, focal, pp;
@@ -2050,6 +2063,8 @@ void train_reset(sng_ctx* c, uint64_t seed) {
     t.rng = Pcg32::seeded(seed);
     t.grid_rng = Pcg32::seeded(t.rng.next_uint());
     t.step = 0; t.grid_ema_step = 0; t.rays_per_batch = 1u << 12; t.measured = 0; t.measured_before = 0;
+    t.sched.ensure(sizeof(TrainSched));
+    t.sched_dirty = true;
     t.target = (uint32_t)c->p("train_batch");
     const uint32_t target = t.target, max_samples = target * 16;
     t.ctrl.ensure(sizeof(TrainCtrl));
@@ -2060,6 +2075,10 @@ void train_reset(sng_ctx* c, uint64_t seed) {
     t.acts.ensure((size_t)((target + 15) / 16) * TRAIN_FEATS * 16 * 2);
     t.partial.ensure((size_t)max_samples * 16); t.rayrec.ensure(max_rays * 48);
     t.cnt_i.ensure(max_rays * 4); t.cbase_i.ensure(max_rays * 4);
+    t.tscr.ensure(max_rays * NERF_STEPS * 4);   // strided by the device's ray count, which the host does not wait for
+    if (!t.h_sched) HIPCHK(hipHostMalloc((void**)&t.h_sched, 2 * sizeof(TrainSched), hipHostMallocDefault));
+    for (hipEvent_t& e : t.sched_ev)
+        if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     // the bitfield the training marcher reads (density grid -> bitfield after every update)
     c->d_grid_f32.ensure((size_t)n_cells * 4);
     c->d_partial.ensure(1024 * sizeof(double));
@@ -2088,10 +2107,12 @@ void train_density_update(sng_ctx* c, hipStream_t s) {
     const uint32_t n_tot = n_uni + n_non;
     t.grid_coords.ensure((size_t)n_tot * 28); t.grid_idx.ensure((size_t)n_tot * 4); t.grid_out.ensure((size_t)n_tot * 8);
     HIPCHK(hipMemsetAsync(t.grid_tmp.p, 0, (size_t)n_cells * 4, s));
-    launch_train_grid_samples(n_uni, t.grid_rng, t.grid_ema_step, c->box, t.grid.as<float>(), t.grid_coords.as<float>(), t.grid_idx.as<uint32_t>(), n_casc, -0.01f, s);
+    const int morton = c->p("train_grid_morton") != 0.0 ? 1 : 0;
+    launch_train_grid_samples(n_uni, t.grid_rng, t.grid_ema_step, c->box, t.grid.as<float>(), t.grid_coords.as<float>(), t.grid_idx.as<uint32_t>(), n_casc, -0.01f,
+                              morton, s);
     t.grid_rng.advance();
     launch_train_grid_samples(n_non, t.grid_rng, t.grid_ema_step, c->box, t.grid.as<float>(), t.grid_coords.as<float>() + (size_t)n_uni * 7,
-                              t.grid_idx.as<uint32_t>() + n_uni, n_casc, NERF_MIN_OPTICAL_THICKNESS, s);
+                              t.grid_idx.as<uint32_t>() + n_uni, n_casc, NERF_MIN_OPTICAL_THICKNESS, morton, s);
     t.grid_rng.advance();
     // density of the training parameters (m_nerf_network->density, use_inference_params = false)
     launch_train_pack(t.p_train.as<uint16_t>(), t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
@@ -2110,10 +2131,10 @@ TrainStepArgs train_args(sng_ctx* c) {
     auto& t = c->tr;
     TrainStepArgs a{};
     a.vol = make_volume(c);
-    a.n_rays = t.rays_per_batch;
+    a.sched = t.sched.as<TrainSched>();
+    a.n_rays_grid = std::min(t.n_rays_est + t.n_rays_est / 4, 1u << 18);   // a lagged estimate plus room for its growth
+    if (c->p("train_grid_est") > 0.0) a.n_rays_grid = (uint32_t)c->p("train_grid_est");   // tests: force the kernels' grid-stride trips
     a.target_batch = t.target;
-    const uint32_t max_samples = t.target * 16;
-    a.max_samples = t.measured_before == 0 ? max_samples : (std::min(t.measured_before, max_samples) + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY;
     a.random_bg = c->p("train_random_bg") != 0.0 ? 1 : 0;
     a.background = mk(0.0f, 0.0f, 0.0f);
     a.loss_scale = 128.0f;   // default_loss_scale<__half>
@@ -2140,14 +2161,22 @@ TrainBatch train_batch(sng_ctx* c) {
 // event is recorded by train_steps)
 void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev = nullptr) {
     auto& t = c->tr;
+    if (t.sched_dirty) {   // host-set batch sizes (reset, snapshot load): train_args' max_inference from measured_before
+        const uint32_t cap = t.target * 16;
+        const TrainSched h{t.rays_per_batch,
+                           t.measured_before == 0 ? cap : (std::min(t.measured_before, cap) + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY,
+                           t.measured, t.measured_before};
+        HIPCHK(hipMemcpyAsync(t.sched.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));   // h is a stack value
+        t.n_rays_est = t.rays_per_batch;
+        t.sched_dirty = false;
+    }
     const TrainStepArgs a = train_args(c);
     const TrainBatch b = train_batch(c);
     const TrainImages im = train_images(c);
-    HIPCHK(hipMemsetAsync(t.ctrl.p, 0, sizeof(TrainCtrl), s));
-    HIPCHK(hipMemsetAsync(t.loss.p, 0, (size_t)a.n_rays * 4, s));
+    launch_train_clear(a, b, s);   // also zeroes the batch counters (TrainCtrl)
     auto mark = [&](int k) { if (ev) HIPCHK(hipEventRecord(ev[k], s)); };
     mark(0);
-    t.tscr.ensure((size_t)a.n_rays * NERF_STEPS * 4);
     launch_train_generate(a, im, b, t.rng, t.tscr.as<float>(), s);
     mark(1);
     if (stage == 1) return;
@@ -2155,8 +2184,8 @@ void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev
     launch_train_pack(t.p_train.as<uint16_t>(), t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
     const NetworkDev net = train_net(c, t.p_train, t.wfrag_train);
     // count = min(numsteps_counter, max_samples): the generator drops rays beyond max_samples
-    launch_train_clamp_count(&b.ctrl->numsteps_counter, a.max_samples, t.ctrl.as<uint32_t>() + 3, s);
-    launch_network(net, b.coords, 7, 0, t.ctrl.as<uint32_t>() + 3, b.mlp_out, 1, (a.max_samples + 15) / 16, s);
+    launch_train_clamp_count(&b.ctrl->numsteps_counter, a.sched, t.ctrl.as<uint32_t>() + 3, s);
+    launch_network(net, b.coords, 7, 0, t.ctrl.as<uint32_t>() + 3, b.mlp_out, 1, (t.target * 16 + 15) / 16, s);
     mark(2);
     if (stage == 2) return;
     launch_train_loss(a, im, b, t.rng, c->d_mean.as<float>(), s);
@@ -2211,8 +2240,10 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
                 t.adam_corr.ensure(((size_t)need + 4096) / 4096 * 4096 * 4);
                 t.adam_corr_n = 0;
             }
-            launch_train_adam_corr(t.adam_corr.as<float>(), t.adam_corr_n + 1, need, o.beta1, o.beta2, s);
-            t.adam_corr_n = need;
+            // the table's whole capacity at once (one small launch per 4096 steps instead of one per step)
+            const uint32_t to = (uint32_t)(t.adam_corr.bytes / 4) - 1;
+            launch_train_adam_corr(t.adam_corr.as<float>(), t.adam_corr_n + 1, to, o.beta1, o.beta2, s);
+            t.adam_corr_n = to;
         }
         o.corr = t.adam_corr.as<float>();
         o.corr_n = t.adam_corr_n;
@@ -2222,32 +2253,30 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
         if (timed) HIPCHK(hipEventRecord(c->train_events[7], s));
         t.rng.advance();
         ++t.step;
-        // NerfCounters::update_after_training (3272-3296): host readback of the two sample counts
-        TrainCtrl h{};
-        HIPCHK(hipMemcpyAsync(&h, t.ctrl.p, sizeof(TrainCtrl), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        if (timed) {
+        // NerfCounters::update_after_training (3272-3296) on the device: the next step reads its batch sizes from there,
+        // so the host queues the steps without waiting for each (the reference syncs on a readback every step)
+        launch_train_sched_update(t.sched.as<TrainSched>(), t.ctrl.as<TrainCtrl>(), t.target, s);
+        // the grid-size estimate follows the device's ray count through the readback slots (correctness never depends
+        // on it: the kernels loop over the device count)
+        if (t.step % 8 == 0) {
+            const uint32_t q = t.sched_slot;
+            if (t.sched_pending[q]) {   // issued 16 steps ago: waits only while the host is further ahead than that
+                HIPCHK(hipEventSynchronize(t.sched_ev[q]));
+                t.n_rays_est = std::max(t.h_sched[q].n_rays, 256u);
+            }
+            HIPCHK(hipMemcpyAsync(&t.h_sched[q], t.sched.p, sizeof(TrainSched), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipEventRecord(t.sched_ev[q], s));
+            t.sched_pending[q] = true;
+            t.sched_slot ^= 1u;
+        }
+        if (timed) {   // per-stage times need the step's events: one wait per step in this mode only
+            HIPCHK(hipStreamSynchronize(s));
             for (int q = 0; q < 7; ++q) {
                 float ms = 0.0f;
                 HIPCHK(hipEventElapsedTime(&ms, c->train_events[q], c->train_events[q + 1]));
                 stage_ms[q] += ms;
             }
             ++timed_steps;
-        }
-        if (h.numsteps_counter == 0 || h.numsteps_compacted == 0) {
-            t.measured = t.measured_before = 0;
-        } else {
-            t.measured_before = h.numsteps_counter;
-            t.measured = h.numsteps_compacted;
-            uint32_t r = (uint32_t)((float)t.rays_per_batch * (float)t.target / (float)t.measured);
-            t.rays_per_batch = std::min((r + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY, 1u << 18);
-        }
-        if (out && k + 1 == n_steps) {
-            std::vector<float> l(std::max<uint32_t>(1, h.ray_counter));
-            const uint32_t nr = std::min<uint32_t>(h.ray_counter, (uint32_t)(t.loss.bytes / 4));
-            if (nr) HIPCHK(hipMemcpy(l.data(), t.loss.p, nr * 4, hipMemcpyDeviceToHost));
-            for (uint32_t i = 0; i < nr; ++i) loss_acc += l[i];
-            t.last_loss = (float)(loss_acc * (double)t.measured / (double)t.target);
         }
     }
     HIPCHK(hipEventRecord(c->ev_end, s));
@@ -2257,6 +2286,22 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
     HIPCHK(hipMemcpyAsync(c->d_params.p, t.p_infer.p, c->n_params * 2, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));
+    if (n_steps) {   // the device's batch sizes and the last step's counters back to the host
+        TrainSched h{};
+        TrainCtrl hc{};
+        HIPCHK(hipMemcpy(&h, t.sched.p, sizeof(h), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&hc, t.ctrl.p, sizeof(hc), hipMemcpyDeviceToHost));
+        t.rays_per_batch = h.n_rays; t.measured = h.measured; t.measured_before = h.measured_before;
+        t.n_rays_est = h.n_rays;
+        t.sched_pending[0] = t.sched_pending[1] = false;
+        if (out) {
+            std::vector<float> l(std::max<uint32_t>(1, hc.ray_counter));
+            const uint32_t nr = std::min<uint32_t>(hc.ray_counter, (uint32_t)(t.loss.bytes / 4));
+            if (nr) HIPCHK(hipMemcpy(l.data(), t.loss.p, nr * 4, hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < nr; ++i) loss_acc += l[i];
+            t.last_loss = (float)(loss_acc * (double)t.measured / (double)t.target);
+        }
+    }
     if (out) {
         std::memset(out, 0, sizeof(*out));
         out->step = t.step;
@@ -2360,6 +2405,9 @@ void ctx_destroy(sng_ctx* c) {
     for (hipEvent_t e : {c->ev_start, c->ev_rt0, c->ev_rt1, c->ev_nerf0, c->ev_nerf1, c->ev_shadow1, c->ev_end, c->ev_rt_go, c->ev_fused0, c->ev_fused1, c->ev_os0, c->ev_os1, c->ev_alive, c->ev_brick}) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->net_events) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->train_events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->tr.sched_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->tr.h_sched) (void)hipHostFree(c->tr.h_sched);
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);
     (void)hipHostFree(c->h_os);

@@ -1461,10 +1461,16 @@ __global__ __launch_bounds__(256) void mean_partial_kernel(const float* __restri
     }
     if (threadIdx.x == 0) partial[blockIdx.x] = sm[0];
 }
-__global__ void mean_final_kernel(const double* __restrict__ partial, int n_part, float* __restrict__ mean) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
+// the partials staged in LDS by coalesced loads, then one lane sums them in index order (the same double sequence;
+// one lane reading global memory in turn took ~70 us)
+__global__ __launch_bounds__(256) void mean_final_kernel(const double* __restrict__ partial, int n_part, float* __restrict__ mean) {
+    __shared__ double sm[1024];
+    for (int i = threadIdx.x; i < n_part && i < 1024; i += blockDim.x) sm[i] = partial[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
         double s = 0.0;
-        for (int i = 0; i < n_part; ++i) s += partial[i];
+#pragma unroll 16
+        for (int i = 0; i < n_part; ++i) s += sm[i];
         *mean = (float)s;
     }
 }
@@ -1672,7 +1678,7 @@ void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid
     const uint32_t n_cells = N * (max_cascade + 1);
     if (grid_f16) hipLaunchKernelGGL(half_to_float_kernel, dim3((n_cells + 255) / 256), dim3(256), 0, s, grid_f16, grid_f32, n_cells);   // else grid_f32 is given
     hipLaunchKernelGGL(mean_partial_kernel, dim3(1024), dim3(256), 0, s, grid_f32, N, partial);
-    hipLaunchKernelGGL(mean_final_kernel, dim3(1), dim3(64), 0, s, partial, 1024, mean);
+    hipLaunchKernelGGL(mean_final_kernel, dim3(1), dim3(256), 0, s, partial, 1024, mean);
     const uint32_t n_el = N / 8 * N_CASCADES;
     hipLaunchKernelGGL(grid_to_bitfield_kernel, dim3((n_el + 255) / 256), dim3(256), 0, s, n_el, N / 8 * (max_cascade + 1), grid_f32, bf, mean);
     for (uint32_t level = 1; level < N_CASCADES; ++level)

@@ -135,10 +135,19 @@ struct TrainCtrl {
     uint32_t pad;
 };
 
+// NerfCounters' batch sizes (testbed_nerf.cu:3272-3296), kept on the device: the step's kernels read them, and
+// train_sched_update_kernel forms the next step's from the step's counters, so the host never waits for a step
+struct TrainSched {
+    uint32_t n_rays;            // rays_per_batch
+    uint32_t max_samples;       // max_inference (from measured_before)
+    uint32_t measured;          // measured_batch_size (after compaction)
+    uint32_t measured_before;   // measured_batch_size_before_compaction
+};
+
 struct TrainStepArgs {
     Volume vol;              // train_aabb, bitfield, max_mip, cone
-    uint32_t n_rays;         // rays_per_batch
-    uint32_t max_samples;    // max_inference
+    const TrainSched* sched; // this step's n_rays / max_samples (device)
+    uint32_t n_rays_grid;    // the host's estimate of n_rays: grid sizes only (the kernels loop over the device count)
     uint32_t target_batch;   // m_training_batch_size
     int random_bg;
     f3 background;
@@ -183,7 +192,11 @@ struct AdamArgs {
     const uint16_t* grads_h;  // fp16 grid gradients (param index - n_matrix), nullptr: every gradient in `grads`
 };
 
-void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, hipStream_t s);
+void launch_train_clamp_count(const uint32_t* in, const TrainSched* sched, uint32_t* out, hipStream_t s);
+// the next step's TrainSched from this step's counters (NerfCounters::update_after_training)
+void launch_train_sched_update(TrainSched* sched, const TrainCtrl* ctrl, uint32_t target, hipStream_t s);
+// zero loss / rayrec / cnt_i for the step's rays (device count)
+void launch_train_clear(const TrainStepArgs& a, const TrainBatch& b, hipStream_t s);
 // tscr: [NERF_STEPS][n_rays] floats of scratch (the first march's sample distances)
 void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, float* tscr, hipStream_t s);
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s);
@@ -196,8 +209,9 @@ void launch_train_adam(const AdamArgs& o, uint64_t n, uint32_t n_matrix, float* 
 // Adam's bias-correction factor for the per-parameter step counts s = from..to (the expression adam_one would form)
 void launch_train_adam_corr(float* corr, uint32_t from, uint32_t to, float beta1, float beta2, hipStream_t s);
 void launch_train_mark_untrained(uint32_t n, float* grid, const TrainImages& im, int clear_visible, hipStream_t s);
+// morton: slots in the Morton order of the samples' first candidate cells when n is a multiple of GRID_CELLS
 void launch_train_grid_samples(uint32_t n, Pcg32 rng, uint32_t step, const aabb& box, const float* grid, float* coords, uint32_t* indices, uint32_t n_cascades,
-                               float thresh, hipStream_t s);
+                               float thresh, int morton, hipStream_t s);
 void launch_train_grid_splat_ema(uint32_t n_samples, const uint32_t* indices, const uint16_t* out4, float* tmp, uint32_t n_cells, float decay, float* grid,
                                  hipStream_t s);
 

@@ -43,73 +43,78 @@ __device__ __forceinline__ f4v mfma16k16(h4v a, h4v b, f4v c) { return __builtin
 // LIN (compile time): the unit-cube linear specialisation (cone 0, one cascade); otherwise the cascaded march with the
 // volume's StepSpace constants (the same float expressions as the cone forms, so the same bits, without their logs)
 template <int BRICK, bool LIN>
-__global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, float* __restrict__ tscr) {
+__global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng0, float* __restrict__ tscr) {
     extern __shared__ uint32_t occ_lds[];
     if constexpr (BRICK == 1) stage_occ_brick(occ_lds, a.vol.occ_brick, a.vol.occ_brick_words);
     const uint32_t* const bricks = BRICK == 1 ? occ_lds : a.vol.occ_brick_g;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    // every lane stays to the wave's reservations below (wave_reserve); a lane without a ray marches nothing
-    const bool in = i < a.n_rays;
-    const uint32_t ii = in ? i : 0u;
-    const uint32_t img = ((ii * im.n) / a.n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
-    rng.advance((uint64_t)ii * N_MAX_RANDOM_SAMPLES_PER_RAY);
-    const f2 uv = train_image_pos(rng, im);
-    const bool live = in && !(read_rgba(im, img, uv).x < 0.0f);   // masked pixel: no samples
-    (void)rng.next_float();                                    // motionblur_time
-    const TrainRay ray = train_ray(im, img, uv);
-    const f3 dn = normalize(ray.d);
-    const aabb box = a.vol.train_aabb;
-    float tmin = fmaxf(aabb_entry(box, ray.o, dn), 0.0f);      // aabb.ray_intersect(...).x, clamped at 0
-    const StepSpace& ss = a.vol.ss;
-    const float startt = LIN ? advance_n_steps(tmin, 0.0f, rng.next_float()) : advance_n_steps(tmin, ss, rng.next_float());
-    const f3 idir = inv(dn);
-    uint32_t j = 0;
-    float t = startt;
-    f3 pos;
-    // unit-cube scenes (cone 0, one cascade): the exact linear specialisation of the occupancy test and
-    // of advance_to_next_voxel that the render marcher uses (sng_math.h, tests/test_host_fastpaths.py)
-    static_assert(BRICK == 0 || LIN, "the brick forms are unit-cube only");
-    const f3 hs = half_sign(dn);
-    float* const ts = tscr + ii;
-    OccCache oc;
-    while (live && aabb_contains(box, pos = ray.o + t * dn) && j < NERF_STEPS) {
-        const float dt = LIN ? calc_dt(t, 0.0f) : calc_dt(t, ss);
-        bool occ;
-        // the cached forms reload a word only when the position leaves the last one (~4.6 samples per cell): each trip
-        // is a dependent load otherwise, and a batch has too few rays to hide that latency
-        if constexpr (BRICK != 0) occ = occupied_brick_c(pos, bricks, oc);
-        else if constexpr (LIN) occ = occupied_linear_c(pos, a.vol.occ_linear, oc);
-        else occ = occupied_at(pos, a.vol.bitfield, mip_from_dt(dt, pos, a.vol.max_mip));
-        // one trip is one sample or one DDA step, as a select: with an if / else the compiler nests a loop of DDA steps
-        // inside the sample loop, and a wave then waits at every sample for its lanes' longest run of empty cells
-        // (measured 3.4x slower)
-        float t_skip;
-        if constexpr (LIN) t_skip = dda_step_linear(t, pos, idir, hs);
-        else t_skip = advance_to_next_voxel(t, ss, pos, dn, idir, mip_from_dt(dt, pos, a.vol.max_mip));
-        if (occ) ts[(size_t)j * a.n_rays] = t;
-        j += occ ? 1u : 0u;
-        t = occ ? t + dt : t_skip;
-    }
-    if (a.debug && live) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
-    const uint32_t numsteps = j;
-    const uint32_t base = wave_reserve(&b.ctrl->numsteps_counter, numsteps, lane);
-    const bool keep = numsteps > 0 && base + numsteps <= a.max_samples;
-    const uint32_t ray_idx = wave_reserve(&b.ctrl->ray_counter, keep ? 1u : 0u, lane);
-    if (!keep) return;
-    b.ray_indices[ray_idx] = i;
-    b.rays[2 * ray_idx] = make_float4(ray.o.x, ray.o.y, ray.o.z, 0.0f);
-    b.rays[2 * ray_idx + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
-    b.numsteps[ray_idx] = make_uint2(numsteps, base);
-    const f3 wd = (dn + 1.0f) * 0.5f;   // warp_direction
-    const f3 diag = box.hi - box.lo;
-    float* co = b.coords + (size_t)base * 7;
-    for (uint32_t k = 0; k < numsteps; ++k) {
-        const float tk = ts[(size_t)k * a.n_rays];
-        const f3 p = ray.o + tk * dn;
-        const f3 wp = (p - box.lo) / diag;   // warp_position = aabb.relative_pos
-        float* c = co + (size_t)k * 7;
-        c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(LIN ? calc_dt(tk, 0.0f) : calc_dt(tk, ss)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+    // grid-stride over the device's ray count (the grid is sized by the host's estimate of it)
+    const uint32_t n_rays = a.sched->n_rays, max_samples = a.sched->max_samples;
+    for (uint32_t vb = blockIdx.x; vb * blockDim.x < n_rays; vb += gridDim.x) {
+        Pcg32 rng = rng0;   // each grid-stride trip starts from the step's stream (the ray's offset is added below)
+        const uint32_t i = vb * blockDim.x + threadIdx.x;
+        const int lane = threadIdx.x & 63;
+        // every lane stays to the wave's reservations below (wave_reserve); a lane without a ray marches nothing
+        const bool in = i < n_rays;
+        const uint32_t ii = in ? i : 0u;
+        const uint32_t img = ((ii * im.n) / n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
+        rng.advance((uint64_t)ii * N_MAX_RANDOM_SAMPLES_PER_RAY);
+        const f2 uv = train_image_pos(rng, im);
+        const bool live = in && !(read_rgba(im, img, uv).x < 0.0f);   // masked pixel: no samples
+        (void)rng.next_float();                                    // motionblur_time
+        const TrainRay ray = train_ray(im, img, uv);
+        const f3 dn = normalize(ray.d);
+        const aabb box = a.vol.train_aabb;
+        float tmin = fmaxf(aabb_entry(box, ray.o, dn), 0.0f);      // aabb.ray_intersect(...).x, clamped at 0
+        const StepSpace& ss = a.vol.ss;
+        const float startt = LIN ? advance_n_steps(tmin, 0.0f, rng.next_float()) : advance_n_steps(tmin, ss, rng.next_float());
+        const f3 idir = inv(dn);
+        uint32_t j = 0;
+        float t = startt;
+        f3 pos;
+        // unit-cube scenes (cone 0, one cascade): the exact linear specialisation of the occupancy test and
+        // of advance_to_next_voxel that the render marcher uses (sng_math.h, tests/test_host_fastpaths.py)
+        static_assert(BRICK == 0 || LIN, "the brick forms are unit-cube only");
+        const f3 hs = half_sign(dn);
+        float* const ts = tscr + ii;
+        OccCache oc;
+        while (live && aabb_contains(box, pos = ray.o + t * dn) && j < NERF_STEPS) {
+            const float dt = LIN ? calc_dt(t, 0.0f) : calc_dt(t, ss);
+            bool occ;
+            // the cached forms reload a word only when the position leaves the last one (~4.6 samples per cell): each trip
+            // is a dependent load otherwise, and a batch has too few rays to hide that latency
+            if constexpr (BRICK != 0) occ = occupied_brick_c(pos, bricks, oc);
+            else if constexpr (LIN) occ = occupied_linear_c(pos, a.vol.occ_linear, oc);
+            else occ = occupied_at(pos, a.vol.bitfield, mip_from_dt(dt, pos, a.vol.max_mip));
+            // one trip is one sample or one DDA step, as a select: with an if / else the compiler nests a loop of DDA steps
+            // inside the sample loop, and a wave then waits at every sample for its lanes' longest run of empty cells
+            // (measured 3.4x slower)
+            float t_skip;
+            if constexpr (LIN) t_skip = dda_step_linear(t, pos, idir, hs);
+            else t_skip = advance_to_next_voxel(t, ss, pos, dn, idir, mip_from_dt(dt, pos, a.vol.max_mip));
+            if (occ) ts[(size_t)j * n_rays] = t;
+            j += occ ? 1u : 0u;
+            t = occ ? t + dt : t_skip;
+        }
+        if (a.debug && live) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
+        const uint32_t numsteps = j;
+        const uint32_t base = wave_reserve(&b.ctrl->numsteps_counter, numsteps, lane);
+        const bool keep = numsteps > 0 && base + numsteps <= max_samples;
+        const uint32_t ray_idx = wave_reserve(&b.ctrl->ray_counter, keep ? 1u : 0u, lane);
+        if (!keep) continue;
+        b.ray_indices[ray_idx] = i;
+        b.rays[2 * ray_idx] = make_float4(ray.o.x, ray.o.y, ray.o.z, 0.0f);
+        b.rays[2 * ray_idx + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
+        b.numsteps[ray_idx] = make_uint2(numsteps, base);
+        const f3 wd = (dn + 1.0f) * 0.5f;   // warp_direction
+        const f3 diag = box.hi - box.lo;
+        float* co = b.coords + (size_t)base * 7;
+        for (uint32_t k = 0; k < numsteps; ++k) {
+            const float tk = ts[(size_t)k * n_rays];
+            const f3 p = ray.o + tk * dn;
+            const f3 wp = (p - box.lo) / diag;   // warp_position = aabb.relative_pos
+            float* c = co + (size_t)k * 7;
+            c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(LIN ? calc_dt(tk, 0.0f) : calc_dt(tk, ss)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
+        }
     }
 }
 
@@ -121,90 +126,94 @@ __global__ __launch_bounds__(64) void train_generate_kernel(TrainStepArgs a, Tra
 // occupied.  Every t is the one the serial march reaches, so the samples are the same; only the number of dependent
 // trips drops (one trip per ~G samples in occupied stretches, where the longest rays spend most of their march).
 template <bool LIN, int G>
-__global__ __launch_bounds__(64) void train_generate_spec_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, float* __restrict__ tscr) {
+__global__ __launch_bounds__(64) void train_generate_spec_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng0, float* __restrict__ tscr) {
     const int lane = threadIdx.x & 63;
     const uint32_t gl = (uint32_t)lane % G, g0 = (uint32_t)lane - gl;
     const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << g0;
-    const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
-    const bool in = i < a.n_rays;
-    const uint32_t ii = in ? i : 0u;
-    const uint32_t img = ((ii * im.n) / a.n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
-    rng.advance((uint64_t)ii * N_MAX_RANDOM_SAMPLES_PER_RAY);
-    const f2 uv = train_image_pos(rng, im);
-    const bool live = in && !(read_rgba(im, img, uv).x < 0.0f);   // masked pixel: no samples
-    (void)rng.next_float();                                    // motionblur_time
-    const TrainRay ray = train_ray(im, img, uv);
-    const f3 dn = normalize(ray.d);
-    const aabb box = a.vol.train_aabb;
-    const float tmin = fmaxf(aabb_entry(box, ray.o, dn), 0.0f);
-    const StepSpace& ss = a.vol.ss;
-    const float startt = LIN ? advance_n_steps(tmin, 0.0f, rng.next_float()) : advance_n_steps(tmin, ss, rng.next_float());
-    const f3 idir = inv(dn);
-    const f3 hs = half_sign(dn);
-    auto step_dt = [&](float t) { return LIN ? calc_dt(t, 0.0f) : calc_dt(t, ss); };
-    auto skip = [&](float t, f3 p) {
-        if constexpr (LIN) return dda_step_linear(t, p, idir, hs);
-        else return advance_to_next_voxel(t, ss, p, dn, idir, mip_from_dt(step_dt(t), p, a.vol.max_mip));
-    };
-    auto occupied = [&](float t, f3 p) {
-        if constexpr (LIN) return occupied_linear(p, a.vol.occ_linear);
-        else return occupied_at(p, a.vol.bitfield, mip_from_dt(step_dt(t), p, a.vol.max_mip));
-    };
-    float* const ts = tscr + ii;
-    uint32_t j = 0;
-    float t = startt;
-    bool dda = false, done = !live;   // uniform over the group
-    while (!done) {
-        float tk = t;
-        if (!dda) {
-            for (uint32_t u = 0; u < gl; ++u) tk = tk + step_dt(tk);
-        } else {
-            for (uint32_t u = 0; u < gl; ++u) tk = skip(tk, ray.o + tk * dn);
+    const uint32_t n_rays = a.sched->n_rays, max_samples = a.sched->max_samples;
+    for (uint32_t vb = blockIdx.x; vb * blockDim.x < n_rays * (uint32_t)G; vb += gridDim.x) {
+        Pcg32 rng = rng0;   // each grid-stride trip starts from the step's stream (the ray's offset is added below)
+        const uint32_t i = (vb * blockDim.x + threadIdx.x) / G;
+        const bool in = i < n_rays;
+        const uint32_t ii = in ? i : 0u;
+        const uint32_t img = ((ii * im.n) / n_rays) % im.n;   // image_idx (nerf_device.cuh:578-597)
+        rng.advance((uint64_t)ii * N_MAX_RANDOM_SAMPLES_PER_RAY);
+        const f2 uv = train_image_pos(rng, im);
+        const bool live = in && !(read_rgba(im, img, uv).x < 0.0f);   // masked pixel: no samples
+        (void)rng.next_float();                                    // motionblur_time
+        const TrainRay ray = train_ray(im, img, uv);
+        const f3 dn = normalize(ray.d);
+        const aabb box = a.vol.train_aabb;
+        const float tmin = fmaxf(aabb_entry(box, ray.o, dn), 0.0f);
+        const StepSpace& ss = a.vol.ss;
+        const float startt = LIN ? advance_n_steps(tmin, 0.0f, rng.next_float()) : advance_n_steps(tmin, ss, rng.next_float());
+        const f3 idir = inv(dn);
+        const f3 hs = half_sign(dn);
+        auto step_dt = [&](float t) { return LIN ? calc_dt(t, 0.0f) : calc_dt(t, ss); };
+        auto skip = [&](float t, f3 p) {
+            if constexpr (LIN) return dda_step_linear(t, p, idir, hs);
+            else return advance_to_next_voxel(t, ss, p, dn, idir, mip_from_dt(step_dt(t), p, a.vol.max_mip));
+        };
+        auto occupied = [&](float t, f3 p) {
+            if constexpr (LIN) return occupied_linear(p, a.vol.occ_linear);
+            else return occupied_at(p, a.vol.bitfield, mip_from_dt(step_dt(t), p, a.vol.max_mip));
+        };
+        float* const ts = tscr + ii;
+        uint32_t j = 0;
+        float t = startt;
+        bool dda = false, done = !live;   // uniform over the group
+        while (!done) {
+            float tk = t;
+            if (!dda) {
+                for (uint32_t u = 0; u < gl; ++u) tk = tk + step_dt(tk);
+            } else {
+                for (uint32_t u = 0; u < gl; ++u) tk = skip(tk, ray.o + tk * dn);
+            }
+            const f3 pk = ray.o + tk * dn;
+            const bool ink = aabb_contains(box, pk) && (dda ? j : j + gl) < NERF_STEPS;
+            const bool occk = ink && occupied(tk, pk);
+            const bool stopk = dda ? (!ink || occk) : !occk;
+            const uint64_t sb = __ballot(stopk) & gmask;
+            const uint32_t m = sb ? (uint32_t)(__ffsll((long long)sb) - 1) - g0 : (uint32_t)G;
+            if (!dda) {
+                if (gl < m) ts[(size_t)(j + gl) * n_rays] = tk;
+                j += m;
+            }
+            if (m == (uint32_t)G) {   // every lane continued the kind: the next trip starts after lane G - 1
+                const float tl = __shfl(tk, (int)(g0 + G - 1), 64);
+                t = dda ? skip(tl, ray.o + tl * dn) : tl + step_dt(tl);
+                continue;
+            }
+            const float tm = __shfl(tk, (int)(g0 + m), 64);
+            const bool inm = __shfl((int)ink, (int)(g0 + m), 64) != 0;
+            if (!inm) { done = true; continue; }
+            if (!dda) { t = skip(tm, ray.o + tm * dn); dda = true; }   // an empty cell inside: its DDA step
+            else { t = tm; dda = false; }                              // an occupied cell: samples from here
         }
-        const f3 pk = ray.o + tk * dn;
-        const bool ink = aabb_contains(box, pk) && (dda ? j : j + gl) < NERF_STEPS;
-        const bool occk = ink && occupied(tk, pk);
-        const bool stopk = dda ? (!ink || occk) : !occk;
-        const uint64_t sb = __ballot(stopk) & gmask;
-        const uint32_t m = sb ? (uint32_t)(__ffsll((long long)sb) - 1) - g0 : (uint32_t)G;
-        if (!dda) {
-            if (gl < m) ts[(size_t)(j + gl) * a.n_rays] = tk;
-            j += m;
+        if (a.debug && live && gl == 0) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
+        const uint32_t numsteps = j;
+        uint32_t base = wave_reserve(&b.ctrl->numsteps_counter, gl == 0 ? numsteps : 0u, lane);
+        base = __shfl(base, (int)g0, 64);
+        const bool keep = numsteps > 0 && base + numsteps <= max_samples;
+        uint32_t ray_idx = wave_reserve(&b.ctrl->ray_counter, gl == 0 && keep ? 1u : 0u, lane);
+        ray_idx = __shfl(ray_idx, (int)g0, 64);
+        if (!keep) continue;
+        if (gl == 0) {
+            b.ray_indices[ray_idx] = i;
+            b.rays[2 * ray_idx] = make_float4(ray.o.x, ray.o.y, ray.o.z, 0.0f);
+            b.rays[2 * ray_idx + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
+            b.numsteps[ray_idx] = make_uint2(numsteps, base);
         }
-        if (m == (uint32_t)G) {   // every lane continued the kind: the next trip starts after lane G - 1
-            const float tl = __shfl(tk, (int)(g0 + G - 1), 64);
-            t = dda ? skip(tl, ray.o + tl * dn) : tl + step_dt(tl);
-            continue;
+        const f3 wd = (dn + 1.0f) * 0.5f;   // warp_direction
+        const f3 diag = box.hi - box.lo;
+        float* co = b.coords + (size_t)base * 7;
+        for (uint32_t k = gl; k < numsteps; k += G) {
+            const float tk = ts[(size_t)k * n_rays];
+            const f3 p = ray.o + tk * dn;
+            const f3 wp = (p - box.lo) / diag;   // warp_position = aabb.relative_pos
+            float* c = co + (size_t)k * 7;
+            c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(step_dt(tk)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
         }
-        const float tm = __shfl(tk, (int)(g0 + m), 64);
-        const bool inm = __shfl((int)ink, (int)(g0 + m), 64) != 0;
-        if (!inm) { done = true; continue; }
-        if (!dda) { t = skip(tm, ray.o + tm * dn); dda = true; }   // an empty cell inside: its DDA step
-        else { t = tm; dda = false; }                              // an occupied cell: samples from here
-    }
-    if (a.debug && live && gl == 0) { b.loss[i] = (float)j; b.coords_c[2 * i] = tmin; b.coords_c[2 * i + 1] = startt; }
-    const uint32_t numsteps = j;
-    uint32_t base = wave_reserve(&b.ctrl->numsteps_counter, gl == 0 ? numsteps : 0u, lane);
-    base = __shfl(base, (int)g0, 64);
-    const bool keep = numsteps > 0 && base + numsteps <= a.max_samples;
-    uint32_t ray_idx = wave_reserve(&b.ctrl->ray_counter, gl == 0 && keep ? 1u : 0u, lane);
-    ray_idx = __shfl(ray_idx, (int)g0, 64);
-    if (!keep) return;
-    if (gl == 0) {
-        b.ray_indices[ray_idx] = i;
-        b.rays[2 * ray_idx] = make_float4(ray.o.x, ray.o.y, ray.o.z, 0.0f);
-        b.rays[2 * ray_idx + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.0f);
-        b.numsteps[ray_idx] = make_uint2(numsteps, base);
-    }
-    const f3 wd = (dn + 1.0f) * 0.5f;   // warp_direction
-    const f3 diag = box.hi - box.lo;
-    float* co = b.coords + (size_t)base * 7;
-    for (uint32_t k = gl; k < numsteps; k += G) {
-        const float tk = ts[(size_t)k * a.n_rays];
-        const f3 p = ray.o + tk * dn;
-        const f3 wp = (p - box.lo) / diag;   // warp_position = aabb.relative_pos
-        float* c = co + (size_t)k * 7;
-        c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(step_dt(tk)); c[4] = wd.x; c[5] = wd.y; c[6] = wd.z;
     }
 }
 
@@ -219,104 +228,108 @@ __global__ __launch_bounds__(64) void train_generate_spec_kernel(TrainStepArgs a
 // stop before each sample), and the lane that owns a sample writes its partial.  (One lane per ray left the chain's
 // per-sample math on the critical path of the longest ray: 0.20 ms per batch.)
 constexpr uint32_t LOSS_G = 16;
-__global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng, const float* __restrict__ mean_density) {
-    const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / LOSS_G;
-    const int lane = threadIdx.x & 63;
-    const uint32_t gl = (uint32_t)lane % LOSS_G, g0 = (uint32_t)lane - gl;   // lane within the ray's group, the group's first lane
-    const bool in = gi < b.ctrl->ray_counter;   // the groups past the last ray stay for the wave's reservation (cn = 0)
-    const uint32_t i = in ? gi : 0u;
-    const uint2 ns = in ? b.numsteps[i] : make_uint2(0u, 0u);
-    const uint32_t numsteps = ns.x, base = ns.y;
-    const float* __restrict__ cin = b.coords + (size_t)base * 7;
-    const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
-    // the ray's target colour first (independent of the chain below, so its image read overlaps it): the same RNG draws
-    // as train_generate_kernel for this ray -- uv, (max_level off), motionblur, then bg
-    const uint32_t ray_idx = b.ray_indices[i];
-    rng.advance((uint64_t)ray_idx * N_MAX_RANDOM_SAMPLES_PER_RAY);
-    const uint32_t img = ((ray_idx * im.n) / a.n_rays) % im.n;
-    const f2 uv = train_image_pos(rng, im);
-    rng.advance(1);   // motionblur_time
-    f3 bg = a.background;
-    if (a.random_bg) { const float x = rng.next_float(), y = rng.next_float(), z = rng.next_float(); bg = mk(x, y, z); }
-    bg = mk(srgb_to_linear(bg.x), srgb_to_linear(bg.y), srgb_to_linear(bg.z));
-    const float4 tex = read_rgba(im, img, uv);
-    bg = mk(linear_to_srgb(bg.x), linear_to_srgb(bg.y), linear_to_srgb(bg.z));
-    f3 target;
-    if (tex.w > 0.0f) {
-        const f3 lin = mk(tex.x / tex.w, tex.y / tex.w, tex.z / tex.w);   // exposure_scale = exp(0) = 1
-        target = mk(linear_to_srgb(lin.x), linear_to_srgb(lin.y), linear_to_srgb(lin.z)) * tex.w + (1.0f - tex.w) * bg;
-    } else {
-        target = bg;
-    }
-    float T = 1.0f;
-    const float EPSILON = 1e-4f;
-    f3 rgb_ray = splat(0.0f);
-    uint32_t cn = 0;
-    bool stop = false;
-    // the next chunk's output and dt are loaded while this chunk's transmittance chain runs (clamped index: the last
-    // sample again past the ray's end, unused)
-    uint2 ow_n = make_uint2(0u, 0u);
-    float wdt_n = 0.0f;
-    if (numsteps) {
-        const uint32_t j0 = min(gl, numsteps - 1);
-        ow_n = *reinterpret_cast<const uint2*>(nout + (size_t)j0 * 4);
-        wdt_n = cin[(size_t)j0 * 7 + 3];
-    }
-    for (uint32_t c0 = 0; c0 < numsteps && !stop; c0 += LOSS_G) {
-        const uint2 ow = ow_n;
-        const float wdt = wdt_n;
+__global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainImages im, TrainBatch b, Pcg32 rng0, const float* __restrict__ mean_density) {
+    const uint32_t n_rays = a.sched->n_rays, n_in = b.ctrl->ray_counter;
+    for (uint32_t vb = blockIdx.x; vb * blockDim.x < n_in * LOSS_G; vb += gridDim.x) {
+        Pcg32 rng = rng0;   // each grid-stride trip starts from the step's stream (the ray's offset is added below)
+        const uint32_t gi = (vb * blockDim.x + threadIdx.x) / LOSS_G;
+        const int lane = threadIdx.x & 63;
+        const uint32_t gl = (uint32_t)lane % LOSS_G, g0 = (uint32_t)lane - gl;   // lane within the ray's group, the group's first lane
+        const bool in = gi < n_in;   // the groups past the last ray stay for the wave's reservation (cn = 0)
+        const uint32_t i = in ? gi : 0u;
+        const uint2 ns = in ? b.numsteps[i] : make_uint2(0u, 0u);
+        const uint32_t numsteps = ns.x, base = ns.y;
+        const float* __restrict__ cin = b.coords + (size_t)base * 7;
+        const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
+        // the ray's target colour first (independent of the chain below, so its image read overlaps it): the same RNG draws
+        // as train_generate_kernel for this ray -- uv, (max_level off), motionblur, then bg
+        const uint32_t ray_idx = b.ray_indices[i];
+        rng.advance((uint64_t)ray_idx * N_MAX_RANDOM_SAMPLES_PER_RAY);
+        const uint32_t img = ((ray_idx * im.n) / n_rays) % im.n;
+        const f2 uv = train_image_pos(rng, im);
+        rng.advance(1);   // motionblur_time
+        f3 bg = a.background;
+        if (a.random_bg) { const float x = rng.next_float(), y = rng.next_float(), z = rng.next_float(); bg = mk(x, y, z); }
+        bg = mk(srgb_to_linear(bg.x), srgb_to_linear(bg.y), srgb_to_linear(bg.z));
+        const float4 tex = read_rgba(im, img, uv);
+        bg = mk(linear_to_srgb(bg.x), linear_to_srgb(bg.y), linear_to_srgb(bg.z));
+        f3 target;
+        if (tex.w > 0.0f) {
+            const f3 lin = mk(tex.x / tex.w, tex.y / tex.w, tex.z / tex.w);   // exposure_scale = exp(0) = 1
+            target = mk(linear_to_srgb(lin.x), linear_to_srgb(lin.y), linear_to_srgb(lin.z)) * tex.w + (1.0f - tex.w) * bg;
+        } else {
+            target = bg;
+        }
+        float T = 1.0f;
+        const float EPSILON = 1e-4f;
+        f3 rgb_ray = splat(0.0f);
+        uint32_t cn = 0;
+        bool stop = false;
+        // the next chunk's output and dt are loaded while this chunk's transmittance chain runs (clamped index: the last
+        // sample again past the ray's end, unused)
+        uint2 ow_n = make_uint2(0u, 0u);
+        float wdt_n = 0.0f;
+        if (numsteps) {
+            const uint32_t j0 = min(gl, numsteps - 1);
+            ow_n = *reinterpret_cast<const uint2*>(nout + (size_t)j0 * 4);
+            wdt_n = cin[(size_t)j0 * 7 + 3];
+        }
+        for (uint32_t c0 = 0; c0 < numsteps && !stop; c0 += LOSS_G) {
+            const uint2 ow = ow_n;
+            const float wdt = wdt_n;
+            {
+                const uint32_t jn = min(c0 + LOSS_G + gl, numsteps - 1);
+                ow_n = *reinterpret_cast<const uint2*>(nout + (size_t)jn * 4);
+                wdt_n = cin[(size_t)jn * 7 + 3];
+            }
+            const float o0 = h2f((uint16_t)(ow.x & 0xffffu)), o1 = h2f((uint16_t)(ow.x >> 16));
+            const float o2 = h2f((uint16_t)(ow.y & 0xffffu)), o3 = h2f((uint16_t)(ow.y >> 16));
+            const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
+            const float dt = unwarp_dt(wdt);
+            const float density = sng_expf(o3);
+            const float alpha = 1.0f - sng_expf(-density * dt);
+            for (uint32_t u = 0; u < LOSS_G; ++u) {
+                if (c0 + u >= numsteps) break;
+                if (T < EPSILON) { stop = true; break; }
+                const int src = (int)(g0 + u);
+                const float au = __shfl(alpha, src, 64);
+                const f3 ru = mk(__shfl(rgb.x, src, 64), __shfl(rgb.y, src, 64), __shfl(rgb.z, src, 64));
+                const float weight = au * T;
+                rgb_ray = rgb_ray + weight * ru;
+                if (gl == u) b.partial[base + cn] = make_float4(T, rgb_ray.x, rgb_ray.y, rgb_ray.z);   // train_dloss_kernel replays from here
+                T *= (1.0f - au);
+                ++cn;
+            }
+        }
+        if (cn == numsteps) rgb_ray = rgb_ray + T * bg;
+        if (!in || gl != 0) continue;
+        // the compaction slot comes from train_compact_kernel (a prefix of the composited counts in the rays' image order)
+        b.cnt_i[ray_idx] = cn;
+        // Huber loss (alpha = 0.1) / 5, loss_and_gradient (nerf_device.cuh:100-117, 601-616)
+        f3 grad;
+        float loss_sum = 0.0f;
         {
-            const uint32_t jn = min(c0 + LOSS_G + gl, numsteps - 1);
-            ow_n = *reinterpret_cast<const uint2*>(nout + (size_t)jn * 4);
-            wdt_n = cin[(size_t)jn * 7 + 3];
+            const float alpha_h = 0.1f;
+            const float dv[3] = {rgb_ray.x - target.x, rgb_ray.y - target.y, rgb_ray.z - target.z};
+            float gv[3];
+            for (int k = 0; k < 3; ++k) {
+                const float ad = fabsf(dv[k]);
+                const float sq = 0.5f / alpha_h * dv[k] * dv[k];
+                const float l = ad > alpha_h ? (ad - 0.5f * alpha_h) : sq;
+                gv[k] = (ad > alpha_h ? (dv[k] > 0 ? 1.0f : -1.0f) : (dv[k] / alpha_h)) / 5.0f;
+                loss_sum += l / 5.0f;
+            }
+            grad = mk(gv[0], gv[1], gv[2]);
         }
-        const float o0 = h2f((uint16_t)(ow.x & 0xffffu)), o1 = h2f((uint16_t)(ow.x >> 16));
-        const float o2 = h2f((uint16_t)(ow.y & 0xffffu)), o3 = h2f((uint16_t)(ow.y >> 16));
-        const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
-        const float dt = unwarp_dt(wdt);
-        const float density = sng_expf(o3);
-        const float alpha = 1.0f - sng_expf(-density * dt);
-        for (uint32_t u = 0; u < LOSS_G; ++u) {
-            if (c0 + u >= numsteps) break;
-            if (T < EPSILON) { stop = true; break; }
-            const int src = (int)(g0 + u);
-            const float au = __shfl(alpha, src, 64);
-            const f3 ru = mk(__shfl(rgb.x, src, 64), __shfl(rgb.y, src, 64), __shfl(rgb.z, src, 64));
-            const float weight = au * T;
-            rgb_ray = rgb_ray + weight * ru;
-            if (gl == u) b.partial[base + cn] = make_float4(T, rgb_ray.x, rgb_ray.y, rgb_ray.z);   // train_dloss_kernel replays from here
-            T *= (1.0f - au);
-            ++cn;
-        }
+        b.loss[i] = (loss_sum / 3.0f) / (float)n_rays;
+        const float loss_scale = a.loss_scale / (float)n_rays;
+        const float l1_reg_density = *mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
+        // the per-sample gradients need only this ray's constants and the forward partials: they are
+        // written by train_dloss_kernel with one wave per ray instead of this lane's serial loop
+        b.rayrec[3 * i] = make_float4(0.0f, 0.0f, __uint_as_float(base), 0.0f);   // slot and count: train_finalize_kernel
+        b.rayrec[3 * i + 1] = make_float4(grad.x, grad.y, grad.z, loss_scale);
+        b.rayrec[3 * i + 2] = make_float4(rgb_ray.x, rgb_ray.y, rgb_ray.z, l1_reg_density);
     }
-    if (cn == numsteps) rgb_ray = rgb_ray + T * bg;
-    if (!in || gl != 0) return;
-    // the compaction slot comes from train_compact_kernel (a prefix of the composited counts in the rays' image order)
-    b.cnt_i[ray_idx] = cn;
-    // Huber loss (alpha = 0.1) / 5, loss_and_gradient (nerf_device.cuh:100-117, 601-616)
-    f3 grad;
-    float loss_sum = 0.0f;
-    {
-        const float alpha_h = 0.1f;
-        const float dv[3] = {rgb_ray.x - target.x, rgb_ray.y - target.y, rgb_ray.z - target.z};
-        float gv[3];
-        for (int k = 0; k < 3; ++k) {
-            const float ad = fabsf(dv[k]);
-            const float sq = 0.5f / alpha_h * dv[k] * dv[k];
-            const float l = ad > alpha_h ? (ad - 0.5f * alpha_h) : sq;
-            gv[k] = (ad > alpha_h ? (dv[k] > 0 ? 1.0f : -1.0f) : (dv[k] / alpha_h)) / 5.0f;
-            loss_sum += l / 5.0f;
-        }
-        grad = mk(gv[0], gv[1], gv[2]);
-    }
-    b.loss[i] = (loss_sum / 3.0f) / (float)a.n_rays;
-    const float loss_scale = a.loss_scale / (float)a.n_rays;
-    const float l1_reg_density = *mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
-    // the per-sample gradients need only this ray's constants and the forward partials: they are
-    // written by train_dloss_kernel with one wave per ray instead of this lane's serial loop
-    b.rayrec[3 * i] = make_float4(0.0f, 0.0f, __uint_as_float(base), 0.0f);   // slot and count: train_finalize_kernel
-    b.rayrec[3 * i + 1] = make_float4(grad.x, grad.y, grad.z, loss_scale);
-    b.rayrec[3 * i + 2] = make_float4(rgb_ray.x, rgb_ray.y, rgb_ray.z, l1_reg_density);
 }
 
 // The compaction of the composited samples into the batch (testbed_nerf.cu:1150: an atomicAdd per ray, so the reference
@@ -325,8 +338,9 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
 // ray's march or composite ran.  (A completion order favours the short rays whenever the batch overflows its target: with
 // 4 rays per wave in the loss kernel that bias was strong enough to collapse the density field within 200 steps.)  One
 // workgroup: ~10^4 rays.
-__global__ __launch_bounds__(1024) void train_compact_kernel(uint32_t n, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ cbase, TrainCtrl* ctrl) {
+__global__ __launch_bounds__(1024) void train_compact_kernel(const TrainSched* __restrict__ sched, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ cbase, TrainCtrl* ctrl) {
     __shared__ uint32_t part[1024];
+    const uint32_t n = sched->n_rays;
     const uint32_t per = (n + 1023u) / 1024u, t0 = threadIdx.x * per, t1 = min(n, t0 + per);
     uint32_t sum = 0;
     for (uint32_t k = t0; k < t1; ++k) sum += cnt[k];
@@ -343,66 +357,72 @@ __global__ __launch_bounds__(1024) void train_compact_kernel(uint32_t n, const u
     if (threadIdx.x == 1023) ctrl->numsteps_compacted = part[1023];
 }
 __global__ __launch_bounds__(256) void train_finalize_kernel(TrainStepArgs a, TrainBatch b) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.ctrl->ray_counter) return;
-    const uint32_t ri = b.ray_indices[i], cn = b.cnt_i[ri], cbase = b.cbase_i[ri];
-    const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
-    if (ccount == 0) {   // past the batch target: no loss and no gradient for this ray (testbed_nerf.cu: compacted_numsteps == 0)
-        b.rayrec[3 * i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        b.loss[i] = 0.0f;
-        return;
+    const uint32_t n_in = b.ctrl->ray_counter;
+    for (uint32_t vb = blockIdx.x; vb * blockDim.x < n_in; vb += gridDim.x) {
+        const uint32_t i = vb * blockDim.x + threadIdx.x;
+        if (i >= n_in) continue;
+        const uint32_t ri = b.ray_indices[i], cn = b.cnt_i[ri], cbase = b.cbase_i[ri];
+        const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
+        if (ccount == 0) {   // past the batch target: no loss and no gradient for this ray (testbed_nerf.cu: compacted_numsteps == 0)
+            b.rayrec[3 * i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            b.loss[i] = 0.0f;
+            continue;
+        }
+        b.rayrec[3 * i].x = __uint_as_float(cbase);
+        b.rayrec[3 * i].y = __uint_as_float(ccount);
     }
-    b.rayrec[3 * i].x = __uint_as_float(cbase);
-    b.rayrec[3 * i].y = __uint_as_float(ccount);
 }
 
 // compute_loss_kernel_train_nerf's gradient loop (testbed_nerf.cu:1209-1275) for the ray's first
 // ccount samples, one wave per ray, lanes over the samples: T and the running rgb come from the
 // forward pass's partials (the same float sequence), so every value is the serial loop's.
 __global__ __launch_bounds__(256) void train_dloss_kernel(TrainStepArgs a, TrainBatch b) {
-    const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t lane = threadIdx.x & 63;
-    if (i >= b.ctrl->ray_counter) return;
-    const float4 r0 = b.rayrec[3 * i], r1 = b.rayrec[3 * i + 1], r2 = b.rayrec[3 * i + 2];
-    if (r0.x == 0.0f && r0.y == 0.0f && r0.z == 0.0f && r0.w == 0.0f) return;   // ray returned before its record (ccount 0)
-    const uint32_t cbase = __float_as_uint(r0.x), ccount = __float_as_uint(r0.y), base = __float_as_uint(r0.z);
-    const f3 grad = mk(r1.x, r1.y, r1.z), rgb_ray = mk(r2.x, r2.y, r2.z);
-    const float loss_scale = r1.w, l1_reg_density = r2.w;
-    const aabb box = a.vol.train_aabb;
-    const f3 diag = box.hi - box.lo;
-    const float4 ro4 = b.rays[2 * i];
-    const f3 ray_o = mk(ro4.x, ro4.y, ro4.z);
-    const float* __restrict__ cin = b.coords + (size_t)base * 7;
-    const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
-    float* __restrict__ cout = b.coords_c + (size_t)cbase * 7;
-    uint16_t* __restrict__ dout = b.dloss + (size_t)cbase * 4;
-    for (uint32_t j = lane; j < ccount; j += 64) {
-        const float* c = cin + (size_t)j * 7;
-        for (int k = 0; k < 7; ++k) cout[(size_t)j * 7 + k] = c[k];
-        const f3 pos = box.lo + mk(c[0], c[1], c[2]) * diag;   // unwarp_position
-        const float depth = length(pos - ray_o);
-        const float dt = unwarp_dt(c[3]);
-        const uint16_t* o = nout + (size_t)j * 4;
-        const float o0 = h2f(o[0]), o1 = h2f(o[1]), o2 = h2f(o[2]), o3 = h2f(o[3]);
-        const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
-        const float density = sng_expf(o3);
-        const float alpha = 1.0f - sng_expf(-density * dt);
-        const float4 pt = b.partial[base + j];
-        const float weight = alpha * pt.x;
-        const f3 rgb_ray2 = mk(pt.y, pt.z, pt.w);
-        const float T = pt.x * (1.0f - alpha);
-        const f3 suffix = rgb_ray - rgb_ray2;
-        const f3 dl_drgb = weight * grad;
-        const float d0 = loss_scale * (dl_drgb.x * (rgb.x * (1.0f - rgb.x)));
-        const float d1 = loss_scale * (dl_drgb.y * (rgb.y * (1.0f - rgb.y)));
-        const float d2 = loss_scale * (dl_drgb.z * (rgb.z * (1.0f - rgb.z)));
-        const float dens_deriv = sng_expf(fminf(fmaxf(o3, -15.0f), 15.0f));
-        const float dl_dmlp = dens_deriv * (dt * dot(grad, T * rgb - suffix));
-        const float d3 = loss_scale * dl_dmlp + (o3 < 0.0f ? -l1_reg_density : 0.0f) + (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f);
-        dout[(size_t)j * 4 + 0] = f2h(d0);
-        dout[(size_t)j * 4 + 1] = f2h(d1);
-        dout[(size_t)j * 4 + 2] = f2h(d2);
-        dout[(size_t)j * 4 + 3] = f2h(d3);
+    const uint32_t n_in = b.ctrl->ray_counter;
+    for (uint32_t vb = blockIdx.x; vb * (blockDim.x >> 6) < n_in; vb += gridDim.x) {
+        const uint32_t i = (vb * blockDim.x + threadIdx.x) >> 6;
+        const uint32_t lane = threadIdx.x & 63;
+        if (i >= n_in) continue;
+        const float4 r0 = b.rayrec[3 * i], r1 = b.rayrec[3 * i + 1], r2 = b.rayrec[3 * i + 2];
+        if (r0.x == 0.0f && r0.y == 0.0f && r0.z == 0.0f && r0.w == 0.0f) continue;   // ray returned before its record (ccount 0)
+        const uint32_t cbase = __float_as_uint(r0.x), ccount = __float_as_uint(r0.y), base = __float_as_uint(r0.z);
+        const f3 grad = mk(r1.x, r1.y, r1.z), rgb_ray = mk(r2.x, r2.y, r2.z);
+        const float loss_scale = r1.w, l1_reg_density = r2.w;
+        const aabb box = a.vol.train_aabb;
+        const f3 diag = box.hi - box.lo;
+        const float4 ro4 = b.rays[2 * i];
+        const f3 ray_o = mk(ro4.x, ro4.y, ro4.z);
+        const float* __restrict__ cin = b.coords + (size_t)base * 7;
+        const uint16_t* __restrict__ nout = b.mlp_out + (size_t)base * 4;
+        float* __restrict__ cout = b.coords_c + (size_t)cbase * 7;
+        uint16_t* __restrict__ dout = b.dloss + (size_t)cbase * 4;
+        for (uint32_t j = lane; j < ccount; j += 64) {
+            const float* c = cin + (size_t)j * 7;
+            for (int k = 0; k < 7; ++k) cout[(size_t)j * 7 + k] = c[k];
+            const f3 pos = box.lo + mk(c[0], c[1], c[2]) * diag;   // unwarp_position
+            const float depth = length(pos - ray_o);
+            const float dt = unwarp_dt(c[3]);
+            const uint16_t* o = nout + (size_t)j * 4;
+            const float o0 = h2f(o[0]), o1 = h2f(o[1]), o2 = h2f(o[2]), o3 = h2f(o[3]);
+            const f3 rgb = mk(logistic(o0), logistic(o1), logistic(o2));
+            const float density = sng_expf(o3);
+            const float alpha = 1.0f - sng_expf(-density * dt);
+            const float4 pt = b.partial[base + j];
+            const float weight = alpha * pt.x;
+            const f3 rgb_ray2 = mk(pt.y, pt.z, pt.w);
+            const float T = pt.x * (1.0f - alpha);
+            const f3 suffix = rgb_ray - rgb_ray2;
+            const f3 dl_drgb = weight * grad;
+            const float d0 = loss_scale * (dl_drgb.x * (rgb.x * (1.0f - rgb.x)));
+            const float d1 = loss_scale * (dl_drgb.y * (rgb.y * (1.0f - rgb.y)));
+            const float d2 = loss_scale * (dl_drgb.z * (rgb.z * (1.0f - rgb.z)));
+            const float dens_deriv = sng_expf(fminf(fmaxf(o3, -15.0f), 15.0f));
+            const float dl_dmlp = dens_deriv * (dt * dot(grad, T * rgb - suffix));
+            const float d3 = loss_scale * dl_dmlp + (o3 < 0.0f ? -l1_reg_density : 0.0f) + (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f);
+            dout[(size_t)j * 4 + 0] = f2h(d0);
+            dout[(size_t)j * 4 + 1] = f2h(d1);
+            dout[(size_t)j * 4 + 2] = f2h(d2);
+            dout[(size_t)j * 4 + 3] = f2h(d3);
+        }
     }
 }
 
@@ -952,10 +972,16 @@ __global__ void train_mark_untrained_kernel(uint32_t n_elements, float* __restri
 
 // generate_grid_samples_nerf_nonuniform (186-215): NerfPosition written as a 7-float coordinate
 // (direction unused by the density output)
+// morton (n_elements a multiple of GRID_CELLS, as in the uniform updates of the first 256 steps): slot t holds the sample
+// i whose first candidate cell is the t-th cell in Morton order (its hashed index is an affine bijection of i mod
+// GRID_CELLS: i = (f - 96925573) * 56924617^-1 - step n mod 2^21), so the network reads neighbouring cells' hash
+// entries together instead of one random cell per lane; the samples, and the splat's max per cell, are the same
 __global__ void train_grid_samples_kernel(uint32_t n_elements, Pcg32 rng, uint32_t step, aabb box, const float* __restrict__ grid_in, float* __restrict__ coords,
-                                          uint32_t* __restrict__ indices, uint32_t n_cascades, float thresh) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_elements) return;
+                                          uint32_t* __restrict__ indices, uint32_t n_cascades, float thresh, int morton) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_elements) return;
+    static_assert(GRID_CELLS == (1u << 21), "the affine inverse below is mod 2^21");
+    const uint32_t i = morton ? (t & ~(GRID_CELLS - 1u)) | ((((t & (GRID_CELLS - 1u)) - 96925573u) * 53369u - step * n_elements) & (GRID_CELLS - 1u)) : t;
     rng.advance((uint64_t)i * 4);
     const uint32_t level = (uint32_t)(rng.next_float() * (float)n_cascades) % n_cascades;
     uint32_t idx = 0;
@@ -969,9 +995,9 @@ __global__ void train_grid_samples_kernel(uint32_t n_elements, Pcg32 rng, uint32
     const float rx = rng.next_float(), ry = rng.next_float(), rz = rng.next_float();
     const f3 pos = ((mk((float)x, (float)y, (float)z) + mk(rx, ry, rz)) / (float)GRID_SIZE - 0.5f) * scalbnf(1.0f, (int)level) + 0.5f;
     const f3 wp = (pos - box.lo) / (box.hi - box.lo);
-    float* c = coords + (size_t)i * 7;
+    float* c = coords + (size_t)t * 7;
     c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(MIN_STEP); c[4] = 0.5f; c[5] = 0.5f; c[6] = 0.5f;
-    indices[i] = idx;
+    indices[t] = idx;
 }
 
 // splat_grid_samples_nerf_max_nearest_neighbor (217-233): optical thickness, atomic max on the bits
@@ -991,23 +1017,60 @@ __global__ void train_grid_ema_kernel(uint32_t n, float decay, float* __restrict
     grid[i] = prev < 0.0f ? prev : fmaxf(prev * decay, tmp[i]);
 }
 
-__global__ void train_clamp_count_kernel(const uint32_t* __restrict__ in, uint32_t cap, uint32_t* __restrict__ out) {
-    if (threadIdx.x == 0) *out = min(*in, cap);
+__global__ void train_clamp_count_kernel(const uint32_t* __restrict__ in, const TrainSched* __restrict__ sched, uint32_t* __restrict__ out) {
+    if (threadIdx.x == 0) *out = min(*in, sched->max_samples);
+}
+
+// NerfCounters::update_after_training (testbed_nerf.cu:3272-3296) on the device: the next step's rays_per_batch from this
+// step's compacted count, with the host expressions' float operations (correctly rounded multiply and divide), and the
+// next max_inference from the count before compaction (train_args' rounding)
+__global__ void train_sched_update_kernel(TrainSched* __restrict__ sched, const TrainCtrl* __restrict__ ctrl, uint32_t target) {
+    if (threadIdx.x != 0) return;
+    TrainSched n = *sched;
+    const uint32_t before = ctrl->numsteps_counter, after = ctrl->numsteps_compacted;
+    if (before == 0 || after == 0) {
+        n.measured = n.measured_before = 0;
+    } else {
+        n.measured_before = before;
+        n.measured = after;
+        const uint32_t r = (uint32_t)__fdiv_rn(__fmul_rn((float)n.n_rays, (float)target), (float)after);
+        n.n_rays = min((r + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY, 1u << 18);
+    }
+    const uint32_t cap = target * 16;
+    n.max_samples = n.measured_before == 0 ? cap : (min(n.measured_before, cap) + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY;
+    *sched = n;
+}
+
+// the per-ray buffers the step fills by ray index, cleared up to the device's ray count
+__global__ __launch_bounds__(256) void train_clear_kernel(const TrainSched* __restrict__ sched, float* __restrict__ loss, float4* __restrict__ rayrec,
+                                                          uint32_t* __restrict__ cnt, TrainCtrl* __restrict__ ctrl) {
+    const uint32_t n = sched->n_rays;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ctrl = TrainCtrl{0u, 0u, 0u, 0u};
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * n; i += gridDim.x * blockDim.x) {
+        rayrec[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (i < n) { loss[i] = 0.0f; cnt[i] = 0u; }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
-void launch_train_clamp_count(const uint32_t* in, uint32_t cap, uint32_t* out, hipStream_t s) {
-    hipLaunchKernelGGL(train_clamp_count_kernel, dim3(1), dim3(64), 0, s, in, cap, out);
+void launch_train_clamp_count(const uint32_t* in, const TrainSched* sched, uint32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(train_clamp_count_kernel, dim3(1), dim3(64), 0, s, in, sched, out);
+}
+void launch_train_sched_update(TrainSched* sched, const TrainCtrl* ctrl, uint32_t target, hipStream_t s) {
+    hipLaunchKernelGGL(train_sched_update_kernel, dim3(1), dim3(64), 0, s, sched, ctrl, target);
+}
+void launch_train_clear(const TrainStepArgs& a, const TrainBatch& b, hipStream_t s) {
+    hipLaunchKernelGGL(train_clear_kernel, dim3(std::max(1u, (3 * a.n_rays_grid + 255) / 256)), dim3(256), 0, s, a.sched, b.loss, b.rayrec, b.cnt_i, b.ctrl);
 }
 void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, float* tscr, hipStream_t s) {
-    const dim3 grid((a.n_rays + 63) / 64);
+    const dim3 grid(std::max(1u, (a.n_rays_grid + 63) / 64));
     const bool lin = a.vol.linear && a.vol.max_mip == 0 && a.vol.cone <= 1e-5f;
     if (a.gen_bricks && lin && a.vol.occ_brick_words && a.vol.occ_brick_words * 4u <= 64u * 1024u)
         hipLaunchKernelGGL((train_generate_kernel<1, true>), grid, dim3(64), a.vol.occ_brick_words * 4, s, a, im, b, rng, tscr);
     else if (a.gen_bricks && lin && a.vol.occ_brick_g)
         hipLaunchKernelGGL((train_generate_kernel<2, true>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
     else if (a.gen_lanes == 8 || a.gen_lanes == 16) {
-        const dim3 g2((a.n_rays * (uint32_t)a.gen_lanes + 63) / 64);
+        const dim3 g2(std::max(1u, (a.n_rays_grid * (uint32_t)a.gen_lanes + 63) / 64));
         if (lin && a.vol.occ_linear) {
             if (a.gen_lanes == 8) hipLaunchKernelGGL((train_generate_spec_kernel<true, 8>), g2, dim3(64), 0, s, a, im, b, rng, tscr);
             else hipLaunchKernelGGL((train_generate_spec_kernel<true, 16>), g2, dim3(64), 0, s, a, im, b, rng, tscr);
@@ -1021,12 +1084,12 @@ void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const 
         hipLaunchKernelGGL((train_generate_kernel<0, false>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
 }
 void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
-    (void)hipMemsetAsync(b.rayrec, 0, (size_t)a.n_rays * 48, s);
-    (void)hipMemsetAsync(b.cnt_i, 0, (size_t)a.n_rays * 4, s);
-    hipLaunchKernelGGL(train_loss_kernel, dim3((a.n_rays * LOSS_G + 255) / 256), dim3(256), 0, s, a, im, b, rng, mean_density);
-    hipLaunchKernelGGL(train_compact_kernel, dim3(1), dim3(1024), 0, s, a.n_rays, b.cnt_i, b.cbase_i, b.ctrl);
-    hipLaunchKernelGGL(train_finalize_kernel, dim3((a.n_rays + 255) / 256), dim3(256), 0, s, a, b);
-    hipLaunchKernelGGL(train_dloss_kernel, dim3((a.n_rays + 3) / 4), dim3(256), 0, s, a, b);
+    // rayrec, cnt_i and loss were cleared at the start of the step (launch_train_clear)
+    const uint32_t n = std::max(1u, a.n_rays_grid);
+    hipLaunchKernelGGL(train_loss_kernel, dim3((n * LOSS_G + 255) / 256), dim3(256), 0, s, a, im, b, rng, mean_density);
+    hipLaunchKernelGGL(train_compact_kernel, dim3(1), dim3(1024), 0, s, a.sched, b.cnt_i, b.cbase_i, b.ctrl);
+    hipLaunchKernelGGL(train_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
+    hipLaunchKernelGGL(train_dloss_kernel, dim3((n + 3) / 4), dim3(256), 0, s, a, b);
     hipLaunchKernelGGL(train_rollover_kernel, dim3((a.target_batch + 255) / 256), dim3(256), 0, s, a, b);
 }
 void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s) {
@@ -1066,9 +1129,10 @@ void launch_train_mark_untrained(uint32_t n, float* grid, const TrainImages& im,
     hipLaunchKernelGGL(train_mark_untrained_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, grid, im, clear_visible);
 }
 void launch_train_grid_samples(uint32_t n, Pcg32 rng, uint32_t step, const aabb& box, const float* grid, float* coords, uint32_t* indices, uint32_t n_cascades,
-                               float thresh, hipStream_t s) {
+                               float thresh, int morton, hipStream_t s) {
     if (!n) return;
-    hipLaunchKernelGGL(train_grid_samples_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, rng, step, box, grid, coords, indices, n_cascades, thresh);
+    hipLaunchKernelGGL(train_grid_samples_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, rng, step, box, grid, coords, indices, n_cascades, thresh,
+                       morton && n % GRID_CELLS == 0 ? 1 : 0);
 }
 void launch_train_grid_splat_ema(uint32_t n_samples, const uint32_t* indices, const uint16_t* out4, float* tmp, uint32_t n_cells, float decay, float* grid,
                                  hipStream_t s) {

@@ -75,17 +75,22 @@ def test_train_generate_matches_oracle(trainer, oracle_lib):
     _check_generate(trainer, oracle_lib)
 
 
-@pytest.mark.parametrize("lanes,bricks", [(1, 0), (16, 0), (1, 1)], ids=["one_lane", "16_lanes", "lds_bricks"])
-def test_train_generate_variants_match_oracle(trainer, oracle_lib, lanes, bricks):
-    """The generator's other forms (train_gen_lanes 1 / 16, train_gen_bricks 1) against the same oracle, bit-exact."""
+@pytest.mark.parametrize("lanes,bricks,est", [(1, 0, 0), (16, 0, 0), (1, 1, 0), (8, 0, 64), (1, 0, 64)],
+                         ids=["one_lane", "16_lanes", "lds_bricks", "8_lanes_grid_stride", "one_lane_grid_stride"])
+def test_train_generate_variants_match_oracle(trainer, oracle_lib, lanes, bricks, est):
+    """The generator's other forms (train_gen_lanes 1 / 16, train_gen_bricks 1) against the same oracle, bit-exact;
+    est > 0 sizes the grid for that many rays (train_grid_est), so every workgroup loops over many rays of the device's
+    ray count (the count the host does not wait for)."""
     eng = trainer["eng"]
     eng.set_param("train_gen_lanes", lanes)
     eng.set_param("train_gen_bricks", bricks)
+    eng.set_param("train_grid_est", est)
     try:
         _check_generate(trainer, oracle_lib)
     finally:
         eng.set_param("train_gen_lanes", 8)
         eng.set_param("train_gen_bricks", 0)
+        eng.set_param("train_grid_est", 0)
 
 
 def _check_generate(trainer, oracle_lib):
@@ -152,8 +157,13 @@ def _loss_reference(T, d):
     return out
 
 
-def test_train_loss_and_output_gradients(trainer):
-    d = _step_state(trainer, 3)
+@pytest.mark.parametrize("est", [0, 64], ids=["grid_estimate", "grid_stride"])
+def test_train_loss_and_output_gradients(trainer, est):
+    trainer["eng"].set_param("train_grid_est", est)
+    try:
+        d = _step_state(trainer, 3)
+    finally:
+        trainer["eng"].set_param("train_grid_est", 0)
     ref = _loss_reference(trainer, d)
     n_comp = int(min(d["ctrl"][2], BATCH))
     assert int(d["ctrl"][2]) == sum(r[0] for r in ref), "compacted sample count"
@@ -245,3 +255,31 @@ def test_train_converges(trainer):
     gt = trainer["imgs"][0].astype(np.float32).reshape(200, 2, 200, 2, 4).mean(axis=(1, 3)) / 255.0
     psnr = 10 * np.log10(1.0 / np.mean((pred - gt[..., :3] * gt[..., 3:4]) ** 2))
     assert psnr > 20.0, psnr
+
+
+def test_grid_update_morton_slots_are_order_only():
+    """The uniform density-grid update with its samples in the Morton order of their cells (train_grid_morton, the
+    default) leaves the same density grid, mean and bitfield as the samples in index order (first step from a reset:
+    the update of step 0 runs on the initial parameters, so both runs see the same network)."""
+    from synerfgine_amd import Engine, Testbed, nerf_data, synthetic
+    imgs, xf, focal, pp = nerf_data.load_nerf_synthetic(os.path.join(REPO, "data", "nerf", "lego400"), max_images=8)
+    out = []
+    for morton in (0, 1):
+        tb = Testbed(0)
+        try:
+            cfg, params = synthetic.random_init(1337)
+            tb.set_nerf_model(cfg, params)
+            eng = Engine(tb)
+            eng.set_param("train_batch", BATCH)
+            eng.set_param("train_grid_morton", morton)
+            tb.set_training_dataset(imgs, xf, focal, pp)
+            tb.train_reset(1337)
+            tb.train(1)
+            out.append((tb.train_debug(0, "grid", np.float32).copy(), tb.density_grid_mean(), tb.density_grid_bitfield().copy()))
+        finally:
+            tb.close()
+    (g0, m0, b0), (g1, m1, b1) = out
+    assert np.count_nonzero(g0 > 0) > 1000
+    np.testing.assert_array_equal(g0.view(np.uint32), g1.view(np.uint32))
+    assert m0 == m1
+    np.testing.assert_array_equal(b0, b1)
