@@ -2181,14 +2181,14 @@ void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev
     mark(1);
     if (stage == 1) return;
     // inference forward of every sample with the training params
-    launch_train_pack(t.p_train.as<uint16_t>(), t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
+    // with the network's count = min(numsteps_counter, max_samples): the generator drops rays beyond max_samples
+    launch_train_pack(t.p_train.as<uint16_t>(), t.wfrag_train.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s, &b.ctrl->numsteps_counter, a.sched,
+                      t.ctrl.as<uint32_t>() + 3);
     const NetworkDev net = train_net(c, t.p_train, t.wfrag_train);
-    // count = min(numsteps_counter, max_samples): the generator drops rays beyond max_samples
-    launch_train_clamp_count(&b.ctrl->numsteps_counter, a.sched, t.ctrl.as<uint32_t>() + 3, s);
     launch_network(net, b.coords, 7, 0, t.ctrl.as<uint32_t>() + 3, b.mlp_out, 1, (t.target * 16 + 15) / 16, s);
     mark(2);
     if (stage == 2) return;
-    launch_train_loss(a, im, b, t.rng, c->d_mean.as<float>(), s);
+    launch_train_loss(a, im, b, t.rng, c->d_mean.as<float>(), stage == 0 ? t.sched.as<TrainSched>() : nullptr, s);
     mark(3);
     if (stage == 3) return;
     const uint64_t n_mlp = 3072 + 7168;
@@ -2253,9 +2253,9 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
         if (timed) HIPCHK(hipEventRecord(c->train_events[7], s));
         t.rng.advance();
         ++t.step;
-        // NerfCounters::update_after_training (3272-3296) on the device: the next step reads its batch sizes from there,
-        // so the host queues the steps without waiting for each (the reference syncs on a readback every step)
-        launch_train_sched_update(t.sched.as<TrainSched>(), t.ctrl.as<TrainCtrl>(), t.target, s);
+        // NerfCounters::update_after_training (3272-3296) ran on the device at the end of the loss stage (train_rollover_kernel):
+        // the next step reads its batch sizes from there, so the host queues the steps without waiting for each (the
+        // reference syncs on a readback every step)
         // the grid-size estimate follows the device's ray count through the readback slots (correctness never depends
         // on it: the kernels loop over the device count)
         if (t.step % 8 == 0) {

@@ -136,7 +136,7 @@ struct TrainCtrl {
 };
 
 // NerfCounters' batch sizes (testbed_nerf.cu:3272-3296), kept on the device: the step's kernels read them, and
-// train_sched_update_kernel forms the next step's from the step's counters, so the host never waits for a step
+// train_rollover_kernel forms the next step's from the step's counters, so the host never waits for a step
 struct TrainSched {
     uint32_t n_rays;            // rays_per_batch
     uint32_t max_samples;       // max_inference (from measured_before)
@@ -192,15 +192,16 @@ struct AdamArgs {
     const uint16_t* grads_h;  // fp16 grid gradients (param index - n_matrix), nullptr: every gradient in `grads`
 };
 
-void launch_train_clamp_count(const uint32_t* in, const TrainSched* sched, uint32_t* out, hipStream_t s);
-// the next step's TrainSched from this step's counters (NerfCounters::update_after_training)
-void launch_train_sched_update(TrainSched* sched, const TrainCtrl* ctrl, uint32_t target, hipStream_t s);
 // zero loss / rayrec / cnt_i for the step's rays (device count)
 void launch_train_clear(const TrainStepArgs& a, const TrainBatch& b, hipStream_t s);
 // tscr: [NERF_STEPS][n_rays] floats of scratch (the first march's sample distances)
 void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, float* tscr, hipStream_t s);
-void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s);
-void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s);
+// sched_next: the next step's batch sizes formed at the end of the stage (NerfCounters::update_after_training); null in the parity hooks
+void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, TrainSched* sched_next,
+                       hipStream_t s);
+// clamp_in / sched / clamp_out: also *clamp_out = min(*clamp_in, sched->max_samples) (the training step's network count)
+void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s, const uint32_t* clamp_in = nullptr,
+                       const TrainSched* sched = nullptr, uint32_t* clamp_out = nullptr);
 void launch_train_field(const TrainStepArgs& a, const TrainBatch& b, const NetworkDev& net, const uint16_t* wfrag, const uint16_t* wfrag_t,
                         const uint16_t* grid, float* ggrad, uint16_t* ggrad_h, hipStream_t s);
 void launch_train_dw(const TrainStepArgs& a, const uint16_t* acts, float* wgrad, uint32_t n_cus, hipStream_t s);

@@ -326,7 +326,7 @@ __global__ __launch_bounds__(256) void train_loss_kernel(TrainStepArgs a, TrainI
         const float l1_reg_density = *mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
         // the per-sample gradients need only this ray's constants and the forward partials: they are
         // written by train_dloss_kernel with one wave per ray instead of this lane's serial loop
-        b.rayrec[3 * i] = make_float4(0.0f, 0.0f, __uint_as_float(base), 0.0f);   // slot and count: train_finalize_kernel
+        b.rayrec[3 * i] = make_float4(0.0f, 0.0f, __uint_as_float(base), 0.0f);
         b.rayrec[3 * i + 1] = make_float4(grad.x, grad.y, grad.z, loss_scale);
         b.rayrec[3 * i + 2] = make_float4(rgb_ray.x, rgb_ray.y, rgb_ray.z, l1_reg_density);
     }
@@ -356,22 +356,6 @@ __global__ __launch_bounds__(1024) void train_compact_kernel(const TrainSched* _
     for (uint32_t k = t0; k < t1; ++k) { cbase[k] = run; run += cnt[k]; }
     if (threadIdx.x == 1023) ctrl->numsteps_compacted = part[1023];
 }
-__global__ __launch_bounds__(256) void train_finalize_kernel(TrainStepArgs a, TrainBatch b) {
-    const uint32_t n_in = b.ctrl->ray_counter;
-    for (uint32_t vb = blockIdx.x; vb * blockDim.x < n_in; vb += gridDim.x) {
-        const uint32_t i = vb * blockDim.x + threadIdx.x;
-        if (i >= n_in) continue;
-        const uint32_t ri = b.ray_indices[i], cn = b.cnt_i[ri], cbase = b.cbase_i[ri];
-        const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
-        if (ccount == 0) {   // past the batch target: no loss and no gradient for this ray (testbed_nerf.cu: compacted_numsteps == 0)
-            b.rayrec[3 * i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            b.loss[i] = 0.0f;
-            continue;
-        }
-        b.rayrec[3 * i].x = __uint_as_float(cbase);
-        b.rayrec[3 * i].y = __uint_as_float(ccount);
-    }
-}
 
 // compute_loss_kernel_train_nerf's gradient loop (testbed_nerf.cu:1209-1275) for the ray's first
 // ccount samples, one wave per ray, lanes over the samples: T and the running rgb come from the
@@ -382,9 +366,15 @@ __global__ __launch_bounds__(256) void train_dloss_kernel(TrainStepArgs a, Train
         const uint32_t i = (vb * blockDim.x + threadIdx.x) >> 6;
         const uint32_t lane = threadIdx.x & 63;
         if (i >= n_in) continue;
+        // the ray's compaction slot and count (a prefix over the rays' image order, train_compact_kernel)
+        const uint32_t ri = b.ray_indices[i], cn = b.cnt_i[ri], cbase = b.cbase_i[ri];
+        const uint32_t ccount = min(a.target_batch - min(a.target_batch, cbase), cn);
+        if (ccount == 0) {   // past the batch target: no loss and no gradient for this ray (testbed_nerf.cu: compacted_numsteps == 0)
+            if (lane == 0) b.loss[i] = 0.0f;
+            continue;
+        }
         const float4 r0 = b.rayrec[3 * i], r1 = b.rayrec[3 * i + 1], r2 = b.rayrec[3 * i + 2];
-        if (r0.x == 0.0f && r0.y == 0.0f && r0.z == 0.0f && r0.w == 0.0f) continue;   // ray returned before its record (ccount 0)
-        const uint32_t cbase = __float_as_uint(r0.x), ccount = __float_as_uint(r0.y), base = __float_as_uint(r0.z);
+        const uint32_t base = __float_as_uint(r0.z);
         const f3 grad = mk(r1.x, r1.y, r1.z), rgb_ray = mk(r2.x, r2.y, r2.z);
         const float loss_scale = r1.w, l1_reg_density = r2.w;
         const aabb box = a.vol.train_aabb;
@@ -426,10 +416,31 @@ __global__ __launch_bounds__(256) void train_dloss_kernel(TrainStepArgs a, Train
     }
 }
 
+// NerfCounters::update_after_training (testbed_nerf.cu:3272-3296) on the device: the next step's rays_per_batch from this
+// step's compacted count, with the host expressions' float operations (correctly rounded multiply and divide), and the
+// next max_inference from the count before compaction (train_args' rounding)
+__device__ void sched_update(TrainSched* __restrict__ sched, const TrainCtrl* __restrict__ ctrl, uint32_t target) {
+    TrainSched n = *sched;
+    const uint32_t before = ctrl->numsteps_counter, after = ctrl->numsteps_compacted;
+    if (before == 0 || after == 0) {
+        n.measured = n.measured_before = 0;
+    } else {
+        n.measured_before = before;
+        n.measured = after;
+        const uint32_t r = (uint32_t)__fdiv_rn(__fmul_rn((float)n.n_rays, (float)target), (float)after);
+        n.n_rays = min((r + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY, 1u << 18);
+    }
+    const uint32_t cap = target * 16;
+    n.max_samples = n.measured_before == 0 ? cap : (min(n.measured_before, cap) + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY;
+    *sched = n;
+}
+
 // tcnn fill_rollover / fill_rollover_and_rescale: entries [n_in, target) repeat entry (i mod n_in);
 // rolled-over gradients are scaled by n_in / target
-__global__ void train_rollover_kernel(TrainStepArgs a, TrainBatch b) {
+// sched_next (training steps, not the parity hooks): one thread also forms the next step's batch sizes (sched_update)
+__global__ void train_rollover_kernel(TrainStepArgs a, TrainBatch b, TrainSched* __restrict__ sched_next) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sched_next && i == 0) sched_update(sched_next, b.ctrl, a.target_batch);
     if (i >= a.target_batch) return;
     const uint32_t n_in = min(b.ctrl->numsteps_compacted, a.target_batch);
     if (n_in == 0 || i < n_in) return;
@@ -449,7 +460,11 @@ __device__ __forceinline__ uint16_t fwd_frag_elem(const uint16_t* W, int n_in, i
     const int k = permuted ? 32 * kb + 16 * (j >= 4) + 4 * g + (j & 3) : 32 * kb + 8 * g + j;
     return W[row * n_in + k];
 }
-__global__ void train_pack_kernel(const uint16_t* __restrict__ p, uint16_t* __restrict__ wfrag, uint16_t* __restrict__ wfrag_t) {
+// clamp_in (the training step's pack): one thread also writes the network's sample count, min(numsteps_counter,
+// max_samples) -- the generator drops rays beyond max_samples
+__global__ void train_pack_kernel(const uint16_t* __restrict__ p, uint16_t* __restrict__ wfrag, uint16_t* __restrict__ wfrag_t, const uint32_t* __restrict__ clamp_in,
+                                  const TrainSched* __restrict__ sched, uint32_t* __restrict__ clamp_out) {
+    if (clamp_in && blockIdx.x == 0 && threadIdx.x == 0) *clamp_out = min(*clamp_in, sched->max_samples);
     const int lane = threadIdx.x & 63, f = blockIdx.x;   // grid: 20 forward + 36 backward fragments
     const uint16_t *dW0 = p, *dW1 = p + 64 * 32, *rW0 = p + 3072, *rW1 = rW0 + 64 * 32, *rW2 = rW1 + 64 * 64;
     if (f < 20) {
@@ -1017,29 +1032,7 @@ __global__ void train_grid_ema_kernel(uint32_t n, float decay, float* __restrict
     grid[i] = prev < 0.0f ? prev : fmaxf(prev * decay, tmp[i]);
 }
 
-__global__ void train_clamp_count_kernel(const uint32_t* __restrict__ in, const TrainSched* __restrict__ sched, uint32_t* __restrict__ out) {
-    if (threadIdx.x == 0) *out = min(*in, sched->max_samples);
-}
 
-// NerfCounters::update_after_training (testbed_nerf.cu:3272-3296) on the device: the next step's rays_per_batch from this
-// step's compacted count, with the host expressions' float operations (correctly rounded multiply and divide), and the
-// next max_inference from the count before compaction (train_args' rounding)
-__global__ void train_sched_update_kernel(TrainSched* __restrict__ sched, const TrainCtrl* __restrict__ ctrl, uint32_t target) {
-    if (threadIdx.x != 0) return;
-    TrainSched n = *sched;
-    const uint32_t before = ctrl->numsteps_counter, after = ctrl->numsteps_compacted;
-    if (before == 0 || after == 0) {
-        n.measured = n.measured_before = 0;
-    } else {
-        n.measured_before = before;
-        n.measured = after;
-        const uint32_t r = (uint32_t)__fdiv_rn(__fmul_rn((float)n.n_rays, (float)target), (float)after);
-        n.n_rays = min((r + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY, 1u << 18);
-    }
-    const uint32_t cap = target * 16;
-    n.max_samples = n.measured_before == 0 ? cap : (min(n.measured_before, cap) + BATCH_SIZE_GRANULARITY - 1) / BATCH_SIZE_GRANULARITY * BATCH_SIZE_GRANULARITY;
-    *sched = n;
-}
 
 // the per-ray buffers the step fills by ray index, cleared up to the device's ray count
 __global__ __launch_bounds__(256) void train_clear_kernel(const TrainSched* __restrict__ sched, float* __restrict__ loss, float4* __restrict__ rayrec,
@@ -1053,12 +1046,6 @@ __global__ __launch_bounds__(256) void train_clear_kernel(const TrainSched* __re
 }
 
 // ---------------------------------------------------------------------------------------------
-void launch_train_clamp_count(const uint32_t* in, const TrainSched* sched, uint32_t* out, hipStream_t s) {
-    hipLaunchKernelGGL(train_clamp_count_kernel, dim3(1), dim3(64), 0, s, in, sched, out);
-}
-void launch_train_sched_update(TrainSched* sched, const TrainCtrl* ctrl, uint32_t target, hipStream_t s) {
-    hipLaunchKernelGGL(train_sched_update_kernel, dim3(1), dim3(64), 0, s, sched, ctrl, target);
-}
 void launch_train_clear(const TrainStepArgs& a, const TrainBatch& b, hipStream_t s) {
     hipLaunchKernelGGL(train_clear_kernel, dim3(std::max(1u, (3 * a.n_rays_grid + 255) / 256)), dim3(256), 0, s, a.sched, b.loss, b.rayrec, b.cnt_i, b.ctrl);
 }
@@ -1083,17 +1070,18 @@ void launch_train_generate(const TrainStepArgs& a, const TrainImages& im, const 
     else
         hipLaunchKernelGGL((train_generate_kernel<0, false>), grid, dim3(64), 0, s, a, im, b, rng, tscr);
 }
-void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, hipStream_t s) {
+void launch_train_loss(const TrainStepArgs& a, const TrainImages& im, const TrainBatch& b, Pcg32 rng, const float* mean_density, TrainSched* sched_next,
+                       hipStream_t s) {
     // rayrec, cnt_i and loss were cleared at the start of the step (launch_train_clear)
     const uint32_t n = std::max(1u, a.n_rays_grid);
     hipLaunchKernelGGL(train_loss_kernel, dim3((n * LOSS_G + 255) / 256), dim3(256), 0, s, a, im, b, rng, mean_density);
     hipLaunchKernelGGL(train_compact_kernel, dim3(1), dim3(1024), 0, s, a.sched, b.cnt_i, b.cbase_i, b.ctrl);
-    hipLaunchKernelGGL(train_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, b);
     hipLaunchKernelGGL(train_dloss_kernel, dim3((n + 3) / 4), dim3(256), 0, s, a, b);
-    hipLaunchKernelGGL(train_rollover_kernel, dim3((a.target_batch + 255) / 256), dim3(256), 0, s, a, b);
+    hipLaunchKernelGGL(train_rollover_kernel, dim3((a.target_batch + 255) / 256), dim3(256), 0, s, a, b, sched_next);
 }
-void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s) {
-    hipLaunchKernelGGL(train_pack_kernel, dim3(56), dim3(64), 0, s, params, wfrag, wfrag_t);
+void launch_train_pack(const uint16_t* params, uint16_t* wfrag, uint16_t* wfrag_t, hipStream_t s, const uint32_t* clamp_in, const TrainSched* sched,
+                       uint32_t* clamp_out) {
+    hipLaunchKernelGGL(train_pack_kernel, dim3(56), dim3(64), 0, s, params, wfrag, wfrag_t, clamp_in, sched, clamp_out);
 }
 void launch_train_field(const TrainStepArgs& a, const TrainBatch& b, const NetworkDev& net, const uint16_t* wfrag, const uint16_t* wfrag_t,
                         const uint16_t* grid, float* ggrad, uint16_t* ggrad_h, hipStream_t s) {
