@@ -297,8 +297,8 @@ def train_leg(steps=200, warmup=50, seed=1337, engine_params=None):
     """BASELINE config C5: online training on the reference's lego set (data/nerf/lego400, 95
     views, every 20th held out as tools/train_lego.py does) from a fresh init, batch 2^18 samples per step
     (m_training_batch_size, testbed.h:1103): `warmup` untimed steps, then `steps` timed ones (host wall clock
-    around sng_train, which syncs once per step for the batch counters as NerfCounters::update_after_training
-    does, testbed_nerf.cu:3272-3296).  fp16 parameters / activations / gradient GEMM operands with f32 master
+    around sng_train; the batch counters of NerfCounters::update_after_training, testbed_nerf.cu:3272-3296, are
+    updated on the device, so the host does not wait for each step as the reference does -- DESIGN.md §7).  fp16 parameters / activations / gradient GEMM operands with f32 master
     weights and accumulation, tcnn's types (BASELINE.json C5 names bf16)."""
     import numpy as np
     from synerfgine_amd import Engine, Testbed, nerf_data, synthetic
