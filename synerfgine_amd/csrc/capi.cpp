@@ -425,6 +425,8 @@ const std::map<std::string, double>& default_params() {
         {"visualized_layer", 0},                // Testbed::m_visualized_layer (testbed.h:1024)
         {"visualized_dimension", -1},           // Testbed::m_visualized_dimension (testbed.h:1023); > -1 selects EncodingVis (testbed_nerf.cu:2491)
         {"train_grid_est", 0},                  // > 0: the per-ray training kernels' grid sized for this many rays (tests of their grid-stride loops)
+        {"train_overlap", 1},                   // the next step's generate on a second stream beside this step's gradients / optimizer
+        {"train_overlap_tail", 0},              // tests: sng_train also generates the next step ahead, for the parity hook
         {"train_grid_morton", 1},               // density-grid update: the uniform samples in the Morton order of their cells (same samples, same grid)
         {"train_gen_bricks", 0},                // training generator's occupancy: 0 the linear words (measured fastest, tools/train_ab.py), 1 the OccBrick blob (LDS when it fits, else global)
         {"train_grid_grad_f16", 1},             // hash-grid gradients in fp16 with packed atomics, tcnn's grad_t (__half2 atomicAdd); 0: f32
@@ -604,6 +606,9 @@ struct sng_ctx {
         bool sched_pending[2] = {false, false};
         uint32_t sched_slot = 0;
         uint32_t n_rays_est = 1u << 12;                // grid sizes only (n_rays_grid)
+        hipStream_t s_gen = nullptr;                   // train_overlap: the next step's generate
+        hipEvent_t ev_gen = nullptr, ev_loss = nullptr;
+        bool pregen = false;                           // the next step's samples are queued on s_gen (train_overlap_tail)
         Pcg32 rng{}, grid_rng{};
         int w = 0, h = 0, n_images = 0;
         DevBuf pixels, xforms, xforms_ray, focal, pp;
@@ -2065,6 +2070,7 @@ void train_reset(sng_ctx* c, uint64_t seed) {
     t.step = 0; t.grid_ema_step = 0; t.rays_per_batch = 1u << 12; t.measured = 0; t.measured_before = 0;
     t.sched.ensure(sizeof(TrainSched));
     t.sched_dirty = true;
+    if (t.pregen) { HIPCHK(hipStreamSynchronize(t.s_gen)); t.pregen = false; }   // a step generated ahead belongs to the old run
     t.target = (uint32_t)c->p("train_batch");
     const uint32_t target = t.target, max_samples = target * 16;
     t.ctrl.ensure(sizeof(TrainCtrl));
@@ -2159,7 +2165,7 @@ TrainBatch train_batch(sng_ctx* c) {
 // 1 = samples generated, 2 = network outputs, 3 = loss / compaction, 4 = gradients
 // ev (train_kernel_times): 8 events bracketing generate | network | loss | gradient clear | field | dW (the optimizer's
 // event is recorded by train_steps)
-void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev = nullptr) {
+void train_sched_push(sng_ctx* c, hipStream_t s) {
     auto& t = c->tr;
     if (t.sched_dirty) {   // host-set batch sizes (reset, snapshot load): train_args' max_inference from measured_before
         const uint32_t cap = t.target * 16;
@@ -2171,14 +2177,32 @@ void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev
         t.n_rays_est = t.rays_per_batch;
         t.sched_dirty = false;
     }
+}
+
+// the step's first stage: the per-ray buffers cleared, the samples generated (rng: the step's stream)
+void train_generate_stage(sng_ctx* c, const Pcg32& rng, hipStream_t s) {
+    auto& t = c->tr;
+    const TrainStepArgs a = train_args(c);
+    const TrainBatch b = train_batch(c);
+    launch_train_clear(a, b, s);   // also zeroes the batch counters (TrainCtrl)
+    launch_train_generate(a, train_images(c), b, rng, t.tscr.as<float>(), s);
+}
+
+// generated: the step's samples were queued ahead on the generator stream (train_steps); ev_loss: recorded after the
+// loss stage (the next step's generate may start from there)
+void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev = nullptr, bool generated = false, hipEvent_t ev_loss = nullptr) {
+    auto& t = c->tr;
+    train_sched_push(c, s);
     const TrainStepArgs a = train_args(c);
     const TrainBatch b = train_batch(c);
     const TrainImages im = train_images(c);
-    launch_train_clear(a, b, s);   // also zeroes the batch counters (TrainCtrl)
     auto mark = [&](int k) { if (ev) HIPCHK(hipEventRecord(ev[k], s)); };
-    mark(0);
-    launch_train_generate(a, im, b, t.rng, t.tscr.as<float>(), s);
-    mark(1);
+    if (!generated) {
+        launch_train_clear(a, b, s);   // also zeroes the batch counters (TrainCtrl)
+        mark(0);
+        launch_train_generate(a, im, b, t.rng, t.tscr.as<float>(), s);
+        mark(1);
+    }
     if (stage == 1) return;
     // inference forward of every sample with the training params
     // with the network's count = min(numsteps_counter, max_samples): the generator drops rays beyond max_samples
@@ -2189,6 +2213,7 @@ void train_forward_backward(sng_ctx* c, int stage, hipStream_t s, hipEvent_t* ev
     mark(2);
     if (stage == 2) return;
     launch_train_loss(a, im, b, t.rng, c->d_mean.as<float>(), stage == 0 ? t.sched.as<TrainSched>() : nullptr, s);
+    if (ev_loss) HIPCHK(hipEventRecord(ev_loss, s));
     mark(3);
     if (stage == 3) return;
     const uint64_t n_mlp = 3072 + 7168;
@@ -2221,11 +2246,36 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
     while (timed && c->train_events.size() < 8) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); c->train_events.push_back(e); }
     double stage_ms[7] = {0, 0, 0, 0, 0, 0, 0};
     uint32_t timed_steps = 0;
+    const bool overlap = !timed && c->p("train_overlap") != 0.0;
+    if (overlap && !t.s_gen) {
+        HIPCHK(hipStreamCreateWithFlags(&t.s_gen, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&t.ev_gen, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&t.ev_loss, hipEventDisableTiming));
+    }
+    bool generated = t.pregen;
+    t.pregen = false;
+    train_sched_push(c, s);
     for (uint32_t k = 0; k < n_steps; ++k) {
         // Testbed::train: training_prep_nerf every clamp(step / 16, 1, 16) steps (testbed.cu:4081-4091)
         const uint32_t skip = std::min(16u, std::max(1u, t.step / 16u));
-        if (t.step % skip == 0) train_density_update(c, s);
-        train_forward_backward(c, 0, s, timed ? c->train_events.data() : nullptr);
+        if (t.step % skip == 0) train_density_update(c, s);   // never on a step generated ahead (below)
+        if (generated) HIPCHK(hipStreamWaitEvent(s, t.ev_gen, 0));
+        train_forward_backward(c, 0, s, timed ? c->train_events.data() : nullptr, generated, overlap ? t.ev_loss : nullptr);
+        generated = false;
+        // the next step's samples depend on this step's batch sizes (formed in the loss stage) and on the occupancy
+        // grid, not on the parameters: unless a density-grid update comes first, they are generated on a second stream
+        // while this step's gradients and optimizer run (train_overlap; not with per-stage timing)
+        if (overlap && k + 1 < n_steps) {
+            const uint32_t ns = t.step + 1, skip_n = std::min(16u, std::max(1u, ns / 16u));
+            if (ns % skip_n != 0) {
+                HIPCHK(hipStreamWaitEvent(t.s_gen, t.ev_loss, 0));
+                Pcg32 r = t.rng;
+                r.advance();
+                train_generate_stage(c, r, t.s_gen);
+                HIPCHK(hipEventRecord(t.ev_gen, t.s_gen));
+                generated = true;
+            }
+        }
         // optimizer_step: Ema(ExponentialDecay(Adam)) (base.json)
         AdamArgs o{};
         const uint32_t decays = t.step >= 20000 ? (t.step - 20000) / 10000 + 1 : 0;
@@ -2277,6 +2327,17 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
                 stage_ms[q] += ms;
             }
             ++timed_steps;
+        }
+    }
+    // tests (train_overlap_tail): the next step generated ahead as in the loop, for the parity hook to check
+    if (overlap && n_steps && c->p("train_overlap_tail") != 0.0) {
+        const uint32_t skip_n = std::min(16u, std::max(1u, t.step / 16u));
+        if (t.step % skip_n != 0) {
+            HIPCHK(hipStreamWaitEvent(t.s_gen, t.ev_loss, 0));
+            train_generate_stage(c, t.rng, t.s_gen);   // t.rng is the next step's stream already
+            HIPCHK(hipEventRecord(t.ev_gen, t.s_gen));
+            HIPCHK(hipStreamWaitEvent(s, t.ev_gen, 0));
+            t.pregen = true;
         }
     }
     HIPCHK(hipEventRecord(c->ev_end, s));
@@ -2407,6 +2468,9 @@ void ctx_destroy(sng_ctx* c) {
     for (hipEvent_t e : c->train_events) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->tr.sched_ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->tr.ev_gen) (void)hipEventDestroy(c->tr.ev_gen);
+    if (c->tr.ev_loss) (void)hipEventDestroy(c->tr.ev_loss);
+    if (c->tr.s_gen) (void)hipStreamDestroy(c->tr.s_gen);
     if (c->tr.h_sched) (void)hipHostFree(c->tr.h_sched);
     (void)hipHostFree(c->h_ctrl);
     (void)hipHostFree(c->h_alive);
@@ -3396,7 +3460,8 @@ int sng_train_debug(sng_ctx* c, int stage, const char* name, void* out, uint64_t
         if (t.n_images == 0) throw SngError(SNG_ERR_STATE, "no training images");
         if (stage > 0) {
             if (t.step == 0 && !c->has_bitfield) train_density_update(c, c->s_nerf);
-            train_forward_backward(c, stage, c->s_nerf);
+            train_forward_backward(c, stage, c->s_nerf, nullptr, t.pregen);   // pregen: samples already generated on s_gen
+            t.pregen = false;
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(c->s_nerf));

@@ -93,6 +93,21 @@ def test_train_generate_variants_match_oracle(trainer, oracle_lib, lanes, bricks
         eng.set_param("train_grid_est", 0)
 
 
+def test_train_generate_ahead_matches_oracle(trainer, oracle_lib):
+    """sng_train generates the next step's samples on a second stream while the current step's gradients and optimizer
+    run (train_overlap); train_overlap_tail leaves the last such step queued, and the parity hook checks it."""
+    eng = trainer["eng"]
+    eng.set_param("train_overlap_tail", 1)
+    try:
+        for _ in range(3):   # a step with a density-grid update due is not generated ahead: try a few
+            trainer["stats"] = trainer["tb"].train(1)
+            if int(trainer["stats"]["step"]) % max(1, min(16, int(trainer["stats"]["step"]) // 16)):
+                break
+        _check_generate(trainer, oracle_lib)
+    finally:
+        eng.set_param("train_overlap_tail", 0)
+
+
 def _check_generate(trainer, oracle_lib):
     import train_ref as R
     O = oracle_lib
