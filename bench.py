@@ -30,7 +30,9 @@ BYTES_PER_SAMPLE = 28 + 8 * 8 * 4 * 2 + 8   # NerfCoordinate read + 8 levels x 8
 FLOPS_PER_SAMPLE = 20480                     # 2*(32*64+64*16) + 2*(32*64+64*64+64*16)
 HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F16_PEAK_TFLOPS = 2500.0                # dense fp16/bf16 MFMA
-ROUND = "r05"
+ROUND = "r06"
+EXTRAS_FILE = f"profiles/bench_extra_{ROUND}.json"   # the legs of this build (bench.py --extras), committed
+LINE_MAX_BYTES = 6000                        # the driver reads the line from an 8 KB stdout tail
 
 WORKLOADS = {
     "c2": "lego NeRF only (show_virtual_obj=0, shadows off)",
@@ -56,8 +58,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c4fox"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-sweep", action="store_true", help="skip the extra legs (C3 nerf_shadow_samples r=2, the reference's "
-                                                            "dmrf-compare-abm --sshadows/--nshadows sweep)")
+    ap.add_argument("--no-sweep", action="store_true", help="skip every leg after the timed region (serialized roofline, BVH "
+                                                            "counters, training)")
+    ap.add_argument("--extras", default=None, metavar="PATH",
+                    help="also run the extra legs (C3 nerf_shadow_samples r=2, the reference's dmrf-compare-abm sweep, the "
+                         "NeRF views, the trained-fox C4 legs) and write the full result to PATH (the stdout line stays compact)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed oracle runs per CPU-baseline leg (median reported)")
     ap.add_argument("--serial-streams", action="store_true", help="run raytracer and NeRF back to back (profiling)")
     ap.add_argument("--cpu-baseline-scale", type=float, default=1.0, help="the C3-sample leg renders the frame at 1/scale linear resolution")
@@ -184,7 +189,7 @@ def cpu_sample_c3(eng_cfg, config, scale, model_name, overrides):
 
 def latest_profile(prefix, config):
     """profiles/<prefix>_<round>_<config>.json of the newest round that has one (this round's first)."""
-    for rnd in (ROUND, "r04", "r03", "r02", "r01"):
+    for rnd in (ROUND, "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", f"{prefix}_{rnd}_{config}.json")
         if os.path.exists(path):
             return path
@@ -370,7 +375,7 @@ def train_leg(steps=200, warmup=50, seed=1337, engine_params=None):
                 "dtype": "fp16 params / activations / GEMM operands / hash-grid gradients (tcnn's grad_t), f32 master weights, MLP gradients and accumulation "
                          "(tcnn's network_precision_t; BASELINE.json C5 says bf16)",
                 "data": "data/nerf/lego400 (the reference's lego set at 400x400), 90 training views, fresh init (seed 1337)",
-                "kernel_profile": "profiles/r04_train_kernel_table.txt (rocprofv3 of tools/train_bench.py)"}
+                "kernel_profile": f"profiles/{ROUND}_train_kernel_table.txt (rocprofv3 of tools/train_bench.py, this build)"}
     finally:
         tb.close()
 
@@ -537,6 +542,250 @@ def nerf_views(model, frames, warmup, cpu_check=True):
     return out
 
 
+def bvh_leg(eng, config, s0):
+    """BVH work of one C3/C4 frame: a lane-level counting frame (rt_count = 1: world queries, box and triangle tests) and a
+    wave-level one (rt_count = 2: wave iterations of the record and triangle loops), both rendered by the counting
+    instantiations of the traversal kernels (bit-identical frames, untimed).  lane_eff = lane work / (64 x wave
+    iterations); useful_frac = the kernel's VALU issue fraction (profiles/sq_*.json) x the record loop's lane_eff."""
+    cnt = {}
+    for mode in (1, 2):
+        eng.set_param("rt_count", mode)
+        eng.frame(spp=0, reset=True)
+        cnt[mode] = eng.rt_counters()
+    eng.set_param("rt_count", 0)
+    lane, wave = cnt[1], cnt[2]
+    eff = {k: {"record_loop": round(lane[k]["box_tests"] / 2 / max(1, 64 * wave[k]["box_tests"]), 4),
+               "tri_loop": round(lane[k]["tri_tests"] / max(1, 64 * wave[k]["tri_tests"]), 4)} for k in ("path", "shadow")}
+    valu = valu_profile(config)
+    useful = {}
+    if valu:
+        for kern, k in (("raytrace_kernel", "path"), ("shadow_rays_kernel", "shadow")):
+            if kern in valu:
+                useful[kern] = round(valu[kern]["frac"] * eff[k]["record_loop"], 4)
+    rt_s = s0.ms_raytrace * 1e-3
+    q = lane["path"]["queries"] + lane["shadow"]["queries"]
+    return {"per_frame": lane, "lane_eff": eff, "valu_roofline": valu, "useful_frac": useful,
+            "rays_per_s": round(q / rt_s, 1) if rt_s > 0 else None, "raytrace_stage_ms": round(s0.ms_raytrace, 3)}
+
+
+def extra_legs(eng, res, args):
+    """The legs behind --extras: C3 with NeRF shadows r = 1/4, the reference's own dmrf-compare-abm sweep, the
+    NeRF-dominated views and orbits, and C4's workload on the trained fox field."""
+    from synerfgine_amd import scene as S
+    out = {}
+    try:
+        if args.config == "c3":
+            NW, NH = res["nerf"]
+            out["c3_nerf_shadow_r"] = frame_cells(eng, [{"nerf_shadow_samples": 1}, {"nerf_shadow_samples": 4}], 5, 1, NW * NH)
+            eng.set_param("nerf_shadow_samples", 1)
+    except Exception as e:
+        out["c3_nerf_shadow_r"] = {"error": repr(e)}
+    try:
+        out["abm_sweep"] = abm_sweep(args.model if args.config not in ("c4", "c4fox") else "lego", 3, 1)
+    except Exception as e:
+        out["abm_sweep"] = {"error": repr(e)}
+    try:
+        if os.path.exists(S.LEGO_INGP):
+            out["nerf_views"] = nerf_views("lego", 10, 2, cpu_check=not args.no_cpu_baseline)
+    except Exception as e:
+        out["nerf_views"] = {"error": repr(e)}
+    try:
+        if args.config != "c4fox":
+            out["c4fox"] = c4fox_leg()
+    except Exception as e:
+        out["c4fox"] = {"error": repr(e)}
+    return out
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def compact_line(full):
+    """The one stdout line: the driver contract's keys, `config`, `roofline` (frac, per-launch rows, the uncontended
+    figure, traffic), `cpu_baseline`, `psnr_vs_oracle` and summaries of the BVH and training legs.  Everything else
+    (the extra legs, notes, per-run lists) goes to --extras' file; the line names the committed one of this build.
+    Kept under LINE_MAX_BYTES: optional parts are dropped, least important first, if it would be longer."""
+    line = _pick(full, ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                        "vs_baseline", "dtype", "data"))
+    line["config"] = _pick(full.get("config", {}), ("workload", "width", "height", "nerf_res", "tiles", "step_schedule",
+                                                    "samples_per_frame", "hit_rays"))
+    if "streams" in full:
+        line["streams"] = full["streams"]
+    if full.get("overrides"):
+        line["overrides"] = full["overrides"]
+    line["stages_ms_last_frame"] = full.get("stages_ms_last_frame")
+    rf = full.get("roofline", {})
+    r = _pick(rf, ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source", "traffic_over_algorithmic",
+                   "algorithmic_bytes_per_sample", "avg_launch_ms", "launches", "samples_in_launches", "per_launch", "mfma_frac"))
+    if "field_sample_weighted" in rf:
+        r["field_sample_weighted"] = _pick(rf["field_sample_weighted"], ("frac",))
+    if "onestep_regime" in rf:
+        r["onestep_regime"] = _pick(rf["onestep_regime"], ("ms",))
+    unc = rf.get("uncontended")
+    if isinstance(unc, dict):
+        r["uncontended"] = _pick(unc, ("frac", "source", "frames_per_s", "error"))
+        alt = (unc.get("alternates") or {}).get("hip_events_this_process")
+        if alt:
+            r["uncontended"]["alternates"] = {"hip_events_this_process": _pick(alt, ("frac", "per_launch"))}
+    line["roofline"] = r
+    b = full.get("bvh")
+    if isinstance(b, dict):
+        v = b.get("valu_roofline") or {}
+        line["bvh"] = {"lane_eff": b.get("lane_eff"), "useful_frac": b.get("useful_frac"), "rays_per_s": b.get("rays_per_s"),
+                       "valu_frac": {k: v[k]["frac"] for k in ("raytrace_kernel", "shadow_rays_kernel") if k in v},
+                       "valu_source": v.get("source"), "error": b.get("error")}
+        line["bvh"] = {k: x for k, x in line["bvh"].items() if x is not None}
+    t = full.get("train")
+    if isinstance(t, dict):
+        rl = t.get("roofline") or {}
+        line["train"] = {**_pick(t, ("steps_per_s", "ms_per_step", "measured_batch", "loss_after", "kernel_profile", "error")),
+                         "stage_ms": rl.get("stage_ms"),
+                         "frac": {k: rl[k].get("frac", rl[k].get("frac_min")) for k in ("network", "field", "dw", "optimizer") if k in rl}}
+    cb = full.get("cpu_baseline")
+    if isinstance(cb, dict):
+        c = _pick(cb, ("value", "unit", "cores", "kind", "sample", "cpu_model", "cgroup_cpu_quota", "error"))
+        legs = cb.get("legs") or {}
+        if "one_thread" in legs:
+            c["one_thread_frames_per_s"] = legs["one_thread"]["frames_per_s"]
+        ws = cb.get("benchmarked_workload_sample")
+        if ws:
+            c["benchmarked_workload_sample"] = _pick(ws, ("frames_per_s", "threads", "seconds"))
+        line["cpu_baseline"] = c
+    if "psnr_vs_oracle" in full:
+        line["psnr_vs_oracle"] = _pick(full["psnr_vs_oracle"], ("db", "max_abs", "frac_within_2_255", "res", "error"))
+    line["extras"] = EXTRAS_FILE
+    for drop in (("roofline", "uncontended", "alternates"), ("roofline", "traffic_source"), ("bvh",), ("train", "stage_ms"),
+                 ("stages_ms_last_frame",), ("roofline", "per_launch"), ("data",), ("config", "tiles")):
+        if len(json.dumps(line)) <= LINE_MAX_BYTES:
+            break
+        d = line
+        for k in drop[:-1]:
+            d = d.get(k, {}) if isinstance(d, dict) else {}
+        if isinstance(d, dict):
+            d.pop(drop[-1], None)
+    return line
+
+
+def emit_line(line):
+    """Rank 0's one JSON line, last on stdout (stderr flushed first so nothing interleaves with it)."""
+    sys.stderr.flush()
+    sys.stdout.write(json.dumps(line) + "\n")
+    sys.stdout.flush()
+
+
+def frame_result(args, stats, elapsed, world, res, bounds, comm, overrides, root_gather, on_dev, model_data):
+    """The full result of the timed frames (rank 0): the driver contract's keys, config, and the roofline of the
+    dominant kernel from the frames' own per-launch HIP events and sample counters.  `stats` are sng_frame_result
+    mirrors (attributes only), so the CPU tests build this from stub frames."""
+    # dominant kernel: fused hash-grid + MLP, timed with hipEvents on its own stream over the timed region.
+    # Samples per launch come from the device counter of the network launches (MarchCtrl::net_samples);
+    # the ray-local fused tail (fused.hip) evaluates the rest of the frame's samples inside its own kernel.
+    ms_net = sum(s.ms_network for s in stats)
+    launches = sum(s.network_launches for s in stats)
+    samples = sum(s.n_samples_network for s in stats)
+    total_samples = sum(s.n_samples for s in stats)          # march samples composited
+    reused = sum(s.n_samples_reused for s in stats)         # of which taken from the boundary-sample cache
+    evaluated = total_samples - reused                      # network evaluations (launches + fused tail)
+    spec_evals = sum(s.spec_evals for s in stats)           # speculative tail rounds: samples their network launches evaluated
+    spec_exec = sum(s.spec_exec for s in stats)             # ... of which composited (the rest: look-ahead past a ray's end)
+    msr_evals = sum(s.msr_evals for s in stats)             # multi-step speculative rounds: samples their launches evaluated
+    msr_exec = sum(s.msr_exec for s in stats)               # ... of which the per-iteration wavefront would have evaluated
+    tail_samples = evaluated - (samples - (spec_evals - spec_exec) - (msr_evals - msr_exec))
+    ms_tail = sum(s.ms_fused_tail for s in stats)
+    os_evals = sum(s.onestep_field_evals for s in stats)   # field evaluations inside the one-step regime's final pass
+    ms_os = sum(s.ms_onestep for s in stats)
+    tail_samples -= os_evals
+    avg_launch_ms = ms_net / max(1, launches)
+    per_launch = per_launch_table(stats)
+    bytes_per_launch = samples * BYTES_PER_SAMPLE / max(1, launches)
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    tflops = samples * FLOPS_PER_SAMPLE / (ms_net * 1e-3) / 1e12 if ms_net > 0 else 0.0
+    tail_gbs = tail_samples * BYTES_PER_SAMPLE / (ms_tail * 1e-3) / 1e9 if ms_tail > 0 else 0.0
+    field_ms = ms_net + ms_tail
+    field_gbs = evaluated * BYTES_PER_SAMPLE / (field_ms * 1e-3) / 1e9 if field_ms > 0 else 0.0
+    prof = traffic_profile(args.config, samples / max(1, launches))
+    traffic = None
+    if prof and "refused" not in prof:
+        net_prof = prof["kernels"].get("nerf_network_kernel")
+        traffic = net_prof.get("hbm_bytes_per_launch") if net_prof else None
+
+    fps = args.steps / elapsed
+    s0 = stats[-1]
+    result = {
+        "metric": METRICS[args.config],
+        "value": round(fps, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp16 (hash grid + MLP, MFMA f16->f32), fp32 (marching, compositing, shading)",
+        "data": (f"snapshot {model_data}" +
+                 (" (base.json NeRF L=8,F=4,T=2^19 trained on-GPU by tools/train_lego.py from the reference's lego set, data/nerf/lego400)"
+                  if args.model == "lego" else "") if args.model != "synthetic" else
+                 "synthetic: random-init base.json NeRF (L=8,F=4,T=2^19) with an analytic density (synthetic.py)") +
+                "; scene JSON + OBJ meshes from scenes/ and data/obj/; synthetic frames (fixed camera, accumulation reset every frame)",
+        "config": {"workload": f"{args.config}: " + WORKLOADS[args.config],
+                   "width": res["mesh"][0], "height": res["mesh"][1], "nerf_res": list(res["nerf"]),
+                   "tiles": f"{world} horizontal bands (rows {bounds}) + " +
+                            (("RCCL gather of the RGBA8 bands to rank 0 (sng_gather_rgba8)" if root_gather else
+                              "RCCL all_gather of RGBA8 tiles" if on_dev else "gloo gather of the RGBA8 bands to rank 0 (tiling.gather_to_root)")
+                             if world > 1 else "no gather"),
+                   "step_schedule": "band-local" if (world > 1 and args.local_schedule) else ("frame-wide (per-iteration alive-count all-reduce)" if world > 1 else "frame-wide"),
+                   "samples_per_frame": int(s0.n_samples), "samples_reused_per_frame": int(s0.n_samples_reused),
+                   "reference_slots_per_frame": int(s0.n_reference_slots),
+                   "wavefront_iterations": int(s0.n_iterations), "fused_tail_from_iteration": int(s0.fused_from_iter),
+                   "onestep_regime": [int(s0.onestep_from_iter), int(s0.onestep_iterations)],
+                   "hit_rays": int(s0.n_hit)},
+        "comm": comm,
+        "streams": "serialized (raytracer then NeRF)" if args.serial_streams else
+                   "concurrent (NeRF head alone, then raytracer || NeRF tail; NeRF stream high priority)",
+        "overrides": overrides,
+        "stages_ms_last_frame": {"frame": round(s0.ms_frame, 3), "raytrace": round(s0.ms_raytrace, 3), "nerf": round(s0.ms_nerf, 3),
+                                 "shadow": round(s0.ms_shadow, 3), "overlay": round(s0.ms_overlay, 3)},
+        "temporal_hints": "the speculative NeRF tail sizes each ray's look-ahead by its pixel's ray life in the previous "
+                          "frame (nerf_spec_hint; exact whatever the hint), read only when the frame repeats that frame's view "
+                          "(spec_view_key); the timed frames repeat one camera, so after the first frame the hints are read; "
+                          "nerf_views.c2_orbit_1deg_per_frame / c3_orbit_1deg_per_frame measure a moving camera",
+        "roofline": {"kernel": "nerf_network_kernel<4,1> (fused hash grid + SH + density/rgb MLP)", "bound": "hbm",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "traffic_source": prof["file"] if prof else None,
+                     "traffic_refused": prof.get("refused") if prof else None,
+                     "traffic_over_algorithmic": round(traffic / bytes_per_launch, 4) if traffic and bytes_per_launch else None,
+                     "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
+                     "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches, "samples_in_launches": int(samples),
+                     "per_launch": per_launch,
+                     "timing": "HIP events recorded by each launch's own dispatch (hipExtLaunchKernelGGL start/stop events) on the NeRF stream over the timed region" +
+                               ("" if args.serial_streams else "; the kernel shares the GPU with the raytracer stream, so this is the "
+                                "contended duration (uncontended: --serial-streams)"),
+                     "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / MFMA_F16_PEAK_TFLOPS, 4),
+                     "fused_tail": {"kernel": "nerf_fused_kernel (march + field + composite, ray-local)", "samples": int(tail_samples),
+                                    "ms": round(ms_tail, 4), "achieved": round(tail_gbs, 1), "frac": round(tail_gbs / HBM_PEAK_GBS, 4),
+                                    "timing": "hipEvents around the tail launch (it runs beside the raytracer on reserved CUs in the "
+                                              "concurrent schedule, so its duration is latency, not throughput)"},
+                     "spec_tail": {"kernels": "spec_generate (K iterations marched ahead per ray) + nerf_network_kernel + spec_composite "
+                                              "(exact replay), per round", "rounds_per_frame": int(s0.spec_rounds),
+                                   "samples_evaluated": int(spec_evals), "samples_composited": int(spec_exec),
+                                   "lookahead_discarded_frac": round(1.0 - spec_exec / spec_evals, 4) if spec_evals else 0.0},
+                     "msr_rounds": {"kernels": "msr_generate (K iterations of S steps marched ahead per ray) + nerf_network_kernel + "
+                                               "msr_count (death histogram) + msr_schedule (committed prefix) + msr_commit (exact replay), "
+                                               "while n_steps is 2..7", "rounds_per_frame": int(s0.msr_rounds),
+                                    "samples_evaluated": int(msr_evals), "samples_committed": int(msr_exec),
+                                    "discarded_frac": round(1.0 - msr_exec / msr_evals, 4) if msr_evals else 0.0},
+                     "onestep_regime": {"kernels": "nerf_onestep_kernel x2 + schedule (trace_alt while n_alive > target/2; ray-local, "
+                                                   "periodic rays composited in a closed loop)", "field_evals": int(os_evals),
+                                        "ms": round(ms_os, 4)},
+                     "field_sample_weighted": {"samples": int(evaluated), "ms": round(field_ms + ms_os, 4),
+                                               "achieved": round(evaluated * BYTES_PER_SAMPLE / ((field_ms + ms_os) * 1e-3) / 1e9, 1) if field_ms + ms_os > 0 else 0.0,
+                                               "frac": round(evaluated * BYTES_PER_SAMPLE / ((field_ms + ms_os) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if field_ms + ms_os > 0 else 0.0}},
+    }
+    return result
+
+
 def dry_run(args, rank, world):
     import torch
     import torch.distributed as dist
@@ -658,117 +907,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel: fused hash-grid + MLP, timed with hipEvents on its own stream over the timed region.
-    # Samples per launch come from the device counter of the network launches (MarchCtrl::net_samples);
-    # the ray-local fused tail (fused.hip) evaluates the rest of the frame's samples inside its own kernel.
-    ms_net = sum(s.ms_network for s in stats)
-    launches = sum(s.network_launches for s in stats)
-    samples = sum(s.n_samples_network for s in stats)
-    total_samples = sum(s.n_samples for s in stats)          # march samples composited
-    reused = sum(s.n_samples_reused for s in stats)         # of which taken from the boundary-sample cache
-    evaluated = total_samples - reused                      # network evaluations (launches + fused tail)
-    spec_evals = sum(s.spec_evals for s in stats)           # speculative tail rounds: samples their network launches evaluated
-    spec_exec = sum(s.spec_exec for s in stats)             # ... of which composited (the rest: look-ahead past a ray's end)
-    msr_evals = sum(s.msr_evals for s in stats)             # multi-step speculative rounds: samples their launches evaluated
-    msr_exec = sum(s.msr_exec for s in stats)               # ... of which the per-iteration wavefront would have evaluated
-    tail_samples = evaluated - (samples - (spec_evals - spec_exec) - (msr_evals - msr_exec))
-    ms_tail = sum(s.ms_fused_tail for s in stats)
-    os_evals = sum(s.onestep_field_evals for s in stats)   # field evaluations inside the one-step regime's final pass
-    ms_os = sum(s.ms_onestep for s in stats)
-    tail_samples -= os_evals
-    avg_launch_ms = ms_net / max(1, launches)
-    per_launch = per_launch_table(stats)
-    bytes_per_launch = samples * BYTES_PER_SAMPLE / max(1, launches)
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    tflops = samples * FLOPS_PER_SAMPLE / (ms_net * 1e-3) / 1e12 if ms_net > 0 else 0.0
-    tail_gbs = tail_samples * BYTES_PER_SAMPLE / (ms_tail * 1e-3) / 1e9 if ms_tail > 0 else 0.0
-    field_ms = ms_net + ms_tail
-    field_gbs = evaluated * BYTES_PER_SAMPLE / (field_ms * 1e-3) / 1e9 if field_ms > 0 else 0.0
-    prof = traffic_profile(args.config, samples / max(1, launches))
-    traffic = None
-    if prof and "refused" not in prof:
-        net_prof = prof["kernels"].get("nerf_network_kernel")
-        traffic = net_prof.get("hbm_bytes_per_launch") if net_prof else None
-
-    result = None
+    result, s0 = None, stats[-1]
     if rank == 0:
-        fps = args.steps / elapsed
-        s0 = stats[-1]
-        result = {
-            "metric": METRICS[args.config],
-            "value": round(fps, 3),
-            "unit": "frames/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "fp16 (hash grid + MLP, MFMA f16->f32), fp32 (marching, compositing, shading)",
-            "data": (f"snapshot {os.path.relpath(S.snapshot_path(args.config, args.model), REPO)}" +
-                     (" (base.json NeRF L=8,F=4,T=2^19 trained on-GPU by tools/train_lego.py from the reference's lego set, data/nerf/lego400)"
-                      if args.model == "lego" else "") if args.model != "synthetic" else
-                     "synthetic: random-init base.json NeRF (L=8,F=4,T=2^19) with an analytic density (synthetic.py)") +
-                    "; scene JSON + OBJ meshes from scenes/ and data/obj/; synthetic frames (fixed camera, accumulation reset every frame)",
-            "config": {"workload": f"{args.config}: " + WORKLOADS[args.config],
-                       "width": MW, "height": MH, "nerf_res": list(res["nerf"]),
-                       "tiles": f"{world} horizontal bands (rows {bounds}) + " +
-                                (("RCCL gather of the RGBA8 bands to rank 0 (sng_gather_rgba8)" if root_gather else
-                                  "RCCL all_gather of RGBA8 tiles" if on_dev else "gloo gather of the RGBA8 bands to rank 0 (tiling.gather_to_root)")
-                                 if world > 1 else "no gather"),
-                       "step_schedule": "band-local" if (world > 1 and args.local_schedule) else ("frame-wide (per-iteration alive-count all-reduce)" if world > 1 else "frame-wide"),
-                       "samples_per_frame": int(s0.n_samples), "samples_reused_per_frame": int(s0.n_samples_reused),
-                       "reference_slots_per_frame": int(s0.n_reference_slots),
-                       "wavefront_iterations": int(s0.n_iterations), "fused_tail_from_iteration": int(s0.fused_from_iter),
-                       "onestep_regime": [int(s0.onestep_from_iter), int(s0.onestep_iterations)],
-                       "hit_rays": int(s0.n_hit)},
-            "comm": comm,
-            "streams": "serialized (raytracer then NeRF)" if args.serial_streams else
-                       "concurrent (NeRF head alone, then raytracer || NeRF tail; NeRF stream high priority)",
-            "overrides": overrides,
-            "stages_ms_last_frame": {"frame": round(s0.ms_frame, 3), "raytrace": round(s0.ms_raytrace, 3), "nerf": round(s0.ms_nerf, 3),
-                                     "shadow": round(s0.ms_shadow, 3), "overlay": round(s0.ms_overlay, 3)},
-            "temporal_hints": "the speculative NeRF tail sizes each ray's look-ahead by its pixel's ray life in the previous "
-                              "frame (nerf_spec_hint; exact whatever the hint), read only when the frame repeats that frame's view "
-                              "(spec_view_key); the timed frames repeat one camera, so after the first frame the hints are read; "
-                              "nerf_views.c2_orbit_1deg_per_frame / c3_orbit_1deg_per_frame measure a moving camera",
-            "roofline": {"kernel": "nerf_network_kernel<4,1> (fused hash grid + SH + density/rgb MLP)", "bound": "hbm",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "traffic_source": prof["file"] if prof else None,
-                         "traffic_refused": prof.get("refused") if prof else None,
-                         "traffic_over_algorithmic": round(traffic / bytes_per_launch, 4) if traffic and bytes_per_launch else None,
-                         "algorithmic_bytes_per_sample": BYTES_PER_SAMPLE,
-                         "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches, "samples_in_launches": int(samples),
-                         "per_launch": per_launch,
-                         "timing": "HIP events recorded by each launch's own dispatch (hipExtLaunchKernelGGL start/stop events) on the NeRF stream over the timed region" +
-                                   ("" if args.serial_streams else "; the kernel shares the GPU with the raytracer stream, so this is the "
-                                    "contended duration (uncontended: --serial-streams)"),
-                         "mfma_tflops": round(tflops, 2), "mfma_frac": round(tflops / MFMA_F16_PEAK_TFLOPS, 4),
-                         "fused_tail": {"kernel": "nerf_fused_kernel (march + field + composite, ray-local)", "samples": int(tail_samples),
-                                        "ms": round(ms_tail, 4), "achieved": round(tail_gbs, 1), "frac": round(tail_gbs / HBM_PEAK_GBS, 4),
-                                        "timing": "hipEvents around the tail launch (it runs beside the raytracer on reserved CUs in the "
-                                                  "concurrent schedule, so its duration is latency, not throughput)"},
-                         "spec_tail": {"kernels": "spec_generate (K iterations marched ahead per ray) + nerf_network_kernel + spec_composite "
-                                                  "(exact replay), per round", "rounds_per_frame": int(s0.spec_rounds),
-                                       "samples_evaluated": int(spec_evals), "samples_composited": int(spec_exec),
-                                       "lookahead_discarded_frac": round(1.0 - spec_exec / spec_evals, 4) if spec_evals else 0.0},
-                         "msr_rounds": {"kernels": "msr_generate (K iterations of S steps marched ahead per ray) + nerf_network_kernel + "
-                                                   "msr_count (death histogram) + msr_schedule (committed prefix) + msr_commit (exact replay), "
-                                                   "while n_steps is 2..7", "rounds_per_frame": int(s0.msr_rounds),
-                                        "samples_evaluated": int(msr_evals), "samples_committed": int(msr_exec),
-                                        "discarded_frac": round(1.0 - msr_exec / msr_evals, 4) if msr_evals else 0.0},
-                         "onestep_regime": {"kernels": "nerf_onestep_kernel x2 + schedule (trace_alt while n_alive > target/2; ray-local, "
-                                                       "periodic rays composited in a closed loop)", "field_evals": int(os_evals),
-                                            "ms": round(ms_os, 4)},
-                         "field_sample_weighted": {"samples": int(evaluated), "ms": round(field_ms + ms_os, 4),
-                                                   "achieved": round(evaluated * BYTES_PER_SAMPLE / ((field_ms + ms_os) * 1e-3) / 1e9, 1) if field_ms + ms_os > 0 else 0.0,
-                                                   "frac": round(evaluated * BYTES_PER_SAMPLE / ((field_ms + ms_os) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if field_ms + ms_os > 0 else 0.0}},
-        }
+        result = frame_result(args, stats, elapsed, world, res, bounds, comm, overrides, root_gather, on_dev,
+                              os.path.relpath(S.snapshot_path(args.config, args.model), REPO))
     if rank == 0 and world == 1 and not args.no_sweep:
         # extra legs, after the timed region: the same workload with the two streams serialized (the roofline kernel's
-        # launches then run alone), C3 with NeRF shadows r = 2 (SURVEY §8d reports r = 0 and r = 2), and the
-        # reference's own sweep (BASELINE.md's scene)
+        # launches then run alone), the BVH work of one counting frame, and the training step (config C5)
         if not args.serial_streams:
             try:
                 NW, NH = res["nerf"]
@@ -783,59 +928,20 @@ def main():
                     "frac": round(same["rocprof_frac"], 4) if same and "rocprof_frac" in same else u["network_roofline_frac"],
                     "source": (f"rocprofv3 kernel trace of the driver-format command ({os.path.relpath(chk, REPO)}, tools/gpu.sh profdriver)"
                                if same and "rocprof_frac" in same else "HIP events of this process (no rocprof check of this round)"),
-                    "per_launch": same.get("per_launch") if same else None,
                     "alternates": {"hip_events_this_process": {"frac": u["network_roofline_frac"], "per_launch": u["network_per_launch"]}},
                     "field_sample_weighted_frac": u["field_sample_weighted_frac"],
                     "frames_per_s": u["frames_per_s"],
                     "note": "the same frames with the raytracer and the NeRF serialized (concurrent_streams=0, 10 frames after "
-                            "the timed region): the network launches run alone. The timed line runs the streams concurrently, "
-                            "where the raytracer's persistent grids leave the NeRF stream rt_reserved_cus CUs, so `frac` above "
-                            "is the launches' duration on that share of the GPU; concurrency is the faster frame"}
+                            "the timed region): the network launches run alone"}
             except Exception as e:
                 result["roofline"]["uncontended"] = {"error": repr(e)}
         try:
-            if args.config == "c3":
-                NW, NH = res["nerf"]
-                result["c3_nerf_shadow_r"] = frame_cells(eng, [{"nerf_shadow_samples": 1}, {"nerf_shadow_samples": 4}], 5, 1, NW * NH)
-                eng.set_param("nerf_shadow_samples", 1)
-        except Exception as e:
-            result["c3_nerf_shadow_r"] = {"error": repr(e)}
-        try:
             if args.config in ("c3", "c4"):
-                # one counting frame (rt_count: the path / shadow kernels' counting instantiations, untimed) -> BVH
-                # work per frame; rates over the raytracer stage of the last timed frame
-                eng.set_param("rt_count", 1)
-                eng.frame(spp=0, reset=True)
-                eng.set_param("rt_count", 0)
-                cnt = eng.rt_counters()
-                rt_s = s0.ms_raytrace * 1e-3
-                q = cnt["path"]["queries"] + cnt["shadow"]["queries"]
-                boxes = cnt["path"]["box_tests"] + cnt["shadow"]["box_tests"]
-                tris = cnt["path"]["tri_tests"] + cnt["shadow"]["tri_tests"]
-                result["bvh"] = {"per_frame": cnt, "valu_roofline": valu_profile(args.config),
-                                 "rays_per_s": round(q / rt_s, 1) if rt_s > 0 else None,
-                                 "box_tests_per_s": round(boxes / rt_s, 1) if rt_s > 0 else None,
-                                 "tri_tests_per_s": round(tris / rt_s, 1) if rt_s > 0 else None,
-                                 "raytrace_stage_ms": round(s0.ms_raytrace, 3),
-                                 "note": "rays = BVH world queries (camera + bounce rays of the path kernel, deferred shadow rays); rates "
-                                         "over the raytracer stream's device time of the last timed frame (path + shadow + accumulate "
-                                         "kernels; in the concurrent schedule the NeRF tail shares the GPU)"}
+                result["bvh"] = bvh_leg(eng, args.config, s0)
         except Exception as e:
             result["bvh"] = {"error": repr(e)}
-        try:
-            result["abm_sweep"] = abm_sweep(args.model if args.config not in ("c4", "c4fox") else "lego", 3, 1)
-        except Exception as e:
-            result["abm_sweep"] = {"error": repr(e)}
-        try:
-            if os.path.exists(S.LEGO_INGP):
-                result["nerf_views"] = nerf_views("lego", 10, 2, cpu_check=not args.no_cpu_baseline)
-        except Exception as e:
-            result["nerf_views"] = {"error": repr(e)}
-        try:
-            if args.config != "c4fox":
-                result["c4fox"] = c4fox_leg()
-        except Exception as e:
-            result["c4fox"] = {"error": repr(e)}
+        if args.extras:
+            result.update(extra_legs(eng, res, args))
         try:
             result["train"] = train_leg()
         except Exception as e:
@@ -860,7 +966,11 @@ def main():
                 result["cpu_baseline"]["benchmarked_workload_sample"] = sample
             except Exception as e:
                 result["psnr_vs_oracle"] = {"error": repr(e)}
-        print(json.dumps(result), flush=True)
+        if args.extras:
+            os.makedirs(os.path.dirname(os.path.abspath(args.extras)), exist_ok=True)
+            with open(args.extras, "w") as f:
+                json.dump(result, f, indent=1)
+        emit_line(compact_line(result))
     if world > 1:
         dist.destroy_process_group()
 

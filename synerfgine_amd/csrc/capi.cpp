@@ -265,15 +265,12 @@ struct HostObject {
     std::vector<BvhNode> nodes;
     std::vector<BvhWide> wide;    // traversal layout of `nodes` (wide_bvh), empty if not representable
     int root_ref = 0;
-    std::vector<BvhQuad> quad;    // four-wide layout (quad_bvh), empty if not representable
-    int root_quad = 0;
-    uint32_t quad_stack = 0;      // stack entries its walk can hold at once (push-far-continue-near)
     m3 rot;
     f3 pos;
     float scale = 1.0f;
     int mat = 0;
     ObjAnim anim;
-    DevBuf d_nodes, d_tris, d_trit, d_wide, d_quad;
+    DevBuf d_nodes, d_tris, d_trit, d_wide;
 };
 
 // BvhWide records of the inner nodes of a TriangleBvhNode array (children at left, left + 1).
@@ -305,59 +302,6 @@ bool wide_bvh(const std::vector<BvhNode>& nodes, std::vector<BvhWide>& wide, int
     }
     root_ref = nodes.empty() ? 0 : ref_of(0);
     if (!ok) wide.clear();
-    return ok;
-}
-
-// BvhQuad records (sng_math.h) of a TriangleBvhNode array: one per binary inner node reachable as a quad child (the
-// root, and the inner grandchildren of every record), its children the binary grandchildren where a binary child is
-// inner, else that child itself.  stack_need: the most stack entries the quad walk holds at once -- along a root-to-leaf
-// path every record pushes its other (children - 1) entries before descending.  Returns false when a leaf range does
-// not fit the BvhWide encoding.
-bool quad_bvh(const std::vector<BvhNode>& nodes, std::vector<BvhQuad>& quad, int& root_ref, uint32_t& stack_need) {
-    quad.clear();
-    stack_need = 0;
-    if (nodes.empty()) { root_ref = 0; return true; }
-    bool ok = true;
-    auto leaf_ref = [&](const BvhNode& n) -> int {
-        const int b = -n.left - 1, e = -n.right - 1;
-        if (b < 0 || e < b || (uint32_t)b >= WIDE_MAX_BEGIN || (uint32_t)(e - b) > WIDE_MAX_COUNT) { ok = false; return 0; }
-        if (((uint32_t)b | ((uint32_t)(e - b) << 24)) == 0x7FFFFFFFu) { ok = false; return 0; }
-        return (int)~((uint32_t)b | ((uint32_t)(e - b) << 24));
-    };
-    // build recursively: returns the ref of binary node i and its stack need
-    std::function<int(int, uint32_t&)> build = [&](int i, uint32_t& need) -> int {
-        const BvhNode& n = nodes[i];
-        if (n.left < 0) { need = 0; return leaf_ref(n); }
-        if ((size_t)n.left + 1 >= nodes.size()) { ok = false; need = 0; return 0; }
-        std::vector<int> kids;
-        for (int c = n.left; c <= n.left + 1; ++c) {
-            const BvhNode& cn = nodes[c];
-            if (cn.left >= 0 && (size_t)cn.left + 1 < nodes.size()) { kids.push_back(cn.left); kids.push_back(cn.left + 1); }
-            else kids.push_back(c);
-        }
-        const int id = (int)quad.size();
-        quad.push_back(BvhQuad{});
-        uint32_t sub = 0;
-        int refs[4] = {WIDE_DONE, WIDE_DONE, WIDE_DONE, WIDE_DONE};
-        float box[6][4];
-        for (int k = 0; k < 4; ++k) { box[0][k] = box[2][k] = box[4][k] = 0.0f; box[1][k] = box[3][k] = box[5][k] = 0.0f; }
-        for (size_t k = 0; k < kids.size(); ++k) {
-            const BvhNode& cn = nodes[kids[k]];
-            for (int a = 0; a < 3; ++a) { box[2 * a][k] = cn.lo[a]; box[2 * a + 1][k] = cn.hi[a]; }
-            uint32_t nk = 0;
-            refs[k] = build(kids[k], nk);
-            sub = std::max(sub, nk);
-        }
-        BvhQuad& q = quad[id];   // (quad may have grown)
-        for (int k = 0; k < 4; ++k) {
-            q.lox[k] = box[0][k]; q.hix[k] = box[1][k]; q.loy[k] = box[2][k]; q.hiy[k] = box[3][k]; q.loz[k] = box[4][k]; q.hiz[k] = box[5][k];
-            q.ref[k] = refs[k];
-        }
-        need = (uint32_t)kids.size() - 1u + sub;
-        return id;
-    };
-    root_ref = build(0, stack_need);
-    if (!ok) quad.clear();
     return ok;
 }
 
@@ -400,9 +344,6 @@ const std::map<std::string, double>& default_params() {
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
-        {"bvh_quad", 0},                        // 1: four-wide BvhQuad records and walk in the shadow kernels (exact: the same closest hit);
-                                                //   measured no faster (round 5: shadow rays 1.247 vs 1.251 ms, C3 A/B 295-298 vs 294-295
-                                                //   frames/s; in the path kernel too it lost 2 % to spills), so off -- DESIGN.md §3
         {"bvh_flat", 1},                        // BvhWide walk keeping the nearer child in a register (exact)
         {"rt_tile", 8},                         // path-kernel tile width: 8 (8x8 pixels per wave) or 4 (4x4, shorter chains)
         {"rt_tile_h", 0},                       // path-kernel tile height: 0 = rt_tile; 4 with rt_tile 8: 8x4 (32 lanes per wave)
@@ -634,7 +575,7 @@ struct sng_ctx {
     DevBuf d_objs, d_lights, d_mats;
     DevBuf d_scene_blob;          // every object's nodes + triangles (traversal kernels copy it to LDS)
     uint32_t scene_f4 = 0, bvh_depth = 0;
-    uint32_t bvh_stack = 0;       // stack entries per lane the scene's walks need (depth + 2, or the quad walk's need + 1)
+    uint32_t bvh_stack = 0;       // stack entries per lane the scene's walks need (depth + 2)
     bool scene_dirty = true;
 
     double p(const char* k) const { return params.at(k); }
@@ -879,14 +820,6 @@ void upload_scene(sng_ctx* c) {
             for (int k = 0; k < 3; ++k) max_coord = std::max(max_coord, std::max(std::fabs(n.lo[k]), std::fabs(n.hi[k])));
         g.fast_slab = (c->p("fast_slab") != 0.0 && max_coord < SLAB_FAST_MAX_COORD) ? 1 : 0;
         const bool wide = c->p("bvh_wide") != 0.0 && wide_bvh(o.nodes, o.wide, o.root_ref);
-        const bool quad = wide && c->p("bvh_quad") != 0.0 && quad_bvh(o.nodes, o.quad, o.root_quad, o.quad_stack);
-        if (quad) {   // the shadow kernels' four-wide walk; the path kernel walks the BvhWide records (both in the blob)
-            upload(o.d_quad, o.quad.data(), std::max<size_t>(1, o.quad.size()) * sizeof(BvhQuad));
-            g.quad = o.d_quad.as<BvhQuad>();
-            g.lds_quad = append(o.quad.data(), o.quad.size() * sizeof(BvhQuad));
-            g.root_quad = o.root_quad;
-            c->bvh_stack = std::max(c->bvh_stack, o.quad_stack + 1u);
-        }
         if (wide) {
             upload(o.d_wide, o.wide.data(), std::max<size_t>(1, o.wide.size()) * sizeof(BvhWide));
             g.wide = o.d_wide.as<BvhWide>();
@@ -2046,6 +1979,12 @@ TrainImages train_images(sng_ctx* c) {
 
 // Testbed::reset_network's training state: fp32 master weights from the current model, zeroed
 // optimizer moments, m_rng = pcg32(seed), density_grid_rng = pcg32(m_rng.next_uint()) (testbed.cu:3654-3667)
+// a step generated ahead on s_gen (train_overlap_tail) is discarded: wait for its kernels, then the next step generates
+// its own samples from the current state
+static void train_drop_pregen(sng_ctx::Train& t) {
+    if (t.pregen) { HIPCHK(hipStreamSynchronize(t.s_gen)); t.pregen = false; }
+}
+
 void train_reset(sng_ctx* c, uint64_t seed) {
     if (!c->has_model) throw SngError(SNG_ERR_STATE, "set or load a model before training");
     auto& t = c->tr;
@@ -2070,7 +2009,7 @@ void train_reset(sng_ctx* c, uint64_t seed) {
     t.step = 0; t.grid_ema_step = 0; t.rays_per_batch = 1u << 12; t.measured = 0; t.measured_before = 0;
     t.sched.ensure(sizeof(TrainSched));
     t.sched_dirty = true;
-    if (t.pregen) { HIPCHK(hipStreamSynchronize(t.s_gen)); t.pregen = false; }   // a step generated ahead belongs to the old run
+    train_drop_pregen(t);   // a step generated ahead belongs to the old run
     t.target = (uint32_t)c->p("train_batch");
     const uint32_t target = t.target, max_samples = target * 16;
     t.ctrl.ensure(sizeof(TrainCtrl));
@@ -2252,6 +2191,9 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
         HIPCHK(hipEventCreateWithFlags(&t.ev_gen, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&t.ev_loss, hipEventDisableTiming));
     }
+    // a step generated ahead (train_overlap_tail) is used as is, except under per-stage timing: its generate stage would
+    // have no events, so it is generated again in the timed step (the same samples: same rng, grid and batch sizes)
+    if (timed) train_drop_pregen(t);
     bool generated = t.pregen;
     t.pregen = false;
     train_sched_push(c, s);
@@ -2329,17 +2271,6 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
             ++timed_steps;
         }
     }
-    // tests (train_overlap_tail): the next step generated ahead as in the loop, for the parity hook to check
-    if (overlap && n_steps && c->p("train_overlap_tail") != 0.0) {
-        const uint32_t skip_n = std::min(16u, std::max(1u, t.step / 16u));
-        if (t.step % skip_n != 0) {
-            HIPCHK(hipStreamWaitEvent(t.s_gen, t.ev_loss, 0));
-            train_generate_stage(c, t.rng, t.s_gen);   // t.rng is the next step's stream already
-            HIPCHK(hipEventRecord(t.ev_gen, t.s_gen));
-            HIPCHK(hipStreamWaitEvent(s, t.ev_gen, 0));
-            t.pregen = true;
-        }
-    }
     HIPCHK(hipEventRecord(c->ev_end, s));
     // inference params (EMA) -> the render path's weights and grid
     launch_train_pack(t.p_infer.as<uint16_t>(), c->d_wfrag.as<uint16_t>(), t.wfrag_t.as<uint16_t>(), s);
@@ -2374,6 +2305,18 @@ void train_steps(sng_ctx* c, uint32_t n_steps, sng_train_stats* out) {
         out->timed_steps = timed_steps;
         float* dst[7] = {&out->ms_generate, &out->ms_network, &out->ms_loss, &out->ms_grad_clear, &out->ms_field, &out->ms_dw, &out->ms_optimizer};
         for (int q = 0; q < 7; ++q) *dst[q] = timed_steps ? (float)(stage_ms[q] / timed_steps) : 0.0f;
+    }
+    // tests (train_overlap_tail): the next step generated ahead as in the loop, for the parity hook to check; queued
+    // after the counters above were read back (its generate stage clears the step's control words and losses)
+    if (overlap && n_steps && c->p("train_overlap_tail") != 0.0) {
+        const uint32_t skip_n = std::min(16u, std::max(1u, t.step / 16u));
+        if (t.step % skip_n != 0) {
+            HIPCHK(hipStreamWaitEvent(t.s_gen, t.ev_loss, 0));
+            train_generate_stage(c, t.rng, t.s_gen);   // t.rng is the next step's stream already
+            HIPCHK(hipEventRecord(t.ev_gen, t.s_gen));
+            HIPCHK(hipStreamWaitEvent(s, t.ev_gen, 0));
+            t.pregen = true;
+        }
     }
 }
 
@@ -2684,9 +2627,14 @@ void load_snapshot(sng_ctx* c, const std::string& path) {
         // load_nerf_post: render_lens = metadata[0].lens (testbed_nerf.cu:3051-3052; NerfDataset from_json reads the global
         // "lens" default, then the image's own, json_binding.h:141-160); render_with_lens_distortion is left as it is
         c->render_lens = Lens{};
+        // the legacy key "camera_distortion" overrides "lens" at both levels, as in from_json(NerfDataset)
         if (ds.contains("lens")) c->render_lens = lens_from_json(ds["lens"]);
-        if (ds.contains("metadata") && ds["metadata"].size() > 0 && ds["metadata"][0].contains("lens"))
-            c->render_lens = lens_from_json(ds["metadata"][0]["lens"]);
+        if (ds.contains("camera_distortion")) c->render_lens = lens_from_json(ds["camera_distortion"]);
+        if (ds.contains("metadata") && ds["metadata"].size() > 0) {
+            const JValue& m0 = ds["metadata"][0];
+            if (m0.contains("lens")) c->render_lens = lens_from_json(m0["lens"]);
+            if (m0.contains("camera_distortion")) c->render_lens = lens_from_json(m0["camera_distortion"]);
+        }
     }
     if (snap.contains("up_dir")) c->up = mk(snap["up_dir"][0].as_float(), snap["up_dir"][1].as_float(), snap["up_dir"][2].as_float());
     if (snap.contains("camera")) {
@@ -3069,7 +3017,7 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
             throw SngError(SNG_ERR_INVALID, "tonemap_curve is an ETonemapCurve: 0 Identity, 1 ACES, 2 Hable, 3 Reinhard");
         c->params[k] = v;
         c->mesh_reset = true;
-        if ((k == "fast_slab" || k == "scene_lds" || k == "bvh_wide" || k == "bvh_quad") && !c->objs.empty()) upload_scene(c);
+        if ((k == "fast_slab" || k == "scene_lds" || k == "bvh_wide") && !c->objs.empty()) upload_scene(c);
     });
 }
 int sng_get_param(sng_ctx* c, const char* key, double* v) {
@@ -3375,6 +3323,7 @@ int sng_train_set_dataset(sng_ctx* c, uint32_t n, uint32_t w, uint32_t h, const 
         if (!c || !rgba || !xf || !focal || !pp || !n || !w || !h) throw SngError(SNG_ERR_INVALID, "bad training dataset");
         HIPCHK(hipSetDevice(c->device));
         auto& t = c->tr;
+        train_drop_pregen(t);   // a step generated ahead read the old images: wait for it, then regenerate
         upload(t.pixels, rgba, (size_t)n * w * h * 4);
         upload(t.xforms, xf, (size_t)n * 12 * 4);
         // generate_training_samples_nerf builds rays from get_xform_given_rolling_shutter (common_device.cuh:
@@ -3398,6 +3347,7 @@ int sng_train_set_lens(sng_ctx* c, const sng_lens* lenses, uint32_t n) {
         if (!c) throw SngError(SNG_ERR_INVALID, "null context");
         HIPCHK(hipSetDevice(c->device));
         auto& t = c->tr;
+        train_drop_pregen(t);   // a step generated ahead used the old lenses
         if (!lenses || n == 0) { t.h_lens.clear(); return; }
         if ((int)n != t.n_images) throw SngError(SNG_ERR_INVALID, "one lens per training image (sng_train_set_dataset) expected");
         std::vector<Lens> h(n);

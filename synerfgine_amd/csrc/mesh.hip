@@ -56,9 +56,7 @@ struct PStack {
 // FixedStack<32> overflow rule can never trigger differently).
 // CNT = true (bench's counting frames only, sng_rt_counters): cnt -> this thread's {world queries,
 // box tests, triangle tests}; the timed kernels are the CNT = false instantiations (no counting code).
-// QUAD = true (the shadow kernels): objects with BvhQuad records take the four-wide walk; the path kernel keeps the
-// binary near-walk (it has no registers to spare: the four-wide walk made it spill, round 5)
-template <bool LDS, bool CNT = false, bool QUAD = false>
+template <bool LDS, bool CNT = false>
 struct TraceCtx {
     int* stack;            // this thread's first stack slot
     int stride;
@@ -73,10 +71,6 @@ struct TraceCtx {
     __device__ __forceinline__ const BvhWide* wide(const ObjectGpu& o) const {
         if constexpr (LDS) return reinterpret_cast<const BvhWide*>(scene + o.lds_wide);
         else return o.wide;
-    }
-    __device__ __forceinline__ const BvhQuad* quad(const ObjectGpu& o) const {
-        if constexpr (LDS) return reinterpret_cast<const BvhQuad*>(scene + o.lds_quad);
-        else return o.quad;
     }
     __device__ __forceinline__ const TriT* tris(const ObjectGpu& o) const {
         if constexpr (LDS) return reinterpret_cast<const TriT*>(scene + o.lds_trit);
@@ -279,106 +273,14 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
     return mint;
 }
 
-// The four-wide walk over BvhQuad records (capi.cpp quad_bvh): one record visit tests up to four boxes -- the binary
-// walk's boxes of two consecutive levels -- with the same slab arithmetic (slab_entry_fast / bvh_box_entry per box),
-// sorts them by entry distance, continues with the nearest whose entry is below mint and pushes the other surviving
-// ones far-first (push far, continue near), so it pops them nearest-first.  Leaves run the same triangle test with
-// the strict `t < mint` update.  The result is the minimum t over the triangles whose boxes the culling keeps, the
-// binary walk's closest hit; only the order of the visits differs (a tie in t between two triangles could then pick
-// the other one: tests/test_gpu_parity.py checks whole frames bit for bit against the TriangleBvhNode walk).
-template <bool FAST>
-__device__ __forceinline__ float bvh_walk_quad(f3 ro, f3 rd, f3 y, const BvhQuad* __restrict__ quad, const TriT* __restrict__ tris, int root_ref,
-                                               int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr, bool cw = false) {
-    const float FMAX = 3.402823466e+38f;
-    PStack st{(lds_int*)stack_lds, (lds_int*)stack_lds, stride};
-    float mint = t_max;
-    int shortest = -1;
-    int cur = root_ref;
-    while (true) {
-        while (cur >= 0) {
-            const float4* r = reinterpret_cast<const float4*>(quad + cur);
-            const int4 rf = *reinterpret_cast<const int4*>(r + 6);
-            float d[4];
-            int f[4] = {rf.x, rf.y, rf.z, rf.w};
-            if constexpr (FAST) {
-                // slab_entry_fast of the four boxes, one axis at a time (the same quotients and min / max, which do not
-                // round, so the order of the axes' combination cannot change a bit): 8 running values instead of the
-                // whole record live at once
-                float tn[4], tx[4];
-                auto axis = [&](const float4 lo4, const float4 hi4, float o, float yy, bool first) {
-                    const float lo[4] = {lo4.x, lo4.y, lo4.z, lo4.w}, hi[4] = {hi4.x, hi4.y, hi4.z, hi4.w};
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const pf2 tt = (pf2{lo[k], hi[k]} - o) * yy;
-                        const float mn = fminf(tt.x, tt.y), mx = fmaxf(tt.x, tt.y);
-                        tn[k] = first ? mn : fmaxf(tn[k], mn);
-                        tx[k] = first ? mx : fminf(tx[k], mx);
-                    }
-                };
-                axis(r[0], r[1], ro.x, y.x, true);
-                axis(r[2], r[3], ro.y, y.y, false);
-                axis(r[4], r[5], ro.z, y.z, false);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) d[k] = (f[k] == WIDE_DONE || tn[k] > tx[k]) ? FMAX : tn[k];
-            } else {
-                const float4 lx = r[0], hx = r[1], ly = r[2], hy = r[3], lz = r[4], hz = r[5];
-                const float lxa[4] = {lx.x, lx.y, lx.z, lx.w}, hxa[4] = {hx.x, hx.y, hx.z, hx.w};
-                const float lya[4] = {ly.x, ly.y, ly.z, ly.w}, hya[4] = {hy.x, hy.y, hy.z, hy.w};
-                const float lza[4] = {lz.x, lz.y, lz.z, lz.w}, hza[4] = {hz.x, hz.y, hz.z, hz.w};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float e = bvh_box_entry(aabb{mk(lxa[k], lya[k], lza[k]), mk(hxa[k], hya[k], hza[k])}, ro, y);
-                    d[k] = f[k] == WIDE_DONE ? FMAX : e;
-                }
-            }
-            if (cnt) cnt[1] += cw ? (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id())
-                                  : (uint32_t)((f[0] != WIDE_DONE) + (f[1] != WIDE_DONE) + (f[2] != WIDE_DONE) + (f[3] != WIDE_DONE));
-            // sorting network (0,1) (2,3) (0,2) (1,3) (1,2): ascending entry distance
-            auto cas = [&](int i, int j) {
-                const bool sw = d[j] < d[i];
-                const float di = d[i], dj = d[j];
-                const int fi = f[i], fj = f[j];
-                d[i] = sw ? dj : di; d[j] = sw ? di : dj;
-                f[i] = sw ? fj : fi; f[j] = sw ? fi : fj;
-            };
-            cas(0, 1); cas(2, 3); cas(0, 2); cas(1, 3); cas(1, 2);
-            if (!(d[0] < mint)) {   // nothing in this record survives: next stack entry
-                cur = st.empty() ? WIDE_DONE : st.pop();
-                continue;
-            }
-            if (d[3] < mint) st.push(f[3]);
-            if (d[2] < mint) st.push(f[2]);
-            if (d[1] < mint) st.push(f[1]);
-            cur = f[0];
-        }
-        if (cur == WIDE_DONE) break;
-        const uint32_t e = ~(uint32_t)cur;
-        const int b = (int)(e & (WIDE_MAX_BEGIN - 1u)), end = b + (int)(e >> 24);
-        if (cnt && !cw) cnt[2] += (uint32_t)(end - b);
-        for (int i = b; i < end; ++i) {
-            if (cnt && cw) cnt[2] += (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id());
-            float t;
-            if (tri_hit(tris + i, ro, rd, mint, t)) { mint = t; shortest = i; }
-        }
-        if (st.empty()) break;
-        cur = st.pop();
-    }
-    tri_out = shortest;
-    return mint;
-}
-
 // t_max < MAX_DEPTH culls everything at or beyond t_max (the result is then min(closest, t_max));
 // only the shadow kernel uses it, where any value >= full_dist yields the same mask.
-template <bool LDS, bool CNT = false, bool QUAD = false>
-__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, const TraceCtx<LDS, CNT, QUAD>& cx, int& tri, float t_max = MAX_DEPTH) {
+template <bool LDS, bool CNT = false>
+__device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu& o, const TraceCtx<LDS, CNT>& cx, int& tri, float t_max = MAX_DEPTH) {
     const f3 oro = mul(o.world_to_obj, ro - o.pos);
     const f3 ord = mul(o.world_to_obj, rd);
     const bool fast = o.fast_slab && slab_fast_ok(oro, ord);
     const f3 y = inv(ord);
-    if (QUAD && o.quad) {
-        if (fast) return bvh_walk_quad<true>(oro, ord, y, cx.quad(o), cx.tris(o), o.root_quad, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
-        return bvh_walk_quad<false>(oro, ord, y, cx.quad(o), cx.tris(o), o.root_quad, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
-    }
     if (o.wide && cx.flat) {
         if (fast) return bvh_walk_near<true>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
         return bvh_walk_near<false>(oro, ord, y, cx.wide(o), cx.tris(o), o.root_ref, cx.stack, cx.stride, tri, t_max, CNT ? cx.cnt : nullptr, CNT && cx.cnt_waves);
@@ -392,8 +294,8 @@ __device__ __forceinline__ float object_intersect(f3 ro, f3 rd, const ObjectGpu&
 }
 
 // sng::depth_test_world (common.cu:36-48)
-template <bool LDS, bool CNT = false, bool QUAD = false>
-__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT, QUAD>& cx, int& out_obj,
+template <bool LDS, bool CNT = false>
+__device__ float depth_test_world(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, int& out_obj,
                                   float t_max = MAX_DEPTH) {
     float depth = MAX_DEPTH;
     const f3 off = origin + dir * MIN_DEPTH;
@@ -414,8 +316,8 @@ struct Hit {
 };
 __device__ __forceinline__ f3 tri_normal(const Tri& t) { return normalize(cross(t.b - t.a, t.c - t.a)); }
 // sng::depth_test_world(+HitRecord) (common.cu:50-67)
-template <bool LDS, bool CNT = false, bool QUAD = false>
-__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT, QUAD>& cx, Hit& h) {
+template <bool LDS, bool CNT = false>
+__device__ int depth_test_world_hit(f3 origin, f3 dir, const ObjectGpu* __restrict__ objs, int n_objs, const TraceCtx<LDS, CNT>& cx, Hit& h) {
     const f3 off = origin + dir * MIN_DEPTH;
     if constexpr (CNT) cx.cnt[0] += 1u;
     // only the winner's (object, triangle, t) stay live across the objects' traversals; its record is formed once
@@ -535,8 +437,8 @@ __device__ __forceinline__ void xorwow_skip(Xorwow& r, uint32_t n) {
 // One neighbour's term of shade_with_shadow: shadow_for_px at (pos, nrm); the k-th point light's sample
 // (Light::sample, 3 draws from the pixel's XORWOW state) is lp[k * lp_stride], drawn beforehand in the
 // reference's order by shadow_draw_kernel.
-template <bool LDS, bool QUAD = false>
-__device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx<LDS, false, QUAD>& cx, f3 pos, f3 nrm, const float4* __restrict__ lp,
+template <bool LDS>
+__device__ __forceinline__ float shadow_term(const ShadowArgs& a, const TraceCtx<LDS, false>& cx, f3 pos, f3 nrm, const float4* __restrict__ lp,
                                              size_t lp_stride) {
     float overall = 1.0f;
     int k = 0;
@@ -629,7 +531,7 @@ __global__ __launch_bounds__(1024) void shadow_term_kernel(ShadowArgs a, uint32_
         __syncthreads();
     }
     int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
-    const TraceCtx<LDS, false, true> cx{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat};
+    const TraceCtx<LDS, false> cx{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat};
     const int lane = threadIdx.x & 63;
     const uint32_t slots = (uint32_t)((2 * a.radius + 1) * (2 * a.radius + 1));
     const uint32_t cps = (n + 63u) / 64u, n_chunks = slots * cps;
@@ -723,15 +625,15 @@ __device__ __forceinline__ f3 cone_random_frame(f3 orig, const m3& frame, float 
 //                colour sums in the original order.  Bit-identical to DEFER = false.
 // Dynamic LDS of the traversal kernels: [scene blob (LDS = true)][stack: stack_depth x blockDim ints].
 // Workgroups are persistent (grid-stride), so each copies the scene blob once.
-template <bool LDS, bool CNT = false, bool QUAD = false>
-__device__ __forceinline__ TraceCtx<LDS, CNT, QUAD> trace_ctx_setup(const RaytraceArgs& a, uint32_t* cnt = nullptr) {
+template <bool LDS, bool CNT = false>
+__device__ __forceinline__ TraceCtx<LDS, CNT> trace_ctx_setup(const RaytraceArgs& a, uint32_t* cnt = nullptr) {
     extern __shared__ float4 smem4[];
     if constexpr (LDS) {
         for (uint32_t k = threadIdx.x; k < a.scene_f4; k += blockDim.x) smem4[k] = a.scene_blob[k];
         __syncthreads();
     }
     int* stack = reinterpret_cast<int*>(smem4 + (LDS ? a.scene_f4 : 0u));
-    return TraceCtx<LDS, CNT, QUAD>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt, a.count_waves};
+    return TraceCtx<LDS, CNT>{stack + threadIdx.x, (int)blockDim.x, reinterpret_cast<const char*>(smem4), a.bvh_flat, cnt, a.count_waves};
 }
 
 // shade_object's light loop of one hit (raytracer.cu:16-50) in deferred form: per (light, shadow
@@ -757,8 +659,8 @@ __device__ __forceinline__ void write_light_samples(const RaytraceArgs& a, const
         }
     }
 }
-template <bool LDS, bool CNT, bool QUAD>
-__device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT, QUAD>& cx, uint32_t kr, uint32_t jp);
+template <bool LDS, bool CNT>
+__device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t kr, uint32_t jp);
 
 // Fused shadow queue of a banded frame (rt_fused_shadow; every wave of the path kernel has at most one tile): each
 // record allocation of a path wave is published in its workgroup's LDS queue once its records are written, and the
@@ -1088,8 +990,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
 // depend on its cap syn + 1 >= full_dist), so the result is bit-identical.
-template <bool LDS, bool CNT, bool QUAD>
-__device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT, QUAD>& cx, uint32_t kr, uint32_t jp) {
+template <bool LDS, bool CNT>
+__device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const RtQueue& q, const TraceCtx<LDS, CNT>& cx, uint32_t kr, uint32_t jp) {
     const float4 s1 = *q.shadow_ray(kr, jp);
     const float4* rk = q.rec + (size_t)kr * q.rec_stride;   // the origin: the record's hit position (header)
     const float4 h0 = rk[0], h1 = rk[1];
@@ -1108,7 +1010,7 @@ __device__ __forceinline__ float trace_shadow_ray(const RaytraceArgs& a, const R
 template <bool LDS, bool CNT = false>
 __global__ __launch_bounds__(1024) void shadow_rays_kernel(RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work) {
     uint32_t counts[3] = {0u, 0u, 0u};
-    const TraceCtx<LDS, CNT, true> cx = trace_ctx_setup<LDS, CNT, true>(a, counts);
+    const TraceCtx<LDS, CNT> cx = trace_ctx_setup<LDS, CNT>(a, counts);
     const uint32_t n_rec = *q.count, total = n_rec * q.nps;
     const int lane = threadIdx.x & 63;
     // 64-ray chunks handed out by SHADOW_NCTR counters in separate memory channels: chunk c belongs to

@@ -773,16 +773,6 @@ struct alignas(16) BvhWide {
     int ref0, ref1, pad0, pad1;
     int pad2[4];
 };
-// Four-wide traversal layout of the same tree (capi.cpp quad_bvh): a record per binary inner node whose children are
-// its grandchildren where a child is inner (2-4 children), the boxes stored axis by axis for four slab tests at once,
-// refs as in BvhWide (WIDE_DONE: empty slot).  112 B = seven 16-B loads; the q-th load of record i sits in LDS slot
-// (7 i + q) mod 16, distinct for 16 consecutive records.  The closest hit is the same minimum over the same
-// triangle tests (tests/test_gpu_parity.py checks the frames bit for bit against the TriangleBvhNode walk); only the
-// visiting order, and with it how many boxes the mint culling prunes, differs.
-struct alignas(16) BvhQuad {
-    float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
-    int ref[4];
-};
 constexpr uint32_t WIDE_MAX_BEGIN = 1u << 24, WIDE_MAX_COUNT = 127u;
 constexpr int WIDE_DONE = (int)0x80000000;   // traversal sentinel; wide_bvh never encodes a leaf as ~0x7FFFFFFF
 // Traversal copy of a triangle (capi.cpp upload_scene): a, e1 = b - a, e2 = c - a and n = cross(e1, e2),
@@ -808,9 +798,6 @@ struct ObjectGpu {                                           // ObjectTransform 
     const BvhWide* wide;            // traversal layout (nullptr: walk the TriangleBvhNode array)
     uint32_t lds_wide;              // its byte offset in the scene blob
     int root_ref;                   // stack entry of the root
-    const BvhQuad* quad;            // four-wide traversal layout (param bvh_quad; nullptr: BvhWide / node walk)
-    uint32_t lds_quad;              // its byte offset in the scene blob
-    int root_quad;                  // stack entry of its root
 };
 struct LightGpu { f3 pos; float intensity; float size; int type; };
 struct MaterialGpu { f3 ka, kd, ks; float n, rg, spec_angle; int type; };

@@ -10,9 +10,11 @@
   render path (ground truth for convergence and parity tests without any dataset).
 """
 import ctypes
+import functools
 import json
 import math
 import os
+import re
 
 import numpy as np
 
@@ -94,8 +96,45 @@ def read_lens(j, lens, principal_point, rolling_shutter):
         lens[0] = mode
 
 
+_PI_F = np.float32(3.14159265358979323846)   # PI() (random_val.cuh:28), a float
+
+
+def _tanf(x):
+    """glibc's tanf, the function the reference's host-side loader calls (nerf_loader.cu is host code here)."""
+    global _libm
+    try:
+        f = _libm.tanf
+    except NameError:
+        import ctypes
+        import ctypes.util
+        _libm = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+        _libm.tanf.restype = ctypes.c_float
+        _libm.tanf.argtypes = [ctypes.c_float]
+        f = _libm.tanf
+    return np.float32(f(float(x)))
+
+
 def _fov_to_focal(res, deg):
-    return 0.5 * res / math.tan(0.5 * deg * math.pi / 180.0)
+    """fov_to_focal_length(int, float) (common_device.cuh:618-620) in float: 0.5f * res / tanf(0.5f * deg * PI() / 180.0f)."""
+    f32 = np.float32
+    arg = f32(f32(f32(f32(0.5) * f32(deg)) * _PI_F) / f32(180.0))
+    return float(f32(f32(0.5) * f32(res)) / _tanf(arg))
+
+
+def _natural_cmp(a, b):
+    """SI::natural::compare (natural_sort.hpp, unvendored; nerf_loader.cu:347-349): runs of digits compare as numbers,
+    everything else character by character."""
+    ca, cb = [t for t in re.split(r"(\d+)", a) if t], [t for t in re.split(r"(\d+)", b) if t]
+    for x, y in zip(ca, cb):
+        if x.isdigit() and y.isdigit():
+            if int(x) != int(y):
+                return -1 if int(x) < int(y) else 1
+        elif x != y:
+            return -1 if x < y else 1
+    return (len(ca) > len(cb)) - (len(ca) < len(cb))
+
+
+_natural_key = functools.cmp_to_key(_natural_cmp)
 
 
 def read_focal_length(j, focal, res):
@@ -104,9 +143,10 @@ def read_focal_length(j, focal, res):
         if f"{a}_fov" in j:
             return _fov_to_focal(r, float(j[f"{a}_fov"]))
         if f"fl_{a}" in j:
-            return float(j[f"fl_{a}"])
+            return float(np.float32(j[f"fl_{a}"]))
         if f"camera_angle_{a}" in j:
-            return _fov_to_focal(r, float(j[f"camera_angle_{a}"]) * 180.0 / math.pi)
+            # (float)json["camera_angle_x"] * 180 / PI(): float arithmetic
+            return _fov_to_focal(r, np.float32(np.float32(np.float32(j[f"camera_angle_{a}"]) * np.float32(180)) / _PI_F))
         return 0.0
     x, y = axis(res[0], "x"), axis(res[1], "y")
     if x != 0.0:
@@ -123,13 +163,15 @@ def read_focal_length(j, focal, res):
 def load_nerf(scene_dir, split_json="transforms.json", max_images=None):
     """load_nerf (nerf_loader.cu:272-700) for one transforms file of 8-bit PNG images: scale 0.33 / offset 0.5 unless
     the file gives them, aabb_scale, the lens / principal point / rolling shutter of read_lens (the file's, then each
-    frame's), the focal length of read_focal_length (the file's, then each frame's), frames kept only when their image
+    frame's), the focal length of read_focal_length (the file's, then each frame's), the frames sorted naturally by
+    file_path (nerf_loader.cu:347-349), frames kept only when their image
     exists (the sharpness branch, threshold 0 by default, nerf_loader.cu:364-386), nerf_matrix_to_ngp.
     Returns a dict: images [n,h,w,4] u8, xforms [n,3,4], focal [n,2], pp [n,2], lenses [(mode, params)], aabb_scale,
     scale, offset, paths."""
     with open(os.path.join(scene_dir, split_json)) as f:
         meta = json.load(f)
-    frames = meta["frames"]
+    # the frames in natural order of their file paths, before the n_frames cull and the sharpness filter
+    frames = sorted(meta["frames"], key=lambda fr: _natural_key(fr["file_path"].replace("\\", "/")))
     if "n_frames" in meta:
         frames = frames[: min(len(frames), int(meta["n_frames"]))]
     if frames and "sharpness" in frames[0]:

@@ -320,48 +320,44 @@ def test_record_lists_equal_chain_walk(config, overrides, rows):
 
 @pytest.mark.parametrize("config,overrides", [("c3", {}), ("c3", {"scene_lds": 0}), ("c3", {"rt_wavefront": 0}), ("c4", {})])
 def test_wide_bvh_layout_equals_node_walk(config, overrides):
-    """The BvhWide traversal layout (bvh_wide=1, bvh_quad=0) and the four-wide BvhQuad walk (bvh_quad=1) reproduce
-    the TriangleBvhNode walk bit for bit."""
+    """The BvhWide traversal layout (bvh_wide=1) reproduces the TriangleBvhNode walk bit for bit."""
     tb, eng, _ = _engine(192, 108, overrides, config=config)
     try:
         m0, n0 = eng.rng_states(1).copy(), eng.rng_states(0).copy()
         out = {}
-        for layout, (wide, quad) in {"node": (0, 0), "wide": (1, 0), "quad": (1, 1)}.items():
+        for layout, wide in {"node": 0, "wide": 1}.items():
             eng.set_rng_states(0, n0)
             eng.set_rng_states(1, m0)
             eng.set_param("bvh_wide", wide)
-            eng.set_param("bvh_quad", quad)
             r = eng.frame()
             out[layout] = (r.download("syn_rgba"), r.download("syn_depth"), r.download("final_rgba"), eng.rng_states(1).copy())
-        for layout in ("wide", "quad"):
-            for a, b in zip(out["node"], out[layout]):
-                assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), layout
-        assert (out["quad"][1] < 100).mean() > 0.02    # objects are in view
+        for a, b in zip(out["node"], out["wide"]):
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert (out["wide"][1] < 100).mean() > 0.02    # objects are in view
     finally:
         tb.close()
 
 
-def test_quad_bvh_full_c3_frame_equals_node_walk():
-    """The four-wide walk at C3's full 1920x1080 (about 19 M path queries and 11 M shadow rays per frame, the
-    lego snapshot + armadillo): colour, depth and the XORWOW states it leaves equal the TriangleBvhNode walk's bit for
-    bit -- no tie in t between two triangles picked differently, and no culling difference, over the whole frame."""
+def test_wide_bvh_full_c3_frame_equals_node_walk():
+    """The default traversal (BvhWide records, push far / continue near, the stack top in registers) at C3's full
+    1920x1080 (about 19 M path queries and 11 M shadow rays per frame, the lego snapshot + armadillo): colour, depth and
+    the XORWOW states it leaves equal the TriangleBvhNode walk's bit for bit over the whole frame."""
     from synerfgine_amd import scene as S
     model = "lego" if os.path.exists(S.LEGO_INGP) else "synthetic"
     tb, eng, _ = S.make_engine("c3", model=model)
     try:
         m0, n0 = eng.rng_states(1).copy(), eng.rng_states(0).copy()
         out = {}
-        for layout, (wide, quad) in {"node": (0, 0), "quad": (1, 1)}.items():
+        for layout, wide in {"node": 0, "wide": 1}.items():
             eng.set_rng_states(0, n0)
             eng.set_rng_states(1, m0)
             eng.set_param("bvh_wide", wide)
-            eng.set_param("bvh_quad", quad)
             r = eng.frame()
             out[layout] = (r.download("syn_rgba"), r.download("syn_depth"), r.download("final_rgba"), eng.rng_states(1).copy())
-        for a, b in zip(out["node"], out["quad"]):
+        for a, b in zip(out["node"], out["wide"]):
             diff = int((a.view(np.uint32) != b.view(np.uint32)).sum())
             assert diff == 0, f"{diff} values differ"
-        assert (out["quad"][1] < 100).mean() > 0.02
+        assert (out["wide"][1] < 100).mean() > 0.02
     finally:
         tb.close()
 

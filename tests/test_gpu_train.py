@@ -213,11 +213,12 @@ def test_train_param_gradients(trainer, grid_f16):
     """train_grid_grad_f16 = 1 accumulates the hash-grid gradients in fp16 with packed atomics, as tcnn does (its grad_t
     is the network's __half); the same bound against the float64 reference holds for both."""
     import train_ref as R
+    saved = trainer["eng"].get_param("train_grid_grad_f16")
     trainer["eng"].set_param("train_grid_grad_f16", grid_f16)
     try:
         d = _step_state(trainer, 4)
     finally:
-        trainer["eng"].set_param("train_grid_grad_f16", 0)
+        trainer["eng"].set_param("train_grid_grad_f16", saved)
     net = R.TorchNetwork(trainer["cfg"], d["params"])
     ref = net.param_grads(d["coords_c"], d["dloss"].astype(np.float64))
     got = d["grads"][: len(ref)].astype(np.float64)
@@ -239,11 +240,12 @@ def test_train_adam_ema_matches_oracle(trainer, oracle_lib, grid_f16):
     pre = {k: tb.train_debug(0, k, dt).copy() for k, dt in (("master", np.float32), ("m1", np.float32), ("m2", np.float32),
                                                              ("steps", np.uint32), ("ema", np.float32))}
     step = int(trainer["stats"]["step"])
+    saved = trainer["eng"].get_param("train_grid_grad_f16")
     trainer["eng"].set_param("train_grid_grad_f16", grid_f16)
     try:
         trainer["stats"] = tb.train(1)
     finally:
-        trainer["eng"].set_param("train_grid_grad_f16", 0)
+        trainer["eng"].set_param("train_grid_grad_f16", saved)
     grads = tb.train_debug(0, "grads", np.float32).copy()
     post = {k: tb.train_debug(0, k, dt) for k, dt in (("master", np.float32), ("m1", np.float32), ("m2", np.float32), ("steps", np.uint32),
                                                       ("ema", np.float32))}
@@ -258,6 +260,7 @@ def test_train_converges(trainer):
     """Loss falls and a held-in view renders with PSNR > 20 dB after a short run (lego400, 8 views)."""
     import math
     tb, eng = trainer["tb"], trainer["eng"]
+    assert eng.get_param("train_grid_grad_f16") == 1   # the shipped default: fp16 packed-atomic grid gradients
     st = tb.train(300)
     assert np.isfinite(st["loss"]) and st["loss"] < 0.01, st
     eng.init(200, 200)
