@@ -42,12 +42,16 @@ WORKLOADS = {
     "c4fox": "C4's workload on a trained cascaded field: the reference's real fox capture (aabb_scale 4, 3 cascades, cone stepping, "
              "trained here by tools/train_fox.py) + bunny/rock/box (scenes/fox-rocks.json: kitchen-rocks.json's meshes, materials and "
              "rendering keys), light_samples 4, nerf_shadow_samples 4",
+    "foxarm": "the reference's own scene for its fox capture (scenes/fox-armadillo.json = scripts/virtual_desc/fox-armadillo.json): "
+              "trained fox .ingp (aabb_scale 4, 3 cascades, cone stepping) + bunny + armadillo, a point and a directional light, "
+              "light_samples 8, path_trace_depth 2, nerf_on_nerf_shadow_threshold 0.942",
 }
 METRICS = {
     "c2": "rendered frames/sec at 800x800 (lego .ingp, NeRF only); PSNR vs ref",
     "c3": "rendered frames/sec at 1920\u00d71080 (lego .ingp + 1 mesh); PSNR vs ref",   # BASELINE.json's metric, verbatim
     "c4": "rendered frames/sec at 1920x1080 (kitchen-like .ingp + 3 meshes, light_samples 4); PSNR vs ref",
     "c4fox": "rendered frames/sec at 1920x1080 (trained fox .ingp + 3 meshes, light_samples 4); PSNR vs ref",
+    "foxarm": "rendered frames/sec at 1920x1080 (trained fox .ingp + fox-armadillo.json); PSNR vs ref",
 }
 
 
@@ -56,7 +60,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c4fox"])
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c4fox", "foxarm"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true", help="skip every leg after the timed region (serialized roofline, BVH "
                                                             "counters, training)")
@@ -425,7 +429,7 @@ def orbit_leg(config, w, h, model, warmup, n=60):
         tb.close()
 
 
-def c4fox_leg(frames=10, warmup=2):
+def c4fox_leg(frames=10, warmup=2, config="c4fox"):
     """C4's workload on a trained cascaded field (config c4fox: the reference's fox capture trained by tools/train_fox.py,
     scenes/fox-rocks.json) at 1920x1080: frames/s, the network launches' per-launch roofline, and the march schedule of
     the frame (trace_alt's one-step regime length, multi-step rounds, how many rays are still alive at the regime's end and
@@ -437,12 +441,13 @@ def c4fox_leg(frames=10, warmup=2):
     from synerfgine_amd import scene as S
     if not os.path.exists(S.FOX_INGP):
         return {"error": "data/fox.ingp not present"}
-    tb, eng, _ = S.make_engine("c4fox", model="fox")
+    tb, eng, _ = S.make_engine(config, model="fox")
     try:
         res = eng.resolution()
         NW, NH = res["nerf"]
         px = NW * NH
-        cells = frame_cells(eng, [{}, {"nerf_onestep": 0}, {"nerf_onestep": 1, "nerf_msr": 0}, {"nerf_onestep": 1, "nerf_msr": 1}], frames, warmup, px)
+        variants = [{}, {"nerf_onestep": 0}, {"nerf_onestep": 1, "nerf_msr": 0}, {"nerf_onestep": 1, "nerf_msr": 1}] if config == "c4fox" else [{}]
+        cells = frame_cells(eng, variants, frames, warmup, px)
         base = cells[0]
         eng.set_param("march_log", 1)
         r = eng.frame(spp=0, reset=True)
@@ -450,7 +455,7 @@ def c4fox_leg(frames=10, warmup=2):
         eng.set_param("march_log", 0)
         alive = log[:, 0].astype(np.int64)
         os_end = r.onestep_from_iter + r.onestep_iterations
-        out = {"workload": WORKLOADS["c4fox"], "snapshot": os.path.relpath(S.FOX_INGP, REPO), "res": [NW, NH],
+        out = {"workload": WORKLOADS[config], "snapshot": os.path.relpath(S.FOX_INGP, REPO), "res": [NW, NH],
                "frames_per_s": base["frames_per_s"], "ms_frame_device": base["ms_frame_device"], "samples_per_px": base["samples_per_px"],
                "reference_slots_per_px": base["reference_slots_per_px"], "hit_frac": base["hit_frac"],
                "network_roofline_frac": base["network_roofline_frac"], "network_per_launch": base["network_per_launch"],
@@ -461,10 +466,11 @@ def c4fox_leg(frames=10, warmup=2):
                             "alive_frac_after_onestep_regime": round(float(alive[os_end]) / px, 5) if os_end < len(alive) else 0.0,
                             "rays_reaching_march_iter": int(alive[-1]) if r.n_iterations >= 10000 else 0,
                             "note": "alive = rays of the iteration (per-iteration march log); a ray still alive at MARCH_ITER (10000) "
-                                    "is a nearly transparent one, the kind that makes 97 % of the synthetic C4 frame's work"},
-               "optimisations": {"onestep_regime_off": {k: cells[1][k] for k in ("frames_per_s", "ms_frame_device", "network_roofline_frac")},
-                                 "msr_rounds_off": {k: cells[2][k] for k in ("frames_per_s", "ms_frame_device", "network_roofline_frac")},
-                                 "default_again": {k: cells[3][k] for k in ("frames_per_s", "ms_frame_device")}}}
+                                    "is a nearly transparent one, the kind that makes 97 % of the synthetic C4 frame's work"}}
+        if config == "c4fox":
+            out["optimisations"] = {"onestep_regime_off": {k: cells[1][k] for k in ("frames_per_s", "ms_frame_device", "network_roofline_frac")},
+                                    "msr_rounds_off": {k: cells[2][k] for k in ("frames_per_s", "ms_frame_device", "network_roofline_frac")},
+                                    "default_again": {k: cells[3][k] for k in ("frames_per_s", "ms_frame_device")}}
         return out
     finally:
         tb.close()
@@ -581,7 +587,7 @@ def extra_legs(eng, res, args):
     except Exception as e:
         out["c3_nerf_shadow_r"] = {"error": repr(e)}
     try:
-        out["abm_sweep"] = abm_sweep(args.model if args.config not in ("c4", "c4fox") else "lego", 3, 1)
+        out["abm_sweep"] = abm_sweep(args.model if args.config not in ("c4", "c4fox", "foxarm") else "lego", 3, 1)
     except Exception as e:
         out["abm_sweep"] = {"error": repr(e)}
     try:
@@ -589,11 +595,12 @@ def extra_legs(eng, res, args):
             out["nerf_views"] = nerf_views("lego", 10, 2, cpu_check=not args.no_cpu_baseline)
     except Exception as e:
         out["nerf_views"] = {"error": repr(e)}
-    try:
-        if args.config != "c4fox":
-            out["c4fox"] = c4fox_leg()
-    except Exception as e:
-        out["c4fox"] = {"error": repr(e)}
+    for cfg in ("c4fox", "foxarm"):
+        try:
+            if args.config != cfg:
+                out[cfg] = c4fox_leg(config=cfg)
+        except Exception as e:
+            out[cfg] = {"error": repr(e)}
     return out
 
 
@@ -828,7 +835,7 @@ def main():
         k, v = kv.split("=", 1)
         overrides[k] = float(v)
     if args.model is None:
-        args.model = "fox" if args.config == "c4fox" else "lego" if (args.config != "c4" and os.path.exists(S.LEGO_INGP)) else "synthetic"
+        args.model = "fox" if args.config in ("c4fox", "foxarm") else "lego" if (args.config != "c4" and os.path.exists(S.LEGO_INGP)) else "synthetic"
     tb, eng, eng_cfg = S.make_engine(args.config, device_id=dev_id, overrides=overrides, model=args.model)
     res = eng.resolution()
     MW, MH = res["mesh"]
@@ -948,7 +955,7 @@ def main():
             result["train"] = {"error": repr(e)}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         try:
-            legs, threads = cpu_baseline_c1(args.model if args.config not in ("c4", "c4fox") else "lego", args.cpu_runs)
+            legs, threads = cpu_baseline_c1(args.model if args.config not in ("c4", "c4fox", "foxarm") else "lego", args.cpu_runs)
             best = legs[threads]
             result["cpu_baseline"] = {
                 "value": best["frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",

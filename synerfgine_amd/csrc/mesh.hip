@@ -134,6 +134,9 @@ __device__ __forceinline__ void flush_counts(unsigned long long* dst, const uint
 // 1.0f / x correctly rounded for every x: recip_rn (sng_math.h) in its range 2^-126 <= |x| < 2^126, the
 // IEEE division for the rest (zero, denormals, results that would be denormal, inf, NaN).
 __device__ __forceinline__ float rcp_exact(float x) {
+#ifdef RT_RCP_FAST
+    return __builtin_amdgcn_rcpf(x);   // A/B build only: the fast-math division's bare reciprocal (1 ulp)
+#endif
     const float ax = fabsf(x);
     if (ax >= 0x1p-126f && ax < 0x1p126f) return recip_rn(x);
     return 1.0f / x;

@@ -19,6 +19,10 @@ CONFIGS = {
     # the reference's real fox capture (aabb_scale 4, OpenCV lens) trained by tools/train_fox.py, camera and object
     # placement of scenes/fox-rocks.json (kitchen-rocks.json's rendering block, materials and meshes)
     "c4fox": dict(scene="fox-rocks.json", width=1920, height=1080, overrides={"light_samples": 4}),
+    # the reference's own scene for the fox capture (scripts/virtual_desc/fox-armadillo.json, copied unmodified): its
+    # camera in the fox frame, a point light + a directional light, bunny + armadillo, nerf_on_nerf_shadow_threshold
+    # 0.942, light_samples 8 -- rendered on the trained fox snapshot
+    "foxarm": dict(scene="fox-armadillo.json", width=1920, height=1080, overrides={}),
     # the scene of every reference measurement in BASELINE.md (scripts/render/profiling.sh:12-18): lego +
     # armadillo/bunny/monkey at 1280x720, swept over --sshadows/--nshadows in {1,2,4,8}
     "abm": dict(scene="dmrf-compare-abm.json", width=1280, height=720, overrides={}),
@@ -30,16 +34,18 @@ LEGO_INGP = os.path.join(REPO, "data", "lego.ingp")
 # the trained fox snapshot (tools/train_fox.py on data/nerf/fox270, the reference's fox capture); config c4fox
 FOX_INGP = os.path.join(REPO, "data", "fox.ingp")
 
+FOX_CONFIGS = ("c4fox", "foxarm")
+
 _MODEL_CACHE = {}
 
 
 def snapshot_path(config, model):
     """.ingp path a (config, model) pair renders, or None for the synthetic content."""
     if model in (None, "synthetic"):
-        if config == "c4fox":
-            raise ValueError("c4fox renders the trained fox snapshot (data/fox.ingp)")
+        if config in FOX_CONFIGS:
+            raise ValueError(f"{config} renders the trained fox snapshot (data/fox.ingp)")
         return None
-    if model == "fox" or (config == "c4fox" and model in ("lego", "default")):
+    if model == "fox" or (config in FOX_CONFIGS and model in ("lego", "default")):
         return FOX_INGP
     if model == "lego":
         if config == "c4":

@@ -12,6 +12,8 @@
 #   sq[:CFG[:ARGS]]        SQ_INSTS_* + SQ_WAVE_CYCLES pass with kernel trace + tools/sq_summary.py (VALU roofline)
 #   ab:CFG:PAIRS:A/B       PAIRS alternating bench.py runs of two settings (A, B: KEY=V[,KEY=V...], '-' for the defaults),
 #                          then tools/bsum.py over the logs (replaces round 4's one-off ab_r04*.sh scripts)
+#   abl:CFG:PAIRS:A/B      as ab, but A and B are library builds (synerfgine_amd/_build_A, e.g. make BUILD=_build_x EXTRA=-D...;
+#                          '-' for the default _build), loaded with SNG_LIB_PATH
 #   sqpy:SCRIPT[:ARGS]     the sq pass over python3 tools/SCRIPT ARGS
 #   py:SCRIPT[:ARGS]       python3 tools/SCRIPT ARGS
 #   profpy:SCRIPT[:ARGS]   rocprofv3 --kernel-trace --stats of python3 tools/SCRIPT ARGS (+ kernel table)
@@ -98,6 +100,18 @@ for step in "$@"; do
         done
       done
       [ $rc -eq 0 ] && python3 tools/bsum.py $OUT/ab$n.*.log | tee $log ;;
+    abl)
+      IFS=: read -r cfg pairs spec <<< "$rest"
+      rc=0
+      for i in $(seq 1 ${pairs:-4}); do
+        for side in A B; do
+          [ $side = A ] && b=${spec%%/*} || b=${spec#*/}
+          [ "$b" = "-" ] && b=_build
+          SNG_LIB_PATH=synerfgine_amd/$b/libsng_hip.so timeout -k 10 600 python3 -u bench.py --config ${cfg:-c3} --no-cpu-baseline --no-sweep > $OUT/abl$n.$side.$i.log 2>&1
+          rc=$?; [ $rc -ne 0 ] && break 2
+        done
+      done
+      [ $rc -eq 0 ] && python3 tools/bsum.py $OUT/abl$n.*.log | tee $log ;;
     sqpy)
       # the SQ pass over python3 tools/SCRIPT ARGS (e.g. train_bench.py) + tools/sq_summary.py
       d=$OUT/sq$n
