@@ -356,7 +356,10 @@ const std::map<std::string, double>& default_params() {
         {"rt_fused_shadow", 1},                 // banded frames: the path kernel's idle waves trace the shadow rays (mesh.hip fq_consume)
         {"rt_fused_tiles_per_wave", 1},         // ... when the band has at most this many path tiles per wave (a full queue is traced in place)
         {"rt_fused_shadow_used", 0},            // (output) 1 when the last frame's path kernel traced its shadow rays itself
-        {"rt_spread", 1},                       // the path kernel's first tiles dealt across all CUs (costliest one per CU / SIMD)
+        {"rt_spread", 1},
+        {"rt_rng", 0},                          // 1: a measurement mode, NOT the reference's RNG order -- each (pixel, sample) its own XORWOW
+                                                //   subsequence, a pixel's samples traced on adjacent lanes (raytrace_sp_kernel); same
+                                                //   expectation, other noise (tests/test_gpu_rt_rng.py); for the band-scaling question                       // the path kernel's first tiles dealt across all CUs (costliest one per CU / SIMD)
         {"nerf_gbuffer", 0},                    // 1: NeRF normals every frame (otherwise only when shadow_on_nerf needs them)
         {"rt_plist", 1},                        // per-pixel hit-record lists for the colour replay (rt_accumulate_kernel)
         {"glow_mode", 0},                       // Testbed::Nerf::glow_mode (testbed.h:871): bits 1 green grid, 2 cut line, 4 mask to alpha,
@@ -523,6 +526,8 @@ struct sng_ctx {
     uint64_t rt_tile_key = 0;             // band geometry the costs belong to
 
     DevBuf rng_nerf, rng_mesh;
+    DevBuf rng_mesh_sp;            // rt_rng = 1: one XORWOW stream per (pixel, light sample), [6][n_px * samples]
+    uint64_t rng_sp_key = 0;
     uint32_t n_rng_nerf = 0, n_rng_mesh = 0;
     DevBuf d_seq;
     MarchCtrl* h_ctrl = nullptr;
@@ -1866,7 +1871,27 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                                       lds_need <= 160u * 1024u ? 1 : 0;
                     c->params["rt_fused_shadow_used"] = ra.fused_shadow;
                 }
-                launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh,
+                uint32_t* rng = c->rng_mesh.as<uint32_t>();
+                uint32_t n_rng = c->n_rng_mesh;
+                if (c->p("rt_rng") != 0.0) {   // per-(pixel, sample) streams, the sample-parallel path kernel
+                    if (!q.plist || ra.counts || ra.bounces > RT_SP_MAX_BOUNCES || ra.samples < 1 || ra.samples > 64)
+                        throw SngError(SNG_ERR_INVALID, "rt_rng 1 needs the record lists (rt_plist), no counting frame, path_trace_depth <= 4 "
+                                                        "and 1..64 light_samples");
+                    const uint64_t n_sp = (uint64_t)MW * MH * ra.samples;
+                    if (n_sp >= (1ull << 32)) throw SngError(SNG_ERR_INVALID, "rt_rng 1: too many (pixel, sample) streams");
+                    const uint64_t key = n_sp ^ ((uint64_t)ra.samples << 40);
+                    if (key != c->rng_sp_key) {   // curand_init(1999, pixel * samples + s, 0)
+                        c->rng_mesh_sp.ensure(n_sp * 24);
+                        launch_xorwow_init((uint32_t)n_sp, PT_SEED, c->d_seq.as<uint32_t>(), c->rng_mesh_sp.as<uint32_t>(), c->s_rt);
+                        c->rng_sp_key = key;
+                    }
+                    rng = c->rng_mesh_sp.as<uint32_t>();
+                    n_rng = (uint32_t)n_sp;
+                    ra.sample_par = 1;
+                    ra.fused_shadow = 0;
+                    c->params["rt_fused_shadow_used"] = 0;
+                }
+                launch_raytrace_wavefront(ra, q, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), rng, n_rng,
                                           c->acc_rgba.as<float4>(), c->acc_depth.as<float>(), sb, c->s_rt);
             } else {
                 launch_raytrace(ra, c->mesh_o.as<float4>(), c->mesh_d.as<float4>(), c->rng_mesh.as<uint32_t>(), c->n_rng_mesh, c->acc_rgba.as<float4>(),
@@ -2402,7 +2427,7 @@ void ctx_destroy(sng_ctx* c) {
     for (auto& o : c->objs) { o.d_nodes.release(); o.d_tris.release(); o.d_trit.release(); o.d_wide.release(); }
     for (DevBuf* b : {&c->d_wfrag, &c->d_grid, &c->d_levels, &c->d_bitfield, &c->d_occ_linear, &c->d_grid_f16, &c->d_grid_f32, &c->d_partial, &c->d_mean, &c->nerf_rgba,
                       &c->nerf_depth, &c->nerf_pos, &c->nerf_nrm, &c->samp, &c->coords, &c->net_out, &c->ctrl, &c->mesh_o, &c->mesh_d, &c->acc_rgba,
-                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_lc, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rng_nerf, &c->rng_mesh, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
+                      &c->acc_depth, &c->final_rgba, &c->final_depth, &c->rt_rec, &c->rt_lc, &c->rt_srec, &c->rt_mask, &c->rt_head, &c->rt_plist, &c->rt_pcount, &c->rt_rval, &c->rt_count, &c->rt_work, &c->rt_tile_cost, &c->rt_tile_order, &c->fused_work, &c->rng_nerf, &c->rng_mesh, &c->rng_mesh_sp, &c->d_seq, &c->d_objs, &c->d_lights, &c->d_mats, &c->d_scene_blob,
                       &c->os_hist, &c->os_state, &c->d_occ_brick, &c->d_occ_brick_aux, &c->rt_counts, &c->spec_t, &c->tail_live, &c->sched_hint, &c->msr_hist, &c->march_log, &c->spec_pre, &c->spec_pre_depth, &c->band_rgba8, &c->display_rgb})
         b->release();
     for (int b = 0; b < 2; ++b) { c->ray_ot[b].release(); c->ray_di[b].release(); c->ray_rgba[b].release(); c->ray_depth[b].release(); c->ray_mw[b].release(); c->ray_lt[b].release(); c->ray_lo[b].release(); c->ray_kk[b].release(); }
@@ -3017,6 +3042,7 @@ int sng_set_param(sng_ctx* c, const char* key, double v) {
             throw SngError(SNG_ERR_INVALID, "tonemap_curve is an ETonemapCurve: 0 Identity, 1 ACES, 2 Hable, 3 Reinhard");
         c->params[k] = v;
         c->mesh_reset = true;
+        if (k == "rt_rng") c->rng_sp_key = 0;   // (re)setting it re-seeds the per-(pixel, sample) streams at the next frame
         if ((k == "fast_slab" || k == "scene_lds" || k == "bvh_wide") && !c->objs.empty()) upload_scene(c);
     });
 }

@@ -6,6 +6,11 @@
 // raytrace and overlay_nerf (synerfgine/raytracer.cu:6-258), and init_rand_state
 // (synerfgine/common.cu:22-26, cuRAND XORWOW seeding restated).
 //
+// Arithmetic: this file is compiled with FMA contraction (-ffp-contract=on, Makefile) and the triangle test's
+// division is the hardware reciprocal -- the reference's --use_fast_math model (CMakeLists.txt:82: nvcc contracts
+// a * b + c and turns x / y into rcp.approx); the NeRF marcher and its schedule (nerf.hip, fused.hip) stay IEEE.
+// The overlay / tonemap, compared bit for bit with the oracle, live in overlay.hip (no contraction).
+//
 // BVH traversal keeps its 32-entry stack in LDS, interleaved by thread
 // ([depth][thread]) so a wave's pushes/pops at equal depth hit 64 distinct
 // banks.  Each pixel keeps its own XORWOW stream in SoA registers for the whole
@@ -131,22 +136,18 @@ __device__ __forceinline__ void flush_counts(unsigned long long* dst, const uint
 // formed first and u, v only when t can win.  The accept set is unchanged: the reference replaces
 // a rejected t by FLT_MAX, which never passes `t < mint` (mint <= MAX_DEPTH), and a NaN t fails
 // both forms; u, v are evaluated with the reference's expressions and comparisons.
-// 1.0f / x correctly rounded for every x: recip_rn (sng_math.h) in its range 2^-126 <= |x| < 2^126, the
-// IEEE division for the rest (zero, denormals, results that would be denormal, inf, NaN).
-__device__ __forceinline__ float rcp_exact(float x) {
-#ifdef RT_RCP_FAST
-    return __builtin_amdgcn_rcpf(x);   // A/B build only: the fast-math division's bare reciprocal (1 ulp)
-#endif
-    const float ax = fabsf(x);
-    if (ax >= 0x1p-126f && ax < 0x1p126f) return recip_rn(x);
-    return 1.0f / x;
-}
 __device__ __forceinline__ bool tri_hit(const TriT* tp, f3 ro, f3 rd, float mint, float& t_out) {
     const float4* p4 = reinterpret_cast<const float4*>(tp);
     const float4 w0 = p4[0], w1 = p4[1], w2 = p4[2];
     const f3 v1v0 = mk(w0.w, w1.x, w1.y), v2v0 = mk(w1.z, w1.w, w2.x), n = mk(w2.y, w2.z, w2.w);
     const f3 rov0 = ro - mk(w0.x, w0.y, w0.z);
-    const float d = rcp_exact(dot(rd, n));
+    // 1.0f / dot(rd, n) as the reference's --use_fast_math build evaluates it (CMakeLists.txt:82: a division becomes
+    // rcp.approx), the hardware reciprocal v_rcp_f32 (1 ulp)
+#ifdef RT_TRI_RCP_EXACT   // A/B builds of the IEEE model (make MESH_EXTRA="-ffp-contract=off -DRT_TRI_RCP_EXACT")
+    const float d = 1.0f / dot(rd, n);
+#else
+    const float d = __builtin_amdgcn_rcpf(dot(rd, n));
+#endif
     const float t = d * -dot(n, rov0);
     if (!(t >= 0.0f && t < mint)) return false;
     const f3 q = cross(rov0, rd);
@@ -989,6 +990,90 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
     if constexpr (CNT) flush_counts(a.counts, counts, lane);
 }
 
+// ---------------------------------------------------------------------------------------------
+// rt_rng = 1: a measurement mode, off by default and NOT the reference's RNG order.  Each (pixel,
+// light sample) draws from its own XORWOW subsequence, curand_init(1999, pixel * S + s, 0) (the same seeding, another
+// subsequence per sample), so the S samples of a pixel are independent and trace on S adjacent lanes at once: a wave
+// holds 64 / S pixels, and the dependent chain of a unit is one sample's bounces instead of a pixel's S samples in
+// turn.  Everything after the path kernel is unchanged: the records carry their sample index, each pixel's record
+// list is written in (sample, bounce) order, so shadow_rays_kernel, rt_record_colour_kernel and rt_accumulate_kernel
+// sum the same terms as for a serial pixel; the bounce-0 positions (the depth) are summed in sample order.  The frame
+// agrees with the reference's in distribution, not bit for bit (tests/test_gpu_rt_rng.py).
+// ---------------------------------------------------------------------------------------------
+template <bool LDS>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_PER_EU))) void raytrace_sp_kernel(
+    RaytraceArgs a, RtQueue q, uint32_t* __restrict__ work, const float4* __restrict__ origins, const float4* __restrict__ dirs,
+    uint32_t* __restrict__ rng, uint32_t n_rng, float* __restrict__ acc_depth) {
+    if (a.started && threadIdx.x == 0) __hip_atomic_store(a.started, a.started_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const TraceCtx<LDS, false> cx = trace_ctx_setup<LDS, false>(a);
+    const int lane = threadIdx.x & 63;
+    const uint32_t S = a.samples, ppw = 64u / S;                     // pixels per wave (1 <= S <= 64)
+    const uint32_t n_px = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W, n_units = (n_px + ppw - 1u) / ppw;
+    const uint32_t sub = (uint32_t)lane / S, s = (uint32_t)lane % S, g0 = sub * S;   // lane -> (pixel of the unit, sample)
+    while (true) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(work, 1u);
+        k = __shfl(k, 0, 64);
+        if (k >= n_units) break;
+        const uint32_t t = k * ppw + sub;
+        const bool active = sub < ppw && t < n_px;
+        const size_t i = (size_t)a.row0 * a.W + (active ? t : 0u);
+        f3 p0 = splat(0.0f), src_p = splat(0.0f), src_d = splat(0.0f);
+        uint32_t nh = 0;
+        int recs[RT_SP_MAX_BOUNCES];
+        if (active) {
+            Xorwow r = load_rng(rng, n_rng, i * S + s);
+            const float4 o4 = origins[i], d4 = dirs[i];
+            src_p = mk(o4.x, o4.y, o4.z);
+            src_d = mk(d4.x, d4.y, d4.z);
+            // raytrace_pixel's sample loop body for sample s (raytracer.cu:101-218), deferred shading
+            const float longi = curand_uniform(r) * a.lens;
+            const float latid = a.lens != 0.0f ? 0.0f : (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+            f3 rp = src_p, rd = cone_random_up(src_d, a.up, longi, latid);
+            float pdf = 1.0f / (float)a.bounces, att = 1.0f;
+            for (uint32_t bounce = 0; bounce < a.bounces; ++bounce) {
+                Hit h;
+                const int hit_obj = depth_test_world_hit(rp, rd, a.objs, a.n_objs, cx, h);
+                if (!bounce) p0 = h.pos;
+                if (hit_obj < 0) break;
+                const MaterialGpu m = a.mats[h.mat];
+                const uint32_t kr = wave_alloc(q.count, lane);
+                recs[nh < RT_SP_MAX_BOUNCES ? nh : 0] = (int)kr;
+                ++nh;
+                write_record_header(q.rec + (size_t)kr * q.rec_stride, -1, s, h.mat, h.pos, pdf, att);
+                write_light_samples(a, q, kr, h.pos, h.normal, rd, m, r);
+                const float spec = m.type == 0 ? PI_F / 2 : m.spec_angle;
+                const float lo = curand_uniform(r) * spec;
+                const float la = (float)((double)curand_uniform(r) * 2.0 * (double)PI_F);
+                rd = cone_random_frame(h.normal, h.perturb, lo, la);
+                rp = h.pos;
+                pdf = 1.0f / fmaxf(1.0f, spec * 2.0f);
+                att = 1.0f * m.rg;
+            }
+            store_rng(rng, n_rng, i * S + s, r);
+        }
+        // the pixel's list in (sample, bounce) order: an exclusive prefix of the hit counts over its S lanes
+        uint32_t off = 0, total = 0;
+        f3 next_pos = splat(0.0f);
+        for (uint32_t j = 0; j < S; ++j) {
+            const uint32_t c = __shfl(nh, (int)(g0 + j), 64);
+            const f3 pj = mk(__shfl(p0.x, (int)(g0 + j), 64), __shfl(p0.y, (int)(g0 + j), 64), __shfl(p0.z, (int)(g0 + j), 64));
+            if (j < s) off += c;
+            total += c;
+            next_pos = next_pos + pj;   // raytrace_pixel's sum over the samples, in sample order
+        }
+        if (active) {
+            int* L = q.plist + (size_t)t * q.max_hits;
+            for (uint32_t b = 0; b < nh && b < RT_SP_MAX_BOUNCES; ++b) L[off + b] = recs[b];
+            if (s == 0) {
+                q.pcount[t] = (uint8_t)total;
+                next_pos = next_pos / (float)S;
+                acc_depth[i] = dot(src_d, next_pos - src_p);
+            }
+        }
+    }
+}
+
 // One shadow ray of the deferred raytracer: shade_object's depth_test_world + depth_test_nerf +
 // mask (raytracer.cu:30-50).  The BVH query is culled at full_dist: any syn >= full_dist gives
 // the same mask (sh = min(nerf, syn, full_dist) and the NeRF march below full_dist does not
@@ -1169,64 +1254,6 @@ __global__ __launch_bounds__(256) void rt_accumulate_kernel(RaytraceArgs a, RtQu
 }
 
 // ---------------------------------------------------------------------------
-// overlay_nerf (raytracer.cu:220-258) with sng_tonemap (synerfgine/common.cu:186-243)
-// ---------------------------------------------------------------------------
-// ETonemapCurve (common.h:113): 0 Identity, 1 ACES, 2 Hable, 3 Reinhard.  The rational curves' constants are the
-// reference's float expressions (folded at compile time); the per-pixel division is IEEE (-fno-fast-math).
-__device__ __forceinline__ f3 sng_tonemap(f3 x, int curve) {
-    if (curve == 0) return x;
-    x = mk(fmaxf(x.x, 0.0f), fmaxf(x.y, 0.0f), fmaxf(x.z, 0.0f));
-    float k0, k1, k2, k3, k4, k5;
-    if (curve == 1) {
-        k0 = 0.6f * 0.6f * 2.51f;
-        k1 = 0.6f * 0.03f;
-        k2 = 0.0f;
-        k3 = 0.6f * 0.6f * 2.43f;
-        k4 = 0.6f * 0.59f;
-        k5 = 0.14f;
-    } else if (curve == 2) {
-        constexpr float A = 0.15f, B = 0.50f, C = 0.10f, D = 0.20f, E = 0.02f, F = 0.30f;
-        constexpr float h0 = A * F - A * E, h1 = C * B * F - B * E, h2 = 0.0f, h3 = A * F, h4 = B * F, h5 = D * F * F;
-        constexpr float W = 11.2f;
-        constexpr float nom = h0 * (W * W) + h1 * W + h2;
-        constexpr float denom = h3 * (W * W) + h4 * W + h5;
-        constexpr float white_scale = denom / nom;
-        k0 = 4.0f * h0 * white_scale;
-        k1 = 2.0f * h1 * white_scale;
-        k2 = h2 * white_scale;
-        k3 = 4.0f * h3;
-        k4 = 2.0f * h4;
-        k5 = h5;
-    } else {
-        const float Y = 0.2126f * x.x + 0.7152f * x.y + 0.0722f * x.z;
-        return x * (1.f / (Y + 1.0f));
-    }
-    const f3 sq = x * x;
-    const f3 nom = sq * k0 + x * k1 + k2;
-    const f3 den = sq * k3 + x * k4 + k5;
-    return mk(nom.x / den.x, nom.y / den.y, nom.z / den.z);
-}
-
-__global__ void overlay_kernel(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
-                               int tonemap, const float4* __restrict__ syn_rgba, const float* __restrict__ syn_depth, const float4* __restrict__ nerf_rgba,
-                               const float* __restrict__ nerf_depth, float4* __restrict__ final_rgba, float* __restrict__ final_depth) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
-    if (t >= n) return;
-    const int x = (int)(t % (uint32_t)W), y = row0 + (int)(t / (uint32_t)W);
-    const int sid = x + y * W;
-    // nerf_res = syn_res / syn_px_scale as in the reference (raytracer.cu:242-246); an index past the NeRF buffer
-    // (a window not divisible by the scale: the reference reads out of bounds) is clamped for memory safety
-    const int nid = min((x / scale) + (y / scale) * nerf_w, n_nerf - 1);
-    const float sdepth = syn_depth[sid];
-    const float4 use = (!show_nerf || sdepth - depth_offset < nerf_depth[nid]) ? syn_rgba[sid] : nerf_rgba[nid];
-    f3 c = sng_tonemap(mk(use.x * exposure_mul, use.y * exposure_mul, use.z * exposure_mul), tonemap);
-    if (srgb) c = mk(linear_to_srgb(c.x), linear_to_srgb(c.y), linear_to_srgb(c.z));
-    final_rgba[sid] = make_float4(c.x, c.y, c.z, use.w);
-    final_depth[sid] = sdepth;
-}
-
-// ---------------------------------------------------------------------------
 // curand_init(PT_SEED, idx, 0): v <- (M^(2^67))^idx v via precomputed powers
 // ---------------------------------------------------------------------------
 __global__ void xorwow_init_kernel(uint32_t n, uint32_t seed_lo, uint32_t seed_hi, const uint32_t* __restrict__ seq_pow /* 32 x 160 x 5 */,
@@ -1329,9 +1356,21 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     const size_t lp = trace_lds_bytes(a, lds, tp) + (a.fused_shadow ? RT_FQ_WORDS * 4u : 0u), ls = trace_lds_bytes(a, lds, ts);
     const uint32_t n_tiles = (((uint32_t)a.W + a.tile - 1) / a.tile) * (((uint32_t)(a.row1 - a.row0) + a.tile_h - 1) / a.tile_h);
     // rt_spread: every CU gets a workgroup (a thin band's tiles then spread over the whole GPU, one wave each)
-    const uint32_t bp = a.spread ? a.persistent_blocks * per_cu : std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * per_cu);
+    const uint32_t bp = (a.spread || a.sample_par) ? a.persistent_blocks * per_cu : std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * per_cu);
     const uint32_t sb = shadow_blocks ? shadow_blocks : a.persistent_blocks * per_cu;
-    if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in
+    if (a.sample_par) {   // rt_rng = 1 (capi.cpp: list mode, no counters, no fused queue): the sample-parallel path kernel
+        if (lds) {
+            allow_lds(raytrace_sp_kernel<true>, lp);
+            allow_lds(shadow_rays_kernel<true>, ls);
+            hipLaunchKernelGGL((raytrace_sp_kernel<true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd);
+            hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+        } else {
+            allow_lds(raytrace_sp_kernel<false>, lp);
+            allow_lds(shadow_rays_kernel<false>, ls);
+            hipLaunchKernelGGL((raytrace_sp_kernel<false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd);
+            hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
+        }
+    } else if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in
         allow_lds(raytrace_kernel<true, true, true>, lp);
         allow_lds(shadow_rays_kernel<true, true>, ls);
         hipLaunchKernelGGL((raytrace_kernel<true, true, true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, acc, accd);
@@ -1366,13 +1405,6 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     hipLaunchKernelGGL(rt_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, q, acc, (const float4*)nullptr, o, d, accd);
 }
 
-void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf, int show_nerf, float depth_offset, float exposure_mul, int srgb,
-                    int tonemap, const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s) {
-    const uint32_t n = (uint32_t)(row1 - row0) * (uint32_t)W;
-    if (!n) return;
-    hipLaunchKernelGGL(overlay_kernel, dim3((n + 255) / 256), dim3(256), 0, s, W, row0, row1, scale, nerf_w, n_nerf, show_nerf, depth_offset, exposure_mul,
-                       srgb, tonemap, syn, synd, nerf, nerfd, fin, find);
-}
 void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(xorwow_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, (uint32_t)seed, (uint32_t)(seed >> 32), seq_pow, st);

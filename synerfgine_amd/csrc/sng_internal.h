@@ -284,7 +284,9 @@ struct RaytraceArgs {
     int fused_shadow;           // the path kernel's idle waves trace the shadow rays (banded frames, mesh.hip fq_consume)
     uint32_t* started;          // rt_first: every path-kernel workgroup writes started_seq here as it lands (nullptr: off)
     uint32_t started_seq;
+    int sample_par;             // rt_rng = 1: per-(pixel, sample) XORWOW streams, a pixel's samples on adjacent lanes (raytrace_sp_kernel)
 };
+constexpr uint32_t RT_SP_MAX_BOUNCES = 4;   // raytrace_sp_kernel keeps a lane's record indices in registers
 
 // fused shadow queue of a banded path kernel (mesh.hip fq_publish / fq_consume): entries per workgroup, LDS words
 constexpr uint32_t RT_FQ_CAP = 1024;

@@ -113,6 +113,8 @@ for ov in CASES:
         full, rf = timed(None, args.reps)
         recs = record()
         n_red = len(recs[1])
+        for _ in range(6):   # the split balanced for this case's costs
+            b = balance_bounds(H, b, [t_band((b[r], b[r + 1]), recs, 2)[0] for r in range(N)])
     res = []
     for r in range(N):
         ms, fr = t_band((b[r], b[r + 1]), recs, args.reps)
@@ -123,7 +125,7 @@ for ov in CASES:
     # the gather: rank 0 receives N - 1 bands of ~H/N rows x W x 4 B, each over its own xGMI link
     gather_ms = (H / N) * W * 4 / (args.gather_gbs * 1e9) * 1e3 + args.ar_us * 1e-3
     pred = worst[0] + comm_ms + gather_ms
-    emit({"overrides": ov, "n": N, "full_ms": round(full, 3), "max_band_ms": round(worst[0], 3),
+    emit({"overrides": ov, "n": N, "bounds": b, "full_ms": round(full, 3), "max_band_ms": round(worst[0], 3),
           "reductions_per_frame": n_red, "priced_allreduce_ms": round(comm_ms, 3), "priced_gather_ms": round(gather_ms, 3),
           "pred_frame_ms": round(pred, 3), "pred_fps": round(1000.0 / pred, 1), "pred_eff": round(full / (N * pred), 3),
           "pred_eff_compute_only": round(full / (N * worst[0]), 3),
