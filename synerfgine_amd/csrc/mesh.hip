@@ -6,9 +6,10 @@
 // raytrace and overlay_nerf (synerfgine/raytracer.cu:6-258), and init_rand_state
 // (synerfgine/common.cu:22-26, cuRAND XORWOW seeding restated).
 //
-// Arithmetic: this file is compiled with FMA contraction (-ffp-contract=on, Makefile) and the triangle test's
-// division is the hardware reciprocal -- the reference's --use_fast_math model (CMakeLists.txt:82: nvcc contracts
-// a * b + c and turns x / y into rcp.approx); the NeRF marcher and its schedule (nerf.hip, fused.hip) stay IEEE.
+// Arithmetic: this file is compiled in the reference's --use_fast_math model (CMakeLists.txt:82; Makefile): FMA
+// contraction (nvcc --fmad=true) and fp32 division / sqrt without the correctly rounded expansions (--prec-div=false,
+// --prec-sqrt=false: x / y and 1 / x become v_rcp_f32 forms, sqrtf v_sqrt_f32); the NeRF marcher and its schedule
+// (nerf.hip, fused.hip) stay IEEE.
 // The overlay / tonemap, compared bit for bit with the oracle, live in overlay.hip (no contraction).
 //
 // BVH traversal keeps its 32-entry stack in LDS, interleaved by thread
@@ -143,7 +144,7 @@ __device__ __forceinline__ bool tri_hit(const TriT* tp, f3 ro, f3 rd, float mint
     const f3 rov0 = ro - mk(w0.x, w0.y, w0.z);
     // 1.0f / dot(rd, n) as the reference's --use_fast_math build evaluates it (CMakeLists.txt:82: a division becomes
     // rcp.approx), the hardware reciprocal v_rcp_f32 (1 ulp)
-#ifdef RT_TRI_RCP_EXACT   // A/B builds of the IEEE model (make MESH_EXTRA="-ffp-contract=off -DRT_TRI_RCP_EXACT")
+#ifdef RT_TRI_RCP_EXACT   // A/B builds of the IEEE model (Makefile: MESH_EXTRA=... -DRT_TRI_RCP_EXACT)
     const float d = 1.0f / dot(rd, n);
 #else
     const float d = __builtin_amdgcn_rcpf(dot(rd, n));
@@ -1010,12 +1011,20 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
     const uint32_t S = a.samples, ppw = 64u / S;                     // pixels per wave (1 <= S <= 64)
     const uint32_t n_px = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W, n_units = (n_px + ppw - 1u) / ppw;
     const uint32_t sub = (uint32_t)lane / S, s = (uint32_t)lane % S, g0 = sub * S;   // lane -> (pixel of the unit, sample)
+    // units claimed a_sp_chunk at a time (capi.cpp: ~8 claims per wave, 1 for thin bands) -- a full frame has ~2.6e5 units,
+    // whose claims on one counter would serialise like the shadow kernel's once did
+    const uint32_t chunk = max(1u, a.sp_chunk);
+    uint32_t k = 0, k_end = 0;
     while (true) {
-        uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(work, 1u);
-        k = __shfl(k, 0, 64);
-        if (k >= n_units) break;
+        if (k >= k_end) {
+            uint32_t c = 0;
+            if (lane == 0) c = atomicAdd(work, 1u);
+            k = __shfl(c, 0, 64) * chunk;
+            if (k >= n_units) break;
+            k_end = min(k + chunk, n_units);
+        }
         const uint32_t t = k * ppw + sub;
+        ++k;
         const bool active = sub < ppw && t < n_px;
         const size_t i = (size_t)a.row0 * a.W + (active ? t : 0u);
         f3 p0 = splat(0.0f), src_p = splat(0.0f), src_d = splat(0.0f);
@@ -1359,15 +1368,18 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     const uint32_t bp = (a.spread || a.sample_par) ? a.persistent_blocks * per_cu : std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * per_cu);
     const uint32_t sb = shadow_blocks ? shadow_blocks : a.persistent_blocks * per_cu;
     if (a.sample_par) {   // rt_rng = 1 (capi.cpp: list mode, no counters, no fused queue): the sample-parallel path kernel
+        RaytraceArgs b = a;   // ~8 claims per wave of the grid (a band's few units: one per claim)
+        const uint32_t ppw = 64u / std::max(1u, a.samples), units = (n + ppw - 1) / ppw, waves = bp * (tp / 64u);
+        b.sp_chunk = std::max(1u, units / (waves * 8u));
         if (lds) {
             allow_lds(raytrace_sp_kernel<true>, lp);
             allow_lds(shadow_rays_kernel<true>, ls);
-            hipLaunchKernelGGL((raytrace_sp_kernel<true>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd);
+            hipLaunchKernelGGL((raytrace_sp_kernel<true>), dim3(bp), dim3(tp), lp, s, b, q, a.work, o, d, rng, n_rng, accd);
             hipLaunchKernelGGL(shadow_rays_kernel<true>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
         } else {
             allow_lds(raytrace_sp_kernel<false>, lp);
             allow_lds(shadow_rays_kernel<false>, ls);
-            hipLaunchKernelGGL((raytrace_sp_kernel<false>), dim3(bp), dim3(tp), lp, s, a, q, a.work, o, d, rng, n_rng, accd);
+            hipLaunchKernelGGL((raytrace_sp_kernel<false>), dim3(bp), dim3(tp), lp, s, b, q, a.work, o, d, rng, n_rng, accd);
             hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
         }
     } else if (lds && a.counts) {   // counting frame (rt_count): the same kernels with the traversal counters compiled in

@@ -285,6 +285,7 @@ struct RaytraceArgs {
     uint32_t* started;          // rt_first: every path-kernel workgroup writes started_seq here as it lands (nullptr: off)
     uint32_t started_seq;
     int sample_par;             // rt_rng = 1: per-(pixel, sample) XORWOW streams, a pixel's samples on adjacent lanes (raytrace_sp_kernel)
+    uint32_t sp_chunk;          // raytrace_sp_kernel: (64 / samples)-pixel units per work claim
 };
 constexpr uint32_t RT_SP_MAX_BOUNCES = 4;   // raytrace_sp_kernel keeps a lane's record indices in registers
 

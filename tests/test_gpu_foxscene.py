@@ -2,7 +2,7 @@
 scenes/): its camera in the fox frame, a point light + a directional light, bunny + armadillo (glossy), and
 nerf_on_nerf_shadow_threshold 0.942, rendered on the trained cascaded fox snapshot (data/fox.ingp: aabb_scale 4,
 3 cascades, cone stepping) -- against the CPU oracle on the same inputs and RNG states.
-Parity is to the restatement (oracle/), which is itself unpinned at the pixel level (DESIGN.md §4)."""
+Parity is to the restatement (oracle/), which is itself unpinned at the pixel level (DESIGN.md §6)."""
 import json
 import os
 

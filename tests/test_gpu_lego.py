@@ -7,9 +7,9 @@ oracle, at BASELINE.json's own configs:
   * a frame-filling lego view (most rays hit the object): same bar, plus the schedule;
   * the MLP outputs on samples of that frame against both accumulation models of the oracle: fp32 over K
     (what the MFMA kernel computes) and tcnn's fp16 WMMA accumulators (nerf_network.h:120,130); the
-    gaps are written to gpurun_out/mlp_accum_gap.json for DESIGN.md §4.
+    gaps are written to gpurun_out/mlp_accum_gap.json for DESIGN.md §6.
 
-Tolerances as in tests/test_gpu_parity.py (DESIGN.md §4).
+Tolerances as in tests/test_gpu_parity.py (DESIGN.md §6).
 """
 import json
 import os

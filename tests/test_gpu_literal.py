@@ -6,7 +6,7 @@ BVH box test, bounding_box.cuh:163-211; powf in the Phong term and the shadow ma
 raytracer.cu:6-57; the overlay's unclamped NeRF index, raytracer.cu:242-246).  The product evaluates restatements
 of the fast-math build (reciprocal-multiply box tests, integer powers by binary exponentiation, the clamped index),
 which the oracle also offers (orc_set_literal(0)).  The frame must meet the whole-frame bar against BOTH: PSNR >= 40 dB
-and >= 99.5 % of pixels within 2/255 (DESIGN.md §4); the measured gaps go to gpurun_out/literal_delta.json.
+and >= 99.5 % of pixels within 2/255 (DESIGN.md §6); the measured gaps go to gpurun_out/literal_delta.json.
 
 sng_tonemap (synerfgine/common.cu:186-243): ACES, Hable and Reinhard, selected by Testbed::m_tonemap_curve, which
 the engine hands to overlay_nerf (engine.cu:406) -- param tonemap_curve, checked curve by curve against the oracle.

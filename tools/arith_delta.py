@@ -40,8 +40,9 @@ def dump(path):
 def cmp(a, b, out=None):
     A, B = np.load(a), np.load(b)
     W = A["syn_depth"].shape[1]
-    st_a, st_b = A["rng_mesh"], B["rng_mesh"]   # [6][n_px]
-    flip = (st_a != st_b).any(axis=0)
+    st_a, st_b = A["rng_mesh"], B["rng_mesh"]
+    ax = 0 if st_a.shape[0] == 6 and st_a.ndim == 2 and st_a.shape[1] != 6 else -1   # [6][n_px] or [n_px][6]
+    flip = (st_a != st_b).any(axis=ax).reshape(-1)
     n_px = flip.size
     hit = (A["syn_depth"] < 1e3).reshape(-1) | (B["syn_depth"] < 1e3).reshape(-1)
     dd = np.abs(A["syn_depth"].astype(np.float64) - B["syn_depth"]).reshape(-1)
