@@ -916,8 +916,9 @@ def main():
 
     result, s0 = None, stats[-1]
     if rank == 0:
+        snap = S.snapshot_path(args.config, args.model)
         result = frame_result(args, stats, elapsed, world, res, bounds, comm, overrides, root_gather, on_dev,
-                              os.path.relpath(S.snapshot_path(args.config, args.model), REPO))
+                              os.path.relpath(snap, REPO) if snap else None)
     if rank == 0 and world == 1 and not args.no_sweep:
         # extra legs, after the timed region: the same workload with the two streams serialized (the roofline kernel's
         # launches then run alone), the BVH work of one counting frame, and the training step (config C5)

@@ -6,16 +6,20 @@
 // raytrace and overlay_nerf (synerfgine/raytracer.cu:6-258), and init_rand_state
 // (synerfgine/common.cu:22-26, cuRAND XORWOW seeding restated).
 //
-// Arithmetic: this file is compiled in the reference's --use_fast_math model (CMakeLists.txt:82; Makefile): FMA
-// contraction (nvcc --fmad=true) and fp32 division / sqrt without the correctly rounded expansions (--prec-div=false,
-// --prec-sqrt=false: x / y and 1 / x become v_rcp_f32 forms, sqrtf v_sqrt_f32); the NeRF marcher and its schedule
-// (nerf.hip, fused.hip) stay IEEE.
+// Arithmetic: this file is compiled with FMA contraction per expression (-ffp-contract=on, Makefile) and the triangle
+// test's division is the hardware reciprocal -- the reference's --use_fast_math model (CMakeLists.txt:82: nvcc
+// contracts a * b + c and turns x / y into rcp.approx); other divisions and sqrt stay correctly rounded, so every
+// kernel variant here computes the same bits (Makefile); the NeRF marcher and its schedule (nerf.hip, fused.hip) are
+// IEEE without contraction.
 // The overlay / tonemap, compared bit for bit with the oracle, live in overlay.hip (no contraction).
 //
 // BVH traversal keeps its 32-entry stack in LDS, interleaved by thread
 // ([depth][thread]) so a wave's pushes/pops at equal depth hit 64 distinct
 // banks.  Each pixel keeps its own XORWOW stream in SoA registers for the whole
 // kernel (one coalesced load/store of 24 B per pixel per frame).
+#ifdef RT_FAST_TRANSCENDENTALS   // A/B builds: the cone-stepping log / exp of this file's shadow marches as __logf / __expf
+#define SNG_FAST_TRANSCENDENTALS
+#endif
 #include <algorithm>
 #include "sng_internal.h"
 #include "sng_math.h"

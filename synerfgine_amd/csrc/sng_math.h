@@ -415,20 +415,31 @@ SNG_HD StepSpace step_space(float cone) {
     k.rlog1p_c = recip_rn(k.log1p_c);
     return k;
 }
+// The per-trip log / exp of the cone-stepping conversions below: the deterministic sng_logf / sng_expf (the NeRF
+// marcher and its schedule, equal on host and device), or -- in a translation unit that defines
+// SNG_FAST_TRANSCENDENTALS before including this header (mesh.hip: the shadow marches of the raytracer and the NeRF
+// shadow pass, in the reference's --use_fast_math model, where logf / expf are __logf / __expf) -- the hardware forms.
+#if defined(SNG_FAST_TRANSCENDENTALS) && defined(__HIP_DEVICE_COMPILE__)
+#define SNG_STEP_EXPF __expf
+#define SNG_STEP_LOGF __logf
+#else
+#define SNG_STEP_EXPF sng_expf
+#define SNG_STEP_LOGF sng_logf
+#endif
 // The two constant divisions as exact reciprocal forms: x / MIN_STEP is div_by (see above), and since
 // MAX_STEP == MIN_STEP * 2^10 exactly, x / MAX_STEP == (x / MIN_STEP) * 2^-10 (power-of-two scaling
 // commutes with rounding in the normal range).
 SNG_HD float to_stepping_space(float t, const StepSpace& k) {
     if (k.cone <= 1e-5f) return div_by(t, MIN_STEP, INV_MIN_STEP);
     if (t <= k.at) return div_by(t - k.at, MIN_STEP, INV_MIN_STEP) + k.a;
-    else if (t <= k.bt) return div_by(sng_logf(t), k.log1p_c, k.rlog1p_c);   // the IEEE quotient (Markstein, as div_by above)
+    else if (t <= k.bt) return div_by(SNG_STEP_LOGF(t), k.log1p_c, k.rlog1p_c);   // the IEEE quotient (Markstein, as div_by above)
     else return div_by(t - k.bt, MIN_STEP, INV_MIN_STEP) * (1.0f / 1024.0f) + k.b;
 }
 static_assert(MAX_STEP == MIN_STEP * 1024.0f, "MAX_STEP / MIN_STEP must be 2^10");
 SNG_HD float from_stepping_space(float n, const StepSpace& k) {
     if (k.cone <= 1e-5f) return n * MIN_STEP;
     if (n <= k.a) return (n - k.a) * MIN_STEP + k.at;
-    else if (n <= k.b) return sng_expf(n * k.log1p_c);
+    else if (n <= k.b) return SNG_STEP_EXPF(n * k.log1p_c);
     else return (n - k.b) * MAX_STEP + k.bt;
 }
 SNG_HD float advance_n_steps(float t, const StepSpace& k, float n) { return from_stepping_space(to_stepping_space(t, k) + n, k); }

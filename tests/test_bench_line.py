@@ -90,3 +90,12 @@ def test_headline_without_legs():
     line = bench.compact_line(_full(legs=False))
     json.loads(json.dumps(line))
     assert "cpu_baseline" not in line and line["value"] > 0
+
+
+def test_line_for_a_synthetic_model_without_snapshot():
+    # config c4 renders the synthetic kitchen-like model (no .ingp): no snapshot path to report
+    stats = [_stub_frame() for _ in range(3)]
+    full = bench.frame_result(_args(config="c4", steps=3, model="synthetic"), stats, 0.01, 1, {"mesh": (1920, 1080), "nerf": (1920, 1080)},
+                              [0, 1080], {}, {}, False, True, None)
+    line = bench.compact_line(full)
+    assert line["data"].startswith("synthetic") and line["metric"] == bench.METRICS["c4"]

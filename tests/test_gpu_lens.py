@@ -152,3 +152,33 @@ def test_render_lens_frame_matches_oracle(lens):
         assert _psnr(got[..., :3], persp[..., :3]) < 35.0, "the lens did not change the frame"
     finally:
         tb.close()
+
+
+@pytest.mark.parametrize("where", ["global", "metadata"])
+def test_snapshot_legacy_camera_distortion_key(tmp_path, where, synthetic_model):
+    """from_json(NerfDataset) (json_binding.h:141-160) also accepts the legacy key "camera_distortion", at the dataset's
+    global level and per image, and it overrides "lens": load_snapshot's render lens follows it."""
+    import zlib
+
+    import msgpack
+    from synerfgine_amd import Testbed, ingp
+    cfg, params, grid = synthetic_model
+    p = tmp_path / "legacy.ingp"
+    ingp.write_ingp(str(p), cfg, params, grid)
+    root = msgpack.unpackb(zlib.decompress(p.read_bytes()), raw=False, strict_map_key=False)
+    ds = root["snapshot"]["nerf"]["dataset"]
+    lens = {"k1": 0.125, "k2": -0.0625, "p1": 0.001, "p2": 0.002}
+    if where == "global":
+        ds["lens"] = {}
+        ds["camera_distortion"] = lens
+    else:
+        ds["metadata"] = [{"lens": {}, "camera_distortion": lens}]
+    p.write_bytes(zlib.compress(msgpack.packb(root, use_bin_type=True), 6))
+    tb = Testbed(0)
+    try:
+        tb.load_snapshot(str(p))
+        mode, prm = tb.render_lens()
+    finally:
+        tb.close()
+    assert mode == 1   # ELensMode::OpenCV
+    np.testing.assert_allclose(prm[:4], [0.125, -0.0625, 0.001, 0.002], rtol=0, atol=1e-7)

@@ -122,3 +122,37 @@ def test_oracle_latlong_equirect_ftheta_directions(oracle_lib):
     assert not ok
     ok, d = O.uv_to_ray_dir(ft, (0.6, 0.5), (640, 480), (1, 1), (0.5, 0.5))
     assert ok and d[1] == 0.0 and np.isclose(math.atan2(d[0], d[2]), 1e-3 * 64.0, rtol=1e-5)
+
+
+def test_loader_sorts_frames_naturally_before_the_cull(tmp_path):
+    """load_nerf sorts the frames by file_path in natural order (SI::natural::compare, nerf_loader.cu:347-349) before
+    the n_frames cull, and converts fields of view with the float expressions of fov_to_focal_length
+    (common_device.cuh:618-620)."""
+    from synerfgine_amd import nerf_data
+    img = np.zeros((4, 6, 4), np.uint8)
+    names = ["r_10", "r_2", "r_1", "r_1a"]
+    for k, n in enumerate(names):
+        img[..., 0] = k
+        _write_png(tmp_path / f"{n}.png", img)
+    eye = [[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, 0], [0, 0, 0, 1]]
+    meta = {"camera_angle_x": 0.6911112070083618, "n_frames": 3,
+            "frames": [{"file_path": f"./{n}.png", "transform_matrix": eye} for n in names]}
+    (tmp_path / "transforms.json").write_text(json.dumps(meta))
+    d = nerf_data.load_nerf(str(tmp_path))
+    assert d["paths"] == ["./r_1.png", "./r_1a.png", "./r_2.png"]   # natural order, then the first n_frames
+    assert [int(x[0, 0, 0]) for x in d["images"]] == [2, 3, 1]
+    f32 = np.float32
+    deg = f32(f32(f32(0.6911112070083618) * f32(180)) / f32(math.pi))
+    ref = f32(f32(0.5) * f32(6)) / f32(np.tan(f32(f32(f32(0.5) * deg) * f32(math.pi)) / f32(180)))
+    assert abs(d["focal"][0][0] - ref) <= 4e-7 * ref
+
+
+def _write_png(path, img):
+    import struct
+    import zlib
+    h, w = img.shape[:2]
+    raw = b"".join(b"\x00" + img[y].tobytes() for y in range(h))
+    def chunk(t, data):
+        return struct.pack(">I", len(data)) + t + data + struct.pack(">I", zlib.crc32(t + data) & 0xFFFFFFFF)
+    path.write_bytes(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 6, 0, 0, 0)) + chunk(b"IDAT", zlib.compress(raw)) +
+                     chunk(b"IEND", b""))
