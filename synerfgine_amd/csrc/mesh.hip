@@ -8,16 +8,18 @@
 //
 // Arithmetic: this file is compiled with FMA contraction per expression (-ffp-contract=on, Makefile) and the triangle
 // test's division is the hardware reciprocal -- the reference's --use_fast_math model (CMakeLists.txt:82: nvcc
-// contracts a * b + c and turns x / y into rcp.approx); other divisions and sqrt stay correctly rounded, so every
-// kernel variant here computes the same bits (Makefile); the NeRF marcher and its schedule (nerf.hip, fused.hip) are
-// IEEE without contraction.
+// contracts a * b + c and turns x / y into rcp.approx), and the cascaded shadow marches' log / exp are __logf /
+// __expf; other divisions and sqrt stay correctly rounded, so every kernel variant here computes the same bits
+// (Makefile); the NeRF marcher and its schedule (nerf.hip, fused.hip) are IEEE without contraction.
 // The overlay / tonemap, compared bit for bit with the oracle, live in overlay.hip (no contraction).
 //
 // BVH traversal keeps its 32-entry stack in LDS, interleaved by thread
 // ([depth][thread]) so a wave's pushes/pops at equal depth hit 64 distinct
 // banks.  Each pixel keeps its own XORWOW stream in SoA registers for the whole
 // kernel (one coalesced load/store of 24 B per pixel per frame).
-#ifdef RT_FAST_TRANSCENDENTALS   // A/B builds: the cone-stepping log / exp of this file's shadow marches as __logf / __expf
+// The cone-stepping log / exp of this file's shadow marches (cascaded scenes) as __logf / __expf, the reference's
+// fast-math forms (sng_math.h SNG_STEP_EXPF); A/B builds of the IEEE model define RT_IEEE_TRANSCENDENTALS
+#ifndef RT_IEEE_TRANSCENDENTALS
 #define SNG_FAST_TRANSCENDENTALS
 #endif
 #include <algorithm>
