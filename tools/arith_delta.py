@@ -1,7 +1,7 @@
 """What the raytracer's arithmetic model changes in a C3 frame: render the benchmarked 1920x1080
 frame (lego snapshot + armadillo, the same RNG states) with a library build and save its layers, then compare two
 builds -- the IEEE model (make BUILD=_build_ieee MESH_EXTRA="-ffp-contract=off -DRT_TRI_RCP_EXACT -DRT_IEEE_TRANSCENDENTALS") against the default
-fast-math model (FMA contraction + the hardware reciprocal in the triangle test; the IEEE build also takes -DRT_IEEE_TRANSCENDENTALS).
+fast-math model (FMA contraction, the hardware reciprocal in the triangle test, __logf / __expf in the cascaded shadow marches).
   SNG_LIB_PATH=<lib> python tools/arith_delta.py dump out.npz
   python tools/arith_delta.py cmp ieee.npz fast.npz [out.json]
 A pixel whose mesh XORWOW state differs after the frame drew a different number of random numbers: some query of its
