@@ -92,16 +92,10 @@ struct TraceCtx {
 
 // One BvhWide record: four 16-B loads (ds_read_b128 from the LDS scene blob).  d0, d1: the entry
 // distances of its two child boxes, exactly as bvh_box_entry / aabb_entry_fast give them.
-#ifdef RT_KEEP_LOADS   // A/B: the record's four loads issued together, before the slab tests (no load sunk into the early-out branch)
-__device__ __forceinline__ void keep_loaded(float4 v) { asm volatile("" : : "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
-#endif
 template <bool FAST>
 __device__ __forceinline__ void wide_visit(const BvhWide* __restrict__ rec, f3 ro, f3 rd, f3 y, float& d0, float& d1, int& ref0, int& ref1) {
     const float4* r = reinterpret_cast<const float4*>(rec);
     const float4 a = r[0], b = r[1], c = r[2], e = r[3];
-#ifdef RT_KEEP_LOADS
-    keep_loaded(a); keep_loaded(b); keep_loaded(c);
-#endif
     if constexpr (FAST) {
         d0 = slab_entry_fast(pf2{a.x, a.y}, pf2{a.z, a.w}, pf2{b.x, b.y}, ro, y);
         d1 = slab_entry_fast(pf2{b.z, b.w}, pf2{c.x, c.y}, pf2{c.z, c.w}, ro, y);
@@ -260,12 +254,7 @@ __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide
             if (cnt) cnt[1] += cw ? (uint32_t)((int)__builtin_amdgcn_readfirstlane(__lane_id()) == (int)__lane_id()) : 2u;
             float d0, d1;
             int r0, r1;
-#ifdef RT_KEEP_LOADS   // (a 24-bit multiply for the record's address: full rate, where v_mul_lo_u32 is quarter rate)
-            wide_visit<FAST>(reinterpret_cast<const BvhWide*>(reinterpret_cast<const char*>(wide) + __umul24((uint32_t)cur, (uint32_t)sizeof(BvhWide))),
-                             ro, rd, y, d0, d1, r0, r1);
-#else
             wide_visit<FAST>(wide + cur, ro, rd, y, d0, d1, r0, r1);
-#endif
             int i0 = r0, i1 = r1;
             if (d0 < d1) { float td = d0; d0 = d1; d1 = td; i0 = r1; i1 = r0; }
             // reference: push(far) if d0 < mint, push(near) if d1 < mint, then pop
