@@ -341,6 +341,7 @@ const std::map<std::string, double>& default_params() {
                                                 //   the frame's critical path, idles ~0.3 ms behind init_rays + generate + network)
         {"rt_reserved_cus", 32},                // concurrent mode: CUs (4 per XCD) the persistent raytracer grids leave to the NeRF stream
         {"linear_marcher", 1},                  // exact unit-cube fast path of the occupancy march
+        {"occ_lin_all", 1},                     // cascaded marchers read every cascade's occupancy from x-fastest rows (same bits, no Morton code)
         {"fast_slab", 1},                       // exact reciprocal-multiply BVH box tests
         {"rt_wavefront", 1},                    // deferred shadow-ray queues for the path tracer
         {"bvh_wide", 1},                        // traversal layout with both child boxes per record (exact)
@@ -689,7 +690,7 @@ void set_density_grid(sng_ctx* c, const uint16_t* grid, uint64_t n_cells) {
     c->d_partial.ensure(1024 * sizeof(double));
     c->d_mean.ensure(sizeof(float));
     c->d_bitfield.ensure((size_t)GRID_CELLS / 8 * N_CASCADES);
-    c->d_occ_linear.ensure((size_t)GRID_CELLS / 8);
+    c->d_occ_linear.ensure((size_t)GRID_CELLS / 8 * N_CASCADES);   // every cascade (Volume::occ_lin_all)
     launch_bitfield(c->d_grid_f16.as<uint16_t>(), c->max_cascade, c->d_grid_f32.as<float>(), c->d_partial.as<double>(), c->d_mean.as<float>(),
                     c->d_bitfield.as<uint8_t>(), c->d_occ_linear.as<uint32_t>(), c->s_nerf);
     build_occ_brick(c, c->s_nerf);
@@ -733,6 +734,7 @@ Volume make_volume(const sng_ctx* c) {
     v.min_transmittance = (float)c->p("min_transmittance");
     v.bitfield = c->d_bitfield.as<uint8_t>();
     v.occ_linear = c->d_occ_linear.as<uint32_t>();
+    if (c->p("occ_lin_all") != 0.0) v.occ_lin_all = v.occ_linear;   // the cascaded marchers' lookups without Morton encoding
     v.linear = (c->max_cascade == 0 && c->cone <= 1e-5f && c->p("linear_marcher") != 0.0) ? 1 : 0;
     // the bricks in LDS when they fit the budget (lego: 521 bricks, 41 KiB)
     const uint32_t words = (OCC_BRICK_HDR_WORDS + 16u * std::max(1u, c->occ_brick_n) + 3u) & ~3u;   // >= 1 brick: branch-free readers
@@ -2054,7 +2056,7 @@ void train_reset(sng_ctx* c, uint64_t seed) {
     c->d_partial.ensure(1024 * sizeof(double));
     c->d_mean.ensure(sizeof(float));
     c->d_bitfield.ensure((size_t)GRID_CELLS / 8 * N_CASCADES);
-    c->d_occ_linear.ensure((size_t)GRID_CELLS / 8);
+    c->d_occ_linear.ensure((size_t)GRID_CELLS / 8 * N_CASCADES);   // every cascade (Volume::occ_lin_all)
     t.ready = true;
 }
 

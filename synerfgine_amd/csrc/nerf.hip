@@ -1498,18 +1498,20 @@ __global__ void bitfield_max_pool_kernel(uint32_t n_elements, const uint8_t* __r
     next[morton3D(x, y, z)] |= bits;
 }
 
-// mip-0 occupancy as x-fastest bit rows: word (z*128 + y)*4 + x/32, bit x%32 == Morton bit (x,y,z).
-// Same bits, cheaper address math for the linear marcher.
+// every cascade's occupancy as x-fastest bit rows: word ((mip*128 + z)*128 + y)*4 + x/32, bit x%32 == Morton bit
+// (x,y,z) of that mip.  Same bits, cheaper address math for the marchers (mip 0 alone: the linear marcher).
 __global__ void bitfield_linear_kernel(const uint8_t* __restrict__ bf, uint32_t* __restrict__ occ) {
-    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= GRID_CELLS / 32) return;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= GRID_CELLS / 32 * N_CASCADES) return;
+    const uint32_t mip = g / (GRID_CELLS / 32), w = g % (GRID_CELLS / 32);
     const uint32_t z = w / (GRID_SIZE * GRID_SIZE / 32), y = (w / (GRID_SIZE / 32)) % GRID_SIZE, x0 = (w % (GRID_SIZE / 32)) * 32;
+    const uint8_t* b8 = bf + (size_t)mip * (GRID_CELLS / 8);
     uint32_t bits = 0;
     for (uint32_t b = 0; b < 32; ++b) {
         const uint32_t m = morton3D(x0 + b, y, z);
-        bits |= (uint32_t)((bf[m >> 3] >> (m & 7)) & 1u) << b;
+        bits |= (uint32_t)((b8[m >> 3] >> (m & 7)) & 1u) << b;
     }
-    occ[w] = bits;
+    occ[g] = bits;
 }
 
 // OccBrick blob (sng_math.h) from the linear mip-0 occupancy: flags, one-block scan, fill
@@ -1684,7 +1686,7 @@ void launch_bitfield(const uint16_t* grid_f16, uint32_t max_cascade, float* grid
     for (uint32_t level = 1; level < N_CASCADES; ++level)
         hipLaunchKernelGGL(bitfield_max_pool_kernel, dim3((N / 64 + 255) / 256), dim3(256), 0, s, N / 64, bf + (size_t)N / 8 * (level - 1),
                            bf + (size_t)N / 8 * level);
-    hipLaunchKernelGGL(bitfield_linear_kernel, dim3(N / 32 / 256), dim3(256), 0, s, bf, occ_linear);
+    hipLaunchKernelGGL(bitfield_linear_kernel, dim3(N / 32 * N_CASCADES / 256), dim3(256), 0, s, bf, occ_linear);
 }
 // dilated brick mask: bit b set when an occupied cell lies in brick b grown by one cell per side.  One
 // thread per (brick, z row of the grown brick); the rows' flags OR into the mask word with an atomic.

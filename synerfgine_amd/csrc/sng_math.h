@@ -502,6 +502,19 @@ SNG_HD bool occupied_at(f3 pos, const uint8_t* bf, uint32_t mip) {
     if (idx == 0xFFFFFFFFu) return false;
     return bf[idx / 8 + (GRID_CELLS * mip) / 8] & (1 << (idx % 8));
 }
+// occupied_at through the x-fastest rows of every cascade (Volume::occ_lin_all): the same cell (cascaded_grid_idx_at's
+// float expressions), the same bit, without the Morton encoding's twelve quarter-rate multiplies
+SNG_HD bool occupied_at_lin(f3 pos, const uint32_t* occ, uint32_t mip) {
+    float mip_scale = scalbnf(1.0f, -(int)mip);
+    pos = pos - splat(0.5f);
+    pos = pos * mip_scale;
+    pos = pos + splat(0.5f);
+    f3 f = pos * (float)GRID_SIZE;
+    int ix = (int)f.x, iy = (int)f.y, iz = (int)f.z;
+    if (ix < 0 || ix >= (int)GRID_SIZE || iy < 0 || iy >= (int)GRID_SIZE || iz < 0 || iz >= (int)GRID_SIZE) return false;
+    const uint32_t w = ((mip * GRID_SIZE + (uint32_t)iz) * GRID_SIZE + (uint32_t)iy) * (GRID_SIZE / 32) + ((uint32_t)ix >> 5);
+    return (occ[w] >> (ix & 31)) & 1u;
+}
 
 // Volume description shared by the marcher, shadow rays and the path tracer.
 struct Volume {
@@ -514,6 +527,7 @@ struct Volume {
     float min_transmittance;
     const uint8_t* bitfield;
     const uint32_t* occ_linear;  // mip-0 occupancy as x-fastest bit rows (same bits as the Morton bitfield)
+    const uint32_t* occ_lin_all; // every cascade's occupancy in that layout, [mip][z][y][x / 32] (nullptr: Morton lookups)
     int linear;                  // cone == 0 && max_mip == 0: the exact fast marcher applies
     StepSpace ss;                // step_space(cone)
     // mip-0 occupancy as 8^3-cell bricks (same bits, OccBrick layout below), small enough to stage in LDS:
@@ -523,6 +537,9 @@ struct Volume {
     const uint32_t* occ_brick_g;  // the same blob in global memory whenever it is built (its size need not be known on the host):
                                   // the training generator reads it through L1 / L2 when it cannot stage it (nullptr: not built)
 };
+SNG_HD bool occupied_vol(f3 pos, const Volume& vol, uint32_t mip) {
+    return vol.occ_lin_all ? occupied_at_lin(pos, vol.occ_lin_all, mip) : occupied_at(pos, vol.bitfield, mip);
+}
 // OccBrick layout (u32 words): [0, 128) = 4096-bit "dilated" brick mask (bit b: an occupied cell lies within one
 // cell of brick b -- the conservative test of path_last_occupied_t), [128, 2176) = u16 slot per brick
 // b = (iz/8)*256 + (iy/8)*16 + ix/8 (0xffff: no occupied cell), then 16 words per occupied brick: word
@@ -684,8 +701,8 @@ SNG_HD float advance_to_occupied(float t, float cone, f3 o, f3 d, f3 idir, uint3
         uint32_t mip = mip_from_pos(pos, N_CASCADES - 1);
         mip = mip < min_mip ? min_mip : mip;
         mip = mip > max_mip ? max_mip : mip;
-        if (!vol.bitfield || occupied_at(pos, vol.bitfield, mip)) return t;
-        while (mip < max_mip && !occupied_at(pos, vol.bitfield, mip + 1)) ++mip;
+        if (!vol.bitfield || occupied_vol(pos, vol, mip)) return t;
+        while (mip < max_mip && !occupied_vol(pos, vol, mip + 1)) ++mip;
         t = advance_to_next_voxel(t, cone, pos, d, idir, mip);
     }
 }
@@ -700,10 +717,10 @@ SNG_HD bool occ_step(float& t, const StepSpace& cone, f3 o, f3 d, f3 idir, uint3
     uint32_t mip = mip_from_pos(pos, N_CASCADES - 1);
     mip = mip < min_mip ? min_mip : mip;
     mip = mip > max_mip ? max_mip : mip;
-    if (!vol.bitfield || occupied_at(pos, vol.bitfield, mip)) return true;
+    if (!vol.bitfield || occupied_vol(pos, vol, mip)) return true;
     // (loading every cascade's byte up front, to save the escalation's dependent loads, measured slower:
     // C4 14.7 -> 13.7 frames/s -- empty-space trips rarely escalate more than once)
-    while (mip < max_mip && !occupied_at(pos, vol.bitfield, mip + 1)) ++mip;
+    while (mip < max_mip && !occupied_vol(pos, vol, mip + 1)) ++mip;
     t = advance_to_next_voxel(t, cone, pos, d, idir, mip);
     return false;
 }
