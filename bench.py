@@ -30,6 +30,15 @@ BYTES_PER_SAMPLE = 28 + 8 * 8 * 4 * 2 + 8   # NerfCoordinate read + 8 levels x 8
 FLOPS_PER_SAMPLE = 20480                     # 2*(32*64+64*16) + 2*(32*64+64*64+64*16)
 HBM_PEAK_GBS = 8000.0                        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_F16_PEAK_TFLOPS = 2500.0                # dense fp16/bf16 MFMA
+# FP32 operations of one BVH box test and one triangle test as the reference writes them (every add, multiply,
+# division, min/max and compare = 1): BoundingBox::ray_intersect (bounding_box.cuh:163-211: 6 subtractions,
+# 6 divisions, 3 swaps as min/max pairs 6, 4 early-out compares, 4 min/max of the candidates = 26) and
+# Triangle::ray_intersect (triangle.cuh:45-59: 3 vector subtractions 9, 2 crosses 18, 4 dots 20, 1 division,
+# 3 scalings by d, u + v, 5 compares = 57), priced against the FP32 vector peak (MI355X_MICROARCH.md: 157.3 TFLOP/s,
+# which counts an FMA as 2)
+BOX_TEST_OPS = 26
+TRI_TEST_OPS = 57
+FP32_VECTOR_PEAK_TFLOPS = 157.3
 ROUND = "r06"
 EXTRAS_FILE = f"profiles/bench_extra_{ROUND}.json"   # the legs of this build (bench.py --extras), committed
 LINE_MAX_BYTES = 6000                        # the driver reads the line from an 8 KB stdout tail
@@ -563,14 +572,19 @@ def bvh_leg(eng, config, s0):
     eff = {k: {"record_loop": round(lane[k]["box_tests"] / 2 / max(1, 64 * wave[k]["box_tests"]), 4),
                "tri_loop": round(lane[k]["tri_tests"] / max(1, 64 * wave[k]["tri_tests"]), 4)} for k in ("path", "shadow")}
     valu = valu_profile(config)
-    useful = {}
+    useful, algo = {}, {}
     if valu:
         for kern, k in (("raytrace_kernel", "path"), ("shadow_rays_kernel", "shadow")):
             if kern in valu:
                 useful[kern] = round(valu[kern]["frac"] * eff[k]["record_loop"], 4)
+                # the tests' own arithmetic over the serialized launch duration of the same SQ pass, at the FP32 vector peak
+                ms = valu[kern]["ms"]
+                ops = lane[k]["box_tests"] * BOX_TEST_OPS + lane[k]["tri_tests"] * TRI_TEST_OPS
+                algo[kern] = round(ops / (ms * 1e-3) / (FP32_VECTOR_PEAK_TFLOPS * 1e12), 4) if ms else None
     rt_s = s0.ms_raytrace * 1e-3
     q = lane["path"]["queries"] + lane["shadow"]["queries"]
-    return {"per_frame": lane, "lane_eff": eff, "valu_roofline": valu, "useful_frac": useful,
+    return {"per_frame": lane, "lane_eff": eff, "valu_roofline": valu, "useful_frac": useful, "algorithmic_flop_frac": algo,
+            "flops_per_test": {"box": BOX_TEST_OPS, "triangle": TRI_TEST_OPS, "peak_tflops": FP32_VECTOR_PEAK_TFLOPS},
             "rays_per_s": round(q / rt_s, 1) if rt_s > 0 else None, "raytrace_stage_ms": round(s0.ms_raytrace, 3)}
 
 
@@ -639,7 +653,8 @@ def compact_line(full):
     b = full.get("bvh")
     if isinstance(b, dict):
         v = b.get("valu_roofline") or {}
-        line["bvh"] = {"lane_eff": b.get("lane_eff"), "useful_frac": b.get("useful_frac"), "rays_per_s": b.get("rays_per_s"),
+        line["bvh"] = {"lane_eff": b.get("lane_eff"), "useful_frac": b.get("useful_frac"),
+                       "algorithmic_flop_frac": b.get("algorithmic_flop_frac"), "rays_per_s": b.get("rays_per_s"),
                        "valu_frac": {k: v[k]["frac"] for k in ("raytrace_kernel", "shadow_rays_kernel") if k in v},
                        "valu_source": v.get("source"), "error": b.get("error")}
         line["bvh"] = {k: x for k, x in line["bvh"].items() if x is not None}

@@ -44,6 +44,7 @@ def _full(n_launch=2, legs=True):
         full["roofline"]["uncontended"] = r05["roofline"]["uncontended"]
         full["bvh"]["lane_eff"] = {"path": {"record_loop": 0.31, "tri_loop": 0.54}, "shadow": {"record_loop": 0.56, "tri_loop": 0.81}}
         full["bvh"]["useful_frac"] = {"raytrace_kernel": 0.10, "shadow_rays_kernel": 0.24}
+        full["bvh"]["algorithmic_flop_frac"] = {"raytrace_kernel": 0.054, "shadow_rays_kernel": 0.20}
     return full
 
 
@@ -65,6 +66,7 @@ def test_line_from_stub_frames_is_compact_and_complete():
     assert {"value", "cores", "kind", "cpu_model"} <= set(line["cpu_baseline"])
     assert {"steps_per_s", "frac"} <= set(line["train"])
     assert line["extras"].startswith("profiles/bench_extra_")
+    assert line["bvh"]["algorithmic_flop_frac"]["shadow_rays_kernel"] > 0
 
 
 def test_worst_case_line_fits():
