@@ -401,7 +401,7 @@ def _srgb(rgba):
 
 def orbit_leg(config, w, h, model, warmup, n=60):
     """The camera orbits the lego 1 degree per frame: nerf_spec_hint on vs off (alternating passes, mean of two each).
-    The hints are read only when a frame repeats the previous frame's view (spec_view_key, capi.cpp), so on the
+    The hints are read only when a frame repeats the previous frame's view (spec_view_key, host_render.cpp), so on the
     orbit both settings march with the opacity policy; the leg shows that hints cost nothing under motion."""
     import math
 

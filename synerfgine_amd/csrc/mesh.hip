@@ -63,7 +63,7 @@ struct PStack {
 };
 
 // Where a traversal finds its stack and the BVH arrays.  LDS = true: every object's nodes and
-// triangles were copied once per workgroup into LDS (scene blob, capi.cpp upload_scene) and the
+// triangles were copied once per workgroup into LDS (scene blob, host_scene.cpp upload_scene) and the
 // stack is only as deep as the deepest BVH needs (max depth + 2 <= 32, so the reference's
 // FixedStack<32> overflow rule can never trigger differently).
 // CNT = true (bench's counting frames only, sng_rt_counters): cnt -> this thread's {world queries,
@@ -240,7 +240,7 @@ __device__ __forceinline__ float bvh_walk_wide(f3 ro, f3 rd, f3 y, const BvhWide
 // straight away (push far, continue near): one LDS store + load less per inner visit that descends.
 // The visiting sequence, `d < mint` culling at push time and triangle order are the reference's, so
 // the result is identical.  (The reference's FixedStack<32> overflow rule cannot fire: the stack
-// never holds more than max BVH depth + 2 <= 32 entries, capi.cpp upload_scene.)
+// never holds more than max BVH depth + 2 <= 32 entries, host_scene.cpp upload_scene.)
 template <bool FAST>
 __device__ __forceinline__ float bvh_walk_near(f3 ro, f3 rd, f3 y, const BvhWide* __restrict__ wide, const TriT* __restrict__ tris, int root_ref,
                                                int* stack_lds, int stride, int& tri_out, float t_max, uint32_t* cnt = nullptr, bool cw = false) {
@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(RT_WAVES_P
     const uint32_t S = a.samples, ppw = 64u / S;                     // pixels per wave (1 <= S <= 64)
     const uint32_t n_px = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W, n_units = (n_px + ppw - 1u) / ppw;
     const uint32_t sub = (uint32_t)lane / S, s = (uint32_t)lane % S, g0 = sub * S;   // lane -> (pixel of the unit, sample)
-    // units claimed a_sp_chunk at a time (capi.cpp: ~8 claims per wave, 1 for thin bands) -- a full frame has ~2.6e5 units,
+    // units claimed a_sp_chunk at a time (host_render.cpp: ~8 claims per wave, 1 for thin bands) -- a full frame has ~2.6e5 units,
     // whose claims on one counter would serialise like the shadow kernel's once did
     const uint32_t chunk = max(1u, a.sp_chunk);
     uint32_t k = 0, k_end = 0;
@@ -1373,7 +1373,7 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
     // rt_spread: every CU gets a workgroup (a thin band's tiles then spread over the whole GPU, one wave each)
     const uint32_t bp = (a.spread || a.sample_par) ? a.persistent_blocks * per_cu : std::min((n_tiles + tp / 64 - 1) / (tp / 64), a.persistent_blocks * per_cu);
     const uint32_t sb = shadow_blocks ? shadow_blocks : a.persistent_blocks * per_cu;
-    if (a.sample_par) {   // rt_rng = 1 (capi.cpp: list mode, no counters, no fused queue): the sample-parallel path kernel
+    if (a.sample_par) {   // rt_rng = 1 (host_render.cpp: list mode, no counters, no fused queue): the sample-parallel path kernel
         RaytraceArgs b = a;   // ~8 claims per wave of the grid (a band's few units: one per claim)
         const uint32_t ppw = 64u / std::max(1u, a.samples), units = (n + ppw - 1) / ppw, waves = bp * (tp / 64u);
         b.sp_chunk = std::max(1u, units / (waves * 8u));
@@ -1414,7 +1414,7 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
             hipLaunchKernelGGL(shadow_rays_kernel<false>, dim3(sb), dim3(ts), ls, s, a, q, a.work + SHADOW_CTR0);
         }
     }
-    if (q.plist) {   // capi.cpp enables the lists only when one wave's staging fits 64 KB
+    if (q.plist) {   // host_render.cpp enables the lists only when one wave's staging fits 64 KB
         const size_t per_wave = 16u * (64u * q.rec_stride + (64u * q.nps + 3u) / 4u);
         const uint32_t waves = (uint32_t)std::max<size_t>(1, std::min<size_t>(4, (160u * 1024u) / per_wave));
         allow_lds(rt_record_colour_kernel, waves * per_wave);

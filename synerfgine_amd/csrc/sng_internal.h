@@ -262,7 +262,7 @@ struct RaytraceArgs {
     float lens;
     int show_nerf_shadow;
     float syn_shadow_factor;
-    // traversal resources (capi.cpp upload_scene / render_frame)
+    // traversal resources (host_scene.cpp upload_scene, host_render.cpp render_frame)
     const float4* scene_blob;   // all objects' BVH nodes + triangles, 16-B aligned (ObjectGpu::lds_nodes or lds_wide, lds_trit)
     uint32_t scene_f4;          // blob size in float4
     int scene_in_lds;           // copy the blob into LDS per workgroup
@@ -434,7 +434,7 @@ void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf
                     int tonemap, const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s);
 void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s);
 
-// error carrying an sng_status code (capi.cpp turns it into the return value + sng_last_error)
+// error carrying an sng_status code (capi.cpp guarded() turns it into the return value + sng_last_error)
 struct SngError : std::runtime_error {
     int code;
     SngError(int c, const std::string& m) : std::runtime_error(m), code(c) {}

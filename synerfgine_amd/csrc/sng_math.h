@@ -787,7 +787,7 @@ SNG_HD float curand_uniform(Xorwow& s) {
 // ---- scene records ------------------------------------------------------------
 struct BvhNode { float lo[3], hi[3]; int left, right; };   // TriangleBvhNode (32 B)
 struct Tri { f3 a, b, c; };                                 // Triangle (36 B)
-// Traversal layout of the same BVH (capi.cpp wide_bvh): one 64-B record per INNER node holding
+// Traversal layout of the same BVH (host_scene.cpp wide_bvh): one 64-B record per INNER node holding
 // both children's boxes and references, so visiting a node is four 16-B loads and a leaf needs none
 // (its triangle range travels in the stack entry).  Each box is stored slab by slab
 // (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z) so that an axis is one packed-f32 register pair.
@@ -803,7 +803,7 @@ struct alignas(16) BvhWide {
 };
 constexpr uint32_t WIDE_MAX_BEGIN = 1u << 24, WIDE_MAX_COUNT = 127u;
 constexpr int WIDE_DONE = (int)0x80000000;   // traversal sentinel; wide_bvh never encodes a leaf as ~0x7FFFFFFF
-// Traversal copy of a triangle (capi.cpp upload_scene): a, e1 = b - a, e2 = c - a and n = cross(e1, e2),
+// Traversal copy of a triangle (host_scene.cpp upload_scene): a, e1 = b - a, e2 = c - a and n = cross(e1, e2),
 // the values Triangle::ray_intersect (triangle.cuh:45-59) forms first, evaluated once on the host with
 // the same float operations, so the test reads them instead of recomputing them per ray.  48 B, three
 // 16-B loads: v = {a.x a.y a.z e1.x | e1.y e1.z e2.x e2.y | e2.z n.x n.y n.z}.

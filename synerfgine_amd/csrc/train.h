@@ -1,4 +1,4 @@
-// train.h -- device structs and helpers of the online training step (train.hip, capi.cpp)
+// train.h -- device structs and helpers of the online training step (train.hip, host_train.cpp)
 #pragma once
 #include "sng_internal.h"
 #include "sng_math.h"

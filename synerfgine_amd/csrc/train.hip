@@ -452,7 +452,7 @@ __global__ void train_rollover_kernel(TrainStepArgs a, TrainBatch b, TrainSched*
 
 // ---------------------------------------------------------------------------------------------
 // MLP weight fragments from an fp16 parameter blob (tcnn order, nerf_network.h:356-371):
-// forward A fragments (20 x 64 lanes x 8, the same image capi.cpp set_model packs on the host)
+// forward A fragments (20 x 64 lanes x 8, the same image host_render.cpp set_model packs on the host)
 // and backward A fragments of W^T (36 x 64 lanes x 4) for v_mfma_f32_16x16x16f16
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint16_t fwd_frag_elem(const uint16_t* W, int n_in, int mb, int kb, bool permuted, int lane, int j) {

@@ -2,7 +2,7 @@
 
 SURVEY.md §8e: rays are independent, so the frame shards into contiguous row bands with no
 data-path collective; halo rows needed by normals (+-2) and NeRF shadows (+-r) are recomputed
-inside sng_render_frame (capi.cpp render_frame), not exchanged.  The exchanges are the frame-wide
+inside sng_render_frame (host_render.cpp render_frame), not exchanged.  The exchanges are the frame-wide
 step schedule (comm.cpp) and the final gather of the RGBA8 bands to rank 0 (sng_gather_rgba8: grouped
 ncclSend / ncclRecv over xGMI, ~1 MB per peer at 1080p); gather_to_root is its gloo rehearsal.
 """

@@ -594,7 +594,7 @@ def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
 @pytest.mark.parametrize("config,target", [("c3", 3000), ("c4", 100000)])
 def test_mid_frame_switch_to_fused_tail_is_exact(config, target):
     """With a small query target the march starts with short iterations and hands over to the fused tail in
-    the middle of the frame (capi.cpp trace_nerf: at a chunk boundary, once n_alive * 8 <= target); the
+    the middle of the frame (host_render.cpp trace_nerf: at a chunk boundary, once n_alive * 8 <= target); the
     result, statistics and per-iteration histograms equal the pure wavefront's bit for bit -- for the linear
     lego-like generate and the cascaded kitchen-like one, with shadows and the mesh on (RNG streams rewound
     between the two renders)."""
