@@ -60,6 +60,7 @@ __global__ __launch_bounds__(256) void nerf_fused_kernel(FusedArgs a) {
     // continue where the per-iteration wavefront stopped: its alive buffer, step counter i and
     // iteration count (all 0-based iteration statistics continue at k0)
     const uint32_t n_rays = a.ctrl->n_alive[a.p];
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->fused_rays_in = n_rays;   // (host_render.cpp spec_adapt)
     // nothing left (the speculative rounds finished every ray), or not a tail after all (tail_prepare's check):
     // leave before the weight fragments are loaded
     if (n_rays == 0 || !a.ctrl->spec_ok) return;

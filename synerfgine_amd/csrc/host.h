@@ -219,6 +219,7 @@ struct sng_ctx {
     DevBuf spec_pre, spec_pre_depth;       // spec_prepare: per network sample {rgb, alpha} and depth
     DevBuf band_rgba8;                     // sng_gather_rgba8: this rank's band as RGBA8
     uint32_t spec_rounds = 0;              // rounds enqueued by the last trace
+    uint32_t spec_rounds_next = 0;         // nerf_spec_adapt: the round count the next trace uses (0: nerf_spec_rounds)
     uint32_t msr_rounds = 0;               // multi-step speculative rounds of the last trace that committed iterations
     DevBuf rt_counts;                      // rt_count frames: path / shadow kernel {queries, box tests, triangle tests}
     bool fused_last = false;               // the last trace finished in the fused kernel
@@ -302,6 +303,7 @@ void resize(sng_ctx* c);
 f2 focal_for(const sng_ctx* c, const int res[2]);
 void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out);
 void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out);
+void spec_adapt(sng_ctx* c);
 // host_scene.cpp
 f3 cam_col(const sng_ctx* c, int i);
 void set_cam_col(sng_ctx* c, int i, f3 v);

@@ -91,6 +91,10 @@ const std::map<std::string, double>& default_params() {
                                                 //   from the first iteration, queued ahead of its device check; C2 1311 -> 1483
                                                 //   frames/s against 1, C3 unchanged)
         {"nerf_spec_rounds", 2},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
+        {"nerf_spec_adapt", 1},                 // ... one round fewer while the last frame's final round evaluated fewer than
+        {"nerf_spec_min_samples", 8192},        //   this many samples (a whole-GPU launch for them costs more than the fused
+                                                //   kernel does), one more when the rays that kernel takes over would fill
+                                                //   one twice over (exact either way)
         {"nerf_spec_budget", 16777216},         // samples one round may generate (K = clamp(budget / (8 n_alive), 1, kmax)); the
                                                 //   sample buffers are sized for it (16.8 M x 60 B ~ 1 GB of the 288 GB)
         {"nerf_spec_hint", 1},                  // a ray looks ahead as far as its pixel's ray lived last frame (exact; 0: opacity policy)

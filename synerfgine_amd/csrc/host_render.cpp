@@ -544,7 +544,8 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // speculative tail rounds (nerf.hip): each marches every alive ray K iterations ahead, one
             // whole-GPU network launch evaluates them, the compositor replays them exactly; the fused
             // kernel below then finishes whatever is still alive
-            const uint32_t rounds = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds"));
+            uint32_t rounds = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds"));
+            if (rounds > 1 && c->p("nerf_spec_adapt") != 0.0 && c->spec_rounds_next) rounds = std::min(rounds, c->spec_rounds_next);
             uint8_t* hint_w = nullptr;   // the hints this frame writes (SpecArgs::hint), nullptr when it writes none
             c->spec_rounds = rounds;
             launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), p, target, a.sched.global, c->s_nerf);
@@ -586,7 +587,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
                 const uint32_t sblocks = std::max(1u, std::min((n_band + 255) / 256, (uint32_t)c->n_cus * 4));
                 hint_w = sa.hint;
                 for (uint32_t r = 0; r < rounds; ++r) {
-                    sa.in = rb[p]; sa.out = rb[p ^ 1]; sa.p = p;
+                    sa.in = rb[p]; sa.out = rb[p ^ 1]; sa.p = p; sa.round = r;
                     // per-ray look-ahead in all but the last round (which then finishes nearly every ray)
                     sa.k_policy = (c->p("nerf_spec_k_policy") != 0.0 && r + 1 < rounds) ? 1 : 0;
                     launch_spec_generate(sa, sblocks, c->s_nerf);
@@ -699,6 +700,22 @@ uint8_t* spec_hint_buf(sng_ctx* c) {
         c->spec_hint_px = px;
     }
     return c->spec_hint.as<uint8_t>();
+}
+
+// nerf_spec_adapt: the next trace's round count from this one's (MarchCtrl read back at the end of the frame).  A final
+// round that evaluated fewer than nerf_spec_min_samples samples is dropped (its rays go to the fused kernel, which
+// marches them ray-locally: C3's second round evaluates ~100 samples in a 15-us whole-GPU launch); a round comes back
+// when the rays the fused kernel takes over would fill one (8 samples each, twice the threshold).  The frame's bits do
+// not depend on the count (the rounds are exact).
+void spec_adapt(sng_ctx* c) {
+    const uint32_t R = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds")), r = c->spec_rounds;
+    if (c->p("nerf_spec_adapt") == 0.0 || R < 2 || !c->fused_last || r == 0) { c->spec_rounds_next = 0; return; }
+    const MarchCtrl& h = *c->h_ctrl;
+    const double min_s = std::max(0.0, c->p("nerf_spec_min_samples"));
+    uint32_t next = std::min(r, R);
+    if (next > 1 && (double)h.spec_round_samples[std::min(next, 4u) - 1] < min_s) --next;
+    else if (next < R && (double)h.fused_rays_in * MAX_STEPS_BETWEEN_COMPACTION >= 2.0 * min_s) ++next;
+    c->spec_rounds_next = next;
 }
 
 // march statistics of the last trace (MarchCtrl read back at the end of the frame)
@@ -1033,6 +1050,7 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
     HIPCHK(hipEventRecord(c->ev_end, c->s_nerf));
     if (show_nerf) HIPCHK(hipMemcpyAsync(c->h_ctrl, c->ctrl.p, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
     HIPCHK(hipStreamSynchronize(c->s_nerf));
+    if (show_nerf) spec_adapt(c);
 
     if (out) {
         std::memset(out, 0, sizeof(*out));
@@ -1092,6 +1110,7 @@ void render_nerf_ngp(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* o
     HIPCHK(hipMemcpyAsync(c->h_ctrl, c->ctrl.p, sizeof(MarchCtrl), hipMemcpyDeviceToHost, c->s_nerf));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->s_nerf));
+    spec_adapt(c);
     if (out) {
         std::memset(out, 0, sizeof(*out));
         out->d_nerf_rgba = c->nerf_rgba.as<float>();

@@ -745,6 +745,7 @@ __global__ __launch_bounds__(THREADS) void spec_composite_kernel(SpecArgs a) {
             ctrl->net_samples += ctrl->n_samples[p];
             ctrl->spec_evals += ctrl->n_samples[p];
         }
+        if (a.round < 4) ctrl->spec_round_samples[a.round] = K ? ctrl->n_samples[p] : 0u;
         ctrl->n_samples[p ^ 1] = 0;
         ctrl->n_reused[p ^ 1] = 0;
     }

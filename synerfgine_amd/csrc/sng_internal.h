@@ -59,6 +59,9 @@ struct MarchCtrl {
     uint32_t spec_kk_valid[2];       // RayBuf::kk of buffer p holds per-ray iteration indices
     uint32_t spec_ok;                // tail_prepare: every later iteration takes 8 steps (else the tail kernels queued
                                      // ahead of that check leave every buffer untouched and the wavefront continues)
+    uint32_t spec_round_samples[4];  // network samples of the frame's speculative rounds 0..3 (spec_composite; sizes the next
+                                     //   frame's round count, nerf_spec_adapt)
+    uint32_t fused_rays_in;          // rays the fused tail kernel took over (after the rounds)
     // multi-step speculative rounds (nerf.hip msr_*), per ping-pong buffer of the round's rays
     uint32_t msr_S[2];               // steps the round's first iteration takes (0: the round is a no-op)
     uint32_t msr_K[2];               // iterations the round marched ahead
@@ -354,6 +357,7 @@ struct SpecArgs {
                                   // tail's first iteration (0: unknown);
                                   // a ray looks ahead just that far (exact whatever the hint: it only sizes the round)
     int hint_read;                // 0: the hints are another view's (the camera moved): written, not read
+    uint32_t round;               // the round's index in the frame's tail (MarchCtrl::spec_round_samples)
 };
 constexpr uint32_t SPEC_KMAX = 16;
 

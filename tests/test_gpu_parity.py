@@ -569,7 +569,7 @@ def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
     launch, the iterations replayed in order with the wavefront's termination) reproduce the per-iteration
     wavefront bit for bit: frame buffers, sample / hit / iteration counts, reference slots and per-iteration
     histograms, for every round / look-ahead shape, both tracers and the cascaded marcher."""
-    tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0}, config)
+    tb, eng, _ = _engine(160, 90, {"show_virtual_obj": 0, "shadow_on_nerf": 0, "nerf_spec_adapt": 0}, config)
     try:
         out = {}
         # fused = 2: the same frame again, its rounds sized by the first frame's per-pixel hints (nerf_spec_hint)
@@ -587,6 +587,38 @@ def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
             for a, b in zip(out[0][0], out[f][0]):
                 assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f
             assert out[0][1:] == out[f][1:], f
+    finally:
+        tb.close()
+
+
+@pytest.mark.parametrize("config,res", [("c3", (480, 270)), ("c2", (400, 400))])
+def test_spec_adapt_changes_rounds_not_bits(config, res):
+    """nerf_spec_adapt: the round count of the speculative tail follows the last frame's final-round sample count
+    (host_render.cpp spec_adapt); the frames are the same bits as with the fixed count."""
+    tb, eng, _ = _engine(res[0], res[1], {}, config)
+    try:
+        rng = [eng.rng_states(0).copy(), eng.rng_states(1).copy()]   # every frame from the same streams
+        got = {}
+        for adapt, minsamp in ((0, 8192), (1, 1 << 30), (1, 0)):
+            eng.set_param("nerf_spec_adapt", adapt)
+            eng.set_param("nerf_spec_min_samples", minsamp)
+            rounds = []
+            for _ in range(3):
+                eng.set_rng_states(0, rng[0])
+                eng.set_rng_states(1, rng[1])
+                r = eng.frame(spp=0, reset=True)
+                rounds.append(r.spec_rounds)
+            got[(adapt, minsamp)] = (rounds, [r.download(b).copy() for b in ("nerf_rgba", "nerf_depth", "final_rgba")],
+                                     (r.n_samples, r.n_hit, r.n_iterations))
+        assert got[(0, 8192)][0] == [2, 2, 2]
+        assert got[(1, 1 << 30)][0][-1] == 1       # every final round "too small": one round
+        assert got[(1, 1 << 30)][0] == [2, 1, 1]     # and it stays there (no growth: few rays left for the fused kernel)
+        assert got[(1, 0)][0][1:] == [2, 2]          # a threshold of 0 never drops a round; the first frame still has the
+                                                     # previous setting's count, the rays it leaves bring the second back
+        for k in got:
+            for a, b in zip(got[(0, 8192)][1], got[k][1]):
+                assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
+            assert got[(0, 8192)][2] == got[k][2], k
     finally:
         tb.close()
 
