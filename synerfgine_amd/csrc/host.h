@@ -197,7 +197,7 @@ struct sng_ctx {
     DevBuf samp, coords, net_out, ctrl;
     size_t ray_cap = 0, sample_cap = 0;
     DevBuf mesh_o, mesh_d, acc_rgba, acc_depth, final_rgba, final_depth;
-    DevBuf rt_rec, rt_lc, rt_srec, rt_mask, rt_head, rt_count, rt_work;   // deferred-shadow raytracer queues
+    DevBuf rt_rec, rt_lc, rt_srec, rt_mask, rt_head, rt_work;   // deferred-shadow raytracer queues (+ work counters)
     DevBuf rt_plist, rt_pcount, rt_rval;   // per-pixel record lists + record colour terms (tile path kernel)
     DevBuf rt_tile_cost, rt_tile_order;   // previous frame's per-tile cost -> this frame's tile order
     DevBuf rt_started;                    // rt_first: the path kernel's landing flag (frame sequence number)

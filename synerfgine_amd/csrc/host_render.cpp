@@ -926,9 +926,8 @@ void render_frame(sng_ctx* c, const sng_frame_params* fp, sng_frame_result* out)
                 c->rt_lc.ensure(cap * 16ull * std::max<uint32_t>(1u, q.nls));
                 c->rt_mask.ensure(cap * 4ull * q.nps);
                 c->rt_head.ensure((uint64_t)MW * MH * 4);
-                c->rt_count.ensure(16);
                 q.rec = c->rt_rec.as<float4>(); q.lc = c->rt_lc.as<float4>(); q.srec = c->rt_srec.as<float4>(); q.mask = c->rt_mask.as<float>();
-                q.head = c->rt_head.as<int>(); q.count = c->rt_count.as<uint32_t>(); q.cap = (uint32_t)cap;
+                q.head = c->rt_head.as<int>(); q.count = ra.work + RT_REC_COUNT; q.cap = (uint32_t)cap;
                 // shadow-ray grid: the CUs the path kernel leaves to the NeRF tail too when rt_shadow_all_cus
                 // (by then the tail has mostly finished)
                 const uint32_t sb = c->p("rt_shadow_all_cus") != 0.0 ? (uint32_t)c->n_cus * 1024u / ra.lds_tpb : 0u;

@@ -1361,7 +1361,9 @@ void launch_raytrace_wavefront(const RaytraceArgs& a, const RtQueue& q, const fl
                                float* accd, uint32_t shadow_blocks, hipStream_t s) {
     const uint32_t n = (uint32_t)(a.row1 - a.row0) * (uint32_t)a.W;
     if (!n) return;
-    (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);   // errors surface through hipGetLastError in the caller
+    // the work counters, the record counter among them (q.count = work + RT_REC_COUNT, host_render.cpp): one clear
+    // (errors surface through hipGetLastError in the caller)
+    if (q.count < a.work || q.count >= a.work + RT_WORK_WORDS) (void)hipMemsetAsync(q.count, 0, sizeof(uint32_t), s);
     (void)hipMemsetAsync(a.work, 0, RT_WORK_WORDS * sizeof(uint32_t), s);
     // path kernel: capped at 128 VGPRs (amdgpu_waves_per_eu(4), a few spills) -> 4 waves/SIMD = 2 x 512-thread workgroups;
     // measured faster than 3 waves/SIMD without spills

@@ -253,6 +253,7 @@ struct ShadowArgs {
 constexpr uint32_t SHADOW_CTR_STRIDE = 256;   // u32 (1 KiB) between counters
 constexpr uint32_t SHADOW_CTR0 = 256;
 constexpr uint32_t RT_WORK_WORDS = SHADOW_CTR0 + SHADOW_NCTR * SHADOW_CTR_STRIDE;
+constexpr uint32_t RT_REC_COUNT = 128;        // work[128]: the hit-record counter (RtQueue::count; cleared with the work words)
 
 struct RaytraceArgs {
     Volume vol;
