@@ -273,8 +273,9 @@ def frame_cells(eng, cells, frames, warmup, px):
     for cell in cells:
         for k, v in cell.items():
             eng.set_param(k, v)
+        warm_launches = 0
         for _ in range(warmup):
-            eng.frame(spp=0, reset=True)
+            warm_launches += int(eng.frame(spp=0, reset=True).network_launches)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         st = [eng.frame(spp=0, reset=True, collect_kernel_times=True) for _ in range(frames)]
@@ -291,6 +292,7 @@ def frame_cells(eng, cells, frames, warmup, px):
                     "hit_frac": round(r.n_hit / px, 4),
                     "network_roofline_frac": round(gbs / HBM_PEAK_GBS, 4), "field_sample_weighted_frac": round(fsw, 4),
                     "network_per_launch": per_launch_table(st),
+                    "network_launches": {"warmup": warm_launches, "timed": int(sum(x.network_launches for x in st))},
                     "stages_ms": {"raytrace": round(r.ms_raytrace, 3), "nerf": round(r.ms_nerf, 3), "shadow": round(r.ms_shadow, 3)}})
     return out
 
@@ -638,14 +640,15 @@ def compact_line(full):
     line["stages_ms_last_frame"] = full.get("stages_ms_last_frame")
     rf = full.get("roofline", {})
     r = _pick(rf, ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_source", "traffic_over_algorithmic",
-                   "algorithmic_bytes_per_sample", "avg_launch_ms", "launches", "samples_in_launches", "per_launch", "mfma_frac"))
+                   "algorithmic_bytes_per_sample", "avg_launch_ms", "launches", "warmup_launches", "samples_in_launches", "per_launch",
+                   "mfma_frac"))
     if "field_sample_weighted" in rf:
         r["field_sample_weighted"] = _pick(rf["field_sample_weighted"], ("frac",))
     if "onestep_regime" in rf:
         r["onestep_regime"] = _pick(rf["onestep_regime"], ("ms",))
     unc = rf.get("uncontended")
     if isinstance(unc, dict):
-        r["uncontended"] = _pick(unc, ("frac", "source", "frames_per_s", "error"))
+        r["uncontended"] = _pick(unc, ("frac", "source", "frames_per_s", "warmup_launches", "launches", "error"))
         alt = (unc.get("alternates") or {}).get("hip_events_this_process")
         if alt:
             r["uncontended"]["alternates"] = {"hip_events_this_process": _pick(alt, ("frac", "per_launch"))}
@@ -911,8 +914,9 @@ def main():
                 T.gather_to_root(tile, bounds, frame)
         return r
 
+    warm_launches = 0   # network launches of the warm-up frames (tools/roofline_check.py aligns the kernel trace on them)
     for _ in range(args.warmup):
-        step(False)
+        warm_launches += int(step(False).network_launches)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -934,6 +938,7 @@ def main():
         snap = S.snapshot_path(args.config, args.model)
         result = frame_result(args, stats, elapsed, world, res, bounds, comm, overrides, root_gather, on_dev,
                               os.path.relpath(snap, REPO) if snap else None)
+        result["roofline"]["warmup_launches"] = warm_launches
     if rank == 0 and world == 1 and not args.no_sweep:
         # extra legs, after the timed region: the same workload with the two streams serialized (the roofline kernel's
         # launches then run alone), the BVH work of one counting frame, and the training step (config C5)
@@ -952,6 +957,7 @@ def main():
                     "source": (f"rocprofv3 kernel trace of the driver-format command ({os.path.relpath(chk, REPO)}, tools/gpu.sh profdriver)"
                                if same and "rocprof_frac" in same else "HIP events of this process (no rocprof check of this round)"),
                     "alternates": {"hip_events_this_process": {"frac": u["network_roofline_frac"], "per_launch": u["network_per_launch"]}},
+                    "warmup_launches": u["network_launches"]["warmup"], "launches": u["network_launches"]["timed"],
                     "field_sample_weighted_frac": u["field_sample_weighted_frac"],
                     "frames_per_s": u["frames_per_s"],
                     "note": "the same frames with the raytracer and the NeRF serialized (concurrent_streams=0, 10 frames after "

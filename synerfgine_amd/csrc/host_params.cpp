@@ -91,7 +91,8 @@ const std::map<std::string, double>& default_params() {
                                                 //   from the first iteration, queued ahead of its device check; C2 1311 -> 1483
                                                 //   frames/s against 1, C3 unchanged)
         {"nerf_spec_rounds", 2},                // speculative tail rounds before the fused kernel finishes the stragglers (nerf.hip)
-        {"nerf_spec_adapt", 1},                 // ... one round fewer while the last frame's final round evaluated fewer than
+        {"nerf_spec_adapt", 1},                 // ... (hybrid frames, NeRF tail beside the raytracer) one round fewer while the
+                                                //   last frame's final round evaluated fewer than
         {"nerf_spec_min_samples", 8192},        //   this many samples (a whole-GPU launch for them costs more than the fused
                                                 //   kernel does), one more when the rays that kernel takes over would fill
                                                 //   one twice over (exact either way)

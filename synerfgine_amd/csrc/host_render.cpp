@@ -251,6 +251,7 @@ uint64_t ref_slots_of(const sng_ctx* c) {
 // own0/own1: the NeRF rows this band owns (the bands of all ranks partition the frame's rows);
 // only used when a schedule communicator is attached (Sched).
 uint8_t* spec_hint_buf(sng_ctx* c);
+bool spec_adapt_on(const sng_ctx* c, const TraceMode& mode);
 
 // The view a frame's NeRF rays come from: camera0 / camera1 / rolling shutter, focal length, screen centre, NeRF
 // resolution and the model (FNV-1a over the bytes).  The speculative rounds read the per-pixel look-ahead hints only
@@ -545,7 +546,7 @@ uint32_t trace_nerf(sng_ctx* c, const sng_frame_params& P, const Volume& vol, co
             // whole-GPU network launch evaluates them, the compositor replays them exactly; the fused
             // kernel below then finishes whatever is still alive
             uint32_t rounds = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds"));
-            if (rounds > 1 && c->p("nerf_spec_adapt") != 0.0 && c->spec_rounds_next) rounds = std::min(rounds, c->spec_rounds_next);
+            if (rounds > 1 && spec_adapt_on(c, mode) && c->spec_rounds_next) rounds = std::min(rounds, c->spec_rounds_next);
             uint8_t* hint_w = nullptr;   // the hints this frame writes (SpecArgs::hint), nullptr when it writes none
             c->spec_rounds = rounds;
             launch_tail_prepare(ctrl, c->fused_work.as<uint32_t>(), p, target, a.sched.global, c->s_nerf);
@@ -705,8 +706,13 @@ uint8_t* spec_hint_buf(sng_ctx* c) {
 // nerf_spec_adapt: the next trace's round count from this one's (MarchCtrl read back at the end of the frame).  A final
 // round that evaluated fewer than nerf_spec_min_samples samples is dropped (its rays go to the fused kernel, which
 // marches them ray-locally: C3's second round evaluates ~100 samples in a 15-us whole-GPU launch); a round comes back
-// when the rays the fused kernel takes over would fill one (8 samples each, twice the threshold).  The frame's bits do
-// not depend on the count (the rounds are exact).
+// when the rays the fused kernel takes over would fill one (8 samples each, twice the threshold).  Only on hybrid
+// frames whose NeRF tail runs beside the raytracer: the fused kernel's ray-local chain for those few rays is longer
+// than the round it replaces (C3: 51 us), so it pays only where the NeRF stream is not the frame's critical path.
+// The frame's bits do not depend on the count (the rounds are exact).
+bool spec_adapt_on(const sng_ctx* c, const TraceMode& mode) {
+    return c->p("nerf_spec_adapt") != 0.0 && !mode.ngp && c->p("concurrent_streams") != 0.0 && c->p("show_virtual_obj") != 0.0 && !c->objs.empty();
+}
 void spec_adapt(sng_ctx* c) {
     const uint32_t R = (uint32_t)std::max(0.0, c->p("nerf_spec_rounds")), r = c->spec_rounds;
     if (c->p("nerf_spec_adapt") == 0.0 || R < 2 || !c->fused_last || r == 0) { c->spec_rounds_next = 0; return; }

@@ -591,10 +591,11 @@ def test_spec_tail_rounds_equal_wavefront(config, ngp_mode, spec):
         tb.close()
 
 
-@pytest.mark.parametrize("config,res", [("c3", (480, 270)), ("c2", (400, 400))])
+@pytest.mark.parametrize("config,res", [("c3", (480, 270)), ("c3", (160, 90)), ("c2", (400, 400))])
 def test_spec_adapt_changes_rounds_not_bits(config, res):
-    """nerf_spec_adapt: the round count of the speculative tail follows the last frame's final-round sample count
-    (host_render.cpp spec_adapt); the frames are the same bits as with the fixed count."""
+    """nerf_spec_adapt: on hybrid frames the round count of the speculative tail follows the last frame's final-round
+    sample count (host_render.cpp spec_adapt); NeRF-only frames (C2) keep nerf_spec_rounds.  The frames are the same
+    bits as with the fixed count."""
     tb, eng, _ = _engine(res[0], res[1], {}, config)
     try:
         rng = [eng.rng_states(0).copy(), eng.rng_states(1).copy()]   # every frame from the same streams
@@ -610,15 +611,18 @@ def test_spec_adapt_changes_rounds_not_bits(config, res):
                 rounds.append(r.spec_rounds)
             got[(adapt, minsamp)] = (rounds, [r.download(b).copy() for b in ("nerf_rgba", "nerf_depth", "final_rgba")],
                                      (r.n_samples, r.n_hit, r.n_iterations))
-        assert got[(0, 8192)][0] == [2, 2, 2]
-        assert got[(1, 1 << 30)][0][-1] == 1       # every final round "too small": one round
-        assert got[(1, 1 << 30)][0] == [2, 1, 1]     # and it stays there (no growth: few rays left for the fused kernel)
-        assert got[(1, 0)][0][1:] == [2, 2]          # a threshold of 0 never drops a round; the first frame still has the
-                                                     # previous setting's count, the rays it leaves bring the second back
         for k in got:
             for a, b in zip(got[(0, 8192)][1], got[k][1]):
                 assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
             assert got[(0, 8192)][2] == got[k][2], k
+        assert got[(0, 8192)][0] == [2, 2, 2]
+        if config == "c2":   # NeRF only: the tail is the frame's critical path, the count stays
+            assert got[(1, 1 << 30)][0] == [2, 2, 2] and got[(1, 0)][0] == [2, 2, 2]
+            return
+        assert got[(1, 1 << 30)][0][-1] == 1       # every final round "too small": one round
+        assert got[(1, 1 << 30)][0] == [2, 1, 1]     # and it stays there (no growth: few rays left for the fused kernel)
+        assert got[(1, 0)][0][1:] == [2, 2]          # a threshold of 0 never drops a round; the first frame still has the
+                                                     # previous setting's count, the rays it leaves bring the second back
     finally:
         tb.close()
 
