@@ -439,7 +439,7 @@ void launch_overlay(int W, int row0, int row1, int scale, int nerf_w, int n_nerf
                     int tonemap, const float4* syn, const float* synd, const float4* nerf, const float* nerfd, float4* fin, float* find, hipStream_t s);
 void launch_xorwow_init(uint32_t n, uint64_t seed, const uint32_t* seq_pow, uint32_t* st, hipStream_t s);
 
-// error carrying an sng_status code (capi.cpp guarded() turns it into the return value + sng_last_error)
+// error carrying an sng_status code (host.h guarded(), around every C ABI entry point, turns it into the return value + sng_last_error)
 struct SngError : std::runtime_error {
     int code;
     SngError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
